@@ -1,0 +1,165 @@
+"""bench.py — ringpop-node hot path on MI355X.
+
+Workload (BASELINE.json configs[1], "C2"): a 10k-server HashRing (100 replica points, ~1M
+tokens, built on the device) answering batched lookupN(key, 3) for 36-byte UUID-format keys.
+One step = one device pass over one resident batch of 2^26 keys (default 15 steps ≈ 1.0B
+lookups). Keys are synthetic (Philox UUID stream) and generated into HBM before
+the timed region. With --gpus N (torchrun, one rank per GPU) every rank builds its own copy
+of the ring and processes its own key stream: no data-path collective ("scaling": "weak").
+
+Printed (rank 0, one JSON line): value = lookupN(3)/s over all ranks, the dominant kernel's
+roofline (48 algorithmic bytes per lookupN(3): 36 B key read + 12 B owner write),
+and the CPU oracle timed on this host as cpu_baseline.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+BYTES_PER_LOOKUPN3 = 48  # 36 B key + 3 x 4 B owners
+METRIC = "ring lookups/s + member-updates merged/s; SWIM round time @100k members"
+
+
+def load_pkg():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ringpop_node_amd", os.path.join(REPO, "ringpop-node_amd", "__init__.py"))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["ringpop_node_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def c2_addr(i):
+    return "10.%d.%d.%d:%d" % ((i >> 16) & 255, (i >> 8) & 255, i & 255, 20800 + i % 36)
+
+
+def cpu_baseline(servers, nkeys, threads):
+    """The oracle (C restatement of lib/ring/index.js) on this host's cores: bounded sample."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle
+    ring = pyoracle.Ring(100)
+    ring.add_remove(servers)
+    keys = pyoracle.uuid_keys(42, 0, nkeys)
+    t0 = time.perf_counter()
+    ring.lookupn_keys(keys, 3, threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": nkeys / dt, "unit": "lookupN(3)/s", "cores": threads, "kind": "port",
+            "sample": "%d UUID keys, lookupN(key,3) on the 10k-server ring, oracle/orc_ring.c, "
+                      "%d pthreads (%.2f s)" % (nkeys, threads, dt)}
+
+
+def pmc_traffic():
+    p = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        d = json.load(f)
+    return d.get("lookupn_hbm_bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=15)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch-log2", type=int, default=26)
+    ap.add_argument("--servers", type=int, default=10000)
+    ap.add_argument("--nrep", type=int, default=3)
+    ap.add_argument("--cpu-keys", type=int, default=1 << 24)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    rpa = load_pkg()
+
+    servers = [c2_addr(i) for i in range(args.servers)]
+    t0 = time.perf_counter()
+    ring = rpa.HashRing(device=local)
+    ring.addRemoveServers(servers)
+    build_ms = (time.perf_counter() - t0) * 1e3
+
+    B = 1 << args.batch_log2
+    nbuf = min(4, max(1, args.steps))
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    keys = [torch.empty(B * 36, dtype=torch.uint8, device="cuda") for _ in range(nbuf)]
+    for j, kb in enumerate(keys):
+        rpa.gen_uuid_keys_dev(42, (rank << 40) + j * B, B, kb.data_ptr(), sp)
+    owners = torch.empty(B * args.nrep, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+
+    def step(s):
+        ring.lookupn_dev(keys[s % nbuf].data_ptr(), B, args.nrep, owners.data_ptr(), None, 36, None, sp)
+
+    for s in range(args.warmup):
+        step(s)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        ev[s][0].record(stream)
+        step(s)
+        ev[s][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms = float(t[0]), float(t[1])
+
+    total = B * args.steps * world
+    if rank == 0:
+        achieved = BYTES_PER_LOOKUPN3 * B / (kern_ms * 1e-3) / 1e9
+        traffic = pmc_traffic()
+        out = {
+            "metric": METRIC,
+            "value": total / elapsed,
+            "unit": "lookupN(3)/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (Philox UUID-v4-format keys, C2 server addresses)",
+            "config": {"workload": "C2: %d-server HashRing x 100 replica points, batched lookupN(n=%d) of "
+                                   "36-byte keys, 2^%d keys per step" % (args.servers, args.nrep, args.batch_log2),
+                       "servers": args.servers, "replica_points": 100, "tokens": ring.size,
+                       "keys_per_step": B, "total_keys": total, "parallelism": "keys sharded, ring replicated"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_lookupn_fixed<36,4>", "kernel_ms": kern_ms,
+                         "bytes_per_unit": BYTES_PER_LOOKUPN3},
+            "ring_build_ms": build_ms,
+        }
+        if not args.no_cpu:
+            th = args.cpu_threads or min(16, os.cpu_count() or 1)
+            out["cpu_baseline"] = cpu_baseline(servers, args.cpu_keys, th)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

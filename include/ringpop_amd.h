@@ -1,0 +1,110 @@
+/*
+ * ringpop_amd.h — C ABI of librpamd.so, the MI355X-native engine for ringpop-node's
+ * data-parallel core (hash ring, SWIM membership merge + checksum, gossip rounds).
+ *
+ * Drop-in boundary: these are the entry points a Node N-API addon (or any FFI) binds to
+ * replace the reference's in-process hot path. Each function names the reference
+ * interface it replaces (paths relative to ringpop v10.9.6). Conventions:
+ *   - every function returns 0 on success or a negative status; rp_last_error() gives the
+ *     thread-local message. Empty results are NOT errors (reference returns null / []).
+ *   - host pointers are borrowed for the duration of the call; *_dev variants take device
+ *     pointers and a HIP stream (void*; NULL = default stream) and are stream-ordered.
+ *   - owner ids are interned server ids (stable for the life of a ring); 0xFFFFFFFF = null.
+ *   - strings are byte ranges (UTF-8): `bytes` + `off[n+1]` (uint32 offsets) or a fixed
+ *     `stride`. Handles are not thread-safe (one HIP stream per handle).
+ */
+#ifndef RINGPOP_AMD_H
+#define RINGPOP_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RP_NULL_ID 0xFFFFFFFFu
+
+/* ------------------------------------------------------------------ common */
+const char *rp_last_error(void);
+/* Library/ABI version (major<<16 | minor). */
+uint32_t rp_version(void);
+/* Number of visible HIP devices (0 when none). */
+int rp_device_count(int *n);
+
+/* ------------------------------------------------------------------ farmhash32
+ * Replaces npm `farmhash` ^0.2.0 hash32 (reference package.json:34), called at
+ * lib/ring/index.js:29,55,102,140,146,166 and lib/membership/index.js:65.
+ * rp_hash32 is the host C++ implementation (the reference's addon is host C++ too);
+ * rp_hash32_batch_dev hashes n device strings (off: n+1 uint64 byte offsets). */
+uint32_t rp_hash32(const char *s, size_t len);
+int rp_hash32_batch_dev(const uint8_t *d_bytes, const uint64_t *d_off, uint64_t n, uint32_t *d_out,
+                        void *stream);
+
+/* Synthetic key stream: n UUID-v4-format 36-byte keys [k0, k0+n) of `seed`,
+ * written at 36-byte stride. */
+int rp_gen_uuid_keys_dev(uint32_t seed, uint64_t k0, uint64_t n, uint8_t *d_out, void *stream);
+
+/* ------------------------------------------------------------------ HashRing
+ * Replaces lib/ring/index.js HashRing (25-189) and its RBTree (lib/ring/rbtree.js) with a
+ * sorted token array in HBM. */
+typedef struct rp_ring rp_ring;
+
+/* new HashRing({replicaPoints}) (lib/ring/index.js:25-34); replica_points 0 => 100. */
+int rp_ring_create(uint32_t replica_points, int device, rp_ring **out);
+int rp_ring_destroy(rp_ring *r);
+
+/* addRemoveServers(serversToAdd, serversToRemove) (lib/ring/index.js:60-94); also the
+ * building block of addServer/removeServer (39-48, 124-133). Tokens are farmhash32 of
+ * server + String(i) computed on the device, unless add_tokens/rem_tokens (n*R uint32,
+ * row j = input server j) carry a caller hashFunc's values (options.hashFunc, :29).
+ * *changed_out = ringChanged. The checksum is recomputed on the device when changed. */
+int rp_ring_add_remove(rp_ring *r,
+                       const char *add_bytes, const uint32_t *add_off, uint32_t n_add,
+                       const uint32_t *add_tokens,
+                       const char *rem_bytes, const uint32_t *rem_off, uint32_t n_rem,
+                       const uint32_t *rem_tokens,
+                       int *changed_out);
+
+/* ring.checksum (lib/ring/index.js:33,96-105): farmhash32 of the sorted server names joined
+ * by ';'. *is_set = 0 while the reference value would still be null. */
+int rp_ring_checksum(rp_ring *r, uint32_t *out, int *is_set);
+/* The joined checksum string (for callers with a custom hashFunc): writes up to cap bytes,
+ * *len = full length. */
+int rp_ring_checksum_string(rp_ring *r, char *buf, uint64_t cap, uint64_t *len);
+/* getServerCount (:107-109), rbtree.size, hasServer (:118-120). */
+int rp_ring_server_count(rp_ring *r, uint32_t *out);
+int rp_ring_token_count(rp_ring *r, uint32_t *out);
+int rp_ring_has_server(rp_ring *r, const char *name, uint32_t len, int *out);
+/* Interned id of a name (RP_NULL_ID if never seen) and id -> name. */
+int rp_ring_server_id(rp_ring *r, const char *name, uint32_t len, uint32_t *id);
+const char *rp_ring_owner_name(rp_ring *r, uint32_t id, uint32_t *len);
+/* Object.keys(servers) in insertion order (getStats, :111-116): ids_out[cap], *n = count. */
+int rp_ring_servers(rp_ring *r, uint32_t *ids_out, uint32_t cap, uint32_t *n);
+/* Copy the sorted (token, owner) arrays to host (in-order rbtree walk). */
+int rp_ring_dump(rp_ring *r, uint32_t *tokens, uint32_t *owners, uint32_t cap);
+
+/* Batched lookup(key) (:145-154) and lookupN(key, n) (:157-189), host buffers in and out
+ * (PCIe-inclusive). Keys: stride > 0 => key i = keys[i*stride .. +stride); else
+ * keys[off[i] .. off[i+1]) with uint64 offsets. lookupN output rows have max(n,1) slots,
+ * unused = RP_NULL_ID; counts (nullable) = result length per key. */
+int rp_ring_lookup(rp_ring *r, const char *keys, const uint64_t *off, uint32_t stride, uint64_t n,
+                   uint32_t *owners);
+int rp_ring_lookupn(rp_ring *r, const char *keys, const uint64_t *off, uint32_t stride, uint64_t n,
+                    int32_t nrep, uint32_t *owners, uint8_t *counts);
+/* Same with precomputed key hashes (hashFunc(key) done by the caller). */
+int rp_ring_lookup_hashes(rp_ring *r, const uint32_t *hashes, uint64_t n, uint32_t *owners);
+int rp_ring_lookupn_hashes(rp_ring *r, const uint32_t *hashes, uint64_t n, int32_t nrep,
+                           uint32_t *owners, uint8_t *counts);
+/* Device-resident forms (the hot path): inputs already in HBM, stream-ordered, no sync. */
+int rp_ring_lookup_dev(rp_ring *r, const uint8_t *d_keys, const uint64_t *d_off, uint32_t stride,
+                       uint64_t n, uint32_t *d_owners, void *stream);
+int rp_ring_lookupn_dev(rp_ring *r, const uint8_t *d_keys, const uint64_t *d_off, uint32_t stride,
+                        uint64_t n, int32_t nrep, uint32_t *d_owners, uint8_t *d_counts, void *stream);
+int rp_ring_lookupn_hashes_dev(rp_ring *r, const uint32_t *d_hashes, uint64_t n, int32_t nrep,
+                               uint32_t *d_owners, uint8_t *d_counts, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

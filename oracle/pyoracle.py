@@ -1,0 +1,179 @@
+"""ctypes view of oracle/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+module, and only as the checker / the timed CPU baseline. The product package
+(ringpop-node_amd/) never imports it.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+NIL = 0xFFFFFFFF
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE, "all"])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        u32p = ctypes.POINTER(ctypes.c_uint32)
+        L.orc_hash32.restype = ctypes.c_uint32
+        L.orc_hash32.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+        L.orc_philox4x32_10.argtypes = [u32p, u32p, u32p]
+        L.orc_uuid_key.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_char_p]
+        L.orc_gen_uuid_keys.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
+        L.orc_c2_addr.restype = ctypes.c_int
+        L.orc_c2_addr.argtypes = [ctypes.c_uint32, ctypes.c_char_p]
+        L.orc_ring_new.restype = ctypes.c_void_p
+        L.orc_ring_new.argtypes = [ctypes.c_uint32]
+        L.orc_ring_free.argtypes = [ctypes.c_void_p]
+        L.orc_ring_add_remove.restype = ctypes.c_int
+        L.orc_ring_add_remove.argtypes = [ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+        L.orc_ring_checksum.restype = ctypes.c_int
+        L.orc_ring_checksum.argtypes = [ctypes.c_void_p, u32p]
+        L.orc_ring_server_count.restype = ctypes.c_uint32
+        L.orc_ring_server_count.argtypes = [ctypes.c_void_p]
+        L.orc_ring_token_count.restype = ctypes.c_uint32
+        L.orc_ring_token_count.argtypes = [ctypes.c_void_p]
+        L.orc_ring_name.restype = ctypes.c_void_p
+        L.orc_ring_name.argtypes = [ctypes.c_void_p, ctypes.c_uint32, u32p]
+        L.orc_ring_dump.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_ring_lookup_hash.restype = ctypes.c_uint32
+        L.orc_ring_lookup_hash.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        L.orc_ring_lookupn_hash.restype = ctypes.c_uint32
+        L.orc_ring_lookupn_hash.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int64, ctypes.c_void_p,
+                                            ctypes.c_uint32]
+        L.orc_ring_lookup_keys.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                           ctypes.c_uint64, ctypes.c_void_p]
+        L.orc_ring_lookupn_keys.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                            ctypes.c_uint64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_ring_lookupn_keys_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64,
+                                               ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+def hash32(s):
+    b = s.encode() if isinstance(s, str) else bytes(s)
+    return lib().orc_hash32(b, len(b))
+
+
+def philox(ctr, key):
+    c = (ctypes.c_uint32 * 4)(*ctr)
+    k = (ctypes.c_uint32 * 2)(*key)
+    o = (ctypes.c_uint32 * 4)()
+    lib().orc_philox4x32_10(c, k, o)
+    return list(o)
+
+
+def uuid_keys(seed, k0, n):
+    """n UUID-v4-format keys as a (n, 36) uint8 array (SURVEY §8d C1/C2 key stream)."""
+    buf = np.empty((n, 36), dtype=np.uint8)
+    lib().orc_gen_uuid_keys(seed, k0, n, buf.ctypes.data)
+    return buf
+
+
+def c2_addr(i):
+    b = ctypes.create_string_buffer(32)
+    n = lib().orc_c2_addr(i, b)
+    return b.raw[:n].decode()
+
+
+def pack_strings(strs):
+    bs = [s.encode() if isinstance(s, str) else bytes(s) for s in strs]
+    off = np.zeros(len(bs) + 1, dtype=np.uint32)
+    off[1:] = np.cumsum([len(b) for b in bs]) if bs else []
+    return b"".join(bs), off
+
+
+class Ring:
+    """Oracle HashRing (restates lib/ring/index.js)."""
+
+    def __init__(self, replica_points=100):
+        self.h = lib().orc_ring_new(replica_points)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_ring_free(self.h)
+            self.h = None
+
+    def add_remove(self, add=None, remove=None, add_tokens=None, rem_tokens=None):
+        add = add or []
+        remove = remove or []
+        ab, ao = pack_strings(add)
+        rb, ro = pack_strings(remove)
+        at = None if add_tokens is None else np.ascontiguousarray(add_tokens, dtype=np.uint32)
+        rt = None if rem_tokens is None else np.ascontiguousarray(rem_tokens, dtype=np.uint32)
+        abuf = ctypes.create_string_buffer(ab, len(ab) + 1)
+        rbuf = ctypes.create_string_buffer(rb, len(rb) + 1)
+        return bool(lib().orc_ring_add_remove(
+            self.h, abuf, ao.ctypes.data, len(add), None if at is None else at.ctypes.data,
+            rbuf, ro.ctypes.data, len(remove), None if rt is None else rt.ctypes.data))
+
+    @property
+    def checksum(self):
+        v = ctypes.c_uint32()
+        return v.value if lib().orc_ring_checksum(self.h, ctypes.byref(v)) else None
+
+    def server_count(self):
+        return lib().orc_ring_server_count(self.h)
+
+    def token_count(self):
+        return lib().orc_ring_token_count(self.h)
+
+    def name(self, i):
+        if i == NIL:
+            return None
+        n = ctypes.c_uint32()
+        p = lib().orc_ring_name(self.h, i, ctypes.byref(n))
+        return ctypes.string_at(p, n.value).decode()
+
+    def dump(self):
+        m = self.token_count()
+        t = np.empty(m, dtype=np.uint32)
+        o = np.empty(m, dtype=np.uint32)
+        lib().orc_ring_dump(self.h, t.ctypes.data, o.ctypes.data)
+        return t, o
+
+    def lookup_hash(self, h):
+        return lib().orc_ring_lookup_hash(self.h, h)
+
+    def lookupn_hash(self, h, n):
+        cap = self.server_count() + 2
+        buf = np.empty(cap, dtype=np.uint32)
+        c = lib().orc_ring_lookupn_hash(self.h, h, n, buf.ctypes.data, cap)
+        return [int(x) for x in buf[:c]]
+
+    def lookup_keys(self, keys):
+        keys = np.ascontiguousarray(keys, dtype=np.uint8)
+        n, stride = keys.shape
+        out = np.empty(n, dtype=np.uint32)
+        lib().orc_ring_lookup_keys(self.h, keys.ctypes.data, stride, None, n, out.ctypes.data)
+        return out
+
+    def lookupn_keys(self, keys, nrep, threads=1):
+        keys = np.ascontiguousarray(keys, dtype=np.uint8)
+        n, stride = keys.shape
+        w = max(nrep, 1)
+        out = np.empty((n, w), dtype=np.uint32)
+        cnt = np.empty(n, dtype=np.uint8)
+        if threads > 1:
+            lib().orc_ring_lookupn_keys_mt(self.h, keys.ctypes.data, stride, n, nrep, out.ctypes.data,
+                                           cnt.ctypes.data, threads)
+        else:
+            lib().orc_ring_lookupn_keys(self.h, keys.ctypes.data, stride, None, n, nrep, out.ctypes.data,
+                                        cnt.ctypes.data)
+        return out, cnt

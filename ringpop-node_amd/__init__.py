@@ -1,0 +1,345 @@
+"""ringpop-node_amd — Python host mirror of ringpop-node's hot-path API over librpamd.so.
+
+The compute lives in HIP kernels behind the C ABI in include/ringpop_amd.h; this module is a
+thin ctypes binding plus a `HashRing` class that keeps the reference's method names,
+argument meanings and error behaviour (lib/ring/index.js), so parity tests read like the
+reference's own tests (test/unit/ring-test.js, hashring_test.js). The Node N-API binding of
+the same C ABI lives in js/ (the drop-in for lib/ring).
+
+There is no CPU fallback: if librpamd.so is missing or no HIP device is visible, calls that
+need the GPU raise RingpopAmdError.
+
+The directory name contains a hyphen, so import it by path:
+    spec = importlib.util.spec_from_file_location("ringpop_node_amd", ".../ringpop-node_amd/__init__.py")
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librpamd.so")
+NULL_ID = 0xFFFFFFFF
+
+_lib = None
+
+
+class RingpopAmdError(RuntimeError):
+    pass
+
+
+def build(arch="gfx950", jobs=8):
+    """Compile librpamd.so in-tree (hipcc cross-compiles without a GPU)."""
+    subprocess.check_call(["make", "-s", "-j%d" % jobs, "-C", os.path.join(_HERE, "csrc"), "ARCH=" + arch])
+
+
+# name -> (restype, argtypes); every symbol declared in include/ringpop_amd.h
+_P = ctypes.c_void_p
+_U32 = ctypes.c_uint32
+_U64 = ctypes.c_uint64
+_I32 = ctypes.c_int32
+_INT = ctypes.c_int
+SIGNATURES = {
+    "rp_last_error": (ctypes.c_char_p, []),
+    "rp_version": (_U32, []),
+    "rp_device_count": (_INT, [_P]),
+    "rp_hash32": (_U32, [ctypes.c_char_p, ctypes.c_size_t]),
+    "rp_hash32_batch_dev": (_INT, [_P, _P, _U64, _P, _P]),
+    "rp_gen_uuid_keys_dev": (_INT, [_U32, _U64, _U64, _P, _P]),
+    "rp_ring_create": (_INT, [_U32, _INT, _P]),
+    "rp_ring_destroy": (_INT, [_P]),
+    "rp_ring_add_remove": (_INT, [_P, _P, _P, _U32, _P, _P, _P, _U32, _P, _P]),
+    "rp_ring_checksum": (_INT, [_P, _P, _P]),
+    "rp_ring_checksum_string": (_INT, [_P, _P, _U64, _P]),
+    "rp_ring_server_count": (_INT, [_P, _P]),
+    "rp_ring_token_count": (_INT, [_P, _P]),
+    "rp_ring_has_server": (_INT, [_P, _P, _U32, _P]),
+    "rp_ring_server_id": (_INT, [_P, _P, _U32, _P]),
+    "rp_ring_owner_name": (_P, [_P, _U32, _P]),
+    "rp_ring_servers": (_INT, [_P, _P, _U32, _P]),
+    "rp_ring_dump": (_INT, [_P, _P, _P, _U32]),
+    "rp_ring_lookup": (_INT, [_P, _P, _P, _U32, _U64, _P]),
+    "rp_ring_lookupn": (_INT, [_P, _P, _P, _U32, _U64, _I32, _P, _P]),
+    "rp_ring_lookup_hashes": (_INT, [_P, _P, _U64, _P]),
+    "rp_ring_lookupn_hashes": (_INT, [_P, _P, _U64, _I32, _P, _P]),
+    "rp_ring_lookup_dev": (_INT, [_P, _P, _P, _U32, _U64, _P, _P]),
+    "rp_ring_lookupn_dev": (_INT, [_P, _P, _P, _U32, _U64, _I32, _P, _P, _P]),
+    "rp_ring_lookupn_hashes_dev": (_INT, [_P, _P, _U64, _I32, _P, _P, _P]),
+}
+
+
+def lib():
+    """Load librpamd.so (fails loudly; there is no fallback implementation)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RingpopAmdError("librpamd.so not built: run `make -C ringpop-node_amd/csrc` "
+                                  "(or __graft_entry__.build())")
+        # PyTorch-ROCm bundles its own libamdhip64 (SONAME libamdhip64.so.7). Loading torch
+        # first makes librpamd bind to that same runtime instance, so device pointers and
+        # streams from torch tensors are valid in our kernels (one HIP runtime per process).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        raise RingpopAmdError("librpamd: %s (status %d)" % (lib().rp_last_error().decode(errors="replace"), rc))
+
+
+def device_count():
+    n = ctypes.c_int()
+    check(lib().rp_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def hash32(s):
+    """farmhash.hash32 (npm farmhash ^0.2.0) — host C++ farmhashmk::Hash32."""
+    b = s.encode() if isinstance(s, str) else bytes(s)
+    return lib().rp_hash32(b, len(b))
+
+
+def _pack(strs):
+    bs = [s.encode() if isinstance(s, str) else bytes(s) for s in strs]
+    off = np.zeros(len(bs) + 1, dtype=np.uint32)
+    if bs:
+        off[1:] = np.cumsum([len(b) for b in bs])
+    blob = b"".join(bs)
+    return ctypes.create_string_buffer(blob, len(blob) + 1), off
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def gen_uuid_keys_dev(seed, k0, n, out_ptr, stream=None):
+    """Fill a device buffer (>= 36*n bytes, 4-byte aligned) with the synthetic key stream."""
+    check(lib().rp_gen_uuid_keys_dev(seed, k0, n, out_ptr, stream))
+
+
+class HashRing:
+    """Mirror of lib/ring/index.js HashRing (25-189) backed by the device ring.
+
+    options: {'replicaPoints': int, 'hashFunc': callable(str)->uint32} as in the reference
+    constructor (lib/ring/index.js:25-34). Events 'added', 'removed', 'checksumComputed'.
+    """
+
+    def __init__(self, options=None, device=0):
+        self.options = dict(options or {})
+        self.replicaPoints = self.options.get("replicaPoints") or 100
+        self.hashFunc = self.options.get("hashFunc")  # None => device farmhash32
+        self._listeners = {}
+        h = ctypes.c_void_p()
+        check(lib().rp_ring_create(self.replicaPoints, device, ctypes.byref(h)))
+        self._h = h
+        self._names = {}
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().rp_ring_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- events (EventEmitter subset)
+    def on(self, ev, fn):
+        self._listeners.setdefault(ev, []).append(fn)
+        return self
+
+    def emit(self, ev, *args):
+        for fn in list(self._listeners.get(ev, [])):
+            fn(*args)
+
+    # -- mutation
+    def _tokens(self, names):
+        if self.hashFunc is None or not names:
+            return None
+        R = self.replicaPoints
+        return np.array([self.hashFunc(s + str(i)) & 0xFFFFFFFF for s in names for i in range(R)],
+                        dtype=np.uint32)
+
+    def addRemoveServers(self, serversToAdd=None, serversToRemove=None):
+        """lib/ring/index.js:60-94; returns ringChanged."""
+        add = list(serversToAdd or [])
+        rem = list(serversToRemove or [])
+        ab, ao = _pack(add)
+        rb, ro = _pack(rem)
+        at = self._tokens(add)
+        rt = self._tokens(rem)
+        changed = ctypes.c_int()
+        check(lib().rp_ring_add_remove(self._h, ab, ao.ctypes.data, len(add), _ptr(at),
+                                       rb, ro.ctypes.data, len(rem), _ptr(rt), ctypes.byref(changed)))
+        if changed.value:
+            self.emit("checksumComputed")
+        return bool(changed.value)
+
+    def addServer(self, name):
+        """lib/ring/index.js:39-48"""
+        if self.hasServer(name):
+            return
+        self.addRemoveServers([name], None)
+        self.emit("added", name)
+
+    def removeServer(self, name):
+        """lib/ring/index.js:124-133"""
+        if not self.hasServer(name):
+            return
+        self.addRemoveServers(None, [name])
+        self.emit("removed", name)
+
+    # -- state
+    @property
+    def checksum(self):
+        v, s = ctypes.c_uint32(), ctypes.c_int()
+        check(lib().rp_ring_checksum(self._h, ctypes.byref(v), ctypes.byref(s)))
+        if not s.value:
+            return None
+        if self.hashFunc is not None:
+            return self.hashFunc(self.checksum_string()) & 0xFFFFFFFF
+        return v.value
+
+    def checksum_string(self):
+        n = ctypes.c_uint64()
+        check(lib().rp_ring_checksum_string(self._h, None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(n.value + 1)
+        check(lib().rp_ring_checksum_string(self._h, buf, n.value, ctypes.byref(n)))
+        return buf.raw[:n.value].decode()
+
+    def getServerCount(self):
+        v = ctypes.c_uint32()
+        check(lib().rp_ring_server_count(self._h, ctypes.byref(v)))
+        return v.value
+
+    @property
+    def size(self):
+        """rbtree.size"""
+        v = ctypes.c_uint32()
+        check(lib().rp_ring_token_count(self._h, ctypes.byref(v)))
+        return v.value
+
+    def hasServer(self, name):
+        b = name.encode()
+        v = ctypes.c_int()
+        check(lib().rp_ring_has_server(self._h, b, len(b), ctypes.byref(v)))
+        return bool(v.value)
+
+    def server_ids(self):
+        n = ctypes.c_uint32()
+        check(lib().rp_ring_servers(self._h, None, 0, ctypes.byref(n)))
+        out = np.empty(max(n.value, 1), dtype=np.uint32)
+        check(lib().rp_ring_servers(self._h, out.ctypes.data, n.value, ctypes.byref(n)))
+        return out[:n.value]
+
+    @property
+    def servers(self):
+        return {self.name(i): True for i in self.server_ids()}
+
+    def getStats(self):
+        return {"checksum": self.checksum, "servers": [self.name(i) for i in self.server_ids()]}
+
+    def name(self, sid):
+        sid = int(sid)
+        if sid == NULL_ID:
+            return None
+        s = self._names.get(sid)
+        if s is None:
+            n = ctypes.c_uint32()
+            p = lib().rp_ring_owner_name(self._h, sid, ctypes.byref(n))
+            if not p:
+                raise RingpopAmdError("unknown server id %d" % sid)
+            s = ctypes.string_at(p, n.value).decode()
+            self._names[sid] = s
+        return s
+
+    def server_id(self, name):
+        b = name.encode()
+        v = ctypes.c_uint32()
+        check(lib().rp_ring_server_id(self._h, b, len(b), ctypes.byref(v)))
+        return v.value
+
+    def dump(self):
+        m = self.size
+        t = np.empty(max(m, 1), dtype=np.uint32)
+        o = np.empty(max(m, 1), dtype=np.uint32)
+        check(lib().rp_ring_dump(self._h, t.ctypes.data, o.ctypes.data, m))
+        return t[:m], o[:m]
+
+    # -- lookups (single-key reference API; batch forms below)
+    def lookup(self, key):
+        """lib/ring/index.js:145-154"""
+        ids = self.lookup_ids([str(key)])
+        return self.name(ids[0])
+
+    def lookupN(self, key, n):
+        """lib/ring/index.js:157-189"""
+        ids, cnt = self.lookupn_ids([str(key)], n)
+        return [self.name(x) for x in ids[0][:cnt[0]]]
+
+    def _key_pack(self, keys):
+        if isinstance(keys, np.ndarray) and keys.ndim == 2 and keys.dtype == np.uint8:
+            return np.ascontiguousarray(keys), None, keys.shape[1], keys.shape[0]
+        bs = [k.encode() if isinstance(k, str) else bytes(k) for k in keys]
+        off = np.zeros(len(bs) + 1, dtype=np.uint64)
+        if bs:
+            off[1:] = np.cumsum([len(b) for b in bs])
+        blob = np.frombuffer(b"".join(bs) + b"\0", dtype=np.uint8)
+        return blob, off, 0, len(bs)
+
+    def lookup_ids(self, keys):
+        """Batched lookup: owner ids (NULL_ID = null)."""
+        if self.hashFunc is not None:
+            hs = np.array([self.hashFunc(k) & 0xFFFFFFFF for k in keys], dtype=np.uint32)
+            return self.lookup_hashes(hs)
+        blob, off, stride, n = self._key_pack(keys)
+        out = np.empty(max(n, 1), dtype=np.uint32)
+        check(lib().rp_ring_lookup(self._h, blob.ctypes.data, _ptr(off), stride, n, out.ctypes.data))
+        return out[:n]
+
+    def lookupn_ids(self, keys, n):
+        """Batched lookupN: (owners[k, max(n,1)], counts[k])."""
+        if self.hashFunc is not None:
+            hs = np.array([self.hashFunc(k) & 0xFFFFFFFF for k in keys], dtype=np.uint32)
+            return self.lookupn_hashes(hs, n)
+        blob, off, stride, k = self._key_pack(keys)
+        w = max(int(n), 1)
+        out = np.empty((max(k, 1), w), dtype=np.uint32)
+        cnt = np.empty(max(k, 1), dtype=np.uint8)
+        check(lib().rp_ring_lookupn(self._h, blob.ctypes.data, _ptr(off), stride, k, int(n), out.ctypes.data,
+                                    cnt.ctypes.data))
+        return out[:k], cnt[:k]
+
+    def lookup_hashes(self, hashes):
+        hs = np.ascontiguousarray(hashes, dtype=np.uint32)
+        out = np.empty(max(len(hs), 1), dtype=np.uint32)
+        check(lib().rp_ring_lookup_hashes(self._h, hs.ctypes.data, len(hs), out.ctypes.data))
+        return out[:len(hs)]
+
+    def lookupn_hashes(self, hashes, n):
+        hs = np.ascontiguousarray(hashes, dtype=np.uint32)
+        w = max(int(n), 1)
+        out = np.empty((max(len(hs), 1), w), dtype=np.uint32)
+        cnt = np.empty(max(len(hs), 1), dtype=np.uint8)
+        check(lib().rp_ring_lookupn_hashes(self._h, hs.ctypes.data, len(hs), int(n), out.ctypes.data,
+                                           cnt.ctypes.data))
+        return out[:len(hs)], cnt[:len(hs)]
+
+    # -- device-resident hot path (pointers from torch tensors / hipMalloc)
+    def lookupn_dev(self, keys_ptr, n, nrep, owners_ptr, counts_ptr=None, stride=36, off_ptr=None, stream=None):
+        check(lib().rp_ring_lookupn_dev(self._h, keys_ptr, off_ptr, stride, n, nrep, owners_ptr, counts_ptr, stream))
+
+    def lookup_dev(self, keys_ptr, n, owners_ptr, stride=36, off_ptr=None, stream=None):
+        check(lib().rp_ring_lookup_dev(self._h, keys_ptr, off_ptr, stride, n, owners_ptr, stream))

@@ -1,0 +1,98 @@
+// rp_common.h — shared plumbing for the librpamd C-ABI: error slot, HIP checks, sizes.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <stdexcept>
+#include <string>
+
+namespace rp {
+
+// Thread-local last-error string behind rp_last_error() (SURVEY §8b "Errors").
+void set_error(const std::string& msg);
+const char* last_error();
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+enum : int {
+    RP_OK = 0,
+    RP_EINVAL = -1,
+    RP_EDEVICE = -2,
+    RP_ENOMEM = -3,
+    RP_ESTATE = -4,
+};
+
+#define RP_HIP(expr)                                                                          \
+    do {                                                                                      \
+        hipError_t rp_e_ = (expr);                                                            \
+        if (rp_e_ != hipSuccess)                                                              \
+            throw ::rp::Error(::rp::RP_EDEVICE, std::string(#expr) + ": " +                   \
+                                                    hipGetErrorString(rp_e_));                \
+    } while (0)
+
+#define RP_REQUIRE(cond, msg)                                                                 \
+    do {                                                                                      \
+        if (!(cond)) throw ::rp::Error(::rp::RP_EINVAL, (msg));                               \
+    } while (0)
+
+// Run a C-ABI body; convert exceptions into an int status + rp_last_error().
+template <class F>
+int guard(F&& f) {
+    try {
+        f();
+        return RP_OK;
+    } catch (const Error& e) {
+        set_error(e.what());
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        set_error("host out of memory");
+        return RP_ENOMEM;
+    } catch (const std::exception& e) {
+        set_error(e.what());
+        return RP_EINVAL;
+    }
+}
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline unsigned grid_for(uint64_t items, unsigned per_block, unsigned cap = 2048) {
+    uint64_t g = (items + per_block - 1) / per_block;
+    if (g == 0) g = 1;
+    return (unsigned)(g > cap ? cap : g);
+}
+
+// Device buffer with explicit capacity (owned by a handle; freed in its destructor).
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    uint64_t cap = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    void reserve(uint64_t n) {  // discards contents
+        if (n <= cap) return;
+        release();
+        uint64_t c = n < 64 ? 64 : n;
+        if (hipMalloc(&p, c * sizeof(T)) != hipSuccess) {
+            p = nullptr;
+            throw Error(RP_ENOMEM, "hipMalloc failed (" + std::to_string(c * sizeof(T)) + " bytes)");
+        }
+        cap = c;
+    }
+    void swap(DevBuf& o) {
+        std::swap(p, o.p);
+        std::swap(cap, o.cap);
+    }
+};
+
+}  // namespace rp

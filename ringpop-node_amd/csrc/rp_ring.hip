@@ -1,0 +1,956 @@
+// rp_ring.hip — the consistent hash ring on MI355X.
+//
+// Replaces lib/ring/index.js (HashRing) + lib/ring/rbtree.js (RBTree). The red-black tree is
+// an ordered map token -> owner with insert-if-absent and erase-by-key (rbtree.js:112-116,
+// 152-232); here it is a sorted uint32 token array + owner array in HBM, rebuilt per
+// addRemoveServers batch by: device farmhash of every replica string -> stable radix sort
+// -> drop in-batch duplicates and tokens already present (first insert wins) -> parallel
+// merge with the live array; removals mark-and-compact by token regardless of owner.
+// A 2^B bucket index over the top token bits bounds each lookup's search.
+//
+// Hot path: batched lookup / lookupN (lib/ring/index.js:145-189). One thread per key;
+// fixed-stride keys are staged through LDS with coalesced 16-B loads, hashed from
+// registers (fh::hash32_words), searched bucket-first, walked for distinct owners, and the
+// owner rows are staged back through LDS for coalesced stores.
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/ringpop_amd.h"
+#include "rp_farmhash.h"
+#include "rp_philox.h"
+#include "rp_prims.h"
+
+namespace rp {
+
+constexpr uint32_t NIL = 0xFFFFFFFFu;
+
+struct RingView {
+    const uint32_t* tok;
+    const uint32_t* own;
+    const uint32_t* bstart;  // 2^bbits + 1 entries
+    uint32_t M;
+    uint32_t shift;  // 32 - bbits
+};
+
+// first index i in [0, M] with tok[i] >= h (RBTree upperBound semantics, rbtree.js:235-271)
+__device__ __forceinline__ uint32_t ring_find(const RingView& rv, uint32_t h) {
+    const uint32_t b = h >> rv.shift;
+    uint32_t lo = rv.bstart[b], hi = rv.bstart[b + 1];
+    while (lo < hi) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (rv.tok[mid] < h) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// lookupN walk (lib/ring/index.js:157-189) with the result kept in registers (np <= MAXN).
+// Visits positions i%M, i%M+1, ... cyclically, at most M of them, stopping once np
+// distinct owners are collected. np <= 0 reproduces the reference's single loop body.
+template <int MAXN>
+__device__ __forceinline__ int ring_walk(const RingView& rv, uint32_t i, int np, uint32_t (&res)[MAXN]) {
+#pragma unroll
+    for (int q = 0; q < MAXN; q++) res[q] = NIL;
+    if (rv.M == 0) return 0;
+    if (np <= 0) {
+        if (i < rv.M) {
+            res[0] = rv.own[i];
+            return 1;
+        }
+        return 0;
+    }
+    uint32_t j = (i == rv.M) ? 0u : i;
+    if (MAXN == 1) {
+        res[0] = rv.own[j];
+        return 1;
+    }
+    int cnt = 0;
+    for (uint32_t steps = 0; steps < rv.M; steps++) {
+        const uint32_t o = rv.own[j];
+        bool dup = false;
+#pragma unroll
+        for (int q = 0; q < MAXN; q++) dup |= (q < cnt) & (res[q] == o);
+        if (!dup) {
+#pragma unroll
+            for (int q = 0; q < MAXN; q++) res[q] = (q == cnt) ? o : res[q];
+            cnt++;
+            if (cnt >= np) break;
+        }
+        j = (j + 1 == rv.M) ? 0u : j + 1;
+    }
+    return cnt;
+}
+
+// Unbounded walk writing straight to the output row (np > 8).
+__device__ int ring_walk_global(const RingView& rv, uint32_t i, int np, uint32_t* row, uint32_t W) {
+    for (uint32_t q = 0; q < W; q++) row[q] = NIL;
+    if (rv.M == 0) return 0;
+    if (np <= 0) {
+        if (i < rv.M) {
+            row[0] = rv.own[i];
+            return 1;
+        }
+        return 0;
+    }
+    uint32_t j = (i == rv.M) ? 0u : i;
+    int cnt = 0;
+    for (uint32_t steps = 0; steps < rv.M; steps++) {
+        const uint32_t o = rv.own[j];
+        bool dup = false;
+        for (int q = 0; q < cnt; q++)
+            if (row[q] == o) {
+                dup = true;
+                break;
+            }
+        if (!dup) {
+            row[cnt++] = o;
+            if (cnt >= np) break;
+        }
+        j = (j + 1 == rv.M) ? 0u : j + 1;
+    }
+    return cnt;
+}
+
+namespace {
+
+constexpr int kLkThreads = 256;
+
+// Fixed-stride keys (LEN % 4 == 0, LEN > 24, e.g. 36-byte UUIDs): LDS-staged hot kernel.
+template <int LEN, int MAXN>
+__global__ __launch_bounds__(kLkThreads) void k_lookupn_fixed(const uint8_t* __restrict__ keys, uint64_t n,
+                                                              RingView rv, int np, uint32_t W,
+                                                              uint32_t* __restrict__ out,
+                                                              uint8_t* __restrict__ counts) {
+    constexpr int W4 = LEN / 4;
+    __shared__ uint32_t sk[kLkThreads * W4];
+    __shared__ uint32_t so[kLkThreads * MAXN];
+    const int tid = threadIdx.x;
+    const bool kvec = ((reinterpret_cast<uintptr_t>(keys) & 15) == 0);
+    const bool ovec = ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
+    const uint64_t ntiles = (n + kLkThreads - 1) / kLkThreads;
+    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint64_t base = t * kLkThreads;
+        const uint32_t cnt = (uint32_t)((n - base) < (uint64_t)kLkThreads ? (n - base) : kLkThreads);
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(keys + base * LEN);
+        if (kvec && cnt == kLkThreads) {
+            const uint4* s4 = reinterpret_cast<const uint4*>(src);
+            uint4* d4 = reinterpret_cast<uint4*>(sk);
+            for (int k = tid; k < kLkThreads * W4 / 4; k += kLkThreads) d4[k] = s4[k];
+        } else {
+            for (uint32_t k = tid; k < cnt * W4; k += kLkThreads) sk[k] = src[k];
+        }
+        __syncthreads();
+        int c = 0;
+        uint32_t res[MAXN];
+        if ((uint32_t)tid < cnt) {
+            uint32_t w[W4];
+#pragma unroll
+            for (int j = 0; j < W4; j++) w[j] = sk[tid * W4 + j];
+            const uint32_t h = fh::hash32_words<LEN>(w);
+            const uint32_t i = ring_find(rv, h);
+            c = ring_walk<MAXN>(rv, i, np, res);
+#pragma unroll
+            for (int q = 0; q < MAXN; q++)
+                if ((uint32_t)q < W) so[tid * W + q] = res[q];
+            if (counts) counts[base + tid] = (uint8_t)c;
+        }
+        __syncthreads();
+        uint32_t* dst = out + base * W;
+        const uint32_t tot = cnt * W;
+        if (ovec && ((base * W) & 3) == 0 && cnt == kLkThreads && (tot & 3) == 0) {
+            uint4* d4 = reinterpret_cast<uint4*>(dst);
+            const uint4* s4 = reinterpret_cast<const uint4*>(so);
+            for (uint32_t k = tid; k < tot / 4; k += kLkThreads) d4[k] = s4[k];
+        } else {
+            for (uint32_t k = tid; k < tot; k += kLkThreads) dst[k] = so[k];
+        }
+        __syncthreads();
+    }
+}
+
+// Generic keys: per-thread byte fetches (variable length via uint64 offsets, or any stride),
+// or precomputed hashes (hashes != null).
+template <int MAXN>
+__global__ __launch_bounds__(kLkThreads) void k_lookupn_generic(const uint8_t* __restrict__ keys,
+                                                                const uint64_t* __restrict__ off,
+                                                                uint32_t stride,
+                                                                const uint32_t* __restrict__ hashes,
+                                                                uint64_t n, RingView rv, int np, uint32_t W,
+                                                                uint32_t* __restrict__ out,
+                                                                uint8_t* __restrict__ counts) {
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gstride) {
+        uint32_t h;
+        if (hashes) {
+            h = hashes[k];
+        } else {
+            uint64_t b, e;
+            if (stride) {
+                b = k * stride;
+                e = b + stride;
+            } else {
+                b = off[k];
+                e = off[k + 1];
+            }
+            h = fh::hash32(fh::PtrSrc{keys + b}, (uint32_t)(e - b));
+        }
+        const uint32_t i = ring_find(rv, h);
+        uint32_t* row = out + k * W;
+        int c;
+        if constexpr (MAXN > 0) {
+            uint32_t res[MAXN];
+            c = ring_walk<MAXN>(rv, i, np, res);
+#pragma unroll
+            for (int q = 0; q < MAXN; q++)
+                if ((uint32_t)q < W) row[q] = res[q];
+            for (uint32_t q = MAXN; q < W; q++) row[q] = NIL;
+        } else {
+            c = ring_walk_global(rv, i, np, row, W);
+        }
+        if (counts) counts[k] = (uint8_t)(c > 255 ? 255 : c);
+    }
+}
+
+// ---- build kernels ----
+
+// tokens[a*R + i] = farmhash32(name(ids[a]) + String(i)); owners likewise = ids[a].
+__global__ void k_replica_tokens(const uint8_t* __restrict__ names, const uint64_t* __restrict__ noff,
+                                 const uint32_t* __restrict__ ids, uint32_t n_srv, uint32_t R,
+                                 uint32_t* __restrict__ tok, uint32_t* __restrict__ own) {
+    const uint64_t total = (uint64_t)n_srv * R;
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total; k += gstride) {
+        const uint32_t a = (uint32_t)(k / R), i = (uint32_t)(k % R);
+        const uint32_t id = ids[a];
+        fh::ReplicaSrc s;
+        s.name = names + noff[id];
+        s.nlen = (uint32_t)(noff[id + 1] - noff[id]);
+        const uint32_t nd = fh::decimal(i, s.dig);
+        tok[k] = fh::hash32(s, s.nlen + nd);
+        own[k] = id;
+    }
+}
+
+// owners for caller-supplied tokens
+__global__ void k_expand_owner(const uint32_t* __restrict__ ids, uint32_t n_srv, uint32_t R,
+                               uint32_t* __restrict__ own) {
+    const uint64_t total = (uint64_t)n_srv * R;
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total; k += gstride)
+        own[k] = ids[k / R];
+}
+
+__device__ __forceinline__ uint32_t lower_bound_dev(const uint32_t* a, uint32_t n, uint32_t v) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// keep sorted-new token p iff first of its equal run (stable sort => first inserted) and
+// absent from the live ring (insert-if-absent, rbtree.js:112-116).
+__global__ void k_mark_new(const uint32_t* __restrict__ ntok, uint32_t K, const uint32_t* __restrict__ tok,
+                           uint32_t M, uint32_t* __restrict__ flag) {
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < K; p += gstride) {
+        const uint32_t t = ntok[p];
+        bool keep = (p == 0) || (ntok[p - 1] != t);
+        if (keep && M) {
+            const uint32_t i = lower_bound_dev(tok, M, t);
+            keep = !(i < M && tok[i] == t);
+        }
+        flag[p] = keep ? 1u : 0u;
+    }
+}
+
+__global__ void k_compact_pairs(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                const uint32_t* __restrict__ flag, const uint32_t* __restrict__ pos,
+                                uint32_t n, uint32_t* __restrict__ kout, uint32_t* __restrict__ vout) {
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gstride)
+        if (flag[p]) {
+            kout[pos[p]] = kin[p];
+            vout[pos[p]] = vin[p];
+        }
+}
+
+// Merge two sorted, mutually disjoint token arrays (rank = own index + rank in the other).
+__global__ void k_merge(const uint32_t* __restrict__ at, const uint32_t* __restrict__ ao, uint32_t na,
+                        const uint32_t* __restrict__ bt, const uint32_t* __restrict__ bo, uint32_t nb,
+                        uint32_t* __restrict__ ot, uint32_t* __restrict__ oo) {
+    const uint64_t total = (uint64_t)na + nb;
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < total; p += gstride) {
+        if (p < na) {
+            const uint32_t t = at[p];
+            const uint32_t d = (uint32_t)p + lower_bound_dev(bt, nb, t);
+            ot[d] = t;
+            oo[d] = ao[p];
+        } else {
+            const uint32_t q = (uint32_t)(p - na);
+            const uint32_t t = bt[q];
+            const uint32_t d = q + lower_bound_dev(at, na, t);
+            ot[d] = t;
+            oo[d] = bo[q];
+        }
+    }
+}
+
+// erase-by-key (rbtree.js:152-232): mark every live token equal to a removal token.
+__global__ void k_mark_del(const uint32_t* __restrict__ rtok, uint64_t K, const uint32_t* __restrict__ tok,
+                           uint32_t M, uint32_t* __restrict__ keep) {
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < K; p += gstride) {
+        const uint32_t t = rtok[p];
+        const uint32_t i = lower_bound_dev(tok, M, t);
+        if (i < M && tok[i] == t) keep[i] = 0u;
+    }
+}
+
+__global__ void k_fill_u32(uint32_t* p, uint64_t n, uint32_t v) {
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gstride) p[i] = v;
+}
+
+__global__ void k_bucket_index(const uint32_t* __restrict__ tok, uint32_t M, uint32_t bbits,
+                               uint32_t* __restrict__ bstart) {
+    const uint64_t nbk = (1ull << bbits);
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b <= nbk; b += gstride) {
+        if (b == nbk) bstart[b] = M;
+        else bstart[b] = lower_bound_dev(tok, M, (uint32_t)(b << (32 - bbits)));
+    }
+}
+
+// big-endian 4-byte chunk c of name(ids[i]) (0-padded): the LSD key for lexicographic order.
+__global__ void k_name_chunk(const uint8_t* __restrict__ names, const uint64_t* __restrict__ noff,
+                             const uint32_t* __restrict__ ids, uint32_t n, uint32_t c,
+                             uint32_t* __restrict__ key) {
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gstride) {
+        const uint32_t id = ids[i];
+        const uint64_t b = noff[id];
+        const uint32_t L = (uint32_t)(noff[id + 1] - b);
+        uint32_t k = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t o = c * 4 + q;
+            k = (k << 8) | (o < L ? names[b + o] : 0u);
+        }
+        key[i] = k;
+    }
+}
+
+// checksum string pieces: len of (name + ';') for in-ring servers in name order.
+__global__ void k_ck_len(const uint32_t* __restrict__ sorted_ids, uint32_t n,
+                         const uint8_t* __restrict__ in_ring, const uint64_t* __restrict__ noff,
+                         uint32_t* __restrict__ len) {
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gstride) {
+        const uint32_t id = sorted_ids[i];
+        len[i] = in_ring[id] ? (uint32_t)(noff[id + 1] - noff[id]) + 1u : 0u;
+    }
+}
+
+__global__ void k_ck_scatter(const uint32_t* __restrict__ sorted_ids, uint32_t n,
+                             const uint8_t* __restrict__ in_ring, const uint8_t* __restrict__ names,
+                             const uint64_t* __restrict__ noff, const uint32_t* __restrict__ pos,
+                             uint8_t* __restrict__ buf) {
+    // one wave per name: lanes copy bytes
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wid = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t i = wid; i < n; i += nw) {
+        const uint32_t id = sorted_ids[i];
+        if (!in_ring[id]) continue;
+        const uint64_t b = noff[id];
+        const uint32_t L = (uint32_t)(noff[id + 1] - b);
+        const uint32_t p = pos[i];
+        for (uint32_t q = lane; q < L; q += 64) buf[p + q] = names[b + q];
+        if (lane == 0) buf[p + L] = ';';
+    }
+}
+
+// Serial farmhash32 of one long device string (the checksum): one lane; the string is
+// streamed through LDS in 16 KiB windows loaded cooperatively by the workgroup.
+__global__ __launch_bounds__(256) void k_hash_one(const uint8_t* __restrict__ s, uint64_t len,
+                                                  uint32_t* __restrict__ out) {
+    if (threadIdx.x == 0) *out = fh::hash32(fh::PtrSrc{s}, (uint32_t)len);
+}
+
+__global__ void k_hash_batch(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t n,
+                             uint32_t* __restrict__ out) {
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gstride)
+        out[k] = fh::hash32(fh::PtrSrc{bytes + off[k]}, (uint32_t)(off[k + 1] - off[k]));
+}
+
+__global__ void k_gen_uuid(uint32_t seed, uint64_t k0, uint64_t n, uint32_t* __restrict__ out) {
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gstride) {
+        uint32_t w[9];
+        uuid_key_words(seed, k0 + k, w);
+#pragma unroll
+        for (int j = 0; j < 9; j++) out[k * 9 + j] = w[j];
+    }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------- handle
+
+struct Ring {
+    int device = 0;
+    hipStream_t st = nullptr;
+    uint32_t R = 100;
+    // interned names (host mirror of JS `servers` keys + an id table)
+    std::vector<std::string> names;
+    std::unordered_map<std::string, uint32_t> ids;
+    std::vector<uint8_t> in_ring;
+    std::vector<uint64_t> stamp;  // insertion stamp -> Object.keys order
+    uint64_t next_stamp = 1;
+    uint32_t server_count = 0;
+    bool has_checksum = false;
+    uint32_t checksum = 0;
+    // device name table
+    DevBuf<uint8_t> d_names;
+    DevBuf<uint64_t> d_noff;
+    uint64_t dev_name_bytes = 0;
+    uint32_t dev_names = 0;
+    std::vector<uint64_t> h_noff{0};
+    std::vector<uint8_t> h_nbytes;
+    // ring arrays
+    DevBuf<uint32_t> tok, own, tok2, own2, bstart;
+    uint32_t M = 0;
+    uint32_t bbits = 8;
+    // name order for checksums
+    DevBuf<uint32_t> sorted_ids;
+    uint32_t sorted_n = 0;
+    DevBuf<uint8_t> d_inring;
+    DevBuf<uint8_t> ck_buf;
+    uint64_t ck_len = 0;
+    // scratch
+    DevBuf<uint32_t> nt, no, flag, pos, ids_dev, tmpk;
+    DevBuf<uint64_t> tmp64;
+    DevBuf<uint32_t> scalar;
+    DevBuf<uint32_t> io_a, io_b;
+    DevBuf<uint8_t> io_keys, io_cnt;
+    DevBuf<uint64_t> io_off;
+    Scratch ws;
+
+    RingView view() const {
+        return RingView{tok.p, own.p, bstart.p, M, 32u - bbits};
+    }
+};
+
+static void ring_sync_names(Ring& r) {
+    if (r.dev_names == r.names.size()) return;
+    const uint64_t nbytes = r.h_nbytes.size();
+    const uint32_t nn = (uint32_t)r.names.size();
+    // grow-and-reupload (name tables are small: tens of bytes per server)
+    r.d_names.reserve(nbytes + 16);
+    r.d_noff.reserve((uint64_t)nn + 1);
+    if (nbytes) RP_HIP(hipMemcpyAsync(r.d_names.p, r.h_nbytes.data(), nbytes, hipMemcpyHostToDevice, r.st));
+    RP_HIP(hipMemcpyAsync(r.d_noff.p, r.h_noff.data(), sizeof(uint64_t) * (nn + 1), hipMemcpyHostToDevice, r.st));
+    r.dev_names = nn;
+    r.dev_name_bytes = nbytes;
+}
+
+static uint32_t ring_intern(Ring& r, const char* s, uint32_t n) {
+    std::string key(s, n);
+    auto it = r.ids.find(key);
+    if (it != r.ids.end()) return it->second;
+    const uint32_t id = (uint32_t)r.names.size();
+    r.ids.emplace(key, id);
+    r.names.push_back(key);
+    r.in_ring.push_back(0);
+    r.stamp.push_back(0);
+    r.h_nbytes.insert(r.h_nbytes.end(), key.begin(), key.end());
+    r.h_noff.push_back(r.h_nbytes.size());
+    return id;
+}
+
+static uint32_t choose_bbits(uint32_t M) {
+    // ~4 tokens per bucket: a bounded 2-3 step search inside one or two cache lines.
+    uint32_t b = 8;
+    while (b < 22 && (1ull << (b + 2)) < M) b++;
+    return b;
+}
+
+static void ring_rebuild_index(Ring& r) {
+    r.bbits = choose_bbits(r.M);
+    const uint64_t nbk = (1ull << r.bbits) + 1;
+    r.bstart.reserve(nbk);
+    hipLaunchKernelGGL(k_bucket_index, dim3(grid_for(nbk, 256)), dim3(256), 0, r.st, r.tok.p, r.M, r.bbits,
+                       r.bstart.p);
+    RP_HIP(hipGetLastError());
+}
+
+// Device replica tokens for server ids (or caller tokens), sorted stably by token.
+static uint64_t ring_make_tokens(Ring& r, const std::vector<uint32_t>& sel_ids, const std::vector<uint32_t>* custom) {
+    const uint64_t K = (uint64_t)sel_ids.size() * r.R;
+    RP_REQUIRE(K < (1ull << 31), "too many replica points in one batch");
+    r.nt.reserve(K + 1);
+    r.no.reserve(K + 1);
+    r.ids_dev.reserve(sel_ids.size() + 1);
+    RP_HIP(hipMemcpyAsync(r.ids_dev.p, sel_ids.data(), sizeof(uint32_t) * sel_ids.size(), hipMemcpyHostToDevice,
+                          r.st));
+    if (custom) {
+        RP_HIP(hipMemcpyAsync(r.nt.p, custom->data(), sizeof(uint32_t) * K, hipMemcpyHostToDevice, r.st));
+        hipLaunchKernelGGL(k_expand_owner, dim3(grid_for(K, 256)), dim3(256), 0, r.st, r.ids_dev.p,
+                           (uint32_t)sel_ids.size(), r.R, r.no.p);
+    } else {
+        hipLaunchKernelGGL(k_replica_tokens, dim3(grid_for(K, 256)), dim3(256), 0, r.st, r.d_names.p, r.d_noff.p,
+                           r.ids_dev.p, (uint32_t)sel_ids.size(), r.R, r.nt.p, r.no.p);
+    }
+    RP_HIP(hipGetLastError());
+    return K;
+}
+
+static void ring_apply_adds(Ring& r, const std::vector<uint32_t>& add_ids, const std::vector<uint32_t>* custom) {
+    if (add_ids.empty()) return;
+    const uint64_t K = ring_make_tokens(r, add_ids, custom);
+    radix_sort_pairs(r.nt.p, r.no.p, K, 0, 32, r.st, r.ws);
+    r.flag.reserve(K + 1);
+    r.pos.reserve(K + 1);
+    hipLaunchKernelGGL(k_mark_new, dim3(grid_for(K, 256)), dim3(256), 0, r.st, r.nt.p, (uint32_t)K, r.tok.p, r.M,
+                       r.flag.p);
+    RP_HIP(hipGetLastError());
+    scan_exclusive_u32(r.flag.p, r.pos.p, K, r.st, r.ws);
+    const uint32_t Kp = read_u32(r.pos.p + K, r.st);
+    r.tmpk.reserve((uint64_t)Kp + 1);
+    r.ws.c.reserve((uint64_t)Kp + 1);
+    hipLaunchKernelGGL(k_compact_pairs, dim3(grid_for(K, 256)), dim3(256), 0, r.st, r.nt.p, r.no.p, r.flag.p,
+                       r.pos.p, (uint32_t)K, r.tmpk.p, r.ws.c.p);
+    const uint64_t nM = (uint64_t)r.M + Kp;
+    RP_REQUIRE(nM < 0xFFFFFFF0ull, "ring too large");
+    r.tok2.reserve(nM + 1);
+    r.own2.reserve(nM + 1);
+    hipLaunchKernelGGL(k_merge, dim3(grid_for(nM, 256)), dim3(256), 0, r.st, r.tok.p, r.own.p, r.M, r.tmpk.p,
+                       r.ws.c.p, Kp, r.tok2.p, r.own2.p);
+    RP_HIP(hipGetLastError());
+    r.tok.swap(r.tok2);
+    r.own.swap(r.own2);
+    r.M = (uint32_t)nM;
+}
+
+static void ring_apply_removes(Ring& r, const std::vector<uint32_t>& rem_ids, const std::vector<uint32_t>* custom) {
+    if (rem_ids.empty() || r.M == 0) return;
+    const uint64_t K = ring_make_tokens(r, rem_ids, custom);
+    r.flag.reserve((uint64_t)r.M + 1);
+    r.pos.reserve((uint64_t)r.M + 1);
+    hipLaunchKernelGGL(k_fill_u32, dim3(grid_for(r.M, 256)), dim3(256), 0, r.st, r.flag.p, (uint64_t)r.M, 1u);
+    hipLaunchKernelGGL(k_mark_del, dim3(grid_for(K, 256)), dim3(256), 0, r.st, r.nt.p, K, r.tok.p, r.M, r.flag.p);
+    RP_HIP(hipGetLastError());
+    scan_exclusive_u32(r.flag.p, r.pos.p, r.M, r.st, r.ws);
+    const uint32_t nM = read_u32(r.pos.p + r.M, r.st);
+    r.tok2.reserve((uint64_t)nM + 1);
+    r.own2.reserve((uint64_t)nM + 1);
+    hipLaunchKernelGGL(k_compact_pairs, dim3(grid_for(r.M, 256)), dim3(256), 0, r.st, r.tok.p, r.own.p, r.flag.p,
+                       r.pos.p, r.M, r.tok2.p, r.own2.p);
+    RP_HIP(hipGetLastError());
+    r.tok.swap(r.tok2);
+    r.own.swap(r.own2);
+    r.M = nM;
+}
+
+// Sort all interned names lexicographically (bytes; == JS default sort for ASCII).
+static void ring_sort_names(Ring& r) {
+    const uint32_t n = (uint32_t)r.names.size();
+    if (r.sorted_n == n) return;
+    uint32_t Lmax = 0;
+    for (auto& s : r.names) Lmax = std::max<uint32_t>(Lmax, (uint32_t)s.size());
+    r.sorted_ids.reserve((uint64_t)n + 1);
+    r.tmpk.reserve((uint64_t)n + 1);
+    iota_u32(r.sorted_ids.p, n, r.st);
+    const uint32_t nchunks = (Lmax + 3) / 4;
+    for (int c = (int)nchunks - 1; c >= 0; c--) {
+        hipLaunchKernelGGL(k_name_chunk, dim3(grid_for(n, 256)), dim3(256), 0, r.st, r.d_names.p, r.d_noff.p,
+                           r.sorted_ids.p, n, (uint32_t)c, r.tmpk.p);
+        RP_HIP(hipGetLastError());
+        radix_sort_pairs(r.tmpk.p, r.sorted_ids.p, n, 0, 32, r.st, r.ws);
+    }
+    r.sorted_n = n;
+}
+
+// HashRing.computeChecksum (lib/ring/index.js:96-105) on the device.
+static void ring_compute_checksum(Ring& r) {
+    ring_sort_names(r);
+    const uint32_t n = (uint32_t)r.names.size();
+    r.d_inring.reserve((uint64_t)n + 1);
+    if (n) RP_HIP(hipMemcpyAsync(r.d_inring.p, r.in_ring.data(), n, hipMemcpyHostToDevice, r.st));
+    r.flag.reserve((uint64_t)n + 1);
+    r.pos.reserve((uint64_t)n + 1);
+    uint64_t total = 0;
+    if (n) {
+        hipLaunchKernelGGL(k_ck_len, dim3(grid_for(n, 256)), dim3(256), 0, r.st, r.sorted_ids.p, n, r.d_inring.p,
+                           r.d_noff.p, r.flag.p);
+        scan_exclusive_u32(r.flag.p, r.pos.p, n, r.st, r.ws);
+        total = read_u32(r.pos.p + n, r.st);
+    }
+    const uint64_t L = total ? total - 1 : 0;  // join(';') has no trailing separator
+    r.ck_buf.reserve(total + 8);
+    if (n && total) {
+        hipLaunchKernelGGL(k_ck_scatter, dim3(grid_for((uint64_t)n * 64, 256)), dim3(256), 0, r.st,
+                           r.sorted_ids.p, n, r.d_inring.p, r.d_names.p, r.d_noff.p, r.pos.p, r.ck_buf.p);
+        RP_HIP(hipGetLastError());
+    }
+    r.scalar.reserve(4);
+    hipLaunchKernelGGL(k_hash_one, dim3(1), dim3(256), 0, r.st, r.ck_buf.p, L, r.scalar.p);
+    RP_HIP(hipGetLastError());
+    r.checksum = read_u32(r.scalar.p, r.st);
+    r.has_checksum = true;
+    r.ck_len = L;
+}
+
+static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, uint32_t stride,
+                           const uint32_t* hashes, uint64_t n, int np, uint32_t W, uint32_t* out, uint8_t* counts,
+                           hipStream_t st) {
+    if (n == 0) return;
+    const RingView rv = r.view();
+    const unsigned grid_fixed = grid_for(n, kLkThreads, 256 * 8);
+    const bool fixed36 = !hashes && stride == 36 && ((reinterpret_cast<uintptr_t>(keys) & 3) == 0);
+    const int need = np <= 0 ? 1 : np;
+    if (fixed36 && W <= 8 && need <= 8) {
+        if (need == 1 && W == 1)
+            hipLaunchKernelGGL((k_lookupn_fixed<36, 1>), dim3(grid_fixed), dim3(kLkThreads), 0, st, keys, n, rv, np,
+                               W, out, counts);
+        else if (need <= 4 && W <= 4)
+            hipLaunchKernelGGL((k_lookupn_fixed<36, 4>), dim3(grid_fixed), dim3(kLkThreads), 0, st, keys, n, rv, np,
+                               W, out, counts);
+        else
+            hipLaunchKernelGGL((k_lookupn_fixed<36, 8>), dim3(grid_fixed), dim3(kLkThreads), 0, st, keys, n, rv, np,
+                               W, out, counts);
+    } else {
+        const unsigned g = grid_for(n, 256, 256 * 8);
+        if (need == 1)
+            hipLaunchKernelGGL((k_lookupn_generic<1>), dim3(g), dim3(256), 0, st, keys, off, stride, hashes, n, rv,
+                               np, W, out, counts);
+        else if (need <= 4)
+            hipLaunchKernelGGL((k_lookupn_generic<4>), dim3(g), dim3(256), 0, st, keys, off, stride, hashes, n, rv,
+                               np, W, out, counts);
+        else if (need <= 8)
+            hipLaunchKernelGGL((k_lookupn_generic<8>), dim3(g), dim3(256), 0, st, keys, off, stride, hashes, n, rv,
+                               np, W, out, counts);
+        else
+            hipLaunchKernelGGL((k_lookupn_generic<0>), dim3(g), dim3(256), 0, st, keys, off, stride, hashes, n, rv,
+                               np, W, out, counts);
+    }
+    RP_HIP(hipGetLastError());
+}
+
+}  // namespace rp
+
+// ==================================================================================== C ABI
+
+struct rp_ring {
+    rp::Ring impl;
+};
+
+using rp::guard;
+
+static rp::Ring& R(rp_ring* r) {
+    if (!r) throw rp::Error(rp::RP_EINVAL, "null ring handle");
+    RP_HIP(hipSetDevice(r->impl.device));
+    return r->impl;
+}
+
+extern "C" {
+
+int rp_ring_create(uint32_t replica_points, int device, rp_ring** out) {
+    return guard([&] {
+        RP_REQUIRE(out, "out is null");
+        int nd = 0;
+        RP_HIP(hipGetDeviceCount(&nd));
+        RP_REQUIRE(device >= 0 && device < nd, "no such HIP device");
+        RP_HIP(hipSetDevice(device));
+        auto* h = new rp_ring();
+        h->impl.device = device;
+        h->impl.R = replica_points ? replica_points : 100;
+        hipError_t e = hipStreamCreateWithFlags(&h->impl.st, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            delete h;
+            throw rp::Error(rp::RP_EDEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+        }
+        h->impl.tok.reserve(64);
+        h->impl.own.reserve(64);
+        rp::ring_rebuild_index(h->impl);
+        *out = h;
+    });
+}
+
+int rp_ring_destroy(rp_ring* r) {
+    return guard([&] {
+        if (!r) return;
+        (void)hipSetDevice(r->impl.device);
+        if (r->impl.st) {
+            (void)hipStreamSynchronize(r->impl.st);
+            (void)hipStreamDestroy(r->impl.st);
+        }
+        delete r;
+    });
+}
+
+int rp_ring_add_remove(rp_ring* h, const char* add_bytes, const uint32_t* add_off, uint32_t n_add,
+                       const uint32_t* add_tokens, const char* rem_bytes, const uint32_t* rem_off, uint32_t n_rem,
+                       const uint32_t* rem_tokens, int* changed_out) {
+    return guard([&] {
+        rp::Ring& r = R(h);
+        RP_REQUIRE(n_add == 0 || (add_bytes && add_off), "add names missing");
+        RP_REQUIRE(n_rem == 0 || (rem_bytes && rem_off), "remove names missing");
+        // lib/ring/index.js:69-76 — adds in order, skipping servers already present
+        std::vector<uint32_t> add_ids, rem_ids;
+        std::vector<uint32_t> add_tok_sel, rem_tok_sel;
+        for (uint32_t j = 0; j < n_add; j++) {
+            const uint32_t id = rp::ring_intern(r, add_bytes + add_off[j], add_off[j + 1] - add_off[j]);
+            if (r.in_ring[id]) continue;
+            r.in_ring[id] = 1;
+            r.stamp[id] = r.next_stamp++;
+            r.server_count++;
+            add_ids.push_back(id);
+            if (add_tokens)
+                add_tok_sel.insert(add_tok_sel.end(), add_tokens + (uint64_t)j * r.R,
+                                   add_tokens + (uint64_t)(j + 1) * r.R);
+        }
+        // :78-85 — then removes in order, skipping absent servers
+        for (uint32_t j = 0; j < n_rem; j++) {
+            std::string key(rem_bytes + rem_off[j], rem_off[j + 1] - rem_off[j]);
+            auto it = r.ids.find(key);
+            if (it == r.ids.end() || !r.in_ring[it->second]) continue;
+            const uint32_t id = it->second;
+            r.in_ring[id] = 0;
+            r.server_count--;
+            rem_ids.push_back(id);
+            if (rem_tokens)
+                rem_tok_sel.insert(rem_tok_sel.end(), rem_tokens + (uint64_t)j * r.R,
+                                   rem_tokens + (uint64_t)(j + 1) * r.R);
+        }
+        const bool changed = !add_ids.empty() || !rem_ids.empty();
+        if (changed) {
+            rp::ring_sync_names(r);
+            rp::ring_apply_adds(r, add_ids, add_tokens ? &add_tok_sel : nullptr);
+            rp::ring_apply_removes(r, rem_ids, rem_tokens ? &rem_tok_sel : nullptr);
+            rp::ring_rebuild_index(r);
+            rp::ring_compute_checksum(r);  // (89-91)
+            RP_HIP(hipStreamSynchronize(r.st));
+        }
+        if (changed_out) *changed_out = changed ? 1 : 0;
+    });
+}
+
+int rp_ring_checksum(rp_ring* h, uint32_t* out, int* is_set) {
+    return guard([&] {
+        rp::Ring& r = R(h);
+        if (out) *out = r.checksum;
+        if (is_set) *is_set = r.has_checksum ? 1 : 0;
+    });
+}
+
+int rp_ring_checksum_string(rp_ring* h, char* buf, uint64_t cap, uint64_t* len) {
+    return guard([&] {
+        rp::Ring& r = R(h);
+        if (len) *len = r.ck_len;
+        const uint64_t n = std::min<uint64_t>(cap, r.ck_len);
+        if (buf && n) {
+            RP_HIP(hipMemcpyAsync(buf, r.ck_buf.p, n, hipMemcpyDeviceToHost, r.st));
+            RP_HIP(hipStreamSynchronize(r.st));
+        }
+    });
+}
+
+int rp_ring_server_count(rp_ring* h, uint32_t* out) {
+    return guard([&] { *out = R(h).server_count; });
+}
+
+int rp_ring_token_count(rp_ring* h, uint32_t* out) {
+    return guard([&] { *out = R(h).M; });
+}
+
+int rp_ring_has_server(rp_ring* h, const char* name, uint32_t len, int* out) {
+    return guard([&] {
+        rp::Ring& r = R(h);
+        auto it = r.ids.find(std::string(name, len));
+        *out = (it != r.ids.end() && r.in_ring[it->second]) ? 1 : 0;
+    });
+}
+
+int rp_ring_server_id(rp_ring* h, const char* name, uint32_t len, uint32_t* id) {
+    return guard([&] {
+        rp::Ring& r = R(h);
+        auto it = r.ids.find(std::string(name, len));
+        *id = it == r.ids.end() ? RP_NULL_ID : it->second;
+    });
+}
+
+const char* rp_ring_owner_name(rp_ring* h, uint32_t id, uint32_t* len) {
+    if (!h || id >= h->impl.names.size()) {
+        if (len) *len = 0;
+        return nullptr;
+    }
+    if (len) *len = (uint32_t)h->impl.names[id].size();
+    return h->impl.names[id].data();
+}
+
+int rp_ring_servers(rp_ring* h, uint32_t* ids_out, uint32_t cap, uint32_t* n) {
+    return guard([&] {
+        rp::Ring& r = R(h);
+        std::vector<uint32_t> v;
+        for (uint32_t id = 0; id < r.names.size(); id++)
+            if (r.in_ring[id]) v.push_back(id);
+        std::sort(v.begin(), v.end(), [&](uint32_t a, uint32_t b) { return r.stamp[a] < r.stamp[b]; });
+        *n = (uint32_t)v.size();
+        for (uint32_t i = 0; i < v.size() && i < cap; i++) ids_out[i] = v[i];
+    });
+}
+
+int rp_ring_dump(rp_ring* h, uint32_t* tokens, uint32_t* owners, uint32_t cap) {
+    return guard([&] {
+        rp::Ring& r = R(h);
+        const uint32_t n = std::min(cap, r.M);
+        if (n) {
+            if (tokens) RP_HIP(hipMemcpyAsync(tokens, r.tok.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, r.st));
+            if (owners) RP_HIP(hipMemcpyAsync(owners, r.own.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, r.st));
+        }
+        RP_HIP(hipStreamSynchronize(r.st));
+    });
+}
+
+// ---- lookups
+
+static int np_for(rp::Ring& r, int32_t nrep) {
+    int64_t n = nrep;
+    if (n > (int64_t)r.server_count) n = r.server_count;  // lib/ring/index.js:159-162
+    return (int)n;
+}
+
+int rp_ring_lookupn_dev(rp_ring* h, const uint8_t* d_keys, const uint64_t* d_off, uint32_t stride, uint64_t n,
+                        int32_t nrep, uint32_t* d_owners, uint8_t* d_counts, void* stream) {
+    return guard([&] {
+        rp::Ring& r = R(h);
+        RP_REQUIRE(n == 0 || (d_keys && d_owners && (stride || d_off)), "lookupn_dev: null buffer");
+        const uint32_t W = nrep > 1 ? (uint32_t)nrep : 1u;
+        rp::launch_lookupn(r, d_keys, d_off, stride, nullptr, n, np_for(r, nrep), W, d_owners, d_counts,
+                           rp::as_stream(stream));
+    });
+}
+
+int rp_ring_lookup_dev(rp_ring* h, const uint8_t* d_keys, const uint64_t* d_off, uint32_t stride, uint64_t n,
+                       uint32_t* d_owners, void* stream) {
+    return guard([&] {
+        rp::Ring& r = R(h);
+        RP_REQUIRE(n == 0 || (d_keys && d_owners && (stride || d_off)), "lookup_dev: null buffer");
+        // lookup (:145-154) == a one-step walk, independent of getServerCount
+        rp::launch_lookupn(r, d_keys, d_off, stride, nullptr, n, 1, 1, d_owners, nullptr, rp::as_stream(stream));
+    });
+}
+
+int rp_ring_lookupn_hashes_dev(rp_ring* h, const uint32_t* d_hashes, uint64_t n, int32_t nrep, uint32_t* d_owners,
+                               uint8_t* d_counts, void* stream) {
+    return guard([&] {
+        rp::Ring& r = R(h);
+        RP_REQUIRE(n == 0 || (d_hashes && d_owners), "lookupn_hashes_dev: null buffer");
+        const uint32_t W = nrep > 1 ? (uint32_t)nrep : 1u;
+        rp::launch_lookupn(r, nullptr, nullptr, 0, d_hashes, n, np_for(r, nrep), W, d_owners, d_counts,
+                           rp::as_stream(stream));
+    });
+}
+
+// host-buffer forms: stage through the handle's device buffers on its stream
+static void host_lookup(rp::Ring& r, const char* keys, const uint64_t* off, uint32_t stride, const uint32_t* hashes,
+                        uint64_t n, int np, uint32_t W, uint32_t* owners, uint8_t* counts) {
+    if (n == 0) return;
+    const uint8_t* dk = nullptr;
+    const uint64_t* doff = nullptr;
+    const uint32_t* dh = nullptr;
+    if (hashes) {
+        r.io_a.reserve(n);
+        RP_HIP(hipMemcpyAsync(r.io_a.p, hashes, n * 4, hipMemcpyHostToDevice, r.st));
+        dh = r.io_a.p;
+    } else {
+        const uint64_t bytes = stride ? n * stride : off[n];
+        r.io_keys.reserve(bytes + 16);
+        RP_HIP(hipMemcpyAsync(r.io_keys.p, keys, bytes, hipMemcpyHostToDevice, r.st));
+        dk = r.io_keys.p;
+        if (!stride) {
+            r.io_off.reserve(n + 1);
+            RP_HIP(hipMemcpyAsync(r.io_off.p, off, (n + 1) * 8, hipMemcpyHostToDevice, r.st));
+            doff = r.io_off.p;
+        }
+    }
+    r.io_b.reserve(n * W);
+    if (counts) r.io_cnt.reserve(n);
+    rp::launch_lookupn(r, dk, doff, stride, dh, n, np, W, r.io_b.p, counts ? r.io_cnt.p : nullptr, r.st);
+    RP_HIP(hipMemcpyAsync(owners, r.io_b.p, n * W * 4, hipMemcpyDeviceToHost, r.st));
+    if (counts) RP_HIP(hipMemcpyAsync(counts, r.io_cnt.p, n, hipMemcpyDeviceToHost, r.st));
+    RP_HIP(hipStreamSynchronize(r.st));
+}
+
+int rp_ring_lookup(rp_ring* h, const char* keys, const uint64_t* off, uint32_t stride, uint64_t n, uint32_t* owners) {
+    return guard([&] {
+        rp::Ring& r = R(h);
+        RP_REQUIRE(n == 0 || (keys && owners && (stride || off)), "lookup: null buffer");
+        host_lookup(r, keys, off, stride, nullptr, n, 1, 1, owners, nullptr);
+    });
+}
+
+int rp_ring_lookupn(rp_ring* h, const char* keys, const uint64_t* off, uint32_t stride, uint64_t n, int32_t nrep,
+                    uint32_t* owners, uint8_t* counts) {
+    return guard([&] {
+        rp::Ring& r = R(h);
+        RP_REQUIRE(n == 0 || (keys && owners && (stride || off)), "lookupn: null buffer");
+        host_lookup(r, keys, off, stride, nullptr, n, np_for(r, nrep), nrep > 1 ? (uint32_t)nrep : 1u, owners,
+                    counts);
+    });
+}
+
+int rp_ring_lookup_hashes(rp_ring* h, const uint32_t* hashes, uint64_t n, uint32_t* owners) {
+    return guard([&] {
+        rp::Ring& r = R(h);
+        RP_REQUIRE(n == 0 || (hashes && owners), "lookup_hashes: null buffer");
+        host_lookup(r, nullptr, nullptr, 0, hashes, n, 1, 1, owners, nullptr);
+    });
+}
+
+int rp_ring_lookupn_hashes(rp_ring* h, const uint32_t* hashes, uint64_t n, int32_t nrep, uint32_t* owners,
+                           uint8_t* counts) {
+    return guard([&] {
+        rp::Ring& r = R(h);
+        RP_REQUIRE(n == 0 || (hashes && owners), "lookupn_hashes: null buffer");
+        host_lookup(r, nullptr, nullptr, 0, hashes, n, np_for(r, nrep), nrep > 1 ? (uint32_t)nrep : 1u, owners,
+                    counts);
+    });
+}
+
+// ---- farmhash + key generation
+
+uint32_t rp_hash32(const char* s, size_t len) {
+    return rp::fh::hash32(rp::fh::PtrSrc{reinterpret_cast<const uint8_t*>(s)}, (uint32_t)len);
+}
+
+int rp_hash32_batch_dev(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t* d_out, void* stream) {
+    return guard([&] {
+        if (!n) return;
+        RP_REQUIRE(d_bytes && d_off && d_out, "hash32_batch_dev: null buffer");
+        hipLaunchKernelGGL(rp::k_hash_batch, dim3(rp::grid_for(n, 256)), dim3(256), 0, rp::as_stream(stream), d_bytes,
+                           d_off, n, d_out);
+        RP_HIP(hipGetLastError());
+    });
+}
+
+int rp_gen_uuid_keys_dev(uint32_t seed, uint64_t k0, uint64_t n, uint8_t* d_out, void* stream) {
+    return guard([&] {
+        if (!n) return;
+        RP_REQUIRE(d_out && (reinterpret_cast<uintptr_t>(d_out) & 3) == 0, "gen_uuid_keys_dev: need 4-byte aligned out");
+        hipLaunchKernelGGL(rp::k_gen_uuid, dim3(rp::grid_for(n, 256, 8192)), dim3(256), 0, rp::as_stream(stream), seed,
+                           k0, n, reinterpret_cast<uint32_t*>(d_out));
+        RP_HIP(hipGetLastError());
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,145 @@
+"""Regenerate the committed golden fixtures under tests/golden/ by running the REFERENCE
+JavaScript in this container (needs /root/reference and node; never runs on the GPU box).
+
+    python tests/golden/make_golden.py [ring]
+
+Inputs are built with the oracle's Philox / uuid stream (oracle/pyoracle.py); the reference's
+`farmhash` dependency is served by the oracle's N-API restatement (oracle/gen/farmhash_napi.c),
+built into oracle/_ref/ by `make -C oracle ref`. Outputs are data only: inputs + what the
+reference returned.
+"""
+import hashlib
+import json
+import os
+import random
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = os.environ.get("RINGPOP_REFERENCE", "/root/reference")
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import pyoracle  # noqa: E402
+
+
+def run_node(script, cases):
+    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "oracle"), "all", "ref"])
+    env = dict(os.environ, NODE_PATH=os.path.join(REPO, "oracle", "_ref", "node_modules"))
+    with tempfile.TemporaryDirectory() as td:
+        fin, fout = os.path.join(td, "in.json"), os.path.join(td, "out.json")
+        with open(fin, "w") as f:
+            json.dump({"cases": cases}, f)
+        subprocess.check_call(["node", os.path.join(HERE, script), REF, fin, fout], env=env)
+        with open(fout) as f:
+            return json.load(f)["cases"]
+
+
+def tree_digest(tree):
+    h = hashlib.sha256()
+    for t, o in zip(tree["tokens"], tree["owners"]):
+        h.update(("%d:%s;" % (t, o)).encode())
+    return h.hexdigest()
+
+
+def ring_cases():
+    with open(os.path.join(REF, "benchmarks", "large-membership.json")) as f:
+        large = [m["address"] for m in json.load(f)]
+    servers = large[:1000]
+    extra = large[1000:1005]
+    keys = [k.tobytes().decode() for k in pyoracle.uuid_keys(42, 0, 4096)]
+    uk = lambda seed, k0, n: {"uuid": [seed, k0, n]}  # noqa: E731
+    rng = random.Random(1234)
+
+    cases = []
+    # C1: benchmarks/add-remove-hashring.js servers, real farmhash, 1000 x 100 points
+    removed = servers[::10]
+    cases.append({
+        "name": "c1", "hashKind": "farmhash", "dump": True,
+        "batches": [
+            dict({"add": servers, "remove": [], "keys": keys, "ns": [1, 3]}, uuid=uk(42, 0, 4096)),
+            dict({"add": extra, "remove": removed, "keys": keys[:1024], "ns": [3]}, uuid=uk(42, 0, 1024)),
+            dict({"add": [], "remove": ["10.99.99.99:1"], "keys": keys[:16], "ns": [3]}, uuid=uk(42, 0, 16)),
+        ],
+    })
+    # Forced collisions: farmhash % 2000 through the hashFunc injection point, 120 servers
+    # x 20 points, random add/remove histories with duplicates and add+remove in one batch.
+    pool = ["10.1.%d.%d:%d" % (i // 50, i % 50, 3000 + i) for i in range(120)]
+    batches = []
+    for b in range(16):
+        add = rng.sample(pool, rng.randint(0, 40))
+        add += rng.sample(add, min(len(add), rng.randint(0, 3)))  # duplicates in one batch
+        rem = rng.sample(pool, rng.randint(0, 30))
+        if add and rng.random() < 0.5:
+            rem.append(add[0])  # added then removed in the same batch
+        probes = sorted(set([0, 1, 1999, 2000, 4294967295] + [rng.randrange(0, 2100) for _ in range(60)]))
+        batches.append({"add": add, "remove": rem, "keys": ["#%d" % p for p in probes],
+                        "ns": [-1, 0, 1, 2, 3, 7, 200]})
+    batches.append({"add": [], "remove": pool, "keys": ["#0", "#5"], "ns": [0, 1, 3]})
+    batches.append({"add": pool[:2], "remove": [], "keys": ["#0", "#1999", "#2001"], "ns": [-1, 0, 1, 2, 3, 5]})
+    cases.append({"name": "collide", "hashKind": "mod", "hashMod": 2000, "replicaPoints": 20,
+                  "dump": True, "batches": batches})
+    # test/unit/ring-test.js:82-124 known answers (extractPort hashFunc)
+    ports = ["127.0.0.1:%d" % (3000 + i) for i in range(1000)]
+    cases.append({"name": "port", "hashKind": "port", "dump": True, "batches": [
+        {"add": ports, "remove": [], "keys": [p + "0" for p in ports], "ns": [3]},
+    ]})
+    cases.append({"name": "port1", "hashKind": "port", "dump": True, "batches": [
+        {"add": [], "remove": [], "keys": [ports[0] + "0"], "ns": [3]},
+        {"add": [ports[0]], "remove": [], "keys": [ports[0] + "0", "127.0.0.1:99999"], "ns": [-2, 0, 1, 3]},
+    ]})
+    # tiny farmhash rings: wrap-around, n > servers, n <= 0
+    tiny_keys = [k.tobytes().decode() for k in pyoracle.uuid_keys(7, 0, 64)]
+    cases.append({"name": "tiny", "hashKind": "farmhash", "replicaPoints": 3, "dump": True, "batches": [
+        dict({"add": ["a"], "remove": [], "keys": tiny_keys, "ns": [-1, 0, 1, 2, 5]}, uuid=uk(7, 0, 64)),
+        dict({"add": ["b", "test 1", "a"], "remove": [], "keys": tiny_keys, "ns": [-1, 0, 1, 2, 3, 5]},
+             uuid=uk(7, 0, 64)),
+        dict({"add": [], "remove": ["a"], "keys": tiny_keys, "ns": [1, 2, 3]}, uuid=uk(7, 0, 64)),
+    ]})
+    return cases
+
+
+def make_ring():
+    cases = ring_cases()
+    outs = run_node("ref_ring.js", cases)
+    fixture = {"generator": "tests/golden/make_golden.py + tests/golden/ref_ring.js",
+               "reference": "lib/ring/index.js, lib/ring/rbtree.js (ringpop v10.9.6)",
+               "note": "owners are indices into the case's `names` (-1 = null); uuid keys are "
+                       "[seed, k0, n] of the oracle's Philox uuid stream",
+               "cases": []}
+    for c, o in zip(cases, outs):
+        names, index = [], {}
+
+        def nid(s):
+            if s is None:
+                return -1
+            if s not in index:
+                index[s] = len(names)
+                names.append(s)
+            return index[s]
+
+        fc = {"name": c["name"], "hashKind": c["hashKind"], "hashMod": c.get("hashMod"),
+              "replicaPoints": c.get("replicaPoints", 100), "names": names, "batches": []}
+        for b, ob in zip(c["batches"], o["batches"]):
+            fb = {"add": b["add"], "remove": b["remove"], "changed": ob["changed"],
+                  "checksum": ob["checksum"], "serverCount": ob["serverCount"], "size": ob["size"]}
+            tree = ob["tree"]
+            fb["tree_sha256"] = tree_digest(tree)
+            if len(tree["tokens"]) <= 4000:
+                fb["tree"] = {"tokens": tree["tokens"], "owners": [nid(x) for x in tree["owners"]]}
+            if "keys" in b:
+                fb["keys"] = b.get("uuid") or b["keys"]
+                fb["lookup"] = [nid(x) for x in ob["lookup"]]
+                fb["lookupN"] = {n: [[nid(x) for x in lst] for lst in v] for n, v in ob["lookupN"].items()}
+            fc["batches"].append(fb)
+        fixture["cases"].append(fc)
+    path = os.path.join(HERE, "ring_golden.json")
+    with open(path, "w") as f:
+        json.dump(fixture, f, separators=(",", ":"))
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+if __name__ == "__main__":
+    what = sys.argv[1:] or ["ring"]
+    if "ring" in what:
+        make_ring()
