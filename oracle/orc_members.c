@@ -1,0 +1,266 @@
+/*
+ * orc_members.c — CPU restatement of ringpop's membership merge and checksum.
+ * TEST INFRASTRUCTURE ONLY (see oracle.h).
+ *
+ * Restates:
+ *   Member.evaluateUpdate / _isLocalOverride / _isOtherOverride  lib/membership/member.js:71-122,155-202
+ *   Membership.update (sequential fold, new members, stash)      lib/membership/index.js:249-324
+ *   Membership.set + mergeMembershipChangesets                   lib/membership/index.js:208-247, merge.js:22-51
+ *   Membership.computeChecksum / generateChecksumString          lib/membership/index.js:48-75,100-123
+ *   Membership.getJoinPosition (Math.random injected: Philox)    lib/membership/index.js:129-131
+ * Members are identified by interned address ids 0..n_names-1 (names given up front).
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "oracle.h"
+
+static const char *const STATUS_STR[4] = {"alive", "suspect", "faulty", "leave"};
+static const uint32_t STATUS_LEN[4] = {5, 7, 6, 5};
+
+struct orc_members {
+    uint32_t n_names;
+    char *nb;
+    uint64_t *noff;
+    uint32_t local_id;
+    int is_ready;
+    uint32_t join_seed;
+    uint64_t join_ctr;
+    /* per id */
+    uint8_t *exists, *status;
+    int64_t *inc;
+    /* members array order (ids) */
+    uint32_t *order;
+    uint32_t count;
+    /* stash (ring of change batches, flattened) */
+    uint32_t *st_id; uint8_t *st_status; int64_t *st_inc; uint32_t *st_batch_end;
+    uint32_t st_n, st_cap, st_batches, st_bcap;
+    int stash_nulled;
+    /* checksum */
+    int has_checksum;
+    uint32_t checksum;
+    uint32_t *sorted; /* ids sorted by address */
+    char *buf;
+    uint64_t buf_cap;
+};
+
+static int cmp_addr(const orc_members *m, uint32_t a, uint32_t b) {
+    uint64_t la = m->noff[a + 1] - m->noff[a], lb = m->noff[b + 1] - m->noff[b];
+    uint64_t l = la < lb ? la : lb;
+    int c = memcmp(m->nb + m->noff[a], m->nb + m->noff[b], l);
+    if (c) return c;
+    return la < lb ? -1 : (la > lb ? 1 : 0);
+}
+
+static const orc_members *g_m;
+static int qcmp(const void *x, const void *y) { return cmp_addr(g_m, *(const uint32_t *)x, *(const uint32_t *)y); }
+
+orc_members *orc_members_new(const char *names, const uint32_t *off, uint32_t n, uint32_t local_id,
+                             uint32_t join_seed) {
+    orc_members *m = (orc_members *)calloc(1, sizeof(orc_members));
+    m->n_names = n;
+    m->nb = (char *)malloc(off[n] + 1);
+    memcpy(m->nb, names, off[n]);
+    m->noff = (uint64_t *)malloc(sizeof(uint64_t) * (n + 1));
+    for (uint32_t i = 0; i <= n; i++) m->noff[i] = off[i];
+    m->local_id = local_id;
+    m->is_ready = 1;
+    m->join_seed = join_seed;
+    m->exists = (uint8_t *)calloc(n, 1);
+    m->status = (uint8_t *)calloc(n, 1);
+    m->inc = (int64_t *)calloc(n, sizeof(int64_t));
+    m->order = (uint32_t *)malloc(sizeof(uint32_t) * (n + 1));
+    m->sorted = (uint32_t *)malloc(sizeof(uint32_t) * (n + 1));
+    for (uint32_t i = 0; i < n; i++) m->sorted[i] = i;
+    g_m = m;
+    qsort(m->sorted, n, sizeof(uint32_t), qcmp);
+    return m;
+}
+
+void orc_members_free(orc_members *m) {
+    if (!m) return;
+    free(m->nb); free(m->noff); free(m->exists); free(m->status); free(m->inc); free(m->order);
+    free(m->st_id); free(m->st_status); free(m->st_inc); free(m->st_batch_end);
+    free(m->sorted); free(m->buf);
+    free(m);
+}
+
+void orc_members_set_ready(orc_members *m, int ready) { m->is_ready = ready; }
+
+/* Math.floor(Math.random() * members.length) with Math.random := philox_u32 / 2^32 */
+static uint32_t join_position(orc_members *m) {
+    uint32_t ctr[4] = {(uint32_t)m->join_ctr, (uint32_t)(m->join_ctr >> 32), 0, 0};
+    uint32_t key[2] = {m->join_seed, 0x4a4f494eu /* 'JOIN' */};
+    uint32_t r[4];
+    orc_philox4x32_10(ctr, key, r);
+    m->join_ctr++;
+    return (uint32_t)(((uint64_t)r[0] * m->count) >> 32);
+}
+
+static void insert_member(orc_members *m, uint32_t id, uint8_t st, int64_t inc, uint32_t pos) {
+    m->exists[id] = 1;
+    m->status[id] = st;
+    m->inc[id] = inc;
+    memmove(m->order + pos + 1, m->order + pos, sizeof(uint32_t) * (m->count - pos));
+    m->order[pos] = id;
+    m->count++;
+}
+
+/* Member._isOtherOverride (member.js:171-202) */
+static int other_override(uint8_t cur, int64_t cur_inc, uint8_t st, int64_t inc) {
+    switch (st) {
+    case 0: return inc > cur_inc;                                        /* isAliveOverride */
+    case 1: return (cur == 1 && inc > cur_inc) || (cur == 2 && inc > cur_inc) ||
+                   (cur == 0 && inc >= cur_inc);                         /* isSuspectOverride */
+    case 2: return (cur == 1 && inc >= cur_inc) || (cur == 2 && inc > cur_inc) ||
+                   (cur == 0 && inc >= cur_inc);                         /* isFaultyOverride */
+    case 3: return cur != 3 && inc >= cur_inc;                           /* isLeaveOverride */
+    }
+    return 0;
+}
+
+static void compute_checksum(orc_members *m) {
+    uint64_t need = 0;
+    for (uint32_t i = 0; i < m->n_names; i++)
+        if (m->exists[i]) need += (m->noff[i + 1] - m->noff[i]) + 7 + 21 + 1;
+    if (need + 1 > m->buf_cap) {
+        m->buf_cap = need + 64;
+        m->buf = (char *)realloc(m->buf, m->buf_cap);
+    }
+    uint64_t o = 0;
+    int first = 1;
+    for (uint32_t k = 0; k < m->n_names; k++) {
+        uint32_t id = m->sorted[k];
+        if (!m->exists[id]) continue;
+        if (!first) m->buf[o++] = ';';
+        first = 0;
+        uint64_t ln = m->noff[id + 1] - m->noff[id];
+        memcpy(m->buf + o, m->nb + m->noff[id], ln);
+        o += ln;
+        memcpy(m->buf + o, STATUS_STR[m->status[id]], STATUS_LEN[m->status[id]]);
+        o += STATUS_LEN[m->status[id]];
+        o += (uint64_t)sprintf(m->buf + o, "%lld", (long long)m->inc[id]);
+    }
+    m->checksum = orc_hash32((const uint8_t *)m->buf, o);
+    m->has_checksum = 1;
+}
+
+/* Membership.update (lib/membership/index.js:249-324). Returns the number of applied updates;
+ * applied_out[k] flags them, new_*_out[k] hold the applied (possibly rewritten) update. */
+uint32_t orc_members_update(orc_members *m, const uint32_t *ids, const uint8_t *status, const int64_t *inc,
+                            uint32_t k, int is_local, int64_t now_ms, uint8_t *applied_out,
+                            uint8_t *new_status_out, int64_t *new_inc_out) {
+    if (k == 0) return 0;
+    if (!is_local && !m->is_ready) { /* stash (259-265) */
+        if (!m->stash_nulled) {
+            if (m->st_n + k > m->st_cap) {
+                while (m->st_n + k > m->st_cap) m->st_cap = m->st_cap ? 2 * m->st_cap : 1024;
+                m->st_id = (uint32_t *)realloc(m->st_id, sizeof(uint32_t) * m->st_cap);
+                m->st_status = (uint8_t *)realloc(m->st_status, m->st_cap);
+                m->st_inc = (int64_t *)realloc(m->st_inc, sizeof(int64_t) * m->st_cap);
+            }
+            if (m->st_batches + 1 > m->st_bcap) {
+                m->st_bcap = m->st_bcap ? 2 * m->st_bcap : 64;
+                m->st_batch_end = (uint32_t *)realloc(m->st_batch_end, sizeof(uint32_t) * m->st_bcap);
+            }
+            memcpy(m->st_id + m->st_n, ids, sizeof(uint32_t) * k);
+            memcpy(m->st_status + m->st_n, status, k);
+            memcpy(m->st_inc + m->st_n, inc, sizeof(int64_t) * k);
+            m->st_n += k;
+            m->st_batch_end[m->st_batches++] = m->st_n;
+        }
+        if (applied_out) memset(applied_out, 0, k);
+        return 0;
+    }
+    uint32_t napplied = 0;
+    for (uint32_t i = 0; i < k; i++) { /* (272-304) sequential fold */
+        uint32_t id = ids[i];
+        uint8_t st = status[i];
+        int64_t in = inc[i];
+        int applied = 0;
+        if (!m->exists[id]) { /* new member: verbatim, random join position (277-291) */
+            insert_member(m, id, st, in, join_position(m));
+            applied = 1;
+        } else if (id == m->local_id && (st == 1 || st == 2)) { /* _isLocalOverride (155-169) */
+            st = 0;
+            in = now_ms;
+            applied = 1;
+        } else if (other_override(m->status[id], m->inc[id], st, in)) {
+            applied = 1;
+        }
+        if (applied) {
+            m->status[id] = st;
+            m->inc[id] = in;
+            napplied++;
+        }
+        if (applied_out) applied_out[i] = (uint8_t)applied;
+        if (new_status_out) new_status_out[i] = st;
+        if (new_inc_out) new_inc_out[i] = in;
+    }
+    if (napplied) compute_checksum(m); /* (306-309) */
+    return napplied;
+}
+
+/* Membership.set (208-247): mergeMembershipChangesets (merge.js:22-51) over the stash, then
+ * append in first-seen order, checksum once. Returns the number of members set. */
+uint32_t orc_members_set(orc_members *m) {
+    if (m->is_ready || m->stash_nulled || m->st_n == 0) return 0;
+    uint32_t *best = (uint32_t *)malloc(sizeof(uint32_t) * m->n_names);
+    uint32_t *seen = (uint32_t *)malloc(sizeof(uint32_t) * (m->st_n + 1));
+    uint32_t nseen = 0;
+    for (uint32_t i = 0; i < m->n_names; i++) best[i] = 0xFFFFFFFFu;
+    for (uint32_t i = 0; i < m->st_n; i++) {
+        uint32_t id = m->st_id[i];
+        if (id == m->local_id) continue; /* skip whoami */
+        if (best[id] == 0xFFFFFFFFu) { best[id] = i; seen[nseen++] = id; }
+        else if (m->st_inc[best[id]] < m->st_inc[i]) best[id] = i; /* strictly greater wins */
+    }
+    for (uint32_t j = 0; j < nseen; j++) {
+        uint32_t id = seen[j];
+        uint32_t i = best[id];
+        if (m->exists[id]) { m->status[id] = m->st_status[i]; m->inc[id] = m->st_inc[i]; continue; }
+        insert_member(m, id, m->st_status[i], m->st_inc[i], m->count);
+    }
+    free(best);
+    free(seen);
+    m->stash_nulled = 1;
+    compute_checksum(m);
+    return nseen;
+}
+
+int orc_members_checksum(const orc_members *m, uint32_t *out) {
+    if (!m->has_checksum) return 0;
+    *out = m->checksum;
+    return 1;
+}
+
+uint32_t orc_members_count(const orc_members *m) { return m->count; }
+
+void orc_members_order(const orc_members *m, uint32_t *ids_out) {
+    memcpy(ids_out, m->order, sizeof(uint32_t) * m->count);
+}
+
+int orc_members_get(const orc_members *m, uint32_t id, uint8_t *status, int64_t *inc) {
+    if (id >= m->n_names || !m->exists[id]) return 0;
+    *status = m->status[id];
+    *inc = m->inc[id];
+    return 1;
+}
+
+/* Write the checksum string (generateChecksumString) into buf (cap bytes); returns length. */
+uint64_t orc_members_checksum_string(orc_members *m, char *buf, uint64_t cap) {
+    compute_checksum(m);
+    uint64_t n = 0;
+    /* recompute length: buf holds the last string */
+    for (uint32_t k = 0, first = 1; k < m->n_names; k++) {
+        uint32_t id = m->sorted[k];
+        if (!m->exists[id]) continue;
+        char tmp[32];
+        n += (first ? 0 : 1) + (m->noff[id + 1] - m->noff[id]) + STATUS_LEN[m->status[id]] +
+             (uint64_t)sprintf(tmp, "%lld", (long long)m->inc[id]);
+        first = 0;
+    }
+    if (buf) memcpy(buf, m->buf, n < cap ? n : cap);
+    return n;
+}

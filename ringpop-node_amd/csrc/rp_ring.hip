@@ -13,6 +13,7 @@
 // registers (fh::hash32_words), searched bucket-first, walked for distinct owners, and the
 // owner rows are staged back through LDS for coalesced stores.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -27,49 +28,80 @@ namespace rp {
 
 constexpr uint32_t NIL = 0xFFFFFFFFu;
 
+static bool getenv_flag(const char* name) {
+    const char* v = getenv(name);
+    return v && *v && *v != '0';
+}
+
 struct RingView {
     const uint32_t* tok;
     const uint32_t* own;
     const uint32_t* bstart;  // 2^bbits + 1 entries
     uint32_t M;
     uint32_t shift;  // 32 - bbits
+
+    // first index i in [0, M] with tok[i] >= h (RBTree upperBound semantics, rbtree.js:235-271)
+    __device__ __forceinline__ uint32_t find(uint32_t h) const {
+        const uint32_t b = h >> shift;
+        uint32_t lo = bstart[b], hi = bstart[b + 1];
+        while (lo < hi) {
+            uint32_t mid = (lo + hi) >> 1;
+            if (tok[mid] < h) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo;
+    }
+    __device__ __forceinline__ uint32_t owner(uint32_t j) const { return own[j]; }
 };
 
-// first index i in [0, M] with tok[i] >= h (RBTree upperBound semantics, rbtree.js:235-271)
-__device__ __forceinline__ uint32_t ring_find(const RingView& rv, uint32_t h) {
-    const uint32_t b = h >> rv.shift;
-    uint32_t lo = rv.bstart[b], hi = rv.bstart[b + 1];
-    while (lo < hi) {
-        uint32_t mid = (lo + hi) >> 1;
-        if (rv.tok[mid] < h) lo = mid + 1;
-        else hi = mid;
+// Packed lookup layout: 2^B buckets on the top B token bits (B chosen for ~4 tokens per
+// bucket); each entry is one uint32 = (token low 32-B bits) << B | owner, so owner ids must be
+// < 2^B. A bucket plus its lookupN successors usually sits inside one 16-entry (64-B) window.
+// The entry array is padded with 0xFFFFFFFF so window loads past M stay in bounds.
+struct PackedView {
+    const uint32_t* ent;
+    const uint32_t* bstart;  // 2^B + 1 entries
+    uint32_t M;
+    uint32_t B;
+
+    __device__ __forceinline__ uint32_t key_of(uint32_t h) const { return (h << B) >> 0; }
+    __device__ __forceinline__ uint32_t find(uint32_t h) const {
+        const uint32_t b = h >> (32 - B);
+        const uint32_t key = h << B;  // the low 32-B bits of h, shifted over the owner field
+        uint32_t lo = bstart[b], hi = bstart[b + 1];
+        while (lo < hi) {
+            uint32_t mid = (lo + hi) >> 1;
+            if (ent[mid] < key) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo;
     }
-    return lo;
-}
+    __device__ __forceinline__ uint32_t owner(uint32_t j) const { return ent[j] & ((1u << B) - 1u); }
+};
 
 // lookupN walk (lib/ring/index.js:157-189) with the result kept in registers (np <= MAXN).
 // Visits positions i%M, i%M+1, ... cyclically, at most M of them, stopping once np
 // distinct owners are collected. np <= 0 reproduces the reference's single loop body.
-template <int MAXN>
-__device__ __forceinline__ int ring_walk(const RingView& rv, uint32_t i, int np, uint32_t (&res)[MAXN]) {
+template <int MAXN, class View>
+__device__ __forceinline__ int ring_walk(const View& rv, uint32_t i, int np, uint32_t (&res)[MAXN]) {
 #pragma unroll
     for (int q = 0; q < MAXN; q++) res[q] = NIL;
     if (rv.M == 0) return 0;
     if (np <= 0) {
         if (i < rv.M) {
-            res[0] = rv.own[i];
+            res[0] = rv.owner(i);
             return 1;
         }
         return 0;
     }
     uint32_t j = (i == rv.M) ? 0u : i;
     if (MAXN == 1) {
-        res[0] = rv.own[j];
+        res[0] = rv.owner(j);
         return 1;
     }
     int cnt = 0;
     for (uint32_t steps = 0; steps < rv.M; steps++) {
-        const uint32_t o = rv.own[j];
+        const uint32_t o = rv.owner(j);
         bool dup = false;
 #pragma unroll
         for (int q = 0; q < MAXN; q++) dup |= (q < cnt) & (res[q] == o);
@@ -85,12 +117,13 @@ __device__ __forceinline__ int ring_walk(const RingView& rv, uint32_t i, int np,
 }
 
 // Unbounded walk writing straight to the output row (np > 8).
-__device__ int ring_walk_global(const RingView& rv, uint32_t i, int np, uint32_t* row, uint32_t W) {
+template <class View>
+__device__ int ring_walk_global(const View& rv, uint32_t i, int np, uint32_t* row, uint32_t W) {
     for (uint32_t q = 0; q < W; q++) row[q] = NIL;
     if (rv.M == 0) return 0;
     if (np <= 0) {
         if (i < rv.M) {
-            row[0] = rv.own[i];
+            row[0] = rv.owner(i);
             return 1;
         }
         return 0;
@@ -98,7 +131,7 @@ __device__ int ring_walk_global(const RingView& rv, uint32_t i, int np, uint32_t
     uint32_t j = (i == rv.M) ? 0u : i;
     int cnt = 0;
     for (uint32_t steps = 0; steps < rv.M; steps++) {
-        const uint32_t o = rv.own[j];
+        const uint32_t o = rv.owner(j);
         bool dup = false;
         for (int q = 0; q < cnt; q++)
             if (row[q] == o) {
@@ -117,32 +150,62 @@ __device__ int ring_walk_global(const RingView& rv, uint32_t i, int np, uint32_t
 namespace {
 
 constexpr int kLkThreads = 256;
+constexpr uint32_t kEntPad = 32;  // padding entries after M in the packed array
+constexpr int kDefaultKPL = 2;     // keys per lane in the probe kernel (RP_LOOKUP_KPL overrides)
 
-// Fixed-stride keys (LEN % 4 == 0, LEN > 24, e.g. 36-byte UUIDs): LDS-staged hot kernel.
-template <int LEN, int MAXN>
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Fixed-stride keys (LEN % 4 == 0, LEN > 24, e.g. 36-byte UUIDs): the hot kernel.
+// Keys stream HBM -> registers -> LDS with 16-B non-temporal loads (read once; they must not
+// evict the ring table from L2). The next tile's loads are issued before the current tile is
+// hashed, so their HBM latency hides under the search. Each lane hashes its key from
+// registers, searches, walks, and the owner rows leave through LDS as 16-B non-temporal stores.
+// MODE is a diagnostic ablation (0 = full; 1 = write the hash; 2 = write the ring index).
+template <int LEN, int MAXN, class View, int MODE = 0>
 __global__ __launch_bounds__(kLkThreads) void k_lookupn_fixed(const uint8_t* __restrict__ keys, uint64_t n,
-                                                              RingView rv, int np, uint32_t W,
+                                                              View rv, int np, uint32_t W,
                                                               uint32_t* __restrict__ out,
                                                               uint8_t* __restrict__ counts) {
-    constexpr int W4 = LEN / 4;
-    __shared__ uint32_t sk[kLkThreads * W4];
-    __shared__ uint32_t so[kLkThreads * MAXN];
+    constexpr int W4 = LEN / 4;                       // dwords per key
+    constexpr int V4 = kLkThreads * W4 / 4;           // 16-B vectors per tile
+    constexpr int PER = (V4 + kLkThreads - 1) / kLkThreads;
+    static_assert((kLkThreads * W4) % 4 == 0, "tile must be a whole number of 16-B vectors");
+    __shared__ __attribute__((aligned(16))) uint32_t sk[kLkThreads * W4];
+    __shared__ __attribute__((aligned(16))) uint32_t so[kLkThreads * MAXN];
     const int tid = threadIdx.x;
     const bool kvec = ((reinterpret_cast<uintptr_t>(keys) & 15) == 0);
     const bool ovec = ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
     const uint64_t ntiles = (n + kLkThreads - 1) / kLkThreads;
-    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const uint64_t nfull = n / kLkThreads;  // tiles with all 256 keys
+
+    u32x4 pre[PER];
+    auto issue = [&](uint64_t t) {
+        const u32x4* s4 = reinterpret_cast<const u32x4*>(keys + t * kLkThreads * LEN);
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const int k = tid + q * kLkThreads;
+            if (k < V4) pre[q] = __builtin_nontemporal_load(s4 + k);
+        }
+    };
+    uint64_t t = blockIdx.x;
+    if (kvec && t < nfull) issue(t);
+    for (; t < ntiles; t += gridDim.x) {
         const uint64_t base = t * kLkThreads;
         const uint32_t cnt = (uint32_t)((n - base) < (uint64_t)kLkThreads ? (n - base) : kLkThreads);
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(keys + base * LEN);
-        if (kvec && cnt == kLkThreads) {
-            const uint4* s4 = reinterpret_cast<const uint4*>(src);
-            uint4* d4 = reinterpret_cast<uint4*>(sk);
-            for (int k = tid; k < kLkThreads * W4 / 4; k += kLkThreads) d4[k] = s4[k];
+        if (kvec && t < nfull) {
+            u32x4* d4 = reinterpret_cast<u32x4*>(sk);
+#pragma unroll
+            for (int q = 0; q < PER; q++) {
+                const int k = tid + q * kLkThreads;
+                if (k < V4) d4[k] = pre[q];
+            }
         } else {
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(keys + base * LEN);
             for (uint32_t k = tid; k < cnt * W4; k += kLkThreads) sk[k] = src[k];
         }
         __syncthreads();
+        const uint64_t tn = t + gridDim.x;
+        if (kvec && tn < nfull) issue(tn);  // in flight while this tile is searched
         int c = 0;
         uint32_t res[MAXN];
         if ((uint32_t)tid < cnt) {
@@ -150,8 +213,19 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_fixed(const uint8_t* __r
 #pragma unroll
             for (int j = 0; j < W4; j++) w[j] = sk[tid * W4 + j];
             const uint32_t h = fh::hash32_words<LEN>(w);
-            const uint32_t i = ring_find(rv, h);
-            c = ring_walk<MAXN>(rv, i, np, res);
+            if constexpr (MODE == 1) {
+#pragma unroll
+                for (int q = 0; q < MAXN; q++) res[q] = h + q;
+                c = 1;
+            } else if constexpr (MODE == 2) {
+                const uint32_t i = rv.find(h);
+#pragma unroll
+                for (int q = 0; q < MAXN; q++) res[q] = i + q;
+                c = 1;
+            } else {
+                const uint32_t i = rv.find(h);
+                c = ring_walk<MAXN>(rv, i, np, res);
+            }
 #pragma unroll
             for (int q = 0; q < MAXN; q++)
                 if ((uint32_t)q < W) so[tid * W + q] = res[q];
@@ -160,10 +234,10 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_fixed(const uint8_t* __r
         __syncthreads();
         uint32_t* dst = out + base * W;
         const uint32_t tot = cnt * W;
-        if (ovec && ((base * W) & 3) == 0 && cnt == kLkThreads && (tot & 3) == 0) {
-            uint4* d4 = reinterpret_cast<uint4*>(dst);
-            const uint4* s4 = reinterpret_cast<const uint4*>(so);
-            for (uint32_t k = tid; k < tot / 4; k += kLkThreads) d4[k] = s4[k];
+        if (ovec && cnt == kLkThreads && (tot & 3) == 0) {
+            u32x4* d4 = reinterpret_cast<u32x4*>(dst);
+            const u32x4* s4 = reinterpret_cast<const u32x4*>(so);
+            for (uint32_t k = tid; k < tot / 4; k += kLkThreads) __builtin_nontemporal_store(s4[k], d4 + k);
         } else {
             for (uint32_t k = tid; k < tot; k += kLkThreads) dst[k] = so[k];
         }
@@ -171,14 +245,214 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_fixed(const uint8_t* __r
     }
 }
 
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
+
+// The C2 hot kernel (packed layout with ~1 token per bucket; lookup / lookupN with n <= 4;
+// 36-byte keys). Every random access is ONE load instruction per key, so it costs one
+// L1->L2 request (each lane of a wave instruction touching a different line is a separate
+// request; PMC showed ~6 requests/key for a binary search + walk):
+//   LDS key words -> farmhash32 -> [bucket lo, hi) as one 8-B load -> the 4 entries at lo as
+//   one 16-B load -> position i = lo + #(entries < key) and the successor owners, from
+//   registers; only when the successors run past those 4 entries, one more 16-B load at i.
+// Each lane owns KPL keys of a 256*KPL-key tile, so each dependent trip serves KPL keys.
+// Keys the 4-entry window cannot answer exactly (bucket longer than 4 with every entry below
+// the key, positions within 3 of the end of the ring, repeated owners among the successors)
+// are appended to a slow list and finished by k_lookupn_fix (binary search + the exact walk).
+template <int LEN, int KPL, int MODE = 0>
+__global__ __launch_bounds__(kLkThreads) void k_lookupn_probe(const uint8_t* __restrict__ keys, uint64_t n,
+                                                              PackedView rv, int np, uint32_t W,
+                                                              uint32_t* __restrict__ out,
+                                                              uint8_t* __restrict__ counts,
+                                                              uint32_t* __restrict__ slow_list,
+                                                              uint32_t* __restrict__ nslow) {
+    constexpr int W4 = LEN / 4;
+    constexpr int TK = kLkThreads * KPL;
+    constexpr int V4 = TK * W4 / 4;
+    constexpr int PER = (V4 + kLkThreads - 1) / kLkThreads;
+    static_assert((TK * W4) % 4 == 0, "tile must be whole 16-B vectors");
+    // one LDS buffer: key words until every lane has hashed, then the owner rows
+    constexpr int SK = TK * W4, SO = TK * 4;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[SK > SO ? SK : SO];
+    uint32_t* const sk = lds;
+    uint32_t* const so = lds;
+    const int tid = threadIdx.x;
+    const bool kvec = ((reinterpret_cast<uintptr_t>(keys) & 15) == 0);
+    const bool ovec = ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
+    const uint64_t ntiles = (n + TK - 1) / TK;
+    const uint32_t B = rv.B;
+    const uint32_t omask = (1u << B) - 1u;
+    const int need = np <= 0 ? 1 : np;
+    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint64_t base = t * TK;
+        const uint32_t cnt = (uint32_t)((n - base) < (uint64_t)TK ? (n - base) : TK);
+        if (kvec && cnt == TK) {
+            const u32x4* s4 = reinterpret_cast<const u32x4*>(keys + base * LEN);
+            u32x4 pre[PER];
+#pragma unroll
+            for (int q = 0; q < PER; q++) {
+                const int k = tid + q * kLkThreads;
+                if (k < V4) pre[q] = __builtin_nontemporal_load(s4 + k);
+            }
+            u32x4* d4 = reinterpret_cast<u32x4*>(sk);
+#pragma unroll
+            for (int q = 0; q < PER; q++) {
+                const int k = tid + q * kLkThreads;
+                if (k < V4) d4[k] = pre[q];
+            }
+        } else {
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(keys + base * LEN);
+            for (uint32_t k = tid; k < cnt * W4; k += kLkThreads) sk[k] = src[k];
+        }
+        __syncthreads();
+        uint32_t h[KPL];
+#pragma unroll
+        for (int k = 0; k < KPL; k++) {
+            const uint32_t kk = tid + k * kLkThreads;
+            uint32_t w[W4];
+#pragma unroll
+            for (int j = 0; j < W4; j++) w[j] = sk[(kk < cnt ? kk : 0) * W4 + j];
+            h[k] = fh::hash32_words<LEN>(w);
+        }
+        __syncthreads();  // sk is reused as so below
+        if constexpr (MODE == 1) {
+#pragma unroll
+            for (int k = 0; k < KPL; k++) {
+                const uint32_t kk = tid + k * kLkThreads;
+                if (kk < cnt) {
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        if ((uint32_t)q < W) so[kk * W + q] = h[k] + q;
+                }
+            }
+        } else {
+            u32x2 bb[KPL];
+#pragma unroll
+            for (int k = 0; k < KPL; k++)
+                bb[k] = *reinterpret_cast<const u32x2_a4*>(rv.bstart + (h[k] >> (32 - B)));
+            u32x4 win[KPL];
+#pragma unroll
+            for (int k = 0; k < KPL; k++) win[k] = *reinterpret_cast<const u32x4_a4*>(rv.ent + bb[k].x);
+#pragma unroll
+            for (int k = 0; k < KPL; k++) {
+                const uint32_t kk = tid + k * kLkThreads;
+                const uint32_t lo = bb[k].x, hi = bb[k].y;
+                const uint32_t key = h[k] << B;
+                const uint32_t len = hi - lo;
+                const uint32_t c = (0u < len && win[k].x < key) + (1u < len && win[k].y < key) +
+                                   (2u < len && win[k].z < key) + (3u < len && win[k].w < key);
+                const uint32_t i = lo + c;
+                bool slow = (c == 4u && len > 4u) | (i + 3u >= rv.M);
+                uint32_t e0, e1, e2, e3;
+                if (4u - c >= (uint32_t)need) {
+                    // successors i.. are win[c..3]
+                    const uint32_t a0 = (c & 1) ? win[k].y : win[k].x, a1 = (c & 1) ? win[k].z : win[k].y;
+                    const uint32_t a2 = (c & 1) ? win[k].w : win[k].z, a3 = win[k].w;
+                    e0 = (c & 2) ? a2 : a0;
+                    e1 = (c & 2) ? a3 : a1;
+                    e2 = a2;
+                    e3 = a3;
+                } else {
+                    const u32x4 sc = *reinterpret_cast<const u32x4_a4*>(rv.ent + (i < rv.M ? i : 0u));
+                    e0 = sc.x;
+                    e1 = sc.y;
+                    e2 = sc.z;
+                    e3 = sc.w;
+                }
+                uint32_t res[4] = {NIL, NIL, NIL, NIL};
+                uint32_t rc = 1;
+                if constexpr (MODE == 2) {
+                    res[0] = i;
+                    res[1] = i + 1;
+                    res[2] = i + 2;
+                    res[3] = i + 3;
+                } else {
+                    const uint32_t o0 = e0 & omask, o1 = e1 & omask, o2 = e2 & omask, o3 = e3 & omask;
+                    // distinct owners in visit order (lib/ring/index.js:173-186)
+                    res[0] = o0;
+                    const uint32_t oq[3] = {o1, o2, o3};
+#pragma unroll
+                    for (int q = 0; q < 3; q++) {
+                        const uint32_t o = oq[q];
+                        const bool dup = (o == res[0]) | (rc > 1 && o == res[1]) | (rc > 2 && o == res[2]);
+                        if (!dup && (int)rc < need) {
+                            res[1] = rc == 1 ? o : res[1];
+                            res[2] = rc == 2 ? o : res[2];
+                            res[3] = rc == 3 ? o : res[3];
+                            rc++;
+                        }
+                    }
+                    slow |= (int)rc < need;  // repeated owners: the walk must go further
+                }
+                if (kk < cnt) {
+                    if (slow) {
+                        const uint32_t pos = atomicAdd(nslow, 1u);
+                        slow_list[pos] = (uint32_t)(base + kk);
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        if ((uint32_t)q < W) so[kk * W + q] = res[q];
+                    if (counts) counts[base + kk] = (uint8_t)rc;
+                }
+            }
+        }
+        __syncthreads();
+        uint32_t* dst = out + base * W;
+        const uint32_t tot = cnt * W;
+        if (ovec && cnt == TK && (tot & 3) == 0) {
+            u32x4* d4 = reinterpret_cast<u32x4*>(dst);
+            const u32x4* s4 = reinterpret_cast<const u32x4*>(so);
+            for (uint32_t k = tid; k < tot / 4; k += kLkThreads) __builtin_nontemporal_store(s4[k], d4 + k);
+        } else {
+            for (uint32_t k = tid; k < tot; k += kLkThreads) dst[k] = so[k];
+        }
+        __syncthreads();
+    }
+}
+
+// Exact completion of the keys k_lookupn_probe deferred (same stream, so it sees the list and
+// overwrites those rows): binary search in the bucket + the reference walk.
+template <int LEN, int MODE = 0>
+__global__ __launch_bounds__(256) void k_lookupn_fix(const uint8_t* __restrict__ keys, PackedView rv, int np,
+                                                     uint32_t W, uint32_t* __restrict__ out,
+                                                     uint8_t* __restrict__ counts,
+                                                     const uint32_t* __restrict__ slow,
+                                                     const uint32_t* __restrict__ nslow) {
+    const uint32_t total = *nslow;
+    const uint32_t gstride = gridDim.x * blockDim.x;
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < total; s += gstride) {
+        const uint64_t k = slow[s];
+        uint32_t w[LEN / 4];
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(keys + k * LEN);
+#pragma unroll
+        for (int j = 0; j < LEN / 4; j++) w[j] = src[j];
+        const uint32_t h = fh::hash32_words<LEN>(w);
+        const uint32_t i = rv.find(h);
+        uint32_t res[4];
+        int c;
+        if constexpr (MODE == 2) {
+            res[0] = i; res[1] = i + 1; res[2] = i + 2; res[3] = i + 3;
+            c = 1;
+        } else {
+            c = ring_walk<4>(rv, i, np, res);
+        }
+        uint32_t* row = out + k * W;
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if ((uint32_t)q < W) row[q] = res[q];
+        if (counts) counts[k] = (uint8_t)c;
+    }
+}
+
 // Generic keys: per-thread byte fetches (variable length via uint64 offsets, or any stride),
 // or precomputed hashes (hashes != null).
-template <int MAXN>
+template <int MAXN, class View>
 __global__ __launch_bounds__(kLkThreads) void k_lookupn_generic(const uint8_t* __restrict__ keys,
                                                                 const uint64_t* __restrict__ off,
                                                                 uint32_t stride,
                                                                 const uint32_t* __restrict__ hashes,
-                                                                uint64_t n, RingView rv, int np, uint32_t W,
+                                                                uint64_t n, View rv, int np, uint32_t W,
                                                                 uint32_t* __restrict__ out,
                                                                 uint8_t* __restrict__ counts) {
     const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
@@ -197,7 +471,7 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_generic(const uint8_t* _
             }
             h = fh::hash32(fh::PtrSrc{keys + b}, (uint32_t)(e - b));
         }
-        const uint32_t i = ring_find(rv, h);
+        const uint32_t i = rv.find(h);
         uint32_t* row = out + k * W;
         int c;
         if constexpr (MAXN > 0) {
@@ -328,6 +602,13 @@ __global__ void k_bucket_index(const uint32_t* __restrict__ tok, uint32_t M, uin
     }
 }
 
+__global__ void k_pack(const uint32_t* __restrict__ tok, const uint32_t* __restrict__ own, uint32_t M,
+                       uint32_t B, uint32_t* __restrict__ ent) {
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < (uint64_t)M + kEntPad; j += gstride)
+        ent[j] = j < M ? ((tok[j] << B) | own[j]) : 0xFFFFFFFFu;
+}
+
 // big-endian 4-byte chunk c of name(ids[i]) (0-padded): the LSD key for lexicographic order.
 __global__ void k_name_chunk(const uint8_t* __restrict__ names, const uint64_t* __restrict__ noff,
                              const uint32_t* __restrict__ ids, uint32_t n, uint32_t c,
@@ -429,6 +710,11 @@ struct Ring {
     DevBuf<uint32_t> tok, own, tok2, own2, bstart;
     uint32_t M = 0;
     uint32_t bbits = 8;
+    // packed lookup layout (valid while every interned id < 2^16)
+    DevBuf<uint32_t> ent, pbstart;
+    DevBuf<uint32_t> slow, nslow;  // deferred keys of the probe kernel
+    bool packed = false;
+    uint32_t pbits = 16;
     // name order for checksums
     DevBuf<uint32_t> sorted_ids;
     uint32_t sorted_n = 0;
@@ -447,6 +733,7 @@ struct Ring {
     RingView view() const {
         return RingView{tok.p, own.p, bstart.p, M, 32u - bbits};
     }
+    PackedView pview() const { return PackedView{ent.p, pbstart.p, M, pbits}; }
 };
 
 static void ring_sync_names(Ring& r) {
@@ -490,6 +777,21 @@ static void ring_rebuild_index(Ring& r) {
     hipLaunchKernelGGL(k_bucket_index, dim3(grid_for(nbk, 256)), dim3(256), 0, r.st, r.tok.p, r.M, r.bbits,
                        r.bstart.p);
     RP_HIP(hipGetLastError());
+    // packed layout: 2^B >= M (about one token per bucket, so the 4 entries at the bucket
+    // start usually hold the answer) and every interned id < 2^B; B <= 24 (64 MB index)
+    uint32_t B = 8;
+    while (B < 24 && ((1ull << B) < r.M || (1ull << B) < r.names.size())) B++;
+    r.packed = (1ull << B) >= r.names.size();
+    if (r.packed) {
+        r.pbits = B;
+        r.ent.reserve((uint64_t)r.M + kEntPad);
+        r.pbstart.reserve((1ull << B) + 1);
+        hipLaunchKernelGGL(k_pack, dim3(grid_for((uint64_t)r.M + kEntPad, 256)), dim3(256), 0, r.st, r.tok.p,
+                           r.own.p, r.M, B, r.ent.p);
+        hipLaunchKernelGGL(k_bucket_index, dim3(grid_for((1ull << B) + 1, 256)), dim3(256), 0, r.st, r.tok.p, r.M,
+                           B, r.pbstart.p);
+        RP_HIP(hipGetLastError());
+    }
 }
 
 // Device replica tokens for server ids (or caller tokens), sorted stably by token.
@@ -609,40 +911,91 @@ static void ring_compute_checksum(Ring& r) {
     r.ck_len = L;
 }
 
+template <class View>
+static void launch_lookupn_view(const View& rv, const uint8_t* keys, const uint64_t* off, uint32_t stride,
+                                const uint32_t* hashes, uint64_t n, int np, uint32_t W, uint32_t* out,
+                                uint8_t* counts, hipStream_t st) {
+    const unsigned grid_fixed = grid_for(n, kLkThreads, 256 * 8);
+    const bool fixed36 = !hashes && stride == 36 && ((reinterpret_cast<uintptr_t>(keys) & 3) == 0);
+    const int need = np <= 0 ? 1 : np;
+    const int ablate = getenv("RP_LOOKUP_ABLATE") ? atoi(getenv("RP_LOOKUP_ABLATE")) : 0;
+    if (fixed36 && W <= 4 && need <= 4 && need > 1 && ablate == 1) {
+        hipLaunchKernelGGL((k_lookupn_fixed<36, 4, View, 1>), dim3(grid_fixed), dim3(kLkThreads), 0, st, keys, n, rv,
+                           np, W, out, counts);
+    } else if (fixed36 && W <= 4 && need <= 4 && need > 1 && ablate == 2) {
+        hipLaunchKernelGGL((k_lookupn_fixed<36, 4, View, 2>), dim3(grid_fixed), dim3(kLkThreads), 0, st, keys, n, rv,
+                           np, W, out, counts);
+    } else if (fixed36 && W <= 8 && need <= 8) {
+        if (need == 1 && W == 1)
+            hipLaunchKernelGGL((k_lookupn_fixed<36, 1, View>), dim3(grid_fixed), dim3(kLkThreads), 0, st, keys, n,
+                               rv, np, W, out, counts);
+        else if (need <= 4 && W <= 4)
+            hipLaunchKernelGGL((k_lookupn_fixed<36, 4, View>), dim3(grid_fixed), dim3(kLkThreads), 0, st, keys, n,
+                               rv, np, W, out, counts);
+        else
+            hipLaunchKernelGGL((k_lookupn_fixed<36, 8, View>), dim3(grid_fixed), dim3(kLkThreads), 0, st, keys, n,
+                               rv, np, W, out, counts);
+    } else {
+        const unsigned g = grid_for(n, 256, 256 * 8);
+        if (need == 1)
+            hipLaunchKernelGGL((k_lookupn_generic<1, View>), dim3(g), dim3(256), 0, st, keys, off, stride, hashes,
+                               n, rv, np, W, out, counts);
+        else if (need <= 4)
+            hipLaunchKernelGGL((k_lookupn_generic<4, View>), dim3(g), dim3(256), 0, st, keys, off, stride, hashes,
+                               n, rv, np, W, out, counts);
+        else if (need <= 8)
+            hipLaunchKernelGGL((k_lookupn_generic<8, View>), dim3(g), dim3(256), 0, st, keys, off, stride, hashes,
+                               n, rv, np, W, out, counts);
+        else
+            hipLaunchKernelGGL((k_lookupn_generic<0, View>), dim3(g), dim3(256), 0, st, keys, off, stride, hashes,
+                               n, rv, np, W, out, counts);
+    }
+    RP_HIP(hipGetLastError());
+}
+
 static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, uint32_t stride,
                            const uint32_t* hashes, uint64_t n, int np, uint32_t W, uint32_t* out, uint8_t* counts,
                            hipStream_t st) {
     if (n == 0) return;
-    const RingView rv = r.view();
-    const unsigned grid_fixed = grid_for(n, kLkThreads, 256 * 8);
+    // the ring is rebuilt on r.st; make the caller's stream wait for it
+    if (st != r.st) RP_HIP(hipStreamSynchronize(r.st));
     const bool fixed36 = !hashes && stride == 36 && ((reinterpret_cast<uintptr_t>(keys) & 3) == 0);
     const int need = np <= 0 ? 1 : np;
-    if (fixed36 && W <= 8 && need <= 8) {
-        if (need == 1 && W == 1)
-            hipLaunchKernelGGL((k_lookupn_fixed<36, 1>), dim3(grid_fixed), dim3(kLkThreads), 0, st, keys, n, rv, np,
-                               W, out, counts);
-        else if (need <= 4 && W <= 4)
-            hipLaunchKernelGGL((k_lookupn_fixed<36, 4>), dim3(grid_fixed), dim3(kLkThreads), 0, st, keys, n, rv, np,
-                               W, out, counts);
-        else
-            hipLaunchKernelGGL((k_lookupn_fixed<36, 8>), dim3(grid_fixed), dim3(kLkThreads), 0, st, keys, n, rv, np,
-                               W, out, counts);
-    } else {
-        const unsigned g = grid_for(n, 256, 256 * 8);
-        if (need == 1)
-            hipLaunchKernelGGL((k_lookupn_generic<1>), dim3(g), dim3(256), 0, st, keys, off, stride, hashes, n, rv,
-                               np, W, out, counts);
-        else if (need <= 4)
-            hipLaunchKernelGGL((k_lookupn_generic<4>), dim3(g), dim3(256), 0, st, keys, off, stride, hashes, n, rv,
-                               np, W, out, counts);
-        else if (need <= 8)
-            hipLaunchKernelGGL((k_lookupn_generic<8>), dim3(g), dim3(256), 0, st, keys, off, stride, hashes, n, rv,
-                               np, W, out, counts);
-        else
-            hipLaunchKernelGGL((k_lookupn_generic<0>), dim3(g), dim3(256), 0, st, keys, off, stride, hashes, n, rv,
-                               np, W, out, counts);
+    const bool use_packed = r.packed && !getenv_flag("RP_RING_WIDE");
+    if (use_packed && fixed36 && W <= 4 && need <= 4 && !getenv_flag("RP_RING_NOWINDOW")) {
+        RP_REQUIRE(n < (1ull << 32), "lookupn: at most 2^32-1 keys per call");
+        r.slow.reserve(n + 1);
+        r.nslow.reserve(1);
+        RP_HIP(hipMemsetAsync(r.nslow.p, 0, sizeof(uint32_t), st));
+        const int ablate = getenv("RP_LOOKUP_ABLATE") ? atoi(getenv("RP_LOOKUP_ABLATE")) : 0;
+        const int kpl = getenv("RP_LOOKUP_KPL") ? atoi(getenv("RP_LOOKUP_KPL")) : kDefaultKPL;
+        const PackedView pv = r.pview();
+#define RP_PROBE(KPL, MODE)                                                                                     \
+    hipLaunchKernelGGL((k_lookupn_probe<36, KPL, MODE>), dim3(grid_for(n, kLkThreads * KPL, 256 * 8)),           \
+                       dim3(kLkThreads), 0, st, keys, n, pv, np, W, out, counts, r.slow.p, r.nslow.p);           \
+    hipLaunchKernelGGL((k_lookupn_fix<36, MODE>), dim3(256), dim3(256), 0, st, keys, pv, np, W, out, counts,     \
+                       r.slow.p, r.nslow.p)
+        if (ablate == 1) {
+            RP_PROBE(2, 1);
+        } else if (ablate == 2) {
+            RP_PROBE(2, 2);
+        } else if (kpl == 1) {
+            RP_PROBE(1, 0);
+        } else if (kpl == 4) {
+            RP_PROBE(4, 0);
+        } else if (kpl == 8) {
+            RP_PROBE(8, 0);
+        } else {
+            RP_PROBE(2, 0);
+        }
+#undef RP_PROBE
+        RP_HIP(hipGetLastError());
+        return;
     }
-    RP_HIP(hipGetLastError());
+    if (use_packed)
+        launch_lookupn_view(r.pview(), keys, off, stride, hashes, n, np, W, out, counts, st);
+    else
+        launch_lookupn_view(r.view(), keys, off, stride, hashes, n, np, W, out, counts, st);
 }
 
 }  // namespace rp

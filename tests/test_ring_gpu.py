@@ -105,7 +105,18 @@ def _random_history(orc, gpu, seed, pool_size, R, nbatches):
     return ring, oracle
 
 
-def test_random_histories_vs_oracle(gpu, orc):
+LAYOUTS = {"window": ("0", "0"), "packed": ("0", "1"), "wide": ("1", "1")}
+
+
+def set_layout(monkeypatch, layout):
+    wide, nowin = LAYOUTS[layout]
+    monkeypatch.setenv("RP_RING_WIDE", wide)
+    monkeypatch.setenv("RP_RING_NOWINDOW", nowin)
+
+
+@pytest.mark.parametrize("layout", list(LAYOUTS))
+def test_random_histories_vs_oracle(gpu, orc, layout, monkeypatch):
+    set_layout(monkeypatch, layout)
     ring, oracle = _random_history(orc, gpu, 3, 300, 100, 12)
     keys = orc.uuid_keys(99, 0, 20000)
     want = oracle.lookup_keys(keys)
@@ -158,7 +169,9 @@ def c2_servers(orc, n):
     return [orc.c2_addr(i) for i in range(n)]
 
 
-def test_device_resident_lookupn_c1_vs_oracle(gpu, orc):
+@pytest.mark.parametrize("layout", list(LAYOUTS))
+def test_device_resident_lookupn_c1_vs_oracle(gpu, orc, layout, monkeypatch):
+    set_layout(monkeypatch, layout)
     # C1 shape (1000 servers x 100 points), 1M device-generated keys, lookup + lookupN(3)
     servers = gu.load("ring_golden.json")["cases"][0]["batches"][0]["add"]
     ring, oracle = gpu.HashRing(), orc.Ring(100)
@@ -222,3 +235,28 @@ def test_edge_cases(gpu):
     assert ring.lookup("k") == "only"
     ids, cnt = ring.lookupn_ids([], 3)
     assert len(ids) == 0 and len(cnt) == 0
+
+
+@pytest.mark.parametrize("nserv,R", [(1, 100), (2, 2000), (3, 700), (5, 5), (40, 1)])
+def test_window_kernel_slow_paths_vs_oracle(gpu, orc, nserv, R, monkeypatch):
+    """Rings that force the window kernel's exact fallbacks: long buckets, runs of one owner,
+    wrap past the last token, rings smaller than the window."""
+    set_layout(monkeypatch, "window")
+    servers = [orc.c2_addr(i + 17) for i in range(nserv)]
+    ring, oracle = gpu.HashRing({"replicaPoints": R}), orc.Ring(R)
+    ring.addRemoveServers(servers)
+    oracle.add_remove(servers)
+    n = 1 << 16
+    d_k = torch.empty(n * 36, dtype=torch.uint8, device="cuda")
+    gpu.gen_uuid_keys_dev(5, 0, n, d_k.data_ptr())
+    keys = orc.uuid_keys(5, 0, n)
+    for nrep in (-1, 0, 1, 2, 3, 4):
+        w = max(nrep, 1)
+        d_o = torch.empty(n * w, dtype=torch.int32, device="cuda")
+        d_c = torch.empty(n, dtype=torch.uint8, device="cuda")
+        ring.lookupn_dev(d_k.data_ptr(), n, nrep, d_o.data_ptr(), d_c.data_ptr())
+        torch.cuda.synchronize()
+        want, wc = oracle.lookupn_keys(keys, nrep)
+        got = d_o.cpu().numpy().view(np.uint32).reshape(n, w)
+        assert np.array_equal(d_c.cpu().numpy(), wc), nrep
+        assert np.array_equal(got, want), nrep

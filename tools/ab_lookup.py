@@ -1,0 +1,77 @@
+"""A/B timing of lookupN kernels in ONE process, interleaved rounds (guide §5.4 rule 24).
+
+    python tools/ab_lookup.py [--servers 10000] [--log2 26] [--rounds 7]
+
+Variants: packed (16-bit owner / 2^16-bucket layout) vs wide (u32 token + owner arrays,
+RP_RING_WIDE=1), for lookup and lookupN(3). Prints median/min ms and lookups/s per variant.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--servers", type=int, default=10000)
+    ap.add_argument("--log2", type=int, default=26)
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--only", default="", help="comma-separated variant names")
+    a = ap.parse_args()
+    rpa = bench.load_pkg()
+    ring = rpa.HashRing()
+    ring.addRemoveServers([bench.c2_addr(i) for i in range(a.servers)])
+    B = 1 << a.log2
+    st = torch.cuda.current_stream()
+    keys = torch.empty(B * 36, dtype=torch.uint8, device="cuda")
+    rpa.gen_uuid_keys_dev(42, 0, B, keys.data_ptr(), st.cuda_stream)
+    out = torch.empty(B * 3, dtype=torch.int32, device="cuda")
+    variants = {
+        "probe/lookupN3": ("0", 3, "0"),
+        "probe-kpl1/lookupN3": ("0", 3, "0"),
+        "probe-kpl4/lookupN3": ("0", 3, "0"),
+        "probe-kpl8/lookupN3": ("0", 3, "0"),
+        "probe/lookup": ("0", 1, "0"),
+        "probe/ablate-hash-only": ("0", 3, "1"),
+        "probe/ablate-hash+find": ("0", 3, "2"),
+        "packed/lookupN3": ("0", 3, "0"),
+        "wide/lookupN3": ("1", 3, "0"),
+        "packed/lookup": ("0", 1, "0"),
+        "wide/lookup": ("1", 1, "0"),
+        "packed/ablate-hash+find": ("0", 3, "2"),
+    }
+    if a.only:
+        variants = {k: v for k, v in variants.items() if k in a.only.split(",")}
+    times = {k: [] for k in variants}
+    for r in range(a.rounds + 1):
+        for name, (wide, n, abl) in variants.items():
+            os.environ["RP_RING_WIDE"] = wide
+            os.environ["RP_LOOKUP_ABLATE"] = abl
+            os.environ["RP_RING_NOWINDOW"] = "0" if name.startswith("probe") else "1"
+            os.environ["RP_LOOKUP_KPL"] = name.split("/")[0][len("probe-kpl"):] if "kpl" in name else "2"
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            if n == 1:
+                ring.lookup_dev(keys.data_ptr(), B, out.data_ptr(), 36, None, st.cuda_stream)
+            else:
+                ring.lookupn_dev(keys.data_ptr(), B, n, out.data_ptr(), None, 36, None, st.cuda_stream)
+            e1.record(st)
+            torch.cuda.synchronize()
+            if r:
+                times[name].append(e0.elapsed_time(e1))
+    res = {}
+    for name, t in times.items():
+        med = float(np.median(t))
+        res[name] = {"median_ms": med, "min_ms": float(np.min(t)), "Glookups_s": B / med / 1e6,
+                     "alg_GBs": (48 if variants[name][1] == 3 else 40) * B / med / 1e6}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
