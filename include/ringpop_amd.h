@@ -104,6 +104,42 @@ int rp_ring_lookupn_dev(rp_ring *r, const uint8_t *d_keys, const uint64_t *d_off
 int rp_ring_lookupn_hashes_dev(rp_ring *r, const uint32_t *d_hashes, uint64_t n, int32_t nrep,
                                uint32_t *d_owners, uint8_t *d_counts, void *stream);
 
+/* ------------------------------------------------------------------ Membership
+ * Replaces the hot path of lib/membership/index.js Membership: update (249-324) with the
+ * Member.evaluateUpdate rules (lib/membership/member.js:71-202) and computeChecksum /
+ * generateChecksumString (48-75, 100-123). Members are interned address ids; status codes
+ * 0 alive, 1 suspect, 2 faulty, 3 leave (member.js:204-209). The JS wrapper keeps the
+ * Member objects, the members array order (getJoinPosition, 129-131) and the isReady stash
+ * (259-265): call update only where the reference would evaluate (ready or isLocal). */
+typedef struct rp_members rp_members;
+
+int rp_members_create(uint32_t capacity, int device, rp_members **out);
+int rp_members_destroy(rp_members *m);
+/* Intern addresses (ids_out[i] for each; existing names keep their id). */
+int rp_members_intern(rp_members *m, const char *bytes, const uint32_t *off, uint32_t n, uint32_t *ids_out);
+/* whoami(): the local member's id (local override, member.js:155-169). */
+int rp_members_set_local(rp_members *m, uint32_t local_id);
+/* Membership.update(changes) for k changes (ids, status, incarnation) evaluated in array order
+ * with Date.now() = now_ms. applied[i]: 0 not applied, 1 applied, 2 created a new member;
+ * new_status/new_inc: the update as applied (local override rewrites it). If anything applied
+ * the checksum is recomputed once. Host buffers (all outputs nullable). */
+int rp_members_update(rp_members *m, const uint32_t *ids, const uint8_t *status, const int64_t *inc, uint32_t k,
+                      int64_t now_ms, uint8_t *applied, uint8_t *new_status, int64_t *new_inc,
+                      uint32_t *n_applied);
+/* Same, device buffers, stream-ordered, no host synchronization (d_n_applied nullable). */
+int rp_members_update_dev(rp_members *m, const uint32_t *d_ids, const uint8_t *d_status, const int64_t *d_inc,
+                          uint32_t k, int64_t now_ms, uint8_t *d_applied, uint8_t *d_new_status,
+                          int64_t *d_new_inc, uint32_t *d_n_applied, void *stream);
+/* membership.checksum (null until the first applied update: *is_set = 0). */
+int rp_members_checksum(rp_members *m, uint32_t *out, int *is_set);
+/* computeChecksum() unconditionally. */
+int rp_members_compute_checksum(rp_members *m);
+/* generateChecksumString() (writes up to cap bytes; *len = full length). */
+int rp_members_checksum_string(rp_members *m, char *buf, uint64_t cap, uint64_t *len);
+/* Member table by id (exists/status/incarnation), cap entries. */
+int rp_members_dump(rp_members *m, uint8_t *exists, uint8_t *status, int64_t *inc, uint32_t cap);
+int rp_members_count(rp_members *m, uint32_t *n_names);
+
 #ifdef __cplusplus
 }
 #endif

@@ -62,6 +62,26 @@ def lib():
                                             ctypes.c_uint64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]
         L.orc_ring_lookupn_keys_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64,
                                                ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.orc_members_new.restype = ctypes.c_void_p
+        L.orc_members_new.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.c_uint32]
+        L.orc_members_free.argtypes = [ctypes.c_void_p]
+        L.orc_members_set_ready.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.orc_members_update.restype = ctypes.c_uint32
+        L.orc_members_update.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_uint32, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_members_set.restype = ctypes.c_uint32
+        L.orc_members_set.argtypes = [ctypes.c_void_p]
+        L.orc_members_checksum.restype = ctypes.c_int
+        L.orc_members_checksum.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_members_count.restype = ctypes.c_uint32
+        L.orc_members_count.argtypes = [ctypes.c_void_p]
+        L.orc_members_order.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_members_get.restype = ctypes.c_int
+        L.orc_members_get.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_members_checksum_string.restype = ctypes.c_uint64
+        L.orc_members_checksum_string.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
         _lib = L
     return _lib
 
@@ -177,3 +197,83 @@ class Ring:
             lib().orc_ring_lookupn_keys(self.h, keys.ctypes.data, stride, None, n, nrep, out.ctypes.data,
                                         cnt.ctypes.data)
         return out, cnt
+
+
+STATUS = {"alive": 0, "suspect": 1, "faulty": 2, "leave": 3}
+STATUS_NAME = {v: k for k, v in STATUS.items()}
+
+
+class Members:
+    """Oracle membership view (restates lib/membership/index.js update/set/checksum)."""
+
+    def __init__(self, names, local=None, join_seed=0):
+        self.names = list(names)
+        self.index = {a: i for i, a in enumerate(self.names)}
+        blob, off = pack_strings(self.names)
+        self._blob = ctypes.create_string_buffer(blob, len(blob) + 1)
+        lid = self.index[local] if local is not None else 0xFFFFFFFF
+        self.h = lib().orc_members_new(self._blob, off.ctypes.data, len(self.names), lid, join_seed)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_members_free(self.h)
+            self.h = None
+
+    def set_ready(self, ready):
+        lib().orc_members_set_ready(self.h, 1 if ready else 0)
+
+    def update_ids(self, ids, status, inc, is_local=False, now_ms=0):
+        ids = np.ascontiguousarray(ids, dtype=np.uint32)
+        st = np.ascontiguousarray(status, dtype=np.uint8)
+        inc = np.ascontiguousarray(inc, dtype=np.int64)
+        k = len(ids)
+        app = np.zeros(max(k, 1), dtype=np.uint8)
+        nst = np.zeros(max(k, 1), dtype=np.uint8)
+        ninc = np.zeros(max(k, 1), dtype=np.int64)
+        n = lib().orc_members_update(self.h, ids.ctypes.data, st.ctypes.data, inc.ctypes.data, k,
+                                     1 if is_local else 0, now_ms, app.ctypes.data, nst.ctypes.data,
+                                     ninc.ctypes.data)
+        return app[:k], nst[:k], ninc[:k], n
+
+    def update(self, changes, is_local=False, now_ms=0):
+        changes = changes if isinstance(changes, list) else [changes]
+        app, nst, ninc, _ = self.update_ids([self.index[c["address"]] for c in changes],
+                                            [STATUS[c["status"]] for c in changes],
+                                            [c["incarnationNumber"] for c in changes], is_local, now_ms)
+        out = []
+        for c, a, s_, i_ in zip(changes, app, nst, ninc):
+            if a:
+                u = dict(c)
+                u["status"] = STATUS_NAME[int(s_)]
+                u["incarnationNumber"] = int(i_)
+                out.append(u)
+        return out
+
+    def set(self):
+        return lib().orc_members_set(self.h)
+
+    @property
+    def checksum(self):
+        v = ctypes.c_uint32()
+        return v.value if lib().orc_members_checksum(self.h, ctypes.byref(v)) else None
+
+    def count(self):
+        return lib().orc_members_count(self.h)
+
+    def order(self):
+        n = self.count()
+        out = np.empty(max(n, 1), dtype=np.uint32)
+        lib().orc_members_order(self.h, out.ctypes.data)
+        return [self.names[i] for i in out[:n]]
+
+    def member(self, address):
+        st, inc = ctypes.c_uint8(), ctypes.c_int64()
+        if not lib().orc_members_get(self.h, self.index[address], ctypes.byref(st), ctypes.byref(inc)):
+            return None
+        return {"address": address, "status": STATUS_NAME[st.value], "incarnationNumber": inc.value}
+
+    def checksum_string(self):
+        n = lib().orc_members_checksum_string(self.h, None, 0)
+        buf = ctypes.create_string_buffer(n + 1)
+        lib().orc_members_checksum_string(self.h, buf, n)
+        return buf.raw[:n].decode()

@@ -66,7 +66,21 @@ SIGNATURES = {
     "rp_ring_lookup_dev": (_INT, [_P, _P, _P, _U32, _U64, _P, _P]),
     "rp_ring_lookupn_dev": (_INT, [_P, _P, _P, _U32, _U64, _I32, _P, _P, _P]),
     "rp_ring_lookupn_hashes_dev": (_INT, [_P, _P, _U64, _I32, _P, _P, _P]),
+    "rp_members_create": (_INT, [_U32, _INT, _P]),
+    "rp_members_destroy": (_INT, [_P]),
+    "rp_members_intern": (_INT, [_P, _P, _P, _U32, _P]),
+    "rp_members_set_local": (_INT, [_P, _U32]),
+    "rp_members_update": (_INT, [_P, _P, _P, _P, _U32, ctypes.c_int64, _P, _P, _P, _P]),
+    "rp_members_update_dev": (_INT, [_P, _P, _P, _P, _U32, ctypes.c_int64, _P, _P, _P, _P, _P]),
+    "rp_members_checksum": (_INT, [_P, _P, _P]),
+    "rp_members_compute_checksum": (_INT, [_P]),
+    "rp_members_checksum_string": (_INT, [_P, _P, _U64, _P]),
+    "rp_members_dump": (_INT, [_P, _P, _P, _P, _U32]),
+    "rp_members_count": (_INT, [_P, _P]),
 }
+
+STATUS = {"alive": 0, "suspect": 1, "faulty": 2, "leave": 3}
+STATUS_NAME = {v: k for k, v in STATUS.items()}
 
 
 def lib():
@@ -343,3 +357,119 @@ class HashRing:
 
     def lookup_dev(self, keys_ptr, n, owners_ptr, stride=36, off_ptr=None, stream=None):
         check(lib().rp_ring_lookup_dev(self._h, keys_ptr, off_ptr, stride, n, owners_ptr, stream))
+
+
+class Membership:
+    """Device member table behind Membership.update / computeChecksum
+    (lib/membership/index.js:48-123, 249-324; rules: lib/membership/member.js:71-202).
+
+    Addresses are interned to ids; `update` takes the reference's change dicts
+    ({address, status, incarnationNumber}) or id/status/inc arrays (`update_ids`).
+    """
+
+    def __init__(self, whoami=None, capacity=1024, device=0, now=None):
+        h = ctypes.c_void_p()
+        check(lib().rp_members_create(capacity, device, ctypes.byref(h)))
+        self._h = h
+        self._names = []
+        self._ids = {}
+        self.now = now or (lambda: 0)
+        if whoami is not None:
+            check(lib().rp_members_set_local(self._h, self.intern([whoami])[0]))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().rp_members_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def intern(self, addresses):
+        new = [a for a in dict.fromkeys(addresses) if a not in self._ids]
+        if new:
+            buf, off = _pack(new)
+            ids = np.empty(len(new), dtype=np.uint32)
+            check(lib().rp_members_intern(self._h, buf, off.ctypes.data, len(new), ids.ctypes.data))
+            for a, i in zip(new, ids):
+                self._ids[a] = int(i)
+                while len(self._names) <= i:
+                    self._names.append(None)
+                self._names[int(i)] = a
+        return [self._ids[a] for a in addresses]
+
+    def address(self, i):
+        return self._names[i]
+
+    def update_ids(self, ids, status, inc, now_ms=None):
+        ids = np.ascontiguousarray(ids, dtype=np.uint32)
+        st = np.ascontiguousarray(status, dtype=np.uint8)
+        inc = np.ascontiguousarray(inc, dtype=np.int64)
+        k = len(ids)
+        app = np.empty(max(k, 1), dtype=np.uint8)
+        nst = np.empty(max(k, 1), dtype=np.uint8)
+        ninc = np.empty(max(k, 1), dtype=np.int64)
+        na = ctypes.c_uint32()
+        now_ms = self.now() if now_ms is None else now_ms
+        check(lib().rp_members_update(self._h, ids.ctypes.data, st.ctypes.data, inc.ctypes.data, k, int(now_ms),
+                                      app.ctypes.data, nst.ctypes.data, ninc.ctypes.data, ctypes.byref(na)))
+        return app[:k], nst[:k], ninc[:k], na.value
+
+    def update(self, changes, now_ms=None):
+        """Membership.update(changes): returns the applied updates (dicts) in batch order."""
+        changes = changes if isinstance(changes, list) else [changes]
+        ids = self.intern([c["address"] for c in changes])
+        app, nst, ninc, _ = self.update_ids(ids, [STATUS[c["status"]] for c in changes],
+                                            [c["incarnationNumber"] for c in changes], now_ms)
+        out = []
+        for c, a, s_, i_ in zip(changes, app, nst, ninc):
+            if a:
+                u = dict(c)
+                u["status"] = STATUS_NAME[int(s_)]
+                u["incarnationNumber"] = int(i_)
+                out.append(u)
+        return out
+
+    @property
+    def checksum(self):
+        v, s_ = ctypes.c_uint32(), ctypes.c_int()
+        check(lib().rp_members_checksum(self._h, ctypes.byref(v), ctypes.byref(s_)))
+        return v.value if s_.value else None
+
+    def compute_checksum(self):
+        check(lib().rp_members_compute_checksum(self._h))
+        return self.checksum
+
+    def generate_checksum_string(self):
+        n = ctypes.c_uint64()
+        check(lib().rp_members_checksum_string(self._h, None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(n.value + 1)
+        check(lib().rp_members_checksum_string(self._h, buf, n.value, ctypes.byref(n)))
+        return buf.raw[:n.value].decode()
+
+    def dump(self):
+        n = ctypes.c_uint32()
+        check(lib().rp_members_count(self._h, ctypes.byref(n)))
+        m = n.value
+        ex = np.empty(max(m, 1), dtype=np.uint8)
+        st = np.empty(max(m, 1), dtype=np.uint8)
+        inc = np.empty(max(m, 1), dtype=np.int64)
+        check(lib().rp_members_dump(self._h, ex.ctypes.data, st.ctypes.data, inc.ctypes.data, m))
+        return ex[:m], st[:m], inc[:m]
+
+    def member(self, address):
+        i = self._ids.get(address)
+        if i is None:
+            return None
+        ex, st, inc = self.dump()
+        if not ex[i]:
+            return None
+        return {"address": address, "status": STATUS_NAME[int(st[i])], "incarnationNumber": int(inc[i])}
+
+    def update_dev(self, d_ids, d_status, d_inc, k, now_ms, d_applied=None, d_new_status=None, d_new_inc=None,
+                   d_n_applied=None, stream=None):
+        check(lib().rp_members_update_dev(self._h, d_ids, d_status, d_inc, k, int(now_ms), d_applied, d_new_status,
+                                          d_new_inc, d_n_applied, stream))

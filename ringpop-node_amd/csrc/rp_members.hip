@@ -1,0 +1,374 @@
+// rp_members.hip — the membership view on MI355X: batched SWIM merge + membership checksum.
+//
+// Replaces the hot loop of lib/membership/index.js Membership.update (249-324: a sequential
+// fold of Member.evaluateUpdate, member.js:71-202) and computeChecksum /
+// generateChecksumString (48-75, 100-123). The fold is order-sensitive only among changes to
+// the same address, so the batch is stably sorted by member id (keeping arrival order inside
+// each id), and one lane folds each id's segment in arrival order while all segments run in
+// parallel. The member table is SoA in HBM (exists u8, status u8, incarnation i64 per id).
+// The checksum string is rebuilt on the device in address order (lengths -> scan -> scatter)
+// and hashed by the long-chain farmhash kernel; every step is gated on "anything applied" read
+// from device memory, so a batch never syncs with the host.
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/ringpop_amd.h"
+#include "rp_hashlong.h"
+#include "rp_names.h"
+#include "rp_swim.h"
+
+namespace rp {
+
+namespace {
+
+__global__ void k_sort_init(const uint32_t* __restrict__ ids, uint32_t k, uint32_t* __restrict__ sk,
+                            uint32_t* __restrict__ sv) {
+    const uint32_t gstride = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < k; i += gstride) {
+        sk[i] = ids[i];
+        sv[i] = i;
+    }
+}
+
+// One lane per id segment of the (id, arrival)-sorted batch: the sequential fold of
+// Membership.update restricted to one address (lib/membership/index.js:272-304).
+// applied: 0 = not applied, 1 = applied to an existing member, 2 = created a new member.
+__global__ void k_fold(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv, uint32_t k,
+                       const uint8_t* __restrict__ ch_status, const int64_t* __restrict__ ch_inc,
+                       uint8_t* __restrict__ exists, uint8_t* __restrict__ status, int64_t* __restrict__ inc,
+                       uint32_t local_id, int64_t now_ms, uint8_t* __restrict__ applied,
+                       uint8_t* __restrict__ new_status, int64_t* __restrict__ new_inc,
+                       uint32_t* __restrict__ n_applied) {
+    const uint32_t gstride = gridDim.x * blockDim.x;
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < k; p += gstride) {
+        const uint32_t id = sk[p];
+        if (p > 0 && sk[p - 1] == id) continue;  // not a segment head
+        bool ex = exists[id] != 0;
+        uint8_t st = status[id];
+        int64_t in = inc[id];
+        uint32_t napp = 0;
+        for (uint32_t q = p; q < k && sk[q] == id; q++) {
+            const uint32_t j = sv[q];
+            uint8_t us = ch_status[j];
+            int64_t ui = ch_inc[j];
+            uint8_t a;
+            if (!ex) {  // _createMember verbatim (index.js:277-291)
+                ex = true;
+                a = 2;
+            } else {
+                a = evaluate_update(st, in, id == local_id, us, ui, now_ms) ? 1 : 0;
+            }
+            if (a) {
+                st = us;
+                in = ui;
+                napp++;
+            }
+            if (applied) applied[j] = a;
+            if (new_status) new_status[j] = us;
+            if (new_inc) new_inc[j] = ui;
+        }
+        exists[id] = ex ? 1 : 0;
+        status[id] = st;
+        inc[id] = in;
+        if (napp) atomicAdd(n_applied, napp);
+    }
+}
+
+// generateChecksumString pieces (index.js:115-120): address + status + incarnation + ';'
+__global__ void k_mck_len(const uint32_t* __restrict__ order, uint32_t n, const uint8_t* __restrict__ exists,
+                          const uint8_t* __restrict__ status, const int64_t* __restrict__ inc,
+                          const uint64_t* __restrict__ noff, const uint32_t* __restrict__ gate,
+                          uint32_t* __restrict__ len) {
+    if (gate && *gate == 0) return;
+    const uint32_t gstride = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gstride) {
+        const uint32_t id = order[i];
+        len[i] = exists[id] ? (uint32_t)(noff[id + 1] - noff[id]) + status_len(status[id]) + dec_len(inc[id]) + 1u : 0u;
+    }
+}
+
+__global__ void k_mck_write(const uint32_t* __restrict__ order, uint32_t n, const uint8_t* __restrict__ exists,
+                            const uint8_t* __restrict__ status, const int64_t* __restrict__ inc,
+                            const uint8_t* __restrict__ names, const uint64_t* __restrict__ noff,
+                            const uint32_t* __restrict__ pos, const uint32_t* __restrict__ gate,
+                            uint8_t* __restrict__ buf) {
+    if (gate && *gate == 0) return;
+    const uint32_t gstride = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gstride) {
+        const uint32_t id = order[i];
+        if (!exists[id]) continue;
+        uint8_t* o = buf + pos[i];
+        const uint64_t b = noff[id];
+        const uint32_t L = (uint32_t)(noff[id + 1] - b);
+        for (uint32_t q = 0; q < L; q++) *o++ = names[b + q];
+        const uint8_t st = status[id];
+        const uint32_t sl = status_len(st);
+        for (uint32_t q = 0; q < sl; q++) *o++ = status_char(st, q);
+        const uint32_t dl = dec_len(inc[id]);
+        dec_write(inc[id], o, dl);
+        o[dl] = ';';
+    }
+}
+
+__global__ void k_copy_grow(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b,
+                            const int64_t* __restrict__ c, uint32_t n, uint8_t* __restrict__ a2,
+                            uint8_t* __restrict__ b2, int64_t* __restrict__ c2, uint32_t n2) {
+    const uint32_t gstride = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += gstride) {
+        a2[i] = i < n ? a[i] : 0;
+        b2[i] = i < n ? b[i] : 0;
+        c2[i] = i < n ? c[i] : 0;
+    }
+}
+
+}  // namespace
+
+struct Members {
+    int device = 0;
+    hipStream_t st = nullptr;
+    NameTable nt;
+    uint32_t local_id = 0xFFFFFFFFu;
+    uint32_t cap = 0;
+    DevBuf<uint8_t> exists, status;
+    DevBuf<int64_t> inc;
+    DevBuf<uint32_t> ck;        // [0] checksum, [1] is_set
+    DevBuf<uint32_t> napplied;  // per-batch applied count (the checksum gate)
+    DevBuf<uint8_t> ck_buf;
+    DevBuf<uint32_t> ck_len, ck_pos;
+    DevBuf<uint32_t> sk, sv;
+    // host-buffer staging
+    DevBuf<uint32_t> io_ids;
+    DevBuf<uint8_t> io_st, io_app, io_nst;
+    DevBuf<int64_t> io_inc, io_ninc;
+    Scratch ws;
+
+    void grow(uint32_t need) {
+        if (need <= cap) return;
+        uint32_t nc = std::max<uint32_t>(need, cap ? cap * 2 : 1024);
+        DevBuf<uint8_t> e2, s2;
+        DevBuf<int64_t> i2;
+        e2.reserve(nc);
+        s2.reserve(nc);
+        i2.reserve(nc);
+        hipLaunchKernelGGL(k_copy_grow, dim3(grid_for(nc, 256)), dim3(256), 0, st, exists.p, status.p, inc.p, cap,
+                           e2.p, s2.p, i2.p, nc);
+        RP_HIP(hipGetLastError());
+        RP_HIP(hipStreamSynchronize(st));
+        exists.swap(e2);
+        status.swap(s2);
+        inc.swap(i2);
+        cap = nc;
+    }
+
+    // Everything below is stream-ordered on `s` and never syncs with the host.
+    void update_dev(const uint32_t* ids, const uint8_t* chs, const int64_t* chi, uint32_t k, int64_t now_ms,
+                    uint8_t* applied, uint8_t* nst, int64_t* ninc, uint32_t* n_applied_out, hipStream_t s) {
+        if (s != st) RP_HIP(hipStreamSynchronize(st));
+        RP_HIP(hipMemsetAsync(napplied.p, 0, sizeof(uint32_t), s));
+        if (k) {
+            sk.reserve(k);
+            sv.reserve(k);
+            hipLaunchKernelGGL(k_sort_init, dim3(grid_for(k, 256)), dim3(256), 0, s, ids, k, sk.p, sv.p);
+            int bits = 8;
+            while (bits < 32 && (1ull << bits) < nt.size()) bits += 8;
+            radix_sort_pairs(sk.p, sv.p, k, 0, bits, s, ws);
+            hipLaunchKernelGGL(k_fold, dim3(grid_for(k, 256)), dim3(256), 0, s, sk.p, sv.p, k, chs, chi, exists.p,
+                               status.p, inc.p, local_id, now_ms, applied, nst, ninc, napplied.p);
+            RP_HIP(hipGetLastError());
+            checksum_dev(s, napplied.p);
+        }
+        if (n_applied_out)
+            RP_HIP(hipMemcpyAsync(n_applied_out, napplied.p, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    }
+
+    // Membership.computeChecksum (index.js:48-75) gated on *gate != 0 (null = always).
+    void checksum_dev(hipStream_t s, const uint32_t* gate) {
+        const uint32_t n = nt.size();
+        if (!n) return;
+        ck_len.reserve(n + 1);
+        ck_pos.reserve(n + 1);
+        // worst-case string: names + ';' + "suspect" + 20 digits per member
+        ck_buf.reserve(nt.h_bytes.size() + (uint64_t)n * 29 + 16);
+        hipLaunchKernelGGL(k_mck_len, dim3(grid_for(n, 256)), dim3(256), 0, s, nt.sorted.p, n, exists.p, status.p,
+                           inc.p, nt.d_noff.p, gate, ck_len.p);
+        RP_HIP(hipGetLastError());
+        scan_exclusive_u32(ck_len.p, ck_pos.p, n, s, ws);
+        hipLaunchKernelGGL(k_mck_write, dim3(grid_for(n, 256)), dim3(256), 0, s, nt.sorted.p, n, exists.p, status.p,
+                           inc.p, nt.d_bytes.p, nt.d_noff.p, ck_pos.p, gate, ck_buf.p);
+        RP_HIP(hipGetLastError());
+        hash_long(ck_buf.p, 0, ck_pos.p + n, gate, ck.p, s);
+    }
+};
+
+}  // namespace rp
+
+// ==================================================================================== C ABI
+
+struct rp_members {
+    rp::Members impl;
+};
+
+using rp::guard;
+
+static rp::Members& MB(rp_members* m) {
+    if (!m) throw rp::Error(rp::RP_EINVAL, "null members handle");
+    RP_HIP(hipSetDevice(m->impl.device));
+    return m->impl;
+}
+
+extern "C" {
+
+int rp_members_create(uint32_t capacity, int device, rp_members** out) {
+    return guard([&] {
+        RP_REQUIRE(out, "out is null");
+        int nd = 0;
+        RP_HIP(hipGetDeviceCount(&nd));
+        RP_REQUIRE(device >= 0 && device < nd, "no such HIP device");
+        RP_HIP(hipSetDevice(device));
+        auto* h = new rp_members();
+        rp::Members& m = h->impl;
+        m.device = device;
+        hipError_t e = hipStreamCreateWithFlags(&m.st, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            delete h;
+            throw rp::Error(rp::RP_EDEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+        }
+        m.ck.reserve(2);
+        m.napplied.reserve(1);
+        RP_HIP(hipMemsetAsync(m.ck.p, 0, 2 * sizeof(uint32_t), m.st));
+        m.grow(capacity ? capacity : 1024);
+        RP_HIP(hipStreamSynchronize(m.st));
+        *out = h;
+    });
+}
+
+int rp_members_destroy(rp_members* m) {
+    return guard([&] {
+        if (!m) return;
+        (void)hipSetDevice(m->impl.device);
+        if (m->impl.st) {
+            (void)hipStreamSynchronize(m->impl.st);
+            (void)hipStreamDestroy(m->impl.st);
+        }
+        delete m;
+    });
+}
+
+int rp_members_intern(rp_members* h, const char* bytes, const uint32_t* off, uint32_t n, uint32_t* ids_out) {
+    return guard([&] {
+        rp::Members& m = MB(h);
+        RP_REQUIRE(n == 0 || (bytes && off), "intern: null names");
+        for (uint32_t i = 0; i < n; i++) {
+            const uint32_t id = m.nt.intern(bytes + off[i], off[i + 1] - off[i]);
+            if (ids_out) ids_out[i] = id;
+        }
+        m.grow(m.nt.size());
+        m.nt.sort(m.st, m.ws);  // address order for checksums (also uploads the names)
+        RP_HIP(hipStreamSynchronize(m.st));
+    });
+}
+
+int rp_members_set_local(rp_members* h, uint32_t local_id) {
+    return guard([&] { MB(h).local_id = local_id; });
+}
+
+int rp_members_update_dev(rp_members* h, const uint32_t* d_ids, const uint8_t* d_status, const int64_t* d_inc,
+                          uint32_t k, int64_t now_ms, uint8_t* d_applied, uint8_t* d_new_status, int64_t* d_new_inc,
+                          uint32_t* d_n_applied, void* stream) {
+    return guard([&] {
+        rp::Members& m = MB(h);
+        RP_REQUIRE(k == 0 || (d_ids && d_status && d_inc), "update_dev: null change buffers");
+        m.update_dev(d_ids, d_status, d_inc, k, now_ms, d_applied, d_new_status, d_new_inc, d_n_applied,
+                     rp::as_stream(stream));
+    });
+}
+
+int rp_members_update(rp_members* h, const uint32_t* ids, const uint8_t* status, const int64_t* inc, uint32_t k,
+                      int64_t now_ms, uint8_t* applied, uint8_t* new_status, int64_t* new_inc, uint32_t* n_applied) {
+    return guard([&] {
+        rp::Members& m = MB(h);
+        RP_REQUIRE(k == 0 || (ids && status && inc), "update: null change buffers");
+        for (uint32_t i = 0; i < k; i++) RP_REQUIRE(ids[i] < m.nt.size(), "update: id was never interned");
+        const uint32_t kk = k ? k : 1;
+        m.io_ids.reserve(kk);
+        m.io_st.reserve(kk);
+        m.io_inc.reserve(kk);
+        m.io_app.reserve(kk);
+        m.io_nst.reserve(kk);
+        m.io_ninc.reserve(kk);
+        if (k) {
+            RP_HIP(hipMemcpyAsync(m.io_ids.p, ids, 4ull * k, hipMemcpyHostToDevice, m.st));
+            RP_HIP(hipMemcpyAsync(m.io_st.p, status, k, hipMemcpyHostToDevice, m.st));
+            RP_HIP(hipMemcpyAsync(m.io_inc.p, inc, 8ull * k, hipMemcpyHostToDevice, m.st));
+        }
+        m.update_dev(m.io_ids.p, m.io_st.p, m.io_inc.p, k, now_ms, m.io_app.p, m.io_nst.p, m.io_ninc.p, nullptr, m.st);
+        if (k) {
+            if (applied) RP_HIP(hipMemcpyAsync(applied, m.io_app.p, k, hipMemcpyDeviceToHost, m.st));
+            if (new_status) RP_HIP(hipMemcpyAsync(new_status, m.io_nst.p, k, hipMemcpyDeviceToHost, m.st));
+            if (new_inc) RP_HIP(hipMemcpyAsync(new_inc, m.io_ninc.p, 8ull * k, hipMemcpyDeviceToHost, m.st));
+        }
+        uint32_t na = 0;
+        RP_HIP(hipMemcpyAsync(&na, m.napplied.p, 4, hipMemcpyDeviceToHost, m.st));
+        RP_HIP(hipStreamSynchronize(m.st));
+        if (n_applied) *n_applied = na;
+    });
+}
+
+int rp_members_checksum(rp_members* h, uint32_t* out, int* is_set) {
+    return guard([&] {
+        rp::Members& m = MB(h);
+        uint32_t v[2];
+        RP_HIP(hipMemcpyAsync(v, m.ck.p, sizeof v, hipMemcpyDeviceToHost, m.st));
+        RP_HIP(hipStreamSynchronize(m.st));
+        if (out) *out = v[0];
+        if (is_set) *is_set = v[1] ? 1 : 0;
+    });
+}
+
+int rp_members_compute_checksum(rp_members* h) {
+    return guard([&] {
+        rp::Members& m = MB(h);
+        m.checksum_dev(m.st, nullptr);
+        RP_HIP(hipStreamSynchronize(m.st));
+    });
+}
+
+int rp_members_checksum_string(rp_members* h, char* buf, uint64_t cap, uint64_t* len) {
+    return guard([&] {
+        rp::Members& m = MB(h);
+        const uint32_t n = m.nt.size();
+        uint32_t total = 0;
+        if (n) {
+            m.checksum_dev(m.st, nullptr);
+            RP_HIP(hipMemcpyAsync(&total, m.ck_pos.p + n, 4, hipMemcpyDeviceToHost, m.st));
+            RP_HIP(hipStreamSynchronize(m.st));
+        }
+        const uint64_t L = total ? total - 1 : 0;
+        if (len) *len = L;
+        const uint64_t c = std::min<uint64_t>(cap, L);
+        if (buf && c) {
+            RP_HIP(hipMemcpyAsync(buf, m.ck_buf.p, c, hipMemcpyDeviceToHost, m.st));
+            RP_HIP(hipStreamSynchronize(m.st));
+        }
+    });
+}
+
+int rp_members_dump(rp_members* h, uint8_t* exists, uint8_t* status, int64_t* inc, uint32_t cap) {
+    return guard([&] {
+        rp::Members& m = MB(h);
+        const uint32_t n = std::min(cap, m.nt.size());
+        if (n) {
+            if (exists) RP_HIP(hipMemcpyAsync(exists, m.exists.p, n, hipMemcpyDeviceToHost, m.st));
+            if (status) RP_HIP(hipMemcpyAsync(status, m.status.p, n, hipMemcpyDeviceToHost, m.st));
+            if (inc) RP_HIP(hipMemcpyAsync(inc, m.inc.p, 8ull * n, hipMemcpyDeviceToHost, m.st));
+        }
+        RP_HIP(hipStreamSynchronize(m.st));
+    });
+}
+
+int rp_members_count(rp_members* h, uint32_t* n_names) {
+    return guard([&] { *n_names = MB(h).nt.size(); });
+}
+
+}  // extern "C"

@@ -1,0 +1,41 @@
+// rp_names.h — interned address table shared by the ring and the membership view.
+//
+// Host side keeps the id <-> string map (the JS caller owns strings anyway); the device keeps
+// a mirror of the bytes + offsets and the ids sorted in byte order (== JS default string sort
+// for ASCII addresses: lib/ring/index.js:100, lib/membership/index.js:102-110), which every
+// checksum string is built in.
+#pragma once
+
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "rp_prims.h"
+
+namespace rp {
+
+struct NameTable {
+    std::vector<std::string> names;
+    std::unordered_map<std::string, uint32_t> ids;
+    std::vector<uint64_t> h_noff{0};
+    std::vector<uint8_t> h_bytes;
+    uint32_t max_len = 0;
+    // device mirror
+    DevBuf<uint8_t> d_bytes;
+    DevBuf<uint64_t> d_noff;
+    uint32_t dev_n = 0;
+    // ids in byte order of their names
+    DevBuf<uint32_t> sorted;
+    uint32_t sorted_n = 0;
+    DevBuf<uint32_t> tmp;
+
+    uint32_t size() const { return (uint32_t)names.size(); }
+    uint32_t find(const char* s, uint32_t n) const;
+    uint32_t intern(const char* s, uint32_t n);
+    // upload new names (stream-ordered)
+    void sync(hipStream_t st);
+    // (re)sort ids by name on the device if names were added
+    void sort(hipStream_t st, Scratch& ws);
+};
+
+}  // namespace rp

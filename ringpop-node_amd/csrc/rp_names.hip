@@ -1,0 +1,78 @@
+// rp_names.hip — interned address table: host map + device mirror + device byte-order sort.
+#include <algorithm>
+
+#include "rp_names.h"
+
+namespace rp {
+
+namespace {
+
+// big-endian 4-byte chunk c of name(ids[i]) (0-padded): the LSD radix key for byte order.
+__global__ void k_name_chunk(const uint8_t* __restrict__ names, const uint64_t* __restrict__ noff,
+                             const uint32_t* __restrict__ ids, uint32_t n, uint32_t c, uint32_t* __restrict__ key) {
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gstride) {
+        const uint32_t id = ids[i];
+        const uint64_t b = noff[id];
+        const uint32_t L = (uint32_t)(noff[id + 1] - b);
+        uint32_t k = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t o = c * 4 + q;
+            k = (k << 8) | (o < L ? names[b + o] : 0u);
+        }
+        key[i] = k;
+    }
+}
+
+}  // namespace
+
+uint32_t NameTable::find(const char* s, uint32_t n) const {
+    auto it = ids.find(std::string(s, n));
+    return it == ids.end() ? 0xFFFFFFFFu : it->second;
+}
+
+uint32_t NameTable::intern(const char* s, uint32_t n) {
+    std::string key(s, n);
+    auto it = ids.find(key);
+    if (it != ids.end()) return it->second;
+    const uint32_t id = (uint32_t)names.size();
+    ids.emplace(key, id);
+    names.push_back(key);
+    h_bytes.insert(h_bytes.end(), key.begin(), key.end());
+    h_noff.push_back(h_bytes.size());
+    max_len = std::max(max_len, n);
+    return id;
+}
+
+void NameTable::sync(hipStream_t st) {
+    if (dev_n == names.size()) return;
+    const uint32_t nn = (uint32_t)names.size();
+    d_bytes.reserve(h_bytes.size() + 16);
+    d_noff.reserve((uint64_t)nn + 1);
+    if (!h_bytes.empty())
+        RP_HIP(hipMemcpyAsync(d_bytes.p, h_bytes.data(), h_bytes.size(), hipMemcpyHostToDevice, st));
+    RP_HIP(hipMemcpyAsync(d_noff.p, h_noff.data(), sizeof(uint64_t) * (nn + 1), hipMemcpyHostToDevice, st));
+    // the async copies read host vectors that may grow later: finish them now
+    RP_HIP(hipStreamSynchronize(st));
+    dev_n = nn;
+}
+
+void NameTable::sort(hipStream_t st, Scratch& ws) {
+    const uint32_t n = (uint32_t)names.size();
+    if (sorted_n == n) return;
+    sync(st);
+    sorted.reserve((uint64_t)n + 1);
+    tmp.reserve((uint64_t)n + 1);
+    iota_u32(sorted.p, n, st);
+    const uint32_t nchunks = (max_len + 3) / 4;
+    for (int c = (int)nchunks - 1; c >= 0; c--) {
+        hipLaunchKernelGGL(k_name_chunk, dim3(grid_for(n, 256)), dim3(256), 0, st, d_bytes.p, d_noff.p, sorted.p, n,
+                           (uint32_t)c, tmp.p);
+        RP_HIP(hipGetLastError());
+        radix_sort_pairs(tmp.p, sorted.p, n, 0, 32, st, ws);
+    }
+    sorted_n = n;
+}
+
+}  // namespace rp

@@ -22,6 +22,8 @@
 #include "../../include/ringpop_amd.h"
 #include "rp_farmhash.h"
 #include "rp_philox.h"
+#include "rp_hashlong.h"
+#include "rp_names.h"
 #include "rp_prims.h"
 
 namespace rp {
@@ -609,25 +611,6 @@ __global__ void k_pack(const uint32_t* __restrict__ tok, const uint32_t* __restr
         ent[j] = j < M ? ((tok[j] << B) | own[j]) : 0xFFFFFFFFu;
 }
 
-// big-endian 4-byte chunk c of name(ids[i]) (0-padded): the LSD key for lexicographic order.
-__global__ void k_name_chunk(const uint8_t* __restrict__ names, const uint64_t* __restrict__ noff,
-                             const uint32_t* __restrict__ ids, uint32_t n, uint32_t c,
-                             uint32_t* __restrict__ key) {
-    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gstride) {
-        const uint32_t id = ids[i];
-        const uint64_t b = noff[id];
-        const uint32_t L = (uint32_t)(noff[id + 1] - b);
-        uint32_t k = 0;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const uint32_t o = c * 4 + q;
-            k = (k << 8) | (o < L ? names[b + o] : 0u);
-        }
-        key[i] = k;
-    }
-}
-
 // checksum string pieces: len of (name + ';') for in-ring servers in name order.
 __global__ void k_ck_len(const uint32_t* __restrict__ sorted_ids, uint32_t n,
                          const uint8_t* __restrict__ in_ring, const uint64_t* __restrict__ noff,
@@ -658,13 +641,6 @@ __global__ void k_ck_scatter(const uint32_t* __restrict__ sorted_ids, uint32_t n
     }
 }
 
-// Serial farmhash32 of one long device string (the checksum): one lane; the string is
-// streamed through LDS in 16 KiB windows loaded cooperatively by the workgroup.
-__global__ __launch_bounds__(256) void k_hash_one(const uint8_t* __restrict__ s, uint64_t len,
-                                                  uint32_t* __restrict__ out) {
-    if (threadIdx.x == 0) *out = fh::hash32(fh::PtrSrc{s}, (uint32_t)len);
-}
-
 __global__ void k_hash_batch(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t n,
                              uint32_t* __restrict__ out) {
     const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
@@ -691,21 +667,13 @@ struct Ring {
     hipStream_t st = nullptr;
     uint32_t R = 100;
     // interned names (host mirror of JS `servers` keys + an id table)
-    std::vector<std::string> names;
-    std::unordered_map<std::string, uint32_t> ids;
+    NameTable nt;
     std::vector<uint8_t> in_ring;
     std::vector<uint64_t> stamp;  // insertion stamp -> Object.keys order
     uint64_t next_stamp = 1;
     uint32_t server_count = 0;
     bool has_checksum = false;
     uint32_t checksum = 0;
-    // device name table
-    DevBuf<uint8_t> d_names;
-    DevBuf<uint64_t> d_noff;
-    uint64_t dev_name_bytes = 0;
-    uint32_t dev_names = 0;
-    std::vector<uint64_t> h_noff{0};
-    std::vector<uint8_t> h_nbytes;
     // ring arrays
     DevBuf<uint32_t> tok, own, tok2, own2, bstart;
     uint32_t M = 0;
@@ -715,14 +683,12 @@ struct Ring {
     DevBuf<uint32_t> slow, nslow;  // deferred keys of the probe kernel
     bool packed = false;
     uint32_t pbits = 16;
-    // name order for checksums
-    DevBuf<uint32_t> sorted_ids;
-    uint32_t sorted_n = 0;
+    // checksum string + value
     DevBuf<uint8_t> d_inring;
     DevBuf<uint8_t> ck_buf;
-    uint64_t ck_len = 0;
+    DevBuf<uint32_t> ck_out;  // [0] hash, [1] set
     // scratch
-    DevBuf<uint32_t> nt, no, flag, pos, ids_dev, tmpk;
+    DevBuf<uint32_t> ntok, nown, flag, pos, ids_dev, tmpk;
     DevBuf<uint64_t> tmp64;
     DevBuf<uint32_t> scalar;
     DevBuf<uint32_t> io_a, io_b;
@@ -736,30 +702,12 @@ struct Ring {
     PackedView pview() const { return PackedView{ent.p, pbstart.p, M, pbits}; }
 };
 
-static void ring_sync_names(Ring& r) {
-    if (r.dev_names == r.names.size()) return;
-    const uint64_t nbytes = r.h_nbytes.size();
-    const uint32_t nn = (uint32_t)r.names.size();
-    // grow-and-reupload (name tables are small: tens of bytes per server)
-    r.d_names.reserve(nbytes + 16);
-    r.d_noff.reserve((uint64_t)nn + 1);
-    if (nbytes) RP_HIP(hipMemcpyAsync(r.d_names.p, r.h_nbytes.data(), nbytes, hipMemcpyHostToDevice, r.st));
-    RP_HIP(hipMemcpyAsync(r.d_noff.p, r.h_noff.data(), sizeof(uint64_t) * (nn + 1), hipMemcpyHostToDevice, r.st));
-    r.dev_names = nn;
-    r.dev_name_bytes = nbytes;
-}
-
 static uint32_t ring_intern(Ring& r, const char* s, uint32_t n) {
-    std::string key(s, n);
-    auto it = r.ids.find(key);
-    if (it != r.ids.end()) return it->second;
-    const uint32_t id = (uint32_t)r.names.size();
-    r.ids.emplace(key, id);
-    r.names.push_back(key);
-    r.in_ring.push_back(0);
-    r.stamp.push_back(0);
-    r.h_nbytes.insert(r.h_nbytes.end(), key.begin(), key.end());
-    r.h_noff.push_back(r.h_nbytes.size());
+    const uint32_t id = r.nt.intern(s, n);
+    if (id >= r.in_ring.size()) {
+        r.in_ring.resize(id + 1, 0);
+        r.stamp.resize(id + 1, 0);
+    }
     return id;
 }
 
@@ -780,8 +728,8 @@ static void ring_rebuild_index(Ring& r) {
     // packed layout: 2^B >= M (about one token per bucket, so the 4 entries at the bucket
     // start usually hold the answer) and every interned id < 2^B; B <= 24 (64 MB index)
     uint32_t B = 8;
-    while (B < 24 && ((1ull << B) < r.M || (1ull << B) < r.names.size())) B++;
-    r.packed = (1ull << B) >= r.names.size();
+    while (B < 24 && ((1ull << B) < r.M || (1ull << B) < r.nt.size())) B++;
+    r.packed = (1ull << B) >= r.nt.size();
     if (r.packed) {
         r.pbits = B;
         r.ent.reserve((uint64_t)r.M + kEntPad);
@@ -798,18 +746,18 @@ static void ring_rebuild_index(Ring& r) {
 static uint64_t ring_make_tokens(Ring& r, const std::vector<uint32_t>& sel_ids, const std::vector<uint32_t>* custom) {
     const uint64_t K = (uint64_t)sel_ids.size() * r.R;
     RP_REQUIRE(K < (1ull << 31), "too many replica points in one batch");
-    r.nt.reserve(K + 1);
-    r.no.reserve(K + 1);
+    r.ntok.reserve(K + 1);
+    r.nown.reserve(K + 1);
     r.ids_dev.reserve(sel_ids.size() + 1);
     RP_HIP(hipMemcpyAsync(r.ids_dev.p, sel_ids.data(), sizeof(uint32_t) * sel_ids.size(), hipMemcpyHostToDevice,
                           r.st));
     if (custom) {
-        RP_HIP(hipMemcpyAsync(r.nt.p, custom->data(), sizeof(uint32_t) * K, hipMemcpyHostToDevice, r.st));
+        RP_HIP(hipMemcpyAsync(r.ntok.p, custom->data(), sizeof(uint32_t) * K, hipMemcpyHostToDevice, r.st));
         hipLaunchKernelGGL(k_expand_owner, dim3(grid_for(K, 256)), dim3(256), 0, r.st, r.ids_dev.p,
-                           (uint32_t)sel_ids.size(), r.R, r.no.p);
+                           (uint32_t)sel_ids.size(), r.R, r.nown.p);
     } else {
-        hipLaunchKernelGGL(k_replica_tokens, dim3(grid_for(K, 256)), dim3(256), 0, r.st, r.d_names.p, r.d_noff.p,
-                           r.ids_dev.p, (uint32_t)sel_ids.size(), r.R, r.nt.p, r.no.p);
+        hipLaunchKernelGGL(k_replica_tokens, dim3(grid_for(K, 256)), dim3(256), 0, r.st, r.nt.d_bytes.p, r.nt.d_noff.p,
+                           r.ids_dev.p, (uint32_t)sel_ids.size(), r.R, r.ntok.p, r.nown.p);
     }
     RP_HIP(hipGetLastError());
     return K;
@@ -818,17 +766,17 @@ static uint64_t ring_make_tokens(Ring& r, const std::vector<uint32_t>& sel_ids, 
 static void ring_apply_adds(Ring& r, const std::vector<uint32_t>& add_ids, const std::vector<uint32_t>* custom) {
     if (add_ids.empty()) return;
     const uint64_t K = ring_make_tokens(r, add_ids, custom);
-    radix_sort_pairs(r.nt.p, r.no.p, K, 0, 32, r.st, r.ws);
+    radix_sort_pairs(r.ntok.p, r.nown.p, K, 0, 32, r.st, r.ws);
     r.flag.reserve(K + 1);
     r.pos.reserve(K + 1);
-    hipLaunchKernelGGL(k_mark_new, dim3(grid_for(K, 256)), dim3(256), 0, r.st, r.nt.p, (uint32_t)K, r.tok.p, r.M,
+    hipLaunchKernelGGL(k_mark_new, dim3(grid_for(K, 256)), dim3(256), 0, r.st, r.ntok.p, (uint32_t)K, r.tok.p, r.M,
                        r.flag.p);
     RP_HIP(hipGetLastError());
     scan_exclusive_u32(r.flag.p, r.pos.p, K, r.st, r.ws);
     const uint32_t Kp = read_u32(r.pos.p + K, r.st);
     r.tmpk.reserve((uint64_t)Kp + 1);
     r.ws.c.reserve((uint64_t)Kp + 1);
-    hipLaunchKernelGGL(k_compact_pairs, dim3(grid_for(K, 256)), dim3(256), 0, r.st, r.nt.p, r.no.p, r.flag.p,
+    hipLaunchKernelGGL(k_compact_pairs, dim3(grid_for(K, 256)), dim3(256), 0, r.st, r.ntok.p, r.nown.p, r.flag.p,
                        r.pos.p, (uint32_t)K, r.tmpk.p, r.ws.c.p);
     const uint64_t nM = (uint64_t)r.M + Kp;
     RP_REQUIRE(nM < 0xFFFFFFF0ull, "ring too large");
@@ -848,7 +796,7 @@ static void ring_apply_removes(Ring& r, const std::vector<uint32_t>& rem_ids, co
     r.flag.reserve((uint64_t)r.M + 1);
     r.pos.reserve((uint64_t)r.M + 1);
     hipLaunchKernelGGL(k_fill_u32, dim3(grid_for(r.M, 256)), dim3(256), 0, r.st, r.flag.p, (uint64_t)r.M, 1u);
-    hipLaunchKernelGGL(k_mark_del, dim3(grid_for(K, 256)), dim3(256), 0, r.st, r.nt.p, K, r.tok.p, r.M, r.flag.p);
+    hipLaunchKernelGGL(k_mark_del, dim3(grid_for(K, 256)), dim3(256), 0, r.st, r.ntok.p, K, r.tok.p, r.M, r.flag.p);
     RP_HIP(hipGetLastError());
     scan_exclusive_u32(r.flag.p, r.pos.p, r.M, r.st, r.ws);
     const uint32_t nM = read_u32(r.pos.p + r.M, r.st);
@@ -862,53 +810,33 @@ static void ring_apply_removes(Ring& r, const std::vector<uint32_t>& rem_ids, co
     r.M = nM;
 }
 
-// Sort all interned names lexicographically (bytes; == JS default sort for ASCII).
-static void ring_sort_names(Ring& r) {
-    const uint32_t n = (uint32_t)r.names.size();
-    if (r.sorted_n == n) return;
-    uint32_t Lmax = 0;
-    for (auto& s : r.names) Lmax = std::max<uint32_t>(Lmax, (uint32_t)s.size());
-    r.sorted_ids.reserve((uint64_t)n + 1);
-    r.tmpk.reserve((uint64_t)n + 1);
-    iota_u32(r.sorted_ids.p, n, r.st);
-    const uint32_t nchunks = (Lmax + 3) / 4;
-    for (int c = (int)nchunks - 1; c >= 0; c--) {
-        hipLaunchKernelGGL(k_name_chunk, dim3(grid_for(n, 256)), dim3(256), 0, r.st, r.d_names.p, r.d_noff.p,
-                           r.sorted_ids.p, n, (uint32_t)c, r.tmpk.p);
-        RP_HIP(hipGetLastError());
-        radix_sort_pairs(r.tmpk.p, r.sorted_ids.p, n, 0, 32, r.st, r.ws);
-    }
-    r.sorted_n = n;
-}
-
-// HashRing.computeChecksum (lib/ring/index.js:96-105) on the device.
+// HashRing.computeChecksum (lib/ring/index.js:96-105) on the device:
+// hash32(Object.keys(servers).sort().join(';')), names in byte order (NameTable::sort).
 static void ring_compute_checksum(Ring& r) {
-    ring_sort_names(r);
-    const uint32_t n = (uint32_t)r.names.size();
+    r.nt.sort(r.st, r.ws);
+    const uint32_t n = r.nt.size();
     r.d_inring.reserve((uint64_t)n + 1);
     if (n) RP_HIP(hipMemcpyAsync(r.d_inring.p, r.in_ring.data(), n, hipMemcpyHostToDevice, r.st));
     r.flag.reserve((uint64_t)n + 1);
     r.pos.reserve((uint64_t)n + 1);
-    uint64_t total = 0;
+    r.ck_buf.reserve(r.nt.h_bytes.size() + n + 16);
+    r.ck_out.reserve(2);
     if (n) {
-        hipLaunchKernelGGL(k_ck_len, dim3(grid_for(n, 256)), dim3(256), 0, r.st, r.sorted_ids.p, n, r.d_inring.p,
-                           r.d_noff.p, r.flag.p);
+        hipLaunchKernelGGL(k_ck_len, dim3(grid_for(n, 256)), dim3(256), 0, r.st, r.nt.sorted.p, n, r.d_inring.p,
+                           r.nt.d_noff.p, r.flag.p);
         scan_exclusive_u32(r.flag.p, r.pos.p, n, r.st, r.ws);
-        total = read_u32(r.pos.p + n, r.st);
-    }
-    const uint64_t L = total ? total - 1 : 0;  // join(';') has no trailing separator
-    r.ck_buf.reserve(total + 8);
-    if (n && total) {
-        hipLaunchKernelGGL(k_ck_scatter, dim3(grid_for((uint64_t)n * 64, 256)), dim3(256), 0, r.st,
-                           r.sorted_ids.p, n, r.d_inring.p, r.d_names.p, r.d_noff.p, r.pos.p, r.ck_buf.p);
+        hipLaunchKernelGGL(k_ck_scatter, dim3(grid_for((uint64_t)n * 64, 256)), dim3(256), 0, r.st, r.nt.sorted.p, n,
+                           r.d_inring.p, r.nt.d_bytes.p, r.nt.d_noff.p, r.pos.p, r.ck_buf.p);
         RP_HIP(hipGetLastError());
+        hash_long(r.ck_buf.p, 0, r.pos.p + n, nullptr, r.ck_out.p, r.st);
+    } else {
+        hash_long(r.ck_buf.p, 0, nullptr, nullptr, r.ck_out.p, r.st);  // "" (empty ring)
     }
-    r.scalar.reserve(4);
-    hipLaunchKernelGGL(k_hash_one, dim3(1), dim3(256), 0, r.st, r.ck_buf.p, L, r.scalar.p);
-    RP_HIP(hipGetLastError());
-    r.checksum = read_u32(r.scalar.p, r.st);
+    uint32_t v[2];
+    RP_HIP(hipMemcpyAsync(v, r.ck_out.p, sizeof v, hipMemcpyDeviceToHost, r.st));
+    RP_HIP(hipStreamSynchronize(r.st));
+    r.checksum = v[0];
     r.has_checksum = true;
-    r.ck_len = L;
 }
 
 template <class View>
@@ -1073,10 +1001,8 @@ int rp_ring_add_remove(rp_ring* h, const char* add_bytes, const uint32_t* add_of
         }
         // :78-85 — then removes in order, skipping absent servers
         for (uint32_t j = 0; j < n_rem; j++) {
-            std::string key(rem_bytes + rem_off[j], rem_off[j + 1] - rem_off[j]);
-            auto it = r.ids.find(key);
-            if (it == r.ids.end() || !r.in_ring[it->second]) continue;
-            const uint32_t id = it->second;
+            const uint32_t id = r.nt.find(rem_bytes + rem_off[j], rem_off[j + 1] - rem_off[j]);
+            if (id == rp::NIL || !r.in_ring[id]) continue;
             r.in_ring[id] = 0;
             r.server_count--;
             rem_ids.push_back(id);
@@ -1086,7 +1012,7 @@ int rp_ring_add_remove(rp_ring* h, const char* add_bytes, const uint32_t* add_of
         }
         const bool changed = !add_ids.empty() || !rem_ids.empty();
         if (changed) {
-            rp::ring_sync_names(r);
+            r.nt.sync(r.st);
             rp::ring_apply_adds(r, add_ids, add_tokens ? &add_tok_sel : nullptr);
             rp::ring_apply_removes(r, rem_ids, rem_tokens ? &rem_tok_sel : nullptr);
             rp::ring_rebuild_index(r);
@@ -1108,8 +1034,16 @@ int rp_ring_checksum(rp_ring* h, uint32_t* out, int* is_set) {
 int rp_ring_checksum_string(rp_ring* h, char* buf, uint64_t cap, uint64_t* len) {
     return guard([&] {
         rp::Ring& r = R(h);
-        if (len) *len = r.ck_len;
-        const uint64_t n = std::min<uint64_t>(cap, r.ck_len);
+        uint64_t L = 0;
+        const uint32_t nn = r.nt.size();
+        if (r.has_checksum && nn) {
+            uint32_t total = 0;
+            RP_HIP(hipMemcpyAsync(&total, r.pos.p + nn, 4, hipMemcpyDeviceToHost, r.st));
+            RP_HIP(hipStreamSynchronize(r.st));
+            L = total ? total - 1 : 0;
+        }
+        if (len) *len = L;
+        const uint64_t n = std::min<uint64_t>(cap, L);
         if (buf && n) {
             RP_HIP(hipMemcpyAsync(buf, r.ck_buf.p, n, hipMemcpyDeviceToHost, r.st));
             RP_HIP(hipStreamSynchronize(r.st));
@@ -1128,33 +1062,32 @@ int rp_ring_token_count(rp_ring* h, uint32_t* out) {
 int rp_ring_has_server(rp_ring* h, const char* name, uint32_t len, int* out) {
     return guard([&] {
         rp::Ring& r = R(h);
-        auto it = r.ids.find(std::string(name, len));
-        *out = (it != r.ids.end() && r.in_ring[it->second]) ? 1 : 0;
+        const uint32_t id = r.nt.find(name, len);
+        *out = (id != rp::NIL && r.in_ring[id]) ? 1 : 0;
     });
 }
 
 int rp_ring_server_id(rp_ring* h, const char* name, uint32_t len, uint32_t* id) {
     return guard([&] {
         rp::Ring& r = R(h);
-        auto it = r.ids.find(std::string(name, len));
-        *id = it == r.ids.end() ? RP_NULL_ID : it->second;
+        *id = r.nt.find(name, len);
     });
 }
 
 const char* rp_ring_owner_name(rp_ring* h, uint32_t id, uint32_t* len) {
-    if (!h || id >= h->impl.names.size()) {
+    if (!h || id >= h->impl.nt.size()) {
         if (len) *len = 0;
         return nullptr;
     }
-    if (len) *len = (uint32_t)h->impl.names[id].size();
-    return h->impl.names[id].data();
+    if (len) *len = (uint32_t)h->impl.nt.names[id].size();
+    return h->impl.nt.names[id].data();
 }
 
 int rp_ring_servers(rp_ring* h, uint32_t* ids_out, uint32_t cap, uint32_t* n) {
     return guard([&] {
         rp::Ring& r = R(h);
         std::vector<uint32_t> v;
-        for (uint32_t id = 0; id < r.names.size(); id++)
+        for (uint32_t id = 0; id < r.nt.size(); id++)
             if (r.in_ring[id]) v.push_back(id);
         std::sort(v.begin(), v.end(), [&](uint32_t a, uint32_t b) { return r.stamp[a] < r.stamp[b]; });
         *n = (uint32_t)v.size();

@@ -139,7 +139,123 @@ def make_ring():
     print("wrote", path, os.path.getsize(path), "bytes")
 
 
+JOIN_TAG = 0x4A4F494E  # 'JOIN' — key[1] of the getJoinPosition Philox stream (oracle/orc_members.c)
+
+
+def join_rands(seed, n):
+    return [pyoracle.philox([k, 0, 0, 0], [seed, JOIN_TAG])[0] for k in range(n)]
+
+
+def membership_cases():
+    with open(os.path.join(REF, "benchmarks", "large-membership.json")) as f:
+        large = json.load(f)
+    addrs = [m["address"] for m in large]
+    statuses = ["alive", "suspect", "faulty", "leave"]
+    cases = []
+    # 1. the override table (member.js:71-202) for a remote and the local member
+    local = "127.0.0.1:3000"
+    for tgt in ("remote", "local"):
+        addr = local if tgt == "local" else "127.0.0.1:3001"
+        for cur in statuses:
+            for upd in statuses:
+                for d in (-1, 0, 1):
+                    ops = []
+                    if tgt == "remote":
+                        ops.append({"type": "update", "changes": [[local, "alive", 1]], "isLocal": True, "now": 1})
+                    ops.append({"type": "update", "changes": [[addr, cur, 100]], "now": 2})
+                    ops.append({"type": "update", "changes": [[addr, upd, 100 + d]], "now": 777, "members": True})
+                    cases.append({"name": "rule/%s/%s/%s/%+d" % (tgt, cur, upd, d), "local": local,
+                                  "joinSeed": 1, "joinRands": join_rands(1, 4), "ops": ops})
+    # 2. random batches with duplicate addresses, new members and local updates
+    rng = random.Random(77)
+    names = addrs[:300]
+    local = names[0]
+    incs = {a: 1434401518824 + rng.randrange(10 ** 6) for a in names}
+    ops = [{"type": "update", "changes": [[local, "alive", incs[local]]], "isLocal": True, "now": 5},
+           {"type": "update", "changes": [[a, "alive", incs[a]] for a in names[1:]], "now": 6, "members": True,
+            "checksumString": True}]
+    pool = list(names)
+    for b in range(8):
+        changes = []
+        for _ in range(600):
+            r = rng.random()
+            if r < 0.03:
+                a = addrs[300 + rng.randrange(100)]
+            elif r < 0.08:
+                a = local
+            elif r < 0.38 and changes:
+                a = changes[rng.randrange(len(changes))][0]  # duplicate address in one batch
+            else:
+                a = rng.choice(pool)
+            st = rng.choices(statuses, weights=[50, 25, 15, 10])[0]
+            base = incs.get(a, 1434401518824)
+            inc = base + rng.choice([-1, 0, 0, 1, 1, 2, 1000])
+            changes.append([a, st, inc])
+        ops.append({"type": "update", "changes": changes, "now": 1434500000000 + b, "members": True,
+                    "checksumString": b == 7})
+    cases.append({"name": "random", "local": local, "joinSeed": 2, "joinRands": join_rands(2, 2000), "ops": ops})
+    # 3. the 1332-member fixture (benchmarks/large-membership.json) then a mixed batch
+    local = addrs[0]
+    ops = [{"type": "update", "changes": [[local, "alive", large[0]["incarnationNumber"]]], "isLocal": True,
+            "now": 7},
+           {"type": "update", "changes": [[m["address"], m["status"], m["incarnationNumber"]] for m in large[1:]],
+            "now": 8, "checksumString": True}]
+    changes = []
+    for _ in range(2000):
+        m = rng.choice(large)
+        changes.append([m["address"], rng.choice(statuses), m["incarnationNumber"] + rng.choice([-1, 0, 1])])
+    ops.append({"type": "update", "changes": changes, "now": 9, "members": True})
+    cases.append({"name": "fixture1332", "local": local, "joinSeed": 3, "joinRands": join_rands(3, 4000), "ops": ops})
+    # 4. stash until ready, then set() (index.js:208-265, merge.js:22-51)
+    local = "127.0.0.1:3000"
+    peers = ["127.0.0.1:%d" % (3001 + i) for i in range(6)]
+    ops = [{"type": "ready", "value": False},
+           {"type": "update", "changes": [[local, "alive", 10]], "isLocal": True, "now": 1},
+           {"type": "update", "changes": [[peers[0], "suspect", 1], [peers[1], "alive", 2], [local, "faulty", 99]]},
+           {"type": "update", "changes": [[peers[0], "alive", 2], [peers[1], "suspect", 1], [peers[2], "faulty", 1]]},
+           {"type": "update", "changes": [[peers[3], "leave", 4], [peers[0], "faulty", 2], [peers[4], "alive", 9]]},
+           {"type": "set", "members": True},
+           {"type": "ready", "value": True},
+           {"type": "update", "changes": [[peers[5], "alive", 1], [peers[2], "alive", 5]], "members": True}]
+    cases.append({"name": "stash-set", "local": local, "joinSeed": 4, "joinRands": join_rands(4, 10), "ops": ops})
+    # 5. membership_test.js:58-146 style: leave overrides and redundant leaves
+    a = "127.0.0.1:3001"
+    ops = [{"type": "update", "changes": [[local, "alive", 50]], "isLocal": True, "now": 1},
+           {"type": "update", "changes": [[a, "alive", 100]]},
+           {"type": "update", "changes": [[a, "leave", 100]]},
+           {"type": "update", "changes": [[a, "leave", 100]]},
+           {"type": "update", "changes": [[local, "leave", 50]]},
+           {"type": "update", "changes": [[local, "leave", 51]], "members": True},
+           {"type": "update", "changes": [[local, "suspect", 51], [a, "alive", 101], [a, "leave", 101]],
+            "now": 4242, "members": True}]
+    cases.append({"name": "leave", "local": local, "joinSeed": 5, "joinRands": join_rands(5, 10), "ops": ops})
+    return cases
+
+
+def make_membership():
+    cases = membership_cases()
+    outs = run_node("ref_membership.js", cases)
+    fixture = {"generator": "tests/golden/make_golden.py + tests/golden/ref_membership.js",
+               "reference": "lib/membership/index.js, member.js, merge.js (ringpop v10.9.6)",
+               "note": "changes are [address, status, incarnationNumber]; applied = [change index, status, inc] "
+                       "in return order; joinRands feed getJoinPosition (floor(r/2^32*len))",
+               "cases": []}
+    for c, o in zip(cases, outs):
+        fops = []
+        for op, oo in zip(c["ops"], o["ops"]):
+            f = dict(op)
+            f.update(oo)
+            fops.append(f)
+        fixture["cases"].append({"name": c["name"], "local": c["local"], "joinSeed": c["joinSeed"], "ops": fops})
+    path = os.path.join(HERE, "membership_golden.json")
+    with open(path, "w") as f:
+        json.dump(fixture, f, separators=(",", ":"))
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
 if __name__ == "__main__":
-    what = sys.argv[1:] or ["ring"]
+    what = sys.argv[1:] or ["ring", "membership"]
     if "ring" in what:
         make_ring()
+    if "membership" in what:
+        make_membership()

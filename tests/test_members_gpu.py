@@ -1,0 +1,119 @@
+"""GPU parity tests of the device membership merge + checksum through the C ABI.
+
+Oracles: tests/golden/membership_golden.json (what the reference Membership did) and
+oracle/orc_members.c (pinned against it in tests/test_oracle_membership.py). Bit-exact:
+applied flags, rewritten updates, member table, checksum strings and checksums.
+"""
+import importlib.util
+import os
+
+import numpy as np
+import pytest
+
+import golden_util as gu
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STAT = {"alive": 0, "suspect": 1, "faulty": 2, "leave": 3}
+
+
+def synth():
+    spec = importlib.util.spec_from_file_location("rp_synth", os.path.join(REPO, "ringpop-node_amd", "synth.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def device_state(m, names):
+    ex, st, inc = m.dump()
+    ids = m.intern(names)
+    return {a: (int(st[i]), int(inc[i])) for a, i in zip(names, ids) if ex[i]}
+
+
+@pytest.mark.parametrize("case_name", ["random", "fixture1332", "leave", "rules"])
+def test_members_match_reference_goldens(gpu, case_name):
+    cases = gu.load("membership_golden.json")["cases"]
+    sel = [c for c in cases if c["name"].startswith("rule/")] if case_name == "rules" else \
+        [c for c in cases if c["name"] == case_name]
+    for case in sel:
+        m = gpu.Membership(whoami=case["local"])
+        for op in case["ops"]:
+            ch = op["changes"]
+            ids = m.intern([c[0] for c in ch])
+            app, nst, ninc, na = m.update_ids(ids, [STAT[c[1]] for c in ch], [c[2] for c in ch],
+                                              now_ms=op.get("now", 0))
+            got = [[i, gpu.STATUS_NAME[int(nst[i])], int(ninc[i])] for i in range(len(ch)) if app[i]]
+            assert got == op["applied"], (case["name"], op.get("now"))
+            assert na == len(got)
+            assert m.checksum == op["checksum"], case["name"]
+            if "members" in op:
+                want = {w[0]: (STAT[w[1]], w[2]) for w in op["members"]}
+                assert device_state(m, list(want)) == want
+            if isinstance(op.get("checksumString"), str):
+                assert m.generate_checksum_string() == op["checksumString"]
+
+
+def test_c3_merge_vs_oracle(gpu, orc):
+    """C3 at full size: 100k members, 100k updates with 1% duplicated addresses."""
+    S = synth()
+    n = k = 100_000
+    names, st0, inc0 = S.c3_members(n)
+    m = gpu.Membership(whoami=names[0], capacity=n)
+    o = orc.Members(names, local=names[0], join_seed=0)
+    ids0 = np.asarray(m.intern(names), dtype=np.uint32)
+    assert (ids0 == np.arange(n)).all()
+    a0, _, _, na0 = m.update_ids(ids0, st0, inc0, now_ms=1)
+    oa0, _, _, ona0 = o.update_ids(ids0, st0, inc0, False, 1)
+    assert na0 == ona0 == n and (a0 == 2).all()
+    assert m.checksum == o.checksum
+    for batch in range(3):
+        ids, us, ui = S.c3_updates(n, k, seed=7 + batch, base_inc=inc0)
+        ga, gs, gi, gna = m.update_ids(ids, us, ui, now_ms=1434500000000 + batch)
+        oa, os_, oi, ona = o.update_ids(ids, us, ui, False, 1434500000000 + batch)
+        assert gna == ona
+        assert np.array_equal(ga > 0, oa > 0)
+        assert np.array_equal(gs[oa > 0], os_[oa > 0]) and np.array_equal(gi[oa > 0], oi[oa > 0])
+        assert m.checksum == o.checksum
+    ex, st, inc = m.dump()
+    for i in range(0, n, 997):
+        want = o.member(names[i])
+        assert (gpu.STATUS_NAME[int(st[i])], int(inc[i])) == (want["status"], want["incarnationNumber"])
+    assert m.generate_checksum_string() == o.checksum_string()
+
+
+def test_update_dev_no_host_sync_path(gpu, orc):
+    S = synth()
+    n = 5000
+    names, st0, inc0 = S.c3_members(n)
+    m = gpu.Membership(whoami=names[1], capacity=n)
+    m.intern(names)
+    o = orc.Members(names, local=names[1])
+    m.update_ids(np.arange(n, dtype=np.uint32), st0, inc0, now_ms=3)
+    o.update_ids(np.arange(n), st0, inc0, False, 3)
+    ids, us, ui = S.c3_updates(n, 20000, seed=11, base_inc=inc0)
+    d_ids = torch.from_numpy(ids.view(np.int32)).cuda()
+    d_st = torch.from_numpy(us).cuda()
+    d_inc = torch.from_numpy(ui).cuda()
+    d_app = torch.empty(len(ids), dtype=torch.uint8, device="cuda")
+    d_na = torch.zeros(1, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    m.update_dev(d_ids.data_ptr(), d_st.data_ptr(), d_inc.data_ptr(), len(ids), 77, d_app.data_ptr(), None, None,
+                 d_na.data_ptr(), st)
+    torch.cuda.synchronize()
+    oa, _, _, ona = o.update_ids(ids, us, ui, False, 77)
+    assert int(d_na.item()) == ona
+    assert np.array_equal(d_app.cpu().numpy() > 0, oa > 0)
+    assert m.checksum == o.checksum
+
+
+def test_empty_and_checksum_null(gpu):
+    m = gpu.Membership(whoami="127.0.0.1:3000")
+    assert m.checksum is None
+    app, _, _, na = m.update_ids([], [], [])
+    assert na == 0 and m.checksum is None
+    m.update([{"address": "127.0.0.1:3000", "status": "alive", "incarnationNumber": 5}])
+    c1 = m.checksum
+    assert c1 is not None
+    assert m.update([{"address": "127.0.0.1:3000", "status": "alive", "incarnationNumber": 5}]) == []
+    assert m.checksum == c1
