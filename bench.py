@@ -61,6 +61,51 @@ def cpu_baseline(servers, nkeys, threads, min_seconds=10.0):
                       % (done, nkeys, done // nkeys, threads, dt)}
 
 
+def merge_bench(rpa, local, n=100_000, k=100_000, batches=20, warmup=3):
+    """C3 (BASELINE.json configs[2]): 100k-member table, batches of 100k updates (1% repeated
+    addresses), Membership.update fold + one checksum per batch, inputs resident in HBM."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("rp_synth", os.path.join(REPO, "ringpop-node_amd", "synth.py"))
+    S = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(S)
+    names, st0, inc0 = S.c3_members(n)
+    m = rpa.Membership(whoami=names[0], capacity=n, device=local)
+    ids0 = np.asarray(m.intern(names), dtype=np.uint32)
+    m.update_ids(ids0, st0, inc0, now_ms=1)
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    bufs = []
+    for b in range(4):
+        ids, us, ui = S.c3_updates(n, k, seed=100 + b, base_inc=inc0)
+        bufs.append((torch.from_numpy(ids.view(np.int32)).cuda(), torch.from_numpy(us).cuda(),
+                     torch.from_numpy(ui).cuda()))
+    app = torch.empty(k, dtype=torch.uint8, device="cuda")
+    nst = torch.empty(k, dtype=torch.uint8, device="cuda")
+    ninc = torch.empty(k, dtype=torch.int64, device="cuda")
+    na = torch.zeros(1, dtype=torch.int32, device="cuda")
+
+    def one(b):
+        d = bufs[b % 4]
+        m.update_dev(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), k, 1434500000000 + b, app.data_ptr(),
+                     nst.data_ptr(), ninc.data_ptr(), na.data_ptr(), sp)
+
+    for b in range(warmup):
+        one(b)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for b in range(batches):
+        one(b)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"workload": "C3: %d-member table, %d updates/batch (1%% repeated addresses), fold + 1 checksum "
+                        "per batch" % (n, k),
+            "updates_per_s": k * batches / dt, "ms_per_batch": dt * 1e3 / batches,
+            "gpu_ms_per_batch": e0.elapsed_time(e1) / batches, "checksum": m.checksum}
+
+
 def pmc_traffic():
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
@@ -81,6 +126,7 @@ def main():
     ap.add_argument("--cpu-keys", type=int, default=1 << 24)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-merge", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -160,6 +206,8 @@ def main():
                          "bytes_per_unit": BYTES_PER_LOOKUPN3},
             "ring_build_ms": build_ms,
         }
+        if not args.no_merge:
+            out["merge"] = merge_bench(rpa, local)
         if not args.no_cpu:
             th = args.cpu_threads or min(16, os.cpu_count() or 1)
             out["cpu_baseline"] = cpu_baseline(servers, args.cpu_keys, th)

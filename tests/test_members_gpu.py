@@ -87,12 +87,12 @@ def test_update_dev_no_host_sync_path(gpu, orc):
     n = 5000
     names, st0, inc0 = S.c3_members(n)
     m = gpu.Membership(whoami=names[1], capacity=n)
-    m.intern(names)
+    dev_id = np.asarray(m.intern(names), dtype=np.uint32)  # whoami was interned first: ids != positions
     o = orc.Members(names, local=names[1])
-    m.update_ids(np.arange(n, dtype=np.uint32), st0, inc0, now_ms=3)
+    m.update_ids(dev_id, st0, inc0, now_ms=3)
     o.update_ids(np.arange(n), st0, inc0, False, 3)
     ids, us, ui = S.c3_updates(n, 20000, seed=11, base_inc=inc0)
-    d_ids = torch.from_numpy(ids.view(np.int32)).cuda()
+    d_ids = torch.from_numpy(dev_id[ids].view(np.int32)).cuda()
     d_st = torch.from_numpy(us).cuda()
     d_inc = torch.from_numpy(ui).cuda()
     d_app = torch.empty(len(ids), dtype=torch.uint8, device="cuda")
