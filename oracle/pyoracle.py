@@ -82,6 +82,18 @@ def lib():
         L.orc_members_get.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
         L.orc_members_checksum_string.restype = ctypes.c_uint64
         L.orc_members_checksum_string.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+        L.orc_sim_new.restype = ctypes.c_void_p
+        L.orc_sim_new.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int64, ctypes.c_void_p,
+                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_sim_free.argtypes = [ctypes.c_void_p]
+        L.orc_sim_step.argtypes = [ctypes.c_void_p]
+        L.orc_sim_round.restype = ctypes.c_int64
+        L.orc_sim_round.argtypes = [ctypes.c_void_p]
+        L.orc_sim_checksums.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_sim_view.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_sim_converged.restype = ctypes.c_int
+        L.orc_sim_converged.argtypes = [ctypes.c_void_p]
+        L.orc_sim_stats.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -277,3 +289,48 @@ class Members:
         buf = ctypes.create_string_buffer(n + 1)
         lib().orc_members_checksum_string(self.h, buf, n)
         return buf.raw[:n].decode()
+
+
+class Sim:
+    """Oracle gossip round model (orc_sim.c)."""
+
+    def __init__(self, names, inc0, dead, seed=11, susp_rounds=25, now0=1434500000000):
+        self.N = len(names)
+        blob, off = pack_strings(names)
+        self._blob = ctypes.create_string_buffer(blob, len(blob) + 1)
+        self._off = off
+        inc0 = np.ascontiguousarray(inc0, dtype=np.int64)
+        dead = np.ascontiguousarray(dead, dtype=np.uint8)
+        self.h = lib().orc_sim_new(self.N, seed, susp_rounds, now0, self._blob, off.ctypes.data, inc0.ctypes.data,
+                                   dead.ctypes.data)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_sim_free(self.h)
+            self.h = None
+
+    def step(self):
+        lib().orc_sim_step(self.h)
+
+    @property
+    def round(self):
+        return lib().orc_sim_round(self.h)
+
+    def checksums(self):
+        out = np.empty(self.N, dtype=np.uint32)
+        lib().orc_sim_checksums(self.h, out.ctypes.data)
+        return out
+
+    def view(self, v):
+        st = np.empty(self.N, dtype=np.uint8)
+        inc = np.empty(self.N, dtype=np.int64)
+        lib().orc_sim_view(self.h, v, st.ctypes.data, inc.ctypes.data)
+        return st, inc
+
+    def converged(self):
+        return bool(lib().orc_sim_converged(self.h))
+
+    def stats(self):
+        out = np.zeros(4, dtype=np.uint64)
+        lib().orc_sim_stats(self.h, out.ctypes.data)
+        return dict(zip(["pings", "pingreqs", "fullsyncs", "applied"], (int(x) for x in out)))

@@ -69,3 +69,20 @@ def c3_updates(n_members, k, seed=7, base_inc=None):
     status = np.where(u < 70, 0, np.where(u < 85, 1, np.where(u < 95, 2, 3))).astype(np.uint8)
     inc = base_inc[ids] + (r3.astype(np.int64) % 3) - 1
     return ids.astype(np.uint32), status, inc.astype(np.int64)
+
+
+TAG_KILL = 0x4B494C4C  # 'KILL'
+NOW0 = BASE_INC + 10 ** 9  # Date.now() at round 0 of the gossip model (+200 ms per round)
+
+
+def kill_set(n, k, seed=11):
+    """the k members killed before round 0 (partial Fisher-Yates over a
+    Philox stream); returns a uint8 mask of length n."""
+    perm = np.arange(n, dtype=np.int64)
+    r = stream(seed, TAG_KILL, max(k, 1))[0]
+    for i in range(k):
+        j = i + int((int(r[i]) * (n - i)) >> 32)
+        perm[i], perm[j] = perm[j], perm[i]
+    dead = np.zeros(n, dtype=np.uint8)
+    dead[perm[:k]] = 1
+    return dead

@@ -253,9 +253,54 @@ def make_membership():
     print("wrote", path, os.path.getsize(path), "bytes")
 
 
+def synth():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("rp_synth", os.path.join(REPO, "ringpop-node_amd", "synth.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def sim_cases():
+    S = synth()
+    cases = []
+    for name, n, k, rounds, susp, seed in [("n16k1", 16, 1, 40, 25, 11), ("n64k2", 64, 2, 45, 25, 11),
+                                           ("n128k3-susp4", 128, 3, 30, 4, 5), ("n200k10", 200, 10, 50, 25, 11)]:
+        cases.append({"name": name, "names": [S.c2_addr(i) for i in range(n)],
+                      "inc0": [int(x) for x in S.c3_members(n)[2]],
+                      "dead": [int(x) for x in S.kill_set(n, k, seed)], "seed": seed, "suspRounds": susp,
+                      "now0": S.NOW0, "rounds": rounds, "views": [0, n - 1]})
+    return cases
+
+
+def make_sim():
+    cases = sim_cases()
+    outs = run_node("ref_sim.js", cases)
+    fixture = {"generator": "tests/golden/make_golden.py + tests/golden/ref_sim.js",
+               "reference": "lib/membership/*, lib/gossip/{dissemination,suspicion}.js, lib/membership/iterator.js, "
+                            "lib/ring, lib/on_membership_event.js (ringpop v10.9.6) in the round model of "
+                            "oracle/orc_sim.c",
+               "note": "rounds[r][v] = node v's membership checksum after round r (0 for killed nodes); "
+                       "finalViews = members arrays [address, status, inc] of the listed nodes",
+               "cases": []}
+    for c, o in zip(cases, outs):
+        f = {k: c[k] for k in ("name", "seed", "suspRounds", "now0", "rounds", "views")}
+        f["n"] = len(c["names"])
+        f["dead"] = c["dead"]
+        f["checksums"] = o["rounds"]
+        f["finalViews"] = o["finalViews"]
+        fixture["cases"].append(f)
+    path = os.path.join(HERE, "sim_golden.json")
+    with open(path, "w") as fh:
+        json.dump(fixture, fh, separators=(",", ":"))
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
 if __name__ == "__main__":
-    what = sys.argv[1:] or ["ring", "membership"]
+    what = sys.argv[1:] or ["ring", "membership", "sim"]
     if "ring" in what:
         make_ring()
     if "membership" in what:
         make_membership()
+    if "sim" in what:
+        make_sim()
