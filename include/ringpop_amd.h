@@ -140,6 +140,35 @@ int rp_members_checksum_string(rp_members *m, char *buf, uint64_t cap, uint64_t 
 int rp_members_dump(rp_members *m, uint8_t *exists, uint8_t *status, int64_t *inc, uint32_t cap);
 int rp_members_count(rp_members *m, uint32_t *n_names);
 
+/* ------------------------------------------------------------------ Gossip simulator
+ * N full ringpop nodes (every node: membership view, dissemination buffer, ring membership,
+ * iterator, suspicion timers; lib/membership, lib/gossip, lib/ring, lib/on_membership_event.js)
+ * advanced in the deterministic round model of DESIGN.md §SWIM round model: ping / ping-req
+ * exchange, piggyback counters with maxPiggybackCount, suspect->faulty timers. No reference
+ * counterpart (the reference is one view per process). names/off: N member addresses;
+ * inc0[N]: initial incarnations (every view starts identical, all alive); dead[N]: members
+ * killed before round 0. seed: Philox seed of the iterator shuffles and ping-req samples;
+ * suspicion_rounds: 5000 ms / 200 ms = 25 by default; now0: Date.now() at round 0. */
+typedef struct rp_sim rp_sim;
+
+int rp_sim_create(uint32_t n, const char *names, const uint32_t *off, const int64_t *inc0, const uint8_t *dead,
+                  uint32_t seed, uint32_t suspicion_rounds, int64_t now0, int device, rp_sim **out);
+int rp_sim_destroy(rp_sim *s);
+/* Advance `rounds` rounds (synchronous) / enqueue them (asynchronous, rp_sim_sync waits). */
+int rp_sim_step(rp_sim *s, uint32_t rounds);
+int rp_sim_step_async(rp_sim *s, uint32_t rounds);
+int rp_sim_sync(rp_sim *s);
+int rp_sim_round(rp_sim *s, int64_t *out);
+/* Every node's membership checksum (0 for killed nodes). */
+int rp_sim_checksums(rp_sim *s, uint32_t *out);
+/* Node v's view: status[N], incarnation[N] (nullable). */
+int rp_sim_view(rp_sim *s, uint32_t v, uint8_t *status, int64_t *inc);
+/* Convergence (scenario-runner.js:152-170): all live checksums equal and every killed member
+ * faulty in every live view. */
+int rp_sim_converged(rp_sim *s, int *out);
+/* pings, ping-reqs, full syncs, applied updates since creation. */
+int rp_sim_stats(rp_sim *s, uint64_t *out4);
+
 #ifdef __cplusplus
 }
 #endif

@@ -77,6 +77,16 @@ SIGNATURES = {
     "rp_members_checksum_string": (_INT, [_P, _P, _U64, _P]),
     "rp_members_dump": (_INT, [_P, _P, _P, _P, _U32]),
     "rp_members_count": (_INT, [_P, _P]),
+    "rp_sim_create": (_INT, [_U32, _P, _P, _P, _P, _U32, _U32, ctypes.c_int64, _INT, _P]),
+    "rp_sim_destroy": (_INT, [_P]),
+    "rp_sim_step": (_INT, [_P, _U32]),
+    "rp_sim_step_async": (_INT, [_P, _U32]),
+    "rp_sim_sync": (_INT, [_P]),
+    "rp_sim_round": (_INT, [_P, _P]),
+    "rp_sim_checksums": (_INT, [_P, _P]),
+    "rp_sim_view": (_INT, [_P, _U32, _P, _P]),
+    "rp_sim_converged": (_INT, [_P, _P]),
+    "rp_sim_stats": (_INT, [_P, _P]),
 }
 
 STATUS = {"alive": 0, "suspect": 1, "faulty": 2, "leave": 3}
@@ -473,3 +483,67 @@ class Membership:
                    d_n_applied=None, stream=None):
         check(lib().rp_members_update_dev(self._h, d_ids, d_status, d_inc, k, int(now_ms), d_applied, d_new_status,
                                           d_new_inc, d_n_applied, stream))
+
+
+class GossipSim:
+    """N full ringpop nodes advanced in the deterministic gossip round model on the device
+    (DESIGN.md §SWIM round model; oracle/orc_sim.c restates it on the CPU)."""
+
+    def __init__(self, names, inc0, dead, seed=11, suspicion_rounds=25, now0=None, device=0):
+        self.N = len(names)
+        buf, off = _pack(names)
+        inc0 = np.ascontiguousarray(inc0, dtype=np.int64)
+        dead = np.ascontiguousarray(dead, dtype=np.uint8)
+        if now0 is None:
+            now0 = 1434401518824 + 10 ** 9
+        h = ctypes.c_void_p()
+        check(lib().rp_sim_create(self.N, buf, off.ctypes.data, inc0.ctypes.data, dead.ctypes.data, seed,
+                                  suspicion_rounds, int(now0), device, ctypes.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().rp_sim_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def step(self, rounds=1):
+        check(lib().rp_sim_step(self._h, rounds))
+
+    def step_async(self, rounds=1):
+        check(lib().rp_sim_step_async(self._h, rounds))
+
+    def sync(self):
+        check(lib().rp_sim_sync(self._h))
+
+    @property
+    def round(self):
+        v = ctypes.c_int64()
+        check(lib().rp_sim_round(self._h, ctypes.byref(v)))
+        return v.value
+
+    def checksums(self):
+        out = np.empty(self.N, dtype=np.uint32)
+        check(lib().rp_sim_checksums(self._h, out.ctypes.data))
+        return out
+
+    def view(self, v):
+        st = np.empty(self.N, dtype=np.uint8)
+        inc = np.empty(self.N, dtype=np.int64)
+        check(lib().rp_sim_view(self._h, v, st.ctypes.data, inc.ctypes.data))
+        return st, inc
+
+    def converged(self):
+        v = ctypes.c_int()
+        check(lib().rp_sim_converged(self._h, ctypes.byref(v)))
+        return bool(v.value)
+
+    def stats(self):
+        out = np.zeros(4, dtype=np.uint64)
+        check(lib().rp_sim_stats(self._h, out.ctypes.data))
+        return dict(zip(["pings", "pingreqs", "fullsyncs", "applied"], (int(x) for x in out)))
