@@ -837,8 +837,7 @@ struct Sim {
 
     void build_inboxes() {
         const uint32_t n = N;
-        keys.reserve(3ull * n + 1);
-        in_src.reserve(n + 1);
+        // every buffer the kernels see through `d` is allocated once in rp_sim_create
         hipLaunchKernelGGL(k_sim_keys, dim3(grid_for(n, 256)), dim3(256), 0, st, target.p, dead.p, n, keys.p, in_src.p);
         radix_sort_pairs(keys.p, in_src.p, n, 0, 32, st, ws);
         hipLaunchKernelGGL(k_csr, dim3(grid_for(n + 1, 256)), dim3(256), 0, st, keys.p, n, n, in_off.p);
@@ -918,7 +917,8 @@ int rp_sim_create(uint32_t n, const char* names, const uint32_t* off, const int6
         S.checksum.reserve(n); S.dirty.reserve(n); S.dead.reserve(n); S.target.reserve(n); S.ck_snap.reserve(n);
         S.inc_snap.reserve(n); S.ping_n.reserve(n); S.resp_n.reserve(n); S.leg_n.reserve(n);
         S.helpers.reserve(3ull * n); S.nhelp.reserve(n); S.lresp_n.reserve(3ull * n);
-        S.in_off.reserve(n + 1ull); S.h_off.reserve(n + 1ull); S.h_src.reserve(3ull * n + 1); S.conv.reserve(1);
+        S.in_off.reserve(n + 1ull); S.in_src.reserve(n + 1ull); S.h_off.reserve(n + 1ull);
+        S.h_src.reserve(3ull * n + 1); S.keys.reserve(3ull * n + 1); S.conv.reserve(1);
         S.ping.reserve(NN); S.resp.reserve(NN); S.leg.reserve(NN); S.lresp.reserve(3 * NN);
         S.cand.reserve((uint64_t)S.grid * n);
         // per-block string buffer: names + ';' + "suspect" + 20 digits per member (also E's staging)
@@ -945,6 +945,14 @@ int rp_sim_create(uint32_t n, const char* names, const uint32_t* off, const int6
         d.strbuf = S.strbuf.p; d.strcap = (strcap + 255) & ~255ull;
         d.in_off = S.in_off.p; d.in_src = S.in_src.p; d.h_off = S.h_off.p; d.h_src = S.h_src.p;
         d.stats = S.stats.p; d.round = 0;
+        {
+            const void* ptrs[] = {d.st, d.inc, d.d_on, d.d_st, d.d_cnt, d.d_src, d.d_inc, d.d_srcinc, d.deadline,
+                                  d.s_inc, d.in_ring, d.order, d.it_idx, d.n_shuf, d.ring_count, d.max_piggy,
+                                  d.checksum, d.dirty, d.dead, d.sorted, d.names, d.noff, d.target, d.ck_snap,
+                                  d.inc_snap, d.ping, d.ping_n, d.resp, d.resp_n, d.leg, d.leg_n, d.helpers, d.nhelp,
+                                  d.lresp, d.lresp_n, d.cand, d.strbuf, d.in_off, d.in_src, d.h_off, d.h_src, d.stats};
+            for (const void* p : ptrs) RP_REQUIRE(p != nullptr, "sim_create: internal buffer not allocated");
+        }
         hipLaunchKernelGGL(rp::k_sim_init, dim3(rp::grid_for(NN, 256, 8192)), dim3(256), 0, S.st, d, S.inc0.p);
         hipLaunchKernelGGL(rp::k_sim_start, dim3(rp::grid_for(n, 64)), dim3(64), 0, S.st, d);
         hipLaunchKernelGGL(rp::k_sim_first_checksum, dim3(1), dim3(rp::kT), 0, S.st, d);
