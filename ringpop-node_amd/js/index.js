@@ -1,0 +1,248 @@
+// index.js — the reference's JS API over the MI355X engine (rpamd.node -> librpamd.so).
+//
+// HashRing is a drop-in for ringpop's lib/ring/index.js (options.Ring plug point,
+// reference index.js:107,133): same constructor options, methods, `checksum` property and
+// events. The RB-tree is replaced by the sorted token table in HBM. Every hash, insert,
+// remove, checksum and lookup runs in HIP kernels; with no device the constructor throws.
+// Batched forms (lookupBatch / lookupNBatch / lookupNHashes) are the point of the engine:
+// one kernel launch for a whole batch of keys.
+//
+// MembershipMerge is the device-side hot loop of Membership.update
+// (lib/membership/index.js:249-324, member.js:71-202) and computeChecksum (48-75).
+// GossipSim runs N full ringpop nodes in the deterministic round model (DESIGN.md §5).
+'use strict';
+var EventEmitter = require('events').EventEmitter;
+var util = require('util');
+var path = require('path');
+
+var native;
+try {
+    native = require(path.join(__dirname, 'rpamd.node'));
+} catch (e) {
+    throw new Error('ringpop_amd: rpamd.node is not built (make -C ringpop-node_amd/js): ' + e.message);
+}
+
+var STATUS = ['alive', 'suspect', 'faulty', 'leave'];
+var STATUS_CODE = {alive: 0, suspect: 1, faulty: 2, leave: 3};
+
+function requireDevice(device) {
+    var n = native.deviceCount();
+    if (n <= device) {
+        throw new Error('ringpop_amd: no HIP device ' + device + ' (visible: ' + n + ')');
+    }
+}
+
+// new HashRing({replicaPoints, hashFunc, device}) — lib/ring/index.js:25-34.
+function HashRing(options) {
+    EventEmitter.call(this);
+    this.options = options || {};
+    this.replicaPoints = this.options.replicaPoints || 100;
+    // options.hashFunc (index.js:29): a caller hash is evaluated here, in JS, and its values
+    // are handed to the device as tokens / key hashes; the default is the device farmhash32.
+    this.hashFunc = this.options.hashFunc || native.hash32;
+    this._customHash = typeof this.options.hashFunc === 'function';
+    this.device = this.options.device || 0;
+    requireDevice(this.device);
+    this._h = native.ringCreate(this.replicaPoints, this.device);
+    this.checksum = null;
+}
+util.inherits(HashRing, EventEmitter);
+
+HashRing.prototype.destroy = function destroy() {
+    native.destroy(this._h);
+};
+
+HashRing.prototype._replicaTokens = function _replicaTokens(servers) {
+    if (!this._customHash || !servers.length) { return null; }
+    var R = this.replicaPoints;
+    var t = new Uint32Array(servers.length * R);
+    for (var j = 0; j < servers.length; j++) {
+        for (var i = 0; i < R; i++) { t[j * R + i] = this.hashFunc(servers[j] + i) >>> 0; }
+    }
+    return t;
+};
+
+HashRing.prototype._refreshChecksum = function _refreshChecksum() {
+    this.checksum = this._customHash ? this.hashFunc(native.ringChecksumString(this._h))
+        : native.ringChecksum(this._h);
+    this.emit('checksumComputed');
+};
+
+// addServer(name) — index.js:39-48
+HashRing.prototype.addServer = function addServer(name) {
+    if (this.hasServer(name)) { return; }
+    native.ringAddRemove(this._h, [name], null, this._replicaTokens([name]), null);
+    this._refreshChecksum();
+    this.emit('added', name);
+};
+
+// removeServer(name) — index.js:124-133
+HashRing.prototype.removeServer = function removeServer(name) {
+    if (!this.hasServer(name)) { return; }
+    native.ringAddRemove(this._h, null, [name], null, this._replicaTokens([name]));
+    this._refreshChecksum();
+    this.emit('removed', name);
+};
+
+// addRemoveServers(add, remove) -> ringChanged — index.js:60-94 (no added/removed events,
+// as in the reference).
+HashRing.prototype.addRemoveServers = function addRemoveServers(serversToAdd, serversToRemove) {
+    serversToAdd = serversToAdd || [];
+    serversToRemove = serversToRemove || [];
+    var changed = native.ringAddRemove(this._h, serversToAdd, serversToRemove,
+        this._replicaTokens(serversToAdd), this._replicaTokens(serversToRemove));
+    if (changed) { this._refreshChecksum(); }
+    return changed;
+};
+
+// computeChecksum() — index.js:96-105 (the device recomputes it on every change; this
+// re-reads it and emits, like the reference).
+HashRing.prototype.computeChecksum = function computeChecksum() {
+    this._refreshChecksum();
+};
+
+HashRing.prototype.getServerCount = function getServerCount() {
+    return native.ringServerCount(this._h);
+};
+
+HashRing.prototype.getStats = function getStats() {
+    return {checksum: this.checksum, servers: native.ringServers(this._h)};
+};
+
+HashRing.prototype.hasServer = function hasServer(name) {
+    return native.ringHasServer(this._h, name);
+};
+
+// lookup(key) — index.js:145-154 (a batch of one; use lookupBatch for throughput).
+HashRing.prototype.lookup = function lookup(str) {
+    return this.lookupBatch([str])[0];
+};
+
+// lookupN(key, n) — index.js:157-189.
+HashRing.prototype.lookupN = function lookupN(str, n) {
+    return this.lookupNBatch([str], n)[0];
+};
+
+HashRing.prototype._hashes = function _hashes(keys) {
+    var h = new Uint32Array(keys.length);
+    for (var i = 0; i < keys.length; i++) { h[i] = this.hashFunc(keys[i]) >>> 0; }
+    return h;
+};
+
+HashRing.prototype._names = function _names(r, nrep) {
+    var w = nrep > 1 ? nrep : 1;
+    var out = new Array(r.counts.length);
+    for (var i = 0; i < r.counts.length; i++) {
+        var row = [];
+        for (var j = 0; j < r.counts[i]; j++) { row.push(native.ringOwnerName(this._h, r.owners[i * w + j])); }
+        out[i] = row;
+    }
+    return out;
+};
+
+// lookup() of every key, one launch.
+HashRing.prototype.lookupBatch = function lookupBatch(keys) {
+    if (this._customHash) {
+        return this._names(native.ringLookupNHashes(this._h, this._hashes(keys), 1), 1)
+            .map(function (row) { return row.length ? row[0] : null; });
+    }
+    return native.ringLookup(this._h, keys);
+};
+
+// lookupN(key, n) of every key, one launch.
+HashRing.prototype.lookupNBatch = function lookupNBatch(keys, n) {
+    if (this._customHash) {
+        return this._names(native.ringLookupNHashes(this._h, this._hashes(keys), n), n);
+    }
+    return native.ringLookupN(this._h, keys, n);
+};
+
+// Id-level batch over precomputed key hashes: {owners: Uint32Array(ids, rows of max(n,1)),
+// counts: Uint8Array}; ownerName(id) maps ids back to server names.
+HashRing.prototype.lookupNHashes = function lookupNHashes(hashes, n) {
+    return native.ringLookupNHashes(this._h, hashes, n);
+};
+
+HashRing.prototype.ownerName = function ownerName(id) {
+    return native.ringOwnerName(this._h, id);
+};
+
+// MembershipMerge(whoami, {capacity, device}) — device state of one Membership: update()
+// folds a changes array in order with the reference's override rules and returns the applied
+// updates (Membership.update's return value, index.js:249-324); checksum as
+// membership.checksum (null until the first applied update).
+function MembershipMerge(whoami, options) {
+    options = options || {};
+    this.device = options.device || 0;
+    requireDevice(this.device);
+    this._h = native.membersCreate(options.capacity || 1024, this.device);
+    this.whoami = whoami;
+    native.membersSetLocal(this._h, native.membersIntern(this._h, [whoami])[0]);
+}
+
+MembershipMerge.prototype.destroy = function destroy() { native.destroy(this._h); };
+
+MembershipMerge.prototype.update = function update(changes, nowMs) {
+    changes = Array.isArray(changes) ? changes : [changes];
+    var k = changes.length;
+    var ids = native.membersIntern(this._h, changes.map(function (c) { return c.address; }));
+    var st = new Uint8Array(k), inc = new Float64Array(k);
+    for (var i = 0; i < k; i++) {
+        var code = STATUS_CODE[changes[i].status];
+        if (code === undefined) { throw new Error('ringpop_amd: unknown status ' + changes[i].status); }
+        st[i] = code;
+        inc[i] = changes[i].incarnationNumber;
+    }
+    var r = native.membersUpdate(this._h, ids, st, inc, nowMs === undefined ? Date.now() : nowMs);
+    var applied = [];
+    for (i = 0; i < k; i++) {
+        if (!r.applied[i]) { continue; }
+        var u = {};
+        for (var key in changes[i]) { u[key] = changes[i][key]; }
+        u.status = STATUS[r.status[i]];
+        u.incarnationNumber = r.inc[i];
+        applied.push(u);
+    }
+    return applied;
+};
+
+Object.defineProperty(MembershipMerge.prototype, 'checksum', {
+    get: function () { return native.membersChecksum(this._h); }
+});
+
+MembershipMerge.prototype.computeChecksum = function computeChecksum() {
+    return native.membersComputeChecksum(this._h);
+};
+
+MembershipMerge.prototype.generateChecksumString = function generateChecksumString() {
+    return native.membersChecksumString(this._h);
+};
+
+// GossipSim(names, {inc0, dead, seed, suspicionRounds, now0, device})
+function GossipSim(names, options) {
+    options = options || {};
+    this.n = names.length;
+    this.device = options.device || 0;
+    requireDevice(this.device);
+    var inc0 = options.inc0 instanceof Float64Array ? options.inc0 : Float64Array.from(options.inc0);
+    var dead = options.dead ? Uint8Array.from(options.dead) : new Uint8Array(this.n);
+    this._h = native.simCreate(names, inc0, dead, options.seed || 0, options.suspicionRounds || 25,
+        options.now0 || 0, this.device);
+}
+
+GossipSim.prototype.destroy = function destroy() { native.destroy(this._h); };
+GossipSim.prototype.step = function step(rounds) { native.simStep(this._h, rounds === undefined ? 1 : rounds); };
+GossipSim.prototype.round = function round() { return native.simRound(this._h); };
+GossipSim.prototype.checksums = function checksums() { return native.simChecksums(this._h, this.n); };
+GossipSim.prototype.view = function view(v) { return native.simView(this._h, v, this.n); };
+GossipSim.prototype.converged = function converged() { return native.simConverged(this._h); };
+GossipSim.prototype.stats = function stats() { return native.simStats(this._h); };
+
+module.exports = {
+    HashRing: HashRing,
+    MembershipMerge: MembershipMerge,
+    GossipSim: GossipSim,
+    hash32: native.hash32,
+    native: native,
+    STATUS: STATUS
+};

@@ -1,0 +1,778 @@
+/*
+ * rpamd_napi.c — Node N-API addon over librpamd.so (include/ringpop_amd.h).
+ *
+ * This is the "thin Node N-API C-ABI addon calling HIP" of BASELINE.json north_star: it
+ * only marshals JS values into the C ABI's plain buffers; every hash, sort, lookup, merge and
+ * gossip round runs in librpamd's HIP kernels. There is no JS or CPU fallback — a missing
+ * library or device raises. The JS classes that mirror the reference's API (lib/ring/index.js
+ * HashRing, Membership.update, farmhash.hash32) are in index.js next to this file.
+ *
+ * Built by ./Makefile (gcc, N-API v3+ headers of the node in this image, rpath to ..).
+ */
+#include <node_api.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/ringpop_amd.h"
+
+/* ------------------------------------------------------------------ helpers */
+#define NAPI_OK(call)                                                                 \
+    do {                                                                              \
+        if ((call) != napi_ok) {                                                      \
+            const napi_extended_error_info *ei_ = NULL;                               \
+            napi_get_last_error_info(env, &ei_);                                      \
+            napi_throw_error(env, NULL, ei_ && ei_->error_message ? ei_->error_message \
+                                                                  : "napi call failed"); \
+            return NULL;                                                              \
+        }                                                                             \
+    } while (0)
+
+#define RP_OK(call)                                                \
+    do {                                                           \
+        if ((call) != 0) {                                         \
+            napi_throw_error(env, "ERR_RINGPOP_AMD", rp_last_error()); \
+            return NULL;                                           \
+        }                                                          \
+    } while (0)
+
+#define ARGS(N)                                                            \
+    size_t argc = (N);                                                     \
+    napi_value argv[(N) > 0 ? (N) : 1];                                    \
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));         \
+    if (argc < (N)) {                                                      \
+        napi_throw_type_error(env, NULL, "wrong number of arguments");     \
+        return NULL;                                                       \
+    }
+
+static napi_value make_u32(napi_env env, uint32_t v) {
+    napi_value out;
+    napi_create_uint32(env, v, &out);
+    return out;
+}
+
+static napi_value make_bool(napi_env env, int v) {
+    napi_value out;
+    napi_get_boolean(env, v != 0, &out);
+    return out;
+}
+
+static napi_value make_null(napi_env env) {
+    napi_value out;
+    napi_get_null(env, &out);
+    return out;
+}
+
+static int is_nullish(napi_env env, napi_value v) {
+    napi_valuetype t;
+    if (napi_typeof(env, v, &t) != napi_ok) return 1;
+    return t == napi_null || t == napi_undefined;
+}
+
+/* Handles are napi externals whose finalizer destroys the native object unless destroy()
+ * already did (the slot is then NULL). */
+typedef struct {
+    int kind; /* 1 ring, 2 members, 3 sim */
+    void *p;
+} handle_t;
+
+static void handle_finalize(napi_env env, void *data, void *hint) {
+    (void)env;
+    (void)hint;
+    handle_t *h = (handle_t *)data;
+    if (h->p) {
+        if (h->kind == 1) rp_ring_destroy((rp_ring *)h->p);
+        if (h->kind == 2) rp_members_destroy((rp_members *)h->p);
+        if (h->kind == 3) rp_sim_destroy((rp_sim *)h->p);
+    }
+    free(h);
+}
+
+static napi_value wrap_handle(napi_env env, int kind, void *p) {
+    handle_t *h = (handle_t *)malloc(sizeof(handle_t));
+    h->kind = kind;
+    h->p = p;
+    napi_value out;
+    if (napi_create_external(env, h, handle_finalize, NULL, &out) != napi_ok) {
+        handle_finalize(env, h, NULL);
+        napi_throw_error(env, NULL, "napi_create_external failed");
+        return NULL;
+    }
+    return out;
+}
+
+static handle_t *get_handle(napi_env env, napi_value v, int kind) {
+    void *data = NULL;
+    if (napi_get_value_external(env, v, &data) != napi_ok || !data ||
+        ((handle_t *)data)->kind != kind) {
+        napi_throw_type_error(env, NULL, "invalid ringpop_amd handle");
+        return NULL;
+    }
+    if (!((handle_t *)data)->p) {
+        napi_throw_error(env, NULL, "ringpop_amd handle already destroyed");
+        return NULL;
+    }
+    return (handle_t *)data;
+}
+
+/* A JS array of strings packed as bytes + offsets (off32 or off64 chosen by the caller). */
+typedef struct {
+    char *bytes;
+    uint32_t *off32;
+    uint64_t *off64;
+    uint32_t n;
+} strpack_t;
+
+static void strpack_free(strpack_t *s) {
+    free(s->bytes);
+    free(s->off32);
+    free(s->off64);
+    memset(s, 0, sizeof(*s));
+}
+
+/* Returns 0 and fills *s, or -1 with a pending JS exception. Non-strings are coerced with
+ * String(x), as the reference's hashFunc(str) would (farmhash takes its argument's string). */
+static int strpack_from_array(napi_env env, napi_value arr, strpack_t *s) {
+    memset(s, 0, sizeof(*s));
+    if (is_nullish(env, arr)) return 0;
+    bool isarr = false;
+    napi_is_array(env, arr, &isarr);
+    if (!isarr) {
+        napi_throw_type_error(env, NULL, "expected an array of strings");
+        return -1;
+    }
+    uint32_t n = 0;
+    napi_get_array_length(env, arr, &n);
+    s->n = n;
+    s->off32 = (uint32_t *)malloc(sizeof(uint32_t) * (n + 1));
+    s->off64 = (uint64_t *)malloc(sizeof(uint64_t) * (n + 1));
+    size_t cap = 64 + (size_t)n * 40, used = 0;
+    s->bytes = (char *)malloc(cap);
+    for (uint32_t i = 0; i < n; i++) {
+        napi_value e, str;
+        napi_get_element(env, arr, i, &e);
+        if (napi_coerce_to_string(env, e, &str) != napi_ok) {
+            strpack_free(s);
+            napi_throw_type_error(env, NULL, "array element is not coercible to string");
+            return -1;
+        }
+        size_t len = 0;
+        napi_get_value_string_utf8(env, str, NULL, 0, &len);
+        if (used + len + 1 > cap) {
+            while (used + len + 1 > cap) cap *= 2;
+            s->bytes = (char *)realloc(s->bytes, cap);
+        }
+        size_t got = 0;
+        napi_get_value_string_utf8(env, str, s->bytes + used, len + 1, &got);
+        s->off32[i] = (uint32_t)used;
+        s->off64[i] = used;
+        used += got;
+    }
+    s->off32[n] = (uint32_t)used;
+    s->off64[n] = used;
+    return 0;
+}
+
+/* Typed-array view of the wanted element type: 0 with data/len, or -1 (data NULL, len 0)
+ * when v is not such a typed array. Zero-length arrays may have data == NULL. */
+static int typed_get(napi_env env, napi_value v, napi_typedarray_type want, void **data, size_t *len) {
+    bool is = false;
+    *data = NULL;
+    *len = 0;
+    if (napi_is_typedarray(env, v, &is) != napi_ok || !is) return -1;
+    napi_typedarray_type t;
+    napi_value ab;
+    size_t boff = 0;
+    napi_get_typedarray_info(env, v, &t, len, data, &ab, &boff);
+    if (t != want) {
+        *data = NULL;
+        *len = 0;
+        return -1;
+    }
+    return 0;
+}
+
+static void *typed_data(napi_env env, napi_value v, napi_typedarray_type want, size_t *len) {
+    void *d = NULL;
+    typed_get(env, v, want, &d, len);
+    return d;
+}
+
+static napi_value new_typed(napi_env env, napi_typedarray_type t, size_t n, size_t elem, void **data) {
+    napi_value ab, out;
+    if (napi_create_arraybuffer(env, n * elem, data, &ab) != napi_ok) return NULL;
+    if (napi_create_typedarray(env, t, n, ab, 0, &out) != napi_ok) return NULL;
+    return out;
+}
+
+static napi_value ring_name(napi_env env, rp_ring *r, uint32_t id) {
+    if (id == RP_NULL_ID) return make_null(env);
+    uint32_t len = 0;
+    const char *p = rp_ring_owner_name(r, id, &len);
+    if (!p) return make_null(env);
+    napi_value s;
+    napi_create_string_utf8(env, p, len, &s);
+    return s;
+}
+
+/* ------------------------------------------------------------------ common */
+static napi_value js_version(napi_env env, napi_callback_info info) {
+    (void)info;
+    return make_u32(env, rp_version());
+}
+
+static napi_value js_device_count(napi_env env, napi_callback_info info) {
+    (void)info;
+    int n = 0;
+    RP_OK(rp_device_count(&n));
+    return make_u32(env, (uint32_t)n);
+}
+
+/* farmhash.hash32(str) (reference package.json:34): host C++ farmhashmk::Hash32 of the UTF-8
+ * bytes, the same code librpamd's kernels run. */
+static napi_value js_hash32(napi_env env, napi_callback_info info) {
+    ARGS(1);
+    napi_value str;
+    NAPI_OK(napi_coerce_to_string(env, argv[0], &str));
+    size_t len = 0;
+    NAPI_OK(napi_get_value_string_utf8(env, str, NULL, 0, &len));
+    char stackbuf[256];
+    char *buf = len < sizeof(stackbuf) ? stackbuf : (char *)malloc(len + 1);
+    napi_get_value_string_utf8(env, str, buf, len + 1, &len);
+    uint32_t h = rp_hash32(buf, len);
+    if (buf != stackbuf) free(buf);
+    return make_u32(env, h);
+}
+
+/* ------------------------------------------------------------------ ring */
+static napi_value js_ring_create(napi_env env, napi_callback_info info) {
+    ARGS(2);
+    uint32_t rp = 0;
+    int32_t dev = 0;
+    NAPI_OK(napi_get_value_uint32(env, argv[0], &rp));
+    NAPI_OK(napi_get_value_int32(env, argv[1], &dev));
+    rp_ring *r = NULL;
+    RP_OK(rp_ring_create(rp, dev, &r));
+    return wrap_handle(env, 1, r);
+}
+
+static napi_value js_destroy(napi_env env, napi_callback_info info) {
+    ARGS(1);
+    void *data = NULL;
+    NAPI_OK(napi_get_value_external(env, argv[0], &data));
+    handle_t *h = (handle_t *)data;
+    if (h && h->p) {
+        if (h->kind == 1) rp_ring_destroy((rp_ring *)h->p);
+        if (h->kind == 2) rp_members_destroy((rp_members *)h->p);
+        if (h->kind == 3) rp_sim_destroy((rp_sim *)h->p);
+        h->p = NULL;
+    }
+    return NULL;
+}
+
+/* addRemoveServers(add[], remove[], addTokens?, removeTokens?) -> ringChanged
+ * (lib/ring/index.js:60-94). Token arrays (Uint32Array, n*replicaPoints) carry a caller
+ * hashFunc's replica hashes (options.hashFunc, :29). */
+static napi_value js_ring_add_remove(napi_env env, napi_callback_info info) {
+    ARGS(5);
+    handle_t *h = get_handle(env, argv[0], 1);
+    if (!h) return NULL;
+    strpack_t add, rem;
+    if (strpack_from_array(env, argv[1], &add)) return NULL;
+    if (strpack_from_array(env, argv[2], &rem)) {
+        strpack_free(&add);
+        return NULL;
+    }
+    size_t n1 = 0, n2 = 0;
+    const uint32_t *at = is_nullish(env, argv[3]) ? NULL : (const uint32_t *)typed_data(env, argv[3], napi_uint32_array, &n1);
+    const uint32_t *rt = is_nullish(env, argv[4]) ? NULL : (const uint32_t *)typed_data(env, argv[4], napi_uint32_array, &n2);
+    int changed = 0;
+    int rc = rp_ring_add_remove((rp_ring *)h->p, add.bytes, add.off32, add.n, at, rem.bytes, rem.off32, rem.n, rt,
+                                &changed);
+    strpack_free(&add);
+    strpack_free(&rem);
+    RP_OK(rc);
+    return make_bool(env, changed);
+}
+
+static napi_value js_ring_checksum(napi_env env, napi_callback_info info) {
+    ARGS(1);
+    handle_t *h = get_handle(env, argv[0], 1);
+    if (!h) return NULL;
+    uint32_t v = 0;
+    int set = 0;
+    RP_OK(rp_ring_checksum((rp_ring *)h->p, &v, &set));
+    return set ? make_u32(env, v) : make_null(env);
+}
+
+static napi_value js_ring_checksum_string(napi_env env, napi_callback_info info) {
+    ARGS(1);
+    handle_t *h = get_handle(env, argv[0], 1);
+    if (!h) return NULL;
+    uint64_t len = 0;
+    RP_OK(rp_ring_checksum_string((rp_ring *)h->p, NULL, 0, &len));
+    char *buf = (char *)malloc(len + 1);
+    int rc = rp_ring_checksum_string((rp_ring *)h->p, buf, len, &len);
+    if (rc) {
+        free(buf);
+        RP_OK(rc);
+    }
+    napi_value s;
+    napi_create_string_utf8(env, buf, len, &s);
+    free(buf);
+    return s;
+}
+
+static napi_value js_ring_server_count(napi_env env, napi_callback_info info) {
+    ARGS(1);
+    handle_t *h = get_handle(env, argv[0], 1);
+    if (!h) return NULL;
+    uint32_t n = 0;
+    RP_OK(rp_ring_server_count((rp_ring *)h->p, &n));
+    return make_u32(env, n);
+}
+
+static napi_value js_ring_token_count(napi_env env, napi_callback_info info) {
+    ARGS(1);
+    handle_t *h = get_handle(env, argv[0], 1);
+    if (!h) return NULL;
+    uint32_t n = 0;
+    RP_OK(rp_ring_token_count((rp_ring *)h->p, &n));
+    return make_u32(env, n);
+}
+
+static napi_value js_ring_has_server(napi_env env, napi_callback_info info) {
+    ARGS(2);
+    handle_t *h = get_handle(env, argv[0], 1);
+    if (!h) return NULL;
+    napi_value str;
+    NAPI_OK(napi_coerce_to_string(env, argv[1], &str));
+    size_t len = 0;
+    napi_get_value_string_utf8(env, str, NULL, 0, &len);
+    char *buf = (char *)malloc(len + 1);
+    napi_get_value_string_utf8(env, str, buf, len + 1, &len);
+    int has = 0;
+    int rc = rp_ring_has_server((rp_ring *)h->p, buf, (uint32_t)len, &has);
+    free(buf);
+    RP_OK(rc);
+    return make_bool(env, has);
+}
+
+/* Object.keys(servers) in insertion order (getStats, lib/ring/index.js:111-116). */
+static napi_value js_ring_servers(napi_env env, napi_callback_info info) {
+    ARGS(1);
+    handle_t *h = get_handle(env, argv[0], 1);
+    if (!h) return NULL;
+    rp_ring *r = (rp_ring *)h->p;
+    uint32_t n = 0;
+    RP_OK(rp_ring_servers(r, NULL, 0, &n));
+    uint32_t *ids = (uint32_t *)malloc(sizeof(uint32_t) * (n ? n : 1));
+    int rc = rp_ring_servers(r, ids, n, &n);
+    if (rc) {
+        free(ids);
+        RP_OK(rc);
+    }
+    napi_value arr;
+    napi_create_array_with_length(env, n, &arr);
+    for (uint32_t i = 0; i < n; i++) napi_set_element(env, arr, i, ring_name(env, r, ids[i]));
+    free(ids);
+    return arr;
+}
+
+static napi_value js_ring_owner_name(napi_env env, napi_callback_info info) {
+    ARGS(2);
+    handle_t *h = get_handle(env, argv[0], 1);
+    if (!h) return NULL;
+    uint32_t id = 0;
+    NAPI_OK(napi_get_value_uint32(env, argv[1], &id));
+    return ring_name(env, (rp_ring *)h->p, id);
+}
+
+/* lookupBatch(h, keys[]) -> names (null for an empty ring), lookup() of every key
+ * (lib/ring/index.js:145-154), one device launch. */
+static napi_value js_ring_lookup(napi_env env, napi_callback_info info) {
+    ARGS(2);
+    handle_t *h = get_handle(env, argv[0], 1);
+    if (!h) return NULL;
+    rp_ring *r = (rp_ring *)h->p;
+    strpack_t keys;
+    if (strpack_from_array(env, argv[1], &keys)) return NULL;
+    uint32_t *own = (uint32_t *)malloc(sizeof(uint32_t) * (keys.n ? keys.n : 1));
+    int rc = rp_ring_lookup(r, keys.bytes, keys.off64, 0, keys.n, own);
+    uint32_t n = keys.n;
+    strpack_free(&keys);
+    if (rc) {
+        free(own);
+        RP_OK(rc);
+    }
+    napi_value arr;
+    napi_create_array_with_length(env, n, &arr);
+    for (uint32_t i = 0; i < n; i++) napi_set_element(env, arr, i, ring_name(env, r, own[i]));
+    free(own);
+    return arr;
+}
+
+/* lookupNBatch(h, keys[], n) -> arrays of names, lookupN() of every key (:157-189). */
+static napi_value js_ring_lookupn(napi_env env, napi_callback_info info) {
+    ARGS(3);
+    handle_t *h = get_handle(env, argv[0], 1);
+    if (!h) return NULL;
+    rp_ring *r = (rp_ring *)h->p;
+    int32_t nrep = 0;
+    NAPI_OK(napi_get_value_int32(env, argv[2], &nrep));
+    strpack_t keys;
+    if (strpack_from_array(env, argv[1], &keys)) return NULL;
+    uint32_t w = nrep > 1 ? (uint32_t)nrep : 1u;
+    uint32_t n = keys.n;
+    uint32_t *own = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)(n ? n : 1) * w);
+    uint8_t *cnt = (uint8_t *)malloc(n ? n : 1);
+    int rc = rp_ring_lookupn(r, keys.bytes, keys.off64, 0, n, nrep, own, cnt);
+    strpack_free(&keys);
+    if (rc) {
+        free(own);
+        free(cnt);
+        RP_OK(rc);
+    }
+    napi_value arr;
+    napi_create_array_with_length(env, n, &arr);
+    for (uint32_t i = 0; i < n; i++) {
+        napi_value row;
+        napi_create_array_with_length(env, cnt[i], &row);
+        for (uint32_t j = 0; j < cnt[i]; j++)
+            napi_set_element(env, row, j, ring_name(env, r, own[(size_t)i * w + j]));
+        napi_set_element(env, arr, i, row);
+    }
+    free(own);
+    free(cnt);
+    return arr;
+}
+
+/* lookupNHashes(h, Uint32Array hashes, n) -> {owners: Uint32Array(ids), counts: Uint8Array}:
+ * the id-level batch for callers with their own hashFunc or that keep owner ids. */
+static napi_value js_ring_lookupn_hashes(napi_env env, napi_callback_info info) {
+    ARGS(3);
+    handle_t *h = get_handle(env, argv[0], 1);
+    if (!h) return NULL;
+    size_t n = 0;
+    void *hv = NULL;
+    if (typed_get(env, argv[1], napi_uint32_array, &hv, &n)) {
+        napi_throw_type_error(env, NULL, "hashes must be a Uint32Array");
+        return NULL;
+    }
+    const uint32_t *hs = (const uint32_t *)hv;
+    int32_t nrep = 0;
+    NAPI_OK(napi_get_value_int32(env, argv[2], &nrep));
+    size_t w = nrep > 1 ? (size_t)nrep : 1;
+    void *od = NULL, *cd = NULL;
+    napi_value owners = new_typed(env, napi_uint32_array, n * w, 4, &od);
+    napi_value counts = new_typed(env, napi_uint8_array, n, 1, &cd);
+    if (!owners || !counts) {
+        napi_throw_error(env, NULL, "allocation failed");
+        return NULL;
+    }
+    if (n) RP_OK(rp_ring_lookupn_hashes((rp_ring *)h->p, hs, n, nrep, (uint32_t *)od, (uint8_t *)cd));
+    napi_value out;
+    napi_create_object(env, &out);
+    napi_set_named_property(env, out, "owners", owners);
+    napi_set_named_property(env, out, "counts", counts);
+    return out;
+}
+
+/* ------------------------------------------------------------------ membership */
+static napi_value js_members_create(napi_env env, napi_callback_info info) {
+    ARGS(2);
+    uint32_t cap = 0;
+    int32_t dev = 0;
+    NAPI_OK(napi_get_value_uint32(env, argv[0], &cap));
+    NAPI_OK(napi_get_value_int32(env, argv[1], &dev));
+    rp_members *m = NULL;
+    RP_OK(rp_members_create(cap, dev, &m));
+    return wrap_handle(env, 2, m);
+}
+
+static napi_value js_members_intern(napi_env env, napi_callback_info info) {
+    ARGS(2);
+    handle_t *h = get_handle(env, argv[0], 2);
+    if (!h) return NULL;
+    strpack_t s;
+    if (strpack_from_array(env, argv[1], &s)) return NULL;
+    void *d = NULL;
+    napi_value ids = new_typed(env, napi_uint32_array, s.n, 4, &d);
+    int rc = s.n ? rp_members_intern((rp_members *)h->p, s.bytes, s.off32, s.n, (uint32_t *)d) : 0;
+    strpack_free(&s);
+    RP_OK(rc);
+    return ids;
+}
+
+static napi_value js_members_set_local(napi_env env, napi_callback_info info) {
+    ARGS(2);
+    handle_t *h = get_handle(env, argv[0], 2);
+    if (!h) return NULL;
+    uint32_t id = 0;
+    NAPI_OK(napi_get_value_uint32(env, argv[1], &id));
+    RP_OK(rp_members_set_local((rp_members *)h->p, id));
+    return NULL;
+}
+
+/* update(h, ids Uint32Array, status Uint8Array, inc Float64Array, nowMs) ->
+ * {applied: Uint8Array, status: Uint8Array, inc: Float64Array, nApplied} — Membership.update
+ * (lib/membership/index.js:249-324) over evaluateUpdate (member.js:71-202). Incarnation
+ * numbers are JS Numbers (Date.now() values), exact as doubles. */
+static napi_value js_members_update(napi_env env, napi_callback_info info) {
+    ARGS(5);
+    handle_t *h = get_handle(env, argv[0], 2);
+    if (!h) return NULL;
+    size_t k = 0, k2 = 0, k3 = 0;
+    const uint32_t *ids = (const uint32_t *)typed_data(env, argv[1], napi_uint32_array, &k);
+    const uint8_t *st = (const uint8_t *)typed_data(env, argv[2], napi_uint8_array, &k2);
+    const double *incd = (const double *)typed_data(env, argv[3], napi_float64_array, &k3);
+    if ((k && (!ids || !st || !incd)) || k2 != k || k3 != k) {
+        napi_throw_type_error(env, NULL, "update expects Uint32Array ids, Uint8Array status, Float64Array inc of equal length");
+        return NULL;
+    }
+    double now = 0;
+    NAPI_OK(napi_get_value_double(env, argv[4], &now));
+    int64_t *inc = (int64_t *)malloc(sizeof(int64_t) * (k ? k : 1));
+    for (size_t i = 0; i < k; i++) inc[i] = (int64_t)incd[i];
+    void *ad = NULL, *sd = NULL, *id = NULL;
+    napi_value applied = new_typed(env, napi_uint8_array, k, 1, &ad);
+    napi_value nst = new_typed(env, napi_uint8_array, k, 1, &sd);
+    napi_value ninc = new_typed(env, napi_float64_array, k, 8, &id);
+    int64_t *ninc64 = (int64_t *)malloc(sizeof(int64_t) * (k ? k : 1));
+    uint32_t napplied = 0;
+    int rc = k ? rp_members_update((rp_members *)h->p, ids, st, inc, (uint32_t)k, (int64_t)now, (uint8_t *)ad,
+                                   (uint8_t *)sd, ninc64, &napplied)
+               : 0;
+    for (size_t i = 0; rc == 0 && i < k; i++) ((double *)id)[i] = (double)ninc64[i];
+    free(inc);
+    free(ninc64);
+    RP_OK(rc);
+    napi_value out;
+    napi_create_object(env, &out);
+    napi_set_named_property(env, out, "applied", applied);
+    napi_set_named_property(env, out, "status", nst);
+    napi_set_named_property(env, out, "inc", ninc);
+    napi_set_named_property(env, out, "nApplied", make_u32(env, napplied));
+    return out;
+}
+
+static napi_value js_members_checksum(napi_env env, napi_callback_info info) {
+    ARGS(1);
+    handle_t *h = get_handle(env, argv[0], 2);
+    if (!h) return NULL;
+    uint32_t v = 0;
+    int set = 0;
+    RP_OK(rp_members_checksum((rp_members *)h->p, &v, &set));
+    return set ? make_u32(env, v) : make_null(env);
+}
+
+static napi_value js_members_compute_checksum(napi_env env, napi_callback_info info) {
+    ARGS(1);
+    handle_t *h = get_handle(env, argv[0], 2);
+    if (!h) return NULL;
+    RP_OK(rp_members_compute_checksum((rp_members *)h->p));
+    return js_members_checksum(env, info);
+}
+
+static napi_value js_members_checksum_string(napi_env env, napi_callback_info info) {
+    ARGS(1);
+    handle_t *h = get_handle(env, argv[0], 2);
+    if (!h) return NULL;
+    uint64_t len = 0;
+    RP_OK(rp_members_checksum_string((rp_members *)h->p, NULL, 0, &len));
+    char *buf = (char *)malloc(len + 1);
+    int rc = rp_members_checksum_string((rp_members *)h->p, buf, len, &len);
+    if (rc) {
+        free(buf);
+        RP_OK(rc);
+    }
+    napi_value s;
+    napi_create_string_utf8(env, buf, len, &s);
+    free(buf);
+    return s;
+}
+
+/* dump(h) -> {exists: Uint8Array, status: Uint8Array, inc: Float64Array} by member id. */
+static napi_value js_members_dump(napi_env env, napi_callback_info info) {
+    ARGS(1);
+    handle_t *h = get_handle(env, argv[0], 2);
+    if (!h) return NULL;
+    rp_members *m = (rp_members *)h->p;
+    uint32_t n = 0;
+    RP_OK(rp_members_count(m, &n));
+    void *ed = NULL, *sd = NULL, *id = NULL;
+    napi_value ex = new_typed(env, napi_uint8_array, n, 1, &ed);
+    napi_value st = new_typed(env, napi_uint8_array, n, 1, &sd);
+    napi_value inc = new_typed(env, napi_float64_array, n, 8, &id);
+    int64_t *i64 = (int64_t *)malloc(sizeof(int64_t) * (n ? n : 1));
+    int rc = n ? rp_members_dump(m, (uint8_t *)ed, (uint8_t *)sd, i64, n) : 0;
+    for (uint32_t i = 0; rc == 0 && i < n; i++) ((double *)id)[i] = (double)i64[i];
+    free(i64);
+    RP_OK(rc);
+    napi_value out;
+    napi_create_object(env, &out);
+    napi_set_named_property(env, out, "exists", ex);
+    napi_set_named_property(env, out, "status", st);
+    napi_set_named_property(env, out, "inc", inc);
+    return out;
+}
+
+/* ------------------------------------------------------------------ gossip simulator */
+/* simCreate(names[], inc0 Float64Array, dead Uint8Array, seed, suspicionRounds, now0, device) */
+static napi_value js_sim_create(napi_env env, napi_callback_info info) {
+    ARGS(7);
+    strpack_t s;
+    if (strpack_from_array(env, argv[0], &s)) return NULL;
+    size_t n1 = 0, n2 = 0;
+    const double *incd = (const double *)typed_data(env, argv[1], napi_float64_array, &n1);
+    const uint8_t *dead = (const uint8_t *)typed_data(env, argv[2], napi_uint8_array, &n2);
+    if (!incd || !dead || n1 != s.n || n2 != s.n) {
+        strpack_free(&s);
+        napi_throw_type_error(env, NULL, "simCreate expects inc0 Float64Array and dead Uint8Array of names.length");
+        return NULL;
+    }
+    uint32_t seed = 0, susp = 0;
+    int32_t dev = 0;
+    double now0 = 0;
+    napi_get_value_uint32(env, argv[3], &seed);
+    napi_get_value_uint32(env, argv[4], &susp);
+    napi_get_value_double(env, argv[5], &now0);
+    napi_get_value_int32(env, argv[6], &dev);
+    int64_t *inc = (int64_t *)malloc(sizeof(int64_t) * (s.n ? s.n : 1));
+    for (uint32_t i = 0; i < s.n; i++) inc[i] = (int64_t)incd[i];
+    rp_sim *sim = NULL;
+    int rc = rp_sim_create(s.n, s.bytes, s.off32, inc, dead, seed, susp, (int64_t)now0, dev, &sim);
+    free(inc);
+    strpack_free(&s);
+    RP_OK(rc);
+    return wrap_handle(env, 3, sim);
+}
+
+static napi_value js_sim_step(napi_env env, napi_callback_info info) {
+    ARGS(2);
+    handle_t *h = get_handle(env, argv[0], 3);
+    if (!h) return NULL;
+    uint32_t rounds = 0;
+    NAPI_OK(napi_get_value_uint32(env, argv[1], &rounds));
+    RP_OK(rp_sim_step((rp_sim *)h->p, rounds));
+    return NULL;
+}
+
+static napi_value js_sim_round(napi_env env, napi_callback_info info) {
+    ARGS(1);
+    handle_t *h = get_handle(env, argv[0], 3);
+    if (!h) return NULL;
+    int64_t r = 0;
+    RP_OK(rp_sim_round((rp_sim *)h->p, &r));
+    napi_value out;
+    napi_create_double(env, (double)r, &out);
+    return out;
+}
+
+static napi_value js_sim_checksums(napi_env env, napi_callback_info info) {
+    ARGS(2);
+    handle_t *h = get_handle(env, argv[0], 3);
+    if (!h) return NULL;
+    uint32_t n = 0;
+    NAPI_OK(napi_get_value_uint32(env, argv[1], &n));
+    void *d = NULL;
+    napi_value out = new_typed(env, napi_uint32_array, n, 4, &d);
+    RP_OK(rp_sim_checksums((rp_sim *)h->p, (uint32_t *)d));
+    return out;
+}
+
+static napi_value js_sim_view(napi_env env, napi_callback_info info) {
+    ARGS(3);
+    handle_t *h = get_handle(env, argv[0], 3);
+    if (!h) return NULL;
+    uint32_t v = 0, n = 0;
+    NAPI_OK(napi_get_value_uint32(env, argv[1], &v));
+    NAPI_OK(napi_get_value_uint32(env, argv[2], &n));
+    void *sd = NULL, *id = NULL;
+    napi_value st = new_typed(env, napi_uint8_array, n, 1, &sd);
+    napi_value inc = new_typed(env, napi_float64_array, n, 8, &id);
+    int64_t *i64 = (int64_t *)malloc(sizeof(int64_t) * (n ? n : 1));
+    int rc = rp_sim_view((rp_sim *)h->p, v, (uint8_t *)sd, i64);
+    for (uint32_t i = 0; rc == 0 && i < n; i++) ((double *)id)[i] = (double)i64[i];
+    free(i64);
+    RP_OK(rc);
+    napi_value out;
+    napi_create_object(env, &out);
+    napi_set_named_property(env, out, "status", st);
+    napi_set_named_property(env, out, "inc", inc);
+    return out;
+}
+
+static napi_value js_sim_converged(napi_env env, napi_callback_info info) {
+    ARGS(1);
+    handle_t *h = get_handle(env, argv[0], 3);
+    if (!h) return NULL;
+    int c = 0;
+    RP_OK(rp_sim_converged((rp_sim *)h->p, &c));
+    return make_bool(env, c);
+}
+
+static napi_value js_sim_stats(napi_env env, napi_callback_info info) {
+    ARGS(1);
+    handle_t *h = get_handle(env, argv[0], 3);
+    if (!h) return NULL;
+    uint64_t s[4] = {0, 0, 0, 0};
+    RP_OK(rp_sim_stats((rp_sim *)h->p, s));
+    static const char *names[4] = {"pings", "pingReqs", "fullSyncs", "applied"};
+    napi_value out;
+    napi_create_object(env, &out);
+    for (int i = 0; i < 4; i++) {
+        napi_value v;
+        napi_create_double(env, (double)s[i], &v);
+        napi_set_named_property(env, out, names[i], v);
+    }
+    return out;
+}
+
+/* ------------------------------------------------------------------ module */
+static napi_value init(napi_env env, napi_value exports) {
+    static const struct {
+        const char *name;
+        napi_callback fn;
+    } fns[] = {
+        {"version", js_version},
+        {"deviceCount", js_device_count},
+        {"hash32", js_hash32},
+        {"destroy", js_destroy},
+        {"ringCreate", js_ring_create},
+        {"ringAddRemove", js_ring_add_remove},
+        {"ringChecksum", js_ring_checksum},
+        {"ringChecksumString", js_ring_checksum_string},
+        {"ringServerCount", js_ring_server_count},
+        {"ringTokenCount", js_ring_token_count},
+        {"ringHasServer", js_ring_has_server},
+        {"ringServers", js_ring_servers},
+        {"ringOwnerName", js_ring_owner_name},
+        {"ringLookup", js_ring_lookup},
+        {"ringLookupN", js_ring_lookupn},
+        {"ringLookupNHashes", js_ring_lookupn_hashes},
+        {"membersCreate", js_members_create},
+        {"membersIntern", js_members_intern},
+        {"membersSetLocal", js_members_set_local},
+        {"membersUpdate", js_members_update},
+        {"membersChecksum", js_members_checksum},
+        {"membersComputeChecksum", js_members_compute_checksum},
+        {"membersChecksumString", js_members_checksum_string},
+        {"membersDump", js_members_dump},
+        {"simCreate", js_sim_create},
+        {"simStep", js_sim_step},
+        {"simRound", js_sim_round},
+        {"simChecksums", js_sim_checksums},
+        {"simView", js_sim_view},
+        {"simConverged", js_sim_converged},
+        {"simStats", js_sim_stats},
+    };
+    for (size_t i = 0; i < sizeof(fns) / sizeof(fns[0]); i++) {
+        napi_value f;
+        napi_create_function(env, fns[i].name, NAPI_AUTO_LENGTH, fns[i].fn, NULL, &f);
+        napi_set_named_property(env, exports, fns[i].name, f);
+    }
+    return exports;
+}
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, init)

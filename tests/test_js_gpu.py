@@ -1,0 +1,50 @@
+"""GPU parity of the Node N-API host (ringpop-node_amd/js): the reference's JS API
+(HashRing, GossipSim) driven from node against the reference goldens. Each test runs one
+node process (tests/js/*.js) that reports its mismatches as JSON."""
+import json
+import os
+import shutil
+import subprocess
+
+import pytest
+
+import golden_util as gu
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(shutil.which("node") is None, reason="node not in this image")]
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run_node(script, payload, tmp_path):
+    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "ringpop-node_amd", "js")])
+    inp = tmp_path / "in.json"
+    inp.write_text(json.dumps(payload))
+    out = subprocess.run(["node", os.path.join(REPO, "tests", "js", script), str(inp)],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def test_js_hashring_matches_reference_goldens(gpu, tmp_path):
+    cases = gu.load("ring_golden.json")["cases"]
+    for c in cases:
+        for b in c["batches"]:
+            if "keys" in b:
+                b["keys"] = gu.keys_of(b)
+            b.pop("tree", None)
+    res = run_node("ring_parity.js", {"cases": cases}, tmp_path)
+    assert res["nfail"] == 0, res["fails"]
+    assert res["checks"] > 500
+
+
+def test_js_gossipsim_matches_reference_goldens(gpu, tmp_path):
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("rp_synth", os.path.join(REPO, "ringpop-node_amd", "synth.py"))
+    S = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(S)
+    cases = []
+    for c in gu.load("sim_golden.json")["cases"][:2]:
+        n = c["n"]
+        cases.append(dict(c, names=[S.c2_addr(i) for i in range(n)], inc0=[int(x) for x in S.c3_members(n)[2]]))
+    res = run_node("sim_parity.js", {"cases": cases}, tmp_path)
+    assert res["nfail"] == 0, res["fails"]
