@@ -106,6 +106,40 @@ def merge_bench(rpa, local, n=100_000, k=100_000, batches=20, warmup=3):
             "gpu_ms_per_batch": e0.elapsed_time(e1) / batches, "checksum": m.checksum}
 
 
+def sim_bench(rpa, local, n=10_000, kill_pct=1, seed=11, max_rounds=300, max_seconds=240.0):
+    """C4 (BASELINE.json configs[3]): n ringpop nodes with full views, kill_pct% killed before
+    round 0, gossip rounds until convergence (scenario-runner.js:152-170 + every
+    killed member faulty everywhere). Reports rounds-to-convergence and device time per round."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("rp_synth", os.path.join(REPO, "ringpop-node_amd", "synth.py"))
+    S = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(S)
+    k = max(1, n * kill_pct // 100)
+    names = [S.c2_addr(i) for i in range(n)]
+    inc0 = S.c3_members(n)[2]
+    dead = S.kill_set(n, k, seed)
+    t0 = time.perf_counter()
+    sim = rpa.GossipSim(names, inc0, dead, seed=seed, suspicion_rounds=25, device=local)
+    torch.cuda.synchronize()
+    create_s = time.perf_counter() - t0
+    rounds, conv, t0 = 0, False, time.perf_counter()
+    per_round = []
+    while rounds < max_rounds and time.perf_counter() - t0 < max_seconds:
+        a = time.perf_counter()
+        sim.step(1)
+        per_round.append(time.perf_counter() - a)
+        rounds += 1
+        if sim.converged():
+            conv = True
+            break
+    dt = time.perf_counter() - t0
+    st = sim.stats()
+    return {"workload": "C4: %d members, full views, %d killed (%d%%), suspicion 25 rounds" % (n, k, kill_pct),
+            "converged": conv, "rounds_to_convergence": rounds if conv else None, "rounds_run": rounds,
+            "ms_per_round": dt * 1e3 / max(rounds, 1), "max_round_ms": max(per_round) * 1e3 if per_round else None,
+            "create_s": create_s, "stats": st}
+
+
 def pmc_traffic():
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
@@ -127,6 +161,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-merge", action="store_true")
+    ap.add_argument("--sim-n", type=int, default=10000, help="C4 members (0: skip the sim leg)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -208,6 +243,8 @@ def main():
         }
         if not args.no_merge:
             out["merge"] = merge_bench(rpa, local)
+        if args.sim_n:
+            out["sim"] = sim_bench(rpa, local, n=args.sim_n)
         if not args.no_cpu:
             th = args.cpu_threads or min(16, os.cpu_count() or 1)
             out["cpu_baseline"] = cpu_baseline(servers, args.cpu_keys, th)
