@@ -13,6 +13,7 @@
 // registers (fh::hash32_words), searched bucket-first, walked for distinct owners, and the
 // owner rows are staged back through LDS for coalesced stores.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -79,6 +80,25 @@ struct PackedView {
         return lo;
     }
     __device__ __forceinline__ uint32_t owner(uint32_t j) const { return ent[j] & ((1u << B) - 1u); }
+};
+
+// Compact lookup layout (the C2 hot path). Sized so the whole table stays in one XCD's 4 MB L2
+// (≈3.5 MB at 10k servers x 100 replicas; the packed layout's 8 MB missed ~half the time):
+//   2^cb buckets on the top cb token bits, cb = floor(log2 M) (1-2 tokens per bucket);
+//   idx[g] = {position of the first token of bucket 8g, 8 x 4-bit token counts of buckets
+//   8g..8g+7} (8 B per 8 buckets); ent = 3 bytes per token, (fp << ob) | owner, where fp is
+//   the top (24 - ob) bits of the token's low 32 - cb bits (all of them when they fit) and
+//   owner < 2^ob. A key's bucket start is one 8-B load plus a nibble sum; its position and
+//   successor owners come from one unaligned 16-B load of 5 entries. A key whose fingerprint
+//   equals one in its bucket (only when fp drops bits) is deferred to the exact fix path.
+struct CompactView {
+    const uint8_t* ent;   // 3 B per token, M + kEnt3Pad entries (+16 B)
+    const uint32_t* idx;  // 2 u32 per group of 8 buckets
+    uint32_t M;
+    uint32_t cb;   // bucket bits (>= 3)
+    uint32_t ob;   // owner bits
+    uint32_t fsh;  // fingerprint = (low 32 - cb bits of the hash) >> fsh
+    uint32_t exact;  // fsh == 0: fingerprints are the whole residual
 };
 
 // lookupN walk (lib/ring/index.js:157-189) with the result kept in registers (np <= MAXN).
@@ -153,6 +173,7 @@ namespace {
 
 constexpr int kLkThreads = 256;
 constexpr uint32_t kEntPad = 32;  // padding entries after M in the packed array
+constexpr uint32_t kEnt3Pad = 16;  // padding entries after M in the compact array (+16 bytes)
 constexpr int kDefaultKPL = 2;     // keys per lane in the probe kernel (RP_LOOKUP_KPL overrides)
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -413,10 +434,216 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_probe(const uint8_t* __r
     }
 }
 
-// Exact completion of the keys k_lookupn_probe deferred (same stream, so it sees the list and
-// overwrites those rows): binary search in the bucket + the reference walk.
-template <int LEN, int MODE = 0>
-__global__ __launch_bounds__(256) void k_lookupn_fix(const uint8_t* __restrict__ keys, PackedView rv, int np,
+typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
+
+// the 5 whole 3-byte entries in a 16-byte window
+__device__ __forceinline__ void ent5(const u32x4_a1 v, uint32_t (&e)[5]) {
+    e[0] = v.x & 0xFFFFFFu;
+    e[1] = (v.x >> 24) | ((v.y & 0xFFFFu) << 8);
+    e[2] = (v.y >> 16) | ((v.z & 0xFFu) << 16);
+    e[3] = v.z >> 8;
+    e[4] = v.w & 0xFFFFFFu;
+}
+
+// distinct owners in visit order (lib/ring/index.js:173-186) from window entries j >= off
+__device__ __forceinline__ uint32_t dedupe5(const uint32_t (&e)[5], uint32_t off, uint32_t omask, uint32_t need,
+                                            uint32_t (&res)[4]) {
+    uint32_t rc = 0;
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        const uint32_t o = e[j] & omask;
+        const bool dup = (rc > 0 && o == res[0]) | (rc > 1 && o == res[1]) | (rc > 2 && o == res[2]);
+        if ((uint32_t)j >= off && !dup && rc < need) {
+            res[0] = rc == 0 ? o : res[0];
+            res[1] = rc == 1 ? o : res[1];
+            res[2] = rc == 2 ? o : res[2];
+            res[3] = rc == 3 ? o : res[3];
+            rc++;
+        }
+    }
+    return rc;
+}
+
+constexpr uint32_t kSlowPerTile = 32;  // deferred-key slots per tile of the compact kernel
+
+// The C2 hot kernel over the compact layout: KPL keys per lane, all of a lane's random loads
+// issued together (the index records, then the entry windows, then any second windows), so
+// each dependent trip overlaps KPL keys. Whole tiles only (the launcher sends the tail to the
+// generic kernel), 16-B aligned keys and output rows of NEED owners. Keys stream HBM -> LDS
+// with 16-B non-temporal loads; owner rows leave through LDS as 16-B non-temporal stores.
+// Per key: window 1 = the 5 entries at the bucket start. If the bucket has more than 5 tokens
+// and all 5 are below the key, window 2 continues the search at lo + 5; if the owners run
+// past window 1, window 2 starts at the position. Deferred to the exact fix path (per-tile
+// slot lists, no global atomics): a fingerprint tie, a bucket of more than 10 tokens, a
+// position within 10 of the ring end (wrap), more repeated owners than the windows cover.
+template <int KPL, int NEED>
+__global__ __launch_bounds__(kLkThreads) void k_lookupn_compact(const uint8_t* __restrict__ keys, uint64_t ntiles,
+                                                                CompactView cv, uint32_t* __restrict__ out,
+                                                                uint8_t* __restrict__ counts,
+                                                                uint32_t* __restrict__ slow_list,
+                                                                uint32_t* __restrict__ slow_cnt) {
+    constexpr int LEN = 36, W4 = LEN / 4;
+    constexpr int TK = kLkThreads * KPL;
+    constexpr int V4 = TK * W4 / 4;
+    constexpr int PER = (V4 + kLkThreads - 1) / kLkThreads;
+    static_assert((TK * W4) % 4 == 0 && (TK * NEED) % 4 == 0, "tile must be whole 16-B vectors");
+    constexpr int SK = TK * W4, SO = TK * NEED;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[SK > SO ? SK : SO];
+    __shared__ uint32_t nslow_tile;
+    uint32_t* const sk = lds;
+    uint32_t* const so = lds;
+    const int tid = threadIdx.x;
+    const uint32_t omask = (1u << cv.ob) - 1u;
+    const uint32_t bsh = 32u - cv.cb;
+    const uint32_t rmask = (1u << bsh) - 1u;
+    const u32x2* idx2 = reinterpret_cast<const u32x2*>(cv.idx);
+    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint64_t base = t * TK;
+        {
+            const u32x4* s4 = reinterpret_cast<const u32x4*>(keys + base * LEN);
+            u32x4 pre[PER];
+#pragma unroll
+            for (int q = 0; q < PER; q++) {
+                const int k = tid + q * kLkThreads;
+                if (k < V4) pre[q] = __builtin_nontemporal_load(s4 + k);
+            }
+#pragma unroll
+            for (int q = 0; q < PER; q++) {
+                const int k = tid + q * kLkThreads;
+                if (k < V4) reinterpret_cast<u32x4*>(sk)[k] = pre[q];
+            }
+        }
+        if (tid == 0) nslow_tile = 0;
+        __syncthreads();
+        uint32_t h[KPL];
+#pragma unroll
+        for (int k = 0; k < KPL; k++) {
+            uint32_t w[W4];
+#pragma unroll
+            for (int j = 0; j < W4; j++) w[j] = sk[(tid + k * kLkThreads) * W4 + j];
+            h[k] = fh::hash32_words<LEN>(w);
+        }
+        __syncthreads();  // sk is reused as so below
+        u32x2 rec[KPL];
+#pragma unroll
+        for (int k = 0; k < KPL; k++) rec[k] = idx2[h[k] >> (bsh + 3u)];
+        uint32_t lo[KPL], bc[KPL];
+        u32x4_a1 win[KPL];
+#pragma unroll
+        for (int k = 0; k < KPL; k++) {
+            const uint32_t s4 = ((h[k] >> bsh) & 7u) * 4u;
+            const uint32_t below = rec[k].y & ((1u << s4) - 1u);
+            const uint32_t x = (below & 0x0F0F0F0Fu) + ((below >> 4) & 0x0F0F0F0Fu);
+            lo[k] = rec[k].x + ((x * 0x01010101u) >> 24);
+            bc[k] = (rec[k].y >> s4) & 15u;
+            win[k] = *reinterpret_cast<const u32x4_a1*>(cv.ent + 3ull * lo[k]);
+        }
+        uint32_t res[KPL][4], rc[KPL], ipos[KPL], kfp[KPL];
+        bool slow[KPL], search[KPL], again[KPL];
+#pragma unroll
+        for (int k = 0; k < KPL; k++) {
+            uint32_t e[5];
+            ent5(win[k], e);
+            kfp[k] = (h[k] & rmask) >> cv.fsh;
+            uint32_t lt = 0;
+            bool tie = false;
+#pragma unroll
+            for (int j = 0; j < 5; j++) {
+                const uint32_t f = e[j] >> cv.ob;
+                const bool inb = (uint32_t)j < bc[k];
+                lt += (inb && f < kfp[k]);
+                tie |= (inb && f == kfp[k]);
+            }
+            search[k] = lt == 5u && bc[k] > 5u;  // the position lies past window 1
+            ipos[k] = lo[k] + lt;
+            slow[k] = (tie && !cv.exact) | (lo[k] + 10u > cv.M);
+            res[k][0] = res[k][1] = res[k][2] = res[k][3] = NIL;
+            rc[k] = search[k] ? 0u : dedupe5(e, lt, omask, NEED, res[k]);
+            again[k] = !slow[k] && (search[k] || rc[k] < (uint32_t)NEED);
+        }
+#pragma unroll
+        for (int k = 0; k < KPL; k++)
+            if (again[k]) win[k] = *reinterpret_cast<const u32x4_a1*>(cv.ent + 3ull * ipos[k]);
+#pragma unroll
+        for (int k = 0; k < KPL; k++) {
+            if (again[k]) {
+                uint32_t e[5];
+                ent5(win[k], e);
+                uint32_t off = 0;
+                if (search[k]) {  // window 2 holds bucket entries 5..9
+                    bool tie = false;
+#pragma unroll
+                    for (int j = 0; j < 5; j++) {
+                        const uint32_t f = e[j] >> cv.ob;
+                        const bool inb = (uint32_t)j + 5u < bc[k];
+                        off += (inb && f < kfp[k]);
+                        tie |= (inb && f == kfp[k]);
+                    }
+                    slow[k] |= (tie && !cv.exact) | (off == 5u && bc[k] > 10u);
+                }
+                res[k][0] = res[k][1] = res[k][2] = res[k][3] = NIL;
+                rc[k] = dedupe5(e, off, omask, NEED, res[k]);
+                slow[k] |= rc[k] < (uint32_t)NEED;
+            }
+            const uint32_t kk = tid + k * kLkThreads;
+            if (slow[k]) {
+                const uint32_t pos = atomicAdd(&nslow_tile, 1u);
+                if (pos < kSlowPerTile) slow_list[t * kSlowPerTile + pos] = (uint32_t)kk;
+            }
+#pragma unroll
+            for (int q = 0; q < NEED; q++) so[kk * NEED + q] = res[k][q];
+            if (counts) counts[base + kk] = (uint8_t)rc[k];
+        }
+        __syncthreads();
+        if (tid == 0) slow_cnt[t] = nslow_tile;
+        u32x4* d4 = reinterpret_cast<u32x4*>(out + base * NEED);
+        const u32x4* s4 = reinterpret_cast<const u32x4*>(so);
+#pragma unroll
+        for (int k = tid; k < TK * NEED / 4; k += kLkThreads) __builtin_nontemporal_store(s4[k], d4 + k);
+        __syncthreads();
+    }
+}
+
+// Exact completion of the keys k_lookupn_compact deferred: thread (tile, slot) redoes its
+// listed key; a tile whose list overflowed is redone whole, strided over its slot threads.
+template <class View>
+__global__ __launch_bounds__(256) void k_lookupn_fix_tiles(const uint8_t* __restrict__ keys, View rv, int np,
+                                                           uint32_t W, uint32_t* __restrict__ out,
+                                                           uint8_t* __restrict__ counts,
+                                                           const uint32_t* __restrict__ slow_list,
+                                                           const uint32_t* __restrict__ slow_cnt, uint64_t ntiles,
+                                                           uint32_t TK) {
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t t = gid / kSlowPerTile;
+    const uint32_t sl = (uint32_t)(gid % kSlowPerTile);
+    if (t >= ntiles) return;
+    const uint32_t c = slow_cnt[t];
+    if (c == 0) return;
+    auto redo = [&](uint64_t k) {
+        uint32_t w[9];
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(keys + k * 36);
+#pragma unroll
+        for (int j = 0; j < 9; j++) w[j] = src[j];
+        const uint32_t h = fh::hash32_words<36>(w);
+        uint32_t res[4];
+        const int cnt = ring_walk<4>(rv, rv.find(h), np, res);
+        uint32_t* row = out + k * W;
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if ((uint32_t)q < W) row[q] = res[q];
+        if (counts) counts[k] = (uint8_t)cnt;
+    };
+    if (c <= kSlowPerTile) {
+        if (sl < c) redo(t * TK + slow_list[t * kSlowPerTile + sl]);
+    } else {
+        for (uint32_t k = sl; k < TK; k += kSlowPerTile) redo(t * TK + k);
+    }
+}
+
+// Exact completion of the keys k_lookupn_probe / k_lookupn_compact deferred (same stream, so it
+// sees the list and overwrites those rows): binary search in the bucket + the reference walk.
+template <int LEN, int MODE = 0, class View = PackedView>
+__global__ __launch_bounds__(256) void k_lookupn_fix(const uint8_t* __restrict__ keys, View rv, int np,
                                                      uint32_t W, uint32_t* __restrict__ out,
                                                      uint8_t* __restrict__ counts,
                                                      const uint32_t* __restrict__ slow,
@@ -611,6 +838,39 @@ __global__ void k_pack(const uint32_t* __restrict__ tok, const uint32_t* __restr
         ent[j] = j < M ? ((tok[j] << B) | own[j]) : 0xFFFFFFFFu;
 }
 
+// compact entries: 3 bytes per token, (fp << ob) | owner; padding entries are all ones
+__global__ void k_pack3(const uint32_t* __restrict__ tok, const uint32_t* __restrict__ own, uint32_t M,
+                        uint32_t cb, uint32_t ob, uint32_t fsh, uint8_t* __restrict__ ent) {
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    const uint32_t rmask = cb == 0 ? 0xFFFFFFFFu : ((1u << (32u - cb)) - 1u);
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < (uint64_t)M + kEnt3Pad + 6; j += gstride) {
+        const uint32_t v = j < M ? ((((tok[j] & rmask) >> fsh) << ob) | own[j]) : 0xFFFFFFu;
+        ent[3 * j + 0] = (uint8_t)v;
+        ent[3 * j + 1] = (uint8_t)(v >> 8);
+        ent[3 * j + 2] = (uint8_t)(v >> 16);
+    }
+}
+
+// compact index: per group of 8 buckets {first position, 8 x 4-bit counts}; *over is set when a
+// bucket holds more than 15 tokens (the layout is then not used)
+__global__ void k_cindex(const uint32_t* __restrict__ bst, uint32_t ngroups, uint32_t* __restrict__ idx,
+                         uint32_t* __restrict__ over) {
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ngroups; g += gstride) {
+        uint32_t nib = 0;
+        bool bad = false;
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            const uint32_t c = bst[g * 8 + s + 1] - bst[g * 8 + s];
+            bad |= c > 15u;
+            nib |= (c > 15u ? 15u : c) << (4 * s);
+        }
+        idx[2 * g] = bst[g * 8];
+        idx[2 * g + 1] = nib;
+        if (bad) atomicOr(over, 1u);
+    }
+}
+
 // checksum string pieces: len of (name + ';') for in-ring servers in name order.
 __global__ void k_ck_len(const uint32_t* __restrict__ sorted_ids, uint32_t n,
                          const uint8_t* __restrict__ in_ring, const uint64_t* __restrict__ noff,
@@ -680,9 +940,14 @@ struct Ring {
     uint32_t bbits = 8;
     // packed lookup layout (valid while every interned id < 2^16)
     DevBuf<uint32_t> ent, pbstart;
-    DevBuf<uint32_t> slow, nslow;  // deferred keys of the probe kernel
+    DevBuf<uint32_t> slow, nslow;  // deferred keys of the probe / compact kernels
     bool packed = false;
     uint32_t pbits = 16;
+    // compact lookup layout (the C2 hot path; valid while every interned id < 2^16)
+    DevBuf<uint8_t> cent;
+    DevBuf<uint32_t> cidx;
+    bool compact = false;
+    uint32_t ccb = 0, cob = 0, cfsh = 0;
     // checksum string + value
     DevBuf<uint8_t> d_inring;
     DevBuf<uint8_t> ck_buf;
@@ -700,6 +965,7 @@ struct Ring {
         return RingView{tok.p, own.p, bstart.p, M, 32u - bbits};
     }
     PackedView pview() const { return PackedView{ent.p, pbstart.p, M, pbits}; }
+    CompactView cview() const { return CompactView{cent.p, cidx.p, M, ccb, cob, cfsh, cfsh == 0}; }
 };
 
 static uint32_t ring_intern(Ring& r, const char* s, uint32_t n) {
@@ -716,6 +982,39 @@ static uint32_t choose_bbits(uint32_t M) {
     uint32_t b = 8;
     while (b < 22 && (1ull << (b + 2)) < M) b++;
     return b;
+}
+
+// The compact layout (CompactView): 2^cb buckets with cb = floor(log2 M), owner ids in ob bits,
+// fingerprints of 24 - ob bits. Not built for tiny rings, more than 2^16 interned names, or a
+// bucket of more than 15 tokens (caller hashFunc values that collide); the packed / wide
+// layouts serve those.
+static void ring_build_compact(Ring& r) {
+    r.compact = false;
+    if (r.M < 64) return;
+    uint32_t ob = 1;
+    while ((1ull << ob) < r.nt.size()) ob++;
+    if (ob > 16) return;
+    uint32_t cb = 3;
+    while (cb < 24 && (2ull << cb) <= r.M) cb++;
+    const uint32_t rb = 32 - cb, fb = 24 - ob;
+    const uint32_t fsh = fb >= rb ? 0 : rb - fb;
+    const uint64_t nbk = 1ull << cb, ngroups = nbk >> 3;
+    r.tmpk.reserve(nbk + 1);
+    hipLaunchKernelGGL(k_bucket_index, dim3(grid_for(nbk + 1, 256)), dim3(256), 0, r.st, r.tok.p, r.M, cb, r.tmpk.p);
+    r.cidx.reserve(2 * ngroups);
+    r.scalar.reserve(1);
+    RP_HIP(hipMemsetAsync(r.scalar.p, 0, sizeof(uint32_t), r.st));
+    hipLaunchKernelGGL(k_cindex, dim3(grid_for(ngroups, 256)), dim3(256), 0, r.st, r.tmpk.p, (uint32_t)ngroups,
+                       r.cidx.p, r.scalar.p);
+    r.cent.reserve(3ull * ((uint64_t)r.M + kEnt3Pad + 6) + 16);
+    hipLaunchKernelGGL(k_pack3, dim3(grid_for((uint64_t)r.M + kEnt3Pad + 6, 256)), dim3(256), 0, r.st, r.tok.p,
+                       r.own.p, r.M, cb, ob, fsh, r.cent.p);
+    RP_HIP(hipGetLastError());
+    if (read_u32(r.scalar.p, r.st) != 0) return;
+    r.compact = true;
+    r.ccb = cb;
+    r.cob = ob;
+    r.cfsh = fsh;
 }
 
 static void ring_rebuild_index(Ring& r) {
@@ -740,6 +1039,7 @@ static void ring_rebuild_index(Ring& r) {
                            B, r.pbstart.p);
         RP_HIP(hipGetLastError());
     }
+    ring_build_compact(r);
 }
 
 // Device replica tokens for server ids (or caller tokens), sorted stably by token.
@@ -890,6 +1190,58 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
     const bool fixed36 = !hashes && stride == 36 && ((reinterpret_cast<uintptr_t>(keys) & 3) == 0);
     const int need = np <= 0 ? 1 : np;
     const bool use_packed = r.packed && !getenv_flag("RP_RING_WIDE");
+    const char* lay = getenv("RP_RING_LAYOUT");  // A/B: "packed" forces the packed probe kernel
+    const bool use_compact = r.compact && !(lay && !strcmp(lay, "packed")) && !getenv_flag("RP_RING_WIDE");
+    const bool aligned16 = ((reinterpret_cast<uintptr_t>(keys) & 15) == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
+    if (use_compact && fixed36 && aligned16 && (uint32_t)need == W && W <= 4 && n >= (uint64_t)kLkThreads * 4) {
+        RP_REQUIRE(n < (1ull << 32), "lookupn: at most 2^32-1 keys per call");
+        const CompactView cv = r.cview();
+        const int kpl = getenv("RP_LOOKUP_KPL") ? atoi(getenv("RP_LOOKUP_KPL")) : 4;
+        const uint64_t TK = (uint64_t)kLkThreads * (kpl == 1 ? 1 : kpl == 2 ? 2 : 4);
+        const uint64_t ntiles = n / TK, done = ntiles * TK;
+        r.slow.reserve(ntiles * kSlowPerTile + 1);
+        r.nslow.reserve(ntiles + 1);
+        const unsigned g = grid_for(ntiles, 1, 256 * 8);
+#define RP_COMPACT(KPL, NEED)                                                                               \
+    hipLaunchKernelGGL((k_lookupn_compact<KPL, NEED>), dim3(g), dim3(kLkThreads), 0, st, keys, ntiles, cv, out,  \
+                       counts, r.slow.p, r.nslow.p)
+#define RP_COMPACT_N(KPL)         \
+    switch (need) {               \
+        case 1: RP_COMPACT(KPL, 1); break; \
+        case 2: RP_COMPACT(KPL, 2); break; \
+        case 3: RP_COMPACT(KPL, 3); break; \
+        default: RP_COMPACT(KPL, 4); break; \
+    }
+        if (kpl == 1) {
+            RP_COMPACT_N(1);
+        } else if (kpl == 2) {
+            RP_COMPACT_N(2);
+        } else {
+            RP_COMPACT_N(4);
+        }
+#undef RP_COMPACT_N
+#undef RP_COMPACT
+        const uint64_t fthreads = ntiles * kSlowPerTile;
+        hipLaunchKernelGGL((k_lookupn_fix_tiles<RingView>), dim3((unsigned)((fthreads + 255) / 256)), dim3(256), 0, st,
+                           keys, r.view(), np, W, out, counts, r.slow.p, r.nslow.p, ntiles, (uint32_t)TK);
+        RP_HIP(hipGetLastError());
+        if (getenv_flag("RP_LOOKUP_DEBUG")) {
+            std::vector<uint32_t> c(ntiles);
+            RP_HIP(hipMemcpyAsync(c.data(), r.nslow.p, 4 * ntiles, hipMemcpyDeviceToHost, st));
+            RP_HIP(hipStreamSynchronize(st));
+            uint64_t tot = 0, over = 0;
+            for (uint32_t x : c) {
+                tot += x;
+                over += x > kSlowPerTile;
+            }
+            fprintf(stderr, "[rp] compact lookupN: %llu keys, %llu deferred, %llu overflowed tiles (cb %u ob %u fsh %u)\n",
+                    (unsigned long long)done, (unsigned long long)tot, (unsigned long long)over, r.ccb, r.cob, r.cfsh);
+        }
+        if (done < n)  // the partial last tile
+            launch_lookupn_view(r.view(), keys + done * 36, nullptr, 36, nullptr, n - done, np, W, out + done * W,
+                                counts ? counts + done : nullptr, st);
+        return;
+    }
     if (use_packed && fixed36 && W <= 4 && need <= 4 && !getenv_flag("RP_RING_NOWINDOW")) {
         RP_REQUIRE(n < (1ull << 32), "lookupn: at most 2^32-1 keys per call");
         r.slow.reserve(n + 1);

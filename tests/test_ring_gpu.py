@@ -105,13 +105,23 @@ def _random_history(orc, gpu, seed, pool_size, R, nbatches):
     return ring, oracle
 
 
-LAYOUTS = {"window": ("0", "0"), "packed": ("0", "1"), "wide": ("1", "1")}
+# lookup layouts/kernels (rp_ring.hip): compact = the default C2 hot path (k_lookupn_compact);
+# window = the packed probe kernel; packed / wide = the generic kernels over those layouts.
+LAYOUTS = {
+    "compact": {},
+    "compact-kpl1": {"RP_LOOKUP_KPL": "1"},
+    "compact-kpl2": {"RP_LOOKUP_KPL": "2"},
+    "window": {"RP_RING_LAYOUT": "packed"},
+    "packed": {"RP_RING_LAYOUT": "packed", "RP_RING_NOWINDOW": "1"},
+    "wide": {"RP_RING_WIDE": "1"},
+}
 
 
 def set_layout(monkeypatch, layout):
-    wide, nowin = LAYOUTS[layout]
-    monkeypatch.setenv("RP_RING_WIDE", wide)
-    monkeypatch.setenv("RP_RING_NOWINDOW", nowin)
+    for k in ("RP_RING_WIDE", "RP_RING_NOWINDOW", "RP_RING_LAYOUT", "RP_LOOKUP_KPL"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in LAYOUTS[layout].items():
+        monkeypatch.setenv(k, v)
 
 
 @pytest.mark.parametrize("layout", list(LAYOUTS))
@@ -219,10 +229,14 @@ def test_c2_full_size_properties(gpu, orc):
     assert ((own[:, 0] != own[:, 1]) & (own[:, 1] != own[:, 2]) & (own[:, 0] != own[:, 2])).all()
     # load balance sanity: every server owns some keys
     assert np.bincount(own[:, 0], minlength=10000).min() > 0
-    idx = np.arange(0, n, 997)
-    sample = np.stack([orc.uuid_keys(42, int(i), 1)[0] for i in idx[:4000]])
-    w, _ = oracle.lookupn_keys(sample, 3)
-    assert np.array_equal(own[idx[:4000]], w)
+    # exact: the first 2^21 keys (fingerprint ties, long buckets and the ring end all occur)
+    m = 1 << 21
+    w, wc = oracle.lookupn_keys(orc.uuid_keys(42, 0, m), 3, threads=8)
+    assert np.array_equal(own[:m], w)
+    d_l = torch.empty(n, dtype=torch.int32, device="cuda")
+    ring.lookup_dev(d_k.data_ptr(), n, d_l.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(d_l.cpu().numpy().view(np.uint32)[:m], w[:, 0])
 
 
 def test_edge_cases(gpu):
@@ -237,16 +251,17 @@ def test_edge_cases(gpu):
     assert len(ids) == 0 and len(cnt) == 0
 
 
-@pytest.mark.parametrize("nserv,R", [(1, 100), (2, 2000), (3, 700), (5, 5), (40, 1)])
-def test_window_kernel_slow_paths_vs_oracle(gpu, orc, nserv, R, monkeypatch):
-    """Rings that force the window kernel's exact fallbacks: long buckets, runs of one owner,
+@pytest.mark.parametrize("layout", ["compact", "compact-kpl1", "window"])
+@pytest.mark.parametrize("nserv,R", [(1, 100), (2, 2000), (3, 700), (5, 5), (40, 1), (64, 3)])
+def test_window_kernel_slow_paths_vs_oracle(gpu, orc, nserv, R, layout, monkeypatch):
+    """Rings that force the window kernels' exact fallbacks: long buckets, runs of one owner,
     wrap past the last token, rings smaller than the window."""
-    set_layout(monkeypatch, "window")
+    set_layout(monkeypatch, layout)
     servers = [orc.c2_addr(i + 17) for i in range(nserv)]
     ring, oracle = gpu.HashRing({"replicaPoints": R}), orc.Ring(R)
     ring.addRemoveServers(servers)
     oracle.add_remove(servers)
-    n = 1 << 16
+    n = (1 << 16) + 77  # a partial last tile goes through the generic kernel
     d_k = torch.empty(n * 36, dtype=torch.uint8, device="cuda")
     gpu.gen_uuid_keys_dev(5, 0, n, d_k.data_ptr())
     keys = orc.uuid_keys(5, 0, n)

@@ -2,8 +2,9 @@
 
     python tools/ab_lookup.py [--servers 10000] [--log2 26] [--rounds 7]
 
-Variants: packed (16-bit owner / 2^16-bucket layout) vs wide (u32 token + owner arrays,
-RP_RING_WIDE=1), for lookup and lookupN(3). Prints median/min ms and lookups/s per variant.
+Variants: the compact layout (default) at 1/2/4 keys per lane, the packed probe kernel
+(RP_RING_LAYOUT=packed), the wide binary-search kernel (RP_RING_WIDE=1), and the hash-only
+ablation, for lookup and lookupN(3). Prints median/min ms and lookups/s per variant.
 """
 import argparse
 import json
@@ -32,29 +33,26 @@ def main():
     keys = torch.empty(B * 36, dtype=torch.uint8, device="cuda")
     rpa.gen_uuid_keys_dev(42, 0, B, keys.data_ptr(), st.cuda_stream)
     out = torch.empty(B * 3, dtype=torch.int32, device="cuda")
+    # name -> (environment, n): compact = the default layout; packed = RP_RING_LAYOUT=packed
     variants = {
-        "probe/lookupN3": ("0", 3, "0"),
-        "probe-kpl1/lookupN3": ("0", 3, "0"),
-        "probe-kpl4/lookupN3": ("0", 3, "0"),
-        "probe-kpl8/lookupN3": ("0", 3, "0"),
-        "probe/lookup": ("0", 1, "0"),
-        "probe/ablate-hash-only": ("0", 3, "1"),
-        "probe/ablate-hash+find": ("0", 3, "2"),
-        "packed/lookupN3": ("0", 3, "0"),
-        "wide/lookupN3": ("1", 3, "0"),
-        "packed/lookup": ("0", 1, "0"),
-        "wide/lookup": ("1", 1, "0"),
-        "packed/ablate-hash+find": ("0", 3, "2"),
+        "compact-kpl4/lookupN3": ({"RP_LOOKUP_KPL": "4"}, 3),
+        "compact-kpl2/lookupN3": ({"RP_LOOKUP_KPL": "2"}, 3),
+        "compact-kpl1/lookupN3": ({"RP_LOOKUP_KPL": "1"}, 3),
+        "compact-kpl4/lookup": ({"RP_LOOKUP_KPL": "4"}, 1),
+        "compact-kpl2/lookup": ({"RP_LOOKUP_KPL": "2"}, 1),
+        "probe/lookupN3": ({"RP_RING_LAYOUT": "packed", "RP_LOOKUP_KPL": "2"}, 3),
+        "probe/ablate-hash-only": ({"RP_RING_LAYOUT": "packed", "RP_LOOKUP_ABLATE": "1"}, 3),
+        "wide/lookupN3": ({"RP_RING_WIDE": "1"}, 3),
     }
     if a.only:
         variants = {k: v for k, v in variants.items() if k in a.only.split(",")}
+    knobs = ("RP_LOOKUP_KPL", "RP_RING_LAYOUT", "RP_LOOKUP_ABLATE", "RP_RING_WIDE")
     times = {k: [] for k in variants}
     for r in range(a.rounds + 1):
-        for name, (wide, n, abl) in variants.items():
-            os.environ["RP_RING_WIDE"] = wide
-            os.environ["RP_LOOKUP_ABLATE"] = abl
-            os.environ["RP_RING_NOWINDOW"] = "0" if name.startswith("probe") else "1"
-            os.environ["RP_LOOKUP_KPL"] = name.split("/")[0][len("probe-kpl"):] if "kpl" in name else "2"
+        for name, (env, n) in variants.items():
+            for kn in knobs:
+                os.environ.pop(kn, None)
+            os.environ.update(env)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
             if n == 1:
