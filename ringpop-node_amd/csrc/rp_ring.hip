@@ -99,6 +99,33 @@ struct CompactView {
     uint32_t ob;   // owner bits
     uint32_t fsh;  // fingerprint = (low 32 - cb bits of the hash) >> fsh
     uint32_t exact;  // fsh == 0: fingerprints are the whole residual
+    uint32_t ablate;  // diagnostics only (RP_LOOKUP_ABLATE): 1 = no second windows, 2 = aligned windows
+};
+
+// Exact view for the compact kernel's deferred keys: the bucket start comes from the compact
+// index (one load) and the position from the exact wide tokens of that bucket, so a deferred
+// key costs ~4 dependent loads instead of a full binary search.
+struct CompactFixView {
+    const uint32_t* tok;
+    const uint32_t* own;
+    const uint32_t* idx;
+    RingView wide;  // buckets of 16+ tokens
+    uint32_t M;
+    uint32_t cb;
+
+    __device__ __forceinline__ uint32_t find(uint32_t h) const {
+        const uint32_t bsh = 32u - cb;
+        const uint32_t g = h >> (bsh + 3u), s4 = ((h >> bsh) & 7u) * 4u;
+        const uint32_t base = idx[2 * g], nib = idx[2 * g + 1];
+        const uint32_t bc = (nib >> s4) & 15u;
+        if (bc == 15u) return wide.find(h);
+        const uint32_t below = nib & ((1u << s4) - 1u);
+        const uint32_t x = (below & 0x0F0F0F0Fu) + ((below >> 4) & 0x0F0F0F0Fu);
+        uint32_t i = base + ((x * 0x01010101u) >> 24);
+        for (uint32_t j = 0; j < bc && tok[i] < h; j++) i++;
+        return i;
+    }
+    __device__ __forceinline__ uint32_t owner(uint32_t j) const { return own[j]; }
 };
 
 // lookupN walk (lib/ring/index.js:157-189) with the result kept in registers (np <= MAXN).
@@ -536,7 +563,7 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_compact(const uint8_t* _
             const uint32_t x = (below & 0x0F0F0F0Fu) + ((below >> 4) & 0x0F0F0F0Fu);
             lo[k] = rec[k].x + ((x * 0x01010101u) >> 24);
             bc[k] = (rec[k].y >> s4) & 15u;
-            win[k] = *reinterpret_cast<const u32x4_a1*>(cv.ent + 3ull * lo[k]);
+            win[k] = *reinterpret_cast<const u32x4_a1*>(cv.ent + ((3ull * lo[k]) & (cv.ablate == 2 ? ~15ull : ~0ull)));
         }
         uint32_t res[KPL][4], rc[KPL], ipos[KPL], kfp[KPL];
         bool slow[KPL], search[KPL], again[KPL];
@@ -559,7 +586,7 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_compact(const uint8_t* _
             slow[k] = (tie && !cv.exact) | (lo[k] + 10u > cv.M);
             res[k][0] = res[k][1] = res[k][2] = res[k][3] = NIL;
             rc[k] = search[k] ? 0u : dedupe5(e, lt, omask, NEED, res[k]);
-            again[k] = !slow[k] && (search[k] || rc[k] < (uint32_t)NEED);
+            again[k] = !slow[k] && (search[k] || rc[k] < (uint32_t)NEED) && cv.ablate != 1;
         }
 #pragma unroll
         for (int k = 0; k < KPL; k++)
@@ -604,8 +631,8 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_compact(const uint8_t* _
     }
 }
 
-// Exact completion of the keys k_lookupn_compact deferred: thread (tile, slot) redoes its
-// listed key; a tile whose list overflowed is redone whole, strided over its slot threads.
+// Exact completion of the keys k_lookupn_compact deferred: one thread per tile redoes the keys
+// on its list (a tile whose list overflowed is redone whole).
 template <class View>
 __global__ __launch_bounds__(256) void k_lookupn_fix_tiles(const uint8_t* __restrict__ keys, View rv, int np,
                                                            uint32_t W, uint32_t* __restrict__ out,
@@ -613,9 +640,7 @@ __global__ __launch_bounds__(256) void k_lookupn_fix_tiles(const uint8_t* __rest
                                                            const uint32_t* __restrict__ slow_list,
                                                            const uint32_t* __restrict__ slow_cnt, uint64_t ntiles,
                                                            uint32_t TK) {
-    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t t = gid / kSlowPerTile;
-    const uint32_t sl = (uint32_t)(gid % kSlowPerTile);
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ntiles) return;
     const uint32_t c = slow_cnt[t];
     if (c == 0) return;
@@ -634,9 +659,9 @@ __global__ __launch_bounds__(256) void k_lookupn_fix_tiles(const uint8_t* __rest
         if (counts) counts[k] = (uint8_t)cnt;
     };
     if (c <= kSlowPerTile) {
-        if (sl < c) redo(t * TK + slow_list[t * kSlowPerTile + sl]);
+        for (uint32_t q = 0; q < c; q++) redo(t * TK + slow_list[t * kSlowPerTile + q]);
     } else {
-        for (uint32_t k = sl; k < TK; k += kSlowPerTile) redo(t * TK + k);
+        for (uint32_t k = 0; k < TK; k++) redo(t * TK + k);
     }
 }
 
@@ -965,7 +990,10 @@ struct Ring {
         return RingView{tok.p, own.p, bstart.p, M, 32u - bbits};
     }
     PackedView pview() const { return PackedView{ent.p, pbstart.p, M, pbits}; }
-    CompactView cview() const { return CompactView{cent.p, cidx.p, M, ccb, cob, cfsh, cfsh == 0}; }
+    CompactView cview() const {
+        const char* a = getenv("RP_LOOKUP_ABLATE");
+        return CompactView{cent.p, cidx.p, M, ccb, cob, cfsh, cfsh == 0, a ? (uint32_t)atoi(a) : 0u};
+    }
 };
 
 static uint32_t ring_intern(Ring& r, const char* s, uint32_t n) {
@@ -996,6 +1024,10 @@ static void ring_build_compact(Ring& r) {
     if (ob > 16) return;
     uint32_t cb = 3;
     while (cb < 24 && (2ull << cb) <= r.M) cb++;
+    if (const char* d = getenv("RP_COMPACT_CB_DELTA")) {  // A/B knob: bucket density
+        const int c = (int)cb + atoi(d);
+        cb = (uint32_t)(c < 3 ? 3 : c > 24 ? 24 : c);
+    }
     const uint32_t rb = 32 - cb, fb = 24 - ob;
     const uint32_t fsh = fb >= rb ? 0 : rb - fb;
     const uint64_t nbk = 1ull << cb, ngroups = nbk >> 3;
@@ -1197,7 +1229,7 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
         RP_REQUIRE(n < (1ull << 32), "lookupn: at most 2^32-1 keys per call");
         const CompactView cv = r.cview();
         const int kpl = getenv("RP_LOOKUP_KPL") ? atoi(getenv("RP_LOOKUP_KPL")) : 4;
-        const uint64_t TK = (uint64_t)kLkThreads * (kpl == 1 ? 1 : kpl == 2 ? 2 : 4);
+        const uint64_t TK = (uint64_t)kLkThreads * (kpl == 1 ? 1 : kpl == 2 ? 2 : kpl == 8 ? 8 : 4);
         const uint64_t ntiles = n / TK, done = ntiles * TK;
         r.slow.reserve(ntiles * kSlowPerTile + 1);
         r.nslow.reserve(ntiles + 1);
@@ -1216,14 +1248,19 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
             RP_COMPACT_N(1);
         } else if (kpl == 2) {
             RP_COMPACT_N(2);
+        } else if (kpl == 8 && need == 3) {
+            RP_COMPACT(8, 3);
         } else {
             RP_COMPACT_N(4);
         }
 #undef RP_COMPACT_N
 #undef RP_COMPACT
-        const uint64_t fthreads = ntiles * kSlowPerTile;
-        hipLaunchKernelGGL((k_lookupn_fix_tiles<RingView>), dim3((unsigned)((fthreads + 255) / 256)), dim3(256), 0, st,
-                           keys, r.view(), np, W, out, counts, r.slow.p, r.nslow.p, ntiles, (uint32_t)TK);
+        const uint64_t fthreads = ntiles;
+        const CompactFixView fv{r.tok.p, r.own.p, r.cidx.p, r.view(), r.M, r.ccb};
+        if (cv.ablate != 3)
+            hipLaunchKernelGGL((k_lookupn_fix_tiles<CompactFixView>), dim3((unsigned)((fthreads + 255) / 256)),
+                               dim3(256), 0, st, keys, fv, np, W, out, counts, r.slow.p, r.nslow.p, ntiles,
+                               (uint32_t)TK);
         RP_HIP(hipGetLastError());
         if (getenv_flag("RP_LOOKUP_DEBUG")) {
             std::vector<uint32_t> c(ntiles);
