@@ -169,6 +169,32 @@ int rp_sim_converged(rp_sim *s, int *out);
 /* pings, ping-reqs, full syncs, applied updates since creation. */
 int rp_sim_stats(rp_sim *s, uint64_t *out4);
 
+/* ---- Sharded simulator (C5): a handle owns the nodes [bounds[shard], bounds[shard+1]) of a
+ * partition of [0, n) into nshards contiguous ranges (bounds NULL = equal ranges); its views
+ * still cover all n members. A round is five stages (rp_sim_stage 0..4) separated by four
+ * message exchanges: after stage k < 4 the outbox holds this shard's messages grouped by
+ * destination shard (rp_sim_outbox: per-destination message / record counts and the device
+ * buffers, 40-byte headers and 24-byte records); before stage k + 1 the caller fills the inbox
+ * with every source's messages for this shard, concatenated in source-shard order
+ * (rp_sim_inbox sizes it and returns the device buffers). rp_sim_exchange_local does the
+ * exchange for handles of one process; across processes the host moves the bytes (RCCL
+ * all-to-all-v; ringpop-node_amd DistGossipSim). Checksums / views / stats are per shard
+ * (checksums: the shard's nodes in id order); convergence reduces rp_sim_converged_local
+ * {live nodes, min checksum, max checksum, killed-not-faulty flag} over the shards. */
+int rp_sim_create_shard(uint32_t n, const char *names, const uint32_t *off, const int64_t *inc0, const uint8_t *dead,
+                        uint32_t seed, uint32_t suspicion_rounds, int64_t now0, int device, const uint32_t *bounds,
+                        uint32_t nshards, uint32_t shard, rp_sim **out);
+int rp_sim_shard_info(rp_sim *s, uint32_t *v0, uint32_t *nl, uint32_t *nshards, uint32_t *shard);
+int rp_sim_stage(rp_sim *s, int stage);
+int rp_sim_outbox(rp_sim *s, uint64_t *nmsg, uint64_t *nrec, void **msg, void **rec);
+int rp_sim_inbox(rp_sim *s, const uint64_t *nmsg, const uint64_t *nrec, void **msg, void **rec);
+int rp_sim_exchange_local(rp_sim *const *shards, uint32_t nshards);
+int rp_sim_converged_local(rp_sim *s, uint32_t *out4);
+
+/* Stream-ordered copy between any host / device buffers (hipMemcpyDefault); NULL stream =
+ * synchronous. Used by hosts that move sharded-simulator messages. */
+int rp_copy(void *dst, const void *src, uint64_t bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

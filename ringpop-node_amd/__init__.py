@@ -87,6 +87,14 @@ SIGNATURES = {
     "rp_sim_view": (_INT, [_P, _U32, _P, _P]),
     "rp_sim_converged": (_INT, [_P, _P]),
     "rp_sim_stats": (_INT, [_P, _P]),
+    "rp_sim_create_shard": (_INT, [_U32, _P, _P, _P, _P, _U32, _U32, ctypes.c_int64, _INT, _P, _U32, _U32, _P]),
+    "rp_sim_shard_info": (_INT, [_P, _P, _P, _P, _P]),
+    "rp_sim_stage": (_INT, [_P, _INT]),
+    "rp_sim_outbox": (_INT, [_P, _P, _P, _P, _P]),
+    "rp_sim_inbox": (_INT, [_P, _P, _P, _P, _P]),
+    "rp_sim_exchange_local": (_INT, [_P, _U32]),
+    "rp_sim_converged_local": (_INT, [_P, _P]),
+    "rp_copy": (_INT, [_P, _P, _U64, _P]),
 }
 
 STATUS = {"alive": 0, "suspect": 1, "faulty": 2, "leave": 3}
@@ -547,3 +555,278 @@ class GossipSim:
         out = np.zeros(4, dtype=np.uint64)
         check(lib().rp_sim_stats(self._h, out.ctypes.data))
         return dict(zip(["pings", "pingreqs", "fullsyncs", "applied"], (int(x) for x in out)))
+
+
+# ---------------------------------------------------------------------------------------------
+# Sharded simulator (C5): nodes partitioned over shards; a round = five stages + four message
+# exchanges (include/ringpop_amd.h "Sharded simulator"). Bytes on the wire per message: a
+# 40-byte header and 24-byte records.
+
+MSG_BYTES = 40
+REC_BYTES = 24
+SIM_STAGES = 5
+
+
+def shard_bounds(n, nshards):
+    """Equal contiguous ranges (the C ABI's default partition)."""
+    return np.array([n * g // nshards for g in range(nshards + 1)], dtype=np.uint32)
+
+
+class SimShard:
+    """One shard handle of the gossip simulator: nodes [v0, v0 + NL) with full views."""
+
+    def __init__(self, names, inc0, dead, nshards, shard, seed=11, suspicion_rounds=25, now0=None, device=0,
+                 bounds=None):
+        self.N = len(names)
+        self.G = nshards
+        self.shard = shard
+        buf, off = _pack(names)
+        inc0 = np.ascontiguousarray(inc0, dtype=np.int64)
+        self.dead = np.ascontiguousarray(dead, dtype=np.uint8)
+        self.bounds = np.ascontiguousarray(bounds if bounds is not None else shard_bounds(self.N, nshards),
+                                           dtype=np.uint32)
+        if now0 is None:
+            now0 = 1434401518824 + 10 ** 9
+        h = ctypes.c_void_p()
+        check(lib().rp_sim_create_shard(self.N, buf, off.ctypes.data, inc0.ctypes.data, self.dead.ctypes.data, seed,
+                                        suspicion_rounds, int(now0), device, self.bounds.ctypes.data, nshards, shard,
+                                        ctypes.byref(h)))
+        self._h = h
+        self.v0 = int(self.bounds[shard])
+        self.NL = int(self.bounds[shard + 1]) - self.v0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().rp_sim_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def stage(self, k):
+        check(lib().rp_sim_stage(self._h, k))
+
+    def outbox(self):
+        """(nmsg[G], nrec[G], device msg pointer, device rec pointer): messages grouped by destination."""
+        nm = np.zeros(self.G, dtype=np.uint64)
+        nr = np.zeros(self.G, dtype=np.uint64)
+        mp, rp_ = ctypes.c_void_p(), ctypes.c_void_p()
+        check(lib().rp_sim_outbox(self._h, nm.ctypes.data, nr.ctypes.data, ctypes.byref(mp), ctypes.byref(rp_)))
+        return nm, nr, mp.value or 0, rp_.value or 0
+
+    def inbox(self, nmsg, nrec):
+        """Size the inbox for per-source counts; returns (device msg pointer, device rec pointer)."""
+        nm = np.ascontiguousarray(nmsg, dtype=np.uint64)
+        nr = np.ascontiguousarray(nrec, dtype=np.uint64)
+        mp, rp_ = ctypes.c_void_p(), ctypes.c_void_p()
+        check(lib().rp_sim_inbox(self._h, nm.ctypes.data, nr.ctypes.data, ctypes.byref(mp), ctypes.byref(rp_)))
+        return mp.value or 0, rp_.value or 0
+
+    @property
+    def round(self):
+        v = ctypes.c_int64()
+        check(lib().rp_sim_round(self._h, ctypes.byref(v)))
+        return v.value
+
+    def checksums(self):
+        out = np.empty(self.NL, dtype=np.uint32)
+        if self.NL:
+            check(lib().rp_sim_checksums(self._h, out.ctypes.data))
+        return out
+
+    def view(self, v):
+        st = np.empty(self.N, dtype=np.uint8)
+        inc = np.empty(self.N, dtype=np.int64)
+        check(lib().rp_sim_view(self._h, v, st.ctypes.data, inc.ctypes.data))
+        return st, inc
+
+    def conv_local(self):
+        out = np.zeros(4, dtype=np.uint32)
+        check(lib().rp_sim_converged_local(self._h, out.ctypes.data))
+        return out
+
+    def stats(self):
+        out = np.zeros(4, dtype=np.uint64)
+        check(lib().rp_sim_stats(self._h, out.ctypes.data))
+        return out
+
+
+def conv_reduce(parts):
+    """Convergence (scenario-runner.js:152-170 + killed members faulty everywhere) from the
+    shards' {live, min checksum, max checksum, killed-not-faulty} parts."""
+    live = sum(int(p[0]) for p in parts)
+    if live == 0:
+        return True
+    lo = min(int(p[1]) for p in parts if int(p[0]))
+    hi = max(int(p[2]) for p in parts if int(p[0]))
+    return lo == hi and not any(int(p[3]) for p in parts)
+
+
+_STAT_NAMES = ["pings", "pingreqs", "fullsyncs", "applied"]
+
+
+class ShardedGossipSim:
+    """The simulator split into `nshards` shard handles inside this process (one device or
+    several: `devices`), exchanging messages with device copies (rp_sim_exchange_local). Same
+    results as GossipSim; used to test the sharded path on one GPU."""
+
+    def __init__(self, names, inc0, dead, nshards, seed=11, suspicion_rounds=25, now0=None, devices=None,
+                 bounds=None):
+        self.N = len(names)
+        self.G = nshards
+        devices = devices or [0] * nshards
+        self.shards = [SimShard(names, inc0, dead, nshards, g, seed, suspicion_rounds, now0, devices[g], bounds)
+                       for g in range(nshards)]
+        self._arr = (ctypes.c_void_p * nshards)(*[s._h.value for s in self.shards])
+
+    def close(self):
+        for s in self.shards:
+            s.close()
+
+    def step(self, rounds=1):
+        for _ in range(rounds):
+            for k in range(SIM_STAGES):
+                for s in self.shards:
+                    s.stage(k)
+                if k < SIM_STAGES - 1:
+                    check(lib().rp_sim_exchange_local(self._arr, self.G))
+
+    @property
+    def round(self):
+        return self.shards[0].round
+
+    def checksums(self):
+        return np.concatenate([s.checksums() for s in self.shards])
+
+    def view(self, v):
+        for s in self.shards:
+            if s.v0 <= v < s.v0 + s.NL:
+                return s.view(v)
+        raise IndexError(v)
+
+    def converged(self):
+        return conv_reduce([s.conv_local() for s in self.shards])
+
+    def stats(self):
+        tot = sum(s.stats() for s in self.shards)
+        return dict(zip(_STAT_NAMES, (int(x) for x in tot)))
+
+
+class MessageExchange:
+    """All-to-all-v of the sharded simulator's messages over torch.distributed: one collective
+    for the per-peer counts, one for the bytes (each peer's segment = its 40-byte headers then
+    its 24-byte records). With the nccl backend (RCCL on ROCm) the bytes stay in HBM and move
+    over xGMI; with gloo they are staged through host memory (tests). `copy(dst, src, nbytes)`
+    moves bytes between the simulator's buffers and the collective's tensors."""
+
+    def __init__(self, group=None, device=None, copy=None):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist, self.group = torch, dist, group
+        self.G = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        backend = dist.get_backend(group)
+        self.on_device = backend == "nccl"
+        self.device = device if self.on_device else "cpu"
+        self._copy = copy
+
+    def copy(self, dst, src, nbytes):
+        if nbytes:
+            if self._copy is not None:
+                self._copy(dst, src, nbytes)
+            else:
+                stream = self.torch.cuda.current_stream().cuda_stream if self.on_device else None
+                check(lib().rp_copy(dst, src, nbytes, stream))
+
+    def exchange(self, out_nmsg, out_nrec, out_msg, out_rec, alloc_in):
+        """out_*: this rank's outbox (counts per destination, buffer addresses, grouped by
+        destination). alloc_in(in_nmsg, in_nrec) -> (msg address, rec address) of the inbox,
+        which receives every source's messages concatenated in source order."""
+        torch, dist, G = self.torch, self.dist, self.G
+        cnt = torch.tensor(np.stack([out_nmsg, out_nrec], axis=1).astype(np.int64).reshape(-1), device=self.device)
+        rcnt = torch.empty_like(cnt)
+        dist.all_to_all_single(rcnt, cnt, group=self.group)
+        rc = rcnt.cpu().numpy().reshape(G, 2)
+        in_nmsg, in_nrec = rc[:, 0].astype(np.uint64), rc[:, 1].astype(np.uint64)
+        seg_out = [int(out_nmsg[g]) * MSG_BYTES + int(out_nrec[g]) * REC_BYTES for g in range(G)]
+        seg_in = [int(in_nmsg[g]) * MSG_BYTES + int(in_nrec[g]) * REC_BYTES for g in range(G)]
+        send = torch.empty(max(1, sum(seg_out)), dtype=torch.uint8, device=self.device)
+        recv = torch.empty(max(1, sum(seg_in)), dtype=torch.uint8, device=self.device)
+        base, mo, ro = send.data_ptr(), 0, 0
+        for g in range(G):
+            nb_m, nb_r = int(out_nmsg[g]) * MSG_BYTES, int(out_nrec[g]) * REC_BYTES
+            self.copy(base, out_msg + mo, nb_m)
+            self.copy(base + nb_m, out_rec + ro, nb_r)
+            base, mo, ro = base + nb_m + nb_r, mo + nb_m, ro + nb_r
+        dist.all_to_all_single(recv[:sum(seg_in)], send[:sum(seg_out)], output_split_sizes=seg_in,
+                               input_split_sizes=seg_out, group=self.group)
+        in_msg, in_rec = alloc_in(in_nmsg, in_nrec)
+        base, mo, ro = recv.data_ptr(), 0, 0
+        for g in range(G):
+            nb_m, nb_r = int(in_nmsg[g]) * MSG_BYTES, int(in_nrec[g]) * REC_BYTES
+            self.copy(in_msg + mo, base, nb_m)
+            self.copy(in_rec + ro, base + nb_m, nb_r)
+            base, mo, ro = base + nb_m + nb_r, mo + nb_m, ro + nb_r
+        if self.on_device:
+            torch.cuda.current_stream().synchronize()
+        return in_nmsg, in_nrec
+
+
+class DistGossipSim:
+    """One shard of the simulator per torch.distributed rank (C5 over 1/2/4/8 GPUs: views
+    sharded by node id range, the four per-round message exchanges as RCCL all-to-all-v).
+    Results equal GossipSim's on the same inputs."""
+
+    def __init__(self, names, inc0, dead, seed=11, suspicion_rounds=25, now0=None, device=0, group=None):
+        import torch.distributed as dist
+        self.dist, self.group = dist, group
+        self.xchg = MessageExchange(group, device=device)
+        self.G, self.rank = self.xchg.G, self.xchg.rank
+        self.N = len(names)
+        self.shard = SimShard(names, inc0, dead, self.G, self.rank, seed, suspicion_rounds, now0, device)
+        self.exchange_bytes = 0
+
+    def close(self):
+        self.shard.close()
+
+    def step(self, rounds=1):
+        sh = self.shard
+        for _ in range(rounds):
+            for k in range(SIM_STAGES):
+                sh.stage(k)
+                if k < SIM_STAGES - 1:
+                    nm, nr, mp, rp_ = sh.outbox()
+                    self.exchange_bytes += int(nm.sum()) * MSG_BYTES + int(nr.sum()) * REC_BYTES
+                    self.xchg.exchange(nm, nr, mp, rp_, sh.inbox)
+
+    @property
+    def round(self):
+        return self.shard.round
+
+    def _allgather(self, arr):
+        import torch
+        t = torch.from_numpy(np.ascontiguousarray(arr))
+        if self.xchg.on_device:
+            t = t.to(self.xchg.device)
+        outs = [torch.empty_like(t) for _ in range(self.G)]
+        self.dist.all_gather(outs, t, group=self.group)
+        return [o.cpu().numpy() for o in outs]
+
+    def converged(self):
+        return conv_reduce(self._allgather(self.shard.conv_local().astype(np.int64)))
+
+    def checksums(self):
+        """All N checksums (gathered; shards may differ in size)."""
+        sizes = np.diff(self.shard.bounds.astype(np.int64))
+        mx = int(sizes.max())
+        mine = np.zeros(mx, dtype=np.int64)
+        mine[:self.shard.NL] = self.shard.checksums()
+        parts = self._allgather(mine)
+        return np.concatenate([p[:int(n)] for p, n in zip(parts, sizes)]).astype(np.uint32)
+
+    def stats(self):
+        tot = sum(self._allgather(self.shard.stats().astype(np.int64)))
+        return dict(zip(_STAT_NAMES, (int(x) for x in tot)))

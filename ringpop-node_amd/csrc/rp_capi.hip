@@ -27,4 +27,13 @@ int rp_device_count(int* n) {
     });
 }
 
+int rp_copy(void* dst, const void* src, uint64_t bytes, void* stream) {
+    return rp::guard([&] {
+        if (!bytes) return;
+        RP_REQUIRE(dst && src, "copy: null pointer");
+        RP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, rp::as_stream(stream)));
+        if (!stream) RP_HIP(hipStreamSynchronize(nullptr));
+    });
+}
+
 }  // extern "C"

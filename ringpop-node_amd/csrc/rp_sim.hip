@@ -1,4 +1,5 @@
-// rp_sim.hip — the gossip protocol of N full ringpop nodes as a batched round simulator.
+// rp_sim.hip — the gossip protocol of N full ringpop nodes as a batched round simulator,
+// optionally sharded by node over several GPUs.
 //
 // Every node v keeps what a ringpop process keeps: its membership view (lib/membership), its
 // dissemination buffer (lib/gossip/dissemination.js), its ring membership + server count (only
@@ -9,16 +10,28 @@
 // one workgroup owns one node at a time (persistent grid); inside a node the records of one
 // message carry distinct addresses and are applied by all 256 lanes at once.
 //
+// Sharding (C5). A handle owns the nodes [v0, v0 + NL) of a partition `bounds` of [0, N) into
+// G contiguous shards; its views still cover all N members. Everything that crosses nodes is a
+// MESSAGE (header Msg + piggybacked records Rec): pings (A -> B), their responses (B -> C),
+// ping-req legs (D1 -> D2) and their responses (D2 -> D3). A round is five stages separated by
+// four exchanges; each stage ends by building an outbox grouped by destination shard (local
+// senders in id order, so the concatenation of the shards' outboxes is in global sender order,
+// which is the order the reference's receivers process them in), and the next stage imports
+// the inbox (the sources' outboxes for this shard, concatenated in shard order). The host moves
+// the bytes: an in-process swap for one shard (rp_sim_step), device copies between handles of
+// one process (rp_sim_exchange_local), or RCCL all-to-all-v between processes (the Python
+// ShardedGossipSim over torch.distributed).
+//
 // HBM layout (sized for 10^5 members on one MI355X):
-//   dense rows [v][a]   status u8 (bit 7: in this node's ring) | incarnation i64 | members-array
+//   dense rows [lv][a]  status u8 (bit 7: in this node's ring) | incarnation i64 | members-array
 //                       order u32 | dissemination slot u16  (15 B per (node, member))
 //   per node            deviation bitmap over address ranks (which rows ever changed), sparse
 //                       change list (dissemination's `changes` map: address, piggyback count,
 //                       source, source incarnation; the status/incarnation of a change always
 //                       equal the view row's), sparse timer list (address, due round, captured
 //                       incarnation); capacities checked, overflow is a loud error
-//   messages            fixed per-sender slots (ping, response, ping-req legs) + a per-round
-//                       arena (ping-req responses, full syncs, staging)
+//   messages            fixed per-sender slots (ping, ping-req legs), a per-round arena
+//                       (responses, full syncs), out/in message buffers (headers + records)
 // Checksums: the membership checksum string of a view is the all-alive base string (address
 // order, built once) with the deviated rows' pieces substituted. Nodes whose views changed are
 // re-checksummed in batch with ONE NODE PER LANE (64 independent farmhash chains per wave,
@@ -46,6 +59,7 @@ constexpr uint32_t TAG_SHUF = 0x53485546u;
 constexpr uint32_t TAG_SAMP = 0x53414d50u;
 constexpr int kHashWin = 512;      // LDS window of pre-mixed chunks for the block checksum chain
 constexpr uint8_t ST_MASK = 3, IN_RING = 0x80;
+constexpr uint32_t kMaxShards = 64;
 // error flags (rp_sim_step reports them)
 constexpr uint32_t ERR_CHANGES = 1, ERR_TIMERS = 2, ERR_ARENA = 4;
 
@@ -65,6 +79,19 @@ __device__ __forceinline__ uint32_t rec_w0(uint32_t a, uint8_t st, uint32_t aux)
     return a | ((uint32_t)st << 23) | (aux << 25);
 }
 
+// A message header (40 bytes): a ping (from sender to target, with the sender's checksum and
+// incarnation: ping-sender.js:71-76), a ping-req leg (tag = leg index; ping-req-sender.js:75-81)
+// or a response (to = the original sender). n = records (NONE = network error); roff = offset of
+// the records in the message buffer's record area.
+struct Msg {
+    uint32_t from, to, n, tag;
+    uint32_t ck, pad;
+    int64_t inc;
+    uint64_t roff;
+};
+static_assert(sizeof(Msg) == 40, "Msg layout is part of the exchange format");
+static_assert(sizeof(Rec) == 24, "Rec layout is part of the exchange format");
+
 struct Change {  // an entry of dissemination's changes map
     uint32_t addr;
     uint32_t cnt;  // piggybackCount
@@ -79,28 +106,33 @@ struct Timer {  // a suspicion timer (suspicion.js:55-84)
     int64_t inc;  // incarnation captured at start (== the row's while the episode lasts)
 };
 
+enum MsgKind : int { K_PING = 0, K_RESP = 1, K_LEG = 2, K_LRESP = 3 };
+
 struct SimDev {
-    uint32_t N, W;  // members, bitmap words per node
+    uint32_t N, W;   // members, bitmap words per node
+    uint32_t v0, NL;  // this shard's nodes [v0, v0 + NL)
+    uint32_t G;       // shards
+    const uint32_t* bounds;  // [G + 1]
     uint32_t seed, susp, Cd, Ct, Cm;
     int64_t now0;
     int64_t round;
-    // dense rows [v][N]
+    // dense rows [lv][N]
     uint8_t* st;
     int64_t* inc;
     uint32_t* order;
     uint16_t* slot;  // 0 = no change, else index + 1 into the node's change list
-    uint32_t* dev;   // [v][W] rows ever changed, by address rank
+    uint32_t* dev;   // [lv][W] rows ever changed, by address rank
     // sparse per node
-    Change* chg;  // [v][Cd]
+    Change* chg;  // [lv][Cd]
     uint32_t* n_chg;
-    Timer* tim;  // [v][Ct]
+    Timer* tim;  // [lv][Ct]
     uint32_t* n_tim;
-    // per node
+    // per local node
     int64_t* it_idx;
     uint32_t *n_shuf, *ring_count, *max_piggy, *checksum;
     uint8_t* dirty;
-    const uint8_t* dead;
-    // names in address order; base checksum string
+    const uint8_t* dead;  // [N] (global)
+    // names in address order; base checksum string (global)
     const uint32_t* sorted;
     const uint32_t* rank;
     const uint8_t* names;
@@ -108,37 +140,46 @@ struct SimDev {
     const uint8_t* sbase;
     const uint64_t* boff;  // [N+1], boff[N] = base length
     const int64_t* inc0;
-    // round scratch and messages
+    // sender side (per local node)
     int32_t* target;
     uint32_t* ck_snap;
     int64_t* inc_snap;
-    Rec* pool;  // [3][N][Cm] fixed slots (ping, response, leg) + arena
+    Rec* pool;  // [2][NL][Cm] fixed slots (ping, leg) + arena
     uint64_t arena0, arena_cap;
     unsigned long long* cursor;  // arena bump pointer (reset every round)
-    uint64_t *resp_off, *lresp_off;
-    uint32_t *ping_n, *resp_n, *leg_n;
-    uint32_t* helpers;  // [N*3]
-    uint32_t* nhelp;    // [N]
-    uint32_t* lresp_n;  // [N*3]  (NONE = network error)
+    uint32_t *ping_n, *leg_n;
+    uint32_t* helpers;  // [NL*3] (global ids)
+    uint32_t* nhelp;    // [NL]
+    uint32_t* leg_nk;   // [NL*3] records of leg k
     uint32_t* cand;     // [grid*N] scratch for ping-req candidate lists
     uint8_t* strbuf;    // [grid * strcap]
     uint64_t strcap;
-    // CSR inboxes
-    const uint32_t* in_off;  // receivers: [N+1]
-    const uint32_t* in_src;  // senders sorted by (target, sender)
-    const uint32_t* h_off;   // helpers: [N+1]
-    const uint32_t* h_src;   // (sender*3 + leg) sorted by (helper, sender, leg)
+    // inbound messages of the current stage
+    const Msg* in_msg;
+    const Rec* in_rec;
+    uint32_t nin;
+    const uint32_t* ib_off;  // [NL+1] inbox CSR (pings / legs) by local receiver
+    const uint32_t* ib_idx;  // message indices, (receiver, arrival) order
+    // receiver side: the response to each inbound message (pool offset; n NONE = network error)
+    uint32_t* rsp_n;
+    uint64_t* rsp_off;
+    // sender side: the inbound response message of each local sender / (sender, leg)
+    uint32_t* resp_idx;   // [NL]
+    uint32_t* lresp_idx;  // [NL*3]
     // stats: pings, pingreqs, fullsyncs, applied
     unsigned long long* stats;
     uint32_t* err;
 };
 
-__device__ __forceinline__ Rec* ping_slot(const SimDev& S, uint32_t v) { return S.pool + (uint64_t)v * S.Cm; }
-__device__ __forceinline__ Rec* resp_slot(const SimDev& S, uint32_t v) {
-    return S.pool + ((uint64_t)S.N + v) * S.Cm;
+__device__ __forceinline__ Rec* ping_slot(const SimDev& S, uint32_t lv) { return S.pool + (uint64_t)lv * S.Cm; }
+__device__ __forceinline__ Rec* leg_slot(const SimDev& S, uint32_t lv) {
+    return S.pool + ((uint64_t)S.NL + lv) * S.Cm;
 }
-__device__ __forceinline__ Rec* leg_slot(const SimDev& S, uint32_t v) {
-    return S.pool + (2ull * S.N + v) * S.Cm;
+
+__device__ __forceinline__ uint32_t shard_of(const SimDev& S, uint32_t v) {
+    uint32_t s = 0;
+    while (s + 1 < S.G && v >= S.bounds[s + 1]) s++;
+    return s;
 }
 
 __device__ __forceinline__ uint32_t philox_u32(uint32_t seed, uint32_t tag, uint32_t c0, uint32_t c1, uint32_t c2) {
@@ -194,8 +235,8 @@ __device__ uint32_t block_scan(uint32_t v, uint32_t* lds, uint32_t* total) {
     return base + x - v;
 }
 
-// thread 0 allocates n records from the round arena; broadcast to the block (NONE-offset on
-// overflow, with the error flag set)
+// thread 0 allocates n records from the round arena; broadcast to the block (~0 on overflow,
+// with the error flag set)
 __device__ uint64_t block_alloc(const SimDev& S, uint64_t n, uint64_t* lds64) {
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -227,11 +268,11 @@ struct Lds {
 
 // ---- checksums
 
-// Membership.computeChecksum (index.js:48-75) of node v by one workgroup: the string is
+// Membership.computeChecksum (index.js:48-75) of local node lv by one workgroup: the string is
 // written to buf in address order, then hashed (one chain lane, 192 pre-mixing lanes).
-__device__ void block_checksum(const SimDev& S, uint32_t v, uint8_t* buf, Lds& L) {
+__device__ void block_checksum(const SimDev& S, uint32_t lv, uint8_t* buf, Lds& L) {
     const uint32_t N = S.N;
-    const uint64_t row = (uint64_t)v * N;
+    const uint64_t row = (uint64_t)lv * N;
     const int tid = threadIdx.x;
     // contiguous member range per thread keeps address order inside each thread's piece
     const uint32_t per = (N + kT - 1) / kT;
@@ -337,15 +378,15 @@ __device__ void block_checksum(const SimDev& S, uint32_t v, uint8_t* buf, Lds& L
         }
     }
     if (tid == 0) {
-        S.checksum[v] = h;
-        S.dirty[v] = 0;
+        S.checksum[lv] = h;
+        S.dirty[lv] = 0;
     }
     __syncthreads();
 }
 
-__device__ __forceinline__ void checksum_if_dirty(const SimDev& S, uint32_t v, Lds& L) {
+__device__ __forceinline__ void checksum_if_dirty(const SimDev& S, uint32_t lv, Lds& L) {
     __syncthreads();
-    if (S.dirty[v]) block_checksum(S, v, S.strbuf + (uint64_t)blockIdx.x * S.strcap, L);
+    if (S.dirty[lv]) block_checksum(S, lv, S.strbuf + (uint64_t)blockIdx.x * S.strcap, L);
 }
 
 // One node's checksum string, seen by one lane: the base string with the deviated rows'
@@ -451,11 +492,11 @@ struct Fwd {
 
 __device__ __forceinline__ uint32_t ldw(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
 
-// Membership checksum of node v computed by this lane alone.
-__device__ uint32_t lane_checksum(const SimDev& S, uint32_t v) {
+// Membership checksum of local node lv computed by this lane alone.
+__device__ uint32_t lane_checksum(const SimDev& S, uint32_t lv) {
     const uint32_t N = S.N;
-    const uint64_t row = (uint64_t)v * N;
-    const LaneView V{S, S.st + row, S.inc + row, S.dev + (uint64_t)v * S.W};
+    const uint64_t row = (uint64_t)lv * N;
+    const LaneView V{S, S.st + row, S.inc + row, S.dev + (uint64_t)lv * S.W};
     // pass 1: length (base length + the deviated pieces' differences) and the last deviation
     int64_t dtot = 0;
     uint32_t last = NONE;
@@ -564,27 +605,29 @@ __device__ uint32_t lane_checksum(const SimDev& S, uint32_t v) {
     return h;
 }
 
-// every live node whose view changed: one node per lane
+// every live local node whose view changed: one node per lane
 __global__ __launch_bounds__(256) void k_ck_lanes(SimDev S) {
-    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= S.N || S.dead[v] || !S.dirty[v]) return;
-    S.checksum[v] = lane_checksum(S, v);
-    S.dirty[v] = 0;
+    const uint32_t lv = blockIdx.x * blockDim.x + threadIdx.x;
+    if (lv >= S.NL || S.dead[S.v0 + lv] || !S.dirty[lv]) return;
+    S.checksum[lv] = lane_checksum(S, lv);
+    S.dirty[lv] = 0;
 }
 
 // ---- membership / dissemination / suspicion on one node
 
-// Membership.update(records) on node v + the 'updated' listeners (on_membership_event.js:86-134):
-// view row, recordChange (dissemination.js:56-72), suspicion start (a suspect update about
-// another member), ring add/remove -> maxPiggybackCount. Records carry distinct addresses (one
-// message), so lanes apply them independently. Returns the number applied (block-uniform).
-__device__ uint32_t block_apply(const SimDev& S, uint32_t v, const Rec* recs, uint32_t n, Lds& L, int64_t now) {
-    const uint64_t row = (uint64_t)v * S.N;
+// Membership.update(records) on local node lv + the 'updated' listeners
+// (on_membership_event.js:86-134): view row, recordChange (dissemination.js:56-72), suspicion
+// start (a suspect update about another member), ring add/remove -> maxPiggybackCount. Records
+// carry distinct addresses (one message), so lanes apply them independently. Returns the number
+// applied (block-uniform).
+__device__ uint32_t block_apply(const SimDev& S, uint32_t lv, const Rec* recs, uint32_t n, Lds& L, int64_t now) {
+    const uint32_t v = S.v0 + lv;
+    const uint64_t row = (uint64_t)lv * S.N;
     uint32_t napp = 0, nadd = 0, nrem = 0;
-    Change* chg = S.chg + (uint64_t)v * S.Cd;
-    Timer* tim = S.tim + (uint64_t)v * S.Ct;
+    Change* chg = S.chg + (uint64_t)lv * S.Cd;
+    Timer* tim = S.tim + (uint64_t)lv * S.Ct;
     __syncthreads();
-    uint32_t nc = S.n_chg[v], nt = S.n_tim[v];
+    uint32_t nc = S.n_chg[lv], nt = S.n_tim[lv];
     for (uint32_t base = 0; base < n; base += kT) {
         const uint32_t i = base + threadIdx.x;
         bool applied = false, need_timer = false, need_new = false;
@@ -613,7 +656,7 @@ __device__ uint32_t block_apply(const SimDev& S, uint32_t v, const Rec* recs, ui
                 S.st[row + a] = us | ir;
                 S.inc[row + a] = ui;
                 const uint32_t k = S.rank[a];
-                atomicOr(&S.dev[(uint64_t)v * S.W + (k >> 5)], 1u << (k & 31));
+                atomicOr(&S.dev[(uint64_t)lv * S.W + (k >> 5)], 1u << (k & 31));
                 need_timer = us == ST_SUSPECT && a != v;
                 slot = S.slot[row + a];
                 need_new = slot == 0;
@@ -650,15 +693,15 @@ __device__ uint32_t block_apply(const SimDev& S, uint32_t v, const Rec* recs, ui
     const uint32_t adds = block_sum(nadd, L.u);
     const uint32_t rems = block_sum(nrem, L.u);
     if (threadIdx.x == 0) {
-        S.n_chg[v] = nc;
-        S.n_tim[v] = nt;
+        S.n_chg[lv] = nc;
+        S.n_tim[lv] = nt;
         if (tot) {
-            S.dirty[v] = 1;
+            S.dirty[lv] = 1;
             atomicAdd(&S.stats[3], (unsigned long long)tot);
             if (adds || rems) {  // ringChanged -> adjustMaxPiggybackCount (dissemination.js:38-55)
-                const uint32_t rc = S.ring_count[v] + adds - rems;
-                S.ring_count[v] = rc;
-                S.max_piggy[v] = 15u * digits(rc);
+                const uint32_t rc = S.ring_count[lv] + adds - rems;
+                S.ring_count[lv] = rc;
+                S.max_piggy[lv] = 15u * digits(rc);
             }
         }
     }
@@ -666,16 +709,16 @@ __device__ uint32_t block_apply(const SimDev& S, uint32_t v, const Rec* recs, ui
     return tot;
 }
 
-// Dissemination._issueAs (dissemination.js:133-176) for node v into out (nullable: discard).
-// Filter: sender != NONE. Entries over maxPiggybackCount are deleted; the list is compacted in
-// place (order kept). Returns the count emitted (block-uniform).
-__device__ uint32_t block_issue(const SimDev& S, uint32_t v, uint32_t sender, int64_t sinc, Rec* out, Lds& L) {
-    const uint64_t row = (uint64_t)v * S.N;
-    Change* chg = S.chg + (uint64_t)v * S.Cd;
+// Dissemination._issueAs (dissemination.js:133-176) for local node lv into out (nullable:
+// discard). Filter: sender != NONE. Entries over maxPiggybackCount are deleted; the list is
+// compacted in place (order kept). Returns the count emitted (block-uniform).
+__device__ uint32_t block_issue(const SimDev& S, uint32_t lv, uint32_t sender, int64_t sinc, Rec* out, Lds& L) {
+    const uint64_t row = (uint64_t)lv * S.N;
+    Change* chg = S.chg + (uint64_t)lv * S.Cd;
     uint32_t emitted = 0, kept = 0;
     __syncthreads();
-    const uint32_t maxp = S.max_piggy[v];
-    const uint32_t nc = S.n_chg[v];
+    const uint32_t maxp = S.max_piggy[lv];
+    const uint32_t nc = S.n_chg[lv];
     for (uint32_t base = 0; base < nc; base += kT) {
         const uint32_t j = base + threadIdx.x;
         bool keep = false, emit = false;
@@ -713,23 +756,28 @@ __device__ uint32_t block_issue(const SimDev& S, uint32_t v, uint32_t sender, in
         emitted += etot;
         __syncthreads();
     }
-    if (threadIdx.x == 0) S.n_chg[v] = kept;
+    if (threadIdx.x == 0) S.n_chg[lv] = kept;
     __syncthreads();
     return emitted;
 }
 
-// issueAsReceiver (dissemination.js:86-119): filtered issue into `out`, else a full sync (into
-// the arena) when the checksums differ. *off_out = pool offset of the message.
-__device__ uint32_t block_issue_receiver(const SimDev& S, uint32_t v, uint32_t sender, int64_t sinc, uint32_t sck,
-                                         uint64_t out_off, uint64_t* off_out, Lds& L) {
-    const uint32_t n = block_issue(S, v, sender, sinc, S.pool + out_off, L);
-    *off_out = out_off;
+// issueAsReceiver (dissemination.js:86-119) of local node lv answering `sender`: the filtered
+// issue, else a full sync when the checksums differ. The answer is written to the round arena;
+// *off_out = its pool offset. Returns the record count, or NONE on arena overflow (the sender
+// then sees a network error; rp_sim_step reports the overflow).
+__device__ uint32_t block_issue_receiver(const SimDev& S, uint32_t lv, uint32_t sender, int64_t sinc, uint32_t sck,
+                                         uint64_t* off_out, Lds& L) {
+    const uint64_t ro = block_alloc(S, S.n_chg[lv], &L.u64);
+    if (ro == ~0ull) return NONE;
+    const uint32_t n = block_issue(S, lv, sender, sinc, S.pool + ro, L);
+    *off_out = ro;
     if (n > 0) return n;
-    checksum_if_dirty(S, v, L);
-    if (S.checksum[v] == sck) return 0;
+    checksum_if_dirty(S, lv, L);
+    if (S.checksum[lv] == sck) return 0;
     const uint64_t fo = block_alloc(S, S.N, &L.u64);
-    if (fo == ~0ull) return 0;
-    const uint64_t row = (uint64_t)v * S.N;
+    if (fo == ~0ull) return NONE;
+    const uint64_t row = (uint64_t)lv * S.N;
+    const uint32_t v = S.v0 + lv;
     Rec* out = S.pool + fo;
     for (uint32_t k = threadIdx.x; k < S.N; k += kT) {  // fullSync: members-array order, source = v
         const uint32_t a = S.order[row + k];
@@ -742,16 +790,17 @@ __device__ uint32_t block_issue_receiver(const SimDev& S, uint32_t v, uint32_t s
 }
 
 // makeSuspect / makeFaulty (index.js:179-202): one update from the local member
-__device__ void block_make(const SimDev& S, uint32_t v, uint32_t a, uint8_t st, int64_t inc, Lds& L, int64_t now,
+__device__ void block_make(const SimDev& S, uint32_t lv, uint32_t a, uint8_t st, int64_t inc, Lds& L, int64_t now,
                            Rec* tmp) {
-    if (threadIdx.x == 0) *tmp = Rec{rec_w0(a, st, 0), v, inc, S.inc[(uint64_t)v * S.N + v]};
+    if (threadIdx.x == 0) *tmp = Rec{rec_w0(a, st, 0), S.v0 + lv, inc, S.inc[(uint64_t)lv * S.N + S.v0 + lv]};
     __syncthreads();
-    block_apply(S, v, tmp, 1, L, now);
+    block_apply(S, lv, tmp, 1, L, now);
 }
 
-__device__ void lane0_shuffle(const SimDev& S, uint32_t v) {
-    const uint64_t row = (uint64_t)v * S.N;
-    const uint32_t sh = S.n_shuf[v]++;
+__device__ void lane0_shuffle(const SimDev& S, uint32_t lv) {
+    const uint64_t row = (uint64_t)lv * S.N;
+    const uint32_t v = S.v0 + lv;
+    const uint32_t sh = S.n_shuf[lv]++;
     for (uint32_t i = S.N - 1; i >= 1; i--) {
         const uint32_t r = philox_u32(S.seed, TAG_SHUF, sh, i, v);
         const uint32_t j = (uint32_t)(((uint64_t)r * (i + 1)) >> 32);
@@ -769,13 +818,14 @@ __device__ __forceinline__ bool pingable(const SimDev& S, uint64_t row, uint32_t
 // MembershipIterator.next (iterator.js:28-51) by one lane: walk the members array (reshuffling
 // on wrap) until a pingable member, or until every distinct address has been visited. Before
 // the first wrap of a walk positions are distinct; after it a bitmap tracks distinct visits.
-__device__ int32_t lane0_iter_next(const SimDev& S, uint32_t v, uint32_t* list, uint32_t* bits) {
+__device__ int32_t lane0_iter_next(const SimDev& S, uint32_t lv, uint32_t* list, uint32_t* bits) {
     const uint32_t N = S.N;
-    const uint64_t row = (uint64_t)v * N;
+    const uint64_t row = (uint64_t)lv * N;
+    const uint32_t v = S.v0 + lv;
     uint32_t nseen = 0, steps = 0;
     bool wrapped = false;
     while (nseen < N) {
-        int64_t idx = S.it_idx[v] + 1;
+        int64_t idx = S.it_idx[lv] + 1;
         if (idx >= (int64_t)N) {
             idx = 0;
             if (!wrapped) {
@@ -783,9 +833,9 @@ __device__ int32_t lane0_iter_next(const SimDev& S, uint32_t v, uint32_t* list, 
                 for (uint32_t q = 0; q < steps; q++) bits[list[q] >> 5] |= 1u << (list[q] & 31);
                 wrapped = true;
             }
-            lane0_shuffle(S, v);
+            lane0_shuffle(S, lv);
         }
-        S.it_idx[v] = idx;
+        S.it_idx[lv] = idx;
         const uint32_t m = S.order[row + idx];
         if (!wrapped) {
             list[steps] = m;
@@ -800,7 +850,7 @@ __device__ int32_t lane0_iter_next(const SimDev& S, uint32_t v, uint32_t* list, 
     return -1;
 }
 
-// ---- phases
+// ---- phases (each over this shard's nodes)
 
 __global__ void k_round_begin(SimDev S) {
     if (blockIdx.x == 0 && threadIdx.x == 0) *S.cursor = 0;
@@ -810,27 +860,28 @@ __global__ void k_round_begin(SimDev S) {
 __global__ __launch_bounds__(kT) void k_phase_a(SimDev S) {
     __shared__ Lds L;
     __shared__ int32_t tgt;
-    for (uint32_t v = blockIdx.x; v < S.N; v += gridDim.x) {
+    for (uint32_t lv = blockIdx.x; lv < S.NL; lv += gridDim.x) {
+        const uint32_t v = S.v0 + lv;
         if (S.dead[v]) {
-            if (threadIdx.x == 0) S.target[v] = -1;
+            if (threadIdx.x == 0) S.target[lv] = -1;
             continue;
         }
-        const uint64_t row = (uint64_t)v * S.N;
+        const uint64_t row = (uint64_t)lv * S.N;
         if (threadIdx.x == 0) {
             uint8_t* scratch = S.strbuf + (uint64_t)blockIdx.x * S.strcap;
-            const int32_t found = lane0_iter_next(S, v, reinterpret_cast<uint32_t*>(scratch),
+            const int32_t found = lane0_iter_next(S, lv, reinterpret_cast<uint32_t*>(scratch),
                                                   reinterpret_cast<uint32_t*>(scratch + 4ull * S.N));
             tgt = found;
-            S.target[v] = found;
+            S.target[lv] = found;
         }
         __syncthreads();
         if (tgt >= 0) {
-            checksum_if_dirty(S, v, L);
-            const uint32_t n = block_issue(S, v, NONE, 0, ping_slot(S, v), L);
+            checksum_if_dirty(S, lv, L);
+            const uint32_t n = block_issue(S, lv, NONE, 0, ping_slot(S, lv), L);
             if (threadIdx.x == 0) {
-                S.ping_n[v] = n;
-                S.ck_snap[v] = S.checksum[v];
-                S.inc_snap[v] = S.inc[row + v];
+                S.ping_n[lv] = n;
+                S.ck_snap[lv] = S.checksum[lv];
+                S.inc_snap[lv] = S.inc[row + v];
                 atomicAdd(&S.stats[0], 1ull);
             }
         }
@@ -838,22 +889,21 @@ __global__ __launch_bounds__(kT) void k_phase_a(SimDev S) {
     }
 }
 
-// B: each live target applies its pings in sender order and answers each one
+// B: each live local target applies its pings in sender order and answers each one
 __global__ __launch_bounds__(kT) void k_phase_b(SimDev S) {
     __shared__ Lds L;
     const int64_t now = S.now0 + 200 * S.round;
-    for (uint32_t j = blockIdx.x; j < S.N; j += gridDim.x) {
-        if (S.dead[j]) continue;
-        const uint32_t b = S.in_off[j], e = S.in_off[j + 1];
+    for (uint32_t lj = blockIdx.x; lj < S.NL; lj += gridDim.x) {
+        const uint32_t b = S.ib_off[lj], e = S.ib_off[lj + 1];
         for (uint32_t q = b; q < e; q++) {
-            const uint32_t v = S.in_src[q];
-            block_apply(S, j, ping_slot(S, v), S.ping_n[v], L, now);
-            uint64_t o;
-            const uint32_t n = block_issue_receiver(S, j, v, S.inc_snap[v], S.ck_snap[v],
-                                                    (uint64_t)(resp_slot(S, v) - S.pool), &o, L);
+            const uint32_t i = S.ib_idx[q];
+            const Msg m = S.in_msg[i];
+            block_apply(S, lj, S.in_rec + m.roff, m.n, L, now);
+            uint64_t o = 0;
+            const uint32_t n = block_issue_receiver(S, lj, m.from, m.inc, m.ck, &o, L);
             if (threadIdx.x == 0) {
-                S.resp_n[v] = n;
-                S.resp_off[v] = o;
+                S.rsp_n[i] = n;
+                S.rsp_off[i] = o;
             }
             __syncthreads();
         }
@@ -865,12 +915,14 @@ __global__ __launch_bounds__(kT) void k_phase_b(SimDev S) {
 __global__ __launch_bounds__(kT) void k_phase_c(SimDev S) {
     __shared__ Lds L;
     const int64_t now = S.now0 + 200 * S.round;
-    for (uint32_t v = blockIdx.x; v < S.N; v += gridDim.x) {
-        const int32_t t = S.target[v];
-        if (S.dead[v] || t < 0 || S.dead[t]) continue;
-        const Rec* r = S.pool + S.resp_off[v];
-        block_apply(S, v, r, S.resp_n[v], L, now);
-        block_apply(S, v, r, S.resp_n[v], L, now);
+    for (uint32_t lv = blockIdx.x; lv < S.NL; lv += gridDim.x) {
+        const uint32_t i = S.resp_idx[lv];
+        if (i == NONE) continue;  // dead sender, no target, dead target
+        const Msg m = S.in_msg[i];
+        if (m.n == NONE) continue;  // the target's arena overflowed (reported)
+        const Rec* r = S.in_rec + m.roff;
+        block_apply(S, lv, r, m.n, L, now);
+        block_apply(S, lv, r, m.n, L, now);
     }
 }
 
@@ -881,11 +933,12 @@ __global__ __launch_bounds__(kT) void k_phase_d1(SimDev S) {
     __shared__ uint32_t ncand;
     const int64_t now = S.now0 + 200 * S.round;
     uint32_t* cand = S.cand + (uint64_t)blockIdx.x * S.N;
-    for (uint32_t v = blockIdx.x; v < S.N; v += gridDim.x) {
-        const int32_t t = S.target[v];
-        if (threadIdx.x == 0) S.nhelp[v] = 0;
+    for (uint32_t lv = blockIdx.x; lv < S.NL; lv += gridDim.x) {
+        const uint32_t v = S.v0 + lv;
+        const int32_t t = S.target[lv];
+        if (threadIdx.x == 0) S.nhelp[lv] = 0;
         if (S.dead[v] || t < 0 || !S.dead[t]) continue;
-        const uint64_t row = (uint64_t)v * S.N;
+        const uint64_t row = (uint64_t)lv * S.N;
         if (threadIdx.x == 0) atomicAdd(&S.stats[1], 1ull);
         // candidates: members-array order, pingable, not the target (index.js:141-150)
         uint32_t written = 0;
@@ -914,29 +967,30 @@ __global__ __launch_bounds__(kT) void k_phase_d1(SimDev S) {
                 const uint32_t x = cand[i];
                 cand[i] = cand[j];
                 cand[j] = x;
-                S.helpers[v * 3 + i] = cand[i];
+                S.helpers[lv * 3 + i] = cand[i];
             }
-            S.nhelp[v] = nh;
+            S.nhelp[lv] = nh;
             ncand = nh;
         }
         __syncthreads();
         if (ncand == 0) {
-            block_make(S, v, (uint32_t)t, ST_SUSPECT, S.inc[row + t], L, now, &tmp);
-            if (threadIdx.x == 0) S.nhelp[v] = 0;
+            block_make(S, lv, (uint32_t)t, ST_SUSPECT, S.inc[row + t], L, now, &tmp);
+            if (threadIdx.x == 0) S.nhelp[lv] = 0;
             __syncthreads();
             continue;
         }
-        checksum_if_dirty(S, v, L);
+        checksum_if_dirty(S, lv, L);
         if (threadIdx.x == 0) {
-            S.ck_snap[v] = S.checksum[v];
-            S.inc_snap[v] = S.inc[row + v];
+            S.ck_snap[lv] = S.checksum[lv];
+            S.inc_snap[lv] = S.inc[row + v];
         }
-        // three issueAsSender() calls; records carry the count after the first one (aux)
-        const uint32_t maxp = S.max_piggy[v];
-        const uint32_t nc = S.n_chg[v];
-        Change* chg = S.chg + (uint64_t)v * S.Cd;
-        Rec* leg = leg_slot(S, v);
-        uint32_t written2 = 0, kept = 0;
+        // three issueAsSender() calls; records carry the count after the first one (aux); leg k
+        // carries the records whose count after the first issue + k <= maxPiggybackCount
+        const uint32_t maxp = S.max_piggy[lv];
+        const uint32_t nc = S.n_chg[lv];
+        Change* chg = S.chg + (uint64_t)lv * S.Cd;
+        Rec* leg = leg_slot(S, lv);
+        uint32_t written2 = 0, kept = 0, nk1 = 0, nk2 = 0;
         for (uint32_t base = 0; base < nc; base += kT) {
             const uint32_t j = base + threadIdx.x;
             bool emit = false, keep = false;
@@ -953,6 +1007,8 @@ __global__ __launch_bounds__(kT) void k_phase_d1(SimDev S) {
                     }
                 }
             }
+            nk1 += (emit && c1 + 1 <= maxp) ? 1u : 0u;
+            nk2 += (emit && c1 + 2 <= maxp) ? 1u : 0u;
             uint32_t ktot, etot;
             const uint32_t kpos = block_scan(keep ? 1u : 0u, L.u, &ktot);
             const uint32_t p = block_scan(emit ? 1u : 0u, L.u, &etot);
@@ -971,67 +1027,35 @@ __global__ __launch_bounds__(kT) void k_phase_d1(SimDev S) {
             kept += ktot;
             __syncthreads();
         }
+        const uint32_t t1 = block_sum(nk1, L.u), t2 = block_sum(nk2, L.u);
         if (threadIdx.x == 0) {
-            S.leg_n[v] = written2;
-            S.n_chg[v] = kept;
+            S.leg_n[lv] = written2;
+            S.leg_nk[lv * 3 + 0] = written2;
+            S.leg_nk[lv * 3 + 1] = t1;
+            S.leg_nk[lv * 3 + 2] = t2;
+            S.n_chg[lv] = kept;
         }
         __syncthreads();
     }
 }
 
-// D2: helpers handle ping-req legs in (sender, leg) order (ping-req.js:26-68)
+// D2: local helpers handle their ping-req legs in (sender, leg) order (ping-req.js:26-68). The
+// legs to dead helpers were never sent (the sender sees a network error).
 __global__ __launch_bounds__(kT) void k_phase_d2(SimDev S) {
     __shared__ Lds L;
     const int64_t now = S.now0 + 200 * S.round;
-    for (uint32_t h = blockIdx.x; h < S.N; h += gridDim.x) {
-        const uint32_t b = S.h_off[h], e = S.h_off[h + 1];
+    for (uint32_t lh = blockIdx.x; lh < S.NL; lh += gridDim.x) {
+        const uint32_t b = S.ib_off[lh], e = S.ib_off[lh + 1];
         for (uint32_t q = b; q < e; q++) {
-            const uint32_t code = S.h_src[q];
-            const uint32_t v = code / 3, k = code % 3;
-            if (S.dead[h]) {
-                if (threadIdx.x == 0) S.lresp_n[code] = NONE;  // network error
-                continue;
-            }
-            // leg k carries the records whose count after the first issue + k <= maxPiggy
-            const uint32_t maxp = S.max_piggy[v];
-            const uint32_t nleg = S.leg_n[v];
-            const Rec* leg = leg_slot(S, v);
-            const uint64_t so = block_alloc(S, nleg, &L.u64);
-            if (so == ~0ull) {  // arena overflow: reported by rp_sim_step; answer as a network error
-                if (threadIdx.x == 0) S.lresp_n[code] = NONE;
-                __syncthreads();
-                continue;
-            }
-            Rec* stage = S.pool + so;
-            uint32_t written = 0;
-            for (uint32_t base = 0; base < nleg; base += kT) {
-                const uint32_t i = base + threadIdx.x;
-                bool ok = false;
-                Rec r{};
-                if (i < nleg) {
-                    r = leg[i];
-                    ok = rec_aux(r) + k <= maxp;
-                }
-                uint32_t tot;
-                const uint32_t p = block_scan(ok ? 1u : 0u, L.u, &tot);
-                if (ok) stage[written + p] = r;
-                written += tot;
-            }
-            __threadfence_block();
-            __syncthreads();
-            block_apply(S, h, stage, written, L, now);
-            block_issue(S, h, NONE, 0, nullptr, L);  // the helper's own ping of the dead target
-            const uint64_t ro = block_alloc(S, S.n_chg[h], &L.u64);
-            if (ro == ~0ull) {
-                if (threadIdx.x == 0) S.lresp_n[code] = NONE;
-                __syncthreads();
-                continue;
-            }
-            uint64_t o;
-            const uint32_t n = block_issue_receiver(S, h, v, S.inc_snap[v], S.ck_snap[v], ro, &o, L);
+            const uint32_t i = S.ib_idx[q];
+            const Msg m = S.in_msg[i];
+            block_apply(S, lh, S.in_rec + m.roff, m.n, L, now);
+            block_issue(S, lh, NONE, 0, nullptr, L);  // the helper's own ping of the dead target
+            uint64_t o = 0;
+            const uint32_t n = block_issue_receiver(S, lh, m.from, m.inc, m.ck, &o, L);
             if (threadIdx.x == 0) {
-                S.lresp_n[code] = n;
-                S.lresp_off[code] = o;
+                S.rsp_n[i] = n;
+                S.rsp_off[i] = o;
             }
             __syncthreads();
         }
@@ -1043,21 +1067,22 @@ __global__ __launch_bounds__(kT) void k_phase_d3(SimDev S) {
     __shared__ Lds L;
     __shared__ Rec tmp;
     const int64_t now = S.now0 + 200 * S.round;
-    for (uint32_t v = blockIdx.x; v < S.N; v += gridDim.x) {
-        const uint32_t nh = S.nhelp[v];
-        if (S.dead[v] || nh == 0) continue;
-        const uint64_t row = (uint64_t)v * S.N;
+    for (uint32_t lv = blockIdx.x; lv < S.NL; lv += gridDim.x) {
+        const uint32_t nh = S.nhelp[lv];
+        if (S.dead[S.v0 + lv] || nh == 0) continue;
+        const uint64_t row = (uint64_t)lv * S.N;
         bool bad = false;
         for (uint32_t k = 0; k < nh; k++) {
-            const uint32_t code = v * 3 + k;
-            const uint32_t n = S.lresp_n[code];
-            if (n == NONE) continue;
-            block_apply(S, v, S.pool + S.lresp_off[code], n, L, now);
+            const uint32_t i = S.lresp_idx[lv * 3 + k];
+            if (i == NONE) continue;  // dead helper: network error
+            const Msg m = S.in_msg[i];
+            if (m.n == NONE) continue;
+            block_apply(S, lv, S.in_rec + m.roff, m.n, L, now);
             bad = true;
         }
         if (bad) {
-            const uint32_t t = (uint32_t)S.target[v];
-            block_make(S, v, t, ST_SUSPECT, S.inc[row + t], L, now, &tmp);
+            const uint32_t t = (uint32_t)S.target[lv];
+            block_make(S, lv, t, ST_SUSPECT, S.inc[row + t], L, now, &tmp);
         }
     }
 }
@@ -1069,13 +1094,14 @@ __global__ __launch_bounds__(kT) void k_phase_d3(SimDev S) {
 __global__ __launch_bounds__(kT) void k_phase_e(SimDev S) {
     __shared__ Lds L;
     const int64_t now = S.now0 + 200 * S.round;
-    for (uint32_t v = blockIdx.x; v < S.N; v += gridDim.x) {
+    for (uint32_t lv = blockIdx.x; lv < S.NL; lv += gridDim.x) {
+        const uint32_t v = S.v0 + lv;
         if (S.dead[v]) continue;
-        const uint64_t row = (uint64_t)v * S.N;
+        const uint64_t row = (uint64_t)lv * S.N;
         const int64_t srci = S.inc[row + v];
-        Rec* stage = ping_slot(S, v);  // free after phase B
-        Timer* tim = S.tim + (uint64_t)v * S.Ct;
-        const uint32_t nt = S.n_tim[v];
+        Rec* stage = ping_slot(S, lv);  // free: the ping left in the exchange after phase A
+        Timer* tim = S.tim + (uint64_t)lv * S.Ct;
+        const uint32_t nt = S.n_tim[lv];
         uint32_t written = 0, kept = 0;
         for (uint32_t base = 0; base < nt; base += kT) {
             const uint32_t i = base + threadIdx.x;
@@ -1096,32 +1122,137 @@ __global__ __launch_bounds__(kT) void k_phase_e(SimDev S) {
             written += ftot;
             __syncthreads();
         }
-        if (threadIdx.x == 0) S.n_tim[v] = kept;
+        if (threadIdx.x == 0) S.n_tim[lv] = kept;
         __threadfence_block();
         __syncthreads();
         if (written > S.Cm) {
             if (threadIdx.x == 0) set_err(S, ERR_TIMERS);
             written = S.Cm;
         }
-        if (written) block_apply(S, v, stage, written, L, now);
+        if (written) block_apply(S, lv, stage, written, L, now);
     }
 }
 
-__global__ void k_sim_keys(const int32_t* __restrict__ target, const uint8_t* __restrict__ dead, uint32_t N,
-                           uint32_t* __restrict__ key, uint32_t* __restrict__ val) {
-    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < N; v += gridDim.x * blockDim.x) {
-        const int32_t t = target[v];
-        key[v] = (dead[v] || t < 0) ? NONE : (uint32_t)t;
-        val[v] = v;
-    }
-}
+// ---- outboxes: messages grouped by destination shard
 
-__global__ void k_help_keys(const uint32_t* __restrict__ helpers, const uint32_t* __restrict__ nhelp, uint32_t N,
-                            uint32_t* __restrict__ key, uint32_t* __restrict__ val) {
-    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < 3 * N; c += gridDim.x * blockDim.x) {
-        const uint32_t v = c / 3, k = c % 3;
-        key[c] = k < nhelp[v] ? helpers[c] : NONE;
+// Candidate c of a message kind: its destination shard (G = none) and the sort value c.
+//   K_PING  c = local sender        -> shard of its live target
+//   K_LEG   c = local sender * 3 + k -> shard of helper k (live helpers only)
+//   K_RESP / K_LRESP c = inbound message (receive order) -> shard of its sender
+__global__ void k_out_keys(SimDev S, int kind, uint32_t C, uint32_t* __restrict__ key, uint32_t* __restrict__ val) {
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+        uint32_t k = S.G;
+        if (kind == K_PING) {
+            const int32_t t = S.target[c];
+            if (!S.dead[S.v0 + c] && t >= 0 && !S.dead[t]) k = shard_of(S, (uint32_t)t);
+        } else if (kind == K_LEG) {
+            const uint32_t lv = c / 3, j = c % 3;
+            if (j < S.nhelp[lv] && !S.dead[S.helpers[c]]) k = shard_of(S, S.helpers[c]);
+        } else {
+            k = shard_of(S, S.in_msg[c].from);
+        }
+        key[c] = k;
         val[c] = c;
+    }
+}
+
+__device__ __forceinline__ uint32_t out_count(const SimDev& S, int kind, uint32_t c) {
+    if (kind == K_PING) return S.ping_n[c];
+    if (kind == K_LEG) return S.leg_nk[c];
+    const uint32_t n = S.rsp_n[c];
+    return n == NONE ? 0u : n;
+}
+
+// records of each sorted message (0 past the last real one)
+__global__ void k_out_counts(SimDev S, int kind, const uint32_t* __restrict__ key, const uint32_t* __restrict__ val,
+                             uint32_t C, uint32_t* __restrict__ cnt) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < C; i += gridDim.x * blockDim.x)
+        cnt[i] = key[i] < S.G ? out_count(S, kind, val[i]) : 0u;
+}
+
+// one workgroup per message: header + records (leg records filtered by the leg's count rule)
+__global__ __launch_bounds__(kT) void k_out_fill(SimDev S, int kind, const uint32_t* __restrict__ key,
+                                                 const uint32_t* __restrict__ val, uint32_t nmsg,
+                                                 const uint32_t* __restrict__ roff, const uint32_t* __restrict__ moff,
+                                                 Msg* __restrict__ out_msg, Rec* __restrict__ out_rec) {
+    __shared__ uint32_t lds[16];
+    for (uint32_t i = blockIdx.x; i < nmsg; i += gridDim.x) {
+        const uint32_t c = val[i], d = key[i];
+        const uint64_t r0 = roff[i], dbase = roff[moff[d]];
+        Msg m{};
+        const Rec* src = nullptr;
+        uint32_t nsrc = 0, k = 0, maxp = 0;
+        if (kind == K_PING) {
+            m = Msg{S.v0 + c, (uint32_t)S.target[c], S.ping_n[c], 0u, S.ck_snap[c], 0u, S.inc_snap[c], r0 - dbase};
+            src = ping_slot(S, c);
+            nsrc = m.n;
+        } else if (kind == K_LEG) {
+            const uint32_t lv = c / 3;
+            k = c % 3;
+            m = Msg{S.v0 + lv, S.helpers[c], S.leg_nk[c], k, S.ck_snap[lv], 0u, S.inc_snap[lv], r0 - dbase};
+            src = leg_slot(S, lv);
+            nsrc = S.leg_n[lv];
+            maxp = S.max_piggy[lv];
+        } else {
+            const Msg q = S.in_msg[c];
+            m = Msg{q.to, q.from, S.rsp_n[c], q.tag, 0u, 0u, 0, r0 - dbase};
+            src = S.pool + S.rsp_off[c];
+            nsrc = m.n == NONE ? 0u : m.n;
+        }
+        if (threadIdx.x == 0) out_msg[i] = m;
+        Rec* dst = out_rec + r0;
+        if (kind != K_LEG || k == 0) {
+            for (uint32_t j = threadIdx.x; j < nsrc; j += kT) dst[j] = src[j];
+        } else {
+            uint32_t w = 0;
+            for (uint32_t base = 0; base < nsrc; base += kT) {
+                const uint32_t j = base + threadIdx.x;
+                Rec r{};
+                bool ok = false;
+                if (j < nsrc) {
+                    r = src[j];
+                    ok = rec_aux(r) + k <= maxp;
+                }
+                uint32_t tot;
+                const uint32_t p = block_scan(ok ? 1u : 0u, lds, &tot);
+                if (ok) dst[w + p] = r;
+                w += tot;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---- inboxes
+
+// inbound record offsets: per-source segments -> one record area
+__global__ void k_in_fix(Msg* __restrict__ msg, uint32_t n, const uint64_t* __restrict__ mbase,
+                         const uint64_t* __restrict__ rbase, uint32_t G) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        uint32_t s = 0;
+        while (s + 1 < G && i >= mbase[s + 1]) s++;
+        msg[i].roff += rbase[s];
+    }
+}
+
+__global__ void k_in_keys(SimDev S, uint32_t* __restrict__ key, uint32_t* __restrict__ val) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < S.nin; i += gridDim.x * blockDim.x) {
+        key[i] = S.in_msg[i].to - S.v0;
+        val[i] = i;
+    }
+}
+
+__global__ void k_fill_none(uint32_t* p, uint32_t n) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = NONE;
+}
+
+// responses: the inbound message index of each local sender (K_RESP) or (sender, leg) (K_LRESP)
+__global__ void k_in_scatter(SimDev S, int kind) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < S.nin; i += gridDim.x * blockDim.x) {
+        const Msg m = S.in_msg[i];
+        const uint32_t lv = m.to - S.v0;
+        if (kind == K_RESP) S.resp_idx[lv] = i;
+        else S.lresp_idx[lv * 3 + m.tag] = i;
     }
 }
 
@@ -1137,45 +1268,52 @@ __global__ void k_csr(const uint32_t* __restrict__ keys, uint32_t n, uint32_t N,
     }
 }
 
-// convergence: every live checksum equal, every killed member faulty in every live view
-// (checksums are fresh: k_ck_lanes ran)
-__global__ void k_converged(SimDev S, uint32_t first_live, uint32_t* __restrict__ flag) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (uint64_t)S.N * S.N;
+// ---- convergence over this shard's live nodes: {live count, min checksum, max checksum,
+// killed members not faulty in some local live view}
+__global__ void k_conv_local(SimDev S, const uint32_t* __restrict__ killed, uint32_t nk, uint32_t* __restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (uint64_t)S.NL * nk;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t v = (uint32_t)(i / S.N), a = (uint32_t)(i % S.N);
-        if (S.dead[v]) continue;
-        if (S.dead[a] && (S.st[i] & ST_MASK) != ST_FAULTY) *flag = 0;
-        if (a == 0 && S.checksum[v] != S.checksum[first_live]) *flag = 0;
+        const uint32_t lv = (uint32_t)(i / nk), a = killed[i % nk];
+        if (S.dead[S.v0 + lv]) continue;
+        if ((S.st[(uint64_t)lv * S.N + a] & ST_MASK) != ST_FAULTY) out[3] = 1;
+    }
+    for (uint32_t lv = blockIdx.x * blockDim.x + threadIdx.x; lv < S.NL; lv += gridDim.x * blockDim.x) {
+        if (S.dead[S.v0 + lv]) continue;
+        atomicAdd(&out[0], 1u);
+        atomicMin(&out[1], S.checksum[lv]);
+        atomicMax(&out[2], S.checksum[lv]);
     }
 }
 
 __global__ void k_sim_init(SimDev S) {
-    const uint64_t NN = (uint64_t)S.N * S.N;
+    const uint64_t NN = (uint64_t)S.NL * S.N;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < NN; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t v = (uint32_t)(i / S.N), a = (uint32_t)(i % S.N);
+        const uint32_t v = S.v0 + (uint32_t)(i / S.N), a = (uint32_t)(i % S.N);
         S.st[i] = ST_ALIVE | IN_RING;
         S.inc[i] = S.inc0[a];
         S.slot[i] = 0;
         // members array after bootstrap: self first (makeAlive), then set() in id order
         S.order[i] = a == 0 ? v : (a <= v ? a - 1 : a);
     }
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (uint64_t)S.N * S.W;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (uint64_t)S.NL * S.W;
          i += (uint64_t)gridDim.x * blockDim.x)
         S.dev[i] = 0;
-    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < S.N; v += gridDim.x * blockDim.x) {
-        S.it_idx[v] = -1;
-        S.n_shuf[v] = 0;
-        S.ring_count[v] = S.N;
-        S.max_piggy[v] = 15u * digits(S.N);
-        S.dirty[v] = 1;  // first checksum by k_ck_lanes
-        S.n_chg[v] = 0;
-        S.n_tim[v] = 0;
+    for (uint32_t lv = blockIdx.x * blockDim.x + threadIdx.x; lv < S.NL; lv += gridDim.x * blockDim.x) {
+        S.it_idx[lv] = -1;
+        S.n_shuf[lv] = 0;
+        S.ring_count[lv] = S.N;
+        S.max_piggy[lv] = 15u * digits(S.N);
+        S.dirty[lv] = 1;  // first checksum by k_ck_lanes
+        S.n_chg[lv] = 0;
+        S.n_tim[lv] = 0;
+        S.target[lv] = -1;
+        S.nhelp[lv] = 0;
     }
 }
 
 __global__ void k_sim_start(SimDev S) {  // gossip.start -> membership.shuffle() on live nodes
-    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < S.N; v += gridDim.x * blockDim.x)
-        if (!S.dead[v]) lane0_shuffle(S, v);
+    for (uint32_t lv = blockIdx.x * blockDim.x + threadIdx.x; lv < S.NL; lv += gridDim.x * blockDim.x)
+        if (!S.dead[S.v0 + lv]) lane0_shuffle(S, lv);
 }
 
 // every node starts with the same view: hash it once, copy to all
@@ -1184,18 +1322,34 @@ __global__ void k_sim_first_checksum(SimDev S) {
 }
 
 __global__ void k_sim_bcast_checksum(SimDev S) {
-    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < S.N; v += gridDim.x * blockDim.x) {
-        S.checksum[v] = S.checksum[0];
-        S.dirty[v] = 0;
+    for (uint32_t lv = blockIdx.x * blockDim.x + threadIdx.x; lv < S.NL; lv += gridDim.x * blockDim.x) {
+        S.checksum[lv] = S.checksum[0];
+        S.dirty[lv] = 0;
     }
 }
 
 }  // namespace
 
+// Exchange buffers: headers + records, grouped by peer shard. nmsg/nrec[G] per peer.
+struct MsgBuf {
+    DevBuf<Msg> msg;
+    DevBuf<Rec> rec;
+    std::vector<uint64_t> nmsg, nrec;
+    uint64_t tot_msg = 0, tot_rec = 0;
+    void swap(MsgBuf& o) {
+        msg.swap(o.msg);
+        rec.swap(o.rec);
+        std::swap(nmsg, o.nmsg);
+        std::swap(nrec, o.nrec);
+        std::swap(tot_msg, o.tot_msg);
+        std::swap(tot_rec, o.tot_rec);
+    }
+};
+
 struct Sim {
     int device = 0;
     hipStream_t st = nullptr;
-    uint32_t N = 0;
+    uint32_t N = 0, NL = 0, v0 = 0, G = 1, shard = 0;
     unsigned grid = 0;
     NameTable nt;
     SimDev d{};
@@ -1203,53 +1357,191 @@ struct Sim {
     DevBuf<int64_t> inc, it_idx, inc_snap, inc0;
     DevBuf<int32_t> target;
     DevBuf<uint16_t> slot;
-    DevBuf<uint32_t> order, dev, n_chg, n_tim, n_shuf, ring_count, max_piggy, checksum, ck_snap, ping_n, resp_n,
-        leg_n, helpers, nhelp, lresp_n, cand, in_off, in_src, h_off, h_src, keys, conv, rank, err;
-    DevBuf<uint64_t> boff, resp_off, lresp_off;
+    DevBuf<uint32_t> order, dev, n_chg, n_tim, n_shuf, ring_count, max_piggy, checksum, ck_snap, ping_n, leg_n,
+        helpers, nhelp, leg_nk, cand, rank, err, bounds, killed, conv;
+    DevBuf<uint32_t> okey, oval, ocnt, ooff, omoff;  // outbox build
+    DevBuf<uint32_t> ib_off, ib_idx, ikey;         // inbox build
+    DevBuf<uint32_t> rsp_n, resp_idx, lresp_idx;
+    DevBuf<uint64_t> boff, rsp_off, ibase;
     DevBuf<Change> chg;
     DevBuf<Timer> tim;
     DevBuf<Rec> pool;
     DevBuf<unsigned long long> stats, cursor;
+    MsgBuf out, in;
     Scratch ws;
     std::vector<uint8_t> h_dead;
-    uint32_t first_live = 0;
+    std::vector<uint32_t> h_bounds;
+    uint32_t nkilled = 0;
     int64_t round = 0;
+    int next_stage = 0;  // 0..4 within a round
 
-    void build_inboxes() {
-        const uint32_t n = N;
-        hipLaunchKernelGGL(k_sim_keys, dim3(grid_for(n, 256)), dim3(256), 0, st, target.p, dead.p, n, keys.p, in_src.p);
-        radix_sort_pairs(keys.p, in_src.p, n, 0, 32, st, ws);
-        hipLaunchKernelGGL(k_csr, dim3(grid_for(n + 1, 256)), dim3(256), 0, st, keys.p, n, n, in_off.p);
-        RP_HIP(hipGetLastError());
-    }
-    void build_helper_inboxes() {
-        const uint32_t n = 3 * N;
-        hipLaunchKernelGGL(k_help_keys, dim3(grid_for(n, 256)), dim3(256), 0, st, helpers.p, nhelp.p, N, keys.p,
-                           h_src.p);
-        radix_sort_pairs(keys.p, h_src.p, n, 0, 32, st, ws);
-        hipLaunchKernelGGL(k_csr, dim3(grid_for(N + 1, 256)), dim3(256), 0, st, keys.p, n, N, h_off.p);
-        RP_HIP(hipGetLastError());
-    }
     void refresh_checksums() {
-        hipLaunchKernelGGL(k_ck_lanes, dim3(grid_for(N, 256, 1u << 20)), dim3(256), 0, st, d);
+        if (NL == 0) return;
+        hipLaunchKernelGGL(k_ck_lanes, dim3(grid_for(NL, 256, 1u << 20)), dim3(256), 0, st, d);
         RP_HIP(hipGetLastError());
     }
-    void step() {
+
+    // Outbox of a message kind: sort candidates by destination shard (stable), scan the record
+    // counts, fill headers + records. Leaves out.nmsg/nrec per destination.
+    void build_out(int kind) {
+        const uint32_t C = kind == K_PING ? NL : kind == K_LEG ? 3 * NL : (uint32_t)in.tot_msg;
+        out.nmsg.assign(G, 0);
+        out.nrec.assign(G, 0);
+        out.tot_msg = out.tot_rec = 0;
+        if (C == 0) return;
+        okey.reserve(C + 1);
+        oval.reserve(C + 1);
+        ocnt.reserve(C + 1);
+        ooff.reserve(C + 1);
+        omoff.reserve(G + 1);
+        hipLaunchKernelGGL(k_out_keys, dim3(grid_for(C, 256)), dim3(256), 0, st, d, kind, C, okey.p, oval.p);
+        if (kind == K_PING || kind == K_LEG) radix_sort_pairs(okey.p, oval.p, C, 0, 8, st, ws);
+        hipLaunchKernelGGL(k_out_counts, dim3(grid_for(C, 256)), dim3(256), 0, st, d, kind, okey.p, oval.p, C, ocnt.p);
+        scan_exclusive_u32(ocnt.p, ooff.p, C, st, ws);
+        hipLaunchKernelGGL(k_csr, dim3(1), dim3(128), 0, st, okey.p, C, G, omoff.p);
+        RP_HIP(hipGetLastError());
+        std::vector<uint32_t> moff(G + 1);
+        RP_HIP(hipMemcpyAsync(moff.data(), omoff.p, 4ull * (G + 1), hipMemcpyDeviceToHost, st));
+        RP_HIP(hipStreamSynchronize(st));
+        std::vector<uint32_t> roff(G + 1);
+        for (uint32_t g = 0; g <= G; g++)
+            RP_HIP(hipMemcpyAsync(&roff[g], ooff.p + moff[g], 4, hipMemcpyDeviceToHost, st));
+        RP_HIP(hipStreamSynchronize(st));
+        out.tot_msg = moff[G];
+        out.tot_rec = roff[G];
+        for (uint32_t g = 0; g < G; g++) {
+            out.nmsg[g] = moff[g + 1] - moff[g];
+            out.nrec[g] = roff[g + 1] - roff[g];
+        }
+        out.msg.reserve(out.tot_msg + 1);
+        out.rec.reserve(out.tot_rec + 1);
+        if (out.tot_msg)
+            hipLaunchKernelGGL(k_out_fill, dim3(grid_for(out.tot_msg, 1, 4096)), dim3(kT), 0, st, d, kind, okey.p,
+                               oval.p, (uint32_t)out.tot_msg, ooff.p, omoff.p, out.msg.p, out.rec.p);
+        RP_HIP(hipGetLastError());
+    }
+
+    // Size the inbox for per-source counts (the caller then fills in.msg / in.rec).
+    void prepare_in(const uint64_t* nmsg, const uint64_t* nrec) {
+        in.nmsg.assign(nmsg, nmsg + G);
+        in.nrec.assign(nrec, nrec + G);
+        in.tot_msg = in.tot_rec = 0;
+        for (uint32_t g = 0; g < G; g++) {
+            in.tot_msg += nmsg[g];
+            in.tot_rec += nrec[g];
+        }
+        RP_REQUIRE(in.tot_msg < (1ull << 32), "sim: too many inbound messages");
+        in.msg.reserve(in.tot_msg + 1);
+        in.rec.reserve(in.tot_rec + 1);
+    }
+
+    // One shard: the outbox is the inbox.
+    void self_exchange() {
+        std::vector<uint64_t> nm = out.nmsg, nr = out.nrec;
+        in.swap(out);
+        in.nmsg = nm;
+        in.nrec = nr;
+    }
+
+    // Bind the inbox to the device view: rebase record offsets per source, then index it.
+    void import_in(int kind) {
+        d.in_msg = in.msg.p;
+        d.in_rec = in.rec.p;
+        d.nin = (uint32_t)in.tot_msg;
+        if (G > 1 && in.tot_msg) {
+            std::vector<uint64_t> base(2 * G);
+            uint64_t m = 0, r = 0;
+            for (uint32_t g = 0; g < G; g++) {
+                base[g] = m;
+                base[G + g] = r;
+                m += in.nmsg[g];
+                r += in.nrec[g];
+            }
+            ibase.reserve(2 * G);
+            RP_HIP(hipMemcpyAsync(ibase.p, base.data(), 16ull * G, hipMemcpyHostToDevice, st));
+            hipLaunchKernelGGL(k_in_fix, dim3(grid_for(in.tot_msg, 256)), dim3(256), 0, st, in.msg.p,
+                               (uint32_t)in.tot_msg, ibase.p, ibase.p + G, G);
+        }
+        const uint32_t n = (uint32_t)in.tot_msg;
+        if (kind == K_PING || kind == K_LEG) {
+            ikey.reserve(n + 1);
+            ib_idx.reserve(n + 1);
+            ib_off.reserve(NL + 1);
+            rsp_n.reserve(n + 1);
+            rsp_off.reserve(n + 1);
+            if (n) {
+                hipLaunchKernelGGL(k_in_keys, dim3(grid_for(n, 256)), dim3(256), 0, st, d, ikey.p, ib_idx.p);
+                int bits = 8;
+                while (bits < 32 && (1ull << bits) <= NL) bits += 8;
+                radix_sort_pairs(ikey.p, ib_idx.p, n, 0, bits, st, ws);
+            }
+            hipLaunchKernelGGL(k_csr, dim3(grid_for(NL + 1, 256)), dim3(256), 0, st, ikey.p, n, NL, ib_off.p);
+            d.ib_off = ib_off.p;
+            d.ib_idx = ib_idx.p;
+            d.rsp_n = rsp_n.p;
+            d.rsp_off = rsp_off.p;
+        } else {
+            uint32_t* idx = kind == K_RESP ? resp_idx.p : lresp_idx.p;
+            const uint32_t cnt = kind == K_RESP ? NL : 3 * NL;
+            hipLaunchKernelGGL(k_fill_none, dim3(grid_for(cnt, 256)), dim3(256), 0, st, idx, cnt);
+            if (n) hipLaunchKernelGGL(k_in_scatter, dim3(grid_for(n, 256)), dim3(256), 0, st, d, kind);
+        }
+        RP_HIP(hipGetLastError());
+    }
+
+    // Stage k of a round. 0: checksums + A -> pings out. 1: pings in, B -> responses out.
+    // 2: responses in, C, D1 -> legs out. 3: legs in, D2 -> leg responses out.
+    // 4: leg responses in, D3, E; the round ends.
+    void stage(int k) {
+        RP_REQUIRE(k == next_stage, "sim: stages must run in order 0..4");
         d.round = round;
-        hipLaunchKernelGGL(k_round_begin, dim3(1), dim3(64), 0, st, d);
-        refresh_checksums();
-        hipLaunchKernelGGL(k_phase_a, dim3(grid), dim3(kT), 0, st, d);
-        build_inboxes();
-        hipLaunchKernelGGL(k_phase_b, dim3(grid), dim3(kT), 0, st, d);
-        hipLaunchKernelGGL(k_phase_c, dim3(grid), dim3(kT), 0, st, d);
-        hipLaunchKernelGGL(k_phase_d1, dim3(grid), dim3(kT), 0, st, d);
-        build_helper_inboxes();
-        hipLaunchKernelGGL(k_phase_d2, dim3(grid), dim3(kT), 0, st, d);
-        hipLaunchKernelGGL(k_phase_d3, dim3(grid), dim3(kT), 0, st, d);
-        hipLaunchKernelGGL(k_phase_e, dim3(grid), dim3(kT), 0, st, d);
+        const unsigned g = grid;
+        switch (k) {
+        case 0:
+            hipLaunchKernelGGL(k_round_begin, dim3(1), dim3(64), 0, st, d);
+            refresh_checksums();
+            if (NL) hipLaunchKernelGGL(k_phase_a, dim3(g), dim3(kT), 0, st, d);
+            build_out(K_PING);
+            break;
+        case 1:
+            import_in(K_PING);
+            if (NL) hipLaunchKernelGGL(k_phase_b, dim3(g), dim3(kT), 0, st, d);
+            build_out(K_RESP);
+            break;
+        case 2:
+            import_in(K_RESP);
+            if (NL) {
+                hipLaunchKernelGGL(k_phase_c, dim3(g), dim3(kT), 0, st, d);
+                hipLaunchKernelGGL(k_phase_d1, dim3(g), dim3(kT), 0, st, d);
+            }
+            build_out(K_LEG);
+            break;
+        case 3:
+            import_in(K_LEG);
+            if (NL) hipLaunchKernelGGL(k_phase_d2, dim3(g), dim3(kT), 0, st, d);
+            build_out(K_LRESP);
+            break;
+        case 4:
+            import_in(K_LRESP);
+            if (NL) {
+                hipLaunchKernelGGL(k_phase_d3, dim3(g), dim3(kT), 0, st, d);
+                hipLaunchKernelGGL(k_phase_e, dim3(g), dim3(kT), 0, st, d);
+            }
+            round++;
+            break;
+        }
         RP_HIP(hipGetLastError());
-        round++;
+        next_stage = (k + 1) % 5;
     }
+
+    void step() {  // one shard: a whole round
+        RP_REQUIRE(G == 1, "sim: a sharded handle advances through rp_sim_stage + an exchange");
+        for (int k = 0; k < 5; k++) {
+            stage(k);
+            if (k < 4) self_exchange();
+        }
+    }
+
     void check_err() {
         uint32_t e = 0;
         RP_HIP(hipMemcpyAsync(&e, err.p, 4, hipMemcpyDeviceToHost, st));
@@ -1258,6 +1550,19 @@ struct Sim {
             throw Error(RP_ESTATE, "sim: a node's dissemination list exceeded its capacity (RP_SIM_CAP)");
         if (e & ERR_TIMERS) throw Error(RP_ESTATE, "sim: a node's suspicion timers exceeded their capacity (RP_SIM_CAP)");
         if (e & ERR_ARENA) throw Error(RP_ESTATE, "sim: the per-round message arena overflowed (RP_SIM_ARENA)");
+    }
+
+    // {live, min checksum, max checksum, some killed member not faulty in a live view}
+    void conv_local(uint32_t* out4) {
+        refresh_checksums();
+        const uint32_t init[4] = {0u, 0xFFFFFFFFu, 0u, 0u};
+        RP_HIP(hipMemcpyAsync(conv.p, init, sizeof init, hipMemcpyHostToDevice, st));
+        if (NL)
+            hipLaunchKernelGGL(k_conv_local, dim3(grid_for((uint64_t)NL * std::max(nkilled, 1u), 256, 8192)), dim3(256),
+                               0, st, d, killed.p, nkilled, conv.p);
+        RP_HIP(hipGetLastError());
+        RP_HIP(hipMemcpyAsync(out4, conv.p, 16, hipMemcpyDeviceToHost, st));
+        RP_HIP(hipStreamSynchronize(st));
     }
 };
 
@@ -1283,135 +1588,170 @@ static uint64_t env_u64(const char* name, uint64_t dflt) {
     return strtoull(s, nullptr, 10);
 }
 
+static void sim_create(uint32_t n, const char* names, const uint32_t* off, const int64_t* inc0, const uint8_t* dead,
+                       uint32_t seed, uint32_t suspicion_rounds, int64_t now0, int device, const uint32_t* bounds,
+                       uint32_t nshards, uint32_t shard, rp_sim** out) {
+    RP_REQUIRE(out && n >= 2 && names && off && inc0 && dead, "sim_create: bad arguments");
+    RP_REQUIRE(n < (1u << 23), "sim_create: at most 2^23 members");
+    RP_REQUIRE(nshards >= 1 && nshards <= rp::kMaxShards && shard < nshards, "sim_create: bad shard");
+    std::vector<uint32_t> bnd(nshards + 1);
+    if (bounds) {
+        bnd.assign(bounds, bounds + nshards + 1);
+    } else {
+        for (uint32_t g = 0; g <= nshards; g++) bnd[g] = (uint32_t)((uint64_t)n * g / nshards);
+    }
+    RP_REQUIRE(bnd[0] == 0 && bnd[nshards] == n, "sim_create: shard bounds must cover [0, n)");
+    for (uint32_t g = 0; g < nshards; g++) RP_REQUIRE(bnd[g] <= bnd[g + 1], "sim_create: shard bounds must be sorted");
+    int nd = 0;
+    RP_HIP(hipGetDeviceCount(&nd));
+    RP_REQUIRE(device >= 0 && device < nd, "no such HIP device");
+    RP_HIP(hipSetDevice(device));
+    auto* h = new rp_sim();
+    rp::Sim& S = h->impl;
+    S.device = device;
+    S.N = n;
+    S.G = nshards;
+    S.shard = shard;
+    S.v0 = bnd[shard];
+    S.NL = bnd[shard + 1] - bnd[shard];
+    S.h_bounds = bnd;
+    if (hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        throw rp::Error(rp::RP_EDEVICE, "hipStreamCreate failed");
+    }
+    try {
+        const uint32_t NL = S.NL, v0 = S.v0;
+        for (uint32_t i = 0; i < n; i++) {
+            const uint32_t id = S.nt.intern(names + off[i], off[i + 1] - off[i]);
+            RP_REQUIRE(id == i, "sim_create: member addresses must be distinct");
+        }
+        S.nt.sort(S.st, S.ws);
+        // address order on the host: the all-alive base checksum string and its piece offsets
+        std::vector<uint32_t> sorted(n), rank(n);
+        RP_HIP(hipMemcpyAsync(sorted.data(), S.nt.sorted.p, 4ull * n, hipMemcpyDeviceToHost, S.st));
+        RP_HIP(hipStreamSynchronize(S.st));
+        std::vector<uint8_t> base;
+        std::vector<uint64_t> boff(n + 1ull);
+        base.reserve(S.nt.h_bytes.size() + 20ull * n + 64);
+        for (uint32_t k = 0; k < n; k++) {
+            const uint32_t a = sorted[k];
+            rank[a] = k;
+            boff[k] = base.size();
+            base.insert(base.end(), S.nt.h_bytes.begin() + (long)S.nt.h_noff[a],
+                        S.nt.h_bytes.begin() + (long)S.nt.h_noff[a + 1]);
+            const char* alive = "alive";
+            base.insert(base.end(), alive, alive + 5);
+            uint8_t dig[24];
+            const uint32_t dl = rp::dec_len(inc0[a]);
+            rp::dec_write(inc0[a], dig, dl);
+            base.insert(base.end(), dig, dig + dl);
+            if (k + 1 < n) base.push_back(';');
+        }
+        boff[n] = base.size();
+        base.resize(base.size() + 64, 0);  // the lane chain reads up to 24 bytes past a chunk
+
+        const uint64_t NN = (uint64_t)NL * n;
+        std::vector<uint32_t> killed;
+        for (uint32_t i = 0; i < n; i++)
+            if (dead[i]) killed.push_back(i);
+        const uint32_t ndead = (uint32_t)killed.size();
+        S.nkilled = ndead;
+        // Capacities. In this model only killed members change state (only they are suspected;
+        // nobody refutes), so a node's changes and timers are bounded by the killed count.
+        const uint64_t cap = std::min<uint64_t>(n, env_u64("RP_SIM_CAP", 2ull * ndead + 256));
+        RP_REQUIRE(cap >= 1 && cap < 65535, "sim_create: RP_SIM_CAP must be in [1, 65534]");
+        S.grid = std::max<uint32_t>(1, std::min<uint32_t>(NL, 256u * 4u));
+        const uint32_t W = (n + 31) / 32;
+        // arena: the round's responses (B and D2 answers of up to cap records, +25 % for shards
+        // receiving more than their share of pings), full syncs and slack
+        const uint64_t arena = env_u64("RP_SIM_ARENA", (NL + NL / 4 + 256) * cap + 8ull * n + 4096);
+        const uint64_t L1 = NL ? NL : 1;
+        S.st_.reserve(NN + 1); S.inc.reserve(NN + 1); S.order.reserve(NN + 1); S.slot.reserve(NN + 1);
+        S.dev.reserve(L1 * W);
+        S.chg.reserve(L1 * cap); S.tim.reserve(L1 * cap);
+        S.n_chg.reserve(L1); S.n_tim.reserve(L1);
+        S.it_idx.reserve(L1); S.n_shuf.reserve(L1); S.ring_count.reserve(L1); S.max_piggy.reserve(L1);
+        S.checksum.reserve(L1); S.dirty.reserve(L1); S.dead.reserve(n); S.target.reserve(L1); S.ck_snap.reserve(L1);
+        S.inc_snap.reserve(L1); S.ping_n.reserve(L1); S.leg_n.reserve(L1);
+        S.helpers.reserve(3 * L1); S.nhelp.reserve(L1); S.leg_nk.reserve(3 * L1);
+        S.resp_idx.reserve(L1); S.lresp_idx.reserve(3 * L1);
+        S.ib_off.reserve(L1 + 1);
+        S.conv.reserve(4);
+        S.killed.reserve(ndead + 1);
+        S.bounds.reserve(nshards + 1);
+        S.pool.reserve(2 * L1 * cap + arena);
+        S.cand.reserve((uint64_t)S.grid * n);
+        // per-block string buffer: names + ';' + "suspect" + 20 digits per member (also the
+        // iterator's scratch)
+        const uint64_t strcap = std::max<uint64_t>(S.nt.h_bytes.size() + 29ull * n + 64, 5ull * n + 64);
+        S.strbuf.reserve((uint64_t)S.grid * ((strcap + 255) & ~255ull));
+        S.stats.reserve(4); S.cursor.reserve(1); S.err.reserve(1);
+        S.inc0.reserve(n); S.rank.reserve(n); S.boff.reserve(n + 1ull); S.sbase.reserve(base.size());
+        RP_HIP(hipMemcpyAsync(S.inc0.p, inc0, 8ull * n, hipMemcpyHostToDevice, S.st));
+        RP_HIP(hipMemcpyAsync(S.rank.p, rank.data(), 4ull * n, hipMemcpyHostToDevice, S.st));
+        RP_HIP(hipMemcpyAsync(S.boff.p, boff.data(), 8ull * (n + 1), hipMemcpyHostToDevice, S.st));
+        RP_HIP(hipMemcpyAsync(S.sbase.p, base.data(), base.size(), hipMemcpyHostToDevice, S.st));
+        RP_HIP(hipMemcpyAsync(S.bounds.p, bnd.data(), 4ull * (nshards + 1), hipMemcpyHostToDevice, S.st));
+        if (ndead) RP_HIP(hipMemcpyAsync(S.killed.p, killed.data(), 4ull * ndead, hipMemcpyHostToDevice, S.st));
+        S.h_dead.assign(dead, dead + n);
+        RP_HIP(hipMemcpyAsync(S.dead.p, S.h_dead.data(), n, hipMemcpyHostToDevice, S.st));
+        RP_HIP(hipMemsetAsync(S.stats.p, 0, 4 * sizeof(unsigned long long), S.st));
+        RP_HIP(hipMemsetAsync(S.err.p, 0, 4, S.st));
+        RP_HIP(hipMemsetAsync(S.cursor.p, 0, 8, S.st));
+        rp::SimDev& d = S.d;
+        d.N = n; d.W = W; d.v0 = v0; d.NL = NL; d.G = nshards; d.bounds = S.bounds.p;
+        d.seed = seed; d.susp = suspicion_rounds; d.now0 = now0;
+        d.Cd = (uint32_t)cap; d.Ct = (uint32_t)cap; d.Cm = (uint32_t)cap;
+        d.st = S.st_.p; d.inc = S.inc.p; d.order = S.order.p; d.slot = S.slot.p; d.dev = S.dev.p;
+        d.chg = S.chg.p; d.n_chg = S.n_chg.p; d.tim = S.tim.p; d.n_tim = S.n_tim.p;
+        d.it_idx = S.it_idx.p; d.n_shuf = S.n_shuf.p; d.ring_count = S.ring_count.p; d.max_piggy = S.max_piggy.p;
+        d.checksum = S.checksum.p; d.dirty = S.dirty.p; d.dead = S.dead.p;
+        d.sorted = S.nt.sorted.p; d.rank = S.rank.p; d.names = S.nt.d_bytes.p; d.noff = S.nt.d_noff.p;
+        d.sbase = S.sbase.p; d.boff = S.boff.p; d.inc0 = S.inc0.p;
+        d.target = S.target.p; d.ck_snap = S.ck_snap.p; d.inc_snap = S.inc_snap.p;
+        d.pool = S.pool.p; d.arena0 = 2ull * L1 * cap; d.arena_cap = arena; d.cursor = S.cursor.p;
+        d.ping_n = S.ping_n.p; d.leg_n = S.leg_n.p; d.helpers = S.helpers.p; d.nhelp = S.nhelp.p;
+        d.leg_nk = S.leg_nk.p; d.cand = S.cand.p;
+        d.strbuf = S.strbuf.p; d.strcap = (strcap + 255) & ~255ull;
+        d.resp_idx = S.resp_idx.p; d.lresp_idx = S.lresp_idx.p;
+        d.stats = S.stats.p; d.err = S.err.p; d.round = 0;
+        {
+            const void* ptrs[] = {d.st, d.inc, d.order, d.slot, d.dev, d.chg, d.n_chg, d.tim, d.n_tim, d.it_idx,
+                                  d.n_shuf, d.ring_count, d.max_piggy, d.checksum, d.dirty, d.dead, d.sorted,
+                                  d.rank, d.names, d.noff, d.sbase, d.boff, d.inc0, d.target, d.ck_snap,
+                                  d.inc_snap, d.pool, d.cursor, d.ping_n, d.leg_n, d.helpers, d.nhelp, d.leg_nk,
+                                  d.cand, d.strbuf, d.resp_idx, d.lresp_idx, d.stats, d.err, d.bounds};
+            for (const void* p : ptrs) RP_REQUIRE(p != nullptr, "sim_create: internal buffer not allocated");
+        }
+        hipLaunchKernelGGL(rp::k_sim_init, dim3(rp::grid_for(NN + 1, 256, 8192)), dim3(256), 0, S.st, d);
+        if (NL) {
+            hipLaunchKernelGGL(rp::k_sim_start, dim3(rp::grid_for(NL, 64)), dim3(64), 0, S.st, d);
+            hipLaunchKernelGGL(rp::k_sim_first_checksum, dim3(1), dim3(64), 0, S.st, d);
+            hipLaunchKernelGGL(rp::k_sim_bcast_checksum, dim3(rp::grid_for(NL, 256)), dim3(256), 0, S.st, d);
+        }
+        RP_HIP(hipGetLastError());
+        RP_HIP(hipStreamSynchronize(S.st));
+    } catch (...) {
+        (void)hipStreamSynchronize(S.st);
+        (void)hipStreamDestroy(S.st);
+        delete h;
+        throw;
+    }
+    *out = h;
+}
+
 extern "C" {
 
 int rp_sim_create(uint32_t n, const char* names, const uint32_t* off, const int64_t* inc0, const uint8_t* dead,
                   uint32_t seed, uint32_t suspicion_rounds, int64_t now0, int device, rp_sim** out) {
-    return guard([&] {
-        RP_REQUIRE(out && n >= 2 && names && off && inc0 && dead, "sim_create: bad arguments");
-        RP_REQUIRE(n < (1u << 23), "sim_create: at most 2^23 members");
-        int nd = 0;
-        RP_HIP(hipGetDeviceCount(&nd));
-        RP_REQUIRE(device >= 0 && device < nd, "no such HIP device");
-        RP_HIP(hipSetDevice(device));
-        auto* h = new rp_sim();
-        rp::Sim& S = h->impl;
-        S.device = device;
-        S.N = n;
-        if (hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking) != hipSuccess) {
-            delete h;
-            throw rp::Error(rp::RP_EDEVICE, "hipStreamCreate failed");
-        }
-        try {
-            for (uint32_t i = 0; i < n; i++) {
-                const uint32_t id = S.nt.intern(names + off[i], off[i + 1] - off[i]);
-                RP_REQUIRE(id == i, "sim_create: member addresses must be distinct");
-            }
-            S.nt.sort(S.st, S.ws);
-            // address order on the host: the all-alive base checksum string and its piece offsets
-            std::vector<uint32_t> sorted(n), rank(n);
-            RP_HIP(hipMemcpyAsync(sorted.data(), S.nt.sorted.p, 4ull * n, hipMemcpyDeviceToHost, S.st));
-            RP_HIP(hipStreamSynchronize(S.st));
-            std::vector<uint8_t> base;
-            std::vector<uint64_t> boff(n + 1ull);
-            base.reserve(S.nt.h_bytes.size() + 20ull * n + 64);
-            for (uint32_t k = 0; k < n; k++) {
-                const uint32_t a = sorted[k];
-                rank[a] = k;
-                boff[k] = base.size();
-                base.insert(base.end(), S.nt.h_bytes.begin() + (long)S.nt.h_noff[a],
-                            S.nt.h_bytes.begin() + (long)S.nt.h_noff[a + 1]);
-                const char* alive = "alive";
-                base.insert(base.end(), alive, alive + 5);
-                uint8_t dig[24];
-                const uint32_t dl = rp::dec_len(inc0[a]);
-                rp::dec_write(inc0[a], dig, dl);
-                base.insert(base.end(), dig, dig + dl);
-                if (k + 1 < n) base.push_back(';');
-            }
-            boff[n] = base.size();
-            base.resize(base.size() + 64, 0);  // the lane chain reads up to 24 bytes past a chunk
+    return guard([&] { sim_create(n, names, off, inc0, dead, seed, suspicion_rounds, now0, device, nullptr, 1, 0, out); });
+}
 
-            const uint64_t NN = (uint64_t)n * n;
-            uint32_t ndead = 0;
-            for (uint32_t i = 0; i < n; i++) ndead += dead[i] ? 1 : 0;
-            // Capacities. In this model only killed members change state (only they are suspected;
-            // nobody refutes), so a node's changes and timers are bounded by the killed count.
-            const uint64_t cap = std::min<uint64_t>(n, env_u64("RP_SIM_CAP", 2ull * ndead + 256));
-            RP_REQUIRE(cap >= 1 && cap < 65535, "sim_create: RP_SIM_CAP must be in [1, 65534]");
-            S.grid = std::min<uint32_t>(n, 256u * 4u);
-            const uint32_t W = (n + 31) / 32;
-            const uint64_t arena =
-                env_u64("RP_SIM_ARENA", 6ull * cap * (2ull * ndead + 64) + 32ull * n + 4096);
-            S.st_.reserve(NN); S.inc.reserve(NN); S.order.reserve(NN); S.slot.reserve(NN);
-            S.dev.reserve((uint64_t)n * W);
-            S.chg.reserve((uint64_t)n * cap); S.tim.reserve((uint64_t)n * cap);
-            S.n_chg.reserve(n); S.n_tim.reserve(n);
-            S.it_idx.reserve(n); S.n_shuf.reserve(n); S.ring_count.reserve(n); S.max_piggy.reserve(n);
-            S.checksum.reserve(n); S.dirty.reserve(n); S.dead.reserve(n); S.target.reserve(n); S.ck_snap.reserve(n);
-            S.inc_snap.reserve(n); S.ping_n.reserve(n); S.resp_n.reserve(n); S.leg_n.reserve(n);
-            S.resp_off.reserve(n); S.lresp_off.reserve(3ull * n);
-            S.helpers.reserve(3ull * n); S.nhelp.reserve(n); S.lresp_n.reserve(3ull * n);
-            S.in_off.reserve(n + 1ull); S.in_src.reserve(n + 1ull); S.h_off.reserve(n + 1ull);
-            S.h_src.reserve(3ull * n + 1); S.keys.reserve(3ull * n + 1); S.conv.reserve(1);
-            S.pool.reserve(3ull * n * cap + arena);
-            S.cand.reserve((uint64_t)S.grid * n);
-            // per-block string buffer: names + ';' + "suspect" + 20 digits per member (also the
-            // iterator's scratch)
-            const uint64_t strcap = std::max<uint64_t>(S.nt.h_bytes.size() + 29ull * n + 64, 5ull * n + 64);
-            S.strbuf.reserve((uint64_t)S.grid * ((strcap + 255) & ~255ull));
-            S.stats.reserve(4); S.cursor.reserve(1); S.err.reserve(1);
-            S.inc0.reserve(n); S.rank.reserve(n); S.boff.reserve(n + 1ull); S.sbase.reserve(base.size());
-            RP_HIP(hipMemcpyAsync(S.inc0.p, inc0, 8ull * n, hipMemcpyHostToDevice, S.st));
-            RP_HIP(hipMemcpyAsync(S.rank.p, rank.data(), 4ull * n, hipMemcpyHostToDevice, S.st));
-            RP_HIP(hipMemcpyAsync(S.boff.p, boff.data(), 8ull * (n + 1), hipMemcpyHostToDevice, S.st));
-            RP_HIP(hipMemcpyAsync(S.sbase.p, base.data(), base.size(), hipMemcpyHostToDevice, S.st));
-            S.h_dead.assign(dead, dead + n);
-            RP_HIP(hipMemcpyAsync(S.dead.p, S.h_dead.data(), n, hipMemcpyHostToDevice, S.st));
-            RP_HIP(hipMemsetAsync(S.stats.p, 0, 4 * sizeof(unsigned long long), S.st));
-            RP_HIP(hipMemsetAsync(S.err.p, 0, 4, S.st));
-            RP_HIP(hipMemsetAsync(S.cursor.p, 0, 8, S.st));
-            S.first_live = 0;
-            while (S.first_live < n && dead[S.first_live]) S.first_live++;
-            rp::SimDev& d = S.d;
-            d.N = n; d.W = W; d.seed = seed; d.susp = suspicion_rounds; d.now0 = now0;
-            d.Cd = (uint32_t)cap; d.Ct = (uint32_t)cap; d.Cm = (uint32_t)cap;
-            d.st = S.st_.p; d.inc = S.inc.p; d.order = S.order.p; d.slot = S.slot.p; d.dev = S.dev.p;
-            d.chg = S.chg.p; d.n_chg = S.n_chg.p; d.tim = S.tim.p; d.n_tim = S.n_tim.p;
-            d.it_idx = S.it_idx.p; d.n_shuf = S.n_shuf.p; d.ring_count = S.ring_count.p; d.max_piggy = S.max_piggy.p;
-            d.checksum = S.checksum.p; d.dirty = S.dirty.p; d.dead = S.dead.p;
-            d.sorted = S.nt.sorted.p; d.rank = S.rank.p; d.names = S.nt.d_bytes.p; d.noff = S.nt.d_noff.p;
-            d.sbase = S.sbase.p; d.boff = S.boff.p; d.inc0 = S.inc0.p;
-            d.target = S.target.p; d.ck_snap = S.ck_snap.p; d.inc_snap = S.inc_snap.p;
-            d.pool = S.pool.p; d.arena0 = 3ull * n * cap; d.arena_cap = arena; d.cursor = S.cursor.p;
-            d.resp_off = S.resp_off.p; d.lresp_off = S.lresp_off.p;
-            d.ping_n = S.ping_n.p; d.resp_n = S.resp_n.p; d.leg_n = S.leg_n.p; d.helpers = S.helpers.p;
-            d.nhelp = S.nhelp.p; d.lresp_n = S.lresp_n.p; d.cand = S.cand.p;
-            d.strbuf = S.strbuf.p; d.strcap = (strcap + 255) & ~255ull;
-            d.in_off = S.in_off.p; d.in_src = S.in_src.p; d.h_off = S.h_off.p; d.h_src = S.h_src.p;
-            d.stats = S.stats.p; d.err = S.err.p; d.round = 0;
-            {
-                const void* ptrs[] = {d.st, d.inc, d.order, d.slot, d.dev, d.chg, d.n_chg, d.tim, d.n_tim, d.it_idx,
-                                      d.n_shuf, d.ring_count, d.max_piggy, d.checksum, d.dirty, d.dead, d.sorted,
-                                      d.rank, d.names, d.noff, d.sbase, d.boff, d.inc0, d.target, d.ck_snap,
-                                      d.inc_snap, d.pool, d.cursor, d.resp_off, d.lresp_off, d.ping_n, d.resp_n,
-                                      d.leg_n, d.helpers, d.nhelp, d.lresp_n, d.cand, d.strbuf, d.in_off, d.in_src,
-                                      d.h_off, d.h_src, d.stats, d.err};
-                for (const void* p : ptrs) RP_REQUIRE(p != nullptr, "sim_create: internal buffer not allocated");
-            }
-            hipLaunchKernelGGL(rp::k_sim_init, dim3(rp::grid_for(NN, 256, 8192)), dim3(256), 0, S.st, d);
-            hipLaunchKernelGGL(rp::k_sim_start, dim3(rp::grid_for(n, 64)), dim3(64), 0, S.st, d);
-            hipLaunchKernelGGL(rp::k_sim_first_checksum, dim3(1), dim3(64), 0, S.st, d);
-            hipLaunchKernelGGL(rp::k_sim_bcast_checksum, dim3(rp::grid_for(n, 256)), dim3(256), 0, S.st, d);
-            RP_HIP(hipGetLastError());
-            RP_HIP(hipStreamSynchronize(S.st));
-        } catch (...) {
-            (void)hipStreamSynchronize(S.st);
-            (void)hipStreamDestroy(S.st);
-            delete h;
-            throw;
-        }
-        *out = h;
+int rp_sim_create_shard(uint32_t n, const char* names, const uint32_t* off, const int64_t* inc0, const uint8_t* dead,
+                        uint32_t seed, uint32_t suspicion_rounds, int64_t now0, int device, const uint32_t* bounds,
+                        uint32_t nshards, uint32_t shard, rp_sim** out) {
+    return guard([&] {
+        sim_create(n, names, off, inc0, dead, seed, suspicion_rounds, now0, device, bounds, nshards, shard, out);
     });
 }
 
@@ -1424,6 +1764,16 @@ int rp_sim_destroy(rp_sim* s) {
             (void)hipStreamDestroy(s->impl.st);
         }
         delete s;
+    });
+}
+
+int rp_sim_shard_info(rp_sim* s, uint32_t* v0, uint32_t* nl, uint32_t* nshards, uint32_t* shard) {
+    return guard([&] {
+        rp::Sim& S = SM(s);
+        if (v0) *v0 = S.v0;
+        if (nl) *nl = S.NL;
+        if (nshards) *nshards = S.G;
+        if (shard) *shard = S.shard;
     });
 }
 
@@ -1446,6 +1796,78 @@ int rp_sim_sync(rp_sim* s) {
     return guard([&] { SM(s).check_err(); });
 }
 
+int rp_sim_stage(rp_sim* s, int stage) {
+    return guard([&] {
+        rp::Sim& S = SM(s);
+        RP_REQUIRE(stage >= 0 && stage <= 4, "sim_stage: stage must be 0..4");
+        S.stage(stage);
+        if (stage == 4) S.check_err();
+    });
+}
+
+int rp_sim_outbox(rp_sim* s, uint64_t* nmsg, uint64_t* nrec, void** msg, void** rec) {
+    return guard([&] {
+        rp::Sim& S = SM(s);
+        RP_HIP(hipStreamSynchronize(S.st));
+        for (uint32_t g = 0; g < S.G; g++) {
+            if (nmsg) nmsg[g] = S.out.nmsg.empty() ? 0 : S.out.nmsg[g];
+            if (nrec) nrec[g] = S.out.nrec.empty() ? 0 : S.out.nrec[g];
+        }
+        if (msg) *msg = S.out.msg.p;
+        if (rec) *rec = S.out.rec.p;
+    });
+}
+
+int rp_sim_inbox(rp_sim* s, const uint64_t* nmsg, const uint64_t* nrec, void** msg, void** rec) {
+    return guard([&] {
+        rp::Sim& S = SM(s);
+        RP_REQUIRE(nmsg && nrec, "sim_inbox: counts required");
+        S.prepare_in(nmsg, nrec);
+        RP_HIP(hipStreamSynchronize(S.st));
+        if (msg) *msg = S.in.msg.p;
+        if (rec) *rec = S.in.rec.p;
+    });
+}
+
+int rp_sim_exchange_local(rp_sim* const* shards, uint32_t nshards) {
+    return guard([&] {
+        RP_REQUIRE(shards && nshards >= 1, "sim_exchange_local: bad arguments");
+        for (uint32_t i = 0; i < nshards; i++) {
+            RP_REQUIRE(shards[i] && shards[i]->impl.G == nshards && shards[i]->impl.shard == i,
+                       "sim_exchange_local: handles must be shards 0..G-1 of one partition");
+            RP_HIP(hipSetDevice(shards[i]->impl.device));
+            RP_HIP(hipStreamSynchronize(shards[i]->impl.st));
+        }
+        for (uint32_t dst = 0; dst < nshards; dst++) {
+            rp::Sim& D = shards[dst]->impl;
+            std::vector<uint64_t> nm(nshards), nr(nshards);
+            for (uint32_t src = 0; src < nshards; src++) {
+                nm[src] = shards[src]->impl.out.nmsg[dst];
+                nr[src] = shards[src]->impl.out.nrec[dst];
+            }
+            D.prepare_in(nm.data(), nr.data());
+            uint64_t mo = 0, ro = 0;
+            for (uint32_t src = 0; src < nshards; src++) {
+                rp::Sim& Sx = shards[src]->impl;
+                uint64_t msrc = 0, rsrc = 0;
+                for (uint32_t g = 0; g < dst; g++) {
+                    msrc += Sx.out.nmsg[g];
+                    rsrc += Sx.out.nrec[g];
+                }
+                if (nm[src])
+                    RP_HIP(hipMemcpyAsync(D.in.msg.p + mo, Sx.out.msg.p + msrc, sizeof(rp::Msg) * nm[src],
+                                          hipMemcpyDeviceToDevice, D.st));
+                if (nr[src])
+                    RP_HIP(hipMemcpyAsync(D.in.rec.p + ro, Sx.out.rec.p + rsrc, sizeof(rp::Rec) * nr[src],
+                                          hipMemcpyDeviceToDevice, D.st));
+                mo += nm[src];
+                ro += nr[src];
+            }
+        }
+        for (uint32_t i = 0; i < nshards; i++) RP_HIP(hipStreamSynchronize(shards[i]->impl.st));
+    });
+}
+
 int rp_sim_round(rp_sim* s, int64_t* out) {
     return guard([&] { *out = SM(s).round; });
 }
@@ -1454,18 +1876,18 @@ int rp_sim_checksums(rp_sim* s, uint32_t* out) {
     return guard([&] {
         rp::Sim& S = SM(s);
         S.refresh_checksums();
-        RP_HIP(hipMemcpyAsync(out, S.checksum.p, 4ull * S.N, hipMemcpyDeviceToHost, S.st));
+        if (S.NL) RP_HIP(hipMemcpyAsync(out, S.checksum.p, 4ull * S.NL, hipMemcpyDeviceToHost, S.st));
         RP_HIP(hipStreamSynchronize(S.st));
-        for (uint32_t v = 0; v < S.N; v++)
-            if (S.h_dead[v]) out[v] = 0;
+        for (uint32_t lv = 0; lv < S.NL; lv++)
+            if (S.h_dead[S.v0 + lv]) out[lv] = 0;
     });
 }
 
 int rp_sim_view(rp_sim* s, uint32_t v, uint8_t* status, int64_t* inc) {
     return guard([&] {
         rp::Sim& S = SM(s);
-        RP_REQUIRE(v < S.N, "sim_view: no such node");
-        const uint64_t row = (uint64_t)v * S.N;
+        RP_REQUIRE(v >= S.v0 && v < S.v0 + S.NL, "sim_view: node not in this shard");
+        const uint64_t row = (uint64_t)(v - S.v0) * S.N;
         if (status) {
             RP_HIP(hipMemcpyAsync(status, S.st_.p + row, S.N, hipMemcpyDeviceToHost, S.st));
         }
@@ -1476,22 +1898,17 @@ int rp_sim_view(rp_sim* s, uint32_t v, uint8_t* status, int64_t* inc) {
     });
 }
 
+int rp_sim_converged_local(rp_sim* s, uint32_t* out4) {
+    return guard([&] { SM(s).conv_local(out4); });
+}
+
 int rp_sim_converged(rp_sim* s, int* out) {
     return guard([&] {
         rp::Sim& S = SM(s);
-        if (S.first_live >= S.N) {
-            *out = 1;
-            return;
-        }
-        S.refresh_checksums();
-        const uint32_t one = 1;
-        RP_HIP(hipMemcpyAsync(S.conv.p, &one, 4, hipMemcpyHostToDevice, S.st));
-        hipLaunchKernelGGL(rp::k_converged, dim3(rp::grid_for((uint64_t)S.N * S.N, 256, 8192)), dim3(256), 0, S.st,
-                           S.d, S.first_live, S.conv.p);
-        uint32_t f = 0;
-        RP_HIP(hipMemcpyAsync(&f, S.conv.p, 4, hipMemcpyDeviceToHost, S.st));
-        RP_HIP(hipStreamSynchronize(S.st));
-        *out = (int)f;
+        RP_REQUIRE(S.G == 1, "sim_converged: a sharded handle reduces rp_sim_converged_local over its shards");
+        uint32_t c[4];
+        S.conv_local(c);
+        *out = (c[0] == 0 || (c[1] == c[2] && c[3] == 0)) ? 1 : 0;
     });
 }
 
