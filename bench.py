@@ -64,10 +64,7 @@ def cpu_baseline(servers, nkeys, threads, min_seconds=10.0):
 def merge_bench(rpa, local, n=100_000, k=100_000, batches=20, warmup=3):
     """C3 (BASELINE.json configs[2]): 100k-member table, batches of 100k updates (1% repeated
     addresses), Membership.update fold + one checksum per batch, inputs resident in HBM."""
-    import importlib.util
-    spec = importlib.util.spec_from_file_location("rp_synth", os.path.join(REPO, "ringpop-node_amd", "synth.py"))
-    S = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(S)
+    S = _synth()
     names, st0, inc0 = S.c3_members(n)
     m = rpa.Membership(whoami=names[0], capacity=n, device=local)
     ids0 = np.asarray(m.intern(names), dtype=np.uint32)
@@ -106,22 +103,39 @@ def merge_bench(rpa, local, n=100_000, k=100_000, batches=20, warmup=3):
             "gpu_ms_per_batch": e0.elapsed_time(e1) / batches, "checksum": m.checksum}
 
 
-def sim_bench(rpa, local, n=10_000, kill_pct=1, seed=11, max_rounds=300, max_seconds=240.0):
-    """C4 (BASELINE.json configs[3]): n ringpop nodes with full views, kill_pct% killed before
-    round 0, gossip rounds until convergence (scenario-runner.js:152-170 + every
-    killed member faulty everywhere). Reports rounds-to-convergence and device time per round."""
+def _synth():
     import importlib.util
     spec = importlib.util.spec_from_file_location("rp_synth", os.path.join(REPO, "ringpop-node_amd", "synth.py"))
     S = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(S)
+    return S
+
+
+def sim_bench(rpa, local, n=10_000, kill_pct=1, seed=11, max_rounds=300, max_seconds=240.0, world=1):
+    """C4 (BASELINE.json configs[3]) and C5 (configs[4]): n ringpop nodes with full views,
+    kill_pct% killed before round 0, gossip rounds until convergence
+    (scenario-runner.js:152-170 + every killed member faulty everywhere). One GPU: one
+    simulator handle. world > 1 (torchrun): the nodes are sharded by id range over the ranks and
+    each round's four message exchanges are RCCL all-to-all-v (DistGossipSim); the timed region
+    is bracketed by barriers and the max over ranks is reported. Reports rounds-to-convergence,
+    wall time per round, exchange bytes."""
+    S = _synth()
     k = max(1, n * kill_pct // 100)
     names = [S.c2_addr(i) for i in range(n)]
     inc0 = S.c3_members(n)[2]
     dead = S.kill_set(n, k, seed)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    sim = rpa.GossipSim(names, inc0, dead, seed=seed, suspicion_rounds=25, device=local)
+    if world > 1:
+        sim = rpa.DistGossipSim(names, inc0, dead, seed=seed, suspicion_rounds=25, device=local)
+    else:
+        sim = rpa.GossipSim(names, inc0, dead, seed=seed, suspicion_rounds=25, device=local)
     torch.cuda.synchronize()
     create_s = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
     rounds, conv, t0 = 0, False, time.perf_counter()
     per_round = []
     while rounds < max_rounds and time.perf_counter() - t0 < max_seconds:
@@ -129,15 +143,29 @@ def sim_bench(rpa, local, n=10_000, kill_pct=1, seed=11, max_rounds=300, max_sec
         sim.step(1)
         per_round.append(time.perf_counter() - a)
         rounds += 1
-        if sim.converged():
+        if sim.converged():  # collective when sharded: every rank leaves at the same round
             conv = True
             break
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     dt = time.perf_counter() - t0
+    t = torch.tensor([dt, create_s, max(per_round) if per_round else 0.0], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt, create_s, mx = (float(x) for x in t)
     st = sim.stats()
-    return {"workload": "C4: %d members, full views, %d killed (%d%%), suspicion 25 rounds" % (n, k, kill_pct),
-            "converged": conv, "rounds_to_convergence": rounds if conv else None, "rounds_run": rounds,
-            "ms_per_round": dt * 1e3 / max(rounds, 1), "max_round_ms": max(per_round) * 1e3 if per_round else None,
-            "create_s": create_s, "stats": st}
+    out = {"workload": "%s: %d members, full views, %d killed (%d%%), suspicion 25 rounds%s"
+                       % ("C5" if n >= 100_000 else "C4", n, k, kill_pct,
+                          ", nodes sharded over %d GPUs (RCCL all-to-all-v message exchange)" % world
+                          if world > 1 else ", one GPU"),
+           "n_gpus": world, "converged": conv, "rounds_to_convergence": rounds if conv else None,
+           "rounds_run": rounds, "ms_per_round": dt * 1e3 / max(rounds, 1), "max_round_ms": mx * 1e3,
+           "create_s": create_s, "stats": st}
+    if world > 1:
+        out["exchange_bytes_per_round_rank0"] = sim.exchange_bytes / max(rounds, 1)
+    sim.close()
+    return out
 
 
 def pmc_traffic():
@@ -161,7 +189,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-merge", action="store_true")
-    ap.add_argument("--sim-n", type=int, default=10000, help="C4 members (0: skip the sim leg)")
+    ap.add_argument("--sim-n", type=int, default=10000, help="C4 members, one GPU (0: skip)")
+    ap.add_argument("--sim5-n", type=int, default=100000, help="C5 members, sharded over all ranks (0: skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -214,6 +243,9 @@ def main():
     elapsed, kern_ms = float(t[0]), float(t[1])
 
     total = B * args.steps * world
+    del keys, owners
+    torch.cuda.empty_cache()
+    sim5 = sim_bench(rpa, local, n=args.sim5_n, world=world) if args.sim5_n else None
     if rank == 0:
         achieved = BYTES_PER_LOOKUPN3 * B / (kern_ms * 1e-3) / 1e9
         traffic = pmc_traffic()
@@ -243,8 +275,10 @@ def main():
         }
         if not args.no_merge:
             out["merge"] = merge_bench(rpa, local)
-        if args.sim_n:
+        if args.sim_n and world == 1:
             out["sim"] = sim_bench(rpa, local, n=args.sim_n)
+        if sim5:
+            out["sim_c5"] = sim5
         if not args.no_cpu:
             th = args.cpu_threads or min(16, os.cpu_count() or 1)
             out["cpu_baseline"] = cpu_baseline(servers, args.cpu_keys, th)
