@@ -263,7 +263,8 @@ __device__ __forceinline__ uint32_t ld32(const uint8_t* p, uint64_t o) {
 struct Lds {
     uint32_t u[16];
     uint64_t u64;
-    uint32_t win[2][kHashWin][8];
+    uint32_t win[2][kHashWin][8] __attribute__((aligned(16)));
+    uint32_t pad[8];  // the chain's one-chunk lookahead past win[1]
 };
 
 // ---- checksums
@@ -327,13 +328,14 @@ __device__ void block_checksum(const SimDev& S, uint32_t lv, uint8_t* buf, Lds& 
             f += a4;
             f = fh::rotr(f, 19) + 113;
         }
+        // chunk c starts at byte 20c of the (256-B aligned) buffer: dword-aligned word loads
+        const uint32_t* bw = reinterpret_cast<const uint32_t*>(buf);
         auto fill = [&](int wb, uint64_t c0, int t0, int nt) {
             for (int j = t0; j < kHashWin; j += nt) {
                 const uint64_t c = c0 + j;
                 if (c >= iters) break;
-                const uint64_t off = c * 20;
-                const uint32_t a = ld32(buf, off), b = ld32(buf, off + 4), cc = ld32(buf, off + 8),
-                               d = ld32(buf, off + 12), e = ld32(buf, off + 16);
+                const uint32_t* q = bw + c * 5;
+                const uint32_t a = q[0], b = q[1], cc = q[2], d = q[3], e = q[4];
                 uint32_t* r = L.win[wb][j];
                 r[0] = a; r[1] = b; r[2] = cc; r[3] = d;
                 r[4] = e; r[5] = premix(d); r[6] = premix(cc); r[7] = premix(b + e * fh::kC1);
@@ -347,19 +349,26 @@ __device__ void block_checksum(const SimDev& S, uint32_t lv, uint8_t* buf, Lds& 
             if (tid >= 64) {
                 if (w + 1 < nwin) fill(cur ^ 1, (w + 1) * kHashWin, tid - 64, kT - 64);
             } else if (tid == 0) {
+                // the serial chain; the next chunk's 8 words are read from LDS while this one
+                // is hashed (the chain is ~7 dependent ops, an LDS read ~100 cycles)
                 const uint64_t c0 = w * kHashWin;
                 const int n = (int)((iters - c0) < (uint64_t)kHashWin ? (iters - c0) : kHashWin);
+                typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+                const u32x4v* rw = reinterpret_cast<const u32x4v*>(&L.win[cur][0][0]);
+                u32x4v x0 = rw[0], x1 = rw[1];
                 for (int j = 0; j < n; j++) {
-                    const uint32_t* r = L.win[cur][j];
-                    const uint32_t a = r[0], b = r[1], c = r[2], d = r[3], e = r[4];
+                    const u32x4v y0 = rw[2 * (j + 1)], y1 = rw[2 * (j + 1) + 1];  // (j + 1 < kHashWin + 1)
+                    const uint32_t a = x0.x, b = x0.y, c = x0.z, d = x0.w, e = x1.x;
                     h += a;
                     g += b;
                     f += c;
-                    h = fh::rotr(h ^ r[5], 19) * 5 + 0xe6546b64u + e;
-                    g = fh::rotr(g ^ r[6], 19) * 5 + 0xe6546b64u + a;
-                    f = fh::rotr(f ^ r[7], 19) * 5 + 0xe6546b64u + d;
+                    h = fh::rotr(h ^ x1.y, 19) * 5 + 0xe6546b64u + e;
+                    g = fh::rotr(g ^ x1.z, 19) * 5 + 0xe6546b64u + a;
+                    f = fh::rotr(f ^ x1.w, 19) * 5 + 0xe6546b64u + d;
                     f += g;
                     g += f;
+                    x0 = y0;
+                    x1 = y1;
                 }
             }
             __syncthreads();
@@ -391,39 +400,77 @@ __device__ __forceinline__ void checksum_if_dirty(const SimDev& S, uint32_t lv, 
 
 // One node's checksum string, seen by one lane: the base string with the deviated rows'
 // pieces substituted. Piece k (address rank k) of the view is name + status + incarnation
-// (+ ';' unless last); clean pieces equal the base string's.
+// (+ ';' unless last); clean pieces equal the base string's. A deviated piece is described once
+// (Piece), when the lane's cursor reaches it; in this model a deviated piece almost always keeps
+// the base incarnation, so it differs from the base piece only in its status word.
+struct Piece {
+    uint32_t k;      // address rank (N: none)
+    uint32_t nl;     // name bytes
+    uint32_t sl;     // status bytes
+    uint32_t blen;   // base piece bytes
+    uint32_t plen;   // this view's piece bytes
+    uint32_t dl;     // digit count
+    uint64_t bpos;   // base offset of the piece
+    uint64_t st64;   // status characters, little-endian
+    int64_t x;       // incarnation
+    bool basedig;    // the digits are the base piece's (incarnation == inc0)
+};
+
+__device__ __forceinline__ uint64_t status_u64(uint8_t s) {
+    uint64_t v = 0;
+    const uint32_t n = status_len(s);
+    for (uint32_t i = 0; i < n; i++) v |= (uint64_t)status_char(s, i) << (8 * i);
+    return v;
+}
+
 struct LaneView {
     const SimDev& S;
     const uint8_t* strow;
     const int64_t* incrow;
     const uint32_t* dev;
 
-    __device__ uint32_t blen(uint32_t k) const { return (uint32_t)(S.boff[k + 1] - S.boff[k]); }
-    __device__ uint32_t plen(uint32_t k) const {
-        const uint32_t a = S.sorted[k];
-        return (uint32_t)(S.noff[a + 1] - S.noff[a]) + status_len(strow[a] & ST_MASK) + dec_len(incrow[a]) +
-               (k + 1 < S.N ? 1u : 0u);
-    }
-    __device__ uint8_t piece_byte(uint32_t k, uint32_t j) const {
-        const uint32_t a = S.sorted[k];
-        const uint64_t nb = S.noff[a];
-        const uint32_t nl = (uint32_t)(S.noff[a + 1] - nb);
-        if (j < nl) return S.names[nb + j];
-        j -= nl;
-        const uint8_t s = strow[a] & ST_MASK;
-        const uint32_t sl = status_len(s);
-        if (j < sl) return status_char(s, j);
-        j -= sl;
-        const int64_t x = incrow[a];
-        if (x == S.inc0[a]) {  // the base piece holds these digits after "alive"
-            const uint64_t p = S.boff[k] + nl + 5u;
-            const uint32_t dl = blen(k) - nl - 5u - (k + 1 < S.N ? 1u : 0u);
-            return j < dl ? S.sbase[p + j] : (uint8_t)';';
+    __device__ Piece piece(uint32_t k) const {
+        Piece P;
+        P.k = k;
+        if (k >= S.N) {
+            P.nl = P.sl = P.blen = P.plen = P.dl = 0;
+            P.bpos = S.boff[S.N];
+            P.st64 = 0;
+            P.x = 0;
+            P.basedig = true;
+            return P;
         }
-        const uint32_t dl = dec_len(x);
-        if (j >= dl) return (uint8_t)';';
+        const uint32_t a = S.sorted[k];
+        const uint8_t s = strow[a] & ST_MASK;
+        P.nl = (uint32_t)(S.noff[a + 1] - S.noff[a]);
+        P.sl = status_len(s);
+        P.st64 = status_u64(s);
+        P.bpos = S.boff[k];
+        P.blen = (uint32_t)(S.boff[k + 1] - P.bpos);
+        const uint32_t sep = k + 1 < S.N ? 1u : 0u;
+        P.x = incrow[a];
+        P.basedig = P.x == S.inc0[a];
+        P.dl = P.basedig ? P.blen - P.nl - 5u - sep : dec_len(P.x);
+        P.plen = P.nl + P.sl + P.dl + sep;
+        return P;
+    }
+    // lane length - base length of deviated piece k (4 loads)
+    __device__ int64_t piece_delta(uint32_t k) const {
+        const uint32_t a = S.sorted[k];
+        const int64_t x = incrow[a], x0 = S.inc0[a];
+        int64_t d = (int64_t)status_len(strow[a] & ST_MASK) - 5;
+        if (x != x0) d += (int64_t)dec_len(x) - (int64_t)dec_len(x0);
+        return d;
+    }
+    __device__ uint8_t piece_byte(const Piece& P, uint32_t j) const {
+        if (j < P.nl) return S.sbase[P.bpos + j];
+        j -= P.nl;
+        if (j < P.sl) return (uint8_t)(P.st64 >> (8 * j));
+        j -= P.sl;
+        if (P.basedig) return S.sbase[P.bpos + P.nl + 5u + j];  // digits (+ ';') of the base piece
+        if (j >= P.dl) return (uint8_t)';';
         uint8_t tmp[24];
-        dec_write(x, tmp, dl);
+        dec_write(P.x, tmp, P.dl);
         return tmp[j];
     }
     // next deviated rank >= k (N if none)
@@ -452,45 +499,57 @@ struct LaneView {
     }
 };
 
-// Forward byte cursor over a lane's string (positions queried in non-decreasing order).
+// Forward cursor over a lane's string (positions queried in non-decreasing order): the current
+// (or next) deviated piece P at lane offset pos, the shift delta of the clean bytes before it,
+// and the base offset of the deviated piece after it.
 struct Fwd {
-    uint32_t nd;    // next (or current) deviated rank
-    uint64_t pos;   // its start in the lane string
-    uint32_t pl;    // its length in the lane string
-    int64_t delta;  // lane position - base position for clean bytes before `pos`
+    Piece P;
+    uint64_t pos;
+    int64_t delta;
+    uint64_t nb2;  // base offset of the next deviated piece after P (base length if none)
 
+    __device__ void load(const LaneView& V, uint32_t k) {
+        P = V.piece(k);
+        pos = (uint64_t)((int64_t)P.bpos + delta);
+        nb2 = V.S.boff[V.next_dev(k < V.S.N ? k + 1 : V.S.N)];
+    }
     __device__ void init(const LaneView& V) {
         delta = 0;
-        nd = V.next_dev(0);
-        if (nd < V.S.N) {
-            pos = V.S.boff[nd];
-            pl = V.plen(nd);
-        } else {
-            pos = ~0ull >> 1;
-            pl = 0;
-        }
+        load(V, V.next_dev(0));
     }
     __device__ void skip_to(const LaneView& V, uint64_t q) {
-        while (nd < V.S.N && q >= pos + pl) {
-            delta += (int64_t)pl - (int64_t)V.blen(nd);
-            nd = V.next_dev(nd + 1);
-            if (nd < V.S.N) {
-                pos = (uint64_t)((int64_t)V.S.boff[nd] + delta);
-                pl = V.plen(nd);
-            } else {
-                pos = ~0ull >> 1;
-                pl = 0;
-            }
+        while (P.k < V.S.N && q >= pos + P.plen) {
+            delta += (int64_t)P.plen - (int64_t)P.blen;
+            load(V, V.next_dev(P.k + 1));
         }
     }
     __device__ uint8_t byte(const LaneView& V, uint64_t q) {
         skip_to(V, q);
         if (q < pos) return V.S.sbase[(uint64_t)((int64_t)q - delta)];
-        return V.piece_byte(nd, (uint32_t)(q - pos));
+        return V.piece_byte(P, (uint32_t)(q - pos));
     }
 };
 
 __device__ __forceinline__ uint32_t ldw(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
+
+// the 5 words of base bytes [o, o + 20)
+__device__ __forceinline__ void base_words(const uint8_t* sbase, uint64_t o, uint32_t (&w)[5]) {
+    const uint8_t* p = sbase + (o & ~3ull);
+    const uint32_t sh = (uint32_t)(o & 3);
+    const uint32_t w0 = ldw(p), w1 = ldw(p + 4), w2 = ldw(p + 8), w3 = ldw(p + 12), w4 = ldw(p + 16),
+                   w5 = ldw(p + 20);
+    w[0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+    w[1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+    w[2] = __builtin_amdgcn_alignbyte(w3, w2, sh);
+    w[3] = __builtin_amdgcn_alignbyte(w4, w3, sh);
+    w[4] = __builtin_amdgcn_alignbyte(w5, w4, sh);
+}
+
+// mask of the low bytes of a word whose lane offsets q (= base + b) are < lim
+__device__ __forceinline__ uint32_t below_mask(int64_t lim, uint64_t base) {
+    const int64_t m = lim - (int64_t)base;
+    return m <= 0 ? 0u : m >= 4 ? 0xFFFFFFFFu : (1u << (8 * m)) - 1u;
+}
 
 // Membership checksum of local node lv computed by this lane alone.
 __device__ uint32_t lane_checksum(const SimDev& S, uint32_t lv) {
@@ -505,7 +564,7 @@ __device__ uint32_t lane_checksum(const SimDev& S, uint32_t lv) {
         while (bits) {
             const uint32_t k = (w << 5) + __builtin_ctz(bits);
             bits &= bits - 1;
-            dtot += (int64_t)V.plen(k) - (int64_t)V.blen(k);
+            dtot += V.piece_delta(k);
             last = k;
         }
     }
@@ -522,22 +581,25 @@ __device__ uint32_t lane_checksum(const SimDev& S, uint32_t lv) {
     {
         uint32_t kd = last;
         int64_t da = dtot;  // delta of the clean bytes after piece kd
+        Piece P{};
         uint64_t E = 0, B = 0;
         if (kd != NONE) {
+            P = V.piece(kd);
             E = (uint64_t)((int64_t)S.boff[kd + 1] + da);
-            B = E - V.plen(kd);
+            B = E - P.plen;
         }
         for (int i = 19; i >= 0; i--) {
             const uint64_t q = len - 20 + (uint64_t)i;
             while (kd != NONE && q < B) {
-                da -= (int64_t)V.plen(kd) - (int64_t)V.blen(kd);
+                da -= (int64_t)P.plen - (int64_t)P.blen;
                 kd = V.prev_dev(kd);
                 if (kd != NONE) {
+                    P = V.piece(kd);
                     E = (uint64_t)((int64_t)S.boff[kd + 1] + da);
-                    B = E - V.plen(kd);
+                    B = E - P.plen;
                 }
             }
-            tail[i] = (kd != NONE && q >= B && q < E) ? V.piece_byte(kd, (uint32_t)(q - B))
+            tail[i] = (kd != NONE && q >= B && q < E) ? V.piece_byte(P, (uint32_t)(q - B))
                                                        : S.sbase[(uint64_t)((int64_t)q - da)];
         }
     }
@@ -562,27 +624,34 @@ __device__ uint32_t lane_checksum(const SimDev& S, uint32_t lv) {
     for (uint64_t c = 0; c < iters; c++) {
         const uint64_t q0 = c * 20;
         F.skip_to(V, q0);
-        uint32_t a, b, cc, d, e;
-        if (q0 + 20 <= F.pos) {  // clean: 20 bytes of the base string at a lane-specific shift
-            const uint64_t o = (uint64_t)((int64_t)q0 - F.delta);
-            const uint8_t* p = S.sbase + (o & ~3ull);
-            const uint32_t sh = (uint32_t)(o & 3);
-            const uint32_t w0 = ldw(p), w1 = ldw(p + 4), w2 = ldw(p + 8), w3 = ldw(p + 12), w4 = ldw(p + 16),
-                           w5 = ldw(p + 20);
-            a = __builtin_amdgcn_alignbyte(w1, w0, sh);
-            b = __builtin_amdgcn_alignbyte(w2, w1, sh);
-            cc = __builtin_amdgcn_alignbyte(w3, w2, sh);
-            d = __builtin_amdgcn_alignbyte(w4, w3, sh);
-            e = __builtin_amdgcn_alignbyte(w5, w4, sh);
+        uint32_t wd[5];
+        if (q0 + 20 <= F.pos) {  // clean: 20 base bytes at this lane's shift
+            base_words(S.sbase, (uint64_t)((int64_t)q0 - F.delta), wd);
+        } else if (F.P.basedig &&
+                   q0 + 20 <= (uint64_t)((int64_t)F.nb2 + F.delta + (int64_t)F.P.plen - (int64_t)F.P.blen)) {
+            // one deviated piece whose only difference is its status: base bytes at shift delta
+            // before the status, the status characters, base bytes at shift delta + sl - 5 after
+            const int64_t s0 = (int64_t)F.pos + F.P.nl, s1 = s0 + F.P.sl;
+            uint32_t w1[5], w2[5];
+            base_words(S.sbase, (uint64_t)((int64_t)q0 - F.delta), w1);
+            base_words(S.sbase, (uint64_t)((int64_t)q0 - F.delta - (int64_t)F.P.sl + 5), w2);
+#pragma unroll
+            for (int i = 0; i < 5; i++) {
+                const uint64_t qb = q0 + 4 * i;
+                const uint32_t m1 = below_mask(s0, qb), m2 = below_mask(s1, qb);
+                const int64_t so = (int64_t)qb - s0;  // status byte index of this word's byte 0
+                const uint32_t sw = so >= 0 ? (so < 8 ? (uint32_t)(F.P.st64 >> (8 * so)) : 0u)
+                                            : (so > -4 ? (uint32_t)(F.P.st64 << (8 * -so)) : 0u);
+                wd[i] = (w1[i] & m1) | (sw & m2 & ~m1) | (w2[i] & ~m2);
+            }
         } else {
-            uint32_t wd[5];
             for (int i = 0; i < 5; i++) {
                 uint32_t x = 0;
                 for (int j = 0; j < 4; j++) x |= (uint32_t)F.byte(V, q0 + 4 * i + j) << (8 * j);
                 wd[i] = x;
             }
-            a = wd[0]; b = wd[1]; cc = wd[2]; d = wd[3]; e = wd[4];
         }
+        const uint32_t a = wd[0], b = wd[1], cc = wd[2], d = wd[3], e = wd[4];
         h += a;
         g += b;
         f += cc;
@@ -926,18 +995,29 @@ __global__ __launch_bounds__(kT) void k_phase_c(SimDev S) {
     }
 }
 
-// D1: ping-req fan-out for senders whose target is dead
-__global__ __launch_bounds__(kT) void k_phase_d1(SimDev S) {
+// The live local senders whose target is dead (the ping-req senders of D1), in any order (their
+// work is independent); every node's helper count is reset.
+__global__ void k_d1_list(SimDev S, uint32_t* __restrict__ list, uint32_t* __restrict__ n) {
+    for (uint32_t lv = blockIdx.x * blockDim.x + threadIdx.x; lv < S.NL; lv += gridDim.x * blockDim.x) {
+        S.nhelp[lv] = 0;
+        const int32_t t = S.target[lv];
+        if (!S.dead[S.v0 + lv] && t >= 0 && S.dead[t]) list[atomicAdd(n, 1u)] = lv;
+    }
+}
+
+// D1: ping-req fan-out for senders whose target is dead (one workgroup per listed sender)
+__global__ __launch_bounds__(kT) void k_phase_d1(SimDev S, const uint32_t* __restrict__ list,
+                                                 const uint32_t* __restrict__ nlist) {
     __shared__ Lds L;
     __shared__ Rec tmp;
     __shared__ uint32_t ncand;
     const int64_t now = S.now0 + 200 * S.round;
     uint32_t* cand = S.cand + (uint64_t)blockIdx.x * S.N;
-    for (uint32_t lv = blockIdx.x; lv < S.NL; lv += gridDim.x) {
+    const uint32_t nl = *nlist;
+    for (uint32_t li = blockIdx.x; li < nl; li += gridDim.x) {
+        const uint32_t lv = list[li];
         const uint32_t v = S.v0 + lv;
         const int32_t t = S.target[lv];
-        if (threadIdx.x == 0) S.nhelp[lv] = 0;
-        if (S.dead[v] || t < 0 || !S.dead[t]) continue;
         const uint64_t row = (uint64_t)lv * S.N;
         if (threadIdx.x == 0) atomicAdd(&S.stats[1], 1ull);
         // candidates: members-array order, pingable, not the target (index.js:141-150)
@@ -1361,7 +1441,7 @@ struct Sim {
         helpers, nhelp, leg_nk, cand, rank, err, bounds, killed, conv;
     DevBuf<uint32_t> okey, oval, ocnt, ooff, omoff;  // outbox build
     DevBuf<uint32_t> ib_off, ib_idx, ikey;         // inbox build
-    DevBuf<uint32_t> rsp_n, resp_idx, lresp_idx;
+    DevBuf<uint32_t> rsp_n, resp_idx, lresp_idx, d1list;
     DevBuf<uint64_t> boff, rsp_off, ibase;
     DevBuf<Change> chg;
     DevBuf<Timer> tim;
@@ -1512,7 +1592,10 @@ struct Sim {
             import_in(K_RESP);
             if (NL) {
                 hipLaunchKernelGGL(k_phase_c, dim3(g), dim3(kT), 0, st, d);
-                hipLaunchKernelGGL(k_phase_d1, dim3(g), dim3(kT), 0, st, d);
+                d1list.reserve(NL + 1);
+                RP_HIP(hipMemsetAsync(d1list.p + NL, 0, 4, st));
+                hipLaunchKernelGGL(k_d1_list, dim3(grid_for(NL, 256)), dim3(256), 0, st, d, d1list.p, d1list.p + NL);
+                hipLaunchKernelGGL(k_phase_d1, dim3(g), dim3(kT), 0, st, d, d1list.p, d1list.p + NL);
             }
             build_out(K_LEG);
             break;

@@ -51,25 +51,34 @@ RP_HD bool evaluate_update(uint8_t cur, int64_t cur_inc, bool is_local_member, u
 }
 
 // Decimal digits of an int64 as JS prints an integral Number (|x| < 2^53 in practice).
+// Comparisons against powers of ten: no 64-bit division on the device.
 RP_HD uint32_t dec_len(int64_t v) {
-    uint64_t u = v < 0 ? (uint64_t)(-(v + 1)) + 1 : (uint64_t)v;
+    const uint64_t u = v < 0 ? (uint64_t)(-(v + 1)) + 1 : (uint64_t)v;
     uint32_t n = 1;
-    while (u >= 10) {
-        u /= 10;
+    uint64_t p = 10;
+    while (n < 20 && u >= p) {
         n++;
+        if (n < 20) p *= 10;
     }
     return n + (v < 0 ? 1u : 0u);
 }
 
+// Writes the n characters of dec_len(v). 64-bit divisions only while the value exceeds 32 bits.
 RP_HD void dec_write(int64_t v, uint8_t* out, uint32_t n) {
     uint64_t u = v < 0 ? (uint64_t)(-(v + 1)) + 1 : (uint64_t)v;
-    for (uint32_t i = n; i-- > 0;) {
-        if (i == 0 && v < 0) {
-            out[0] = '-';
-            break;
-        }
-        out[i] = (uint8_t)('0' + u % 10);
-        u /= 10;
+    const uint32_t lo = v < 0 ? 1u : 0u;
+    if (v < 0) out[0] = '-';
+    uint32_t i = n;
+    while (u > 0xFFFFFFFFull && i > lo) {
+        const uint64_t q = u / 10;
+        out[--i] = (uint8_t)('0' + (uint32_t)(u - q * 10));
+        u = q;
+    }
+    uint32_t w = (uint32_t)u;
+    while (i > lo) {
+        const uint32_t q = w / 10;
+        out[--i] = (uint8_t)('0' + (w - q * 10));
+        w = q;
     }
 }
 

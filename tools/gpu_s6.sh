@@ -1,0 +1,5 @@
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out/s6
+timeout -k 10 300 python -u -m pytest tests/test_sim_gpu.py tests/test_sim_shard_gpu.py tests/test_members_gpu.py -x -q --timeout 200 --timeout-method thread > gpurun_out/s6/pytest.log 2>&1 &&
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/s6/prof -o run -- python -u tools/sim_probe.py 100000 1 60 > gpurun_out/s6/sim100k.log 2>&1
