@@ -154,6 +154,8 @@ struct SimDev {
     uint32_t* cand;     // [grid*N] scratch for ping-req candidate lists
     uint8_t* strbuf;    // [grid * strcap]
     uint64_t strcap;
+    uint4* dlist;       // [NL][dcap] a lane checksum's deviated pieces, address order
+    uint32_t dcap;
     // inbound messages of the current stage
     const Msg* in_msg;
     const Rec* in_rec;
@@ -268,135 +270,6 @@ struct Lds {
 };
 
 // ---- checksums
-
-// Membership.computeChecksum (index.js:48-75) of local node lv by one workgroup: the string is
-// written to buf in address order, then hashed (one chain lane, 192 pre-mixing lanes).
-__device__ void block_checksum(const SimDev& S, uint32_t lv, uint8_t* buf, Lds& L) {
-    const uint32_t N = S.N;
-    const uint64_t row = (uint64_t)lv * N;
-    const int tid = threadIdx.x;
-    // contiguous member range per thread keeps address order inside each thread's piece
-    const uint32_t per = (N + kT - 1) / kT;
-    const uint32_t b0 = min(N, per * tid), b1 = min(N, b0 + per);
-    uint32_t mine = 0;
-    for (uint32_t k = b0; k < b1; k++) {
-        const uint32_t a = S.sorted[k];
-        mine += (uint32_t)(S.noff[a + 1] - S.noff[a]) + status_len(S.st[row + a] & ST_MASK) + dec_len(S.inc[row + a]) +
-                1u;
-    }
-    uint32_t total;
-    uint32_t o = block_scan(mine, L.u, &total);
-    for (uint32_t k = b0; k < b1; k++) {
-        const uint32_t a = S.sorted[k];
-        const uint64_t nb = S.noff[a];
-        const uint32_t nl = (uint32_t)(S.noff[a + 1] - nb);
-        for (uint32_t q = 0; q < nl; q++) buf[o++] = S.names[nb + q];
-        const uint8_t st = S.st[row + a] & ST_MASK;
-        const uint32_t sl = status_len(st);
-        for (uint32_t q = 0; q < sl; q++) buf[o++] = status_char(st, q);
-        const int64_t in = S.inc[row + a];
-        const uint32_t dl = dec_len(in);
-        dec_write(in, buf + o, dl);
-        o += dl;
-        buf[o++] = ';';
-    }
-    __threadfence_block();
-    __syncthreads();
-    const uint64_t len = total ? total - 1 : 0;
-    uint32_t h = 0;
-    if (len <= 24) {
-        if (tid == 0) h = fh::hash32(fh::PtrSrc{buf}, (uint32_t)len);
-    } else {
-        const uint64_t iters = (len - 1) / 20;
-        uint32_t g = 0, f = 0;
-        if (tid == 0) {
-            const uint32_t L = (uint32_t)len;
-            h = L;
-            g = fh::kC1 * L;
-            f = g;
-            const uint32_t a0 = premix(ld32(buf, len - 4)), a1 = premix(ld32(buf, len - 8)),
-                           a2 = premix(ld32(buf, len - 16)), a3 = premix(ld32(buf, len - 12)),
-                           a4 = premix(ld32(buf, len - 20));
-            h ^= a0;
-            h = fh::rotr(h, 19) * 5 + 0xe6546b64u;
-            h ^= a2;
-            h = fh::rotr(h, 19) * 5 + 0xe6546b64u;
-            g ^= a1;
-            g = fh::rotr(g, 19) * 5 + 0xe6546b64u;
-            g ^= a3;
-            g = fh::rotr(g, 19) * 5 + 0xe6546b64u;
-            f += a4;
-            f = fh::rotr(f, 19) + 113;
-        }
-        // chunk c starts at byte 20c of the (256-B aligned) buffer: dword-aligned word loads
-        const uint32_t* bw = reinterpret_cast<const uint32_t*>(buf);
-        auto fill = [&](int wb, uint64_t c0, int t0, int nt) {
-            for (int j = t0; j < kHashWin; j += nt) {
-                const uint64_t c = c0 + j;
-                if (c >= iters) break;
-                const uint32_t* q = bw + c * 5;
-                const uint32_t a = q[0], b = q[1], cc = q[2], d = q[3], e = q[4];
-                uint32_t* r = L.win[wb][j];
-                r[0] = a; r[1] = b; r[2] = cc; r[3] = d;
-                r[4] = e; r[5] = premix(d); r[6] = premix(cc); r[7] = premix(b + e * fh::kC1);
-            }
-        };
-        fill(0, 0, tid, kT);
-        __syncthreads();
-        const uint64_t nwin = (iters + kHashWin - 1) / kHashWin;
-        for (uint64_t w = 0; w < nwin; w++) {
-            const int cur = (int)(w & 1);
-            if (tid >= 64) {
-                if (w + 1 < nwin) fill(cur ^ 1, (w + 1) * kHashWin, tid - 64, kT - 64);
-            } else if (tid == 0) {
-                // the serial chain; the next chunk's 8 words are read from LDS while this one
-                // is hashed (the chain is ~7 dependent ops, an LDS read ~100 cycles)
-                const uint64_t c0 = w * kHashWin;
-                const int n = (int)((iters - c0) < (uint64_t)kHashWin ? (iters - c0) : kHashWin);
-                typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-                const u32x4v* rw = reinterpret_cast<const u32x4v*>(&L.win[cur][0][0]);
-                u32x4v x0 = rw[0], x1 = rw[1];
-                for (int j = 0; j < n; j++) {
-                    const u32x4v y0 = rw[2 * (j + 1)], y1 = rw[2 * (j + 1) + 1];  // (j + 1 < kHashWin + 1)
-                    const uint32_t a = x0.x, b = x0.y, c = x0.z, d = x0.w, e = x1.x;
-                    h += a;
-                    g += b;
-                    f += c;
-                    h = fh::rotr(h ^ x1.y, 19) * 5 + 0xe6546b64u + e;
-                    g = fh::rotr(g ^ x1.z, 19) * 5 + 0xe6546b64u + a;
-                    f = fh::rotr(f ^ x1.w, 19) * 5 + 0xe6546b64u + d;
-                    f += g;
-                    g += f;
-                    x0 = y0;
-                    x1 = y1;
-                }
-            }
-            __syncthreads();
-        }
-        if (tid == 0) {
-            g = fh::rotr(g, 11) * fh::kC1;
-            g = fh::rotr(g, 17) * fh::kC1;
-            f = fh::rotr(f, 11) * fh::kC1;
-            f = fh::rotr(f, 17) * fh::kC1;
-            h = fh::rotr(h + g, 19);
-            h = h * 5 + 0xe6546b64u;
-            h = fh::rotr(h, 17) * fh::kC1;
-            h = fh::rotr(h + f, 19);
-            h = h * 5 + 0xe6546b64u;
-            h = fh::rotr(h, 17) * fh::kC1;
-        }
-    }
-    if (tid == 0) {
-        S.checksum[lv] = h;
-        S.dirty[lv] = 0;
-    }
-    __syncthreads();
-}
-
-__device__ __forceinline__ void checksum_if_dirty(const SimDev& S, uint32_t lv, Lds& L) {
-    __syncthreads();
-    if (S.dirty[lv]) block_checksum(S, lv, S.strbuf + (uint64_t)blockIdx.x * S.strcap, L);
-}
 
 // One node's checksum string, seen by one lane: the base string with the deviated rows'
 // pieces substituted. Piece k (address rank k) of the view is name + status + incarnation
@@ -674,11 +547,559 @@ __device__ uint32_t lane_checksum(const SimDev& S, uint32_t lv) {
     return h;
 }
 
-// every live local node whose view changed: one node per lane
+// Membership.computeChecksum (index.js:48-75) of local node lv by one workgroup, without
+// materialising the string: the view's deviated pieces are listed in address order with their
+// lane offsets (a scan of the deviation bitmap + a prefix sum of the length differences), then
+// 192 lanes produce the 20-byte chunks (base words at the right shift, or bytes of a deviated
+// piece) and pre-mix them into double-buffered LDS windows while one lane runs the serial chain.
+struct DevTab {  // per-block scratch in strbuf
+    uint32_t* k;     // deviated ranks, address order
+    int64_t* db;     // lane - base shift of the clean bytes before piece i
+    uint64_t* pos;   // lane offset of piece i
+    uint64_t* end;   // lane offset past piece i
+    uint32_t n;
+    int64_t dtot;    // shift after the last piece
+};
+
+// first piece i whose lane end is > q (n if none)
+__device__ __forceinline__ uint32_t tab_find(const DevTab& T, uint64_t q) {
+    uint32_t lo = 0, hi = T.n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (T.end[mid] <= q) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// byte cursor over the table (positions in non-decreasing order)
+struct TabCursor {
+    uint32_t i;
+    uint32_t pk;  // rank whose Piece is cached (NONE: none)
+    Piece P;
+    __device__ uint8_t byte(const LaneView& V, const DevTab& T, uint64_t q) {
+        while (i < T.n && q >= T.end[i]) i++;
+        const int64_t db = i < T.n ? T.db[i] : T.dtot;
+        if (i >= T.n || q < T.pos[i]) return V.S.sbase[(uint64_t)((int64_t)q - db)];
+        if (pk != T.k[i]) {
+            pk = T.k[i];
+            P = V.piece(pk);
+        }
+        return V.piece_byte(P, (uint32_t)(q - T.pos[i]));
+    }
+};
+
+__device__ void block_checksum(const SimDev& S, uint32_t lv, uint8_t* scratch, Lds& L) {
+    const uint32_t N = S.N;
+    const uint64_t row = (uint64_t)lv * N;
+    const LaneView V{S, S.st + row, S.inc + row, S.dev + (uint64_t)lv * S.W};
+    const int tid = threadIdx.x;
+    const uint64_t o1 = ((4ull * N) + 7) & ~7ull;
+    DevTab T;
+    T.k = reinterpret_cast<uint32_t*>(scratch);
+    T.db = reinterpret_cast<int64_t*>(scratch + o1);
+    T.pos = reinterpret_cast<uint64_t*>(scratch + o1 + 8ull * N);
+    T.end = reinterpret_cast<uint64_t*>(scratch + o1 + 16ull * N);
+    // deviated ranks in address order (contiguous bitmap words per thread)
+    {
+        const uint32_t per = (S.W + kT - 1) / kT;
+        const uint32_t w0 = min(S.W, per * tid), w1 = min(S.W, w0 + per);
+        uint32_t cnt = 0;
+        for (uint32_t w = w0; w < w1; w++) cnt += __builtin_popcount(V.dev[w]);
+        uint32_t nd;
+        uint32_t o = block_scan(cnt, L.u, &nd);
+        for (uint32_t w = w0; w < w1; w++) {
+            uint32_t bits = V.dev[w];
+            while (bits) {
+                T.k[o++] = (w << 5) + __builtin_ctz(bits);
+                bits &= bits - 1;
+            }
+        }
+        T.n = nd;
+    }
+    __threadfence_block();
+    __syncthreads();
+    // shifts: prefix sums of the pieces' length differences (|sum| < 2^31)
+    int32_t run = 0;
+    for (uint32_t base = 0; base < T.n; base += kT) {
+        const uint32_t i = base + tid;
+        int32_t d = 0;
+        uint32_t k = 0;
+        if (i < T.n) {
+            k = T.k[i];
+            d = (int32_t)V.piece_delta(k);
+        }
+        uint32_t tot;
+        const int32_t ex = (int32_t)block_scan((uint32_t)d, L.u, &tot);
+        if (i < T.n) {
+            const int64_t db = (int64_t)run + ex;
+            T.db[i] = db;
+            T.pos[i] = (uint64_t)((int64_t)S.boff[k] + db);
+            T.end[i] = (uint64_t)((int64_t)S.boff[k + 1] + db + d);
+        }
+        run += (int32_t)tot;
+    }
+    T.dtot = run;
+    __threadfence_block();
+    __syncthreads();
+    const uint64_t len = (uint64_t)((int64_t)S.boff[N] + run);
+    uint32_t h = 0;
+    if (len <= 24) {
+        if (tid == 0) {
+            uint8_t b[24];
+            TabCursor C{0, NONE, Piece{}};
+            for (uint32_t q = 0; q < (uint32_t)len; q++) b[q] = C.byte(V, T, q);
+            h = fh::hash32(fh::PtrSrc{b}, (uint32_t)len);
+        }
+    } else {
+        const uint64_t iters = (len - 1) / 20;
+        uint32_t g = 0, f = 0;
+        if (tid == 0) {
+            uint8_t tb[20];
+            TabCursor C{tab_find(T, len - 20), NONE, Piece{}};
+            for (int i = 0; i < 20; i++) tb[i] = C.byte(V, T, len - 20 + i);
+            auto tw = [&](int o) {
+                return (uint32_t)tb[o] | ((uint32_t)tb[o + 1] << 8) | ((uint32_t)tb[o + 2] << 16) |
+                       ((uint32_t)tb[o + 3] << 24);
+            };
+            const uint32_t L32 = (uint32_t)len;
+            h = L32;
+            g = fh::kC1 * L32;
+            f = g;
+            h ^= premix(tw(16));
+            h = fh::rotr(h, 19) * 5 + 0xe6546b64u;
+            h ^= premix(tw(4));
+            h = fh::rotr(h, 19) * 5 + 0xe6546b64u;
+            g ^= premix(tw(12));
+            g = fh::rotr(g, 19) * 5 + 0xe6546b64u;
+            g ^= premix(tw(8));
+            g = fh::rotr(g, 19) * 5 + 0xe6546b64u;
+            f += premix(tw(0));
+            f = fh::rotr(f, 19) + 113;
+        }
+        // lanes [t0, t0 + nt) produce window wb = chunks [c0, c0 + kHashWin), a contiguous run each
+        auto fill = [&](int wb, uint64_t c0, int idx, int nt) {
+            const uint64_t n = (iters - c0) < (uint64_t)kHashWin ? (iters - c0) : kHashWin;
+            const uint64_t per = (n + nt - 1) / nt;
+            const uint64_t ja = (uint64_t)idx * per, jb = ja + per < n ? ja + per : n;
+            if (ja >= jb) return;
+            TabCursor C{tab_find(T, (c0 + ja) * 20), NONE, Piece{}};
+            for (uint64_t j = ja; j < jb; j++) {
+                const uint64_t q0 = (c0 + j) * 20;
+                while (C.i < T.n && q0 >= T.end[C.i]) C.i++;
+                uint32_t wd[5];
+                if (C.i >= T.n || q0 + 20 <= T.pos[C.i]) {
+                    const int64_t db = C.i < T.n ? T.db[C.i] : T.dtot;
+                    base_words(S.sbase, (uint64_t)((int64_t)q0 - db), wd);
+                } else {
+                    TabCursor D = C;
+                    for (int i = 0; i < 5; i++) {
+                        uint32_t x = 0;
+                        for (int b = 0; b < 4; b++) x |= (uint32_t)D.byte(V, T, q0 + 4 * i + b) << (8 * b);
+                        wd[i] = x;
+                    }
+                    C.pk = D.pk;
+                    C.P = D.P;
+                }
+                uint32_t* r = L.win[wb][j];
+                r[0] = wd[0]; r[1] = wd[1]; r[2] = wd[2]; r[3] = wd[3];
+                r[4] = wd[4]; r[5] = premix(wd[3]); r[6] = premix(wd[2]); r[7] = premix(wd[1] + wd[4] * fh::kC1);
+            }
+        };
+        fill(0, 0, tid, kT);
+        __syncthreads();
+        const uint64_t nwin = (iters + kHashWin - 1) / kHashWin;
+        for (uint64_t w = 0; w < nwin; w++) {
+            const int cur = (int)(w & 1);
+            if (tid >= 64) {
+                if (w + 1 < nwin) fill(cur ^ 1, (w + 1) * kHashWin, tid - 64, kT - 64);
+            } else if (tid == 0) {
+                // the serial chain; the next chunk's 8 words are read from LDS while this one
+                // is hashed (the chain is ~7 dependent ops, an LDS read ~100 cycles)
+                const uint64_t c0 = w * kHashWin;
+                const int n = (int)((iters - c0) < (uint64_t)kHashWin ? (iters - c0) : kHashWin);
+                typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+                const u32x4v* rw = reinterpret_cast<const u32x4v*>(&L.win[cur][0][0]);
+                u32x4v x0 = rw[0], x1 = rw[1];
+                for (int j = 0; j < n; j++) {
+                    const u32x4v y0 = rw[2 * (j + 1)], y1 = rw[2 * (j + 1) + 1];  // (j + 1 < kHashWin + 1)
+                    const uint32_t a = x0.x, b = x0.y, c = x0.z, d = x0.w, e = x1.x;
+                    h += a;
+                    g += b;
+                    f += c;
+                    h = fh::rotr(h ^ x1.y, 19) * 5 + 0xe6546b64u + e;
+                    g = fh::rotr(g ^ x1.z, 19) * 5 + 0xe6546b64u + a;
+                    f = fh::rotr(f ^ x1.w, 19) * 5 + 0xe6546b64u + d;
+                    f += g;
+                    g += f;
+                    x0 = y0;
+                    x1 = y1;
+                }
+            }
+            __syncthreads();
+        }
+        if (tid == 0) {
+            g = fh::rotr(g, 11) * fh::kC1;
+            g = fh::rotr(g, 17) * fh::kC1;
+            f = fh::rotr(f, 11) * fh::kC1;
+            f = fh::rotr(f, 17) * fh::kC1;
+            h = fh::rotr(h + g, 19);
+            h = h * 5 + 0xe6546b64u;
+            h = fh::rotr(h, 17) * fh::kC1;
+            h = fh::rotr(h + f, 19);
+            h = h * 5 + 0xe6546b64u;
+            h = fh::rotr(h, 17) * fh::kC1;
+        }
+    }
+    if (tid == 0) {
+        S.checksum[lv] = h;
+        S.dirty[lv] = 0;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void checksum_if_dirty(const SimDev& S, uint32_t lv, Lds& L) {
+    __syncthreads();
+    if (S.dirty[lv]) block_checksum(S, lv, S.strbuf + (uint64_t)blockIdx.x * S.strcap, L);
+}
+
+// Base-string ring of one wave in LDS. The wave's lanes hash different views in lockstep (chunk
+// c of every lane's string at the same time); their base offsets differ only by each lane's
+// running shift, within [q0 - DHI, q0 + 112 - DLO]. The ring keeps base bytes [hi - kRing, hi)
+// (its first 24 words mirrored past its end, so a group's 21 words never wrap) and one more 1-KB
+// slice in flight in registers (16 B per lane): every chunk's words come from LDS instead of an
+// L2 round trip.
+constexpr uint32_t kRing = 16384, kSlice = 1024, kRingW = kRing / 4;
+typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
+
+struct BaseRing {
+    uint32_t* ring;  // kRingW + 24 words
+    uint32_t hi;
+    u32x4s pend;
+    __device__ void start(const uint8_t* sbase, int lane) {
+        hi = 0;
+        pend = *reinterpret_cast<const u32x4s*>(sbase + lane * 16);
+    }
+    // wave-uniform: make base bytes [.., need) resident
+    __device__ void ensure(const uint8_t* sbase, uint32_t need, int lane) {
+        while (hi < need) {
+            const uint32_t w = ((hi >> 2) + lane * 4) & (kRingW - 1);
+            *reinterpret_cast<u32x4s*>(&ring[w]) = pend;
+            if (w < 24) *reinterpret_cast<u32x4s*>(&ring[kRingW + w]) = pend;
+            hi += kSlice;
+            pend = *reinterpret_cast<const u32x4s*>(sbase + hi + lane * 16);
+        }
+    }
+    __device__ __forceinline__ void words(uint32_t o, uint32_t (&w)[5]) const {
+        const uint32_t* p = ring + ((o >> 2) & (kRingW - 1));
+        const uint32_t sh = o & 3;
+        const uint32_t x0 = p[0], x1 = p[1], x2 = p[2], x3 = p[3], x4 = p[4], x5 = p[5];
+        w[0] = __builtin_amdgcn_alignbyte(x1, x0, sh);
+        w[1] = __builtin_amdgcn_alignbyte(x2, x1, sh);
+        w[2] = __builtin_amdgcn_alignbyte(x3, x2, sh);
+        w[3] = __builtin_amdgcn_alignbyte(x4, x3, sh);
+        w[4] = __builtin_amdgcn_alignbyte(x5, x4, sh);
+    }
+};
+
+__device__ __forceinline__ int64_t wave_min64(int64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int64_t u = __shfl_xor(v, o, 64);
+        v = u < v ? u : v;
+    }
+    return v;
+}
+__device__ __forceinline__ int64_t wave_max64(int64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int64_t u = __shfl_xor(v, o, 64);
+        v = u > v ? u : v;
+    }
+    return v;
+}
+
+// A lane's cursor over its listed deviated pieces (uint4 {base offset, member, blen | nl << 8 |
+// status << 16 | basedig << 18, rank}), in 32-bit lane coordinates: the current piece spans
+// [pos, pend) at shift delta before it; nxt (the next entry) is loaded one piece ahead, so a
+// piece boundary costs no dependent memory round trip.
+struct LaneCursor {
+    const uint4* dl;
+    uint32_t i, n;
+    uint4 cur, nxt;
+    uint32_t pos, pend, nl, sl, blen, nstart;  // nstart: lane offset of the next piece
+    int32_t delta;
+    uint64_t st64;
+    bool basedig;
+
+    __device__ uint4 entry(const SimDev& S, uint32_t j) const {
+        return j < n ? dl[j] : uint4{(uint32_t)S.boff[S.N], 0u, 0u, S.N};
+    }
+    __device__ void set(const SimDev& S, const LaneView& V) {
+        if (cur.w >= S.N) {  // past the last deviated piece
+            pos = pend = nstart = 0xFFFFFFF0u;
+            nl = sl = blen = 0;
+            st64 = 0;
+            basedig = true;
+            return;
+        }
+        blen = cur.z & 0xFFu;
+        nl = (cur.z >> 8) & 0xFFu;
+        const uint8_t s = (uint8_t)((cur.z >> 16) & 3u);
+        sl = status_len(s);
+        st64 = status_u64(s);
+        basedig = (cur.z >> 18) & 1u;
+        const uint32_t sep = cur.w + 1 < S.N ? 1u : 0u;
+        const uint32_t dl = basedig ? blen - nl - 5u - sep : dec_len(V.incrow[cur.y]);
+        const uint32_t plen = nl + sl + dl + sep;
+        pos = (uint32_t)((int32_t)cur.x + delta);
+        pend = pos + plen;
+        nstart = nxt.w >= S.N ? 0xFFFFFFF0u : (uint32_t)((int32_t)nxt.x + delta + (int32_t)plen - (int32_t)blen);
+    }
+    __device__ void init(const SimDev& S, const LaneView& V, const uint4* list, uint32_t cnt) {
+        dl = list;
+        n = cnt;
+        i = 0;
+        delta = 0;
+        cur = entry(S, 0);
+        nxt = entry(S, 1);
+        set(S, V);
+    }
+    __device__ void advance(const SimDev& S, const LaneView& V) {
+        delta += (int32_t)(pend - pos) - (int32_t)blen;
+        cur = nxt;
+        i++;
+        nxt = entry(S, i + 1);
+        set(S, V);
+    }
+    __device__ Piece piece(const SimDev& S, const LaneView& V) const { return V.piece(cur.w); }
+};
+
+// byte q of a lane's string by a cursor copy that may walk past several pieces (rare path)
+__device__ uint8_t lane_byte(const SimDev& S, const LaneView& V, LaneCursor& C, uint32_t q) {
+    while (q >= C.pend && C.cur.w < S.N) C.advance(S, V);
+    if (q < C.pos || C.cur.w >= S.N) return S.sbase[(uint32_t)((int32_t)q - C.delta)];
+    return V.piece_byte(V.piece(C.cur.w), q - C.pos);
+}
+
+// Every live local node whose view changed: one node per lane, the wave's 64 chains in lockstep
+// over a shared LDS ring of the base string. A view with more deviated pieces than its list holds,
+// or a wave whose lanes drift further apart than the ring allows, uses the L2 path
+// (lane_checksum).
 __global__ __launch_bounds__(256) void k_ck_lanes(SimDev S) {
+    __shared__ __attribute__((aligned(16))) uint32_t rings[4][kRingW + 24];
+    const int lane = threadIdx.x & 63;
     const uint32_t lv = blockIdx.x * blockDim.x + threadIdx.x;
-    if (lv >= S.NL || S.dead[S.v0 + lv] || !S.dirty[lv]) return;
-    S.checksum[lv] = lane_checksum(S, lv);
+    const bool act = lv < S.NL && !S.dead[S.v0 + lv] && S.dirty[lv];
+    if (__ballot(act) == 0) return;  // wave-uniform
+    const uint32_t N = S.N;
+    const uint64_t row = (uint64_t)(act ? lv : 0) * N;
+    const LaneView V{S, S.st + row, S.inc + row, S.dev + (uint64_t)(act ? lv : 0) * S.W};
+    // pass 1: length, last deviation, the running shift's range; the deviated pieces are listed
+    // (address order) for the main loop, which then never scans the bitmap or chases member
+    // tables at a piece boundary
+    int64_t dtot = 0, dlo = 0, dhi = 0;
+    uint32_t last = NONE, nd = 0;
+    uint4* dl = S.dlist + (uint64_t)(act ? lv : 0) * S.dcap;
+    if (act) {
+        for (uint32_t w = 0; w < S.W; w++) {
+            uint32_t bits = V.dev[w];
+            while (bits) {
+                const uint32_t k = (w << 5) + __builtin_ctz(bits);
+                bits &= bits - 1;
+                const uint32_t a = S.sorted[k];
+                const uint8_t st = V.strow[a] & ST_MASK;
+                const int64_t x = V.incrow[a], x0 = S.inc0[a];
+                int64_t d = (int64_t)status_len(st) - 5;
+                if (x != x0) d += (int64_t)dec_len(x) - (int64_t)dec_len(x0);
+                if (nd < S.dcap) {
+                    const uint32_t bpos = (uint32_t)S.boff[k];
+                    const uint32_t blen = (uint32_t)(S.boff[k + 1] - bpos);
+                    const uint32_t nl = (uint32_t)(S.noff[a + 1] - S.noff[a]);
+                    dl[nd] = uint4{bpos, a, blen | (nl << 8) | ((uint32_t)st << 16) | ((x == x0 ? 1u : 0u) << 18),
+                                   k};
+                }
+                nd++;
+                dtot += d;
+                dlo = dtot < dlo ? dtot : dlo;
+                dhi = dtot > dhi ? dtot : dhi;
+                last = k;
+            }
+        }
+    }
+    const uint64_t len = (uint64_t)((int64_t)S.boff[N] + dtot);
+    const bool ring_ok = __ballot(act && (nd > S.dcap || len > 0x7FFFFFF0ull)) == 0 &&
+                         wave_max64(act ? dhi : 0) - wave_min64(act ? dlo : 0) <= (int64_t)(kRing - 2 * kSlice - 256);
+    if (!ring_ok) {  // wave-uniform
+        if (act) {
+            S.checksum[lv] = lane_checksum(S, lv);
+            S.dirty[lv] = 0;
+        }
+        return;
+    }
+    const int64_t DLO = wave_min64(act ? dlo : 0);
+    uint32_t h = 0, g = 0, f = 0;
+    uint32_t iters = 0;
+    if (act) {
+        if (len <= 24) {
+            uint8_t buf[24];
+            Fwd F;
+            F.init(V);
+            for (uint32_t q = 0; q < (uint32_t)len; q++) buf[q] = F.byte(V, q);
+            h = fh::hash32(fh::PtrSrc{buf}, (uint32_t)len);
+        } else {
+            uint8_t tail[20];
+            uint32_t kd = last;
+            int64_t da = dtot;
+            Piece P{};
+            uint64_t E = 0, B = 0;
+            if (kd != NONE) {
+                P = V.piece(kd);
+                E = (uint64_t)((int64_t)S.boff[kd + 1] + da);
+                B = E - P.plen;
+            }
+            for (int i = 19; i >= 0; i--) {
+                const uint64_t q = len - 20 + (uint64_t)i;
+                while (kd != NONE && q < B) {
+                    da -= (int64_t)P.plen - (int64_t)P.blen;
+                    kd = V.prev_dev(kd);
+                    if (kd != NONE) {
+                        P = V.piece(kd);
+                        E = (uint64_t)((int64_t)S.boff[kd + 1] + da);
+                        B = E - P.plen;
+                    }
+                }
+                tail[i] = (kd != NONE && q >= B && q < E) ? V.piece_byte(P, (uint32_t)(q - B))
+                                                           : S.sbase[(uint64_t)((int64_t)q - da)];
+            }
+            auto tw = [&](int o) {
+                return (uint32_t)tail[o] | ((uint32_t)tail[o + 1] << 8) | ((uint32_t)tail[o + 2] << 16) |
+                       ((uint32_t)tail[o + 3] << 24);
+            };
+            h = (uint32_t)len;
+            g = fh::kC1 * (uint32_t)len;
+            f = g;
+            h ^= premix(tw(16));
+            h = fh::rotr(h, 19) * 5 + 0xe6546b64u;
+            h ^= premix(tw(4));
+            h = fh::rotr(h, 19) * 5 + 0xe6546b64u;
+            g ^= premix(tw(12));
+            g = fh::rotr(g, 19) * 5 + 0xe6546b64u;
+            g ^= premix(tw(8));
+            g = fh::rotr(g, 19) * 5 + 0xe6546b64u;
+            f += premix(tw(0));
+            f = fh::rotr(f, 19) + 113;
+            iters = (uint32_t)((len - 1) / 20);
+        }
+    }
+    const uint32_t maxit = (uint32_t)wave_max64((int64_t)iters);
+    BaseRing R{rings[threadIdx.x >> 6], 0, {}};
+    R.start(S.sbase, lane);
+    LaneCursor C;
+    if (act) C.init(S, V, dl, nd);
+    const uint32_t lead = (uint32_t)(160 - DLO) + kSlice;  // ring lookahead past a group's q0
+    // Groups of 4 chunks: the words of all 4 are read from the ring assuming they are clean (one
+    // straight run of 21 LDS words at the current shift), the rare chunks that touch a deviated
+    // piece are redone through the cursor, then the 4 chunks' pre-mixes and the serial chain run
+    // straight-line (instruction-level parallelism for a lone wave per SIMD).
+    for (uint32_t c0 = 0; c0 < maxit; c0 += 4) {
+        const uint32_t q0 = c0 * 20;
+        R.ensure(S.sbase, q0 + lead, lane);
+        if (c0 >= iters) continue;
+        while (__builtin_expect(q0 >= C.pend, 0) && C.cur.w < N) C.advance(S, V);
+        uint32_t wd[4][5];
+        {
+            const uint32_t o = (uint32_t)((int32_t)q0 - C.delta);
+            const uint32_t* p = R.ring + ((o >> 2) & (kRingW - 1));
+            const uint32_t sh = o & 3;
+            uint32_t x[21];
+#pragma unroll
+            for (int i = 0; i < 21; i++) x[i] = p[i];  // (the ring mirrors 8 words past its end)
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+#pragma unroll
+                for (int i = 0; i < 5; i++) wd[j][i] = __builtin_amdgcn_alignbyte(x[5 * j + i + 1], x[5 * j + i], sh);
+        }
+        const uint32_t ng = iters - c0 < 4 ? iters - c0 : 4;  // chunks of this group
+        if (__builtin_expect(q0 + 20 * ng > C.pos, 0)) {
+            // the first chunk that touches the piece under the cursor, and every later one of the group
+            uint32_t j0 = C.pos > q0 ? (C.pos - q0) / 20 : 0;
+            for (uint32_t j = j0; j < ng; j++) {
+                const uint32_t qj = q0 + 20 * j;
+                while (qj >= C.pend && C.cur.w < N) C.advance(S, V);
+                uint32_t w[5];
+                if (qj + 20 <= C.pos) {
+                    R.words((uint32_t)((int32_t)qj - C.delta), w);
+                } else if (C.basedig && qj + 20 <= C.nstart) {
+                    // one deviated piece whose only difference is its status: base bytes at shift
+                    // delta before the status, the status characters, base bytes at shift
+                    // delta + sl - 5 after
+                    const int32_t s0 = (int32_t)(C.pos + C.nl), s1 = s0 + (int32_t)C.sl;
+                    uint32_t w1[5], w2[5];
+                    const uint32_t o1 = (uint32_t)((int32_t)qj - C.delta);
+                    R.words(o1, w1);
+                    R.words(o1 - C.sl + 5u, w2);
+#pragma unroll
+                    for (int i = 0; i < 5; i++) {
+                        const int32_t qb = (int32_t)qj + 4 * i;
+                        const int32_t m1 = s0 - qb, m2 = s1 - qb;
+                        const uint32_t k1 = m1 <= 0 ? 0u : m1 >= 4 ? 0xFFFFFFFFu : (1u << (8 * m1)) - 1u;
+                        const uint32_t k2 = m2 <= 0 ? 0u : m2 >= 4 ? 0xFFFFFFFFu : (1u << (8 * m2)) - 1u;
+                        const int32_t so = -m1;  // status byte index of this word's byte 0
+                        const uint32_t sw = so >= 0 ? (so < 8 ? (uint32_t)(C.st64 >> (8 * so)) : 0u)
+                                                    : (so > -4 ? (uint32_t)(C.st64 << (8 * -so)) : 0u);
+                        w[i] = (w1[i] & k1) | (sw & k2 & ~k1) | (w2[i] & ~k2);
+                    }
+                } else {
+                    LaneCursor T = C;  // bytes across piece boundaries: a copy walks ahead
+                    for (int i = 0; i < 5; i++) {
+                        uint32_t x = 0;
+                        for (int b = 0; b < 4; b++) x |= (uint32_t)lane_byte(S, V, T, qj + 4 * i + b) << (8 * b);
+                        w[i] = x;
+                    }
+                }
+#pragma unroll
+                for (int jj = 0; jj < 4; jj++)
+                    if ((uint32_t)jj == j)
+#pragma unroll
+                        for (int i = 0; i < 5; i++) wd[jj][i] = w[i];
+            }
+        }
+        uint32_t p5[4], p6[4], p7[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            p5[j] = premix(wd[j][3]);
+            p6[j] = premix(wd[j][2]);
+            p7[j] = premix(wd[j][1] + wd[j][4] * fh::kC1);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if ((uint32_t)j < ng) {
+                h += wd[j][0];
+                g += wd[j][1];
+                f += wd[j][2];
+                h = fh::rotr(h ^ p5[j], 19) * 5 + 0xe6546b64u + wd[j][4];
+                g = fh::rotr(g ^ p6[j], 19) * 5 + 0xe6546b64u + wd[j][0];
+                f = fh::rotr(f ^ p7[j], 19) * 5 + 0xe6546b64u + wd[j][3];
+                f += g;
+                g += f;
+            }
+        }
+    }
+    if (!act) return;
+    if (len > 24) {
+        g = fh::rotr(g, 11) * fh::kC1;
+        g = fh::rotr(g, 17) * fh::kC1;
+        f = fh::rotr(f, 11) * fh::kC1;
+        f = fh::rotr(f, 17) * fh::kC1;
+        h = fh::rotr(h + g, 19);
+        h = h * 5 + 0xe6546b64u;
+        h = fh::rotr(h, 17) * fh::kC1;
+        h = fh::rotr(h + f, 19);
+        h = h * 5 + 0xe6546b64u;
+        h = fh::rotr(h, 17) * fh::kC1;
+    }
+    S.checksum[lv] = h;
     S.dirty[lv] = 0;
 }
 
@@ -1446,6 +1867,7 @@ struct Sim {
     DevBuf<Change> chg;
     DevBuf<Timer> tim;
     DevBuf<Rec> pool;
+    DevBuf<uint4> dlist;
     DevBuf<unsigned long long> stats, cursor;
     MsgBuf out, in;
     Scratch ws;
@@ -1731,7 +2153,9 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
             if (k + 1 < n) base.push_back(';');
         }
         boff[n] = base.size();
-        base.resize(base.size() + 64, 0);  // the lane chain reads up to 24 bytes past a chunk
+        // the lane chain reads up to 24 bytes past a chunk; the LDS ring loads whole 1-KB slices
+        // up to ~3 KB past the end
+        base.resize(((base.size() + 64 + 1023) & ~1023ull) + 32768, 0);
 
         const uint64_t NN = (uint64_t)NL * n;
         std::vector<uint32_t> killed;
@@ -1764,6 +2188,12 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
         S.bounds.reserve(nshards + 1);
         S.pool.reserve(2 * L1 * cap + arena);
         S.cand.reserve((uint64_t)S.grid * n);
+        // lane checksums list each view's deviated pieces (16 B each); a view with more than dcap
+        // falls back to scanning its bitmap
+        uint64_t dcap = std::min<uint64_t>(n, 2ull * ndead + 256);
+        const uint64_t dbudget = env_u64("RP_SIM_DLIST_BYTES", 16ull << 30);
+        if (L1 * dcap * 16 > dbudget) dcap = std::max<uint64_t>(1, dbudget / (16 * L1));
+        S.dlist.reserve(L1 * dcap);
         // per-block string buffer: names + ';' + "suspect" + 20 digits per member (also the
         // iterator's scratch)
         const uint64_t strcap = std::max<uint64_t>(S.nt.h_bytes.size() + 29ull * n + 64, 5ull * n + 64);
@@ -1796,6 +2226,7 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
         d.ping_n = S.ping_n.p; d.leg_n = S.leg_n.p; d.helpers = S.helpers.p; d.nhelp = S.nhelp.p;
         d.leg_nk = S.leg_nk.p; d.cand = S.cand.p;
         d.strbuf = S.strbuf.p; d.strcap = (strcap + 255) & ~255ull;
+        d.dlist = S.dlist.p; d.dcap = (uint32_t)dcap;
         d.resp_idx = S.resp_idx.p; d.lresp_idx = S.lresp_idx.p;
         d.stats = S.stats.p; d.err = S.err.p; d.round = 0;
         {
