@@ -63,8 +63,7 @@ def _free_port():
     return p
 
 
-def test_dist_two_ranks_gloo_matches_unsharded(gpu, tmp_path):
-    n, k, seed, susp, rounds, G = 400, 6, 7, 25, 45, 2
+def _run_dist(gpu, tmp_path, G, backend, n=400, k=6, seed=7, susp=25, rounds=45):
     out = str(tmp_path / "dist.npz")
     port = _free_port()
     worker = os.path.join(REPO, "tests", "workers", "dist_sim_worker.py")
@@ -73,7 +72,7 @@ def test_dist_two_ranks_gloo_matches_unsharded(gpu, tmp_path):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(G), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, worker, str(n), str(k), str(seed), str(susp), str(rounds),
-                                       out, "gloo"], env=env))
+                                       out, backend], env=env))
     rcs = [p.wait(timeout=100) for p in procs]
     assert rcs == [0] * G
     d = np.load(out)
@@ -88,3 +87,13 @@ def test_dist_two_ranks_gloo_matches_unsharded(gpu, tmp_path):
     assert conv == int(d["conv"]) >= 0
     assert [ref.stats()[x] for x in gpu._STAT_NAMES] == d["stats"].tolist()
     assert int(d["xbytes"]) > 0
+
+
+def test_dist_two_ranks_gloo_matches_unsharded(gpu, tmp_path):
+    _run_dist(gpu, tmp_path, 2, "gloo")
+
+
+def test_dist_one_rank_nccl_matches_unsharded(gpu, tmp_path):
+    """The RCCL transport (device tensors, rp_copy on torch's stream, all_to_all_single over
+    nccl) on the one GPU of the box; a multi-GPU node runs the same code with G ranks."""
+    _run_dist(gpu, tmp_path, 1, "nccl")
