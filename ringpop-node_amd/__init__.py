@@ -19,7 +19,7 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librpamd.so")
+LIB_PATH = os.environ.get("RP_AMD_LIB") or os.path.join(_HERE, "librpamd.so")  # override: A/B builds
 NULL_ID = 0xFFFFFFFF
 
 _lib = None

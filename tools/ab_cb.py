@@ -32,7 +32,7 @@ ref = None
 times = {}
 for rd in range(a.rounds + 1):
     for d, r in rings.items():
-        for kpl in ("4", "4a3", "2"):
+        for kpl in ("4", "2"):
             os.environ["RP_LOOKUP_KPL"] = kpl[0]
             os.environ["RP_LOOKUP_ABLATE"] = kpl[2:] if "a" in kpl else "0"
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
