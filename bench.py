@@ -168,6 +168,29 @@ def sim_bench(rpa, local, n=10_000, kill_pct=1, seed=11, max_rounds=300, max_sec
     return out
 
 
+def sim_cpu_baseline(n=10_000, kill_pct=1, seed=11, min_seconds=10.0, max_rounds=40):
+    """The C4 simulator on this host: the oracle (oracle/orc_sim.c, one thread: the reference
+    runs one view per process, this restatement runs every view sequentially) for as many rounds
+    as fit in ~min_seconds. Reported as ms per round next to the device's."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle
+    S = _synth()
+    k = max(1, n * kill_pct // 100)
+    names = [S.c2_addr(i) for i in range(n)]
+    sim = pyoracle.Sim(names, S.c3_members(n)[2], S.kill_set(n, k, seed), seed=seed, susp_rounds=25,
+                       now0=1434401518824 + 10 ** 9)
+    rounds, t0 = 0, time.perf_counter()
+    while rounds < max_rounds:
+        sim.step()
+        rounds += 1
+        if time.perf_counter() - t0 >= min_seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": dt * 1e3 / rounds, "unit": "ms/round", "cores": 1, "kind": "port",
+            "sample": "C4 (%d members, %d killed): the first %d rounds of oracle/orc_sim.c, one thread, %.1f s"
+                      % (n, k, rounds, dt)}
+
+
 def pmc_traffic():
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
@@ -282,6 +305,8 @@ def main():
         if not args.no_cpu:
             th = args.cpu_threads or min(16, os.cpu_count() or 1)
             out["cpu_baseline"] = cpu_baseline(servers, args.cpu_keys, th)
+            if args.sim_n and "sim" in out:
+                out["sim"]["cpu_baseline"] = sim_cpu_baseline(args.sim_n)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -997,81 +997,97 @@ __global__ __launch_bounds__(256) void k_ck_lanes(SimDev S) {
     R.start(S.sbase, lane);
     LaneCursor C;
     if (act) C.init(S, V, dl, nd);
-    const uint32_t lead = (uint32_t)(160 - DLO) + kSlice;  // ring lookahead past a group's q0
-    // Groups of 4 chunks: the words of all 4 are read from the ring assuming they are clean (one
-    // straight run of 21 LDS words at the current shift), the rare chunks that touch a deviated
-    // piece are redone through the cursor, then the 4 chunks' pre-mixes and the serial chain run
-    // straight-line (instruction-level parallelism for a lone wave per SIMD).
-    for (uint32_t c0 = 0; c0 < maxit; c0 += 4) {
-        const uint32_t q0 = c0 * 20;
-        R.ensure(S.sbase, q0 + lead, lane);
-        if (c0 >= iters) continue;
-        while (__builtin_expect(q0 >= C.pend, 0) && C.cur.w < N) C.advance(S, V);
-        uint32_t wd[4][5];
-        {
-            const uint32_t o = (uint32_t)((int32_t)q0 - C.delta);
-            const uint32_t* p = R.ring + ((o >> 2) & (kRingW - 1));
-            const uint32_t sh = o & 3;
-            uint32_t x[21];
+    const uint32_t lead = (uint32_t)(240 - DLO) + kSlice;  // ring lookahead past a group's q0
+    // Groups of 4 chunks, software-pipelined: while the serial chain consumes group g, group g+1's
+    // words are read from the ring assuming they are clean (one straight run of 21 LDS words at
+    // the current shift) and pre-mixed, in the same basic block, so the two independent
+    // instruction streams hide each other's latency (a lone wave per SIMD). The rare chunks that
+    // touch a deviated piece are then redone through the cursor.
+    uint32_t wd[4][5], p5[4], p6[4], p7[4];
+    // group words at the cursor's shift (speculative) + their pre-mixes
+    auto produce = [&](uint32_t q, uint32_t (&w)[4][5], uint32_t (&a5)[4], uint32_t (&a6)[4], uint32_t (&a7)[4]) {
+        const uint32_t o = (uint32_t)((int32_t)q - C.delta);
+        const uint32_t* p = R.ring + ((o >> 2) & (kRingW - 1));
+        const uint32_t sh = o & 3;
+        uint32_t x[21];
 #pragma unroll
-            for (int i = 0; i < 21; i++) x[i] = p[i];  // (the ring mirrors 8 words past its end)
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-#pragma unroll
-                for (int i = 0; i < 5; i++) wd[j][i] = __builtin_amdgcn_alignbyte(x[5 * j + i + 1], x[5 * j + i], sh);
-        }
-        const uint32_t ng = iters - c0 < 4 ? iters - c0 : 4;  // chunks of this group
-        if (__builtin_expect(q0 + 20 * ng > C.pos, 0)) {
-            // the first chunk that touches the piece under the cursor, and every later one of the group
-            uint32_t j0 = C.pos > q0 ? (C.pos - q0) / 20 : 0;
-            for (uint32_t j = j0; j < ng; j++) {
-                const uint32_t qj = q0 + 20 * j;
-                while (qj >= C.pend && C.cur.w < N) C.advance(S, V);
-                uint32_t w[5];
-                if (qj + 20 <= C.pos) {
-                    R.words((uint32_t)((int32_t)qj - C.delta), w);
-                } else if (C.basedig && qj + 20 <= C.nstart) {
-                    // one deviated piece whose only difference is its status: base bytes at shift
-                    // delta before the status, the status characters, base bytes at shift
-                    // delta + sl - 5 after
-                    const int32_t s0 = (int32_t)(C.pos + C.nl), s1 = s0 + (int32_t)C.sl;
-                    uint32_t w1[5], w2[5];
-                    const uint32_t o1 = (uint32_t)((int32_t)qj - C.delta);
-                    R.words(o1, w1);
-                    R.words(o1 - C.sl + 5u, w2);
-#pragma unroll
-                    for (int i = 0; i < 5; i++) {
-                        const int32_t qb = (int32_t)qj + 4 * i;
-                        const int32_t m1 = s0 - qb, m2 = s1 - qb;
-                        const uint32_t k1 = m1 <= 0 ? 0u : m1 >= 4 ? 0xFFFFFFFFu : (1u << (8 * m1)) - 1u;
-                        const uint32_t k2 = m2 <= 0 ? 0u : m2 >= 4 ? 0xFFFFFFFFu : (1u << (8 * m2)) - 1u;
-                        const int32_t so = -m1;  // status byte index of this word's byte 0
-                        const uint32_t sw = so >= 0 ? (so < 8 ? (uint32_t)(C.st64 >> (8 * so)) : 0u)
-                                                    : (so > -4 ? (uint32_t)(C.st64 << (8 * -so)) : 0u);
-                        w[i] = (w1[i] & k1) | (sw & k2 & ~k1) | (w2[i] & ~k2);
-                    }
-                } else {
-                    LaneCursor T = C;  // bytes across piece boundaries: a copy walks ahead
-                    for (int i = 0; i < 5; i++) {
-                        uint32_t x = 0;
-                        for (int b = 0; b < 4; b++) x |= (uint32_t)lane_byte(S, V, T, qj + 4 * i + b) << (8 * b);
-                        w[i] = x;
-                    }
-                }
-#pragma unroll
-                for (int jj = 0; jj < 4; jj++)
-                    if ((uint32_t)jj == j)
-#pragma unroll
-                        for (int i = 0; i < 5; i++) wd[jj][i] = w[i];
-            }
-        }
-        uint32_t p5[4], p6[4], p7[4];
+        for (int i = 0; i < 21; i++) x[i] = p[i];  // (the ring mirrors 24 words past its end)
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            p5[j] = premix(wd[j][3]);
-            p6[j] = premix(wd[j][2]);
-            p7[j] = premix(wd[j][1] + wd[j][4] * fh::kC1);
+#pragma unroll
+            for (int i = 0; i < 5; i++) w[j][i] = __builtin_amdgcn_alignbyte(x[5 * j + i + 1], x[5 * j + i], sh);
+            a5[j] = premix(w[j][3]);
+            a6[j] = premix(w[j][2]);
+            a7[j] = premix(w[j][1] + w[j][4] * fh::kC1);
         }
+    };
+    // redo the chunks of the group at q that touch the piece under the cursor (and later ones)
+    auto fixup = [&](uint32_t q, uint32_t ng, uint32_t (&w4)[4][5], uint32_t (&a5)[4], uint32_t (&a6)[4],
+                     uint32_t (&a7)[4]) {
+        const uint32_t j0 = C.pos > q ? (C.pos - q) / 20 : 0;
+        for (uint32_t j = j0; j < ng; j++) {
+            const uint32_t qj = q + 20 * j;
+            while (qj >= C.pend && C.cur.w < N) C.advance(S, V);
+            uint32_t w[5];
+            if (qj + 20 <= C.pos) {
+                R.words((uint32_t)((int32_t)qj - C.delta), w);
+            } else if (C.basedig && qj + 20 <= C.nstart) {
+                // one deviated piece whose only difference is its status: base bytes at shift
+                // delta before the status, the status characters, base bytes at shift
+                // delta + sl - 5 after
+                const int32_t s0 = (int32_t)(C.pos + C.nl), s1 = s0 + (int32_t)C.sl;
+                uint32_t w1[5], w2[5];
+                const uint32_t o1 = (uint32_t)((int32_t)qj - C.delta);
+                R.words(o1, w1);
+                R.words(o1 - C.sl + 5u, w2);
+#pragma unroll
+                for (int i = 0; i < 5; i++) {
+                    const int32_t qb = (int32_t)qj + 4 * i;
+                    const int32_t m1 = s0 - qb, m2 = s1 - qb;
+                    const uint32_t k1 = m1 <= 0 ? 0u : m1 >= 4 ? 0xFFFFFFFFu : (1u << (8 * m1)) - 1u;
+                    const uint32_t k2 = m2 <= 0 ? 0u : m2 >= 4 ? 0xFFFFFFFFu : (1u << (8 * m2)) - 1u;
+                    const int32_t so = -m1;  // status byte index of this word's byte 0
+                    const uint32_t sw = so >= 0 ? (so < 8 ? (uint32_t)(C.st64 >> (8 * so)) : 0u)
+                                                : (so > -4 ? (uint32_t)(C.st64 << (8 * -so)) : 0u);
+                    w[i] = (w1[i] & k1) | (sw & k2 & ~k1) | (w2[i] & ~k2);
+                }
+            } else {
+                LaneCursor T = C;  // bytes across piece boundaries: a copy walks ahead
+                for (int i = 0; i < 5; i++) {
+                    uint32_t x = 0;
+                    for (int b = 0; b < 4; b++) x |= (uint32_t)lane_byte(S, V, T, qj + 4 * i + b) << (8 * b);
+                    w[i] = x;
+                }
+            }
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++)
+                if ((uint32_t)jj == j) {
+#pragma unroll
+                    for (int i = 0; i < 5; i++) w4[jj][i] = w[i];
+                    a5[jj] = premix(w[3]);
+                    a6[jj] = premix(w[2]);
+                    a7[jj] = premix(w[1] + w[4] * fh::kC1);
+                }
+        }
+    };
+    auto ngroup = [&](uint32_t c0) { return c0 >= iters ? 0u : (iters - c0 < 4 ? iters - c0 : 4u); };
+    // group 0
+    R.ensure(S.sbase, lead, lane);
+    if (act && iters) {
+        while (0 >= C.pend && C.cur.w < N) C.advance(S, V);
+        produce(0, wd, p5, p6, p7);
+        if (__builtin_expect(20 * ngroup(0) > C.pos, 0)) fixup(0, ngroup(0), wd, p5, p6, p7);
+    }
+    for (uint32_t c0 = 0; c0 < maxit; c0 += 4) {
+        const uint32_t q1 = (c0 + 4) * 20;  // the next group
+        R.ensure(S.sbase, q1 + lead, lane);
+        const uint32_t ng = ngroup(c0), ng1 = ngroup(c0 + 4);
+        uint32_t nw[4][5], n5[4], n6[4], n7[4];
+        if (ng1) {
+            while (__builtin_expect(q1 >= C.pend, 0) && C.cur.w < N) C.advance(S, V);
+        }
+        // one basic block: the next group's words + pre-mixes beside this group's chain
+        produce(q1, nw, n5, n6, n7);
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             if ((uint32_t)j < ng) {
@@ -1084,6 +1100,15 @@ __global__ __launch_bounds__(256) void k_ck_lanes(SimDev S) {
                 f += g;
                 g += f;
             }
+        }
+        if (__builtin_expect(ng1 && q1 + 20 * ng1 > C.pos, 0)) fixup(q1, ng1, nw, n5, n6, n7);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+#pragma unroll
+            for (int i = 0; i < 5; i++) wd[j][i] = nw[j][i];
+            p5[j] = n5[j];
+            p6[j] = n6[j];
+            p7[j] = n7[j];
         }
     }
     if (!act) return;
