@@ -39,6 +39,7 @@
 // one node's checksum in the middle of a phase, by one workgroup (one chain lane fed by
 // pre-mixing lanes).
 #include <algorithm>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -289,12 +290,16 @@ struct Piece {
     bool basedig;    // the digits are the base piece's (incarnation == inc0)
 };
 
+// the status's checksum spelling as little-endian bytes ("alive" "suspect" "faulty" "leave")
 __device__ __forceinline__ uint64_t status_u64(uint8_t s) {
-    uint64_t v = 0;
-    const uint32_t n = status_len(s);
-    for (uint32_t i = 0; i < n; i++) v |= (uint64_t)status_char(s, i) << (8 * i);
+    uint64_t v = 0x6576696c61ull;        // alive
+    v = s == 1 ? 0x74636570737573ull : v;  // suspect
+    v = s == 2 ? 0x79746c756166ull : v;    // faulty
+    v = s == 3 ? 0x6576616c65ull : v;      // leave
     return v;
 }
+// status_len without branches: lengths 5 7 6 5 as nibbles
+__device__ __forceinline__ uint32_t status_len_nb(uint32_t s) { return (0x5675u >> (4 * (s & 3))) & 15u; }
 
 struct LaneView {
     const SimDev& S;
@@ -826,7 +831,7 @@ __device__ __forceinline__ int64_t wave_max64(int64_t v) {
 struct LaneCursor {
     const uint4* dl;
     uint32_t i, n;
-    uint4 cur, nxt;
+    uint4 cur, nxt, nn;  // nn: prefetched one piece ahead, first used by the advance after next
     uint32_t pos, pend, nl, sl, blen, nstart;  // nstart: lane offset of the next piece
     int32_t delta;
     uint64_t st64;
@@ -835,7 +840,8 @@ struct LaneCursor {
     __device__ uint4 entry(const SimDev& S, uint32_t j) const {
         return j < n ? dl[j] : uint4{(uint32_t)S.boff[S.N], 0u, 0u, S.N};
     }
-    __device__ void set(const SimDev& S, const LaneView& V) {
+    // everything from the list record (pass 1 packed the view's piece length in): no loads
+    __device__ void set(const SimDev& S) {
         if (cur.w >= S.N) {  // past the last deviated piece
             pos = pend = nstart = 0xFFFFFFF0u;
             nl = sl = blen = 0;
@@ -846,31 +852,31 @@ struct LaneCursor {
         blen = cur.z & 0xFFu;
         nl = (cur.z >> 8) & 0xFFu;
         const uint8_t s = (uint8_t)((cur.z >> 16) & 3u);
-        sl = status_len(s);
+        sl = status_len_nb(s);
         st64 = status_u64(s);
         basedig = (cur.z >> 18) & 1u;
-        const uint32_t sep = cur.w + 1 < S.N ? 1u : 0u;
-        const uint32_t dl = basedig ? blen - nl - 5u - sep : dec_len(V.incrow[cur.y]);
-        const uint32_t plen = nl + sl + dl + sep;
+        const uint32_t plen = (cur.z >> 19) & 0xFFu;
         pos = (uint32_t)((int32_t)cur.x + delta);
         pend = pos + plen;
         nstart = nxt.w >= S.N ? 0xFFFFFFF0u : (uint32_t)((int32_t)nxt.x + delta + (int32_t)plen - (int32_t)blen);
     }
-    __device__ void init(const SimDev& S, const LaneView& V, const uint4* list, uint32_t cnt) {
+    __device__ void init(const SimDev& S, const LaneView&, const uint4* list, uint32_t cnt) {
         dl = list;
         n = cnt;
         i = 0;
         delta = 0;
         cur = entry(S, 0);
         nxt = entry(S, 1);
-        set(S, V);
+        nn = entry(S, 2);
+        set(S);
     }
-    __device__ void advance(const SimDev& S, const LaneView& V) {
+    __device__ void advance(const SimDev& S, const LaneView&) {
         delta += (int32_t)(pend - pos) - (int32_t)blen;
         cur = nxt;
+        nxt = nn;
         i++;
-        nxt = entry(S, i + 1);
-        set(S, V);
+        nn = entry(S, i + 2);
+        set(S);
     }
     __device__ Piece piece(const SimDev& S, const LaneView& V) const { return V.piece(cur.w); }
 };
@@ -880,6 +886,41 @@ __device__ uint8_t lane_byte(const SimDev& S, const LaneView& V, LaneCursor& C, 
     while (q >= C.pend && C.cur.w < S.N) C.advance(S, V);
     if (q < C.pos || C.cur.w >= S.N) return S.sbase[(uint32_t)((int32_t)q - C.delta)];
     return V.piece_byte(V.piece(C.cur.w), q - C.pos);
+}
+
+// Pass 1 of a lane checksum: list the view's deviated pieces (address order; the uint4 records
+// of LaneCursor) and return the string's shift range, total, last deviated rank and count.
+__device__ void lane_pass1(const SimDev& S, const LaneView& V, uint4* dl, int64_t& dtot, int64_t& dlo,
+                           int64_t& dhi, uint32_t& last, uint32_t& nd) {
+    dtot = dlo = dhi = 0;
+    last = NONE;
+    nd = 0;
+    for (uint32_t w = 0; w < S.W; w++) {
+        uint32_t bits = V.dev[w];
+        while (bits) {
+            const uint32_t k = (w << 5) + __builtin_ctz(bits);
+            bits &= bits - 1;
+            const uint32_t a = S.sorted[k];
+            const uint8_t st = V.strow[a] & ST_MASK;
+            const int64_t x = V.incrow[a], x0 = S.inc0[a];
+            int64_t d = (int64_t)status_len(st) - 5;
+            if (x != x0) d += (int64_t)dec_len(x) - (int64_t)dec_len(x0);
+            if (nd < S.dcap) {
+                const uint32_t bpos = (uint32_t)S.boff[k];
+                const uint32_t blen = (uint32_t)(S.boff[k + 1] - bpos);
+                const uint32_t nl = (uint32_t)(S.noff[a + 1] - S.noff[a]);
+                const uint32_t plen = (uint32_t)((int64_t)blen + d);
+                if (plen > 0xFFu) nd = S.dcap;  // a piece too long for the record: this lane falls back
+                dl[nd < S.dcap ? nd : 0] =
+                    uint4{bpos, a, blen | (nl << 8) | ((uint32_t)st << 16) | ((x == x0 ? 1u : 0u) << 18) | (plen << 19), k};
+            }
+            nd++;
+            dtot += d;
+            dlo = dtot < dlo ? dtot : dlo;
+            dhi = dtot > dhi ? dtot : dhi;
+            last = k;
+        }
+    }
 }
 
 // Every live local node whose view changed: one node per lane, the wave's 64 chains in lockstep
@@ -901,32 +942,7 @@ __global__ __launch_bounds__(256) void k_ck_lanes(SimDev S) {
     int64_t dtot = 0, dlo = 0, dhi = 0;
     uint32_t last = NONE, nd = 0;
     uint4* dl = S.dlist + (uint64_t)(act ? lv : 0) * S.dcap;
-    if (act) {
-        for (uint32_t w = 0; w < S.W; w++) {
-            uint32_t bits = V.dev[w];
-            while (bits) {
-                const uint32_t k = (w << 5) + __builtin_ctz(bits);
-                bits &= bits - 1;
-                const uint32_t a = S.sorted[k];
-                const uint8_t st = V.strow[a] & ST_MASK;
-                const int64_t x = V.incrow[a], x0 = S.inc0[a];
-                int64_t d = (int64_t)status_len(st) - 5;
-                if (x != x0) d += (int64_t)dec_len(x) - (int64_t)dec_len(x0);
-                if (nd < S.dcap) {
-                    const uint32_t bpos = (uint32_t)S.boff[k];
-                    const uint32_t blen = (uint32_t)(S.boff[k + 1] - bpos);
-                    const uint32_t nl = (uint32_t)(S.noff[a + 1] - S.noff[a]);
-                    dl[nd] = uint4{bpos, a, blen | (nl << 8) | ((uint32_t)st << 16) | ((x == x0 ? 1u : 0u) << 18),
-                                   k};
-                }
-                nd++;
-                dtot += d;
-                dlo = dtot < dlo ? dtot : dlo;
-                dhi = dtot > dhi ? dtot : dhi;
-                last = k;
-            }
-        }
-    }
+    if (act) lane_pass1(S, V, dl, dtot, dlo, dhi, last, nd);
     const uint64_t len = (uint64_t)((int64_t)S.boff[N] + dtot);
     const bool ring_ok = __ballot(act && (nd > S.dcap || len > 0x7FFFFFF0ull)) == 0 &&
                          wave_max64(act ? dhi : 0) - wave_min64(act ? dlo : 0) <= (int64_t)(kRing - 2 * kSlice - 256);
@@ -1126,6 +1142,297 @@ __global__ __launch_bounds__(256) void k_ck_lanes(SimDev S) {
     }
     S.checksum[lv] = h;
     S.dirty[lv] = 0;
+}
+
+// ---- producer/consumer lane checksums
+
+// The chain's initial state from the string's last 20 bytes (farmhashmk Hash32, len > 24), or
+// the whole hash for len <= 24 (returned in h with *done).
+__device__ void lane_chain_init(const SimDev& S, const LaneView& V, uint64_t len, int64_t dtot, uint32_t last,
+                                uint32_t& h, uint32_t& g, uint32_t& f, bool& done) {
+    done = false;
+    if (len <= 24) {
+        uint8_t buf[24];
+        Fwd F;
+        F.init(V);
+        for (uint32_t q = 0; q < (uint32_t)len; q++) buf[q] = F.byte(V, q);
+        h = fh::hash32(fh::PtrSrc{buf}, (uint32_t)len);
+        done = true;
+        return;
+    }
+    uint8_t tail[20];
+    uint32_t kd = last;
+    int64_t da = dtot;
+    Piece P{};
+    uint64_t E = 0, B = 0;
+    if (kd != NONE) {
+        P = V.piece(kd);
+        E = (uint64_t)((int64_t)S.boff[kd + 1] + da);
+        B = E - P.plen;
+    }
+    for (int i = 19; i >= 0; i--) {
+        const uint64_t q = len - 20 + (uint64_t)i;
+        while (kd != NONE && q < B) {
+            da -= (int64_t)P.plen - (int64_t)P.blen;
+            kd = V.prev_dev(kd);
+            if (kd != NONE) {
+                P = V.piece(kd);
+                E = (uint64_t)((int64_t)S.boff[kd + 1] + da);
+                B = E - P.plen;
+            }
+        }
+        tail[i] = (kd != NONE && q >= B && q < E) ? V.piece_byte(P, (uint32_t)(q - B))
+                                                   : S.sbase[(uint64_t)((int64_t)q - da)];
+    }
+    auto tw = [&](int o) {
+        return (uint32_t)tail[o] | ((uint32_t)tail[o + 1] << 8) | ((uint32_t)tail[o + 2] << 16) |
+               ((uint32_t)tail[o + 3] << 24);
+    };
+    h = (uint32_t)len;
+    g = fh::kC1 * (uint32_t)len;
+    f = g;
+    h ^= premix(tw(16));
+    h = fh::rotr(h, 19) * 5 + 0xe6546b64u;
+    h ^= premix(tw(4));
+    h = fh::rotr(h, 19) * 5 + 0xe6546b64u;
+    g ^= premix(tw(12));
+    g = fh::rotr(g, 19) * 5 + 0xe6546b64u;
+    g ^= premix(tw(8));
+    g = fh::rotr(g, 19) * 5 + 0xe6546b64u;
+    f += premix(tw(0));
+    f = fh::rotr(f, 19) + 113;
+}
+
+// x * 5 as one full-rate shift-add (the compiler otherwise may pick a 64-bit multiply-add)
+__device__ __forceinline__ uint32_t mul5(uint32_t x) {
+    uint32_t r;
+    asm("v_lshl_add_u32 %0, %1, 2, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
+__device__ __forceinline__ uint32_t chain_final(uint32_t h, uint32_t g, uint32_t f) {
+    g = fh::rotr(g, 11) * fh::kC1;
+    g = fh::rotr(g, 17) * fh::kC1;
+    f = fh::rotr(f, 11) * fh::kC1;
+    f = fh::rotr(f, 17) * fh::kC1;
+    h = fh::rotr(h + g, 19);
+    h = h * 5 + 0xe6546b64u;
+    h = fh::rotr(h, 17) * fh::kC1;
+    h = fh::rotr(h + f, 19);
+    h = h * 5 + 0xe6546b64u;
+    h = fh::rotr(h, 17) * fh::kC1;
+    return h;
+}
+
+// The 20-byte chunk of a lane's string at qj through its cursor (advancing it): base words at
+// the cursor's shift, a status-only piece as a word overlay, or bytes across pieces.
+__device__ void cursor_chunk(const SimDev& S, const LaneView& V, LaneCursor& C, const BaseRing& R, uint32_t qj,
+                             uint32_t (&w)[5]) {
+    while (qj >= C.pend && C.cur.w < S.N) C.advance(S, V);
+    if (qj + 20 <= C.pos) {
+        R.words((uint32_t)((int32_t)qj - C.delta), w);
+    } else if (C.basedig && qj + 20 <= C.nstart) {
+        const int32_t s0 = (int32_t)(C.pos + C.nl), s1 = s0 + (int32_t)C.sl;
+        uint32_t w1[5], w2[5];
+        const uint32_t o1 = (uint32_t)((int32_t)qj - C.delta);
+        R.words(o1, w1);
+        R.words(o1 - C.sl + 5u, w2);
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+            const int32_t qb = (int32_t)qj + 4 * i;
+            const int32_t m1 = s0 - qb, m2 = s1 - qb;
+            const uint32_t k1 = m1 <= 0 ? 0u : m1 >= 4 ? 0xFFFFFFFFu : (1u << (8 * m1)) - 1u;
+            const uint32_t k2 = m2 <= 0 ? 0u : m2 >= 4 ? 0xFFFFFFFFu : (1u << (8 * m2)) - 1u;
+            const int32_t so = -m1;
+            const uint32_t sw = so >= 0 ? (so < 8 ? (uint32_t)(C.st64 >> (8 * so)) : 0u)
+                                        : (so > -4 ? (uint32_t)(C.st64 << (8 * -so)) : 0u);
+            w[i] = (w1[i] & k1) | (sw & k2 & ~k1) | (w2[i] & ~k2);
+        }
+    } else {
+        LaneCursor T = C;
+        for (int i = 0; i < 5; i++) {
+            uint32_t x = 0;
+            for (int b = 0; b < 4; b++) x |= (uint32_t)lane_byte(S, V, T, qj + 4 * i + b) << (8 * b);
+            w[i] = x;
+        }
+    }
+}
+
+// Every live local node whose view changed, 64 nodes per workgroup: wave 0 runs the 64 serial
+// chains (only the chain's ~17 dependent-ish ops per chunk), waves 1-3 produce the chunks' words
+// and pre-mixes one epoch ahead (each a 4-chunk group per epoch, from a shared LDS ring of the
+// base string kept by wave 1) into double-buffered LDS. A view's checksum is one serial chain,
+// so this is what bounds a refresh when few waves share a SIMD (the sharded case).
+constexpr int kEp = 12;  // chunks per epoch (3 producers x 4)
+__global__ __launch_bounds__(256) void k_ck_pc(SimDev S) {
+    __shared__ __attribute__((aligned(16))) uint32_t ring[kRingW + 24];
+    __shared__ __attribute__((aligned(16))) u32x4s stage[2][kEp][2][64];
+    __shared__ uint32_t s_nd[64], s_iters[64];
+    __shared__ int32_t s_red[4];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t lv = blockIdx.x * 64 + lane;
+    const bool act = lv < S.NL && !S.dead[S.v0 + lv] && S.dirty[lv];
+    if (!__syncthreads_or(act ? 1 : 0)) return;
+    const uint32_t N = S.N;
+    const uint64_t row = (uint64_t)(act ? lv : 0) * N;
+    const LaneView V{S, S.st + row, S.inc + row, S.dev + (uint64_t)(act ? lv : 0) * S.W};
+    uint4* dl = S.dlist + (uint64_t)(act ? lv : 0) * S.dcap;
+    uint32_t h = 0, g = 0, f = 0;
+    uint64_t len = 0;
+    bool done = false;
+    if (wv == 0) {
+        int64_t dtot = 0, dlo = 0, dhi = 0;
+        uint32_t last = NONE, nd = 0;
+        if (act) lane_pass1(S, V, dl, dtot, dlo, dhi, last, nd);
+        len = (uint64_t)((int64_t)S.boff[N] + dtot);
+        const bool bad = act && (nd > S.dcap || len > 0x7FFFFFF0ull);
+        uint32_t iters = 0;
+        if (act && !bad) {
+            lane_chain_init(S, V, len, dtot, last, h, g, f, done);
+            iters = done ? 0u : (uint32_t)((len - 1) / 20);
+        }
+        s_nd[lane] = nd;
+        s_iters[lane] = iters;
+        const int64_t DLO = wave_min64(act ? dlo : 0), DHI = wave_max64(act ? dhi : 0);
+        // the ring holds two epochs ahead of the producers plus a slice being refilled
+        const bool okw = __ballot(bad) == 0 && DHI - DLO <= (int64_t)(kRing - 3 * kSlice - 4 * kEp * 20 - 256);
+        const int64_t MX = wave_max64((int64_t)iters);
+        if (lane == 0) {
+            s_red[0] = okw ? 1 : 0;
+            s_red[1] = (int32_t)DLO;
+            s_red[2] = (int32_t)MX;
+        }
+    }
+    __syncthreads();
+    if (!s_red[0]) {  // block-uniform: too many deviations for the list or the ring
+        if (wv == 0 && act) {
+            S.checksum[lv] = lane_checksum(S, lv);
+            S.dirty[lv] = 0;
+        }
+        return;
+    }
+    const int32_t DLO = s_red[1];
+    const uint32_t maxit = (uint32_t)s_red[2];
+    const uint32_t nep = (maxit + kEp - 1) / kEp;
+    const uint32_t lead = (uint32_t)(2 * kEp * 20 + 64 - DLO) + kSlice;
+    BaseRing R;
+    R.ring = ring;
+    R.hi = 0;
+    LaneCursor C;
+    uint32_t iters = s_iters[lane];
+    if (wv >= 1) {
+        if (act && iters) C.init(S, V, dl, s_nd[lane]);
+        if (wv == 1) {
+            R.start(S.sbase, lane);
+            R.ensure(S.sbase, lead, lane);  // epochs 0 and 1
+        }
+    }
+    // producer p (1..3) owns chunks [e*kEp + 4(p-1), +4) of epoch e
+    auto produce = [&](uint32_t e) {
+        const uint32_t c0 = e * kEp + 4 * (wv - 1);
+        const uint32_t ng = c0 >= iters ? 0u : (iters - c0 < 4 ? iters - c0 : 4u);
+        if (!ng) return;
+        const uint32_t q = c0 * 20;
+        while (q >= C.pend && C.cur.w < N) C.advance(S, V);
+        uint32_t w4[4][5];
+        {
+            const uint32_t o = (uint32_t)((int32_t)q - C.delta);
+            const uint32_t* p = R.ring + ((o >> 2) & (kRingW - 1));
+            const uint32_t sh = o & 3;
+            uint32_t x[21];
+#pragma unroll
+            for (int i = 0; i < 21; i++) x[i] = p[i];
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+#pragma unroll
+                for (int i = 0; i < 5; i++) w4[j][i] = __builtin_amdgcn_alignbyte(x[5 * j + i + 1], x[5 * j + i], sh);
+        }
+        if (__builtin_expect(q + 20 * ng > C.pos, 0)) {
+            const uint32_t j0 = C.pos > q ? (C.pos - q) / 20 : 0;
+            for (uint32_t j = j0; j < ng; j++) {
+                uint32_t w[5];
+                cursor_chunk(S, V, C, R, q + 20 * j, w);
+#pragma unroll
+                for (int jj = 0; jj < 4; jj++)
+                    if ((uint32_t)jj == j)
+#pragma unroll
+                        for (int i = 0; i < 5; i++) w4[jj][i] = w[i];
+            }
+        }
+        const int b = e & 1;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int slot = 4 * (wv - 1) + j;
+            stage[b][slot][0][lane] = u32x4s{w4[j][0], w4[j][1], w4[j][2], w4[j][3]};
+            stage[b][slot][1][lane] = u32x4s{w4[j][4], premix(w4[j][3]), premix(w4[j][2]),
+                                             premix(w4[j][1] + w4[j][4] * fh::kC1)};
+        }
+    };
+    __syncthreads();  // the ring holds epochs 0 and 1
+    if (wv >= 1 && act) produce(0);
+    __syncthreads();
+#ifdef RP_CK_PROF
+    uint64_t t_work = 0, t_bar = 0, t0 = clock64();
+#endif
+    for (uint32_t e = 0; e < nep; e++) {
+#ifdef RP_CK_PROF
+        const uint64_t ta = clock64();
+#endif
+        if (wv == 0) {
+            if (act) {
+                const int b = e & 1;
+                const uint32_t c0 = e * kEp;
+                auto step = [&](const u32x4s& x0, const u32x4s& x1) {
+                    h += x0.x;
+                    g += x0.y;
+                    f += x0.z;
+                    h = mul5(fh::rotr(h ^ x1.y, 19)) + 0xe6546b64u + x1.x;
+                    g = mul5(fh::rotr(g ^ x1.z, 19)) + 0xe6546b64u + x0.x;
+                    f = mul5(fh::rotr(f ^ x1.w, 19)) + 0xe6546b64u + x0.w;
+                    f += g;
+                    g += f;
+                };
+                if (__ballot(c0 + kEp > iters) == 0) {
+                    // every lane takes the whole epoch: all loads issued up front, no branches
+                    u32x4s x[kEp][2];
+#pragma unroll
+                    for (int j = 0; j < kEp; j++) {
+                        x[j][0] = stage[b][j][0][lane];
+                        x[j][1] = stage[b][j][1][lane];
+                    }
+#pragma unroll
+                    for (int j = 0; j < kEp; j++) step(x[j][0], x[j][1]);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < kEp; j++)
+                        if (c0 + j < iters) step(stage[b][j][0][lane], stage[b][j][1][lane]);
+                }
+            }
+        } else {
+            if (act && e + 1 < nep) produce(e + 1);
+            // the ring one epoch further ahead (the producers of the next iteration read it after
+            // the barrier; nobody reads the slices being replaced any more)
+            if (wv == 1) R.ensure(S.sbase, (e + 2) * kEp * 20 + lead, lane);
+        }
+#ifdef RP_CK_PROF
+        const uint64_t tb = clock64();
+        t_work += tb - ta;
+#endif
+        __syncthreads();
+#ifdef RP_CK_PROF
+        t_bar += clock64() - tb;
+#endif
+    }
+#ifdef RP_CK_PROF
+    if (lane == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2))
+        printf("ckprof blk %u wave %d: epochs %u maxit %u total %llu work %llu bar %llu (cyc/chunk %.1f)\n", blockIdx.x,
+               wv, nep, maxit, (unsigned long long)(clock64() - t0), (unsigned long long)t_work,
+               (unsigned long long)t_bar, (double)(clock64() - t0) / (maxit ? maxit : 1));
+#endif
+    if (wv == 0 && act) {
+        S.checksum[lv] = done ? h : chain_final(h, g, f);
+        S.dirty[lv] = 0;
+    }
 }
 
 // ---- membership / dissemination / suspicion on one node
@@ -1902,9 +2209,27 @@ struct Sim {
     int64_t round = 0;
     int next_stage = 0;  // 0..4 within a round
 
+    uint32_t cus = 0;  // compute units of the device (first refresh)
     void refresh_checksums() {
         if (NL == 0) return;
-        hipLaunchKernelGGL(k_ck_lanes, dim3(grid_for(NL, 256, 1u << 20)), dim3(256), 0, st, d);
+        // One chain per lane either way. With no more 64-node groups than CUs (a shard, C4) each
+        // group gets a whole CU: its chain wave plus three producer waves (k_ck_pc, ~130 cycles
+        // per chunk). With more groups than CUs the machine is issue-bound on the chunks'
+        // multiplies, and one wave per group without producers (k_ck_lanes) does less work.
+        // RP_SIM_CK=pc|lanes overrides.
+        if (cus == 0) {
+            int dev = 0, n = 0;
+            RP_HIP(hipGetDevice(&dev));
+            RP_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+            cus = (uint32_t)(n > 0 ? n : 1);
+        }
+        const uint32_t groups = (NL + 63) / 64;
+        const char* m = getenv("RP_SIM_CK");
+        const bool pc = m ? strcmp(m, "lanes") != 0 : groups <= cus;
+        if (pc)
+            hipLaunchKernelGGL(k_ck_pc, dim3(groups), dim3(256), 0, st, d);
+        else
+            hipLaunchKernelGGL(k_ck_lanes, dim3(grid_for(NL, 256, 1u << 20)), dim3(256), 0, st, d);
         RP_HIP(hipGetLastError());
     }
 

@@ -64,3 +64,21 @@ def test_sim_vs_oracle(gpu, orc, n, k, seed, susp):
         gs, gi = g.view(v)
         os_, oi = o.view(v)
         assert np.array_equal(gs, os_) and np.array_equal(gi, oi)
+
+
+@pytest.mark.parametrize("kernel", ["pc", "lanes"])
+def test_sim_checksum_kernels_vs_oracle(gpu, orc, monkeypatch, kernel):
+    """Both lane-checksum kernels (k_ck_pc: chain wave + producer waves; k_ck_lanes: one wave per
+    64 nodes), forced through RP_SIM_CK, against the oracle on a case with many deviations."""
+    monkeypatch.setenv("RP_SIM_CK", kernel)
+    S = synth()
+    n, k, seed, susp = 900, 60, 5, 6
+    names = [S.c2_addr(i) for i in range(n)]
+    inc0 = S.c3_members(n)[2]
+    dead = S.kill_set(n, k, seed)
+    g = gpu.GossipSim(names, inc0, dead, seed=seed, suspicion_rounds=susp)
+    o = orc.Sim(names, inc0, dead, seed=seed, susp_rounds=susp, now0=1434401518824 + 10 ** 9)
+    for r in range(30):
+        g.step()
+        o.step()
+        assert np.array_equal(g.checksums(), o.checksums()), "round %d" % r
