@@ -4,7 +4,7 @@ set -u
 OUT=${1:-gpurun_out/pmc_ub}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-for grp in "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum" "TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum" "TCP_TOTAL_READ_sum TCP_PENDING_STALL_CYCLES_sum" "TCP_READ_TAGCONFLICT_STALL_CYCLES_sum TCP_TCR_TCP_STALL_CYCLES_sum"; do
+for grp in "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum"; do
   tag=$(echo $grp | cut -d' ' -f1 )
   timeout -s KILL 60 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$OUT/$tag" -o run -- ./tools/ub_lookup 5120 q > "$OUT/$tag.log" 2>&1
   echo "pmc $tag rc=$?"

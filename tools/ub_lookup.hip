@@ -35,7 +35,7 @@ typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
 
 constexpr int T = 256, LEN = 36, W4 = 9;
 
-enum { NONE = 0, R16, R8R16, LINE64, COOP64, R16U, R16A2, R8R16U };
+enum { NONE = 0, R16, R8R16, LINE64, COOP64, R16U, R16A2, R8R16U, R16W4, R16W8 };
 
 // per-key table probe; KPL keys are issued together so their loads overlap
 template <int MODE, int KPL>
@@ -53,6 +53,22 @@ __device__ __forceinline__ void probe(const uint32_t (&h)[KPL], const uint32_t* 
         for (int k = 0; k < KPL; k++) {
             const uint32_t l = (uint32_t)(((uint64_t)h[k] * nlines64) >> 32);
             v[k] = *reinterpret_cast<const u32x4*>(tab + l * 16 + (h[k] & 3) * 4);
+        }
+#pragma unroll
+        for (int k = 0; k < KPL; k++) {
+            r[k][0] ^= v[k].x + v[k].w;
+            r[k][1] ^= v[k].y;
+            r[k][2] ^= v[k].z;
+        }
+    } else if constexpr (MODE == R16W4 || MODE == R16W8) {
+        // a 16-B load at a 4-B (R16W4) or 8-B (R16W8) aligned, not 16-B aligned, address
+        const uint32_t nent = nlines64 * 64 / 3 - 16;
+        u32x4 v[KPL];
+#pragma unroll
+        for (int k = 0; k < KPL; k++) {
+            const uint32_t pos = (uint32_t)(((uint64_t)h[k] * nent) >> 32);
+            const uintptr_t a = (uintptr_t)(reinterpret_cast<const uint8_t*>(tab) + 3ull * pos) & (MODE == R16W4 ? ~(uintptr_t)3 : ~(uintptr_t)7);
+            v[k] = *reinterpret_cast<const u32x4_a1*>(a);
         }
 #pragma unroll
         for (int k = 0; k < KPL; k++) {
@@ -486,6 +502,8 @@ int main(int argc, char** argv) {
         k_ub<R16, 4, false><<<grid, T>>>(keys, n, tab, nl, out);
         k_ub<R16U, 4, false><<<grid, T>>>(keys, n, tab, nl, out);
         k_ub<R16A2, 4, false><<<grid, T>>>(keys, n, tab, nl, out);
+        k_ub<R16W4, 4, false><<<grid, T>>>(keys, n, tab, nl, out);
+        k_ub<R16W8, 4, false><<<grid, T>>>(keys, n, tab, nl, out);
         k_ub<R8R16U, 4, false><<<grid, T>>>(keys, n, tab, nl, out);
         k_ub<COOP64, 4, false><<<grid, T>>>(keys, n, tab, nl, out);
         CK(hipDeviceSynchronize());
@@ -512,6 +530,8 @@ int main(int argc, char** argv) {
         row<R16, 4, false>("r16", keys, n, tab, out, grid);
         row<R16U, 4, false>("r16u", keys, n, tab, out, grid);
         row<R16A2, 4, false>("r16a2", keys, n, tab, out, grid);
+        row<R16W4, 4, false>("r16w4", keys, n, tab, out, grid);
+        row<R16W8, 4, false>("r16w8", keys, n, tab, out, grid);
         row<R8R16, 4, false>("r8r16", keys, n, tab, out, grid);
         row<R8R16U, 4, false>("r8r16u", keys, n, tab, out, grid);
         row<COOP64, 4, false>("coop64", keys, n, tab, out, grid);
