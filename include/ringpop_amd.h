@@ -40,6 +40,10 @@ int rp_device_count(int *n);
 uint32_t rp_hash32(const char *s, size_t len);
 int rp_hash32_batch_dev(const uint8_t *d_bytes, const uint64_t *d_off, uint64_t n, uint32_t *d_out,
                         void *stream);
+/* farmhash32 of ONE long device string d_bytes[0, len) (the checksum strings of
+ * lib/ring/index.js:96-105 and lib/membership/index.js:48-75 are hashed this way): one serial
+ * chain fed by producer lanes. d_out[0] = hash (d_out must hold 2 uint32). */
+int rp_hash32_long_dev(const uint8_t *d_bytes, uint64_t len, uint32_t *d_out, void *stream);
 
 /* Synthetic key stream: n UUID-v4-format 36-byte keys [k0, k0+n) of `seed`,
  * written at 36-byte stride. */

@@ -4,7 +4,7 @@
 // string runs on one lane. Everything in a chunk that does not depend on the chain state
 // (the five words and the three Murmur pre-mixes rotr(x*c1,17)*c2 of d, c and b+e*c1) is
 // computed ahead by the other 192 lanes of the workgroup into a double-buffered LDS window;
-// the chain lane then does ~7 dependent ops per chunk. Per-view parallel checksums (the
+// the chain lane then does 5 dependent ops per chunk (the regrouping below). Per-view parallel checksums (the
 // simulator) use one lane per view instead.
 #include "rp_farmhash.h"
 #include "rp_hashlong.h"
@@ -20,6 +20,32 @@ __device__ __forceinline__ uint32_t premix(uint32_t x) { return fh::rotr(x * fh:
 
 __device__ __forceinline__ uint32_t ld32(const uint8_t* p, uint64_t o) {
     return (uint32_t)p[o] | ((uint32_t)p[o + 1] << 8) | ((uint32_t)p[o + 2] << 16) | ((uint32_t)p[o + 3] << 24);
+}
+
+// The chain in "pre-added" form. farmhashmk's chunk step (h += a; g += b; f += c; then three
+// Murmur rounds; f += g; g += f) is regrouped so that each state word enters a chunk with the
+// chunk's addend already folded in (hp = h + a, gp = g + b, fp = f + c), and the combine with
+// the next chunk's addends is one precomputed constant per word:
+//   r_x = rotr(xp ^ premix_x, 19)                         (x = h, g, f)
+//   hp' = 5 r_h + (K + e + a')
+//   fp' = 5 (r_f + r_g) + (2K + a + d + c')               (= f + g + c' of the original)
+//   gp' = 5 (r_f + 2 r_g) + (3K + 2a + d + b')            (= g + f + b')
+// where a', b', c' are the next chunk's words (0 after the last chunk, which leaves plain h, g,
+// f). The dependent path per chunk drops from 7 to 5 VALU ops; the six per-chunk words
+// {premix(d), premix(c), premix(b + e c1), K + e + a', 2K + a + d + c', 3K + 2a + d + b'} are
+// independent of the chain and precomputed by the producer lanes.
+constexpr uint32_t kK = 0xe6546b64u;
+
+// (a << sh) + b as one v_lshl_add_u32 (inline asm keeps the compiler from re-associating the
+// chain's sums into a longer dependent sequence)
+template <int SH>
+__device__ __forceinline__ uint32_t lshl_add(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(SH), "v"(b));
+    return r;
+}
+__device__ __forceinline__ uint32_t mul5_add(uint32_t x, uint32_t c) {  // 5x + c: two dependent ops
+    return lshl_add<2>(x, x + c);
 }
 
 __global__ __launch_bounds__(kHlThreads) void k_hash_long(const uint8_t* __restrict__ s, uint64_t len_host,
@@ -43,46 +69,58 @@ __global__ __launch_bounds__(kHlThreads) void k_hash_long(const uint8_t* __restr
     }
     const bool aligned = (reinterpret_cast<uintptr_t>(s) & 3) == 0;
     const uint64_t iters = (len - 1) / 20;
+    auto word = [&](uint64_t o) -> uint32_t {
+        return aligned ? *reinterpret_cast<const uint32_t*>(s + o) : ld32(s, o);
+    };
     auto fill = [&](int buf, uint64_t c0, int t0, int nt) {
         for (int j = t0; j < kWin; j += nt) {
             const uint64_t c = c0 + j;
             if (c >= iters) break;
             const uint64_t o = c * 20;
-            uint32_t a, b, cc, d, e;
-            if (aligned) {
-                const uint32_t* w = reinterpret_cast<const uint32_t*>(s + o);
-                a = w[0]; b = w[1]; cc = w[2]; d = w[3]; e = w[4];
-            } else {
-                a = ld32(s, o); b = ld32(s, o + 4); cc = ld32(s, o + 8); d = ld32(s, o + 12); e = ld32(s, o + 16);
+            const uint32_t a = word(o), b = word(o + 4), cc = word(o + 8), d = word(o + 12), e = word(o + 16);
+            uint32_t a2 = 0, b2 = 0, c2 = 0;
+            if (c + 1 < iters) {
+                a2 = word(o + 20);
+                b2 = word(o + 24);
+                c2 = word(o + 28);
             }
             uint32_t* r = win[buf][j];
-            r[0] = a; r[1] = b; r[2] = cc; r[3] = d;
-            r[4] = e; r[5] = premix(d); r[6] = premix(cc); r[7] = premix(b + e * fh::kC1);
+            *reinterpret_cast<uint4*>(r) = uint4{premix(d), premix(cc), premix(b + e * fh::kC1), kK + e + a2};
+            *reinterpret_cast<uint2*>(r + 4) = uint2{2u * kK + a + d + c2, 3u * kK + 2u * a + d + b2};
         }
     };
-    // chain state (lane 0 only)
-    uint32_t h = 0, g = 0, f = 0;
+    // chain state (lane 0 only), pre-added with chunk 0's words
+    uint32_t hp = 0, gp = 0, fp = 0;
     if (tid == 0) {
         const uint32_t L = (uint32_t)len;
-        h = L;
-        g = fh::kC1 * L;
-        f = g;
+        uint32_t h = L, g = fh::kC1 * L, f = g;
         const uint32_t a0 = premix(ld32(s, len - 4)), a1 = premix(ld32(s, len - 8)), a2 = premix(ld32(s, len - 16)),
                        a3 = premix(ld32(s, len - 12)), a4 = premix(ld32(s, len - 20));
         h ^= a0;
-        h = fh::rotr(h, 19) * 5 + 0xe6546b64u;
+        h = fh::rotr(h, 19) * 5 + kK;
         h ^= a2;
-        h = fh::rotr(h, 19) * 5 + 0xe6546b64u;
+        h = fh::rotr(h, 19) * 5 + kK;
         g ^= a1;
-        g = fh::rotr(g, 19) * 5 + 0xe6546b64u;
+        g = fh::rotr(g, 19) * 5 + kK;
         g ^= a3;
-        g = fh::rotr(g, 19) * 5 + 0xe6546b64u;
+        g = fh::rotr(g, 19) * 5 + kK;
         f += a4;
         f = fh::rotr(f, 19) + 113;
+        hp = h + word(0);
+        gp = g + word(4);
+        fp = f + word(8);
     }
     fill(0, 0, tid, kHlThreads);
     __syncthreads();
     const uint64_t nwin = (iters + kWin - 1) / kWin;
+    auto step = [&](const uint4 x, const uint2 y) {
+        const uint32_t rh = __builtin_amdgcn_alignbit(hp ^ x.x, hp ^ x.x, 19);
+        const uint32_t rg = __builtin_amdgcn_alignbit(gp ^ x.y, gp ^ x.y, 19);
+        const uint32_t rf = __builtin_amdgcn_alignbit(fp ^ x.z, fp ^ x.z, 19);
+        hp = mul5_add(rh, x.w);
+        fp = mul5_add(rf + rg, y.x);
+        gp = mul5_add(lshl_add<1>(rg, rf), y.y);
+    };
     for (uint64_t w = 0; w < nwin; w++) {
         const int cur = (int)(w & 1);
         if (tid >= 64) {
@@ -90,31 +128,34 @@ __global__ __launch_bounds__(kHlThreads) void k_hash_long(const uint8_t* __restr
         } else if (tid == 0) {
             const uint64_t c0 = w * kWin;
             const int n = (int)((iters - c0) < (uint64_t)kWin ? (iters - c0) : kWin);
-            for (int j = 0; j < n; j++) {
-                const uint32_t* r = win[cur][j];
-                const uint32_t a = r[0], b = r[1], c = r[2], d = r[3], e = r[4];
-                h += a;
-                g += b;
-                f += c;
-                h = fh::rotr(h ^ r[5], 19) * 5 + 0xe6546b64u + e;
-                g = fh::rotr(g ^ r[6], 19) * 5 + 0xe6546b64u + a;
-                f = fh::rotr(f ^ r[7], 19) * 5 + 0xe6546b64u + d;
-                f += g;
-                g += f;
+            int j = 0;
+            for (; j + 8 <= n; j += 8) {  // the LDS reads of 8 chunks issued ahead of their steps
+                uint4 x[8];
+                uint2 y[8];
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    x[q] = *reinterpret_cast<const uint4*>(win[cur][j + q]);
+                    y[q] = *reinterpret_cast<const uint2*>(win[cur][j + q] + 4);
+                }
+#pragma unroll
+                for (int q = 0; q < 8; q++) step(x[q], y[q]);
             }
+            for (; j < n; j++)
+                step(*reinterpret_cast<const uint4*>(win[cur][j]), *reinterpret_cast<const uint2*>(win[cur][j] + 4));
         }
         __syncthreads();
     }
     if (tid == 0) {
+        uint32_t h = hp, g = gp, f = fp;  // the last chunk's next-words were 0
         g = fh::rotr(g, 11) * fh::kC1;
         g = fh::rotr(g, 17) * fh::kC1;
         f = fh::rotr(f, 11) * fh::kC1;
         f = fh::rotr(f, 17) * fh::kC1;
         h = fh::rotr(h + g, 19);
-        h = h * 5 + 0xe6546b64u;
+        h = h * 5 + kK;
         h = fh::rotr(h, 17) * fh::kC1;
         h = fh::rotr(h + f, 19);
-        h = h * 5 + 0xe6546b64u;
+        h = h * 5 + kK;
         h = fh::rotr(h, 17) * fh::kC1;
         out[0] = h;
         out[1] = 1;

@@ -1618,6 +1618,14 @@ int rp_hash32_batch_dev(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t 
     });
 }
 
+int rp_hash32_long_dev(const uint8_t* d_bytes, uint64_t len, uint32_t* d_out, void* stream) {
+    return guard([&] {
+        RP_REQUIRE(d_out && (d_bytes || len == 0), "hash32_long_dev: null buffer");
+        RP_REQUIRE(len < (1ull << 32), "hash32_long_dev: at most 2^32-1 bytes");
+        rp::hash_long(d_bytes, len, nullptr, nullptr, d_out, rp::as_stream(stream));
+    });
+}
+
 int rp_gen_uuid_keys_dev(uint32_t seed, uint64_t k0, uint64_t n, uint8_t* d_out, void* stream) {
     return guard([&] {
         if (!n) return;

@@ -275,3 +275,17 @@ def test_window_kernel_slow_paths_vs_oracle(gpu, orc, nserv, R, layout, monkeypa
         got = d_o.cpu().numpy().view(np.uint32).reshape(n, w)
         assert np.array_equal(d_c.cpu().numpy(), wc), nrep
         assert np.array_equal(got, want), nrep
+
+
+@pytest.mark.parametrize("length", [0, 7, 24, 25, 44, 45, 164, 165, 20 * 1024 + 1, 20 * 1024 + 20,
+                                    20 * 1024 * 3 + 7, 100_003, 3_620_017])
+def test_device_long_hash_vs_oracle(gpu, orc, length):
+    """rp_hash32_long_dev (the checksum strings' serial chain, k_hash_long) at lengths around
+    the 20-byte chunk, the 8-chunk unroll and the 1024-chunk LDS window boundaries."""
+    rng = np.random.default_rng(length)
+    b = rng.integers(0, 256, size=length + 1, dtype=np.uint8)
+    d = torch.from_numpy(b).cuda()
+    out = torch.zeros(2, dtype=torch.int32, device="cuda")
+    gpu.check(gpu.lib().rp_hash32_long_dev(d.data_ptr(), length, out.data_ptr(), None))
+    torch.cuda.synchronize()
+    assert int(out.cpu().numpy().view(np.uint32)[0]) == orc.hash32(bytes(b[:length]))
