@@ -110,43 +110,76 @@ __global__ __launch_bounds__(kHlThreads) void k_hash_long(const uint8_t* __restr
         gp = g + word(4);
         fp = f + word(8);
     }
+    __shared__ uint32_t s_h;
+    if (tid == 0) s_h = hp;  // the h chain runs on wave 1 (lane 64)
     fill(0, 0, tid, kHlThreads);
     __syncthreads();
+    if (tid == 64) hp = s_h;
     const uint64_t nwin = (iters + kWin - 1) / kWin;
-    auto step = [&](const uint4 x, const uint2 y) {
-        const uint32_t rh = __builtin_amdgcn_alignbit(hp ^ x.x, hp ^ x.x, 19);
+#ifdef RP_CK_PROF
+    uint64_t t_chain = 0;
+    const uint64_t t_start = clock64();
+#endif
+    // One wave issues about one VALU op per 4 cycles, so a lone chain is issue-bound: h (which
+    // never mixes with g and f before the finalisation) runs on lane 64 while lane 0 runs the
+    // coupled (g, f) pair; waves 2-3 produce the next window.
+    auto step_gf = [&](const uint4 x, const uint2 y) {
         const uint32_t rg = __builtin_amdgcn_alignbit(gp ^ x.y, gp ^ x.y, 19);
         const uint32_t rf = __builtin_amdgcn_alignbit(fp ^ x.z, fp ^ x.z, 19);
-        hp = mul5_add(rh, x.w);
         fp = mul5_add(rf + rg, y.x);
         gp = mul5_add(lshl_add<1>(rg, rf), y.y);
     };
+    auto step_h = [&](const uint4 x) {
+        const uint32_t rh = __builtin_amdgcn_alignbit(hp ^ x.x, hp ^ x.x, 19);
+        hp = mul5_add(rh, x.w);
+    };
     for (uint64_t w = 0; w < nwin; w++) {
         const int cur = (int)(w & 1);
-        if (tid >= 64) {
-            if (w + 1 < nwin) fill(cur ^ 1, (w + 1) * kWin, tid - 64, kHlThreads - 64);
-        } else if (tid == 0) {
+        if (tid >= 128) {
+            if (w + 1 < nwin) fill(cur ^ 1, (w + 1) * kWin, tid - 128, kHlThreads - 128);
+        } else if (tid == 0 || tid == 64) {
+#ifdef RP_CK_PROF
+            const uint64_t tc0 = clock64();
+#endif
             const uint64_t c0 = w * kWin;
             const int n = (int)((iters - c0) < (uint64_t)kWin ? (iters - c0) : kWin);
-            int j = 0;
-            for (; j + 8 <= n; j += 8) {  // the LDS reads of 8 chunks issued ahead of their steps
-                uint4 x[8];
-                uint2 y[8];
+            if (tid == 0) {
+                int j = 0;
+                for (; j + 8 <= n; j += 8) {  // the LDS reads of 8 chunks issued ahead of their steps
+                    uint4 x[8];
+                    uint2 y[8];
 #pragma unroll
-                for (int q = 0; q < 8; q++) {
-                    x[q] = *reinterpret_cast<const uint4*>(win[cur][j + q]);
-                    y[q] = *reinterpret_cast<const uint2*>(win[cur][j + q] + 4);
+                    for (int q = 0; q < 8; q++) {
+                        x[q] = *reinterpret_cast<const uint4*>(win[cur][j + q]);
+                        y[q] = *reinterpret_cast<const uint2*>(win[cur][j + q] + 4);
+                    }
+#pragma unroll
+                    for (int q = 0; q < 8; q++) step_gf(x[q], y[q]);
                 }
+                for (; j < n; j++)
+                    step_gf(*reinterpret_cast<const uint4*>(win[cur][j]),
+                            *reinterpret_cast<const uint2*>(win[cur][j] + 4));
+            } else {
+                int j = 0;
+                for (; j + 8 <= n; j += 8) {
+                    uint4 x[8];
 #pragma unroll
-                for (int q = 0; q < 8; q++) step(x[q], y[q]);
+                    for (int q = 0; q < 8; q++) x[q] = *reinterpret_cast<const uint4*>(win[cur][j + q]);
+#pragma unroll
+                    for (int q = 0; q < 8; q++) step_h(x[q]);
+                }
+                for (; j < n; j++) step_h(*reinterpret_cast<const uint4*>(win[cur][j]));
             }
-            for (; j < n; j++)
-                step(*reinterpret_cast<const uint4*>(win[cur][j]), *reinterpret_cast<const uint2*>(win[cur][j] + 4));
+#ifdef RP_CK_PROF
+            if (tid == 0) t_chain += clock64() - tc0;
+#endif
         }
         __syncthreads();
     }
+    if (tid == 64) s_h = hp;
+    __syncthreads();
     if (tid == 0) {
-        uint32_t h = hp, g = gp, f = fp;  // the last chunk's next-words were 0
+        uint32_t h = s_h, g = gp, f = fp;  // the last chunk's next-words were 0
         g = fh::rotr(g, 11) * fh::kC1;
         g = fh::rotr(g, 17) * fh::kC1;
         f = fh::rotr(f, 11) * fh::kC1;
@@ -159,6 +192,10 @@ __global__ __launch_bounds__(kHlThreads) void k_hash_long(const uint8_t* __restr
         h = fh::rotr(h, 17) * fh::kC1;
         out[0] = h;
         out[1] = 1;
+#ifdef RP_CK_PROF
+        printf("hlprof iters %llu total %llu chain %llu cycles (%.1f per chunk)\n", (unsigned long long)iters,
+               (unsigned long long)(clock64() - t_start), (unsigned long long)t_chain, (double)t_chain / iters);
+#endif
     }
 }
 

@@ -552,6 +552,15 @@ __device__ uint32_t lane_checksum(const SimDev& S, uint32_t lv) {
     return h;
 }
 
+// (a << SH) + b as one v_lshl_add_u32 (inline asm: the compiler would re-associate the chain's
+// sums into a longer dependent sequence)
+template <int SH>
+__device__ __forceinline__ uint32_t lshl_add(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(SH), "v"(b));
+    return r;
+}
+
 // Membership.computeChecksum (index.js:48-75) of local node lv by one workgroup, without
 // materialising the string: the view's deviated pieces are listed in address order with their
 // lane offsets (a scan of the deviation bitmap + a prefix sum of the length differences), then
@@ -595,6 +604,10 @@ struct TabCursor {
 };
 
 __device__ void block_checksum(const SimDev& S, uint32_t lv, uint8_t* scratch, Lds& L) {
+#ifdef RP_CK_PROF
+    const uint64_t bt0 = clock64();
+    uint64_t bt_chain = 0, bt_fill = 0;
+#endif
     const uint32_t N = S.N;
     const uint64_t row = (uint64_t)lv * N;
     const LaneView V{S, S.st + row, S.inc + row, S.dev + (uint64_t)lv * S.W};
@@ -645,6 +658,9 @@ __device__ void block_checksum(const SimDev& S, uint32_t lv, uint8_t* scratch, L
         run += (int32_t)tot;
     }
     T.dtot = run;
+#ifdef RP_CK_PROF
+    const uint64_t bt1 = clock64();
+#endif
     __threadfence_block();
     __syncthreads();
     const uint64_t len = (uint64_t)((int64_t)S.boff[N] + run);
@@ -714,36 +730,79 @@ __device__ void block_checksum(const SimDev& S, uint32_t lv, uint8_t* scratch, L
         fill(0, 0, tid, kT);
         __syncthreads();
         const uint64_t nwin = (iters + kHashWin - 1) / kHashWin;
+        uint32_t gq = g - f, fq = 2u * f - g, gq2 = 2u * (g - f);  // f = fq + gq, g = fq + gq2
         for (uint64_t w = 0; w < nwin; w++) {
             const int cur = (int)(w & 1);
             if (tid >= 64) {
+#ifdef RP_CK_PROF
+                const uint64_t tf0 = clock64();
+#endif
                 if (w + 1 < nwin) fill(cur ^ 1, (w + 1) * kHashWin, tid - 64, kT - 64);
+#ifdef RP_CK_PROF
+                bt_fill += clock64() - tf0;
+#endif
             } else if (tid == 0) {
+#ifdef RP_CK_PROF
+                const uint64_t tc0 = clock64();
+#endif
                 // the serial chain; the next chunk's 8 words are read from LDS while this one
                 // is hashed (the chain is ~7 dependent ops, an LDS read ~100 cycles)
                 const uint64_t c0 = w * kHashWin;
                 const int n = (int)((iters - c0) < (uint64_t)kHashWin ? (iters - c0) : kHashWin);
                 typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+                // Deferred combine: the state is (h, fq, gq, gq2) with f = fq + gq, g = fq + gq2
+                // (gq2 = 2 gq, built from the same rotate), so the chunk's "f += g; g += f" is
+                // folded into the next chunk's add3s: 5 dependent ops per chunk instead of 7.
                 const u32x4v* rw = reinterpret_cast<const u32x4v*>(&L.win[cur][0][0]);
-                u32x4v x0 = rw[0], x1 = rw[1];
-                for (int j = 0; j < n; j++) {
-                    const u32x4v y0 = rw[2 * (j + 1)], y1 = rw[2 * (j + 1) + 1];  // (j + 1 < kHashWin + 1)
+                auto step = [&](const u32x4v x0, const u32x4v x1) {
                     const uint32_t a = x0.x, b = x0.y, c = x0.z, d = x0.w, e = x1.x;
-                    h += a;
-                    g += b;
-                    f += c;
-                    h = fh::rotr(h ^ x1.y, 19) * 5 + 0xe6546b64u + e;
-                    g = fh::rotr(g ^ x1.z, 19) * 5 + 0xe6546b64u + a;
-                    f = fh::rotr(f ^ x1.w, 19) * 5 + 0xe6546b64u + d;
-                    f += g;
-                    g += f;
-                    x0 = y0;
-                    x1 = y1;
+                    const uint32_t ka = 0xe6546b64u + a;
+                    const uint32_t hp = h + a, fp = fq + gq + c, gp = fq + gq2 + b;
+                    const uint32_t rh = fh::rotr(hp ^ x1.y, 19), rg = fh::rotr(gp ^ x1.z, 19),
+                                   rf = fh::rotr(fp ^ x1.w, 19);
+                    h = lshl_add<2>(rh, rh + (0xe6546b64u + e));
+                    gq = lshl_add<2>(rg, rg + ka);
+                    gq2 = lshl_add<3>(rg, lshl_add<1>(rg, 2u * ka));
+                    fq = lshl_add<2>(rf, rf + (0xe6546b64u + d));
+                };
+                // LDS reads issued 8 chunks at a time, the next batch's before this batch's steps
+                // (an LDS read is ~100 cycles, a chain step ~40)
+                int j = 0;
+                if (n >= 8) {
+                    u32x4v x[2][8][2];
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        x[0][q][0] = rw[2 * q];
+                        x[0][q][1] = rw[2 * q + 1];
+                    }
+                    for (; j + 8 <= n; j += 8) {
+                        const bool nx = j + 16 <= n;
+                        if (nx) {
+#pragma unroll
+                            for (int q = 0; q < 8; q++) {
+                                x[1][q][0] = rw[2 * (j + 8 + q)];
+                                x[1][q][1] = rw[2 * (j + 8 + q) + 1];
+                            }
+                        }
+#pragma unroll
+                        for (int q = 0; q < 8; q++) step(x[0][q][0], x[0][q][1]);
+#pragma unroll
+                        for (int q = 0; q < 8; q++) {
+                            x[0][q][0] = x[1][q][0];
+                            x[0][q][1] = x[1][q][1];
+                        }
+                    }
                 }
+                for (; j < n; j++) step(rw[2 * j], rw[2 * j + 1]);
+#ifdef RP_CK_PROF
+                bt_chain += clock64() - tc0;
+#endif
             }
             __syncthreads();
         }
         if (tid == 0) {
+            f = fq + gq;
+            g = fq + gq2;
             g = fh::rotr(g, 11) * fh::kC1;
             g = fh::rotr(g, 17) * fh::kC1;
             f = fh::rotr(f, 11) * fh::kC1;
@@ -760,6 +819,12 @@ __device__ void block_checksum(const SimDev& S, uint32_t lv, uint8_t* scratch, L
         S.checksum[lv] = h;
         S.dirty[lv] = 0;
     }
+#ifdef RP_CK_PROF
+    if ((tid == 0 || tid == 64) && blockIdx.x == 0)
+        printf("bckprof tid %d lv %u: table %llu total %llu chain %llu fill %llu cycles\n", tid, lv,
+               (unsigned long long)(bt1 - bt0), (unsigned long long)(clock64() - bt0), (unsigned long long)bt_chain,
+               (unsigned long long)bt_fill);
+#endif
     __syncthreads();
 }
 
@@ -1263,8 +1328,11 @@ __device__ void cursor_chunk(const SimDev& S, const LaneView& V, LaneCursor& C, 
 // and pre-mixes one epoch ahead (each a 4-chunk group per epoch, from a shared LDS ring of the
 // base string kept by wave 1) into double-buffered LDS. A view's checksum is one serial chain,
 // so this is what bounds a refresh when few waves share a SIMD (the sharded case).
-constexpr int kEp = 12;  // chunks per epoch (3 producers x 4)
-__global__ __launch_bounds__(256) void k_ck_pc(SimDev S) {
+// NP producer waves (3: 256-thread blocks; 7: 512-thread blocks, two waves per SIMD), each
+// producing 4 chunks per epoch.
+template <int NP>
+__global__ __launch_bounds__(64 * (NP + 1)) void k_ck_pc(SimDev S) {
+    constexpr int kEp = 4 * NP;  // chunks per epoch
     __shared__ __attribute__((aligned(16))) uint32_t ring[kRingW + 24];
     __shared__ __attribute__((aligned(16))) u32x4s stage[2][kEp][2][64];
     __shared__ uint32_t s_nd[64], s_iters[64];
@@ -1393,15 +1461,26 @@ __global__ __launch_bounds__(256) void k_ck_pc(SimDev S) {
                     g += f;
                 };
                 if (__ballot(c0 + kEp > iters) == 0) {
-                    // every lane takes the whole epoch: all loads issued up front, no branches
-                    u32x4s x[kEp][2];
+                    // every lane takes the whole epoch: loads issued a 4-chunk group ahead, no
+                    // branches
+                    u32x4s x[2][4][2];
 #pragma unroll
-                    for (int j = 0; j < kEp; j++) {
-                        x[j][0] = stage[b][j][0][lane];
-                        x[j][1] = stage[b][j][1][lane];
+                    for (int j = 0; j < 4; j++) {
+                        x[0][j][0] = stage[b][j][0][lane];
+                        x[0][j][1] = stage[b][j][1][lane];
                     }
 #pragma unroll
-                    for (int j = 0; j < kEp; j++) step(x[j][0], x[j][1]);
+                    for (int q = 0; q < NP; q++) {
+                        if (q + 1 < NP) {
+#pragma unroll
+                            for (int j = 0; j < 4; j++) {
+                                x[(q + 1) & 1][j][0] = stage[b][4 * (q + 1) + j][0][lane];
+                                x[(q + 1) & 1][j][1] = stage[b][4 * (q + 1) + j][1][lane];
+                            }
+                        }
+#pragma unroll
+                        for (int j = 0; j < 4; j++) step(x[q & 1][j][0], x[q & 1][j][1]);
+                    }
                 } else {
 #pragma unroll
                     for (int j = 0; j < kEp; j++)
@@ -2226,8 +2305,10 @@ struct Sim {
         const uint32_t groups = (NL + 63) / 64;
         const char* m = getenv("RP_SIM_CK");
         const bool pc = m ? strcmp(m, "lanes") != 0 : groups <= cus;
-        if (pc)
-            hipLaunchKernelGGL(k_ck_pc, dim3(groups), dim3(256), 0, st, d);
+        if (pc && !(m && !strcmp(m, "pc3")))
+            hipLaunchKernelGGL(k_ck_pc<7>, dim3(groups), dim3(512), 0, st, d);
+        else if (pc)
+            hipLaunchKernelGGL(k_ck_pc<3>, dim3(groups), dim3(256), 0, st, d);
         else
             hipLaunchKernelGGL(k_ck_lanes, dim3(grid_for(NL, 256, 1u << 20)), dim3(256), 0, st, d);
         RP_HIP(hipGetLastError());
