@@ -698,6 +698,29 @@ __device__ void block_checksum(const SimDev& S, uint32_t lv, uint8_t* scratch, L
             f += premix(tw(0));
             f = fh::rotr(f, 19) + 113;
         }
+        // The chain in pre-added form (as rp_hashlong.hip): the state enters chunk j as
+        // hp = h + a_j, gp = g + b_j, fp = f + c_j, and chunk j's record holds
+        // {premix(d), premix(c), premix(b + e c1), K + e + a', 2K + a + d + c', 3K + 2a + d + b'}
+        // with a', b', c' the next chunk's first words (0 after the last chunk).
+        constexpr uint32_t kK = 0xe6546b64u;
+        // the 20 bytes of chunk c as words (TabCursor C is advanced to c)
+        auto chunk_words = [&](TabCursor& C, uint64_t c, uint32_t (&wd)[5]) {
+            const uint64_t q0 = c * 20;
+            while (C.i < T.n && q0 >= T.end[C.i]) C.i++;
+            if (C.i >= T.n || q0 + 20 <= T.pos[C.i]) {
+                const int64_t db = C.i < T.n ? T.db[C.i] : T.dtot;
+                base_words(S.sbase, (uint64_t)((int64_t)q0 - db), wd);
+            } else {
+                TabCursor D = C;
+                for (int i = 0; i < 5; i++) {
+                    uint32_t x = 0;
+                    for (int b = 0; b < 4; b++) x |= (uint32_t)D.byte(V, T, q0 + 4 * i + b) << (8 * b);
+                    wd[i] = x;
+                }
+                C.pk = D.pk;
+                C.P = D.P;
+            }
+        };
         // lanes [t0, t0 + nt) produce window wb = chunks [c0, c0 + kHashWin), a contiguous run each
         auto fill = [&](int wb, uint64_t c0, int idx, int nt) {
             const uint64_t n = (iters - c0) < (uint64_t)kHashWin ? (iters - c0) : kHashWin;
@@ -705,104 +728,101 @@ __device__ void block_checksum(const SimDev& S, uint32_t lv, uint8_t* scratch, L
             const uint64_t ja = (uint64_t)idx * per, jb = ja + per < n ? ja + per : n;
             if (ja >= jb) return;
             TabCursor C{tab_find(T, (c0 + ja) * 20), NONE, Piece{}};
+            uint32_t wd[5];
+            chunk_words(C, c0 + ja, wd);
             for (uint64_t j = ja; j < jb; j++) {
-                const uint64_t q0 = (c0 + j) * 20;
-                while (C.i < T.n && q0 >= T.end[C.i]) C.i++;
-                uint32_t wd[5];
-                if (C.i >= T.n || q0 + 20 <= T.pos[C.i]) {
-                    const int64_t db = C.i < T.n ? T.db[C.i] : T.dtot;
-                    base_words(S.sbase, (uint64_t)((int64_t)q0 - db), wd);
-                } else {
-                    TabCursor D = C;
-                    for (int i = 0; i < 5; i++) {
-                        uint32_t x = 0;
-                        for (int b = 0; b < 4; b++) x |= (uint32_t)D.byte(V, T, q0 + 4 * i + b) << (8 * b);
-                        wd[i] = x;
-                    }
-                    C.pk = D.pk;
-                    C.P = D.P;
-                }
+                uint32_t nx[5] = {0, 0, 0, 0, 0};
+                if (c0 + j + 1 < iters) chunk_words(C, c0 + j + 1, nx);
                 uint32_t* r = L.win[wb][j];
-                r[0] = wd[0]; r[1] = wd[1]; r[2] = wd[2]; r[3] = wd[3];
-                r[4] = wd[4]; r[5] = premix(wd[3]); r[6] = premix(wd[2]); r[7] = premix(wd[1] + wd[4] * fh::kC1);
+                *reinterpret_cast<uint4*>(r) =
+                    uint4{premix(wd[3]), premix(wd[2]), premix(wd[1] + wd[4] * fh::kC1), kK + wd[4] + nx[0]};
+                *reinterpret_cast<uint2*>(r + 4) =
+                    uint2{2u * kK + wd[0] + wd[3] + nx[2], 3u * kK + 2u * wd[0] + wd[3] + nx[1]};
+#pragma unroll
+                for (int i = 0; i < 5; i++) wd[i] = nx[i];
             }
         };
+        // chunk 0's addends, then the h chain moves to lane 64 (it never mixes with g and f
+        // before the finalisation; one wave issues ~1 VALU op per 4 cycles, so splitting the
+        // chain over two waves shortens it)
+        if (tid == 0) {
+            TabCursor C0{0, NONE, Piece{}};
+            uint32_t w0[5];
+            chunk_words(C0, 0, w0);
+            L.u[0] = h + w0[0];
+            g += w0[1];
+            f += w0[2];
+        }
         fill(0, 0, tid, kT);
         __syncthreads();
+        uint32_t hp = L.u[0], gp = g, fp = f;
+        __syncthreads();
         const uint64_t nwin = (iters + kHashWin - 1) / kHashWin;
-        uint32_t gq = g - f, fq = 2u * f - g, gq2 = 2u * (g - f);  // f = fq + gq, g = fq + gq2
         for (uint64_t w = 0; w < nwin; w++) {
             const int cur = (int)(w & 1);
-            if (tid >= 64) {
+            if (tid >= 128) {
 #ifdef RP_CK_PROF
                 const uint64_t tf0 = clock64();
 #endif
-                if (w + 1 < nwin) fill(cur ^ 1, (w + 1) * kHashWin, tid - 64, kT - 64);
+                if (w + 1 < nwin) fill(cur ^ 1, (w + 1) * kHashWin, tid - 128, kT - 128);
 #ifdef RP_CK_PROF
                 bt_fill += clock64() - tf0;
 #endif
-            } else if (tid == 0) {
+            } else if (tid == 0 || tid == 64) {
 #ifdef RP_CK_PROF
                 const uint64_t tc0 = clock64();
 #endif
-                // the serial chain; the next chunk's 8 words are read from LDS while this one
-                // is hashed (the chain is ~7 dependent ops, an LDS read ~100 cycles)
                 const uint64_t c0 = w * kHashWin;
                 const int n = (int)((iters - c0) < (uint64_t)kHashWin ? (iters - c0) : kHashWin);
-                typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-                // Deferred combine: the state is (h, fq, gq, gq2) with f = fq + gq, g = fq + gq2
-                // (gq2 = 2 gq, built from the same rotate), so the chunk's "f += g; g += f" is
-                // folded into the next chunk's add3s: 5 dependent ops per chunk instead of 7.
-                const u32x4v* rw = reinterpret_cast<const u32x4v*>(&L.win[cur][0][0]);
-                auto step = [&](const u32x4v x0, const u32x4v x1) {
-                    const uint32_t a = x0.x, b = x0.y, c = x0.z, d = x0.w, e = x1.x;
-                    const uint32_t ka = 0xe6546b64u + a;
-                    const uint32_t hp = h + a, fp = fq + gq + c, gp = fq + gq2 + b;
-                    const uint32_t rh = fh::rotr(hp ^ x1.y, 19), rg = fh::rotr(gp ^ x1.z, 19),
-                                   rf = fh::rotr(fp ^ x1.w, 19);
-                    h = lshl_add<2>(rh, rh + (0xe6546b64u + e));
-                    gq = lshl_add<2>(rg, rg + ka);
-                    gq2 = lshl_add<3>(rg, lshl_add<1>(rg, 2u * ka));
-                    fq = lshl_add<2>(rf, rf + (0xe6546b64u + d));
-                };
-                // LDS reads issued 8 chunks at a time, the next batch's before this batch's steps
-                // (an LDS read is ~100 cycles, a chain step ~40)
-                int j = 0;
-                if (n >= 8) {
-                    u32x4v x[2][8][2];
-#pragma unroll
-                    for (int q = 0; q < 8; q++) {
-                        x[0][q][0] = rw[2 * q];
-                        x[0][q][1] = rw[2 * q + 1];
-                    }
+                if (tid == 0) {  // (g, f): LDS reads 8 chunks ahead of their steps
+                    auto step = [&](const uint4 x, const uint2 y) {
+                        const uint32_t rg = fh::rotr(gp ^ x.y, 19), rf = fh::rotr(fp ^ x.z, 19);
+                        fp = lshl_add<2>(rf + rg, (rf + rg) + y.x);
+                        const uint32_t s2 = lshl_add<1>(rg, rf);
+                        gp = lshl_add<2>(s2, s2 + y.y);
+                    };
+                    int j = 0;
                     for (; j + 8 <= n; j += 8) {
-                        const bool nx = j + 16 <= n;
-                        if (nx) {
-#pragma unroll
-                            for (int q = 0; q < 8; q++) {
-                                x[1][q][0] = rw[2 * (j + 8 + q)];
-                                x[1][q][1] = rw[2 * (j + 8 + q) + 1];
-                            }
-                        }
-#pragma unroll
-                        for (int q = 0; q < 8; q++) step(x[0][q][0], x[0][q][1]);
+                        uint4 x[8];
+                        uint2 y[8];
 #pragma unroll
                         for (int q = 0; q < 8; q++) {
-                            x[0][q][0] = x[1][q][0];
-                            x[0][q][1] = x[1][q][1];
+                            x[q] = *reinterpret_cast<const uint4*>(L.win[cur][j + q]);
+                            y[q] = *reinterpret_cast<const uint2*>(L.win[cur][j + q] + 4);
                         }
+#pragma unroll
+                        for (int q = 0; q < 8; q++) step(x[q], y[q]);
                     }
+                    for (; j < n; j++)
+                        step(*reinterpret_cast<const uint4*>(L.win[cur][j]),
+                             *reinterpret_cast<const uint2*>(L.win[cur][j] + 4));
+                } else {  // h
+                    auto step = [&](const uint4 x) {
+                        const uint32_t rh = fh::rotr(hp ^ x.x, 19);
+                        hp = lshl_add<2>(rh, rh + x.w);
+                    };
+                    int j = 0;
+                    for (; j + 8 <= n; j += 8) {
+                        uint4 x[8];
+#pragma unroll
+                        for (int q = 0; q < 8; q++) x[q] = *reinterpret_cast<const uint4*>(L.win[cur][j + q]);
+#pragma unroll
+                        for (int q = 0; q < 8; q++) step(x[q]);
+                    }
+                    for (; j < n; j++) step(*reinterpret_cast<const uint4*>(L.win[cur][j]));
                 }
-                for (; j < n; j++) step(rw[2 * j], rw[2 * j + 1]);
 #ifdef RP_CK_PROF
-                bt_chain += clock64() - tc0;
+                if (tid == 0) bt_chain += clock64() - tc0;
 #endif
             }
             __syncthreads();
         }
+        if (tid == 64) L.u[1] = hp;
+        __syncthreads();
         if (tid == 0) {
-            f = fq + gq;
-            g = fq + gq2;
+            h = L.u[1];  // the last chunk's next-words were 0: plain h, g, f
+            g = gp;
+            f = fp;
             g = fh::rotr(g, 11) * fh::kC1;
             g = fh::rotr(g, 17) * fh::kC1;
             f = fh::rotr(f, 11) * fh::kC1;
