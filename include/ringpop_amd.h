@@ -135,6 +135,18 @@ int rp_members_update_dev(rp_members *m, const uint32_t *d_ids, const uint8_t *d
                           uint32_t k, int64_t now_ms, uint8_t *d_applied, uint8_t *d_new_status,
                           int64_t *d_new_inc, uint32_t *d_n_applied, void *stream);
 /* membership.checksum (null until the first applied update: *is_set = 0). */
+/* Membership.set (lib/membership/index.js:208-247) over the stash of k changes received while
+ * not ready (arrival order; the caller keeps the stash, index.js:259-265):
+ * mergeMembershipChangesets (lib/membership/merge.js:22-51: the local member skipped, the
+ * strictly greatest incarnation per address wins, the first one on ties), then every picked
+ * change is set verbatim (existing members overwritten, unknown addresses created), then the
+ * checksum is computed once. pick (k entries) receives the indices of the picked changes in
+ * first-seen address order (the order the caller appends new Member objects in), npick their
+ * count. The _dev form takes device buffers and never syncs with the host. */
+int rp_members_set(rp_members *m, const uint32_t *ids, const uint8_t *status, const int64_t *inc, uint32_t k,
+                   uint32_t *pick, uint32_t *npick);
+int rp_members_set_dev(rp_members *m, const uint32_t *d_ids, const uint8_t *d_status, const int64_t *d_inc,
+                       uint32_t k, uint32_t *d_pick, uint32_t *d_npick, void *stream);
 int rp_members_checksum(rp_members *m, uint32_t *out, int *is_set);
 /* computeChecksum() unconditionally. */
 int rp_members_compute_checksum(rp_members *m);

@@ -73,6 +73,8 @@ SIGNATURES = {
     "rp_members_set_local": (_INT, [_P, _U32]),
     "rp_members_update": (_INT, [_P, _P, _P, _P, _U32, ctypes.c_int64, _P, _P, _P, _P]),
     "rp_members_update_dev": (_INT, [_P, _P, _P, _P, _U32, ctypes.c_int64, _P, _P, _P, _P, _P]),
+    "rp_members_set": (_INT, [_P, _P, _P, _P, _U32, _P, _P]),
+    "rp_members_set_dev": (_INT, [_P, _P, _P, _P, _U32, _P, _P, _P]),
     "rp_members_checksum": (_INT, [_P, _P, _P]),
     "rp_members_compute_checksum": (_INT, [_P]),
     "rp_members_checksum_string": (_INT, [_P, _P, _U64, _P]),
@@ -393,6 +395,11 @@ class Membership:
         self._names = []
         self._ids = {}
         self.now = now or (lambda: 0)
+        # isReady + the stash of remote changes received before it (index.js:259-265), kept on
+        # the host as the reference's JS side keeps it; set() merges it on the device
+        self.is_ready = True
+        self._stash = []
+        self._stash_nulled = False
         if whoami is not None:
             check(lib().rp_members_set_local(self._h, self.intern([whoami])[0]))
 
@@ -423,11 +430,19 @@ class Membership:
     def address(self, i):
         return self._names[i]
 
-    def update_ids(self, ids, status, inc, now_ms=None):
+    def set_ready(self, ready):
+        self.is_ready = bool(ready)
+
+    def update_ids(self, ids, status, inc, now_ms=None, is_local=False):
         ids = np.ascontiguousarray(ids, dtype=np.uint32)
         st = np.ascontiguousarray(status, dtype=np.uint8)
         inc = np.ascontiguousarray(inc, dtype=np.int64)
         k = len(ids)
+        if not is_local and not self.is_ready:  # stashed, nothing applied (index.js:259-265)
+            if not self._stash_nulled:
+                self._stash.append((ids.copy(), st.copy(), inc.copy()))
+            z = np.zeros(k, dtype=np.uint8)
+            return z, st.copy(), inc.copy(), 0
         app = np.empty(max(k, 1), dtype=np.uint8)
         nst = np.empty(max(k, 1), dtype=np.uint8)
         ninc = np.empty(max(k, 1), dtype=np.int64)
@@ -451,6 +466,23 @@ class Membership:
                 u["incarnationNumber"] = int(i_)
                 out.append(u)
         return out
+
+    def set(self):
+        """Membership.set (index.js:208-247): merge the stash on the device
+        (mergeMembershipChangesets) and set the picked members; returns the picked changes'
+        (address, status, inc) in first-seen order."""
+        if self.is_ready or self._stash_nulled or not self._stash:
+            return []
+        ids = np.concatenate([x[0] for x in self._stash])
+        st = np.concatenate([x[1] for x in self._stash])
+        inc = np.concatenate([x[2] for x in self._stash])
+        pick = np.empty(len(ids), dtype=np.uint32)
+        npick = ctypes.c_uint32()
+        check(lib().rp_members_set(self._h, ids.ctypes.data, st.ctypes.data, inc.ctypes.data, len(ids),
+                                   pick.ctypes.data, ctypes.byref(npick)))
+        self._stash = []
+        self._stash_nulled = True
+        return [(self._names[int(ids[j])], STATUS_NAME[int(st[j])], int(inc[j])) for j in pick[:npick.value]]
 
     @property
     def checksum(self):

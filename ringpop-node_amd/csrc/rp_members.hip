@@ -75,6 +75,55 @@ __global__ void k_fold(const uint32_t* __restrict__ sk, const uint32_t* __restri
     }
 }
 
+// mergeMembershipChangesets (lib/membership/merge.js:22-51) over the (id, arrival)-sorted
+// stash: one lane per id segment skips the local member, keeps the change with the strictly
+// greatest incarnation (the first one on ties) and marks it at the segment's first arrival
+// index, so that compacting the marks in index order gives first-seen address order.
+__global__ void k_merge_pick(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv, uint32_t k,
+                             const int64_t* __restrict__ ch_inc, uint32_t local_id, uint32_t* __restrict__ mark) {
+    const uint32_t gstride = gridDim.x * blockDim.x;
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < k; p += gstride) {
+        const uint32_t id = sk[p];
+        if ((p > 0 && sk[p - 1] == id) || id == local_id) continue;
+        const uint32_t first = sv[p];
+        uint32_t best = first;
+        int64_t bi = ch_inc[first];
+        for (uint32_t q = p + 1; q < k && sk[q] == id; q++) {
+            const uint32_t j = sv[q];
+            if (ch_inc[j] > bi) {
+                bi = ch_inc[j];
+                best = j;
+            }
+        }
+        mark[first] = best + 1u;
+    }
+}
+
+__global__ void k_flag_nonzero(const uint32_t* __restrict__ mark, uint32_t k, uint32_t* __restrict__ flag) {
+    const uint32_t gstride = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < k; i += gstride) flag[i] = mark[i] ? 1u : 0u;
+}
+
+// Membership.set (index.js:208-247) for the picked changes, in first-seen order: an existing
+// member takes the change's status and incarnation verbatim, an unknown address is created.
+__global__ void k_set_apply(const uint32_t* __restrict__ mark, const uint32_t* __restrict__ pos, uint32_t k,
+                            const uint32_t* __restrict__ ids, const uint8_t* __restrict__ chs,
+                            const int64_t* __restrict__ chi, uint8_t* __restrict__ exists,
+                            uint8_t* __restrict__ status, int64_t* __restrict__ inc, uint32_t* __restrict__ pick,
+                            uint32_t* __restrict__ npick) {
+    const uint32_t gstride = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < k; i += gstride) {
+        if (i == 0 && npick) *npick = pos[k];
+        const uint32_t m = mark[i];
+        if (!m) continue;
+        const uint32_t j = m - 1u, id = ids[j];
+        exists[id] = 1;
+        status[id] = chs[j];
+        inc[id] = chi[j];
+        if (pick) pick[pos[i]] = j;
+    }
+}
+
 // generateChecksumString pieces (index.js:115-120): address + status + incarnation + ';'
 __global__ void k_mck_len(const uint32_t* __restrict__ order, uint32_t n, const uint8_t* __restrict__ exists,
                           const uint8_t* __restrict__ status, const int64_t* __restrict__ inc,
@@ -137,8 +186,9 @@ struct Members {
     DevBuf<uint8_t> ck_buf;
     DevBuf<uint32_t> ck_len, ck_pos;
     DevBuf<uint32_t> sk, sv;
+    DevBuf<uint32_t> mk, mpos;  // set: merge marks and their positions
     // host-buffer staging
-    DevBuf<uint32_t> io_ids;
+    DevBuf<uint32_t> io_ids, io_pick;
     DevBuf<uint8_t> io_st, io_app, io_nst;
     DevBuf<int64_t> io_inc, io_ninc;
     Scratch ws;
@@ -180,6 +230,32 @@ struct Members {
         }
         if (n_applied_out)
             RP_HIP(hipMemcpyAsync(n_applied_out, napplied.p, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    }
+
+    // Membership.set over a stash of k changes (arrival order): merge, set, checksum once.
+    void set_dev(const uint32_t* ids, const uint8_t* chs, const int64_t* chi, uint32_t k, uint32_t* pick,
+                 uint32_t* npick, hipStream_t s) {
+        if (s != st) RP_HIP(hipStreamSynchronize(st));
+        if (!k) {
+            if (npick) RP_HIP(hipMemsetAsync(npick, 0, sizeof(uint32_t), s));
+            return;
+        }
+        sk.reserve(k);
+        sv.reserve(k);
+        mk.reserve(k);
+        mpos.reserve(k + 1);
+        hipLaunchKernelGGL(k_sort_init, dim3(grid_for(k, 256)), dim3(256), 0, s, ids, k, sk.p, sv.p);
+        int bits = 8;
+        while (bits < 32 && (1ull << bits) < nt.size()) bits += 8;
+        radix_sort_pairs(sk.p, sv.p, k, 0, bits, s, ws);
+        RP_HIP(hipMemsetAsync(mk.p, 0, 4ull * k, s));
+        hipLaunchKernelGGL(k_merge_pick, dim3(grid_for(k, 256)), dim3(256), 0, s, sk.p, sv.p, k, chi, local_id, mk.p);
+        hipLaunchKernelGGL(k_flag_nonzero, dim3(grid_for(k, 256)), dim3(256), 0, s, mk.p, k, mpos.p);
+        scan_exclusive_u32(mpos.p, mpos.p, k, s, ws);
+        hipLaunchKernelGGL(k_set_apply, dim3(grid_for(k, 256)), dim3(256), 0, s, mk.p, mpos.p, k, ids, chs, chi,
+                           exists.p, status.p, inc.p, pick, npick);
+        RP_HIP(hipGetLastError());
+        checksum_dev(s, nullptr);
     }
 
     // Membership.computeChecksum (index.js:48-75) gated on *gate != 0 (null = always).
@@ -312,6 +388,40 @@ int rp_members_update(rp_members* h, const uint32_t* ids, const uint8_t* status,
         RP_HIP(hipMemcpyAsync(&na, m.napplied.p, 4, hipMemcpyDeviceToHost, m.st));
         RP_HIP(hipStreamSynchronize(m.st));
         if (n_applied) *n_applied = na;
+    });
+}
+
+int rp_members_set_dev(rp_members* h, const uint32_t* d_ids, const uint8_t* d_status, const int64_t* d_inc,
+                       uint32_t k, uint32_t* d_pick, uint32_t* d_npick, void* stream) {
+    return guard([&] {
+        rp::Members& m = MB(h);
+        RP_REQUIRE(k == 0 || (d_ids && d_status && d_inc), "set_dev: null change buffers");
+        m.set_dev(d_ids, d_status, d_inc, k, d_pick, d_npick, rp::as_stream(stream));
+    });
+}
+
+int rp_members_set(rp_members* h, const uint32_t* ids, const uint8_t* status, const int64_t* inc, uint32_t k,
+                   uint32_t* pick, uint32_t* npick) {
+    return guard([&] {
+        rp::Members& m = MB(h);
+        RP_REQUIRE(k == 0 || (ids && status && inc), "set: null change buffers");
+        for (uint32_t i = 0; i < k; i++) RP_REQUIRE(ids[i] < m.nt.size(), "set: id was never interned");
+        const uint32_t kk = k ? k : 1;
+        m.io_ids.reserve(kk + 1);
+        m.io_st.reserve(kk);
+        m.io_inc.reserve(kk);
+        m.io_pick.reserve(kk + 1);
+        if (k) {
+            RP_HIP(hipMemcpyAsync(m.io_ids.p, ids, 4ull * k, hipMemcpyHostToDevice, m.st));
+            RP_HIP(hipMemcpyAsync(m.io_st.p, status, k, hipMemcpyHostToDevice, m.st));
+            RP_HIP(hipMemcpyAsync(m.io_inc.p, inc, 8ull * k, hipMemcpyHostToDevice, m.st));
+        }
+        m.set_dev(m.io_ids.p, m.io_st.p, m.io_inc.p, k, m.io_pick.p, m.io_pick.p + kk, m.st);
+        uint32_t np = 0;
+        RP_HIP(hipMemcpyAsync(&np, m.io_pick.p + kk, 4, hipMemcpyDeviceToHost, m.st));
+        RP_HIP(hipStreamSynchronize(m.st));
+        if (pick && np) RP_HIP(hipMemcpy(pick, m.io_pick.p, 4ull * np, hipMemcpyDeviceToHost));
+        if (npick) *npick = np;
     });
 }
 

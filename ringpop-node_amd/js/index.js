@@ -206,6 +206,26 @@ MembershipMerge.prototype.update = function update(changes, nowMs) {
     return applied;
 };
 
+// set(stash) — Membership.set (index.js:208-247) over the changes stashed while !isReady
+// (index.js:259-265; the caller keeps the stash and the Member objects): merged on the device
+// (mergeMembershipChangesets, merge.js:22-51), set, checksum once. Returns the picked changes
+// in first-seen order, the order new Member objects are appended in.
+MembershipMerge.prototype.set = function set(stash) {
+    var k = stash.length;
+    var ids = native.membersIntern(this._h, stash.map(function (c) { return c.address; }));
+    var st = new Uint8Array(k), inc = new Float64Array(k);
+    for (var i = 0; i < k; i++) {
+        var code = STATUS_CODE[stash[i].status];
+        if (code === undefined) { throw new Error('ringpop_amd: unknown status ' + stash[i].status); }
+        st[i] = code;
+        inc[i] = stash[i].incarnationNumber;
+    }
+    var pick = native.membersSet(this._h, ids, st, inc);
+    var out = [];
+    for (i = 0; i < pick.length; i++) { out.push(stash[pick[i]]); }
+    return out;
+};
+
 Object.defineProperty(MembershipMerge.prototype, 'checksum', {
     get: function () { return native.membersChecksum(this._h); }
 });

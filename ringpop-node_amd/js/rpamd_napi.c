@@ -556,6 +556,38 @@ static napi_value js_members_update(napi_env env, napi_callback_info info) {
     return out;
 }
 
+/* set(h, ids Uint32Array, status Uint8Array, inc Float64Array) -> Uint32Array of picked stash
+ * indices in first-seen order — Membership.set (lib/membership/index.js:208-247) over the stash
+ * the JS side kept while !isReady: mergeMembershipChangesets (merge.js:22-51) + set + checksum. */
+static napi_value js_members_set(napi_env env, napi_callback_info info) {
+    ARGS(4);
+    handle_t *h = get_handle(env, argv[0], 2);
+    if (!h) return NULL;
+    size_t k = 0, k2 = 0, k3 = 0;
+    const uint32_t *ids = (const uint32_t *)typed_data(env, argv[1], napi_uint32_array, &k);
+    const uint8_t *st = (const uint8_t *)typed_data(env, argv[2], napi_uint8_array, &k2);
+    const double *incd = (const double *)typed_data(env, argv[3], napi_float64_array, &k3);
+    if ((k && (!ids || !st || !incd)) || k2 != k || k3 != k) {
+        napi_throw_type_error(env, NULL, "set expects Uint32Array ids, Uint8Array status, Float64Array inc of equal length");
+        return NULL;
+    }
+    int64_t *inc = (int64_t *)malloc(sizeof(int64_t) * (k ? k : 1));
+    uint32_t *pick = (uint32_t *)malloc(sizeof(uint32_t) * (k ? k : 1));
+    for (size_t i = 0; i < k; i++) inc[i] = (int64_t)incd[i];
+    uint32_t np = 0;
+    int rc = rp_members_set((rp_members *)h->p, ids, st, inc, (uint32_t)k, pick, &np);
+    free(inc);
+    if (rc) {
+        free(pick);
+        RP_OK(rc);
+    }
+    void *pd = NULL;
+    napi_value out = new_typed(env, napi_uint32_array, np, 4, &pd);
+    if (np) memcpy(pd, pick, 4ull * np);
+    free(pick);
+    return out;
+}
+
 static napi_value js_members_checksum(napi_env env, napi_callback_info info) {
     ARGS(1);
     handle_t *h = get_handle(env, argv[0], 2);
@@ -755,6 +787,7 @@ static napi_value init(napi_env env, napi_value exports) {
         {"membersIntern", js_members_intern},
         {"membersSetLocal", js_members_set_local},
         {"membersUpdate", js_members_update},
+        {"membersSet", js_members_set},
         {"membersChecksum", js_members_checksum},
         {"membersComputeChecksum", js_members_compute_checksum},
         {"membersChecksumString", js_members_checksum_string},

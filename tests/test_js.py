@@ -18,7 +18,7 @@ pytestmark = pytest.mark.skipif(NODE is None or not os.path.isdir("/usr/include/
 EXPORTS = ["version", "deviceCount", "hash32", "destroy", "ringCreate", "ringAddRemove", "ringChecksum",
            "ringChecksumString", "ringServerCount", "ringTokenCount", "ringHasServer", "ringServers",
            "ringOwnerName", "ringLookup", "ringLookupN", "ringLookupNHashes", "membersCreate", "membersIntern",
-           "membersSetLocal", "membersUpdate", "membersChecksum", "membersComputeChecksum",
+           "membersSetLocal", "membersUpdate", "membersSet", "membersChecksum", "membersComputeChecksum",
            "membersChecksumString", "membersDump", "simCreate", "simStep", "simRound", "simChecksums",
            "simView", "simConverged", "simStats"]
 

@@ -117,3 +117,67 @@ def test_empty_and_checksum_null(gpu):
     assert c1 is not None
     assert m.update([{"address": "127.0.0.1:3000", "status": "alive", "incarnationNumber": 5}]) == []
     assert m.checksum == c1
+
+
+def test_stash_set_matches_reference_golden(gpu):
+    """isReady=false stash + Membership.set (index.js:208-247, merge.js:22-51) on the device,
+    against the reference's recorded run (membership_golden.json 'stash-set')."""
+    case = next(c for c in gu.load("membership_golden.json")["cases"] if c["name"] == "stash-set")
+    m = gpu.Membership(whoami=case["local"])
+    for op in case["ops"]:
+        if op["type"] == "ready":
+            m.set_ready(op["value"])
+        elif op["type"] == "set":
+            m.set()
+        else:
+            ch = op["changes"]
+            ids = m.intern([c[0] for c in ch])
+            app, nst, ninc, _ = m.update_ids(ids, [STAT[c[1]] for c in ch], [c[2] for c in ch],
+                                             now_ms=op.get("now", 0), is_local=op.get("isLocal", False))
+            got = [[i, gpu.STATUS_NAME[int(nst[i])], int(ninc[i])] for i in range(len(ch)) if app[i]]
+            assert got == op["applied"]
+        assert m.checksum == op["checksum"], op["type"]
+        if "members" in op:
+            want = {w[0]: (STAT[w[1]], w[2]) for w in op["members"]}
+            assert device_state(m, list(want)) == want
+
+
+def test_bootstrap_set_vs_oracle(gpu, orc):
+    """The bulk bootstrap path at scale: 8 join responses x 20k members (overlapping addresses,
+    incarnation ties, the local member inside), merged and set on the device; member table
+    and checksum against the oracle, picks against mergeMembershipChangesets restated here."""
+    S = synth()
+    n, R, per = 30_000, 8, 20_000
+    names = [S.c2_addr(i) for i in range(n)]
+    rng = np.random.default_rng(5)
+    ids = np.concatenate([rng.choice(n, size=per, replace=False) for _ in range(R)]).astype(np.uint32)
+    st = rng.integers(0, 4, size=len(ids)).astype(np.uint8)
+    inc = (1434401518824 + rng.integers(0, 3, size=len(ids))).astype(np.int64)
+    m = gpu.Membership(whoami=names[0], capacity=n)
+    assert m.intern(names) == list(range(n))
+    o = orc.Members(names, local=names[0])
+    m.set_ready(False)
+    o.set_ready(False)
+    for r in range(R):
+        sl = slice(r * per, (r + 1) * per)
+        m.update_ids(ids[sl], st[sl], inc[sl])
+        o.update_ids(ids[sl], st[sl], inc[sl])
+    picks = m.set()
+    assert o.set() == len(picks)
+    best, first = {}, []
+    for j, a in enumerate(ids.tolist()):
+        if a == 0:
+            continue
+        if a not in best:
+            best[a] = j
+            first.append(a)
+        elif inc[best[a]] < inc[j]:
+            best[a] = j
+    assert picks == [(names[a], gpu.STATUS_NAME[int(st[best[a]])], int(inc[best[a]])) for a in first]
+    assert m.checksum == o.checksum
+    ex, dst, dinc = m.dump()
+    for a in range(n):
+        om = o.member(names[a])
+        assert (om is None) == (not ex[a])
+        if om:
+            assert (gpu.STATUS_NAME[int(dst[a])], int(dinc[a])) == (om["status"], om["incarnationNumber"])
