@@ -108,6 +108,25 @@ int rp_ring_lookupn_dev(rp_ring *r, const uint8_t *d_keys, const uint64_t *d_off
 int rp_ring_lookupn_hashes_dev(rp_ring *r, const uint32_t *d_hashes, uint64_t n, int32_t nrep,
                                uint32_t *d_owners, uint8_t *d_counts, void *stream);
 
+/* Keys grouped by owner: RingPop.handleOrProxyAll's keysByDest = _.groupBy(keys, this.lookup)
+ * (index.js:609-667, :616) and RequestProxySend.lookupKeys (lib/request-proxy/send.js:171-179).
+ * Every key is looked up (lib/ring/index.js:145-154); on an empty ring every key gets self_id
+ * (RingPop.lookup's whoami() fallback, index.js:434-451). Outputs:
+ *   dests[0 .. *ndest)        the distinct owners in first-seen order = Object.keys(keysByDest)
+ *                             (lookupKeys' result); capacity min(n, server_count + 1)
+ *   group_off[0 .. *ndest]    group g holds perm[group_off[g] .. group_off[g+1])
+ *   perm[0 .. n)              key indices; each group keeps input order (keysByDest[dest])
+ * The _dev form takes device buffers (group_off holding n + 1) and never syncs with the host
+ * unless the ring is empty. */
+int rp_ring_group_keys_dev(rp_ring *r, const uint8_t *d_keys, const uint64_t *d_off, uint32_t stride, uint64_t n,
+                           uint32_t self_id, uint32_t *d_dests, uint32_t *d_group_off, uint32_t *d_perm,
+                           uint32_t *d_ndest, void *stream);
+int rp_ring_group_keys(rp_ring *r, const char *keys, const uint64_t *off, uint32_t stride, uint64_t n,
+                       uint32_t self_id, uint32_t *dests, uint32_t *group_off, uint32_t *perm, uint32_t *ndest);
+/* Same with a caller hashFunc's key hashes (options.hashFunc, lib/ring/index.js:29). */
+int rp_ring_group_hashes(rp_ring *r, const uint32_t *hashes, uint64_t n, uint32_t self_id, uint32_t *dests,
+                         uint32_t *group_off, uint32_t *perm, uint32_t *ndest);
+
 /* ------------------------------------------------------------------ Membership
  * Replaces the hot path of lib/membership/index.js Membership: update (249-324) with the
  * Member.evaluateUpdate rules (lib/membership/member.js:71-202) and computeChecksum /

@@ -67,6 +67,9 @@ SIGNATURES = {
     "rp_ring_lookup_dev": (_INT, [_P, _P, _P, _U32, _U64, _P, _P]),
     "rp_ring_lookupn_dev": (_INT, [_P, _P, _P, _U32, _U64, _I32, _P, _P, _P]),
     "rp_ring_lookupn_hashes_dev": (_INT, [_P, _P, _U64, _I32, _P, _P, _P]),
+    "rp_ring_group_keys_dev": (_INT, [_P, _P, _P, _U32, _U64, _U32, _P, _P, _P, _P, _P]),
+    "rp_ring_group_keys": (_INT, [_P, _P, _P, _U32, _U64, _U32, _P, _P, _P, _P]),
+    "rp_ring_group_hashes": (_INT, [_P, _P, _U64, _U32, _P, _P, _P, _P]),
     "rp_members_create": (_INT, [_U32, _INT, _P]),
     "rp_members_destroy": (_INT, [_P]),
     "rp_members_intern": (_INT, [_P, _P, _P, _U32, _P]),
@@ -371,6 +374,46 @@ class HashRing:
         check(lib().rp_ring_lookupn_hashes(self._h, hs.ctypes.data, len(hs), int(n), out.ctypes.data,
                                            cnt.ctypes.data))
         return out[:len(hs)], cnt[:len(hs)]
+
+    # -- keys grouped by owner: handleOrProxyAll (index.js:609-667) / lookupKeys (send.js:171-179)
+    def group_ids(self, keys, self_id=NULL_ID):
+        """(dests, group_off, perm): owners in first-seen order, group bounds, key indices."""
+        n = len(keys)
+        dests = np.empty(max(n, 1), dtype=np.uint32)
+        goff = np.empty(max(n, 1) + 1, dtype=np.uint32)
+        perm = np.empty(max(n, 1), dtype=np.uint32)
+        nd = ctypes.c_uint32()
+        if self.hashFunc is not None:
+            hs = np.array([self.hashFunc(k) & 0xFFFFFFFF for k in keys], dtype=np.uint32)
+            check(lib().rp_ring_group_hashes(self._h, hs.ctypes.data, n, self_id, dests.ctypes.data,
+                                             goff.ctypes.data, perm.ctypes.data, ctypes.byref(nd)))
+        else:
+            blob, off, stride, n = self._key_pack(keys)
+            check(lib().rp_ring_group_keys(self._h, blob.ctypes.data, _ptr(off), stride, n, self_id,
+                                           dests.ctypes.data, goff.ctypes.data, perm.ctypes.data, ctypes.byref(nd)))
+        k = nd.value
+        return dests[:k], goff[:k + 1], perm[:n]
+
+    def groupBy(self, keys, whoami=None):
+        """_.groupBy(keys, ringpop.lookup) as handleOrProxyAll builds keysByDest (index.js:616):
+        {dest: [keys in input order]} with dests in first-seen order; an empty ring's null
+        owner falls back to whoami (RingPop.lookup, index.js:434-451)."""
+        keys = [k if isinstance(k, (bytes, np.ndarray)) else str(k) for k in keys]
+        dests, goff, perm = self.group_ids(keys, self_id=NULL_ID)
+        out = {}
+        for g, d in enumerate(dests):
+            out[whoami if d == NULL_ID else self.name(d)] = [keys[i] for i in perm[goff[g]:goff[g + 1]]]
+        return out
+
+    def lookupKeys(self, keys, whoami=None):
+        """RequestProxySend.lookupKeys (lib/request-proxy/send.js:171-179)."""
+        dests, _, _ = self.group_ids([str(k) for k in keys], self_id=NULL_ID)
+        return [whoami if d == NULL_ID else self.name(d) for d in dests]
+
+    def group_dev(self, keys_ptr, n, dests_ptr, goff_ptr, perm_ptr, ndest_ptr, self_id=NULL_ID, stride=36,
+                  off_ptr=None, stream=None):
+        check(lib().rp_ring_group_keys_dev(self._h, keys_ptr, off_ptr, stride, n, self_id, dests_ptr, goff_ptr,
+                                           perm_ptr, ndest_ptr, stream))
 
     # -- device-resident hot path (pointers from torch tensors / hipMalloc)
     def lookupn_dev(self, keys_ptr, n, nrep, owners_ptr, counts_ptr=None, stride=36, off_ptr=None, stream=None):

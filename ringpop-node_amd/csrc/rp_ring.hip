@@ -984,6 +984,8 @@ struct Ring {
     DevBuf<uint32_t> io_a, io_b;
     DevBuf<uint8_t> io_keys, io_cnt;
     DevBuf<uint64_t> io_off;
+    // group keys by owner (handleOrProxyAll)
+    DevBuf<uint32_t> grp_own, grp_key, grp_first, grp_dk, grp_dv, grp_rank;
     Scratch ws;
 
     RingView view() const {
@@ -1315,6 +1317,116 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
         launch_lookupn_view(r.view(), keys, off, stride, hashes, n, np, W, out, counts, st);
 }
 
+// ------------------------------------------------------------------- group keys by owner
+// RingPop.handleOrProxyAll's keysByDest = _.groupBy(keys, this.lookup) (index.js:609-667, :616)
+// and RequestProxySend.lookupKeys (lib/request-proxy/send.js:171-179). _.groupBy appends each
+// key to its owner's list in input order and Object.keys(keysByDest) lists the owners in
+// first-seen order, so: first[s] = min key index owned by s; the owners ranked by first[s];
+// a stable sort of the key indices by that rank.
+
+__global__ void k_grp_first(const uint32_t* __restrict__ own, uint64_t n, uint32_t* __restrict__ first) {
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gstride) {
+        const uint32_t s = own[i];
+        // a plain (possibly stale) read first: once an owner's first key is known, later keys
+        // skip the atomic
+        if ((uint32_t)i < first[s]) atomicMin(first + s, (uint32_t)i);
+    }
+}
+
+// (first index, owner) pairs to sort; unseen owners sort after every seen one (key n)
+__global__ void k_grp_dest_keys(const uint32_t* __restrict__ first, uint32_t S, uint32_t n,
+                                uint32_t* __restrict__ dk, uint32_t* __restrict__ dv) {
+    const uint32_t gstride = gridDim.x * blockDim.x;
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < S; s += gstride) {
+        const uint32_t f = first[s];
+        dk[s] = f < n ? f : n;
+        dv[s] = s;
+    }
+}
+
+// owners in first-seen order: dests[p], rank[owner] = p, *ndest
+__global__ void k_grp_rank(const uint32_t* __restrict__ dk, const uint32_t* __restrict__ dv, uint32_t S, uint32_t n,
+                           uint32_t* __restrict__ rank, uint32_t* __restrict__ dests, uint32_t* __restrict__ ndest) {
+    const uint32_t gstride = gridDim.x * blockDim.x;
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < S; p += gstride) {
+        if (dk[p] >= n) continue;
+        rank[dv[p]] = p;
+        dests[p] = dv[p];
+        if (p + 1 == S || dk[p + 1] >= n) *ndest = p + 1;
+    }
+}
+
+// sort keys: the owner's rank; values: the key index (stable sort keeps input order per group)
+__global__ void k_grp_keys(const uint32_t* __restrict__ own, uint64_t n, const uint32_t* __restrict__ rank,
+                           uint32_t* __restrict__ gk, uint32_t* __restrict__ perm) {
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gstride) {
+        gk[i] = rank[own[i]];
+        perm[i] = (uint32_t)i;
+    }
+}
+
+// group_off[g] = first position of rank g in the sorted keys; group_off[ndest] = n
+__global__ void k_grp_bounds(const uint32_t* __restrict__ gk, uint64_t n, uint32_t* __restrict__ goff) {
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gstride) {
+        const uint32_t g = gk[p];
+        if (p == 0 || gk[p - 1] != g) goff[g] = (uint32_t)p;
+        if (p + 1 == n) goff[g + 1] = (uint32_t)n;
+    }
+}
+
+static int bits_for(uint64_t v) {  // radix bits (multiple of 8) that hold every value <= v
+    int b = 8;
+    while (b < 32 && (v >> b)) b += 8;
+    return b;
+}
+
+// keys (or caller hashes) -> owners -> groups; buffers as rp_ring_group_keys_dev documents
+static void group_keys(Ring& r, const uint8_t* keys, const uint64_t* off, uint32_t stride, const uint32_t* hashes,
+                       uint64_t n, uint32_t self_id, uint32_t* dests, uint32_t* goff, uint32_t* perm,
+                       uint32_t* ndest, hipStream_t st) {
+    RP_REQUIRE(n < 0xFFFFFFFFull, "group_keys: at most 2^32-2 keys per call");
+    if (st != r.st) RP_HIP(hipStreamSynchronize(r.st));
+    if (n == 0 || r.M == 0) {
+        // lookup returns null for every key and RingPop.lookup answers whoami() (index.js:434-451):
+        // one group (self) holding every key in order, or no group at all
+        const uint32_t h[3] = {self_id, 0u, (uint32_t)n};
+        const uint32_t nd = n ? 1u : 0u;
+        RP_HIP(hipMemcpyAsync(ndest, &nd, 4, hipMemcpyHostToDevice, st));
+        if (n) {
+            RP_HIP(hipMemcpyAsync(dests, h, 4, hipMemcpyHostToDevice, st));
+            RP_HIP(hipMemcpyAsync(goff, h + 1, 8, hipMemcpyHostToDevice, st));
+            iota_u32(perm, n, st);
+        } else {
+            RP_HIP(hipMemsetAsync(goff, 0, 4, st));
+        }
+        RP_HIP(hipStreamSynchronize(st));  // h lives on this stack frame
+        return;
+    }
+    const uint32_t S = r.nt.size();
+    r.grp_own.reserve(n);
+    r.grp_key.reserve(n);
+    r.grp_first.reserve(S);
+    r.grp_dk.reserve(S);
+    r.grp_dv.reserve(S);
+    r.grp_rank.reserve(S);
+    launch_lookupn(r, keys, off, stride, hashes, n, 1, 1, r.grp_own.p, nullptr, st);
+    RP_HIP(hipMemsetAsync(r.grp_first.p, 0xFF, 4ull * S, st));
+    hipLaunchKernelGGL(k_grp_first, dim3(grid_for(n, 256, 256 * 16)), dim3(256), 0, st, r.grp_own.p, n, r.grp_first.p);
+    hipLaunchKernelGGL(k_grp_dest_keys, dim3(grid_for(S, 256)), dim3(256), 0, st, r.grp_first.p, S, (uint32_t)n,
+                       r.grp_dk.p, r.grp_dv.p);
+    radix_sort_pairs(r.grp_dk.p, r.grp_dv.p, S, 0, bits_for(n), st, r.ws);
+    hipLaunchKernelGGL(k_grp_rank, dim3(grid_for(S, 256)), dim3(256), 0, st, r.grp_dk.p, r.grp_dv.p, S, (uint32_t)n,
+                       r.grp_rank.p, dests, ndest);
+    hipLaunchKernelGGL(k_grp_keys, dim3(grid_for(n, 256, 256 * 16)), dim3(256), 0, st, r.grp_own.p, n, r.grp_rank.p,
+                       r.grp_key.p, perm);
+    radix_sort_pairs(r.grp_key.p, perm, n, 0, bits_for(S - 1), st, r.ws);
+    hipLaunchKernelGGL(k_grp_bounds, dim3(grid_for(n, 256, 256 * 16)), dim3(256), 0, st, r.grp_key.p, n, goff);
+    RP_HIP(hipGetLastError());
+}
+
 }  // namespace rp
 
 // ==================================================================================== C ABI
@@ -1599,6 +1711,78 @@ int rp_ring_lookupn_hashes(rp_ring* h, const uint32_t* hashes, uint64_t n, int32
         RP_REQUIRE(n == 0 || (hashes && owners), "lookupn_hashes: null buffer");
         host_lookup(r, nullptr, nullptr, 0, hashes, n, np_for(r, nrep), nrep > 1 ? (uint32_t)nrep : 1u, owners,
                     counts);
+    });
+}
+
+// ---- group keys by owner (handleOrProxyAll / lookupKeys)
+
+int rp_ring_group_keys_dev(rp_ring* h, const uint8_t* d_keys, const uint64_t* d_off, uint32_t stride, uint64_t n,
+                           uint32_t self_id, uint32_t* d_dests, uint32_t* d_group_off, uint32_t* d_perm,
+                           uint32_t* d_ndest, void* stream) {
+    return guard([&] {
+        rp::Ring& r = R(h);
+        RP_REQUIRE(d_dests && d_group_off && d_perm && d_ndest, "group_keys_dev: null output buffer");
+        RP_REQUIRE(n == 0 || (d_keys && (stride || d_off)), "group_keys_dev: null key buffer");
+        rp::group_keys(r, d_keys, d_off, stride, nullptr, n, self_id, d_dests, d_group_off, d_perm, d_ndest,
+                       rp::as_stream(stream));
+    });
+}
+
+// host-buffer forms: keys (or a caller hashFunc's key hashes) in, groups out
+static void host_group(rp::Ring& r, const char* keys, const uint64_t* off, uint32_t stride, const uint32_t* hashes,
+                       uint64_t n, uint32_t self_id, uint32_t* dests, uint32_t* goff, uint32_t* perm, uint32_t* ndest) {
+    RP_REQUIRE(dests && goff && perm && ndest, "group_keys: null output buffer");
+    const uint8_t* dk = nullptr;
+    const uint64_t* doff = nullptr;
+    const uint32_t* dh = nullptr;
+    if (n && hashes) {
+        r.io_a.reserve(n);
+        RP_HIP(hipMemcpyAsync(r.io_a.p, hashes, n * 4, hipMemcpyHostToDevice, r.st));
+        dh = r.io_a.p;
+    } else if (n) {
+        const uint64_t bytes = stride ? n * stride : off[n];
+        r.io_keys.reserve(bytes + 16);
+        RP_HIP(hipMemcpyAsync(r.io_keys.p, keys, bytes, hipMemcpyHostToDevice, r.st));
+        dk = r.io_keys.p;
+        if (!stride) {
+            r.io_off.reserve(n + 1);
+            RP_HIP(hipMemcpyAsync(r.io_off.p, off, (n + 1) * 8, hipMemcpyHostToDevice, r.st));
+            doff = r.io_off.p;
+        }
+    }
+    // io_b = [perm n | group_off n+1 | dests n | ndest 1]
+    const uint64_t nn = n ? n : 1;
+    r.io_b.reserve(3 * nn + 2);
+    uint32_t* dperm = r.io_b.p;
+    uint32_t* dgoff = dperm + nn;
+    uint32_t* ddest = dgoff + nn + 1;
+    uint32_t* dnd = ddest + nn;
+    rp::group_keys(r, dk, doff, stride, dh, n, self_id, ddest, dgoff, dperm, dnd, r.st);
+    uint32_t nd = 0;
+    RP_HIP(hipMemcpyAsync(&nd, dnd, 4, hipMemcpyDeviceToHost, r.st));
+    RP_HIP(hipStreamSynchronize(r.st));
+    *ndest = nd;
+    if (n) RP_HIP(hipMemcpyAsync(perm, dperm, n * 4, hipMemcpyDeviceToHost, r.st));
+    if (nd) RP_HIP(hipMemcpyAsync(dests, ddest, 4ull * nd, hipMemcpyDeviceToHost, r.st));
+    RP_HIP(hipMemcpyAsync(goff, dgoff, 4ull * (nd + 1), hipMemcpyDeviceToHost, r.st));
+    RP_HIP(hipStreamSynchronize(r.st));
+}
+
+int rp_ring_group_keys(rp_ring* h, const char* keys, const uint64_t* off, uint32_t stride, uint64_t n,
+                       uint32_t self_id, uint32_t* dests, uint32_t* group_off, uint32_t* perm, uint32_t* ndest) {
+    return guard([&] {
+        rp::Ring& r = R(h);
+        RP_REQUIRE(n == 0 || (keys && (stride || off)), "group_keys: null key buffer");
+        host_group(r, keys, off, stride, nullptr, n, self_id, dests, group_off, perm, ndest);
+    });
+}
+
+int rp_ring_group_hashes(rp_ring* h, const uint32_t* hashes, uint64_t n, uint32_t self_id, uint32_t* dests,
+                         uint32_t* group_off, uint32_t* perm, uint32_t* ndest) {
+    return guard([&] {
+        rp::Ring& r = R(h);
+        RP_REQUIRE(n == 0 || hashes, "group_hashes: null hash buffer");
+        host_group(r, nullptr, nullptr, 0, hashes, n, self_id, dests, group_off, perm, ndest);
     });
 }
 

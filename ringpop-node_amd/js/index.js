@@ -157,6 +157,28 @@ HashRing.prototype.lookupNBatch = function lookupNBatch(keys, n) {
     return native.ringLookupN(this._h, keys, n);
 };
 
+// keysByDest of RingPop.handleOrProxyAll (index.js:609-667: _.groupBy(keys, this.lookup), :616)
+// in one device pass: {dest: [keys in input order]}, dests in first-seen order (the order
+// Object.keys(keysByDest) and RequestProxySend.lookupKeys, send.js:171-179, report). On an
+// empty ring every key goes to whoami (RingPop.lookup, index.js:434-451).
+HashRing.prototype.groupByOwner = function groupByOwner(keys, whoami) {
+    var g = native.ringGroupKeys(this._h, this._customHash ? this._hashes(keys) : keys);
+    var out = {};
+    for (var d = 0; d < g.dests.length; d++) {
+        var dest = g.dests[d] === null ? whoami : g.dests[d];
+        var list = new Array(g.groupOff[d + 1] - g.groupOff[d]);
+        for (var p = g.groupOff[d], j = 0; p < g.groupOff[d + 1]; p++, j++) { list[j] = keys[g.perm[p]]; }
+        out[dest] = list;
+    }
+    return out;
+};
+
+// RequestProxySend.lookupKeys (lib/request-proxy/send.js:171-179): distinct owners, first seen.
+HashRing.prototype.lookupKeys = function lookupKeys(keys, whoami) {
+    var g = native.ringGroupKeys(this._h, this._customHash ? this._hashes(keys) : keys);
+    return g.dests.map(function (d) { return d === null ? whoami : d; });
+};
+
 // Id-level batch over precomputed key hashes: {owners: Uint32Array(ids, rows of max(n,1)),
 // counts: Uint8Array}; ownerName(id) maps ids back to server names.
 HashRing.prototype.lookupNHashes = function lookupNHashes(hashes, n) {

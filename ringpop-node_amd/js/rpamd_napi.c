@@ -412,6 +412,57 @@ static napi_value js_ring_lookup(napi_env env, napi_callback_info info) {
     return arr;
 }
 
+/* groupKeys(h, keys[] | Uint32Array hashes) -> {dests: [name|null], groupOff: Uint32Array,
+ * perm: Uint32Array}: handleOrProxyAll's _.groupBy(keys, lookup) (index.js:609-667, :616) and
+ * lookupKeys (lib/request-proxy/send.js:171-179) on the device. A null dest = the empty ring's
+ * null owner (the caller substitutes whoami(), index.js:434-451). */
+static napi_value js_ring_group_keys(napi_env env, napi_callback_info info) {
+    ARGS(2);
+    handle_t *h = get_handle(env, argv[0], 1);
+    if (!h) return NULL;
+    rp_ring *r = (rp_ring *)h->p;
+    bool is_typed = false;
+    napi_is_typedarray(env, argv[1], &is_typed);
+    size_t n = 0;
+    void *hv = NULL;
+    strpack_t keys;
+    memset(&keys, 0, sizeof(keys));
+    if (is_typed) {
+        if (typed_get(env, argv[1], napi_uint32_array, &hv, &n)) {
+            napi_throw_type_error(env, NULL, "hashes must be a Uint32Array");
+            return NULL;
+        }
+    } else {
+        if (strpack_from_array(env, argv[1], &keys)) return NULL;
+        n = keys.n;
+    }
+    size_t nn = n ? n : 1;
+    uint32_t *dests = (uint32_t *)malloc(sizeof(uint32_t) * nn);
+    void *gd = NULL, *pd = NULL;
+    napi_value goff = new_typed(env, napi_uint32_array, nn + 1, 4, &gd);
+    napi_value perm = new_typed(env, napi_uint32_array, n, 4, &pd);
+    uint32_t nd = 0;
+    uint32_t pdummy = 0;
+    int rc = is_typed ? rp_ring_group_hashes(r, (const uint32_t *)hv, n, RP_NULL_ID, dests, (uint32_t *)gd,
+                                             n ? (uint32_t *)pd : &pdummy, &nd)
+                      : rp_ring_group_keys(r, keys.bytes, keys.off64, 0, n, RP_NULL_ID, dests, (uint32_t *)gd,
+                                           n ? (uint32_t *)pd : &pdummy, &nd);
+    if (!is_typed) strpack_free(&keys);
+    if (rc) {
+        free(dests);
+        RP_OK(rc);
+    }
+    napi_value arr, out;
+    napi_create_array_with_length(env, nd, &arr);
+    for (uint32_t i = 0; i < nd; i++) napi_set_element(env, arr, i, ring_name(env, r, dests[i]));
+    free(dests);
+    napi_create_object(env, &out);
+    napi_set_named_property(env, out, "dests", arr);
+    napi_set_named_property(env, out, "groupOff", goff);
+    napi_set_named_property(env, out, "perm", perm);
+    return out;
+}
+
 /* lookupNBatch(h, keys[], n) -> arrays of names, lookupN() of every key (:157-189). */
 static napi_value js_ring_lookupn(napi_env env, napi_callback_info info) {
     ARGS(3);
@@ -783,6 +834,7 @@ static napi_value init(napi_env env, napi_value exports) {
         {"ringLookup", js_ring_lookup},
         {"ringLookupN", js_ring_lookupn},
         {"ringLookupNHashes", js_ring_lookupn_hashes},
+        {"ringGroupKeys", js_ring_group_keys},
         {"membersCreate", js_members_create},
         {"membersIntern", js_members_intern},
         {"membersSetLocal", js_members_set_local},

@@ -53,6 +53,16 @@ input.cases.forEach(function (c) {
             var got = ring.lookupNBatch(b.keys, parseInt(n, 10)).map(function (row) { return row.map(toIdx); });
             eq(tag + ' lookupN ' + n, got, b.lookupN[n]);
         });
+        // handleOrProxyAll's keysByDest = _.groupBy(keys, lookup) (index.js:616) and lookupKeys
+        // (send.js:171-179), expected from the reference's recorded owners; JSON.stringify
+        // keeps key order, so the first-seen dest order is checked too
+        var want = {};
+        b.keys.forEach(function (k, i) {
+            var d = b.lookup[i] < 0 ? 'self:0' : c.names[b.lookup[i]];
+            (want[d] = want[d] || []).push(k);
+        });
+        eq(tag + ' groupByOwner', ring.groupByOwner(b.keys, 'self:0'), want);
+        eq(tag + ' lookupKeys', ring.lookupKeys(b.keys, 'self:0'), Object.keys(want));
         // the single-key forms on a few keys
         for (var i = 0; i < Math.min(4, b.keys.length); i++) {
             eq(tag + ' lookup1', toIdx(ring.lookup(b.keys[i])), b.lookup[i]);

@@ -17,7 +17,7 @@ pytestmark = pytest.mark.skipif(NODE is None or not os.path.isdir("/usr/include/
 
 EXPORTS = ["version", "deviceCount", "hash32", "destroy", "ringCreate", "ringAddRemove", "ringChecksum",
            "ringChecksumString", "ringServerCount", "ringTokenCount", "ringHasServer", "ringServers",
-           "ringOwnerName", "ringLookup", "ringLookupN", "ringLookupNHashes", "membersCreate", "membersIntern",
+           "ringOwnerName", "ringLookup", "ringLookupN", "ringLookupNHashes", "ringGroupKeys", "membersCreate", "membersIntern",
            "membersSetLocal", "membersUpdate", "membersSet", "membersChecksum", "membersComputeChecksum",
            "membersChecksumString", "membersDump", "simCreate", "simStep", "simRound", "simChecksums",
            "simView", "simConverged", "simStats"]
