@@ -175,6 +175,36 @@ int rp_members_checksum_string(rp_members *m, char *buf, uint64_t cap, uint64_t 
 int rp_members_dump(rp_members *m, uint8_t *exists, uint8_t *status, int64_t *inc, uint32_t cap);
 int rp_members_count(rp_members *m, uint32_t *n_names);
 
+/* ------------------------------------------------------------------ Gossip wire bodies
+ * Change records as the JSON text ringpop sends (device buffers; addresses are ids interned in
+ * the members handle m). Replaces the per-message JSON.stringify / safeParse of:
+ *   issueAs record {id, source, sourceIncarnationNumber, address, status, incarnationNumber}
+ *                  (lib/gossip/dissemination.js:163-170)        form 0; d_ids (36 B each) nullable
+ *   fullSync record {source, address, status, incarnationNumber} (dissemination.js:64-73)  form 1
+ *   body 0: bare changes array; 1: ping request {checksum, changes, source, sourceIncarnationNumber}
+ *   (lib/gossip/ping-sender.js:71-76); 2: ping response {changes} (server/protocol/ping.js:45-48).
+ * Encode: message j holds records [msg_rec_off[j], msg_rec_off[j+1]); d_out_off[0..n_msgs] gets
+ * the byte offsets; with d_out null only the offsets are computed (size query). Synchronous. */
+int rp_wire_encode_changes_dev(rp_members *m, uint32_t n_msgs, const uint32_t *d_msg_rec_off, uint64_t n_rec,
+                               const uint32_t *d_addr, const uint32_t *d_src, const uint8_t *d_status,
+                               const int64_t *d_inc, const int64_t *d_src_inc, const uint8_t *d_ids, int form,
+                               int body, const uint32_t *d_msg_checksum, const uint32_t *d_msg_source,
+                               const int64_t *d_msg_source_inc, uint8_t *d_out, uint64_t *d_out_off, void *stream);
+/* Decode n_msgs JSON texts d_buf[d_msg_off[j] .. d_msg_off[j+1]) — a changes array, or a body
+ * object whose `changes` member is one (server/protocol/ping.js:27-36 reads the same members).
+ * d_msg_rec_off[0..n_msgs] gets record offsets (total in [n_msgs]); records beyond rec_cap are
+ * counted, not written. Per record: address id (0xFFFFFFFF if not interned; d_addr_off/len give
+ * its bytes), source id, status, incarnationNumber, sourceIncarnationNumber (INT64_MIN if absent),
+ * byte offset of `id` (~0 if absent). d_err[j] = 0, or 1 + the failing byte's offset in message j
+ * (its records are then dropped). Nullable: d_src, d_src_inc, d_id_off, d_addr_off, d_addr_len and
+ * the three d_msg_* header columns. */
+int rp_wire_decode_changes_dev(rp_members *m, const uint8_t *d_buf, const uint64_t *d_msg_off, uint32_t n_msgs,
+                               uint32_t *d_msg_rec_off, uint32_t rec_cap, uint32_t *d_addr, uint32_t *d_src,
+                               uint8_t *d_status, int64_t *d_inc, int64_t *d_src_inc, uint64_t *d_id_off,
+                               uint64_t *d_addr_off, uint32_t *d_addr_len, uint64_t *d_err,
+                               uint32_t *d_msg_checksum, uint32_t *d_msg_source, int64_t *d_msg_source_inc,
+                               void *stream);
+
 /* ------------------------------------------------------------------ Gossip simulator
  * N full ringpop nodes (every node: membership view, dissemination buffer, ring membership,
  * iterator, suspicion timers; lib/membership, lib/gossip, lib/ring, lib/on_membership_event.js)

@@ -83,6 +83,10 @@ SIGNATURES = {
     "rp_members_checksum_string": (_INT, [_P, _P, _U64, _P]),
     "rp_members_dump": (_INT, [_P, _P, _P, _P, _U32]),
     "rp_members_count": (_INT, [_P, _P]),
+    "rp_wire_encode_changes_dev": (_INT, [_P, _U32, _P, _U64, _P, _P, _P, _P, _P, _P, _INT, _INT, _P, _P, _P, _P,
+                                          _P, _P]),
+    "rp_wire_decode_changes_dev": (_INT, [_P, _P, _P, _U32, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                          _P, _P]),
     "rp_sim_create": (_INT, [_U32, _P, _P, _P, _P, _U32, _U32, ctypes.c_int64, _INT, _P]),
     "rp_sim_destroy": (_INT, [_P]),
     "rp_sim_step": (_INT, [_P, _U32]),
@@ -906,3 +910,75 @@ class DistGossipSim:
     def stats(self):
         tot = sum(self._allgather(self.shard.stats().astype(np.int64)))
         return dict(zip(_STAT_NAMES, (int(x) for x in tot)))
+
+
+# ------------------------------------------------------------------ gossip wire bodies
+# Device JSON codec of change records (rp_wire_*_dev): dissemination.js:163-170 / 64-73 records,
+# ping bodies ping-sender.js:71-76 and server/protocol/ping.js:45-48. torch is only the device
+# buffer plumbing here.
+WIRE_FORM = {"issueAs": 0, "fullSync": 1}
+WIRE_BODY = {"array": 0, "ping": 1, "pingResponse": 2}
+
+
+def _dev(a, dtype):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=dtype)).cuda()
+
+
+def wire_encode(members, msg_rec_off, addr, src, status, inc, src_inc=None, ids=None, form="issueAs",
+                body="array", msg_checksum=None, msg_source=None, msg_source_inc=None):
+    """Encode message j = records [msg_rec_off[j], msg_rec_off[j+1]) on the device; returns
+    (bytes, out_off) on the host. addr/src/msg_source are ids interned in `members`; ids is an
+    (n_rec, 36) uint8 array of uuid strings or None (id omitted)."""
+    import torch
+    n_msgs = len(msg_rec_off) - 1
+    n_rec = len(addr)
+    z64 = np.zeros(max(n_rec, 1), dtype=np.int64)
+    d = dict(off=_dev(msg_rec_off, np.uint32), addr=_dev(addr if n_rec else [0], np.uint32),
+             src=_dev(src if n_rec else [0], np.uint32), st=_dev(status if n_rec else [0], np.uint8),
+             inc=_dev(inc if n_rec else [0], np.int64),
+             sinc=_dev(src_inc if src_inc is not None and n_rec else z64, np.int64))
+    d_ids = _dev(np.asarray(ids, dtype=np.uint8).reshape(-1), np.uint8) if ids is not None and n_rec else None
+    hdr = [None, None, None]
+    if WIRE_BODY[body] == 1:
+        hdr = [_dev(msg_checksum, np.uint32), _dev(msg_source, np.uint32), _dev(msg_source_inc, np.int64)]
+    out_off = torch.zeros(n_msgs + 1, dtype=torch.int64, device="cuda")
+    p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    args = [members._h, n_msgs, p(d["off"]), n_rec, p(d["addr"]), p(d["src"]), p(d["st"]), p(d["inc"]),
+            p(d["sinc"]), p(d_ids), WIRE_FORM[form], WIRE_BODY[body], p(hdr[0]), p(hdr[1]), p(hdr[2])]
+    check(lib().rp_wire_encode_changes_dev(*args, None, out_off.data_ptr(), None))
+    total = int(out_off[-1].item())
+    out = torch.empty(max(total, 1), dtype=torch.uint8, device="cuda")
+    check(lib().rp_wire_encode_changes_dev(*args, out.data_ptr(), out_off.data_ptr(), None))
+    return out[:total].cpu().numpy().tobytes(), out_off.cpu().numpy().astype(np.uint64)
+
+
+def wire_decode(members, texts):
+    """Decode JSON texts (changes arrays or ping bodies) on the device. Returns a dict of numpy
+    columns: rec_off, addr, src, status, inc, src_inc, id_off, addr_off, addr_len, err and the
+    per-message checksum / source / source_inc."""
+    import torch
+    texts = [t.encode() if isinstance(t, str) else bytes(t) for t in texts]
+    n = len(texts)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(t) for t in texts])
+    buf = _dev(np.frombuffer(b"".join(texts) or b"\0", dtype=np.uint8), np.uint8)
+    d_off = _dev(off, np.uint64)
+    cap = max(sum(t.count(b"{") for t in texts), 1)
+    e = lambda dt, k=cap: torch.empty(k, dtype=dt, device="cuda")  # noqa: E731
+    c = dict(rec_off=e(torch.int32, n + 1), addr=e(torch.int32), src=e(torch.int32), status=e(torch.uint8),
+             inc=e(torch.int64), src_inc=e(torch.int64), id_off=e(torch.int64), addr_off=e(torch.int64),
+             addr_len=e(torch.int32), err=e(torch.int64, max(n, 1)), checksum=e(torch.int32, max(n, 1)),
+             source=e(torch.int32, max(n, 1)), source_inc=e(torch.int64, max(n, 1)))
+    p = {k: v.data_ptr() for k, v in c.items()}
+    check(lib().rp_wire_decode_changes_dev(members._h, buf.data_ptr(), d_off.data_ptr(), n, p["rec_off"], cap,
+                                           p["addr"], p["src"], p["status"], p["inc"], p["src_inc"], p["id_off"],
+                                           p["addr_off"], p["addr_len"], p["err"], p["checksum"], p["source"],
+                                           p["source_inc"], None))
+    h = {k: v.cpu().numpy() for k, v in c.items()}
+    k = int(h["rec_off"][n])
+    u32 = lambda a: a.view(np.uint32)  # noqa: E731
+    return dict(rec_off=u32(h["rec_off"]), addr=u32(h["addr"])[:k], src=u32(h["src"])[:k], status=h["status"][:k],
+                inc=h["inc"][:k], src_inc=h["src_inc"][:k], id_off=h["id_off"][:k].view(np.uint64),
+                addr_off=h["addr_off"][:k], addr_len=h["addr_len"][:k], err=h["err"][:n],
+                checksum=u32(h["checksum"])[:n], source=u32(h["source"])[:n], source_inc=h["source_inc"][:n])

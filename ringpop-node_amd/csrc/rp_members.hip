@@ -287,6 +287,18 @@ struct rp_members {
 
 using rp::guard;
 
+static rp::Members& MB(rp_members* m);
+
+namespace rp {
+// The interned addresses the wire codec (rp_wire.hip) reads and resolves against.
+NameTable& members_names(rp_members* h, hipStream_t* st, Scratch** ws) {
+    Members& m = MB(h);
+    *st = m.st;
+    *ws = &m.ws;
+    return m.nt;
+}
+}  // namespace rp
+
 static rp::Members& MB(rp_members* m) {
     if (!m) throw rp::Error(rp::RP_EINVAL, "null members handle");
     RP_HIP(hipSetDevice(m->impl.device));

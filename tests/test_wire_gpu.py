@@ -1,0 +1,169 @@
+"""GPU parity tests of the gossip wire codec through the C ABI (rp_wire_encode_changes_dev /
+rp_wire_decode_changes_dev): change records as dissemination.js:163-170 / 64-73 emit them,
+wrapped as ping-sender.js:71-76 and server/protocol/ping.js:45-48 bodies.
+
+Oracle: tests/golden/wire_golden.json (the reference's Dissemination run in node) and
+oracle/pywire.py (pinned against it in tests/test_oracle_wire.py). Bit-exact bytes.
+"""
+import json
+import os
+import random
+import sys
+import uuid
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
+import pywire  # noqa: E402
+
+ST = {"alive": 0, "suspect": 1, "faulty": 2, "leave": 3}
+NULL = 0xFFFFFFFF
+INT64_MIN = -(2 ** 63)
+
+
+def golden():
+    with open(os.path.join(HERE, "golden", "wire_golden.json")) as f:
+        return json.load(f)["cases"]
+
+
+def split(blob, off):
+    return [blob[int(off[j]):int(off[j + 1])].decode() for j in range(len(off) - 1)]
+
+
+def encode_cases(gpu, m, cases, form, body):
+    rec_off, addr, src, st, inc, sinc, ids = [0], [], [], [], [], [], []
+    cks, msrc, msinc = [], [], []
+    for c in cases:
+        if form == "issueAs":
+            rows = [(ch[0], ch[3], ch[1], ch[2], ch[4], ch[5]) for ch in c["changes"]]
+        else:
+            rows = [(mm[0], c["whoami"], mm[1], mm[2], 0, None) for mm in c["members"]]
+        for a, s_, status, i_, si, id_ in rows:
+            addr.append(m.intern([a])[0])
+            src.append(m.intern([s_])[0])
+            st.append(ST[status])
+            inc.append(i_)
+            sinc.append(si)
+            ids.append(np.frombuffer(id_.encode(), dtype=np.uint8) if id_ else None)
+        rec_off.append(len(addr))
+        cks.append(c["checksum"])
+        msrc.append(m.intern([c["whoami"]])[0])
+        msinc.append(c["whoamiInc"])
+    have_ids = form == "issueAs" and all(x is not None for x in ids)
+    idarr = np.stack(ids) if have_ids and ids else None
+    blob, off = gpu.wire_encode(m, np.array(rec_off), np.array(addr), np.array(src), np.array(st), np.array(inc),
+                                np.array(sinc), idarr, form=form, body=body, msg_checksum=cks, msg_source=msrc,
+                                msg_source_inc=msinc)
+    return split(blob, off)
+
+
+def test_encode_matches_reference_golden(gpu):
+    cases = golden()
+    m = gpu.Membership()
+    with_ids = [c for c in cases if all(ch[5] for ch in c["changes"])]
+    no_ids = [c for c in cases if c not in with_ids]
+    assert no_ids  # the golden holds an id-less case
+    for group in (with_ids, no_ids):
+        assert encode_cases(gpu, m, group, "issueAs", "array") == [c["out"]["issueAs"] for c in group]
+        assert encode_cases(gpu, m, group, "issueAs", "ping") == [c["out"]["ping"] for c in group]
+        assert encode_cases(gpu, m, group, "issueAs", "pingResponse") == [c["out"]["pingResponse"] for c in group]
+    assert encode_cases(gpu, m, cases, "fullSync", "array") == [c["out"]["fullSync"] for c in cases]
+
+
+def test_decode_reference_golden(gpu):
+    cases = golden()
+    m = gpu.Membership()
+    for c in cases:
+        m.intern([mm[0] for mm in c["members"]])
+    texts = []
+    for c in cases:
+        texts += [c["out"]["ping"], c["out"]["issueAs"], c["out"]["pingResponse"], c["out"]["fullSync"]]
+    d = gpu.wire_decode(m, texts)
+    assert (d["err"] == 0).all()
+    for j, t in enumerate(texts):
+        want = pywire.decode(t)
+        a, b = int(d["rec_off"][j]), int(d["rec_off"][j + 1])
+        assert b - a == len(want)
+        raw = t.encode()
+        for k, w in zip(range(a, b), want):
+            assert m.address(int(d["addr"][k])) == w["address"]
+            assert m.address(int(d["src"][k])) == w["source"]
+            assert int(d["status"][k]) == ST[w["status"]]
+            assert int(d["inc"][k]) == w["incarnationNumber"]
+            assert int(d["src_inc"][k]) == w.get("sourceIncarnationNumber", INT64_MIN)
+            if "id" in w:
+                o = int(d["id_off"][k]) - int(sum(len(x.encode()) for x in texts[:j]))
+                assert raw[o:o + 36].decode() == w["id"]
+            else:
+                assert int(d["id_off"][k]) == 2 ** 64 - 1
+    # ping headers (ping.js:27-36)
+    for i, c in enumerate(cases):
+        assert int(d["checksum"][4 * i]) == c["checksum"]
+        assert m.address(int(d["source"][4 * i])) == c["whoami"]
+        assert int(d["source_inc"][4 * i]) == c["whoamiInc"]
+
+
+def test_decode_tolerates_json_layout_and_flags_errors(gpu):
+    m = gpu.Membership()
+    m.intern(["10.0.0.1:1", "10.0.0.2:2"])
+    texts = [
+        ' { "changes" : [ {"status":"faulty", "extra":{"a":[1,{"b":"]"}]}, "incarnationNumber": 7,'
+        ' "address":"10.0.0.2:2"} ] , "checksum": 5 }\n',
+        '[{"address":"10.0.0.9:9","status":"alive","incarnationNumber":-3}]',  # not interned
+        '[]',
+        '[{"address":"10.0.0.1:1","status":"dead","incarnationNumber":1}]',  # bad status
+        '[{"address":"10.0.0.1:1","status":"alive","incarnationNumber":1.5}]',  # non-integral
+        '[{"address":"10.0\\u002e0.1:1","status":"alive","incarnationNumber":1}]',  # escape
+        '[{"address":"10.0.0.1:1","status":"alive"}]',  # missing incarnationNumber
+        '{"checksum":1}',  # no changes
+        '[{"address":"10.0.0.1:1","status":"leave","incarnationNumber":2}',  # truncated
+        '[{"address":"10.0.0.1:1","status":"leave","incarnationNumber":2}] x',  # trailing bytes
+        '',
+    ]
+    d = gpu.wire_decode(m, texts)
+    ok = [int(e) == 0 for e in d["err"]]
+    assert ok == [True, True, True] + [False] * 8
+    ro = d["rec_off"]
+    assert list(np.diff(ro)) == [1, 1, 0] + [0] * 8
+    assert m.address(int(d["addr"][0])) == "10.0.0.2:2" and int(d["status"][0]) == 2 and int(d["inc"][0]) == 7
+    assert int(d["src"][0]) == NULL and int(d["checksum"][0]) == 5
+    assert int(d["addr"][1]) == NULL and int(d["inc"][1]) == -3
+    o, n = int(d["addr_off"][1]), int(d["addr_len"][1])
+    base = len(texts[0].encode())
+    assert (texts[0] + texts[1]).encode()[o:o + n] == b"10.0.0.9:9" and o > base
+
+
+@pytest.mark.parametrize("n_msgs,max_recs", [(1, 0), (3000, 40), (20000, 90)])
+def test_round_trip_large(gpu, n_msgs, max_recs):
+    """encode -> decode identity at gossip scale, plus the oracle's bytes on a sample."""
+    rng = np.random.default_rng(n_msgs)
+    names = ["10.%d.%d.%d:%d" % (i >> 16, (i >> 8) & 255, i & 255, 3000 + i % 997) for i in range(5000)]
+    m = gpu.Membership()
+    m.intern(names)
+    counts = rng.integers(0, max_recs + 1, n_msgs)
+    rec_off = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint32)
+    k = int(rec_off[-1])
+    addr = rng.integers(0, len(names), k).astype(np.uint32)
+    src = rng.integers(0, len(names), k).astype(np.uint32)
+    st = rng.integers(0, 4, k).astype(np.uint8)
+    inc = rng.integers(-5, 2 ** 53, k).astype(np.int64)
+    sinc = rng.integers(0, 2 ** 53, k).astype(np.int64)
+    pyr = random.Random(n_msgs)
+    ids_s = [str(uuid.UUID(int=pyr.getrandbits(128), version=4)) for _ in range(k)]
+    ids = np.frombuffer("".join(ids_s).encode(), dtype=np.uint8).reshape(k, 36) if k else None
+    blob, off = gpu.wire_encode(m, rec_off, addr, src, st, inc, sinc, ids)
+    texts = split(blob, off)
+    for j in sorted(set(rng.integers(0, n_msgs, 50).tolist())):
+        recs = [pywire.issue_as_record(ids_s[r], names[src[r]], int(sinc[r]), names[addr[r]],
+                                       pywire.STATUS_NAME[st[r]], int(inc[r])) for r in range(rec_off[j], rec_off[j + 1])]
+        assert texts[j] == pywire.body(recs)
+    d = gpu.wire_decode(m, texts)
+    assert (d["err"] == 0).all()
+    assert (d["rec_off"] == rec_off).all()
+    assert (d["addr"] == addr).all() and (d["src"] == src).all() and (d["status"] == st).all()
+    assert (d["inc"] == inc).all() and (d["src_inc"] == sinc).all()
