@@ -191,6 +191,63 @@ def sim_cpu_baseline(n=10_000, kill_pct=1, seed=11, min_seconds=10.0, max_rounds
                       % (n, k, rounds, dt)}
 
 
+def wire_bench(rpa, dev, n_msgs=100_000, recs=32, reps=5):
+    """Gossip wire bodies (rp_wire_*): n_msgs ping request bodies (ping-sender.js:71-76), each
+    carrying `recs` issueAs change records (dissemination.js:163-170) over the C5 address set,
+    encoded to JSON and decoded back on the device. Reported as records/s and JSON GB/s (the
+    bytes written by the encoder / read by the decoder; both are bounded by HBM)."""
+    import ctypes
+    S = _synth()
+    n = 100_000
+    m = rpa.Membership(device=dev)
+    m.intern([S.c2_addr(i) for i in range(n)])
+    k = n_msgs * recs
+    g = torch.Generator(device="cuda").manual_seed(5)
+    ri = lambda hi, cnt, dt: torch.randint(0, hi, (cnt,), generator=g, device="cuda", dtype=dt)  # noqa: E731
+    rec_off = torch.arange(0, k + 1, recs, device="cuda", dtype=torch.int32)
+    addr, src = ri(n, k, torch.int32), ri(n, k, torch.int32)
+    st = ri(4, k, torch.uint8)
+    inc = ri(10 ** 7, k, torch.int64) + 1434401500000
+    sinc = ri(10 ** 7, k, torch.int64) + 1434401500000
+    ids = ri(16, k * 36, torch.uint8) + ord("a")
+    ck, msrc = ri(2 ** 31, n_msgs, torch.int32), ri(n, n_msgs, torch.int32)
+    msinc = ri(10 ** 7, n_msgs, torch.int64) + 1434401500000
+    out_off = torch.zeros(n_msgs + 1, dtype=torch.int64, device="cuda")
+    L = rpa.lib()
+    args = [m._h, n_msgs, rec_off.data_ptr(), k, addr.data_ptr(), src.data_ptr(), st.data_ptr(), inc.data_ptr(),
+            sinc.data_ptr(), ids.data_ptr(), 0, 1, ck.data_ptr(), msrc.data_ptr(), msinc.data_ptr()]
+    rpa.check(L.rp_wire_encode_changes_dev(*args, None, out_off.data_ptr(), None))
+    total = int(out_off[-1].item())
+    out = torch.empty(total, dtype=torch.uint8, device="cuda")
+    rec_off2 = torch.empty(n_msgs + 1, dtype=torch.int32, device="cuda")
+    e = lambda dt: torch.empty(k, dtype=dt, device="cuda")  # noqa: E731
+    cols = [e(torch.int32), e(torch.int32), e(torch.uint8), e(torch.int64), e(torch.int64)]
+    err = torch.empty(n_msgs, dtype=torch.int64, device="cuda")
+
+    def enc():
+        rpa.check(L.rp_wire_encode_changes_dev(*args, out.data_ptr(), out_off.data_ptr(), None))
+
+    def dec():
+        rpa.check(L.rp_wire_decode_changes_dev(m._h, out.data_ptr(), out_off.data_ptr(), n_msgs, rec_off2.data_ptr(),
+                                               k, *[c.data_ptr() for c in cols], None, None, None, err.data_ptr(),
+                                               None, None, None, None))
+        torch.cuda.synchronize()
+
+    res = {}
+    for name, fn in (("encode", enc), ("decode", dec)):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        dt = (time.perf_counter() - t0) / reps
+        res[name] = {"ms": dt * 1e3, "records_per_s": k / dt, "json_GBps": total / dt / 1e9}
+    ok = bool((err == 0).all().item()) and bool(torch.equal(cols[0], addr)) and bool(torch.equal(cols[3], inc))
+    m.close()
+    return {"workload": "%d ping request bodies x %d issueAs change records (C5 addresses), JSON encode + decode"
+                        % (n_msgs, recs), "json_bytes": total, "round_trip_ok": ok, **res}
+
+
 def pmc_traffic():
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
@@ -212,6 +269,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-merge", action="store_true")
+    ap.add_argument("--no-wire", action="store_true")
     ap.add_argument("--sim-n", type=int, default=10000, help="C4 members, one GPU (0: skip)")
     ap.add_argument("--sim5-n", type=int, default=100000, help="C5 members, sharded over all ranks (0: skip)")
     args = ap.parse_args()
@@ -302,6 +360,8 @@ def main():
             out["sim"] = sim_bench(rpa, local, n=args.sim_n)
         if sim5:
             out["sim_c5"] = sim5
+        if not args.no_wire:
+            out["wire"] = wire_bench(rpa, local)
         if not args.no_cpu:
             th = args.cpu_threads or min(16, os.cpu_count() or 1)
             out["cpu_baseline"] = cpu_baseline(servers, args.cpu_keys, th)

@@ -962,7 +962,7 @@ def wire_decode(members, texts):
     n = len(texts)
     off = np.zeros(n + 1, dtype=np.uint64)
     off[1:] = np.cumsum([len(t) for t in texts])
-    buf = _dev(np.frombuffer(b"".join(texts) or b"\0", dtype=np.uint8), np.uint8)
+    buf = _dev(np.frombuffer(b"".join(texts) or b"\0", dtype=np.uint8).copy(), np.uint8)
     d_off = _dev(off, np.uint64)
     cap = max(sum(t.count(b"{") for t in texts), 1)
     e = lambda dt, k=cap: torch.empty(k, dtype=dt, device="cuda")  # noqa: E731

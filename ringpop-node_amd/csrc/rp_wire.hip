@@ -194,6 +194,48 @@ __global__ void k_rec_write(Names nm, Recs R, Msgs M, uint32_t n_msgs, uint64_t 
     }
 }
 
+// Same records staged through LDS: each thread assembles its record in its own slot (65-dword
+// stride, so the 64 lanes' byte writes fall in distinct banks), then the wave stores the 64
+// records one after another with consecutive lanes on consecutive bytes — coalesced HBM
+// writes instead of 64 scattered byte streams. Records longer than a slot go direct.
+constexpr uint32_t kSlot = 260;
+constexpr uint32_t kWrThreads = 256;
+
+__global__ __launch_bounds__(kWrThreads) void k_rec_write_lds(Names nm, Recs R, Msgs M, uint32_t n_msgs,
+                                                              uint64_t n_rec, const uint32_t* moff,
+                                                              const uint32_t* rec_scan, uint8_t* out) {
+    __shared__ uint8_t buf[kWrThreads * kSlot];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint8_t* mine = buf + threadIdx.x * kSlot;
+    for (uint64_t base = blockIdx.x * (uint64_t)kWrThreads; base < n_rec; base += (uint64_t)gridDim.x * kWrThreads) {
+        const uint64_t r = base + threadIdx.x;
+        uint32_t len = 0;
+        uint64_t dst = 0;
+        if (r < n_rec) {
+            const uint32_t m = msg_of(M.rec_off, n_msgs, r);
+            Sink h{nullptr};
+            emit_head(h, M, m);
+            dst = moff[m] + h.n + (rec_scan[r] - rec_scan[M.rec_off[m]]);
+            const uint32_t full = rec_scan[r + 1] - rec_scan[r];
+            const bool comma = r + 1 < M.rec_off[m + 1];
+            Sink s{full <= kSlot ? mine : out + dst};
+            emit_record(s, nm, R, r);
+            if (comma) s.out[s.n] = ',';
+            len = full <= kSlot ? full : 0;
+        }
+        __syncthreads();
+        const uint8_t* wbuf = buf + wv * 64 * kSlot;
+        for (int j = 0; j < 64; j++) {
+            const uint32_t lj = __shfl(len, j);
+            const uint64_t dj = ((uint64_t)(uint32_t)__shfl((uint32_t)(dst >> 32), j) << 32) |
+                                (uint32_t)__shfl((uint32_t)dst, j);
+            const uint8_t* src = wbuf + j * kSlot;
+            for (uint32_t b = lane; b < lj; b += 64) out[dj + b] = src[b];
+        }
+        __syncthreads();
+    }
+}
+
 // ------------------------------------------------------------------ decoder
 struct In {
     const uint8_t* buf;
@@ -533,8 +575,8 @@ int rp_wire_encode_changes_dev(rp_members* m, uint32_t n_msgs, const uint32_t* d
                            n_msgs, mscan.p, rscan.p, d_out, d_out_off);
         RP_HIP(hipGetLastError());
         if (d_out && n_rec) {
-            hipLaunchKernelGGL(rp::k_rec_write, dim3(rp::grid_for(n_rec, 256)), dim3(256), 0, st, nm, R, M, n_msgs,
-                               n_rec, mscan.p, rscan.p, d_out);
+            hipLaunchKernelGGL(rp::k_rec_write_lds, dim3(rp::grid_for(n_rec, rp::kWrThreads, 4096)),
+                               dim3(rp::kWrThreads), 0, st, nm, R, M, n_msgs, n_rec, mscan.p, rscan.p, d_out);
             RP_HIP(hipGetLastError());
         }
         RP_HIP(hipStreamSynchronize(st));  // scratch buffers are local
