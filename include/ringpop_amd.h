@@ -190,6 +190,13 @@ int rp_wire_encode_changes_dev(rp_members *m, uint32_t n_msgs, const uint32_t *d
                                const int64_t *d_inc, const int64_t *d_src_inc, const uint8_t *d_ids, int form,
                                int body, const uint32_t *d_msg_checksum, const uint32_t *d_msg_source,
                                const int64_t *d_msg_source_inc, uint8_t *d_out, uint64_t *d_out_off, void *stream);
+/* Host-buffer form (staged through the handle's device; PCIe-bound): out NULL = size query
+ * (out_off filled); otherwise cap >= out_off[n_msgs]. n_rec = msg_rec_off[n_msgs]. */
+int rp_wire_encode_changes(rp_members *m, uint32_t n_msgs, const uint32_t *msg_rec_off, const uint32_t *addr,
+                           const uint32_t *src, const uint8_t *status, const int64_t *inc, const int64_t *src_inc,
+                           const uint8_t *ids, int form, int body, const uint32_t *msg_checksum,
+                           const uint32_t *msg_source, const int64_t *msg_source_inc, uint8_t *out, uint64_t cap,
+                           uint64_t *out_off);
 /* Decode n_msgs JSON texts d_buf[d_msg_off[j] .. d_msg_off[j+1]) — a changes array, or a body
  * object whose `changes` member is one (server/protocol/ping.js:27-36 reads the same members).
  * d_msg_rec_off[0..n_msgs] gets record offsets (total in [n_msgs]); records beyond rec_cap are
@@ -204,6 +211,10 @@ int rp_wire_decode_changes_dev(rp_members *m, const uint8_t *d_buf, const uint64
                                uint64_t *d_addr_off, uint32_t *d_addr_len, uint64_t *d_err,
                                uint32_t *d_msg_checksum, uint32_t *d_msg_source, int64_t *d_msg_source_inc,
                                void *stream);
+/* Host-buffer form of the decoder (record columns nullable; at most rec_cap records copied). */
+int rp_wire_decode_changes(rp_members *m, const char *buf, const uint64_t *msg_off, uint32_t n_msgs,
+                           uint32_t *msg_rec_off, uint32_t rec_cap, uint32_t *addr, uint32_t *src, uint8_t *status,
+                           int64_t *inc, int64_t *src_inc, uint64_t *err);
 
 /* ------------------------------------------------------------------ Gossip simulator
  * N full ringpop nodes (every node: membership view, dissemination buffer, ring membership,

@@ -85,6 +85,8 @@ SIGNATURES = {
     "rp_members_count": (_INT, [_P, _P]),
     "rp_wire_encode_changes_dev": (_INT, [_P, _U32, _P, _U64, _P, _P, _P, _P, _P, _P, _INT, _INT, _P, _P, _P, _P,
                                           _P, _P]),
+    "rp_wire_encode_changes": (_INT, [_P, _U32, _P, _P, _P, _P, _P, _P, _P, _INT, _INT, _P, _P, _P, _P, _U64, _P]),
+    "rp_wire_decode_changes": (_INT, [_P, _P, _P, _U32, _P, _U32, _P, _P, _P, _P, _P, _P]),
     "rp_wire_decode_changes_dev": (_INT, [_P, _P, _P, _U32, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                           _P, _P]),
     "rp_sim_create": (_INT, [_U32, _P, _P, _P, _P, _U32, _U32, ctypes.c_int64, _INT, _P]),

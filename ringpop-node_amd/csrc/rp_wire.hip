@@ -619,3 +619,96 @@ int rp_wire_decode_changes_dev(rp_members* m, const uint8_t* d_buf, const uint64
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------ host-buffer forms
+// For callers holding host memory (the N-API addon, ctypes): stage through the handle's
+// device, run the _dev form on the handle's stream, copy back. PCIe-bound.
+namespace {
+template <class T>
+T* stage(rp::DevBuf<T>& d, const T* h, uint64_t n, hipStream_t st) {
+    if (!h) return nullptr;
+    d.reserve(n ? n : 1);
+    if (n) RP_HIP(hipMemcpyAsync(d.p, h, sizeof(T) * n, hipMemcpyHostToDevice, st));
+    return d.p;
+}
+}  // namespace
+
+extern "C" {
+
+int rp_wire_encode_changes(rp_members* m, uint32_t n_msgs, const uint32_t* msg_rec_off, const uint32_t* addr,
+                           const uint32_t* src, const uint8_t* status, const int64_t* inc, const int64_t* src_inc,
+                           const uint8_t* ids, int form, int body, const uint32_t* msg_checksum,
+                           const uint32_t* msg_source, const int64_t* msg_source_inc, uint8_t* out, uint64_t cap,
+                           uint64_t* out_off) {
+    return guard([&] {
+        RP_REQUIRE(m && msg_rec_off && out_off, "null handle / offsets");
+        hipStream_t st;
+        rp::Scratch* ws;
+        rp::members_names(m, &st, &ws);
+        const uint64_t n_rec = msg_rec_off[n_msgs];
+        rp::DevBuf<uint32_t> d_ro, d_a, d_s, d_ck, d_ms;
+        rp::DevBuf<uint8_t> d_st, d_ids, d_out;
+        rp::DevBuf<int64_t> d_i, d_si, d_msi;
+        rp::DevBuf<uint64_t> d_oo;
+        stage(d_ro, msg_rec_off, (uint64_t)n_msgs + 1, st);
+        const bool ping = body == 1;
+        d_oo.reserve((uint64_t)n_msgs + 1);
+        auto run = [&](uint8_t* o) {
+            const int rc = rp_wire_encode_changes_dev(
+                m, n_msgs, d_ro.p, n_rec, stage(d_a, addr, n_rec, st), stage(d_s, src, n_rec, st),
+                stage(d_st, status, n_rec, st), stage(d_i, inc, n_rec, st), stage(d_si, src_inc, n_rec, st),
+                stage(d_ids, ids, n_rec * 36, st), form, body, ping ? stage(d_ck, msg_checksum, n_msgs, st) : nullptr,
+                ping ? stage(d_ms, msg_source, n_msgs, st) : nullptr,
+                ping ? stage(d_msi, msg_source_inc, n_msgs, st) : nullptr, o, d_oo.p, st);
+            if (rc) throw rp::Error(rc, rp_last_error());
+        };
+        run(nullptr);
+        RP_HIP(hipMemcpy(out_off, d_oo.p, sizeof(uint64_t) * (n_msgs + 1), hipMemcpyDeviceToHost));
+        const uint64_t total = out_off[n_msgs];
+        if (!out) return;  // size query
+        RP_REQUIRE(cap >= total, "encode: output buffer too small (query the size with out = NULL)");
+        d_out.reserve(total ? total : 1);
+        run(d_out.p);
+        if (total) RP_HIP(hipMemcpy(out, d_out.p, total, hipMemcpyDeviceToHost));
+    });
+}
+
+int rp_wire_decode_changes(rp_members* m, const char* buf, const uint64_t* msg_off, uint32_t n_msgs,
+                           uint32_t* msg_rec_off, uint32_t rec_cap, uint32_t* addr, uint32_t* src, uint8_t* status,
+                           int64_t* inc, int64_t* src_inc, uint64_t* err) {
+    return guard([&] {
+        RP_REQUIRE(m && msg_off && msg_rec_off && err, "null handle / offsets / errors");
+        hipStream_t st;
+        rp::Scratch* ws;
+        rp::members_names(m, &st, &ws);
+        const uint64_t nb = msg_off[n_msgs];
+        rp::DevBuf<uint8_t> d_buf, d_st;
+        rp::DevBuf<uint64_t> d_off, d_err;
+        rp::DevBuf<uint32_t> d_ro, d_a, d_s;
+        rp::DevBuf<int64_t> d_i, d_si;
+        stage(d_buf, reinterpret_cast<const uint8_t*>(buf), nb, st);
+        if (!buf) d_buf.reserve(1);
+        stage(d_off, msg_off, (uint64_t)n_msgs + 1, st);
+        d_ro.reserve((uint64_t)n_msgs + 1);
+        d_err.reserve(n_msgs ? n_msgs : 1);
+        const uint64_t c = rec_cap ? rec_cap : 1;
+        d_a.reserve(c); d_s.reserve(c); d_st.reserve(c); d_i.reserve(c); d_si.reserve(c);
+        const int rc = rp_wire_decode_changes_dev(m, d_buf.p, d_off.p, n_msgs, d_ro.p, rec_cap, d_a.p, d_s.p, d_st.p,
+                                                  d_i.p, d_si.p, nullptr, nullptr, nullptr, d_err.p, nullptr, nullptr,
+                                                  nullptr, st);
+        if (rc) throw rp::Error(rc, rp_last_error());
+        RP_HIP(hipStreamSynchronize(st));
+        RP_HIP(hipMemcpy(msg_rec_off, d_ro.p, sizeof(uint32_t) * (n_msgs + 1), hipMemcpyDeviceToHost));
+        if (n_msgs) RP_HIP(hipMemcpy(err, d_err.p, sizeof(uint64_t) * n_msgs, hipMemcpyDeviceToHost));
+        const uint64_t k = std::min<uint64_t>(msg_rec_off[n_msgs], rec_cap);
+        if (k) {
+            if (addr) RP_HIP(hipMemcpy(addr, d_a.p, 4 * k, hipMemcpyDeviceToHost));
+            if (src) RP_HIP(hipMemcpy(src, d_s.p, 4 * k, hipMemcpyDeviceToHost));
+            if (status) RP_HIP(hipMemcpy(status, d_st.p, k, hipMemcpyDeviceToHost));
+            if (inc) RP_HIP(hipMemcpy(inc, d_i.p, 8 * k, hipMemcpyDeviceToHost));
+            if (src_inc) RP_HIP(hipMemcpy(src_inc, d_si.p, 8 * k, hipMemcpyDeviceToHost));
+        }
+    });
+}
+
+}  // extern "C"

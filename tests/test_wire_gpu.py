@@ -167,3 +167,50 @@ def test_round_trip_large(gpu, n_msgs, max_recs):
     assert (d["rec_off"] == rec_off).all()
     assert (d["addr"] == addr).all() and (d["src"] == src).all() and (d["status"] == st).all()
     assert (d["inc"] == inc).all() and (d["src_inc"] == sinc).all()
+
+
+def test_host_buffer_forms_match_device_forms(gpu):
+    """rp_wire_encode_changes / rp_wire_decode_changes (host buffers) == the _dev forms."""
+    import ctypes
+    cases = golden()
+    m = gpu.Membership()
+    c = cases[2]
+    want = encode_cases(gpu, m, [c], "issueAs", "ping")[0]
+    L = gpu.lib()
+    ro = np.array([0, len(c["changes"])], dtype=np.uint32)
+    addr = np.array(m.intern([ch[0] for ch in c["changes"]]), dtype=np.uint32)
+    src = np.array(m.intern([ch[3] for ch in c["changes"]]), dtype=np.uint32)
+    st = np.array([ST[ch[1]] for ch in c["changes"]], dtype=np.uint8)
+    inc = np.array([ch[2] for ch in c["changes"]], dtype=np.int64)
+    sinc = np.array([ch[4] for ch in c["changes"]], dtype=np.int64)
+    ids = np.frombuffer("".join(ch[5] for ch in c["changes"]).encode(), dtype=np.uint8).copy()
+    ck = np.array([c["checksum"]], dtype=np.uint32)
+    ms = np.array(m.intern([c["whoami"]]), dtype=np.uint32)
+    msi = np.array([c["whoamiInc"]], dtype=np.int64)
+    off = np.zeros(2, dtype=np.uint64)
+    args = [m._h, 1, ro.ctypes.data, addr.ctypes.data, src.ctypes.data, st.ctypes.data, inc.ctypes.data,
+            sinc.ctypes.data, ids.ctypes.data, 0, 1, ck.ctypes.data, ms.ctypes.data, msi.ctypes.data]
+    gpu.check(L.rp_wire_encode_changes(*args, None, 0, off.ctypes.data))
+    out = np.zeros(int(off[1]), dtype=np.uint8)
+    assert L.rp_wire_encode_changes(*args, out.ctypes.data, len(out) - 1, off.ctypes.data) != 0  # too small
+    gpu.check(L.rp_wire_encode_changes(*args, out.ctypes.data, len(out), off.ctypes.data))
+    assert out.tobytes().decode() == want == c["out"]["ping"]
+    texts = [want.encode(), b"[", c["out"]["fullSync"].encode()]
+    moff = np.concatenate([[0], np.cumsum([len(t) for t in texts])]).astype(np.uint64)
+    blob = b"".join(texts)
+    cap = 1000
+    rro = np.zeros(4, dtype=np.uint32)
+    a2, s2 = np.zeros(cap, dtype=np.uint32), np.zeros(cap, dtype=np.uint32)
+    st2, i2, si2 = np.zeros(cap, dtype=np.uint8), np.zeros(cap, dtype=np.int64), np.zeros(cap, dtype=np.int64)
+    err = np.zeros(3, dtype=np.uint64)
+    m.intern([mm[0] for mm in c["members"]])
+    gpu.check(L.rp_wire_decode_changes(m._h, blob, moff.ctypes.data, 3, rro.ctypes.data, cap, a2.ctypes.data,
+                                       s2.ctypes.data, st2.ctypes.data, i2.ctypes.data, si2.ctypes.data,
+                                       err.ctypes.data))
+    assert err[0] == 0 and err[1] != 0 and err[2] == 0
+    k = len(c["changes"])
+    assert list(np.diff(rro)) == [k, 0, len(c["members"])]
+    assert (a2[:k] == addr).all() and (s2[:k] == src).all() and (st2[:k] == st).all() and (i2[:k] == inc).all()
+    assert (si2[:k] == sinc).all()
+    fs = pywire.decode(c["out"]["fullSync"])
+    assert [m.address(int(x)) for x in a2[k:k + len(fs)]] == [r["address"] for r in fs]
