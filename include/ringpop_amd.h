@@ -267,6 +267,29 @@ int rp_sim_inbox(rp_sim *s, const uint64_t *nmsg, const uint64_t *nrec, void **m
 int rp_sim_exchange_local(rp_sim *const *shards, uint32_t nshards);
 int rp_sim_converged_local(rp_sim *s, uint32_t *out4);
 
+/* ---- Scenarios. Events run before phase A of their round, in the order given:
+ *   RP_SIM_KILL    the node goes down (crash / SIGSTOP, scripts/tick-cluster.js:417-470): it
+ *                  neither acts nor answers; its state is kept
+ *   RP_SIM_REVIVE  it comes back with that state (SIGCONT)
+ *   RP_SIM_LEAVE   the admin leave (server/admin/member.js:70-98): makeLeave(whoami, own
+ *                  incarnation) (lib/membership/index.js:191-195), as the convergence scenarios
+ *                  send it (benchmarks/convergence-time/scenarios/); its LocalMemberLeaveEvent
+ *                  stops the node's gossip loop and suspicion (on_membership_event.js:32-40). A
+ *                  node that is down, or left already, ignores it.
+ * Convergence then reads: every node that is up and has not left holds the same checksum, each
+ * member that left is `leave` and each other member that is down `faulty` in those views.
+ * dead[] = down from the start (never started gossip; gossip/index.js:97 never shuffled). */
+typedef struct rp_sim_event {
+    uint32_t round, kind, node, reserved;
+} rp_sim_event;
+enum { RP_SIM_KILL = 0, RP_SIM_REVIVE = 1, RP_SIM_LEAVE = 2 };
+int rp_sim_create_scenario(uint32_t n, const char *names, const uint32_t *off, const int64_t *inc0,
+                           const uint8_t *dead, uint32_t seed, uint32_t suspicion_rounds, int64_t now0, int device,
+                           const uint32_t *bounds, uint32_t nshards, uint32_t shard, const rp_sim_event *events,
+                           uint32_t n_events, rp_sim **out);
+/* Every local node's dissemination.maxPiggybackCount (dissemination.js:38-55), [shard nodes]. */
+int rp_sim_piggyback(rp_sim *s, uint32_t *out);
+
 /* Stream-ordered copy between any host / device buffers (hipMemcpyDefault); NULL stream =
  * synchronous. Used by hosts that move sharded-simulator messages. */
 int rp_copy(void *dst, const void *src, uint64_t bytes, void *stream);

@@ -94,6 +94,10 @@ def lib():
         L.orc_sim_converged.restype = ctypes.c_int
         L.orc_sim_converged.argtypes = [ctypes.c_void_p]
         L.orc_sim_stats.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_sim_event.restype = ctypes.c_int
+        L.orc_sim_event.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32]
+        L.orc_sim_set_threads.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.orc_sim_piggyback.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -291,18 +295,34 @@ class Members:
         return buf.raw[:n].decode()
 
 
-class Sim:
-    """Oracle gossip round model (orc_sim.c)."""
+SIM_EVENT = {"kill": 0, "revive": 1, "leave": 2}
 
-    def __init__(self, names, inc0, dead, seed=11, susp_rounds=25, now0=1434500000000):
+
+class Sim:
+    """Oracle gossip round model (orc_sim.c). events: (round, kind, node) with kind in
+    SIM_EVENT, applied before that round (a node down from round r on, back up, or leaving)."""
+
+    def __init__(self, names, inc0, dead, seed=11, susp_rounds=25, now0=1434500000000, events=(), threads=None):
         self.N = len(names)
+        self.events = sorted(((int(r), SIM_EVENT.get(k, k), int(v)) for r, k, v in events),
+                             key=lambda e: e[0])
         blob, off = pack_strings(names)
         self._blob = ctypes.create_string_buffer(blob, len(blob) + 1)
         self._off = off
         inc0 = np.ascontiguousarray(inc0, dtype=np.int64)
         dead = np.ascontiguousarray(dead, dtype=np.uint8)
-        self.h = lib().orc_sim_new(self.N, seed, susp_rounds, now0, self._blob, off.ctypes.data, inc0.ctypes.data,
-                                   dead.ctypes.data)
+        prev = os.environ.get("ORC_SIM_THREADS")
+        if threads:
+            os.environ["ORC_SIM_THREADS"] = str(int(threads))
+        try:
+            self.h = lib().orc_sim_new(self.N, seed, susp_rounds, now0, self._blob, off.ctypes.data,
+                                       inc0.ctypes.data, dead.ctypes.data)
+        finally:
+            if threads:
+                if prev is None:
+                    os.environ.pop("ORC_SIM_THREADS", None)
+                else:
+                    os.environ["ORC_SIM_THREADS"] = prev
 
     def __del__(self):
         if getattr(self, "h", None):
@@ -310,6 +330,10 @@ class Sim:
             self.h = None
 
     def step(self):
+        r = self.round
+        for er, k, v in self.events:
+            if er == r:
+                lib().orc_sim_event(self.h, k, v)
         lib().orc_sim_step(self.h)
 
     @property
@@ -329,6 +353,11 @@ class Sim:
 
     def converged(self):
         return bool(lib().orc_sim_converged(self.h))
+
+    def piggyback(self):
+        out = np.empty(self.N, dtype=np.uint32)
+        lib().orc_sim_piggyback(self.h, out.ctypes.data)
+        return out
 
     def stats(self):
         out = np.zeros(4, dtype=np.uint64)

@@ -106,6 +106,9 @@ SIGNATURES = {
     "rp_sim_inbox": (_INT, [_P, _P, _P, _P, _P]),
     "rp_sim_exchange_local": (_INT, [_P, _U32]),
     "rp_sim_converged_local": (_INT, [_P, _P]),
+    "rp_sim_create_scenario": (_INT, [_U32, _P, _P, _P, _P, _U32, _U32, ctypes.c_int64, _INT, _P, _U32, _U32, _P, _U32,
+                                      _P]),
+    "rp_sim_piggyback": (_INT, [_P, _P]),
     "rp_copy": (_INT, [_P, _P, _U64, _P]),
 }
 
@@ -575,21 +578,40 @@ class Membership:
                                           d_new_inc, d_n_applied, stream))
 
 
+SIM_EVENT = {"kill": 0, "revive": 1, "leave": 2}
+
+
+def _events(events):
+    """(round, kind, node) triples -> rp_sim_event[] (uint32 x 4 each); kind a SIM_EVENT name or code."""
+    ev = np.zeros((max(len(events), 1), 4), dtype=np.uint32)
+    for i, (r, k, v) in enumerate(events):
+        ev[i, :3] = (int(r), SIM_EVENT.get(k, k), int(v))
+    return ev, len(events)
+
+
+def _sim_create(names, inc0, dead, seed, suspicion_rounds, now0, device, bounds, nshards, shard, events):
+    buf, off = _pack(names)
+    inc0 = np.ascontiguousarray(inc0, dtype=np.int64)
+    dead = np.ascontiguousarray(dead, dtype=np.uint8)
+    if now0 is None:
+        now0 = 1434401518824 + 10 ** 9
+    ev, nev = _events(events or [])
+    h = ctypes.c_void_p()
+    check(lib().rp_sim_create_scenario(len(names), buf, off.ctypes.data, inc0.ctypes.data, dead.ctypes.data, seed,
+                                       suspicion_rounds, int(now0), device,
+                                       None if bounds is None else bounds.ctypes.data, nshards, shard,
+                                       ev.ctypes.data, nev, ctypes.byref(h)))
+    return h
+
+
 class GossipSim:
     """N full ringpop nodes advanced in the deterministic gossip round model on the device
-    (DESIGN.md §SWIM round model; oracle/orc_sim.c restates it on the CPU)."""
+    (DESIGN.md §SWIM round model; oracle/orc_sim.c restates it on the CPU). events: scenario
+    (round, kind, node) triples, kind in SIM_EVENT (include/ringpop_amd.h "Scenarios")."""
 
-    def __init__(self, names, inc0, dead, seed=11, suspicion_rounds=25, now0=None, device=0):
+    def __init__(self, names, inc0, dead, seed=11, suspicion_rounds=25, now0=None, device=0, events=()):
         self.N = len(names)
-        buf, off = _pack(names)
-        inc0 = np.ascontiguousarray(inc0, dtype=np.int64)
-        dead = np.ascontiguousarray(dead, dtype=np.uint8)
-        if now0 is None:
-            now0 = 1434401518824 + 10 ** 9
-        h = ctypes.c_void_p()
-        check(lib().rp_sim_create(self.N, buf, off.ctypes.data, inc0.ctypes.data, dead.ctypes.data, seed,
-                                  suspicion_rounds, int(now0), device, ctypes.byref(h)))
-        self._h = h
+        self._h = _sim_create(names, inc0, dead, seed, suspicion_rounds, now0, device, None, 1, 0, events)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -638,6 +660,12 @@ class GossipSim:
         check(lib().rp_sim_stats(self._h, out.ctypes.data))
         return dict(zip(["pings", "pingreqs", "fullsyncs", "applied"], (int(x) for x in out)))
 
+    def piggyback(self):
+        """Every node's dissemination.maxPiggybackCount."""
+        out = np.empty(self.N, dtype=np.uint32)
+        check(lib().rp_sim_piggyback(self._h, out.ctypes.data))
+        return out
+
 
 # ---------------------------------------------------------------------------------------------
 # Sharded simulator (C5): nodes partitioned over shards; a round = five stages + four message
@@ -658,22 +686,15 @@ class SimShard:
     """One shard handle of the gossip simulator: nodes [v0, v0 + NL) with full views."""
 
     def __init__(self, names, inc0, dead, nshards, shard, seed=11, suspicion_rounds=25, now0=None, device=0,
-                 bounds=None):
+                 bounds=None, events=()):
         self.N = len(names)
         self.G = nshards
         self.shard = shard
-        buf, off = _pack(names)
-        inc0 = np.ascontiguousarray(inc0, dtype=np.int64)
         self.dead = np.ascontiguousarray(dead, dtype=np.uint8)
         self.bounds = np.ascontiguousarray(bounds if bounds is not None else shard_bounds(self.N, nshards),
                                            dtype=np.uint32)
-        if now0 is None:
-            now0 = 1434401518824 + 10 ** 9
-        h = ctypes.c_void_p()
-        check(lib().rp_sim_create_shard(self.N, buf, off.ctypes.data, inc0.ctypes.data, self.dead.ctypes.data, seed,
-                                        suspicion_rounds, int(now0), device, self.bounds.ctypes.data, nshards, shard,
-                                        ctypes.byref(h)))
-        self._h = h
+        self._h = _sim_create(names, inc0, self.dead, seed, suspicion_rounds, now0, device, self.bounds, nshards,
+                              shard, events)
         self.v0 = int(self.bounds[shard])
         self.NL = int(self.bounds[shard + 1]) - self.v0
 
@@ -735,6 +756,12 @@ class SimShard:
         check(lib().rp_sim_stats(self._h, out.ctypes.data))
         return out
 
+    def piggyback(self):
+        out = np.empty(self.NL, dtype=np.uint32)
+        if self.NL:
+            check(lib().rp_sim_piggyback(self._h, out.ctypes.data))
+        return out
+
 
 def conv_reduce(parts):
     """Convergence (scenario-runner.js:152-170 + killed members faulty everywhere) from the
@@ -756,12 +783,12 @@ class ShardedGossipSim:
     results as GossipSim; used to test the sharded path on one GPU."""
 
     def __init__(self, names, inc0, dead, nshards, seed=11, suspicion_rounds=25, now0=None, devices=None,
-                 bounds=None):
+                 bounds=None, events=()):
         self.N = len(names)
         self.G = nshards
         devices = devices or [0] * nshards
-        self.shards = [SimShard(names, inc0, dead, nshards, g, seed, suspicion_rounds, now0, devices[g], bounds)
-                       for g in range(nshards)]
+        self.shards = [SimShard(names, inc0, dead, nshards, g, seed, suspicion_rounds, now0, devices[g], bounds,
+                                events) for g in range(nshards)]
         self._arr = (ctypes.c_void_p * nshards)(*[s._h.value for s in self.shards])
 
     def close(self):
@@ -795,6 +822,9 @@ class ShardedGossipSim:
     def stats(self):
         tot = sum(s.stats() for s in self.shards)
         return dict(zip(_STAT_NAMES, (int(x) for x in tot)))
+
+    def piggyback(self):
+        return np.concatenate([s.piggyback() for s in self.shards])
 
 
 class MessageExchange:
@@ -862,13 +892,14 @@ class DistGossipSim:
     sharded by node id range, the four per-round message exchanges as RCCL all-to-all-v).
     Results equal GossipSim's on the same inputs."""
 
-    def __init__(self, names, inc0, dead, seed=11, suspicion_rounds=25, now0=None, device=0, group=None):
+    def __init__(self, names, inc0, dead, seed=11, suspicion_rounds=25, now0=None, device=0, group=None, events=()):
         import torch.distributed as dist
         self.dist, self.group = dist, group
         self.xchg = MessageExchange(group, device=device)
         self.G, self.rank = self.xchg.G, self.xchg.rank
         self.N = len(names)
-        self.shard = SimShard(names, inc0, dead, self.G, self.rank, seed, suspicion_rounds, now0, device)
+        self.shard = SimShard(names, inc0, dead, self.G, self.rank, seed, suspicion_rounds, now0, device,
+                              events=events)
         self.exchange_bytes = 0
 
     def close(self):

@@ -24,7 +24,7 @@
 //
 // HBM layout (sized for 10^5 members on one MI355X):
 //   dense rows [lv][a]  status u8 (bit 7: in this node's ring) | incarnation i64 | members-array
-//                       order u32 | dissemination slot u16  (15 B per (node, member))
+//                       order u32 | dissemination slot u32  (17 B per (node, member))
 //   per node            deviation bitmap over address ranks (which rows ever changed), sparse
 //                       change list (dissemination's `changes` map: address, piggyback count,
 //                       source, source incarnation; the status/incarnation of a change always
@@ -121,7 +121,7 @@ struct SimDev {
     uint8_t* st;
     int64_t* inc;
     uint32_t* order;
-    uint16_t* slot;  // 0 = no change, else index + 1 into the node's change list
+    uint32_t* slot;  // 0 = no change, else index + 1 into the node's change list
     uint32_t* dev;   // [lv][W] rows ever changed, by address rank
     // sparse per node
     Change* chg;  // [lv][Cd]
@@ -132,7 +132,8 @@ struct SimDev {
     int64_t* it_idx;
     uint32_t *n_shuf, *ring_count, *max_piggy, *checksum;
     uint8_t* dirty;
-    const uint8_t* dead;  // [N] (global)
+    const uint8_t* dead;  // [N] (global): down this round (never started, crashed, suspended)
+    uint8_t* stopped;     // [NL] own status became leave: gossip.stop() + suspicion.stopAll()
     // names in address order; base checksum string (global)
     const uint32_t* sorted;
     const uint32_t* rank;
@@ -295,7 +296,7 @@ __device__ __forceinline__ uint64_t status_u64(uint8_t s) {
     uint64_t v = 0x6576696c61ull;        // alive
     v = s == 1 ? 0x74636570737573ull : v;  // suspect
     v = s == 2 ? 0x79746c756166ull : v;    // faulty
-    v = s == 3 ? 0x6576616c65ull : v;      // leave
+    v = s == 3 ? 0x657661656cull : v;      // leave
     return v;
 }
 // status_len without branches: lengths 5 7 6 5 as nibbles
@@ -1544,11 +1545,12 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_ck_pc(SimDev S) {
 __device__ uint32_t block_apply(const SimDev& S, uint32_t lv, const Rec* recs, uint32_t n, Lds& L, int64_t now) {
     const uint32_t v = S.v0 + lv;
     const uint64_t row = (uint64_t)lv * S.N;
-    uint32_t napp = 0, nadd = 0, nrem = 0;
+    uint32_t napp = 0, nadd = 0, nrem = 0, nleave = 0;
     Change* chg = S.chg + (uint64_t)lv * S.Cd;
     Timer* tim = S.tim + (uint64_t)lv * S.Ct;
     __syncthreads();
     uint32_t nc = S.n_chg[lv], nt = S.n_tim[lv];
+    const bool stopped = S.stopped[lv] != 0;
     for (uint32_t base = 0; base < n; base += kT) {
         const uint32_t i = base + threadIdx.x;
         bool applied = false, need_timer = false, need_new = false;
@@ -1578,7 +1580,9 @@ __device__ uint32_t block_apply(const SimDev& S, uint32_t lv, const Rec* recs, u
                 S.inc[row + a] = ui;
                 const uint32_t k = S.rank[a];
                 atomicOr(&S.dev[(uint64_t)lv * S.W + (k >> 5)], 1u << (k & 31));
-                need_timer = us == ST_SUSPECT && a != v;
+                need_timer = us == ST_SUSPECT && a != v && !stopped;
+                // the local member becoming `leave` (LocalMemberLeaveEvent, member.js:87-95)
+                if (a == v && us == ST_LEAVE && (cur & ST_MASK) != ST_LEAVE) nleave++;
                 slot = S.slot[row + a];
                 need_new = slot == 0;
             }
@@ -1601,7 +1605,7 @@ __device__ uint32_t block_apply(const SimDev& S, uint32_t lv, const Rec* recs, u
                 const uint32_t idx = nc + cpos;
                 if (idx < S.Cd) {
                     chg[idx] = Change{a, 0u, r.src, 0u, r.srcinc};
-                    S.slot[row + a] = (uint16_t)(idx + 1);
+                    S.slot[row + a] = idx + 1;
                 } else {
                     set_err(S, ERR_CHANGES);
                 }
@@ -1613,9 +1617,13 @@ __device__ uint32_t block_apply(const SimDev& S, uint32_t lv, const Rec* recs, u
     const uint32_t tot = block_sum(napp, L.u);
     const uint32_t adds = block_sum(nadd, L.u);
     const uint32_t rems = block_sum(nrem, L.u);
+    const uint32_t leaves = block_sum(nleave, L.u);
     if (threadIdx.x == 0) {
         S.n_chg[lv] = nc;
-        S.n_tim[lv] = nt;
+        // gossip.stop() + suspicion.stopAll() (on_membership_event.js:32-40): every timer is
+        // cleared, the ones this batch started included (they start after the event)
+        S.n_tim[lv] = leaves ? 0u : nt;
+        if (leaves) S.stopped[lv] = 1;
         if (tot) {
             S.dirty[lv] = 1;
             atomicAdd(&S.stats[3], (unsigned long long)tot);
@@ -1664,7 +1672,7 @@ __device__ uint32_t block_issue(const SimDev& S, uint32_t lv, uint32_t sender, i
         if (j < nc) {
             if (keep) {
                 chg[kept + kpos] = c;
-                S.slot[row + c.addr] = (uint16_t)(kept + kpos + 1);
+                S.slot[row + c.addr] = kept + kpos + 1;
             } else {
                 S.slot[row + c.addr] = 0;
             }
@@ -1783,7 +1791,7 @@ __global__ __launch_bounds__(kT) void k_phase_a(SimDev S) {
     __shared__ int32_t tgt;
     for (uint32_t lv = blockIdx.x; lv < S.NL; lv += gridDim.x) {
         const uint32_t v = S.v0 + lv;
-        if (S.dead[v]) {
+        if (S.dead[v] || S.stopped[lv]) {  // down, or its gossip loop stopped by a leave
             if (threadIdx.x == 0) S.target[lv] = -1;
             continue;
         }
@@ -1947,7 +1955,7 @@ __global__ __launch_bounds__(kT) void k_phase_d1(SimDev S, const uint32_t* __res
             if (j < nc) {
                 if (keep) {
                     chg[kept + kpos] = c;
-                    S.slot[row + c.addr] = (uint16_t)(kept + kpos + 1);
+                    S.slot[row + c.addr] = kept + kpos + 1;
                 } else {
                     S.slot[row + c.addr] = 0;
                 }
@@ -2028,7 +2036,7 @@ __global__ __launch_bounds__(kT) void k_phase_e(SimDev S) {
     const int64_t now = S.now0 + 200 * S.round;
     for (uint32_t lv = blockIdx.x; lv < S.NL; lv += gridDim.x) {
         const uint32_t v = S.v0 + lv;
-        if (S.dead[v]) continue;
+        if (S.dead[v] || S.stopped[lv]) continue;
         const uint64_t row = (uint64_t)lv * S.N;
         const int64_t srci = S.inc[row + v];
         Rec* stage = ping_slot(S, lv);  // free: the ping left in the exchange after phase A
@@ -2062,6 +2070,20 @@ __global__ __launch_bounds__(kT) void k_phase_e(SimDev S) {
             written = S.Cm;
         }
         if (written) block_apply(S, lv, stage, written, L, now);
+    }
+}
+
+// Scenario leaves (server/admin/member.js:92-93): makeLeave(whoami, own incarnation) on each
+// listed local node whose own status is not `leave` yet (a redundant leave is refused, :84-89)
+__global__ __launch_bounds__(kT) void k_leave(SimDev S, const uint32_t* __restrict__ list, uint32_t n) {
+    __shared__ Lds L;
+    __shared__ Rec tmp;
+    const int64_t now = S.now0 + 200 * S.round;
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const uint32_t lv = list[i], v = S.v0 + lv;
+        const uint64_t row = (uint64_t)lv * S.N;
+        if ((S.st[row + v] & ST_MASK) == ST_LEAVE) continue;
+        block_make(S, lv, v, ST_LEAVE, S.inc[row + v], L, now, &tmp);
     }
 }
 
@@ -2200,17 +2222,20 @@ __global__ void k_csr(const uint32_t* __restrict__ keys, uint32_t n, uint32_t N,
     }
 }
 
-// ---- convergence over this shard's live nodes: {live count, min checksum, max checksum,
-// killed members not faulty in some local live view}
-__global__ void k_conv_local(SimDev S, const uint32_t* __restrict__ killed, uint32_t nk, uint32_t* __restrict__ out) {
+// ---- convergence over this shard's nodes that are up and have not left (scenario-runner.js's
+// hostToAliveWorker): {count, min checksum, max checksum, some wanted member not at its wanted
+// status in one of those views}. want[i] = member | status << 24: a member that left must be
+// `leave`, any other member that is down `faulty`.
+__global__ void k_conv_local(SimDev S, const uint8_t* __restrict__ skip, const uint32_t* __restrict__ want,
+                             uint32_t nk, uint32_t* __restrict__ out) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (uint64_t)S.NL * nk;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t lv = (uint32_t)(i / nk), a = killed[i % nk];
-        if (S.dead[S.v0 + lv]) continue;
-        if ((S.st[(uint64_t)lv * S.N + a] & ST_MASK) != ST_FAULTY) out[3] = 1;
+        const uint32_t lv = (uint32_t)(i / nk), w = want[i % nk], a = w & 0xFFFFFFu;
+        if (skip[S.v0 + lv]) continue;
+        if ((S.st[(uint64_t)lv * S.N + a] & ST_MASK) != (w >> 24)) out[3] = 1;
     }
     for (uint32_t lv = blockIdx.x * blockDim.x + threadIdx.x; lv < S.NL; lv += gridDim.x * blockDim.x) {
-        if (S.dead[S.v0 + lv]) continue;
+        if (skip[S.v0 + lv]) continue;
         atomicAdd(&out[0], 1u);
         atomicMin(&out[1], S.checksum[lv]);
         atomicMax(&out[2], S.checksum[lv]);
@@ -2240,6 +2265,7 @@ __global__ void k_sim_init(SimDev S) {
         S.n_tim[lv] = 0;
         S.target[lv] = -1;
         S.nhelp[lv] = 0;
+        S.stopped[lv] = 0;
     }
 }
 
@@ -2285,12 +2311,12 @@ struct Sim {
     unsigned grid = 0;
     NameTable nt;
     SimDev d{};
-    DevBuf<uint8_t> st_, dirty, dead, strbuf, sbase;
+    DevBuf<uint8_t> st_, dirty, dead, strbuf, sbase, stopped, cskip;
     DevBuf<int64_t> inc, it_idx, inc_snap, inc0;
     DevBuf<int32_t> target;
-    DevBuf<uint16_t> slot;
+    DevBuf<uint32_t> slot;
     DevBuf<uint32_t> order, dev, n_chg, n_tim, n_shuf, ring_count, max_piggy, checksum, ck_snap, ping_n, leg_n,
-        helpers, nhelp, leg_nk, cand, rank, err, bounds, killed, conv;
+        helpers, nhelp, leg_nk, cand, rank, err, bounds, want, conv, leave_list;
     DevBuf<uint32_t> okey, oval, ocnt, ooff, omoff;  // outbox build
     DevBuf<uint32_t> ib_off, ib_idx, ikey;         // inbox build
     DevBuf<uint32_t> rsp_n, resp_idx, lresp_idx, d1list;
@@ -2302,9 +2328,12 @@ struct Sim {
     DevBuf<unsigned long long> stats, cursor;
     MsgBuf out, in;
     Scratch ws;
-    std::vector<uint8_t> h_dead;
+    std::vector<uint8_t> h_dead, h_left;
     std::vector<uint32_t> h_bounds;
-    uint32_t nkilled = 0;
+    std::vector<rp_sim_event> events;  // the scenario, by round
+    size_t next_event = 0;
+    uint32_t nwant = 0;
+    bool conv_dirty = true;
     int64_t round = 0;
     int next_stage = 0;  // 0..4 within a round
 
@@ -2451,6 +2480,7 @@ struct Sim {
         const unsigned g = grid;
         switch (k) {
         case 0:
+            apply_events();
             hipLaunchKernelGGL(k_round_begin, dim3(1), dim3(64), 0, st, d);
             refresh_checksums();
             if (NL) hipLaunchKernelGGL(k_phase_a, dim3(g), dim3(kT), 0, st, d);
@@ -2508,14 +2538,60 @@ struct Sim {
         if (e & ERR_ARENA) throw Error(RP_ESTATE, "sim: the per-round message arena overflowed (RP_SIM_ARENA)");
     }
 
-    // {live, min checksum, max checksum, some killed member not faulty in a live view}
+    // The scenario's events of this round, before phase A: a node goes down or comes back (every
+    // shard keeps the global down flags), or leaves (on the shard that owns it).
+    void apply_events() {
+        bool down_changed = false;
+        std::vector<uint32_t> leaves;
+        while (next_event < events.size() && events[next_event].round <= (uint64_t)round) {
+            const rp_sim_event& e = events[next_event++];
+            if (e.round != (uint64_t)round) continue;
+            if (e.kind == RP_SIM_KILL || e.kind == RP_SIM_REVIVE) {
+                const uint8_t dv = e.kind == RP_SIM_KILL ? 1 : 0;
+                down_changed |= h_dead[e.node] != dv;
+                h_dead[e.node] = dv;
+            } else if (!h_dead[e.node] && !h_left[e.node]) {
+                h_left[e.node] = 1;
+                if (e.node >= v0 && e.node < v0 + NL) leaves.push_back(e.node - v0);
+            }
+            conv_dirty = true;
+        }
+        if (down_changed) RP_HIP(hipMemcpyAsync(dead.p, h_dead.data(), N, hipMemcpyHostToDevice, st));
+        if (!leaves.empty()) {
+            leave_list.reserve(leaves.size());
+            RP_HIP(hipMemcpyAsync(leave_list.p, leaves.data(), 4 * leaves.size(), hipMemcpyHostToDevice, st));
+            d.round = round;
+            hipLaunchKernelGGL(k_leave, dim3((unsigned)std::min<size_t>(leaves.size(), 1024)), dim3(kT), 0, st, d,
+                               leave_list.p, (uint32_t)leaves.size());
+            RP_HIP(hipGetLastError());
+        }
+        if (down_changed || !leaves.empty()) RP_HIP(hipStreamSynchronize(st));  // host vectors reused
+    }
+
+    // {live, min checksum, max checksum, some wanted member not at its wanted status}
     void conv_local(uint32_t* out4) {
         refresh_checksums();
+        if (conv_dirty) {
+            std::vector<uint32_t> w;
+            std::vector<uint8_t> skip(N);
+            for (uint32_t a = 0; a < N; a++) {
+                if (h_left[a]) w.push_back(a | ((uint32_t)ST_LEAVE << 24));
+                else if (h_dead[a]) w.push_back(a | ((uint32_t)ST_FAULTY << 24));
+                skip[a] = h_dead[a] | h_left[a];
+            }
+            nwant = (uint32_t)w.size();
+            want.reserve(nwant + 1);
+            cskip.reserve(N);
+            if (nwant) RP_HIP(hipMemcpyAsync(want.p, w.data(), 4ull * nwant, hipMemcpyHostToDevice, st));
+            RP_HIP(hipMemcpyAsync(cskip.p, skip.data(), N, hipMemcpyHostToDevice, st));
+            RP_HIP(hipStreamSynchronize(st));
+            conv_dirty = false;
+        }
         const uint32_t init[4] = {0u, 0xFFFFFFFFu, 0u, 0u};
         RP_HIP(hipMemcpyAsync(conv.p, init, sizeof init, hipMemcpyHostToDevice, st));
         if (NL)
-            hipLaunchKernelGGL(k_conv_local, dim3(grid_for((uint64_t)NL * std::max(nkilled, 1u), 256, 8192)), dim3(256),
-                               0, st, d, killed.p, nkilled, conv.p);
+            hipLaunchKernelGGL(k_conv_local, dim3(grid_for((uint64_t)NL * std::max(nwant, 1u), 256, 8192)), dim3(256),
+                               0, st, d, cskip.p, want.p, nwant, conv.p);
         RP_HIP(hipGetLastError());
         RP_HIP(hipMemcpyAsync(out4, conv.p, 16, hipMemcpyDeviceToHost, st));
         RP_HIP(hipStreamSynchronize(st));
@@ -2546,8 +2622,12 @@ static uint64_t env_u64(const char* name, uint64_t dflt) {
 
 static void sim_create(uint32_t n, const char* names, const uint32_t* off, const int64_t* inc0, const uint8_t* dead,
                        uint32_t seed, uint32_t suspicion_rounds, int64_t now0, int device, const uint32_t* bounds,
-                       uint32_t nshards, uint32_t shard, rp_sim** out) {
+                       uint32_t nshards, uint32_t shard, const rp_sim_event* events, uint32_t n_events,
+                       rp_sim** out) {
     RP_REQUIRE(out && n >= 2 && names && off && inc0 && dead, "sim_create: bad arguments");
+    RP_REQUIRE(n_events == 0 || events, "sim_create: events missing");
+    for (uint32_t i = 0; i < n_events; i++)
+        RP_REQUIRE(events[i].node < n && events[i].kind <= RP_SIM_LEAVE, "sim_create: bad event");
     RP_REQUIRE(n < (1u << 23), "sim_create: at most 2^23 members");
     RP_REQUIRE(nshards >= 1 && nshards <= rp::kMaxShards && shard < nshards, "sim_create: bad shard");
     std::vector<uint32_t> bnd(nshards + 1);
@@ -2609,20 +2689,30 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
         base.resize(((base.size() + 64 + 1023) & ~1023ull) + 32768, 0);
 
         const uint64_t NN = (uint64_t)NL * n;
-        std::vector<uint32_t> killed;
-        for (uint32_t i = 0; i < n; i++)
-            if (dead[i]) killed.push_back(i);
-        const uint32_t ndead = (uint32_t)killed.size();
-        S.nkilled = ndead;
-        // Capacities. In this model only killed members change state (only they are suspected;
-        // nobody refutes), so a node's changes and timers are bounded by the killed count.
+        // Capacities. Only the members the scenario touches ever change state in any view (a
+        // node is suspected only when it stops answering; only a suspected or leaving member's
+        // row moves, refutations included), so a node's changes and timers are bounded by them.
+        std::vector<uint8_t> touched(dead, dead + n);
+        uint32_t nrevive = 0;
+        for (uint32_t i = 0; i < n_events; i++) {
+            touched[events[i].node] = 1;
+            nrevive += events[i].kind == RP_SIM_REVIVE;
+        }
+        uint32_t ndead = 0;
+        for (uint32_t i = 0; i < n; i++) ndead += touched[i];
         const uint64_t cap = std::min<uint64_t>(n, env_u64("RP_SIM_CAP", 2ull * ndead + 256));
-        RP_REQUIRE(cap >= 1 && cap < 65535, "sim_create: RP_SIM_CAP must be in [1, 65534]");
+        RP_REQUIRE(cap >= 1 && cap <= 0xFFFFFFFEull, "sim_create: RP_SIM_CAP out of range");
+        S.events.assign(events, events + n_events);
+        std::stable_sort(S.events.begin(), S.events.end(),
+                         [](const rp_sim_event& a, const rp_sim_event& b) { return a.round < b.round; });
+        S.h_left.assign(n, 0);
         S.grid = std::max<uint32_t>(1, std::min<uint32_t>(NL, 256u * 4u));
         const uint32_t W = (n + 31) / 32;
         // arena: the round's responses (B and D2 answers of up to cap records, +25 % for shards
-        // receiving more than their share of pings), full syncs and slack
-        const uint64_t arena = env_u64("RP_SIM_ARENA", (NL + NL / 4 + 256) * cap + 8ull * n + 4096);
+        // receiving more than their share of pings), full syncs (a handful per round, more while
+        // revived nodes catch up) and slack
+        const uint64_t arena =
+            env_u64("RP_SIM_ARENA", (NL + NL / 4 + 256) * cap + (8ull + 2ull * nrevive) * n + 4096);
         const uint64_t L1 = NL ? NL : 1;
         S.st_.reserve(NN + 1); S.inc.reserve(NN + 1); S.order.reserve(NN + 1); S.slot.reserve(NN + 1);
         S.dev.reserve(L1 * W);
@@ -2635,7 +2725,7 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
         S.resp_idx.reserve(L1); S.lresp_idx.reserve(3 * L1);
         S.ib_off.reserve(L1 + 1);
         S.conv.reserve(4);
-        S.killed.reserve(ndead + 1);
+        S.stopped.reserve(L1);
         S.bounds.reserve(nshards + 1);
         S.pool.reserve(2 * L1 * cap + arena);
         S.cand.reserve((uint64_t)S.grid * n);
@@ -2656,7 +2746,6 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
         RP_HIP(hipMemcpyAsync(S.boff.p, boff.data(), 8ull * (n + 1), hipMemcpyHostToDevice, S.st));
         RP_HIP(hipMemcpyAsync(S.sbase.p, base.data(), base.size(), hipMemcpyHostToDevice, S.st));
         RP_HIP(hipMemcpyAsync(S.bounds.p, bnd.data(), 4ull * (nshards + 1), hipMemcpyHostToDevice, S.st));
-        if (ndead) RP_HIP(hipMemcpyAsync(S.killed.p, killed.data(), 4ull * ndead, hipMemcpyHostToDevice, S.st));
         S.h_dead.assign(dead, dead + n);
         RP_HIP(hipMemcpyAsync(S.dead.p, S.h_dead.data(), n, hipMemcpyHostToDevice, S.st));
         RP_HIP(hipMemsetAsync(S.stats.p, 0, 4 * sizeof(unsigned long long), S.st));
@@ -2669,7 +2758,7 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
         d.st = S.st_.p; d.inc = S.inc.p; d.order = S.order.p; d.slot = S.slot.p; d.dev = S.dev.p;
         d.chg = S.chg.p; d.n_chg = S.n_chg.p; d.tim = S.tim.p; d.n_tim = S.n_tim.p;
         d.it_idx = S.it_idx.p; d.n_shuf = S.n_shuf.p; d.ring_count = S.ring_count.p; d.max_piggy = S.max_piggy.p;
-        d.checksum = S.checksum.p; d.dirty = S.dirty.p; d.dead = S.dead.p;
+        d.checksum = S.checksum.p; d.dirty = S.dirty.p; d.dead = S.dead.p; d.stopped = S.stopped.p;
         d.sorted = S.nt.sorted.p; d.rank = S.rank.p; d.names = S.nt.d_bytes.p; d.noff = S.nt.d_noff.p;
         d.sbase = S.sbase.p; d.boff = S.boff.p; d.inc0 = S.inc0.p;
         d.target = S.target.p; d.ck_snap = S.ck_snap.p; d.inc_snap = S.inc_snap.p;
@@ -2685,7 +2774,7 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
                                   d.n_shuf, d.ring_count, d.max_piggy, d.checksum, d.dirty, d.dead, d.sorted,
                                   d.rank, d.names, d.noff, d.sbase, d.boff, d.inc0, d.target, d.ck_snap,
                                   d.inc_snap, d.pool, d.cursor, d.ping_n, d.leg_n, d.helpers, d.nhelp, d.leg_nk,
-                                  d.cand, d.strbuf, d.resp_idx, d.lresp_idx, d.stats, d.err, d.bounds};
+                                  d.cand, d.strbuf, d.resp_idx, d.lresp_idx, d.stats, d.err, d.bounds, d.stopped};
             for (const void* p : ptrs) RP_REQUIRE(p != nullptr, "sim_create: internal buffer not allocated");
         }
         hipLaunchKernelGGL(rp::k_sim_init, dim3(rp::grid_for(NN + 1, 256, 8192)), dim3(256), 0, S.st, d);
@@ -2709,14 +2798,35 @@ extern "C" {
 
 int rp_sim_create(uint32_t n, const char* names, const uint32_t* off, const int64_t* inc0, const uint8_t* dead,
                   uint32_t seed, uint32_t suspicion_rounds, int64_t now0, int device, rp_sim** out) {
-    return guard([&] { sim_create(n, names, off, inc0, dead, seed, suspicion_rounds, now0, device, nullptr, 1, 0, out); });
+    return guard([&] {
+        sim_create(n, names, off, inc0, dead, seed, suspicion_rounds, now0, device, nullptr, 1, 0, nullptr, 0, out);
+    });
 }
 
 int rp_sim_create_shard(uint32_t n, const char* names, const uint32_t* off, const int64_t* inc0, const uint8_t* dead,
                         uint32_t seed, uint32_t suspicion_rounds, int64_t now0, int device, const uint32_t* bounds,
                         uint32_t nshards, uint32_t shard, rp_sim** out) {
     return guard([&] {
-        sim_create(n, names, off, inc0, dead, seed, suspicion_rounds, now0, device, bounds, nshards, shard, out);
+        sim_create(n, names, off, inc0, dead, seed, suspicion_rounds, now0, device, bounds, nshards, shard, nullptr, 0,
+                   out);
+    });
+}
+
+int rp_sim_create_scenario(uint32_t n, const char* names, const uint32_t* off, const int64_t* inc0, const uint8_t* dead,
+                           uint32_t seed, uint32_t suspicion_rounds, int64_t now0, int device, const uint32_t* bounds,
+                           uint32_t nshards, uint32_t shard, const rp_sim_event* events, uint32_t n_events,
+                           rp_sim** out) {
+    return guard([&] {
+        sim_create(n, names, off, inc0, dead, seed, suspicion_rounds, now0, device, bounds, nshards, shard, events,
+                   n_events, out);
+    });
+}
+
+int rp_sim_piggyback(rp_sim* s, uint32_t* out) {
+    return guard([&] {
+        rp::Sim& S = SM(s);
+        if (S.NL) RP_HIP(hipMemcpyAsync(out, S.max_piggy.p, 4ull * S.NL, hipMemcpyDeviceToHost, S.st));
+        RP_HIP(hipStreamSynchronize(S.st));
     });
 }
 

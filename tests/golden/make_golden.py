@@ -270,6 +270,29 @@ def sim_cases():
                       "inc0": [int(x) for x in S.c3_members(n)[2]],
                       "dead": [int(x) for x in S.kill_set(n, k, seed)], "seed": seed, "suspRounds": susp,
                       "now0": S.NOW0, "rounds": rounds, "views": [0, n - 1]})
+    # Scenario cases: the branches the kill-only cases never take.
+    #  - n100k1-digits: the ring server count crosses a power of ten (100 -> 99), so
+    #    adjustMaxPiggybackCount (dissemination.js:38-55) re-values maxPiggybackCount 45 -> 30
+    #  - n40-leave: admin leave (server/admin/member.js:92-93 -> makeLeave) as the convergence
+    #    scenarios send it, plus a node that crashes mid-run (it had started gossiping)
+    #  - n64-half-leave: benchmarks/convergence-time/scenarios/half-cluster-failure.js (half the
+    #    hosts leave at once)
+    #  - n24-revive: a node down from round 0 comes back after every change about it expired:
+    #    it is answered with a full sync (dissemination.js:100-114) and refutes its own faulty
+    #    status (member.js:76-81); a second node is suspended briefly and refutes `suspect`
+    ev = lambda *e: [list(x) for x in e]  # noqa: E731
+    scen = [("n100k1-digits", 100, 1, 60, 25, 13, []),
+            ("n40-leave", 40, 1, 70, 6, 17, ev((2, "leave", 3), (5, "kill", 9), (10, "leave", 7), (11, "leave", 7),
+                                              (30, "leave", 20), (30, "kill", 21))),
+            ("n64-half-leave", 64, 0, 60, 25, 19, ev(*[(1, "leave", v) for v in range(0, 64, 2)])),
+            ("n24-revive", 24, 0, 110, 8, 23, ev((0, "kill", 4), (3, "kill", 6), (12, "revive", 6),
+                                                 (60, "revive", 4), (70, "kill", 11), (71, "leave", 12)))]
+    for name, n, k, rounds, susp, seed, events in scen:
+        cases.append({"name": name, "names": [S.c2_addr(i) for i in range(n)],
+                      "inc0": [int(x) for x in S.c3_members(n)[2]],
+                      "dead": [int(x) for x in S.kill_set(n, k, seed)] if k else [0] * n, "seed": seed,
+                      "suspRounds": susp, "now0": S.NOW0, "rounds": rounds, "views": [0, n - 1],
+                      "events": events})
     return cases
 
 
@@ -280,14 +303,20 @@ def make_sim():
                "reference": "lib/membership/*, lib/gossip/{dissemination,suspicion}.js, lib/membership/iterator.js, "
                             "lib/ring, lib/on_membership_event.js (ringpop v10.9.6) in the round model of "
                             "oracle/orc_sim.c",
-               "note": "rounds[r][v] = node v's membership checksum after round r (0 for killed nodes); "
-                       "finalViews = members arrays [address, status, inc] of the listed nodes",
+               "note": "checksums[r][v] = node v's membership checksum after round r (0 while v is down); "
+                       "maxPiggyback[r][v] = v's dissemination.maxPiggybackCount after round r; fullSyncs = "
+                       "full syncs the reference sent (its 'full-sync' stat); events [round, kind, node] run "
+                       "before that round; finalViews = members arrays [address, status, inc] of the listed "
+                       "nodes",
                "cases": []}
     for c, o in zip(cases, outs):
         f = {k: c[k] for k in ("name", "seed", "suspRounds", "now0", "rounds", "views")}
         f["n"] = len(c["names"])
         f["dead"] = c["dead"]
+        f["events"] = c.get("events", [])
         f["checksums"] = o["rounds"]
+        f["maxPiggyback"] = o["maxPiggyback"]
+        f["fullSyncs"] = o["fullSyncs"]
         f["finalViews"] = o["finalViews"]
         fixture["cases"].append(f)
     path = os.path.join(HERE, "sim_golden.json")

@@ -5,6 +5,12 @@
 //
 //   NODE_PATH=oracle/_ref/node_modules node tests/golden/ref_sim.js <ref_root> <in.json> <out.json>
 //
+// Scenario events (c.events = [[round, kind, node], ...], applied before that round's phase A):
+// 'kill' (the node stops: crash / SIGSTOP, scripts/tick-cluster.js:417-470), 'revive' (SIGCONT:
+// back with its state intact), 'leave' (the admin leave handler, server/admin/member.js:70-98:
+// makeLeave(whoami, localMember.incarnationNumber), as benchmarks/convergence-time/scenarios/
+// send it).
+//
 // Reference code doing the work per node: lib/membership (Membership, Member, merge),
 // lib/gossip/dissemination.js, lib/gossip/suspicion.js, lib/membership/iterator.js,
 // lib/ring (HashRing, only for maxPiggybackCount), lib/on_membership_event.js (wiring).
@@ -70,10 +76,11 @@ function FakeRingpop(whoami) {
         return {dampScoringEnabled: false, dampScoringDecayEnabled: false, dampScoringInitial: 0}[k];
     }};
     this.membershipUpdateRollup = {trackUpdates: function () {}};
+    this.fullSyncs = 0;
 }
 util.inherits(FakeRingpop, EventEmitter);
 FakeRingpop.prototype.whoami = function () { return this.hostPort; };
-FakeRingpop.prototype.stat = function () {};
+FakeRingpop.prototype.stat = function (type, key) { if (key === 'full-sync') { this.fullSyncs++; } };
 
 function digits(n) { var d = 0; while (n) { d++; n = Math.floor(n / 10); } return d; }
 function wire(x) { return JSON.parse(JSON.stringify(x)); }
@@ -92,6 +99,9 @@ input.cases.forEach(function (c) {
         rp.dissemination = new Dissemination(rp);
         rp.suspicion = new Suspicion({ringpop: rp, suspicionTimeout: 5000});
         rp.memberIterator = new MembershipIterator(rp);
+        // the protocol-period loop is the harness's phase A; a local leave stops it
+        // (LocalMemberLeaveEvent -> gossip.stop(), on_membership_event.js:32-40)
+        rp.gossip = {isStopped: false, stop: function () { this.isStopped = true; }};
         onMembershipEvent.register(rp);
         var m = rp.membership;
         var nsh = 0;
@@ -128,14 +138,27 @@ input.cases.forEach(function (c) {
         if (!dead[v]) { m.shuffle(); }  // gossip.start (gossip/index.js:97)
         return rp;
     });
-    function live(v) { return !dead[v]; }
-    var co = {name: c.name, rounds: []};
+    var down = dead.slice();
+    function live(v) { return !down[v]; }
+    var co = {name: c.name, rounds: [], maxPiggyback: []};
     for (round = 0; round < c.rounds; round++) {
+        (c.events || []).forEach(function (e) {
+            if (e[0] !== round) { return; }
+            var v = e[2];
+            if (e[1] === 'kill') { down[v] = 1; }
+            if (e[1] === 'revive') { down[v] = 0; }
+            if (e[1] === 'leave') {  // server/admin/member.js:76-93, while the node is up
+                var lm = nodes[v].membership.localMember;
+                if (live(v) && lm.status !== 'leave') {
+                    nodes[v].membership.makeLeave(c.names[v], lm.incarnationNumber);
+                }
+            }
+        });
         var target = [], ping = [], resp = [];
         // A
         for (var v = 0; v < N; v++) {
             target[v] = -1;
-            if (!live(v)) { continue; }
+            if (!live(v) || nodes[v].gossip.isStopped) { continue; }
             var t = nodes[v].memberIterator.next();
             if (!t) { continue; }
             target[v] = idOf[t.address];
@@ -215,7 +238,9 @@ input.cases.forEach(function (c) {
         var cks = [];
         for (v = 0; v < N; v++) { cks.push(live(v) ? nodes[v].membership.checksum : 0); }
         co.rounds.push(cks);
+        co.maxPiggyback.push(nodes.map(function (x) { return x.dissemination.maxPiggybackCount; }));
     }
+    co.fullSyncs = nodes.reduce(function (a, x) { return a + x.fullSyncs; }, 0);
     co.finalViews = (c.views || []).map(function (v) {
         return nodes[v].membership.members.map(function (x) { return [x.address, x.status, x.incarnationNumber]; });
     });

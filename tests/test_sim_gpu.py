@@ -22,21 +22,50 @@ def synth():
     return mod
 
 
-@pytest.mark.parametrize("case_name", ["n16k1", "n64k2", "n128k3-susp4", "n200k10"])
-def test_sim_matches_reference_goldens(gpu, case_name):
+CASES = [c["name"] for c in gu.load("sim_golden.json")["cases"]]
+
+
+def _golden_sim(gpu, case, G=None):
     S = synth()
-    case = next(c for c in gu.load("sim_golden.json")["cases"] if c["name"] == case_name)
     n = case["n"]
     names = [S.c2_addr(i) for i in range(n)]
-    sim = gpu.GossipSim(names, S.c3_members(n)[2], np.array(case["dead"], dtype=np.uint8), seed=case["seed"],
-                        suspicion_rounds=case["suspRounds"], now0=case["now0"])
+    args = (names, S.c3_members(n)[2], np.array(case["dead"], dtype=np.uint8))
+    kw = dict(seed=case["seed"], suspicion_rounds=case["suspRounds"], now0=case["now0"], events=case["events"])
+    return names, (gpu.ShardedGossipSim(*args, G, **kw) if G else gpu.GossipSim(*args, **kw))
+
+
+@pytest.mark.parametrize("case_name", CASES)
+def test_sim_matches_reference_goldens(gpu, case_name):
+    """Every node's checksum and maxPiggybackCount after every round, the full syncs sent and the
+    final member tables equal what the reference modules produced (tests/golden/ref_sim.js),
+    including the scenario cases: admin leaves, crashes mid-run, revivals answered with a full
+    sync that refute `faulty`, and a ring size crossing a power of ten (maxPiggyback 45 -> 30)."""
+    case = next(c for c in gu.load("sim_golden.json")["cases"] if c["name"] == case_name)
+    names, sim = _golden_sim(gpu, case)
     for r, want in enumerate(case["checksums"]):
         sim.step()
         assert sim.checksums().tolist() == want, "round %d" % r
+        assert sim.piggyback().tolist() == case["maxPiggyback"][r], "round %d" % r
+    assert sim.stats()["fullsyncs"] == case["fullSyncs"]
     for v, view in zip(case["views"], case["finalViews"]):
         st, inc = sim.view(v)
-        got = {names[i]: (int(st[i]), int(inc[i])) for i in range(n)}
+        got = {names[i]: (int(st[i]), int(inc[i])) for i in range(case["n"])}
         assert got == {a: (STAT[s], i) for a, s, i in view}
+    sim.close()
+
+
+@pytest.mark.parametrize("case_name", ["n40-leave", "n24-revive", "n64-half-leave"])
+def test_sharded_sim_matches_reference_goldens(gpu, case_name):
+    """The same scenario goldens through the sharded path (3 shard handles, message exchanges
+    between them): a leave runs on the shard that owns the node, down flags on every shard."""
+    case = next(c for c in gu.load("sim_golden.json")["cases"] if c["name"] == case_name)
+    _, sim = _golden_sim(gpu, case, G=3)
+    for r, want in enumerate(case["checksums"]):
+        sim.step()
+        assert sim.checksums().tolist() == want, "round %d" % r
+        assert sim.piggyback().tolist() == case["maxPiggyback"][r], "round %d" % r
+    assert sim.stats()["fullsyncs"] == case["fullSyncs"]
+    sim.close()
 
 
 @pytest.mark.parametrize("n,k,seed,susp", [(500, 5, 3, 25), (1000, 10, 11, 25), (777, 40, 9, 7)])
@@ -82,3 +111,36 @@ def test_sim_checksum_kernels_vs_oracle(gpu, orc, monkeypatch, kernel):
         g.step()
         o.step()
         assert np.array_equal(g.checksums(), o.checksums()), "round %d" % r
+
+
+def test_sim_dlist_overflow_falls_back_to_bitmap(gpu, orc, monkeypatch):
+    """RP_SIM_DLIST_BYTES small enough that every view's deviated-piece list overflows: the lane
+    checksums must take the bitmap-scan fallback and still match the oracle every round."""
+    monkeypatch.setenv("RP_SIM_DLIST_BYTES", str(16 * 600 * 4))  # 4 pieces per view
+    S = synth()
+    n, k, seed, susp = 600, 30, 4, 5
+    names = [S.c2_addr(i) for i in range(n)]
+    inc0 = S.c3_members(n)[2]
+    dead = S.kill_set(n, k, seed)
+    ev = [(3, "leave", 5), (20, "revive", int(np.flatnonzero(dead)[0]))]
+    g = gpu.GossipSim(names, inc0, dead, seed=seed, suspicion_rounds=susp, events=ev)
+    o = orc.Sim(names, inc0, dead, seed=seed, susp_rounds=susp, now0=1434401518824 + 10 ** 9, events=ev)
+    for r in range(40):
+        g.step()
+        o.step()
+        assert np.array_equal(g.checksums(), o.checksums()), "round %d" % r
+    assert g.stats() == o.stats()
+    g.close()
+
+
+def test_sim_capacity_overflow_is_loud(gpu, monkeypatch):
+    """A dissemination list past its capacity is reported, never silently truncated."""
+    monkeypatch.setenv("RP_SIM_CAP", "3")
+    S = synth()
+    n = 200
+    g = gpu.GossipSim([S.c2_addr(i) for i in range(n)], S.c3_members(n)[2], S.kill_set(n, 20, 3), seed=3,
+                      suspicion_rounds=3)
+    with pytest.raises(gpu.RingpopAmdError, match="capacity"):
+        for _ in range(30):
+            g.step()
+    g.close()
