@@ -4,26 +4,33 @@ Workload (BASELINE.json configs[1], "C2"): a 10k-server HashRing (100 replica po
 tokens, built on the device) answering batched lookupN(key, 3) for 36-byte UUID-format keys.
 One step = one device pass over one resident batch of 2^26 keys (default 15 steps ≈ 1.0B
 lookups). Keys are synthetic (Philox UUID stream) and generated into HBM before
-the timed region. With --gpus N (torchrun, one rank per GPU) every rank builds its own copy
-of the ring and processes its own key stream: no data-path collective ("scaling": "weak").
+the timed region. With --gpus N every rank (one process per GPU) builds its own copy of the
+ring and processes its own key stream: no data-path collective ("scaling": "weak").
+
+Launch: `torchrun --nproc-per-node N bench.py --gpus N` (RANK / LOCAL_RANK / WORLD_SIZE from the
+environment), or `python bench.py --gpus N`, which starts the N rank processes itself before
+anything touches the GPU.
 
 Printed (rank 0, one JSON line): value = lookupN(3)/s over all ranks, the dominant kernel's
 roofline (48 algorithmic bytes per lookupN(3): 36 B key read + 12 B owner write),
-and the CPU oracle timed on this host as cpu_baseline.
+the CPU oracle timed on this host as cpu_baseline, and the other configs' legs: C3 merge
+(+ fold roofline, CPU baselines), C4 and C5 gossip simulations (+ traffic, per-round spread,
+CPU baselines), the wire codec.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 import numpy as np
-import torch
-import torch.distributed as dist
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 BYTES_PER_LOOKUPN3 = 48  # 36 B key + 3 x 4 B owners
+BYTES_PER_UPDATE = 49  # 16 B change + 16 B row read + 16 B row write + 1 B flag (SURVEY §8d)
 METRIC = "ring lookups/s + member-updates merged/s; SWIM round time @100k members"
 
 
@@ -36,18 +43,66 @@ def load_pkg():
     return mod
 
 
+def _synth():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("rp_synth", os.path.join(REPO, "ringpop-node_amd", "synth.py"))
+    S = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(S)
+    return S
+
+
+def _oracle():
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle
+    return pyoracle
+
+
 def c2_addr(i):
     return "10.%d.%d.%d:%d" % ((i >> 16) & 255, (i >> 8) & 255, i & 255, 20800 + i % 36)
 
 
+def host_cores():
+    """Host threads this job may use: the box's CPU share (OMP_NUM_THREADS, 16 per GPU on the
+    pool) or the affinity mask."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(aff, int(omp))) if omp and omp.isdigit() else aff
+
+
+def host_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count(), "threads_used": host_cores()}
+
+
+def pct(xs, q):
+    return float(np.percentile(np.asarray(xs, dtype=np.float64), q)) if len(xs) else None
+
+
+# ------------------------------------------------------------------ CPU baselines (oracle)
+
 def cpu_baseline(servers, nkeys, threads, min_seconds=10.0):
     """The oracle (C restatement of lib/ring/index.js) on this host's cores: a bounded sample of
-    the same workload (nkeys UUID keys, lookupN(key, 3)), repeated until >= min_seconds of wall."""
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import pyoracle
+    the same workload (nkeys UUID keys, lookupN(key, 3)), repeated until >= min_seconds of wall;
+    also one pass on one thread."""
+    pyoracle = _oracle()
     ring = pyoracle.Ring(100)
     ring.add_remove(servers)
     keys = pyoracle.uuid_keys(42, 0, nkeys)
+    n1 = max(1, nkeys // 16)
+    t0 = time.perf_counter()
+    ring.lookupn_keys(keys[:n1], 3, threads=1)
+    one = n1 / (time.perf_counter() - t0)
     done, t0 = 0, time.perf_counter()
     while True:
         ring.lookupn_keys(keys, 3, threads=threads)
@@ -56,14 +111,85 @@ def cpu_baseline(servers, nkeys, threads, min_seconds=10.0):
         if dt >= min_seconds:
             break
     return {"value": done / dt, "unit": "lookupN(3)/s", "cores": threads, "kind": "port",
+            "value_1thread": one,
             "sample": "%d lookupN(key,3) (%d UUID keys x %d passes) on the same 10k-server ring, "
-                      "oracle/orc_ring.c (farmhash32 + binary search + walk), %d pthreads, %.1f s"
-                      % (done, nkeys, done // nkeys, threads, dt)}
+                      "oracle/orc_ring.c (farmhash32 + binary search + walk), %d pthreads, %.1f s; 1 thread: %d keys"
+                      % (done, nkeys, done // nkeys, threads, dt, n1)}
 
 
-def merge_bench(rpa, local, n=100_000, k=100_000, batches=20, warmup=3):
+def merge_cpu_baseline(n, k, threads):
+    """C3 on the host: the oracle's Membership.update (oracle/orc_members.c: sequential fold +
+    one checksum per batch, as lib/membership/index.js:249-324 runs) on one thread, and the fold
+    sharded by id over `threads` threads (checksum still one serial hash)."""
+    pyoracle = _oracle()
+    S = _synth()
+    names, st0, inc0 = S.c3_members(n)
+    m = pyoracle.Members(names, local=names[0])
+    m.set_ready(True)
+    m.update_ids(np.arange(n, dtype=np.uint32), st0, inc0, now_ms=1)
+    # every batch is fresh against the table (incarnations move forward 3 per batch), so every
+    # batch applies most of its updates and pays the checksum, as the reference's benchmark does
+    nb = 96
+    batches = [S.c3_updates(n, k, seed=100 + b, base_inc=inc0 + 3 * b) for b in range(2 * nb)]
+    L = pyoracle.lib()
+    import ctypes
+    L.orc_members_update_mt.restype = ctypes.c_uint32
+    L.orc_members_update_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_uint32, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]
+    res = {}
+    for label, T, b0 in (("1thread", 1, 0), ("all", threads, nb)):
+        done, t0, b = 0, time.perf_counter(), b0
+        while time.perf_counter() - t0 < 4.0 and b < b0 + nb:
+            ids, us, ui = batches[b]
+            if T == 1:
+                m.update_ids(ids, us, ui, now_ms=1434500000000 + b)
+            else:
+                L.orc_members_update_mt(m.h, ids.ctypes.data, us.ctypes.data, ui.ctypes.data, k,
+                                        1434500000000 + b, T, None)
+            done += k
+            b += 1
+        dt = time.perf_counter() - t0
+        res[label] = (done / dt, b - b0, dt)
+    return {"value": res["all"][0], "unit": "updates/s", "cores": threads, "kind": "port",
+            "value_1thread": res["1thread"][0],
+            "sample": "C3 batches of %d updates over %d members incl. one checksum per batch: %d batches on 1 "
+                      "thread (oracle/orc_members.c sequential fold) in %.1f s; %d batches with the fold sharded "
+                      "by id over %d threads in %.1f s" % (k, n, res["1thread"][1], res["1thread"][2],
+                                                            res["all"][1], threads, res["all"][2])}
+
+
+def sim_cpu_baseline(n, kill_pct=1, seed=11, min_seconds=15.0, max_rounds=60, threads=1):
+    """The simulator on this host: the oracle (oracle/orc_sim.c; the reference runs one view per
+    process, this restatement runs every view) for as many rounds as fit in ~min_seconds."""
+    pyoracle = _oracle()
+    S = _synth()
+    k = max(1, n * kill_pct // 100)
+    names = [S.c2_addr(i) for i in range(n)]
+    t0 = time.perf_counter()
+    sim = pyoracle.Sim(names, S.c3_members(n)[2], S.kill_set(n, k, seed), seed=seed, susp_rounds=25,
+                       now0=1434401518824 + 10 ** 9, threads=threads)
+    create_s = time.perf_counter() - t0
+    rounds, t0 = 0, time.perf_counter()
+    while rounds < max_rounds:
+        sim.step()
+        rounds += 1
+        if time.perf_counter() - t0 >= min_seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": dt * 1e3 / rounds, "unit": "ms/round", "cores": threads, "kind": "port",
+            "create_s": create_s,
+            "sample": "%d members, %d down: the first %d rounds of oracle/orc_sim.c on %d threads, %.1f s (+%.1f s "
+                      "to create the views); early rounds are cheaper than the dissemination peak"
+                      % (n, k, rounds, threads, dt, create_s)}
+
+
+# ------------------------------------------------------------------ device legs
+
+def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=20, warmup=3):
     """C3 (BASELINE.json configs[2]): 100k-member table, batches of 100k updates (1% repeated
-    addresses), Membership.update fold + one checksum per batch, inputs resident in HBM."""
+    addresses), Membership.update fold + one checksum per batch, inputs resident in HBM. Also:
+    the fold alone (checksum deferred) against the HBM roofline at 49 B/update, the checksum
+    chain alone, and the fold at a batch large enough not to be launch-bound."""
     S = _synth()
     names, st0, inc0 = S.c3_members(n)
     m = rpa.Membership(whoami=names[0], capacity=n, device=local)
@@ -71,9 +197,11 @@ def merge_bench(rpa, local, n=100_000, k=100_000, batches=20, warmup=3):
     m.update_ids(ids0, st0, inc0, now_ms=1)
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
+    # fresh batches (incarnations +3 per batch: most updates apply, every batch pays the
+    # checksum), all resident in HBM before the timed region
     bufs = []
-    for b in range(4):
-        ids, us, ui = S.c3_updates(n, k, seed=100 + b, base_inc=inc0)
+    for b in range(warmup + 2 * batches):
+        ids, us, ui = S.c3_updates(n, k, seed=100 + b, base_inc=inc0 + 3 * b)
         bufs.append((torch.from_numpy(ids.view(np.int32)).cuda(), torch.from_numpy(us).cuda(),
                      torch.from_numpy(ui).cuda()))
     app = torch.empty(k, dtype=torch.uint8, device="cuda")
@@ -81,10 +209,10 @@ def merge_bench(rpa, local, n=100_000, k=100_000, batches=20, warmup=3):
     ninc = torch.empty(k, dtype=torch.int64, device="cuda")
     na = torch.zeros(1, dtype=torch.int32, device="cuda")
 
-    def one(b):
-        d = bufs[b % 4]
-        m.update_dev(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), k, 1434500000000 + b, app.data_ptr(),
-                     nst.data_ptr(), ninc.data_ptr(), na.data_ptr(), sp)
+    def one(b, mm=m, bb=bufs, kk=k):
+        d = bb[b % len(bb)]
+        mm.update_dev(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), kk, 1434500000000 + b, app.data_ptr(),
+                      nst.data_ptr(), ninc.data_ptr(), na.data_ptr(), sp)
 
     for b in range(warmup):
         one(b)
@@ -97,28 +225,77 @@ def merge_bench(rpa, local, n=100_000, k=100_000, batches=20, warmup=3):
     e1.record(stream)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    return {"workload": "C3: %d-member table, %d updates/batch (1%% repeated addresses), fold + 1 checksum "
-                        "per batch" % (n, k),
-            "updates_per_s": k * batches / dt, "ms_per_batch": dt * 1e3 / batches,
-            "gpu_ms_per_batch": e0.elapsed_time(e1) / batches, "checksum": m.checksum}
+    out = {"workload": "C3: %d-member table, %d updates/batch (1%% repeated addresses), fold + 1 checksum "
+                       "per batch" % (n, k),
+           "updates_per_s": k * batches / dt, "ms_per_batch": dt * 1e3 / batches,
+           "gpu_ms_per_batch": e0.elapsed_time(e1) / batches, "checksum": m.checksum}
+    # the fold alone (sort + k_fold), HIP events per batch on the launch stream
+    rpa.check(rpa.lib().rp_members_defer_checksum(m._h, 1))
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(batches)]
+    for b in range(batches):
+        evs[b][0].record(stream)
+        one(warmup + batches + b)
+        evs[b][1].record(stream)
+    torch.cuda.synchronize()
+    fold_ms = float(np.mean([a.elapsed_time(c) for a, c in evs]))
+    rpa.check(rpa.lib().rp_members_defer_checksum(m._h, 0))
+    # the checksum chain alone (string build + one farmhash over ~3.6 MB)
+    t0 = time.perf_counter()
+    for _ in range(5):
+        m.compute_checksum()
+    ck_ms = (time.perf_counter() - t0) * 1e3 / 5
+    slen = len(m.generate_checksum_string())
+    ach = BYTES_PER_UPDATE * k / (fold_ms * 1e-3) / 1e9
+    out["fold"] = {"ms_per_batch": fold_ms, "bytes_per_update": BYTES_PER_UPDATE,
+                   "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": ach / HBM_PEAK_GBS,
+                                "note": "k_sort_init + radix sort + k_fold per 100k-update batch (HIP events); "
+                                        "launch-bound at this batch size"}}
+    out["checksum_chain"] = {"ms": ck_ms, "string_bytes": slen, "GBps": slen / (ck_ms * 1e-3) / 1e9,
+                             "note": "one serial farmhash chain (not rooflined, SURVEY §8d)"}
+    m.close()
+    # a batch large enough that the fold is not launch-bound: 2^22 members, 2^22 updates
+    nb = 1 << 22
+    names_b = [c2_addr(i) for i in range(nb)]
+    mb = rpa.Membership(whoami=names_b[0], capacity=nb, device=local)
+    idb = np.asarray(mb.intern(names_b), dtype=np.uint32)
+    incb = S.c3_members(nb)[2]
+    mb.update_ids(idb, np.zeros(nb, np.uint8), incb, now_ms=1)
+    rpa.check(rpa.lib().rp_members_defer_checksum(mb._h, 1))
+    big = [tuple(torch.from_numpy(x).cuda() for x in (a.view(np.int32), s_, i_))
+           for a, s_, i_ in [S.c3_updates(nb, nb, seed=300 + b, base_inc=incb + 3 * b) for b in range(7)]]
+    app = torch.empty(nb, dtype=torch.uint8, device="cuda")
+    nst = torch.empty(nb, dtype=torch.uint8, device="cuda")
+    ninc = torch.empty(nb, dtype=torch.int64, device="cuda")
+    one(0, mb, big, nb)
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(6)]
+    for b in range(6):
+        evs[b][0].record(stream)
+        one(b + 1, mb, big, nb)
+        evs[b][1].record(stream)
+    torch.cuda.synchronize()
+    big_ms = float(np.mean([a.elapsed_time(c) for a, c in evs]))
+    achb = BYTES_PER_UPDATE * nb / (big_ms * 1e-3) / 1e9
+    out["fold_large"] = {"members": nb, "updates_per_batch": nb, "ms_per_batch": big_ms,
+                         "updates_per_s": nb / (big_ms * 1e-3),
+                         "roofline": {"bound": "hbm", "achieved": achb, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                      "frac": achb / HBM_PEAK_GBS}}
+    mb.close()
+    del big, app, nst, ninc
+    torch.cuda.empty_cache()
+    return out
 
 
-def _synth():
-    import importlib.util
-    spec = importlib.util.spec_from_file_location("rp_synth", os.path.join(REPO, "ringpop-node_amd", "synth.py"))
-    S = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(S)
-    return S
-
-
-def sim_bench(rpa, local, n=10_000, kill_pct=1, seed=11, max_rounds=300, max_seconds=240.0, world=1):
+def sim_bench(rpa, torch, dist, local, n=10_000, kill_pct=1, seed=11, max_rounds=300, max_seconds=240.0, world=1,
+              reduce_max=None):
     """C4 (BASELINE.json configs[3]) and C5 (configs[4]): n ringpop nodes with full views,
-    kill_pct% killed before round 0, gossip rounds until convergence
-    (scenario-runner.js:152-170 + every killed member faulty everywhere). One GPU: one
-    simulator handle. world > 1 (torchrun): the nodes are sharded by id range over the ranks and
-    each round's four message exchanges are RCCL all-to-all-v (DistGossipSim); the timed region
-    is bracketed by barriers and the max over ranks is reported. Reports rounds-to-convergence,
-    wall time per round, exchange bytes."""
+    kill_pct% down from the start, gossip rounds until convergence
+    (scenario-runner.js:152-170 + every down member faulty everywhere). One GPU: one simulator
+    handle. world > 1: the nodes are sharded by id range over the ranks and each round's four
+    message exchanges are RCCL all-to-all-v (DistGossipSim); the timed region is bracketed by
+    barriers and the max over ranks is reported. Reports rounds-to-convergence, wall time per
+    round (mean, p50, p95, max and the worst round), exchange bytes and the traffic of §8d."""
     S = _synth()
     k = max(1, n * kill_pct // 100)
     names = [S.c2_addr(i) for i in range(n)]
@@ -150,53 +327,42 @@ def sim_bench(rpa, local, n=10_000, kill_pct=1, seed=11, max_rounds=300, max_sec
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    t = torch.tensor([dt, create_s, max(per_round) if per_round else 0.0], dtype=torch.float64, device="cuda")
+    pr = np.asarray(per_round if per_round else [0.0])
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt, create_s, mx = (float(x) for x in t)
+        pr = np.asarray(reduce_max(list(pr)))  # round r's time = the slowest rank's
+    dt, create_s = reduce_max([dt, create_s]) if world > 1 else (dt, create_s)
     st = sim.stats()
-    out = {"workload": "%s: %d members, full views, %d killed (%d%%), suspicion 25 rounds%s"
+    cnt = sim.counters()
+    msg_bytes = 40 * cnt["messages"] + 24 * cnt["records"] + BYTES_PER_UPDATE * cnt["applied"]
+    hashed = cnt["views_hashed"] * cnt["base_len"]
+    out = {"workload": "%s: %d members, full views, %d down (%d%%), suspicion 25 rounds%s"
                        % ("C5" if n >= 100_000 else "C4", n, k, kill_pct,
                           ", nodes sharded over %d GPUs (RCCL all-to-all-v message exchange)" % world
                           if world > 1 else ", one GPU"),
            "n_gpus": world, "converged": conv, "rounds_to_convergence": rounds if conv else None,
-           "rounds_run": rounds, "ms_per_round": dt * 1e3 / max(rounds, 1), "max_round_ms": mx * 1e3,
-           "create_s": create_s, "stats": st}
+           "rounds_run": rounds, "ms_per_round": dt * 1e3 / max(rounds, 1),
+           "round_ms": {"p50": pct(pr * 1e3, 50), "p95": pct(pr * 1e3, 95), "max": float(pr.max() * 1e3),
+                        "worst_round": int(pr.argmax())},
+           "create_s": create_s, "stats": st,
+           "traffic": {"messages": cnt["messages"], "records": cnt["records"], "applied": cnt["applied"],
+                       "message_and_merge_bytes": msg_bytes,
+                       "message_and_merge_GBps": msg_bytes / dt / 1e9,
+                       "views_hashed": cnt["views_hashed"], "checksum_bytes_hashed": hashed,
+                       "checksum_GBps": hashed / dt / 1e9,
+                       "note": "bytes per SURVEY §8d: 40 B per message header + 24 B per change record sent + "
+                               "49 B per applied update; checksum bytes = views re-hashed x the %d-byte "
+                               "checksum string (serial chains: throughput, not a roofline)" % cnt["base_len"]}}
     if world > 1:
         out["exchange_bytes_per_round_rank0"] = sim.exchange_bytes / max(rounds, 1)
     sim.close()
     return out
 
 
-def sim_cpu_baseline(n=10_000, kill_pct=1, seed=11, min_seconds=10.0, max_rounds=40):
-    """The C4 simulator on this host: the oracle (oracle/orc_sim.c, one thread: the reference
-    runs one view per process, this restatement runs every view sequentially) for as many rounds
-    as fit in ~min_seconds. Reported as ms per round next to the device's."""
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import pyoracle
-    S = _synth()
-    k = max(1, n * kill_pct // 100)
-    names = [S.c2_addr(i) for i in range(n)]
-    sim = pyoracle.Sim(names, S.c3_members(n)[2], S.kill_set(n, k, seed), seed=seed, susp_rounds=25,
-                       now0=1434401518824 + 10 ** 9)
-    rounds, t0 = 0, time.perf_counter()
-    while rounds < max_rounds:
-        sim.step()
-        rounds += 1
-        if time.perf_counter() - t0 >= min_seconds:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": dt * 1e3 / rounds, "unit": "ms/round", "cores": 1, "kind": "port",
-            "sample": "C4 (%d members, %d killed): the first %d rounds of oracle/orc_sim.c, one thread, %.1f s"
-                      % (n, k, rounds, dt)}
-
-
-def wire_bench(rpa, dev, n_msgs=100_000, recs=32, reps=5):
+def wire_bench(rpa, torch, dev, n_msgs=100_000, recs=32, reps=5):
     """Gossip wire bodies (rp_wire_*): n_msgs ping request bodies (ping-sender.js:71-76), each
     carrying `recs` issueAs change records (dissemination.js:163-170) over the C5 address set,
     encoded to JSON and decoded back on the device. Reported as records/s and JSON GB/s (the
     bytes written by the encoder / read by the decoder; both are bounded by HBM)."""
-    import ctypes
     S = _synth()
     n = 100_000
     m = rpa.Membership(device=dev)
@@ -212,11 +378,12 @@ def wire_bench(rpa, dev, n_msgs=100_000, recs=32, reps=5):
     ids = ri(16, k * 36, torch.uint8) + ord("a")
     ck, msrc = ri(2 ** 31, n_msgs, torch.int32), ri(n, n_msgs, torch.int32)
     msinc = ri(10 ** 7, n_msgs, torch.int64) + 1434401500000
-    out_off = torch.zeros(n_msgs + 1, dtype=torch.int64, device="cuda")
+    out_off = torch.empty(n_msgs + 1, dtype=torch.int64, device="cuda")
     L = rpa.lib()
+    sp = torch.cuda.current_stream().cuda_stream
     args = [m._h, n_msgs, rec_off.data_ptr(), k, addr.data_ptr(), src.data_ptr(), st.data_ptr(), inc.data_ptr(),
             sinc.data_ptr(), ids.data_ptr(), 0, 1, ck.data_ptr(), msrc.data_ptr(), msinc.data_ptr()]
-    rpa.check(L.rp_wire_encode_changes_dev(*args, None, out_off.data_ptr(), None))
+    rpa.check(L.rp_wire_encode_changes_dev(*args, None, out_off.data_ptr(), sp))
     total = int(out_off[-1].item())
     out = torch.empty(total, dtype=torch.uint8, device="cuda")
     rec_off2 = torch.empty(n_msgs + 1, dtype=torch.int32, device="cuda")
@@ -225,12 +392,12 @@ def wire_bench(rpa, dev, n_msgs=100_000, recs=32, reps=5):
     err = torch.empty(n_msgs, dtype=torch.int64, device="cuda")
 
     def enc():
-        rpa.check(L.rp_wire_encode_changes_dev(*args, out.data_ptr(), out_off.data_ptr(), None))
+        rpa.check(L.rp_wire_encode_changes_dev(*args, out.data_ptr(), out_off.data_ptr(), sp))
 
     def dec():
         rpa.check(L.rp_wire_decode_changes_dev(m._h, out.data_ptr(), out_off.data_ptr(), n_msgs, rec_off2.data_ptr(),
                                                k, *[c.data_ptr() for c in cols], None, None, None, err.data_ptr(),
-                                               None, None, None, None))
+                                               None, None, None, sp))
         torch.cuda.synchronize()
 
     res = {}
@@ -240,6 +407,7 @@ def wire_bench(rpa, dev, n_msgs=100_000, recs=32, reps=5):
         t0 = time.perf_counter()
         for _ in range(reps):
             fn()
+        torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / reps
         res[name] = {"ms": dt * 1e3, "records_per_s": k / dt, "json_GBps": total / dt / 1e9}
     ok = bool((err == 0).all().item()) and bool(torch.equal(cols[0], addr)) and bool(torch.equal(cols[3], inc))
@@ -251,10 +419,43 @@ def wire_bench(rpa, dev, n_msgs=100_000, recs=32, reps=5):
 def pmc_traffic():
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
-        return None
+        return None, None
     with open(p) as f:
         d = json.load(f)
-    return d.get("lookupn_hbm_bytes_per_launch")
+    return d.get("lookupn_hbm_bytes_per_launch"), d.get("measured_on")
+
+
+# ------------------------------------------------------------------ launcher
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n):
+    """`python bench.py --gpus N` without torchrun: start N fresh rank processes (one per GPU)
+    before this process touches the GPU, wait, exit with the worst status."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    try:
+        for p in procs:
+            rc = max(rc, p.wait())
+            if rc:
+                break
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
 
 
 def main():
@@ -272,14 +473,34 @@ def main():
     ap.add_argument("--no-wire", action="store_true")
     ap.add_argument("--sim-n", type=int, default=10000, help="C4 members, one GPU (0: skip)")
     ap.add_argument("--sim5-n", type=int, default=100000, help="C5 members, sharded over all ranks (0: skip)")
+    ap.add_argument("--sim5-cpu", type=int, default=1, help="time the C5 oracle sample (rank 0, N=1)")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+
+    import torch
+    import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    assert world == args.gpus, "WORLD_SIZE=%d but --gpus %d" % (world, args.gpus)
+    ndev = torch.cuda.device_count()
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, ndev)
     torch.cuda.set_device(local)
+    backend = os.environ.get("RP_BENCH_BACKEND", "nccl")  # gloo: ranks sharing one GPU (tests)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+
+    def reduce_max(vals):
+        t = torch.tensor(vals, dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return [float(x) for x in t.cpu()]
+
     rpa = load_pkg()
 
     servers = [c2_addr(i) for i in range(args.servers)]
@@ -318,18 +539,16 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms = float(t[0]), float(t[1])
+    elapsed, kern_ms = reduce_max([elapsed, kern_ms])
 
     total = B * args.steps * world
     del keys, owners
     torch.cuda.empty_cache()
-    sim5 = sim_bench(rpa, local, n=args.sim5_n, world=world) if args.sim5_n else None
+    sim5 = sim_bench(rpa, torch, dist, local, n=args.sim5_n, world=world, reduce_max=reduce_max) \
+        if args.sim5_n else None
     if rank == 0:
         achieved = BYTES_PER_LOOKUPN3 * B / (kern_ms * 1e-3) / 1e9
-        traffic = pmc_traffic()
+        traffic, traffic_src = pmc_traffic()
         out = {
             "metric": METRIC,
             "value": total / elapsed,
@@ -348,27 +567,33 @@ def main():
                        "servers": args.servers, "replica_points": 100, "tokens": ring.size,
                        "keys_per_step": B, "total_keys": total, "parallelism": "keys sharded, ring replicated"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_measured_on": traffic_src,
                          "kernel": "k_lookupn_compact<4,3> (+ k_lookupn_fix_tiles for deferred keys)",
                          "kernel_ms": kern_ms,
                          "bytes_per_unit": BYTES_PER_LOOKUPN3},
             "ring_build_ms": build_ms,
+            "host": host_info(),
         }
+        th = args.cpu_threads or host_cores()
         if not args.no_merge:
-            out["merge"] = merge_bench(rpa, local)
+            out["merge"] = merge_bench(rpa, torch, local)
+            if not args.no_cpu and world == 1:
+                out["merge"]["cpu_baseline"] = merge_cpu_baseline(100_000, 100_000, th)
         if args.sim_n and world == 1:
-            out["sim"] = sim_bench(rpa, local, n=args.sim_n)
+            out["sim"] = sim_bench(rpa, torch, dist, local, n=args.sim_n)
         if sim5:
             out["sim_c5"] = sim5
         if not args.no_wire:
-            out["wire"] = wire_bench(rpa, local)
-        if not args.no_cpu:
-            th = args.cpu_threads or min(16, os.cpu_count() or 1)
+            out["wire"] = wire_bench(rpa, torch, local)
+        if not args.no_cpu and world == 1:
             out["cpu_baseline"] = cpu_baseline(servers, args.cpu_keys, th)
             if args.sim_n and "sim" in out:
-                out["sim"]["cpu_baseline"] = sim_cpu_baseline(args.sim_n)
+                out["sim"]["cpu_baseline"] = sim_cpu_baseline(args.sim_n, threads=th)
+            if sim5 and args.sim5_cpu:
+                out["sim_c5"]["cpu_baseline"] = sim_cpu_baseline(args.sim5_n, threads=th, min_seconds=20.0)
         print(json.dumps(out), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -169,6 +169,10 @@ int rp_members_set_dev(rp_members *m, const uint32_t *d_ids, const uint8_t *d_st
 int rp_members_checksum(rp_members *m, uint32_t *out, int *is_set);
 /* computeChecksum() unconditionally. */
 int rp_members_compute_checksum(rp_members *m);
+/* defer != 0: update no longer recomputes the checksum after each batch (the reference does,
+ * index.js:306-309); a caller folding many batches calls rp_members_compute_checksum once at the
+ * end. Default off. */
+int rp_members_defer_checksum(rp_members *m, int defer);
 /* generateChecksumString() (writes up to cap bytes; *len = full length). */
 int rp_members_checksum_string(rp_members *m, char *buf, uint64_t cap, uint64_t *len);
 /* Member table by id (exists/status/incarnation), cap entries. */
@@ -249,10 +253,12 @@ int rp_sim_stats(rp_sim *s, uint64_t *out4);
  * partition of [0, n) into nshards contiguous ranges (bounds NULL = equal ranges); its views
  * still cover all n members. A round is five stages (rp_sim_stage 0..4) separated by four
  * message exchanges: after stage k < 4 the outbox holds this shard's messages grouped by
- * destination shard (rp_sim_outbox: per-destination message / record counts and the device
- * buffers, 40-byte headers and 24-byte records); before stage k + 1 the caller fills the inbox
- * with every source's messages for this shard, concatenated in source-shard order
- * (rp_sim_inbox sizes it and returns the device buffers). rp_sim_exchange_local does the
+ * destination shard (rp_sim_outbox: per-destination message / record counts and ONE device
+ * buffer holding, for each destination in shard order, a segment of its 40-byte headers then
+ * its 24-byte records); before stage k + 1 the caller fills the inbox (rp_sim_inbox sizes it for
+ * the per-source counts and returns its device buffer) with every source's segment for this
+ * shard, in source-shard order — one all-to-all-v moves the bytes as they lie. The buffers are
+ * owned by the handle and valid until its next stage. rp_sim_exchange_local does the
  * exchange for handles of one process; across processes the host moves the bytes (RCCL
  * all-to-all-v; ringpop-node_amd DistGossipSim). Checksums / views / stats are per shard
  * (checksums: the shard's nodes in id order); convergence reduces rp_sim_converged_local
@@ -262,8 +268,8 @@ int rp_sim_create_shard(uint32_t n, const char *names, const uint32_t *off, cons
                         uint32_t nshards, uint32_t shard, rp_sim **out);
 int rp_sim_shard_info(rp_sim *s, uint32_t *v0, uint32_t *nl, uint32_t *nshards, uint32_t *shard);
 int rp_sim_stage(rp_sim *s, int stage);
-int rp_sim_outbox(rp_sim *s, uint64_t *nmsg, uint64_t *nrec, void **msg, void **rec);
-int rp_sim_inbox(rp_sim *s, const uint64_t *nmsg, const uint64_t *nrec, void **msg, void **rec);
+int rp_sim_outbox(rp_sim *s, uint64_t *nmsg, uint64_t *nrec, void **buf);
+int rp_sim_inbox(rp_sim *s, const uint64_t *nmsg, const uint64_t *nrec, void **buf);
 int rp_sim_exchange_local(rp_sim *const *shards, uint32_t nshards);
 int rp_sim_converged_local(rp_sim *s, uint32_t *out4);
 
@@ -289,6 +295,10 @@ int rp_sim_create_scenario(uint32_t n, const char *names, const uint32_t *off, c
                            uint32_t n_events, rp_sim **out);
 /* Every local node's dissemination.maxPiggybackCount (dissemination.js:38-55), [shard nodes]. */
 int rp_sim_piggyback(rp_sim *s, uint32_t *out);
+/* Traffic since creation: {pings, ping-reqs, full syncs, applied updates, messages sent, change
+ * records sent, views hashed, bytes of the all-alive checksum string (a view's string length
+ * within a few bytes per deviated member)}. */
+int rp_sim_counters(rp_sim *s, uint64_t *out8);
 
 /* Stream-ordered copy between any host / device buffers (hipMemcpyDefault); NULL stream =
  * synchronous. Used by hosts that move sharded-simulator messages. */

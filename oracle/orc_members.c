@@ -11,6 +11,7 @@
  * Members are identified by interned address ids 0..n_names-1 (names given up front).
  */
 #include <stdio.h>
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -199,6 +200,67 @@ uint32_t orc_members_update(orc_members *m, const uint32_t *ids, const uint8_t *
         if (new_inc_out) new_inc_out[i] = in;
     }
     if (napplied) compute_checksum(m); /* (306-309) */
+    return napplied;
+}
+
+/* The same fold on T threads for a batch that creates no member (the C3 CPU baseline on all
+ * host cores): the fold is order-sensitive only within one address, so thread t folds, in
+ * arrival order, the changes whose id % T == t; the checksum is then computed once (serial). */
+typedef struct {
+    orc_members *m;
+    const uint32_t *ids;
+    const uint8_t *status;
+    const int64_t *inc;
+    uint32_t k, t, T;
+    int64_t now_ms;
+    uint8_t *applied;
+    uint32_t napplied;
+} fold_job;
+
+static void *fold_worker(void *p) {
+    fold_job *j = (fold_job *)p;
+    orc_members *m = j->m;
+    for (uint32_t i = 0; i < j->k; i++) {
+        uint32_t id = j->ids[i];
+        if (id % j->T != j->t) continue;
+        uint8_t st = j->status[i];
+        int64_t in = j->inc[i];
+        int applied = 0;
+        if (id == m->local_id && (st == 1 || st == 2)) {
+            st = 0;
+            in = j->now_ms;
+            applied = 1;
+        } else if (other_override(m->status[id], m->inc[id], st, in)) {
+            applied = 1;
+        }
+        if (applied) {
+            m->status[id] = st;
+            m->inc[id] = in;
+            j->napplied++;
+        }
+        if (j->applied) j->applied[i] = (uint8_t)applied;
+    }
+    return NULL;
+}
+
+uint32_t orc_members_update_mt(orc_members *m, const uint32_t *ids, const uint8_t *status, const int64_t *inc,
+                               uint32_t k, int64_t now_ms, int threads, uint8_t *applied_out) {
+    for (uint32_t i = 0; i < k; i++)
+        if (!m->exists[ids[i]] || !m->is_ready) return 0xFFFFFFFFu; /* only the no-create, ready case */
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    fold_job jobs[256];
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = (fold_job){m, ids, status, inc, k, (uint32_t)t, (uint32_t)threads, now_ms, applied_out, 0};
+        pthread_create(&th[t], NULL, fold_worker, &jobs[t]);
+    }
+    uint32_t napplied = 0;
+    for (int t = 0; t < threads; t++) {
+        pthread_join(th[t], NULL);
+        napplied += jobs[t].napplied;
+    }
+    if (napplied) compute_checksum(m);
     return napplied;
 }
 

@@ -102,13 +102,15 @@ SIGNATURES = {
     "rp_sim_create_shard": (_INT, [_U32, _P, _P, _P, _P, _U32, _U32, ctypes.c_int64, _INT, _P, _U32, _U32, _P]),
     "rp_sim_shard_info": (_INT, [_P, _P, _P, _P, _P]),
     "rp_sim_stage": (_INT, [_P, _INT]),
-    "rp_sim_outbox": (_INT, [_P, _P, _P, _P, _P]),
-    "rp_sim_inbox": (_INT, [_P, _P, _P, _P, _P]),
+    "rp_sim_outbox": (_INT, [_P, _P, _P, _P]),
+    "rp_sim_inbox": (_INT, [_P, _P, _P, _P]),
     "rp_sim_exchange_local": (_INT, [_P, _U32]),
     "rp_sim_converged_local": (_INT, [_P, _P]),
     "rp_sim_create_scenario": (_INT, [_U32, _P, _P, _P, _P, _U32, _U32, ctypes.c_int64, _INT, _P, _U32, _U32, _P, _U32,
                                       _P]),
     "rp_sim_piggyback": (_INT, [_P, _P]),
+    "rp_sim_counters": (_INT, [_P, _P]),
+    "rp_members_defer_checksum": (_INT, [_P, _INT]),
     "rp_copy": (_INT, [_P, _P, _U64, _P]),
 }
 
@@ -666,6 +668,11 @@ class GossipSim:
         check(lib().rp_sim_piggyback(self._h, out.ctypes.data))
         return out
 
+    def counters(self):
+        out = np.zeros(8, dtype=np.uint64)
+        check(lib().rp_sim_counters(self._h, out.ctypes.data))
+        return dict(zip(_COUNTER_NAMES, (int(x) for x in out)))
+
 
 # ---------------------------------------------------------------------------------------------
 # Sharded simulator (C5): nodes partitioned over shards; a round = five stages + four message
@@ -713,20 +720,22 @@ class SimShard:
         check(lib().rp_sim_stage(self._h, k))
 
     def outbox(self):
-        """(nmsg[G], nrec[G], device msg pointer, device rec pointer): messages grouped by destination."""
+        """(nmsg[G], nrec[G], device buffer): per destination in shard order, a segment of
+        nmsg[g] 40-byte headers then nrec[g] 24-byte records."""
         nm = np.zeros(self.G, dtype=np.uint64)
         nr = np.zeros(self.G, dtype=np.uint64)
-        mp, rp_ = ctypes.c_void_p(), ctypes.c_void_p()
-        check(lib().rp_sim_outbox(self._h, nm.ctypes.data, nr.ctypes.data, ctypes.byref(mp), ctypes.byref(rp_)))
-        return nm, nr, mp.value or 0, rp_.value or 0
+        bp = ctypes.c_void_p()
+        check(lib().rp_sim_outbox(self._h, nm.ctypes.data, nr.ctypes.data, ctypes.byref(bp)))
+        return nm, nr, bp.value or 0
 
     def inbox(self, nmsg, nrec):
-        """Size the inbox for per-source counts; returns (device msg pointer, device rec pointer)."""
+        """Size the inbox for per-source counts; returns its device buffer (to be filled with the
+        sources' segments in source order)."""
         nm = np.ascontiguousarray(nmsg, dtype=np.uint64)
         nr = np.ascontiguousarray(nrec, dtype=np.uint64)
-        mp, rp_ = ctypes.c_void_p(), ctypes.c_void_p()
-        check(lib().rp_sim_inbox(self._h, nm.ctypes.data, nr.ctypes.data, ctypes.byref(mp), ctypes.byref(rp_)))
-        return mp.value or 0, rp_.value or 0
+        bp = ctypes.c_void_p()
+        check(lib().rp_sim_inbox(self._h, nm.ctypes.data, nr.ctypes.data, ctypes.byref(bp)))
+        return bp.value or 0
 
     @property
     def round(self):
@@ -762,6 +771,11 @@ class SimShard:
             check(lib().rp_sim_piggyback(self._h, out.ctypes.data))
         return out
 
+    def counters(self):
+        out = np.zeros(8, dtype=np.uint64)
+        check(lib().rp_sim_counters(self._h, out.ctypes.data))
+        return out
+
 
 def conv_reduce(parts):
     """Convergence (scenario-runner.js:152-170 + killed members faulty everywhere) from the
@@ -775,6 +789,7 @@ def conv_reduce(parts):
 
 
 _STAT_NAMES = ["pings", "pingreqs", "fullsyncs", "applied"]
+_COUNTER_NAMES = _STAT_NAMES + ["messages", "records", "views_hashed", "base_len"]
 
 
 class ShardedGossipSim:
@@ -823,16 +838,30 @@ class ShardedGossipSim:
         tot = sum(s.stats() for s in self.shards)
         return dict(zip(_STAT_NAMES, (int(x) for x in tot)))
 
+    def counters(self):
+        c = sum(s.counters() for s in self.shards)
+        c[7] = self.shards[0].counters()[7]
+        return dict(zip(_COUNTER_NAMES, (int(x) for x in c)))
+
     def piggyback(self):
         return np.concatenate([s.piggyback() for s in self.shards])
 
 
+class _DeviceBytes:
+    """A device byte range seen by torch without a copy (__cuda_array_interface__)."""
+
+    def __init__(self, ptr, n):
+        self.__cuda_array_interface__ = {"shape": (int(n),), "typestr": "|u1", "data": (int(ptr), False),
+                                         "version": 2, "strides": None}
+
+
 class MessageExchange:
     """All-to-all-v of the sharded simulator's messages over torch.distributed: one collective
-    for the per-peer counts, one for the bytes (each peer's segment = its 40-byte headers then
-    its 24-byte records). With the nccl backend (RCCL on ROCm) the bytes stay in HBM and move
-    over xGMI; with gloo they are staged through host memory (tests). `copy(dst, src, nbytes)`
-    moves bytes between the simulator's buffers and the collective's tensors."""
+    for the per-peer counts, one for the bytes. The simulator's outbox already holds one segment
+    per destination ([40-byte headers | 24-byte records]) and its inbox takes one segment per
+    source, so with the nccl backend (RCCL on ROCm) the collective reads the outbox and writes
+    the inbox in HBM directly, over xGMI, with no staging copies. With gloo the bytes go through
+    one host buffer each way (`copy(dst, src, nbytes)` moves them; tests)."""
 
     def __init__(self, group=None, device=None, copy=None):
         import torch
@@ -842,8 +871,12 @@ class MessageExchange:
         self.rank = dist.get_rank(group)
         backend = dist.get_backend(group)
         self.on_device = backend == "nccl"
-        self.device = device if self.on_device else "cpu"
+        self.device = torch.device("cuda", device) if self.on_device and isinstance(device, int) else \
+            (device if self.on_device else "cpu")
         self._copy = copy
+        self._cnt = torch.zeros(2 * self.G, dtype=torch.int64, device=self.device)
+        self._rcnt = torch.zeros(2 * self.G, dtype=torch.int64, device=self.device)
+        self._host = {}  # gloo staging buffers, kept across rounds
 
     def copy(self, dst, src, nbytes):
         if nbytes:
@@ -853,37 +886,41 @@ class MessageExchange:
                 stream = self.torch.cuda.current_stream().cuda_stream if self.on_device else None
                 check(lib().rp_copy(dst, src, nbytes, stream))
 
-    def exchange(self, out_nmsg, out_nrec, out_msg, out_rec, alloc_in):
-        """out_*: this rank's outbox (counts per destination, buffer addresses, grouped by
-        destination). alloc_in(in_nmsg, in_nrec) -> (msg address, rec address) of the inbox,
-        which receives every source's messages concatenated in source order."""
+    def _staging(self, key, n):
+        t = self._host.get(key)
+        if t is None or t.numel() < n:
+            t = self.torch.empty(max(n, 1) + max(n, 1) // 2, dtype=self.torch.uint8)
+            self._host[key] = t
+        return t
+
+    def exchange(self, out_nmsg, out_nrec, out_buf, alloc_in):
+        """out_*: this rank's outbox (counts per destination, its packed buffer's address).
+        alloc_in(in_nmsg, in_nrec) -> the inbox's address, which receives every source's segment
+        for this rank in source order."""
         torch, dist, G = self.torch, self.dist, self.G
-        cnt = torch.tensor(np.stack([out_nmsg, out_nrec], axis=1).astype(np.int64).reshape(-1), device=self.device)
-        rcnt = torch.empty_like(cnt)
-        dist.all_to_all_single(rcnt, cnt, group=self.group)
-        rc = rcnt.cpu().numpy().reshape(G, 2)
+        self._cnt.copy_(torch.from_numpy(np.stack([out_nmsg, out_nrec], axis=1).astype(np.int64).reshape(-1)))
+        dist.all_to_all_single(self._rcnt, self._cnt, group=self.group)
+        rc = self._rcnt.cpu().numpy().reshape(G, 2)
         in_nmsg, in_nrec = rc[:, 0].astype(np.uint64), rc[:, 1].astype(np.uint64)
         seg_out = [int(out_nmsg[g]) * MSG_BYTES + int(out_nrec[g]) * REC_BYTES for g in range(G)]
         seg_in = [int(in_nmsg[g]) * MSG_BYTES + int(in_nrec[g]) * REC_BYTES for g in range(G)]
-        send = torch.empty(max(1, sum(seg_out)), dtype=torch.uint8, device=self.device)
-        recv = torch.empty(max(1, sum(seg_in)), dtype=torch.uint8, device=self.device)
-        base, mo, ro = send.data_ptr(), 0, 0
-        for g in range(G):
-            nb_m, nb_r = int(out_nmsg[g]) * MSG_BYTES, int(out_nrec[g]) * REC_BYTES
-            self.copy(base, out_msg + mo, nb_m)
-            self.copy(base + nb_m, out_rec + ro, nb_r)
-            base, mo, ro = base + nb_m + nb_r, mo + nb_m, ro + nb_r
-        dist.all_to_all_single(recv[:sum(seg_in)], send[:sum(seg_out)], output_split_sizes=seg_in,
-                               input_split_sizes=seg_out, group=self.group)
-        in_msg, in_rec = alloc_in(in_nmsg, in_nrec)
-        base, mo, ro = recv.data_ptr(), 0, 0
-        for g in range(G):
-            nb_m, nb_r = int(in_nmsg[g]) * MSG_BYTES, int(in_nrec[g]) * REC_BYTES
-            self.copy(in_msg + mo, base, nb_m)
-            self.copy(in_rec + ro, base + nb_m, nb_r)
-            base, mo, ro = base + nb_m + nb_r, mo + nb_m, ro + nb_r
+        tot_out, tot_in = sum(seg_out), sum(seg_in)
+        in_buf = alloc_in(in_nmsg, in_nrec)
         if self.on_device:
+            send = torch.as_tensor(_DeviceBytes(out_buf, tot_out), device=self.device) if tot_out else \
+                torch.empty(0, dtype=torch.uint8, device=self.device)
+            recv = torch.as_tensor(_DeviceBytes(in_buf, tot_in), device=self.device) if tot_in else \
+                torch.empty(0, dtype=torch.uint8, device=self.device)
+            dist.all_to_all_single(recv, send, output_split_sizes=seg_in, input_split_sizes=seg_out,
+                                   group=self.group)
             torch.cuda.current_stream().synchronize()
+        else:
+            send = self._staging("send", tot_out)
+            recv = self._staging("recv", tot_in)
+            self.copy(send.data_ptr(), out_buf, tot_out)
+            dist.all_to_all_single(recv[:tot_in], send[:tot_out], output_split_sizes=seg_in,
+                                   input_split_sizes=seg_out, group=self.group)
+            self.copy(in_buf, recv.data_ptr(), tot_in)
         return in_nmsg, in_nrec
 
 
@@ -911,9 +948,9 @@ class DistGossipSim:
             for k in range(SIM_STAGES):
                 sh.stage(k)
                 if k < SIM_STAGES - 1:
-                    nm, nr, mp, rp_ = sh.outbox()
+                    nm, nr, buf = sh.outbox()
                     self.exchange_bytes += int(nm.sum()) * MSG_BYTES + int(nr.sum()) * REC_BYTES
-                    self.xchg.exchange(nm, nr, mp, rp_, sh.inbox)
+                    self.xchg.exchange(nm, nr, buf, sh.inbox)
 
     @property
     def round(self):
@@ -943,6 +980,11 @@ class DistGossipSim:
     def stats(self):
         tot = sum(self._allgather(self.shard.stats().astype(np.int64)))
         return dict(zip(_STAT_NAMES, (int(x) for x in tot)))
+
+    def counters(self):
+        c = sum(self._allgather(self.shard.counters().astype(np.int64)))
+        c[7] = self.shard.counters()[7]
+        return dict(zip(_COUNTER_NAMES, (int(x) for x in c)))
 
 
 # ------------------------------------------------------------------ gossip wire bodies

@@ -179,6 +179,7 @@ struct Members {
     NameTable nt;
     uint32_t local_id = 0xFFFFFFFFu;
     uint32_t cap = 0;
+    bool defer_ck = false;  // rp_members_defer_checksum
     DevBuf<uint8_t> exists, status;
     DevBuf<int64_t> inc;
     DevBuf<uint32_t> ck;        // [0] checksum, [1] is_set
@@ -226,7 +227,7 @@ struct Members {
             hipLaunchKernelGGL(k_fold, dim3(grid_for(k, 256)), dim3(256), 0, s, sk.p, sv.p, k, chs, chi, exists.p,
                                status.p, inc.p, local_id, now_ms, applied, nst, ninc, napplied.p);
             RP_HIP(hipGetLastError());
-            checksum_dev(s, napplied.p);
+            if (!defer_ck) checksum_dev(s, napplied.p);
         }
         if (n_applied_out)
             RP_HIP(hipMemcpyAsync(n_applied_out, napplied.p, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
@@ -446,6 +447,10 @@ int rp_members_checksum(rp_members* h, uint32_t* out, int* is_set) {
         if (out) *out = v[0];
         if (is_set) *is_set = v[1] ? 1 : 0;
     });
+}
+
+int rp_members_defer_checksum(rp_members* h, int defer) {
+    return guard([&] { MB(h).defer_ck = defer != 0; });
 }
 
 int rp_members_compute_checksum(rp_members* h) {

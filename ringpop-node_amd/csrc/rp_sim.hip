@@ -82,8 +82,9 @@ __device__ __forceinline__ uint32_t rec_w0(uint32_t a, uint8_t st, uint32_t aux)
 
 // A message header (40 bytes): a ping (from sender to target, with the sender's checksum and
 // incarnation: ping-sender.js:71-76), a ping-req leg (tag = leg index; ping-req-sender.js:75-81)
-// or a response (to = the original sender). n = records (NONE = network error); roff = offset of
-// the records in the message buffer's record area.
+// or a response (to = the original sender). n = records (NONE = network error); roff = where its
+// records are: in an outbox, the index of the first one in its destination's record area; once
+// imported, the byte offset of the first one in the inbox buffer.
 struct Msg {
     uint32_t from, to, n, tag;
     uint32_t ck, pad;
@@ -159,8 +160,8 @@ struct SimDev {
     uint4* dlist;       // [NL][dcap] a lane checksum's deviated pieces, address order
     uint32_t dcap;
     // inbound messages of the current stage
-    const Msg* in_msg;
-    const Rec* in_rec;
+    const Msg* in_msg;      // headers, gathered in arrival order
+    const uint8_t* in_buf;  // the inbox: per source shard [headers | records]
     uint32_t nin;
     const uint32_t* ib_off;  // [NL+1] inbox CSR (pings / legs) by local receiver
     const uint32_t* ib_idx;  // message indices, (receiver, arrival) order
@@ -178,6 +179,10 @@ struct SimDev {
 __device__ __forceinline__ Rec* ping_slot(const SimDev& S, uint32_t lv) { return S.pool + (uint64_t)lv * S.Cm; }
 __device__ __forceinline__ Rec* leg_slot(const SimDev& S, uint32_t lv) {
     return S.pool + ((uint64_t)S.NL + lv) * S.Cm;
+}
+
+__device__ __forceinline__ const Rec* msg_recs(const SimDev& S, const Msg& m) {
+    return reinterpret_cast<const Rec*>(S.in_buf + m.roff);
 }
 
 __device__ __forceinline__ uint32_t shard_of(const SimDev& S, uint32_t v) {
@@ -851,7 +856,10 @@ __device__ void block_checksum(const SimDev& S, uint32_t lv, uint8_t* scratch, L
 
 __device__ __forceinline__ void checksum_if_dirty(const SimDev& S, uint32_t lv, Lds& L) {
     __syncthreads();
-    if (S.dirty[lv]) block_checksum(S, lv, S.strbuf + (uint64_t)blockIdx.x * S.strcap, L);
+    if (S.dirty[lv]) {
+        if (threadIdx.x == 0) atomicAdd(&S.stats[4], 1ull);  // views hashed
+        block_checksum(S, lv, S.strbuf + (uint64_t)blockIdx.x * S.strcap, L);
+    }
 }
 
 // Base-string ring of one wave in LDS. The wave's lanes hash different views in lockstep (chunk
@@ -1785,6 +1793,16 @@ __global__ void k_round_begin(SimDev S) {
     if (blockIdx.x == 0 && threadIdx.x == 0) *S.cursor = 0;
 }
 
+// views the batch refresh is about to hash (stats[4])
+__global__ void k_count_dirty(SimDev S) {
+    uint32_t c = 0;
+    for (uint32_t lv = blockIdx.x * blockDim.x + threadIdx.x; lv < S.NL; lv += gridDim.x * blockDim.x)
+        c += (!S.dead[S.v0 + lv] && S.dirty[lv]) ? 1u : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(&S.stats[4], (unsigned long long)c);
+}
+
 // A: iterator.next() + issueAsSender() for every live node (checksums are fresh: k_ck_lanes ran)
 __global__ __launch_bounds__(kT) void k_phase_a(SimDev S) {
     __shared__ Lds L;
@@ -1827,7 +1845,7 @@ __global__ __launch_bounds__(kT) void k_phase_b(SimDev S) {
         for (uint32_t q = b; q < e; q++) {
             const uint32_t i = S.ib_idx[q];
             const Msg m = S.in_msg[i];
-            block_apply(S, lj, S.in_rec + m.roff, m.n, L, now);
+            block_apply(S, lj, msg_recs(S, m), m.n, L, now);
             uint64_t o = 0;
             const uint32_t n = block_issue_receiver(S, lj, m.from, m.inc, m.ck, &o, L);
             if (threadIdx.x == 0) {
@@ -1849,7 +1867,7 @@ __global__ __launch_bounds__(kT) void k_phase_c(SimDev S) {
         if (i == NONE) continue;  // dead sender, no target, dead target
         const Msg m = S.in_msg[i];
         if (m.n == NONE) continue;  // the target's arena overflowed (reported)
-        const Rec* r = S.in_rec + m.roff;
+        const Rec* r = msg_recs(S, m);
         block_apply(S, lv, r, m.n, L, now);
         block_apply(S, lv, r, m.n, L, now);
     }
@@ -1989,7 +2007,7 @@ __global__ __launch_bounds__(kT) void k_phase_d2(SimDev S) {
         for (uint32_t q = b; q < e; q++) {
             const uint32_t i = S.ib_idx[q];
             const Msg m = S.in_msg[i];
-            block_apply(S, lh, S.in_rec + m.roff, m.n, L, now);
+            block_apply(S, lh, msg_recs(S, m), m.n, L, now);
             block_issue(S, lh, NONE, 0, nullptr, L);  // the helper's own ping of the dead target
             uint64_t o = 0;
             const uint32_t n = block_issue_receiver(S, lh, m.from, m.inc, m.ck, &o, L);
@@ -2017,7 +2035,7 @@ __global__ __launch_bounds__(kT) void k_phase_d3(SimDev S) {
             if (i == NONE) continue;  // dead helper: network error
             const Msg m = S.in_msg[i];
             if (m.n == NONE) continue;
-            block_apply(S, lv, S.in_rec + m.roff, m.n, L, now);
+            block_apply(S, lv, msg_recs(S, m), m.n, L, now);
             bad = true;
         }
         if (bad) {
@@ -2124,15 +2142,19 @@ __global__ void k_out_counts(SimDev S, int kind, const uint32_t* __restrict__ ke
         cnt[i] = key[i] < S.G ? out_count(S, kind, val[i]) : 0u;
 }
 
-// one workgroup per message: header + records (leg records filtered by the leg's count rule)
+// one workgroup per message: header + records (leg records filtered by the leg's count rule),
+// into the packed outbox: destination d's segment at byte seg[d] holds its headers, then its
+// records
 __global__ __launch_bounds__(kT) void k_out_fill(SimDev S, int kind, const uint32_t* __restrict__ key,
                                                  const uint32_t* __restrict__ val, uint32_t nmsg,
                                                  const uint32_t* __restrict__ roff, const uint32_t* __restrict__ moff,
-                                                 Msg* __restrict__ out_msg, Rec* __restrict__ out_rec) {
+                                                 const uint64_t* __restrict__ seg, uint8_t* __restrict__ out) {
     __shared__ uint32_t lds[16];
     for (uint32_t i = blockIdx.x; i < nmsg; i += gridDim.x) {
         const uint32_t c = val[i], d = key[i];
         const uint64_t r0 = roff[i], dbase = roff[moff[d]];
+        Msg* out_msg = reinterpret_cast<Msg*>(out + seg[d]) - moff[d];
+        Rec* out_rec = reinterpret_cast<Rec*>(out + seg[d] + sizeof(Msg) * (uint64_t)(moff[d + 1] - moff[d])) - dbase;
         Msg m{};
         const Rec* src = nullptr;
         uint32_t nsrc = 0, k = 0, maxp = 0;
@@ -2179,13 +2201,19 @@ __global__ __launch_bounds__(kT) void k_out_fill(SimDev S, int kind, const uint3
 
 // ---- inboxes
 
-// inbound record offsets: per-source segments -> one record area
-__global__ void k_in_fix(Msg* __restrict__ msg, uint32_t n, const uint64_t* __restrict__ mbase,
-                         const uint64_t* __restrict__ rbase, uint32_t G) {
+// the inbox's headers in arrival order (sources in shard order), their record offsets made
+// absolute byte offsets into the inbox. tab = {message base [G + 1], segment byte offset [G]}
+__global__ void k_in_gather(Msg* __restrict__ msg, uint32_t n, const uint8_t* __restrict__ buf,
+                            const uint64_t* __restrict__ tab, uint32_t G) {
+    const uint64_t* mbase = tab;
+    const uint64_t* segb = tab + G + 1;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         uint32_t s = 0;
         while (s + 1 < G && i >= mbase[s + 1]) s++;
-        msg[i].roff += rbase[s];
+        const uint64_t nm = mbase[s + 1] - mbase[s];
+        Msg m = reinterpret_cast<const Msg*>(buf + segb[s])[i - mbase[s]];
+        m.roff = segb[s] + sizeof(Msg) * nm + sizeof(Rec) * m.roff;
+        msg[i] = m;
     }
 }
 
@@ -2288,15 +2316,28 @@ __global__ void k_sim_bcast_checksum(SimDev S) {
 
 }  // namespace
 
-// Exchange buffers: headers + records, grouped by peer shard. nmsg/nrec[G] per peer.
+// An exchange buffer: one segment per peer shard, in shard order, each holding that peer's
+// 40-byte headers then its 24-byte records (nmsg/nrec[G]). The outbox is sent and the inbox
+// received as they lie (one all-to-all-v), kept across rounds and grown geometrically.
 struct MsgBuf {
-    DevBuf<Msg> msg;
-    DevBuf<Rec> rec;
+    DevBuf<uint8_t> buf;
     std::vector<uint64_t> nmsg, nrec;
     uint64_t tot_msg = 0, tot_rec = 0;
+    uint64_t seg_bytes(uint32_t g) const { return sizeof(Msg) * nmsg[g] + sizeof(Rec) * nrec[g]; }
+    uint64_t seg_off(uint32_t g) const {
+        uint64_t o = 0;
+        for (uint32_t h = 0; h < g; h++) o += seg_bytes(h);
+        return o;
+    }
+    uint64_t bytes() const { return sizeof(Msg) * tot_msg + sizeof(Rec) * tot_rec; }
+    void size_for(uint64_t b) {
+        if (b + 8 > buf.cap) {
+            const uint64_t c = std::max<uint64_t>(b + 8, buf.cap + buf.cap / 2);
+            buf.reserve(c);
+        }
+    }
     void swap(MsgBuf& o) {
-        msg.swap(o.msg);
-        rec.swap(o.rec);
+        buf.swap(o.buf);
         std::swap(nmsg, o.nmsg);
         std::swap(nrec, o.nrec);
         std::swap(tot_msg, o.tot_msg);
@@ -2318,6 +2359,8 @@ struct Sim {
     DevBuf<uint32_t> order, dev, n_chg, n_tim, n_shuf, ring_count, max_piggy, checksum, ck_snap, ping_n, leg_n,
         helpers, nhelp, leg_nk, cand, rank, err, bounds, want, conv, leave_list;
     DevBuf<uint32_t> okey, oval, ocnt, ooff, omoff;  // outbox build
+    DevBuf<uint64_t> oseg;                           // outbox segment offsets
+    DevBuf<Msg> imsg;                                // inbox headers, gathered
     DevBuf<uint32_t> ib_off, ib_idx, ikey;         // inbox build
     DevBuf<uint32_t> rsp_n, resp_idx, lresp_idx, d1list;
     DevBuf<uint64_t> boff, rsp_off, ibase;
@@ -2334,6 +2377,7 @@ struct Sim {
     size_t next_event = 0;
     uint32_t nwant = 0;
     bool conv_dirty = true;
+    uint64_t sent_msgs = 0, sent_recs = 0, base_len = 0;  // traffic counters (rp_sim_counters)
     int64_t round = 0;
     int next_stage = 0;  // 0..4 within a round
 
@@ -2352,6 +2396,7 @@ struct Sim {
             cus = (uint32_t)(n > 0 ? n : 1);
         }
         const uint32_t groups = (NL + 63) / 64;
+        hipLaunchKernelGGL(k_count_dirty, dim3(grid_for(NL, 256, 1024)), dim3(256), 0, st, d);
         const char* m = getenv("RP_SIM_CK");
         const bool pc = m ? strcmp(m, "lanes") != 0 : groups <= cus;
         if (pc && !(m && !strcmp(m, "pc3")))
@@ -2391,19 +2436,25 @@ struct Sim {
         RP_HIP(hipStreamSynchronize(st));
         out.tot_msg = moff[G];
         out.tot_rec = roff[G];
+        sent_msgs += out.tot_msg;
+        sent_recs += out.tot_rec;
+        std::vector<uint64_t> seg(G + 1);
         for (uint32_t g = 0; g < G; g++) {
             out.nmsg[g] = moff[g + 1] - moff[g];
             out.nrec[g] = roff[g + 1] - roff[g];
         }
-        out.msg.reserve(out.tot_msg + 1);
-        out.rec.reserve(out.tot_rec + 1);
+        for (uint32_t g = 0; g <= G; g++) seg[g] = out.seg_off(g);
+        out.size_for(out.bytes());
+        oseg.reserve(G + 1);
+        RP_HIP(hipMemcpyAsync(oseg.p, seg.data(), 8ull * (G + 1), hipMemcpyHostToDevice, st));
         if (out.tot_msg)
             hipLaunchKernelGGL(k_out_fill, dim3(grid_for(out.tot_msg, 1, 4096)), dim3(kT), 0, st, d, kind, okey.p,
-                               oval.p, (uint32_t)out.tot_msg, ooff.p, omoff.p, out.msg.p, out.rec.p);
+                               oval.p, (uint32_t)out.tot_msg, ooff.p, omoff.p, oseg.p, out.buf.p);
+        RP_HIP(hipStreamSynchronize(st));  // seg (host) is reused
         RP_HIP(hipGetLastError());
     }
 
-    // Size the inbox for per-source counts (the caller then fills in.msg / in.rec).
+    // Size the inbox for per-source counts (the caller then fills in.buf, segments in source order).
     void prepare_in(const uint64_t* nmsg, const uint64_t* nrec) {
         in.nmsg.assign(nmsg, nmsg + G);
         in.nrec.assign(nrec, nrec + G);
@@ -2413,8 +2464,7 @@ struct Sim {
             in.tot_rec += nrec[g];
         }
         RP_REQUIRE(in.tot_msg < (1ull << 32), "sim: too many inbound messages");
-        in.msg.reserve(in.tot_msg + 1);
-        in.rec.reserve(in.tot_rec + 1);
+        in.size_for(in.bytes());
     }
 
     // One shard: the outbox is the inbox.
@@ -2425,24 +2475,26 @@ struct Sim {
         in.nrec = nr;
     }
 
-    // Bind the inbox to the device view: rebase record offsets per source, then index it.
+    // Bind the inbox to the device view: gather the headers (absolute record offsets), index them.
     void import_in(int kind) {
-        d.in_msg = in.msg.p;
-        d.in_rec = in.rec.p;
+        imsg.reserve(in.tot_msg + 1);
+        d.in_msg = imsg.p;
+        d.in_buf = in.buf.p;
         d.nin = (uint32_t)in.tot_msg;
-        if (G > 1 && in.tot_msg) {
-            std::vector<uint64_t> base(2 * G);
-            uint64_t m = 0, r = 0;
+        if (in.tot_msg) {
+            std::vector<uint64_t> tab(2 * G + 1);
+            uint64_t m = 0;
             for (uint32_t g = 0; g < G; g++) {
-                base[g] = m;
-                base[G + g] = r;
+                tab[g] = m;
                 m += in.nmsg[g];
-                r += in.nrec[g];
+                tab[G + 1 + g] = in.seg_off(g);
             }
-            ibase.reserve(2 * G);
-            RP_HIP(hipMemcpyAsync(ibase.p, base.data(), 16ull * G, hipMemcpyHostToDevice, st));
-            hipLaunchKernelGGL(k_in_fix, dim3(grid_for(in.tot_msg, 256)), dim3(256), 0, st, in.msg.p,
-                               (uint32_t)in.tot_msg, ibase.p, ibase.p + G, G);
+            tab[G] = m;
+            ibase.reserve(2 * G + 1);
+            RP_HIP(hipMemcpyAsync(ibase.p, tab.data(), 8ull * (2 * G + 1), hipMemcpyHostToDevice, st));
+            hipLaunchKernelGGL(k_in_gather, dim3(grid_for(in.tot_msg, 256)), dim3(256), 0, st, imsg.p,
+                               (uint32_t)in.tot_msg, in.buf.p, ibase.p, G);
+            RP_HIP(hipStreamSynchronize(st));  // tab (host) is reused
         }
         const uint32_t n = (uint32_t)in.tot_msg;
         if (kind == K_PING || kind == K_LEG) {
@@ -2739,7 +2791,8 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
         // iterator's scratch)
         const uint64_t strcap = std::max<uint64_t>(S.nt.h_bytes.size() + 29ull * n + 64, 5ull * n + 64);
         S.strbuf.reserve((uint64_t)S.grid * ((strcap + 255) & ~255ull));
-        S.stats.reserve(4); S.cursor.reserve(1); S.err.reserve(1);
+        S.stats.reserve(8); S.cursor.reserve(1); S.err.reserve(1);
+        S.base_len = boff[n];
         S.inc0.reserve(n); S.rank.reserve(n); S.boff.reserve(n + 1ull); S.sbase.reserve(base.size());
         RP_HIP(hipMemcpyAsync(S.inc0.p, inc0, 8ull * n, hipMemcpyHostToDevice, S.st));
         RP_HIP(hipMemcpyAsync(S.rank.p, rank.data(), 4ull * n, hipMemcpyHostToDevice, S.st));
@@ -2748,7 +2801,7 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
         RP_HIP(hipMemcpyAsync(S.bounds.p, bnd.data(), 4ull * (nshards + 1), hipMemcpyHostToDevice, S.st));
         S.h_dead.assign(dead, dead + n);
         RP_HIP(hipMemcpyAsync(S.dead.p, S.h_dead.data(), n, hipMemcpyHostToDevice, S.st));
-        RP_HIP(hipMemsetAsync(S.stats.p, 0, 4 * sizeof(unsigned long long), S.st));
+        RP_HIP(hipMemsetAsync(S.stats.p, 0, 8 * sizeof(unsigned long long), S.st));
         RP_HIP(hipMemsetAsync(S.err.p, 0, 4, S.st));
         RP_HIP(hipMemsetAsync(S.cursor.p, 0, 8, S.st));
         rp::SimDev& d = S.d;
@@ -2822,6 +2875,20 @@ int rp_sim_create_scenario(uint32_t n, const char* names, const uint32_t* off, c
     });
 }
 
+int rp_sim_counters(rp_sim* s, uint64_t* out8) {
+    return guard([&] {
+        rp::Sim& S = SM(s);
+        unsigned long long v[8];
+        RP_HIP(hipMemcpyAsync(v, S.stats.p, sizeof v, hipMemcpyDeviceToHost, S.st));
+        RP_HIP(hipStreamSynchronize(S.st));
+        for (int i = 0; i < 4; i++) out8[i] = v[i];
+        out8[4] = S.sent_msgs;
+        out8[5] = S.sent_recs;
+        out8[6] = v[4];
+        out8[7] = S.base_len;
+    });
+}
+
 int rp_sim_piggyback(rp_sim* s, uint32_t* out) {
     return guard([&] {
         rp::Sim& S = SM(s);
@@ -2880,7 +2947,7 @@ int rp_sim_stage(rp_sim* s, int stage) {
     });
 }
 
-int rp_sim_outbox(rp_sim* s, uint64_t* nmsg, uint64_t* nrec, void** msg, void** rec) {
+int rp_sim_outbox(rp_sim* s, uint64_t* nmsg, uint64_t* nrec, void** buf) {
     return guard([&] {
         rp::Sim& S = SM(s);
         RP_HIP(hipStreamSynchronize(S.st));
@@ -2888,19 +2955,17 @@ int rp_sim_outbox(rp_sim* s, uint64_t* nmsg, uint64_t* nrec, void** msg, void** 
             if (nmsg) nmsg[g] = S.out.nmsg.empty() ? 0 : S.out.nmsg[g];
             if (nrec) nrec[g] = S.out.nrec.empty() ? 0 : S.out.nrec[g];
         }
-        if (msg) *msg = S.out.msg.p;
-        if (rec) *rec = S.out.rec.p;
+        if (buf) *buf = S.out.buf.p;
     });
 }
 
-int rp_sim_inbox(rp_sim* s, const uint64_t* nmsg, const uint64_t* nrec, void** msg, void** rec) {
+int rp_sim_inbox(rp_sim* s, const uint64_t* nmsg, const uint64_t* nrec, void** buf) {
     return guard([&] {
         rp::Sim& S = SM(s);
         RP_REQUIRE(nmsg && nrec, "sim_inbox: counts required");
         S.prepare_in(nmsg, nrec);
         RP_HIP(hipStreamSynchronize(S.st));
-        if (msg) *msg = S.in.msg.p;
-        if (rec) *rec = S.in.rec.p;
+        if (buf) *buf = S.in.buf.p;
     });
 }
 
@@ -2921,22 +2986,12 @@ int rp_sim_exchange_local(rp_sim* const* shards, uint32_t nshards) {
                 nr[src] = shards[src]->impl.out.nrec[dst];
             }
             D.prepare_in(nm.data(), nr.data());
-            uint64_t mo = 0, ro = 0;
             for (uint32_t src = 0; src < nshards; src++) {
                 rp::Sim& Sx = shards[src]->impl;
-                uint64_t msrc = 0, rsrc = 0;
-                for (uint32_t g = 0; g < dst; g++) {
-                    msrc += Sx.out.nmsg[g];
-                    rsrc += Sx.out.nrec[g];
-                }
-                if (nm[src])
-                    RP_HIP(hipMemcpyAsync(D.in.msg.p + mo, Sx.out.msg.p + msrc, sizeof(rp::Msg) * nm[src],
+                const uint64_t b = Sx.out.seg_bytes(dst);
+                if (b)
+                    RP_HIP(hipMemcpyAsync(D.in.buf.p + D.in.seg_off(src), Sx.out.buf.p + Sx.out.seg_off(dst), b,
                                           hipMemcpyDeviceToDevice, D.st));
-                if (nr[src])
-                    RP_HIP(hipMemcpyAsync(D.in.rec.p + ro, Sx.out.rec.p + rsrc, sizeof(rp::Rec) * nr[src],
-                                          hipMemcpyDeviceToDevice, D.st));
-                mo += nm[src];
-                ro += nr[src];
             }
         }
         for (uint32_t i = 0; i < nshards; i++) RP_HIP(hipStreamSynchronize(shards[i]->impl.st));

@@ -1,7 +1,7 @@
 """CPU (gloo, world_size 2) test of the sharded simulator's message exchange
-(ringpop-node_amd MessageExchange): per-peer counts, then one all-to-all-v of each peer's
-40-byte headers followed by its 24-byte records, unpacked into an inbox that concatenates the
-sources in rank order. Host buffers stand in for device buffers (copy = memmove)."""
+(ringpop-node_amd MessageExchange): per-peer counts, then one all-to-all-v of the packed outbox
+(per destination: 40-byte headers then 24-byte records) into an inbox holding the sources'
+segments in rank order. Host buffers stand in for device buffers (copy = memmove)."""
 import ctypes
 import os
 import socket
@@ -22,16 +22,19 @@ def _port():
     return p
 
 
+def _segment(rank, g, nm, nr):
+    """rank's segment for destination g: nm headers encoding (rank, g, i), nr records (rank, g, j)."""
+    parts = [np.full(40, (rank * 16 + g) * 8 + i % 8, dtype=np.uint8) for i in range(nm)]
+    parts += [np.full(24, 200 - (rank * 16 + g + j % 4), dtype=np.uint8) for j in range(nr)]
+    return np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+
+
 def _outbox(rank, G, rnd):
-    """Synthetic outbox of `rank`: for each destination g, rnd-dependent message/record counts;
-    message bytes encode (rank, g, i), record bytes (rank, g, j)."""
+    """Synthetic packed outbox of `rank`: for each destination g, rnd-dependent counts."""
     nm = np.array([(rank * 3 + g * 5 + rnd) % 4 for g in range(G)], dtype=np.uint64)
     nr = np.array([(rank * 7 + g * 2 + rnd) % 6 for g in range(G)], dtype=np.uint64)
-    msg = np.concatenate([np.full(40, (rank * 16 + g) * 8 + i % 8, dtype=np.uint8)
-                          for g in range(G) for i in range(int(nm[g]))] or [np.zeros(0, np.uint8)])
-    rec = np.concatenate([np.full(24, 200 - (rank * 16 + g + j % 4), dtype=np.uint8)
-                          for g in range(G) for j in range(int(nr[g]))] or [np.zeros(0, np.uint8)])
-    return nm, nr, msg, rec
+    segs = [_segment(rank, g, int(nm[g]), int(nr[g])) for g in range(G)]
+    return nm, nr, segs
 
 
 def _worker(rank, G, port, q):
@@ -44,30 +47,25 @@ def _worker(rank, G, port, q):
     x = rpa.MessageExchange(copy=lambda dst, src, nb: ctypes.memmove(dst, src, nb))
     ok = True
     for rnd in range(3):
-        nm, nr, msg, rec = _outbox(rank, G, rnd)
-        msg = np.ascontiguousarray(msg) if msg.size else np.zeros(1, np.uint8)
-        rec = np.ascontiguousarray(rec) if rec.size else np.zeros(1, np.uint8)
+        nm, nr, segs = _outbox(rank, G, rnd)
+        out = np.concatenate(segs + [np.zeros(1, np.uint8)])
         box = {}
 
         def alloc(in_nm, in_nr):
-            box["m"] = np.zeros(max(1, int(in_nm.sum()) * 40), np.uint8)
-            box["r"] = np.zeros(max(1, int(in_nr.sum()) * 24), np.uint8)
-            return box["m"].ctypes.data, box["r"].ctypes.data
+            box["b"] = np.zeros(max(1, int(in_nm.sum()) * 40 + int(in_nr.sum()) * 24), np.uint8)
+            return box["b"].ctypes.data
 
-        in_nm, in_nr = x.exchange(nm, nr, msg.ctypes.data, rec.ctypes.data, alloc)
+        in_nm, in_nr = x.exchange(nm, nr, out.ctypes.data, alloc)
         # expected: sources in rank order, each source's segment for this rank
-        want_m, want_r, want_nm, want_nr = [], [], [], []
+        want, want_nm, want_nr = [], [], []
         for s in range(G):
-            snm, snr, smsg, srec = _outbox(s, G, rnd)
-            mo = int(snm[:rank].sum()) * 40
-            ro = int(snr[:rank].sum()) * 24
-            want_m.append(smsg[mo:mo + int(snm[rank]) * 40])
-            want_r.append(srec[ro:ro + int(snr[rank]) * 24])
+            snm, snr, ssegs = _outbox(s, G, rnd)
+            want.append(ssegs[rank])
             want_nm.append(int(snm[rank]))
             want_nr.append(int(snr[rank]))
         ok &= in_nm.tolist() == want_nm and in_nr.tolist() == want_nr
-        wm, wr = np.concatenate(want_m), np.concatenate(want_r)
-        ok &= np.array_equal(box["m"][:wm.size], wm) and np.array_equal(box["r"][:wr.size], wr)
+        w = np.concatenate(want)
+        ok &= np.array_equal(box["b"][:w.size], w)
     q.put((rank, bool(ok)))
     dist.destroy_process_group()
 
