@@ -48,17 +48,9 @@ __device__ __forceinline__ uint32_t mul5_add(uint32_t x, uint32_t c) {  // 5x + 
     return lshl_add<2>(x, x + c);
 }
 
-__global__ __launch_bounds__(kHlThreads) void k_hash_long(const uint8_t* __restrict__ s, uint64_t len_host,
-                                                          const uint32_t* __restrict__ d_total,
-                                                          const uint32_t* __restrict__ d_gate,
-                                                          uint32_t* __restrict__ out) {
+// One string's chain by the whole workgroup (see the kernels below).
+__device__ void hash_long_block(const uint8_t* __restrict__ s, uint64_t len, uint32_t* __restrict__ out) {
     __shared__ __attribute__((aligned(16))) uint32_t win[2][kWin][8];
-    if (d_gate && *d_gate == 0) return;
-    uint64_t len = len_host;
-    if (d_total) {
-        const uint32_t t = *d_total;
-        len = t ? t - 1 : 0;
-    }
     const int tid = threadIdx.x;
     if (len <= 24) {
         if (tid == 0) {
@@ -199,11 +191,41 @@ __global__ __launch_bounds__(kHlThreads) void k_hash_long(const uint8_t* __restr
     }
 }
 
+__global__ __launch_bounds__(kHlThreads) void k_hash_long(const uint8_t* __restrict__ s, uint64_t len_host,
+                                                          const uint32_t* __restrict__ d_total,
+                                                          const uint32_t* __restrict__ d_gate,
+                                                          uint32_t* __restrict__ out) {
+    if (d_gate && *d_gate == 0) return;
+    uint64_t len = len_host;
+    if (d_total) {
+        const uint32_t t = *d_total;
+        len = t ? t - 1 : 0;
+    }
+    hash_long_block(s, len, out);
+}
+
+// Many strings at once, one workgroup (one serial chain + its producers) per string: string b
+// is s + b * stride, meta[4b] = its builder's total (length + 1), meta[4b + 1] = its gate (0:
+// skip); the hash goes to meta[4b + 2] (meta[4b + 3] = 1).
+__global__ __launch_bounds__(kHlThreads) void k_hash_long_multi(const uint8_t* __restrict__ s, uint64_t stride,
+                                                                uint32_t* __restrict__ meta) {
+    uint32_t* m = meta + 4ull * blockIdx.x;
+    if (m[1] == 0) return;
+    const uint32_t t = m[0];
+    hash_long_block(s + stride * blockIdx.x, t ? t - 1 : 0, m + 2);
+}
+
 }  // namespace
 
 void hash_long(const uint8_t* d_s, uint64_t len, const uint32_t* d_total, const uint32_t* d_gate, uint32_t* d_out,
                hipStream_t st) {
     hipLaunchKernelGGL(k_hash_long, dim3(1), dim3(kHlThreads), 0, st, d_s, len, d_total, d_gate, d_out);
+    RP_HIP(hipGetLastError());
+}
+
+void hash_long_multi(const uint8_t* d_s, uint64_t stride, uint32_t n, uint32_t* d_meta, hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_hash_long_multi, dim3(n), dim3(kHlThreads), 0, st, d_s, stride, d_meta);
     RP_HIP(hipGetLastError());
 }
 

@@ -160,6 +160,24 @@ __global__ void k_mck_write(const uint32_t* __restrict__ order, uint32_t n, cons
     }
 }
 
+// a pending checksum slot's total (string length + 1) and gate value, captured at build time
+__global__ void k_slot_meta(const uint32_t* __restrict__ total, const uint32_t* __restrict__ gate,
+                            uint32_t* __restrict__ meta) {
+    const uint32_t g = gate ? *gate : 1u;
+    meta[0] = g ? *total : 0u;
+    meta[1] = g;
+    meta[3] = 0;
+}
+
+// the group's results in batch order: the membership checksum is the last gated batch's hash
+__global__ void k_ck_commit(const uint32_t* __restrict__ meta, uint32_t n, uint32_t* __restrict__ ck) {
+    for (uint32_t b = 0; b < n; b++)
+        if (meta[4 * b + 1] && meta[4 * b + 3]) {
+            ck[0] = meta[4 * b + 2];
+            ck[1] = 1;
+        }
+}
+
 __global__ void k_copy_grow(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b,
                             const int64_t* __restrict__ c, uint32_t n, uint8_t* __restrict__ a2,
                             uint8_t* __restrict__ b2, int64_t* __restrict__ c2, uint32_t n2) {
@@ -184,7 +202,15 @@ struct Members {
     DevBuf<int64_t> inc;
     DevBuf<uint32_t> ck;        // [0] checksum, [1] is_set
     DevBuf<uint32_t> napplied;  // per-batch applied count (the checksum gate)
-    DevBuf<uint8_t> ck_buf;
+    // Checksum strings wait in slots until read or until kSlots are pending, then one launch
+    // hashes them side by side (one serial chain per workgroup): a batched caller pays one
+    // chain's latency per group instead of per batch. Reads flush first.
+    static constexpr uint32_t kSlots = 32;
+    DevBuf<uint8_t> ck_buf;   // kSlots strings of slot_bytes
+    uint64_t slot_bytes = 0;
+    DevBuf<uint32_t> ck_meta;  // [kSlots][4]: total, gate, hash, done
+    uint32_t npending = 0;
+    hipStream_t pend_st = nullptr;  // the stream the pending strings were built on
     DevBuf<uint32_t> ck_len, ck_pos;
     DevBuf<uint32_t> sk, sv;
     DevBuf<uint32_t> mk, mpos;  // set: merge marks and their positions
@@ -259,22 +285,55 @@ struct Members {
         checksum_dev(s, nullptr);
     }
 
-    // Membership.computeChecksum (index.js:48-75) gated on *gate != 0 (null = always).
+    // Membership.computeChecksum (index.js:48-75) gated on *gate != 0 (null = always): the
+    // string is built now (it reflects the table after this batch) into the next slot; its hash
+    // lands in ck when the group is flushed.
     void checksum_dev(hipStream_t s, const uint32_t* gate) {
         const uint32_t n = nt.size();
         if (!n) return;
         ck_len.reserve(n + 1);
         ck_pos.reserve(n + 1);
         // worst-case string: names + ';' + "suspect" + 20 digits per member
-        ck_buf.reserve(nt.h_bytes.size() + (uint64_t)n * 29 + 16);
+        const uint64_t need = (nt.h_bytes.size() + (uint64_t)n * 29 + 16 + 255) & ~255ull;
+        if (npending && (s != pend_st || need > slot_bytes)) {  // keep the group on one stream
+            flush_checksums();
+            RP_HIP(hipStreamSynchronize(pend_st));
+        }
+        if (need > slot_bytes) {
+            ck_buf.release();
+            ck_buf.reserve(need * kSlots);
+            slot_bytes = need;
+        }
+        if (npending == kSlots) flush_checksums();
+        pend_st = s;
+        ck_meta.reserve(4 * kSlots);
+        uint8_t* buf = ck_buf.p + slot_bytes * npending;
         hipLaunchKernelGGL(k_mck_len, dim3(grid_for(n, 256)), dim3(256), 0, s, nt.sorted.p, n, exists.p, status.p,
                            inc.p, nt.d_noff.p, gate, ck_len.p);
         RP_HIP(hipGetLastError());
         scan_exclusive_u32(ck_len.p, ck_pos.p, n, s, ws);
         hipLaunchKernelGGL(k_mck_write, dim3(grid_for(n, 256)), dim3(256), 0, s, nt.sorted.p, n, exists.p, status.p,
-                           inc.p, nt.d_bytes.p, nt.d_noff.p, ck_pos.p, gate, ck_buf.p);
+                           inc.p, nt.d_bytes.p, nt.d_noff.p, ck_pos.p, gate, buf);
+        hipLaunchKernelGGL(k_slot_meta, dim3(1), dim3(1), 0, s, ck_pos.p + n, gate, ck_meta.p + 4 * npending);
         RP_HIP(hipGetLastError());
-        hash_long(ck_buf.p, 0, ck_pos.p + n, gate, ck.p, s);
+        npending++;
+    }
+
+    // hash every pending string (side by side), then commit the last gated one to ck; ordered on
+    // the stream that built them
+    void flush_checksums() {
+        if (!npending) return;
+        hash_long_multi(ck_buf.p, slot_bytes, npending, ck_meta.p, pend_st);
+        hipLaunchKernelGGL(k_ck_commit, dim3(1), dim3(1), 0, pend_st, ck_meta.p, npending, ck.p);
+        RP_HIP(hipGetLastError());
+        npending = 0;
+    }
+    // flush and wait, before a host read of the checksum on the handle's stream
+    void settle_checksums() {
+        if (!npending) return;
+        hipStream_t p = pend_st;
+        flush_checksums();
+        RP_HIP(hipStreamSynchronize(p));
     }
 };
 
@@ -441,6 +500,7 @@ int rp_members_set(rp_members* h, const uint32_t* ids, const uint8_t* status, co
 int rp_members_checksum(rp_members* h, uint32_t* out, int* is_set) {
     return guard([&] {
         rp::Members& m = MB(h);
+        m.settle_checksums();
         uint32_t v[2];
         RP_HIP(hipMemcpyAsync(v, m.ck.p, sizeof v, hipMemcpyDeviceToHost, m.st));
         RP_HIP(hipStreamSynchronize(m.st));
@@ -457,7 +517,7 @@ int rp_members_compute_checksum(rp_members* h) {
     return guard([&] {
         rp::Members& m = MB(h);
         m.checksum_dev(m.st, nullptr);
-        RP_HIP(hipStreamSynchronize(m.st));
+        m.settle_checksums();
     });
 }
 
@@ -466,8 +526,10 @@ int rp_members_checksum_string(rp_members* h, char* buf, uint64_t cap, uint64_t*
         rp::Members& m = MB(h);
         const uint32_t n = m.nt.size();
         uint32_t total = 0;
+        const uint8_t* str = nullptr;
         if (n) {
             m.checksum_dev(m.st, nullptr);
+            str = m.ck_buf.p + m.slot_bytes * (m.npending - 1);
             RP_HIP(hipMemcpyAsync(&total, m.ck_pos.p + n, 4, hipMemcpyDeviceToHost, m.st));
             RP_HIP(hipStreamSynchronize(m.st));
         }
@@ -475,9 +537,10 @@ int rp_members_checksum_string(rp_members* h, char* buf, uint64_t cap, uint64_t*
         if (len) *len = L;
         const uint64_t c = std::min<uint64_t>(cap, L);
         if (buf && c) {
-            RP_HIP(hipMemcpyAsync(buf, m.ck_buf.p, c, hipMemcpyDeviceToHost, m.st));
+            RP_HIP(hipMemcpyAsync(buf, str, c, hipMemcpyDeviceToHost, m.st));
             RP_HIP(hipStreamSynchronize(m.st));
         }
+        m.settle_checksums();
     });
 }
 

@@ -181,3 +181,32 @@ def test_bootstrap_set_vs_oracle(gpu, orc):
         assert (om is None) == (not ex[a])
         if om:
             assert (gpu.STATUS_NAME[int(dst[a])], int(dinc[a])) == (om["status"], om["incarnationNumber"])
+
+
+@pytest.mark.parametrize("nbatches,tail_noops", [(5, 0), (37, 3), (70, 0)])
+def test_grouped_checksums_across_unread_batches(gpu, orc, nbatches, tail_noops):
+    """Device batches whose checksums are never read in between: their strings wait in slots and
+    are hashed side by side (32 per launch). A read after the last batch must equal the oracle's
+    checksum after the same sequence — including when the last batches applied nothing (the
+    checksum is then the last applying batch's), and across several full groups."""
+    S = synth()
+    n = k = 20_000
+    names, st0, inc0 = S.c3_members(n)
+    m = gpu.Membership(whoami=names[0], capacity=n)
+    o = orc.Members(names, local=names[0], join_seed=0)
+    ids0 = np.asarray(m.intern(names), dtype=np.uint32)
+    m.update_ids(ids0, st0, inc0, now_ms=1)
+    o.update_ids(ids0, st0, inc0, False, 1)
+    stream = torch.cuda.current_stream()
+    app = torch.empty(k, dtype=torch.uint8, device="cuda")
+    na = torch.zeros(1, dtype=torch.int32, device="cuda")
+    batches = [S.c3_updates(n, k, seed=50 + b, base_inc=inc0 + 3 * b) for b in range(nbatches)]
+    batches += [batches[-1]] * tail_noops  # re-applying the last batch changes nothing... mostly
+    for b, (ids, us, ui) in enumerate(batches):
+        d = [torch.from_numpy(ids.view(np.int32)).cuda(), torch.from_numpy(us).cuda(), torch.from_numpy(ui).cuda()]
+        m.update_dev(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), k, 1434500000000 + b, app.data_ptr(),
+                     None, None, na.data_ptr(), stream.cuda_stream)
+        o.update_ids(ids, us, ui, False, 1434500000000 + b)
+    torch.cuda.synchronize()
+    assert m.checksum == o.checksum
+    assert m.generate_checksum_string() == o.checksum_string()
