@@ -180,42 +180,105 @@ int rp_members_dump(rp_members *m, uint8_t *exists, uint8_t *status, int64_t *in
 int rp_members_count(rp_members *m, uint32_t *n_names);
 
 /* ------------------------------------------------------------------ Gossip wire bodies
- * Change records as the JSON text ringpop sends (device buffers; addresses are ids interned in
- * the members handle m). Replaces the per-message JSON.stringify / safeParse of:
- *   issueAs record {id, source, sourceIncarnationNumber, address, status, incarnationNumber}
- *                  (lib/gossip/dissemination.js:163-170)        form 0; d_ids (36 B each) nullable
+ * Change records as the JSON text ringpop sends (addresses are ids interned in the members
+ * handle m). Replaces the per-message JSON.stringify / safeParse of:
+ *   issueAs record  {id, source, sourceIncarnationNumber, address, status, incarnationNumber}
+ *                   (lib/gossip/dissemination.js:163-170)                                form 0
  *   fullSync record {source, address, status, incarnationNumber} (dissemination.js:64-73)  form 1
- *   body 0: bare changes array; 1: ping request {checksum, changes, source, sourceIncarnationNumber}
- *   (lib/gossip/ping-sender.js:71-76); 2: ping response {changes} (server/protocol/ping.js:45-48).
- * Encode: message j holds records [msg_rec_off[j], msg_rec_off[j+1]); d_out_off[0..n_msgs] gets
- * the byte offsets; with d_out null only the offsets are computed (size query). Synchronous. */
+ * and the bodies around them (RP_WIRE_BODY_*):
+ *   ARRAY             the bare changes array
+ *   PING              {checksum, changes, source, sourceIncarnationNumber}  lib/gossip/ping-sender.js:71-76
+ *   PING_RESPONSE     {changes}                                              server/protocol/ping.js:45-48
+ *   PINGREQ           {checksum, changes, source, sourceIncarnationNumber, target}
+ *                                                                    lib/gossip/ping-req-sender.js:75-81
+ *   PINGREQ_RESPONSE  {changes, pingStatus, target}                     server/protocol/ping-req.js:61-65
+ *   JOIN_RESPONSE     {app, coordinator, membership, membershipChecksum}  server/protocol/join.js:128-133
+ *                     (membership = the fullSync records; coordinator = the source column,
+ *                     membershipChecksum = the checksum column, app = one string for the batch)
+ * JSON.stringify leaves an undefined member out; per record: an ids row whose first byte is NUL,
+ * a src of RP_NULL_ID, a src_inc of INT64_MIN (or a null column) are absent and not written.
+ * Message j holds records [msg_rec_off[j], msg_rec_off[j+1]): msg_rec_off[0] = 0, not
+ * decreasing, msg_rec_off[n_msgs] = n_rec. Every id and offset is validated on the device before
+ * anything is written (RP_EINVAL otherwise). Encode writes d_out_off[0..n_msgs] (byte offsets);
+ * with d_out null only the offsets are computed (size query). Synchronous. */
+enum {
+    RP_WIRE_BODY_ARRAY = 0,
+    RP_WIRE_BODY_PING = 1,
+    RP_WIRE_BODY_PING_RESPONSE = 2,
+    RP_WIRE_BODY_PINGREQ = 3,
+    RP_WIRE_BODY_PINGREQ_RESPONSE = 4,
+    RP_WIRE_BODY_JOIN_RESPONSE = 5
+};
+typedef struct rp_wire_records {  /* n_rec entries each */
+    const uint32_t *addr, *src;     /* member ids (src: RP_NULL_ID = absent) */
+    const uint8_t *status;          /* 0 alive 1 suspect 2 faulty 3 leave */
+    const int64_t *inc, *src_inc;   /* incarnationNumber; sourceIncarnationNumber (INT64_MIN / null = absent) */
+    const uint8_t *ids;             /* 36-byte uuids per record, nullable */
+} rp_wire_records;
+typedef struct rp_wire_headers {  /* n_msgs entries each, as the body needs them */
+    const uint32_t *checksum;       /* PING, PINGREQ: checksum; JOIN_RESPONSE: membershipChecksum */
+    const uint32_t *source;         /* PING, PINGREQ: source; JOIN_RESPONSE: coordinator */
+    const int64_t *source_inc;      /* PING, PINGREQ: sourceIncarnationNumber */
+    const uint32_t *target;         /* PINGREQ, PINGREQ_RESPONSE: target */
+    const uint8_t *ping_status;     /* PINGREQ_RESPONSE: pingStatus (0 / 1) */
+    const char *app;                /* JOIN_RESPONSE: app (host string, app_len bytes, no escapes) */
+    uint32_t app_len;
+} rp_wire_headers;
+int rp_wire_encode_dev(rp_members *m, uint32_t n_msgs, const uint32_t *d_msg_rec_off, uint64_t n_rec,
+                       const rp_wire_records *d_recs, int form, int body, const rp_wire_headers *d_hdr,
+                       uint8_t *d_out, uint64_t *d_out_off, void *stream);
+/* Host-buffer form (staged through the handle's device; PCIe-bound; ids checked on the host):
+ * out NULL = size query (out_off filled); otherwise cap >= out_off[n_msgs]. */
+int rp_wire_encode(rp_members *m, uint32_t n_msgs, const uint32_t *msg_rec_off, const rp_wire_records *recs,
+                   int form, int body, const rp_wire_headers *hdr, uint8_t *out, uint64_t cap, uint64_t *out_off);
+
+/* Decode n_msgs JSON texts buf[msg_off[j] .. msg_off[j+1]) — a changes array, or a body object
+ * whose `changes` (join response: `membership`) member is one; any key order, JSON whitespace,
+ * unknown members skipped (server/protocol/ping.js:27-36 reads the same members). msg_rec_off[0..n_msgs]
+ * gets record offsets (total in [n_msgs]); records beyond rec_cap are counted, not written. Per
+ * record: address id (RP_NULL_ID if not interned; addr_off / addr_len give its bytes), source id
+ * (RP_NULL_ID: absent or not interned), status, incarnationNumber, sourceIncarnationNumber
+ * (INT64_MIN if absent), byte offset of `id` (~0 if absent). Per message: checksum /
+ * membershipChecksum, source / coordinator, sourceIncarnationNumber, target, pingStatus (0xFF if
+ * absent); err[j] = 0, or 1 + the failing byte's offset in message j (its records are then
+ * dropped). Strings with escapes and non-integral numbers are rejected (addresses and uuids
+ * never hold one). Every column except addr / status / inc is nullable. */
+typedef struct rp_wire_records_out {
+    uint32_t *addr, *src;
+    uint8_t *status;
+    int64_t *inc, *src_inc;
+    uint64_t *id_off, *addr_off;
+    uint32_t *addr_len;
+} rp_wire_records_out;
+typedef struct rp_wire_headers_out {
+    uint32_t *checksum, *source;
+    int64_t *source_inc;
+    uint32_t *target;
+    uint8_t *ping_status;
+} rp_wire_headers_out;
+int rp_wire_decode_dev(rp_members *m, const uint8_t *d_buf, const uint64_t *d_msg_off, uint32_t n_msgs,
+                       uint32_t *d_msg_rec_off, uint32_t rec_cap, const rp_wire_records_out *d_recs,
+                       const rp_wire_headers_out *d_hdr, uint64_t *d_err, void *stream);
+int rp_wire_decode(rp_members *m, const char *buf, const uint64_t *msg_off, uint32_t n_msgs, uint32_t *msg_rec_off,
+                   uint32_t rec_cap, const rp_wire_records_out *recs, const rp_wire_headers_out *hdr, uint64_t *err);
+
+/* The first round's column-list forms of the same codec (bodies 0..2). */
 int rp_wire_encode_changes_dev(rp_members *m, uint32_t n_msgs, const uint32_t *d_msg_rec_off, uint64_t n_rec,
                                const uint32_t *d_addr, const uint32_t *d_src, const uint8_t *d_status,
                                const int64_t *d_inc, const int64_t *d_src_inc, const uint8_t *d_ids, int form,
                                int body, const uint32_t *d_msg_checksum, const uint32_t *d_msg_source,
                                const int64_t *d_msg_source_inc, uint8_t *d_out, uint64_t *d_out_off, void *stream);
-/* Host-buffer form (staged through the handle's device; PCIe-bound): out NULL = size query
- * (out_off filled); otherwise cap >= out_off[n_msgs]. n_rec = msg_rec_off[n_msgs]. */
 int rp_wire_encode_changes(rp_members *m, uint32_t n_msgs, const uint32_t *msg_rec_off, const uint32_t *addr,
                            const uint32_t *src, const uint8_t *status, const int64_t *inc, const int64_t *src_inc,
                            const uint8_t *ids, int form, int body, const uint32_t *msg_checksum,
                            const uint32_t *msg_source, const int64_t *msg_source_inc, uint8_t *out, uint64_t cap,
                            uint64_t *out_off);
-/* Decode n_msgs JSON texts d_buf[d_msg_off[j] .. d_msg_off[j+1]) — a changes array, or a body
- * object whose `changes` member is one (server/protocol/ping.js:27-36 reads the same members).
- * d_msg_rec_off[0..n_msgs] gets record offsets (total in [n_msgs]); records beyond rec_cap are
- * counted, not written. Per record: address id (0xFFFFFFFF if not interned; d_addr_off/len give
- * its bytes), source id, status, incarnationNumber, sourceIncarnationNumber (INT64_MIN if absent),
- * byte offset of `id` (~0 if absent). d_err[j] = 0, or 1 + the failing byte's offset in message j
- * (its records are then dropped). Nullable: d_src, d_src_inc, d_id_off, d_addr_off, d_addr_len and
- * the three d_msg_* header columns. */
 int rp_wire_decode_changes_dev(rp_members *m, const uint8_t *d_buf, const uint64_t *d_msg_off, uint32_t n_msgs,
                                uint32_t *d_msg_rec_off, uint32_t rec_cap, uint32_t *d_addr, uint32_t *d_src,
                                uint8_t *d_status, int64_t *d_inc, int64_t *d_src_inc, uint64_t *d_id_off,
                                uint64_t *d_addr_off, uint32_t *d_addr_len, uint64_t *d_err,
                                uint32_t *d_msg_checksum, uint32_t *d_msg_source, int64_t *d_msg_source_inc,
                                void *stream);
-/* Host-buffer form of the decoder (record columns nullable; at most rec_cap records copied). */
 int rp_wire_decode_changes(rp_members *m, const char *buf, const uint64_t *msg_off, uint32_t n_msgs,
                            uint32_t *msg_rec_off, uint32_t rec_cap, uint32_t *addr, uint32_t *src, uint8_t *status,
                            int64_t *inc, int64_t *src_inc, uint64_t *err);

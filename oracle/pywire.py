@@ -15,10 +15,13 @@ def _dumps(o):
 
 
 def issue_as_record(id_, source, source_inc, address, status, inc):
-    """dissemination.js:163-170 (an undefined id is dropped, as JSON.stringify does)."""
+    """dissemination.js:163-170 (an undefined member is dropped, as JSON.stringify does)."""
     r = {"id": id_} if id_ is not None else {}
-    r.update(source=source, sourceIncarnationNumber=source_inc, address=address, status=status,
-             incarnationNumber=inc)
+    if source is not None:
+        r["source"] = source
+    if source_inc is not None:
+        r["sourceIncarnationNumber"] = source_inc
+    r.update(address=address, status=status, incarnationNumber=inc)
     return r
 
 
@@ -27,16 +30,27 @@ def full_sync_record(source, address, status, inc):
     return {"source": source, "address": address, "status": status, "incarnationNumber": inc}
 
 
-def body(changes, kind="array", checksum=None, source=None, source_inc=None):
+def body(changes, kind="array", checksum=None, source=None, source_inc=None, target=None, ping_status=None,
+         app=None):
     if kind == "ping":  # ping-sender.js:71-76
         return _dumps({"checksum": checksum, "changes": changes, "source": source,
                        "sourceIncarnationNumber": source_inc})
     if kind == "pingResponse":  # server/protocol/ping.js:45-48
         return _dumps({"changes": changes})
+    if kind == "pingReq":  # ping-req-sender.js:75-81
+        return _dumps({"checksum": checksum, "changes": changes, "source": source,
+                       "sourceIncarnationNumber": source_inc, "target": target})
+    if kind == "pingReqResponse":  # server/protocol/ping-req.js:61-65
+        return _dumps({"changes": changes, "pingStatus": bool(ping_status), "target": target})
+    if kind == "joinResponse":  # server/protocol/join.js:128-133 (membership = fullSync records)
+        return _dumps({"app": app, "coordinator": source, "membership": changes, "membershipChecksum": checksum})
     return _dumps(changes)
 
 
 def decode(text):
-    """The changes of a body or a bare array (server/protocol/ping.js:27-36 reads `changes`)."""
+    """The changes of a body or a bare array (server/protocol/ping.js:27-36 reads `changes`; a
+    join response carries them as `membership`)."""
     o = json.loads(text)
-    return o if isinstance(o, list) else o["changes"]
+    if isinstance(o, list):
+        return o
+    return o["membership"] if "membership" in o else o["changes"]

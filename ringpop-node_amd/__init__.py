@@ -109,6 +109,10 @@ SIGNATURES = {
     "rp_sim_create_scenario": (_INT, [_U32, _P, _P, _P, _P, _U32, _U32, ctypes.c_int64, _INT, _P, _U32, _U32, _P, _U32,
                                       _P]),
     "rp_sim_piggyback": (_INT, [_P, _P]),
+    "rp_wire_encode_dev": (_INT, [_P, _U32, _P, _U64, _P, _INT, _INT, _P, _P, _P, _P]),
+    "rp_wire_encode": (_INT, [_P, _U32, _P, _P, _INT, _INT, _P, _P, _U64, _P]),
+    "rp_wire_decode_dev": (_INT, [_P, _P, _P, _U32, _P, _U32, _P, _P, _P, _P]),
+    "rp_wire_decode": (_INT, [_P, _P, _P, _U32, _P, _U32, _P, _P, _P]),
     "rp_sim_counters": (_INT, [_P, _P]),
     "rp_members_defer_checksum": (_INT, [_P, _INT]),
     "rp_copy": (_INT, [_P, _P, _U64, _P]),
@@ -992,46 +996,74 @@ class DistGossipSim:
 # ping bodies ping-sender.js:71-76 and server/protocol/ping.js:45-48. torch is only the device
 # buffer plumbing here.
 WIRE_FORM = {"issueAs": 0, "fullSync": 1}
-WIRE_BODY = {"array": 0, "ping": 1, "pingResponse": 2}
+WIRE_BODY = {"array": 0, "ping": 1, "pingResponse": 2, "pingReq": 3, "pingReqResponse": 4, "joinResponse": 5}
+INT64_MIN = -(1 << 63)
+
+
+class WireRecords(ctypes.Structure):
+    """rp_wire_records (include/ringpop_amd.h)."""
+    _fields_ = [("addr", _P), ("src", _P), ("status", _P), ("inc", _P), ("src_inc", _P), ("ids", _P)]
+
+
+class WireHeaders(ctypes.Structure):
+    """rp_wire_headers."""
+    _fields_ = [("checksum", _P), ("source", _P), ("source_inc", _P), ("target", _P), ("ping_status", _P),
+                ("app", ctypes.c_char_p), ("app_len", _U32)]
+
+
+class WireRecordsOut(ctypes.Structure):
+    """rp_wire_records_out."""
+    _fields_ = [("addr", _P), ("src", _P), ("status", _P), ("inc", _P), ("src_inc", _P), ("id_off", _P),
+                ("addr_off", _P), ("addr_len", _P)]
+
+
+class WireHeadersOut(ctypes.Structure):
+    """rp_wire_headers_out."""
+    _fields_ = [("checksum", _P), ("source", _P), ("source_inc", _P), ("target", _P), ("ping_status", _P)]
 
 
 def _dev(a, dtype):
     import torch
-    return torch.from_numpy(np.ascontiguousarray(a, dtype=dtype)).cuda()
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=dtype).copy()).cuda()
 
 
 def wire_encode(members, msg_rec_off, addr, src, status, inc, src_inc=None, ids=None, form="issueAs",
-                body="array", msg_checksum=None, msg_source=None, msg_source_inc=None):
+                body="array", msg_checksum=None, msg_source=None, msg_source_inc=None, msg_target=None,
+                msg_ping_status=None, app=None):
     """Encode message j = records [msg_rec_off[j], msg_rec_off[j+1]) on the device; returns
-    (bytes, out_off) on the host. addr/src/msg_source are ids interned in `members`; ids is an
-    (n_rec, 36) uint8 array of uuid strings or None (id omitted)."""
+    (bytes, out_off) on the host. addr/src/msg_source/msg_target are ids interned in `members`
+    (src NULL_ID = no source member); src_inc None or INT64_MIN entries = absent; ids is an
+    (n_rec, 36) uint8 array of uuid strings (a row starting with 0 = absent) or None."""
     import torch
     n_msgs = len(msg_rec_off) - 1
     n_rec = len(addr)
-    z64 = np.zeros(max(n_rec, 1), dtype=np.int64)
     d = dict(off=_dev(msg_rec_off, np.uint32), addr=_dev(addr if n_rec else [0], np.uint32),
              src=_dev(src if n_rec else [0], np.uint32), st=_dev(status if n_rec else [0], np.uint8),
-             inc=_dev(inc if n_rec else [0], np.int64),
-             sinc=_dev(src_inc if src_inc is not None and n_rec else z64, np.int64))
-    d_ids = _dev(np.asarray(ids, dtype=np.uint8).reshape(-1), np.uint8) if ids is not None and n_rec else None
-    hdr = [None, None, None]
-    if WIRE_BODY[body] == 1:
-        hdr = [_dev(msg_checksum, np.uint32), _dev(msg_source, np.uint32), _dev(msg_source_inc, np.int64)]
-    out_off = torch.zeros(n_msgs + 1, dtype=torch.int64, device="cuda")
+             inc=_dev(inc if n_rec else [0], np.int64))
+    d["sinc"] = _dev(src_inc, np.int64) if src_inc is not None and n_rec else None
+    d["ids"] = _dev(np.asarray(ids, dtype=np.uint8).reshape(-1), np.uint8) if ids is not None and n_rec else None
+    col = lambda x, dt: None if x is None or n_msgs == 0 else _dev(x, dt)  # noqa: E731
+    h = dict(ck=col(msg_checksum, np.uint32), ms=col(msg_source, np.uint32), msi=col(msg_source_inc, np.int64),
+             tg=col(msg_target, np.uint32), ps=col(msg_ping_status, np.uint8))
     p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
-    args = [members._h, n_msgs, p(d["off"]), n_rec, p(d["addr"]), p(d["src"]), p(d["st"]), p(d["inc"]),
-            p(d["sinc"]), p(d_ids), WIRE_FORM[form], WIRE_BODY[body], p(hdr[0]), p(hdr[1]), p(hdr[2])]
-    check(lib().rp_wire_encode_changes_dev(*args, None, out_off.data_ptr(), None))
+    recs = WireRecords(p(d["addr"]), p(d["src"]), p(d["st"]), p(d["inc"]), p(d["sinc"]), p(d["ids"]))
+    appb = (app.encode() if isinstance(app, str) else app) if app is not None else None
+    hdr = WireHeaders(p(h["ck"]), p(h["ms"]), p(h["msi"]), p(h["tg"]), p(h["ps"]), appb, len(appb or b""))
+    stream = torch.cuda.current_stream().cuda_stream
+    out_off = torch.empty(n_msgs + 1, dtype=torch.int64, device="cuda")
+    args = [members._h, n_msgs, p(d["off"]), n_rec, ctypes.byref(recs), WIRE_FORM[form], WIRE_BODY[body],
+            ctypes.byref(hdr)]
+    check(lib().rp_wire_encode_dev(*args, None, out_off.data_ptr(), stream))
     total = int(out_off[-1].item())
     out = torch.empty(max(total, 1), dtype=torch.uint8, device="cuda")
-    check(lib().rp_wire_encode_changes_dev(*args, out.data_ptr(), out_off.data_ptr(), None))
+    check(lib().rp_wire_encode_dev(*args, out.data_ptr(), out_off.data_ptr(), stream))
     return out[:total].cpu().numpy().tobytes(), out_off.cpu().numpy().astype(np.uint64)
 
 
 def wire_decode(members, texts):
-    """Decode JSON texts (changes arrays or ping bodies) on the device. Returns a dict of numpy
-    columns: rec_off, addr, src, status, inc, src_inc, id_off, addr_off, addr_len, err and the
-    per-message checksum / source / source_inc."""
+    """Decode JSON texts (changes arrays or any of the bodies) on the device. Returns a dict of
+    numpy columns: rec_off, addr, src, status, inc, src_inc, id_off, addr_off, addr_len, err and
+    the per-message checksum / source / source_inc / target / ping_status."""
     import torch
     texts = [t.encode() if isinstance(t, str) else bytes(t) for t in texts]
     n = len(texts)
@@ -1041,19 +1073,24 @@ def wire_decode(members, texts):
     d_off = _dev(off, np.uint64)
     cap = max(sum(t.count(b"{") for t in texts), 1)
     e = lambda dt, k=cap: torch.empty(k, dtype=dt, device="cuda")  # noqa: E731
+    m1 = max(n, 1)
     c = dict(rec_off=e(torch.int32, n + 1), addr=e(torch.int32), src=e(torch.int32), status=e(torch.uint8),
              inc=e(torch.int64), src_inc=e(torch.int64), id_off=e(torch.int64), addr_off=e(torch.int64),
-             addr_len=e(torch.int32), err=e(torch.int64, max(n, 1)), checksum=e(torch.int32, max(n, 1)),
-             source=e(torch.int32, max(n, 1)), source_inc=e(torch.int64, max(n, 1)))
+             addr_len=e(torch.int32), err=e(torch.int64, m1), checksum=e(torch.int32, m1),
+             source=e(torch.int32, m1), source_inc=e(torch.int64, m1), target=e(torch.int32, m1),
+             ping_status=e(torch.uint8, m1))
     p = {k: v.data_ptr() for k, v in c.items()}
-    check(lib().rp_wire_decode_changes_dev(members._h, buf.data_ptr(), d_off.data_ptr(), n, p["rec_off"], cap,
-                                           p["addr"], p["src"], p["status"], p["inc"], p["src_inc"], p["id_off"],
-                                           p["addr_off"], p["addr_len"], p["err"], p["checksum"], p["source"],
-                                           p["source_inc"], None))
+    recs = WireRecordsOut(p["addr"], p["src"], p["status"], p["inc"], p["src_inc"], p["id_off"], p["addr_off"],
+                          p["addr_len"])
+    hdr = WireHeadersOut(p["checksum"], p["source"], p["source_inc"], p["target"], p["ping_status"])
+    check(lib().rp_wire_decode_dev(members._h, buf.data_ptr(), d_off.data_ptr(), n, p["rec_off"], cap,
+                                   ctypes.byref(recs), ctypes.byref(hdr), p["err"],
+                                   torch.cuda.current_stream().cuda_stream))
     h = {k: v.cpu().numpy() for k, v in c.items()}
     k = int(h["rec_off"][n])
     u32 = lambda a: a.view(np.uint32)  # noqa: E731
     return dict(rec_off=u32(h["rec_off"]), addr=u32(h["addr"])[:k], src=u32(h["src"])[:k], status=h["status"][:k],
                 inc=h["inc"][:k], src_inc=h["src_inc"][:k], id_off=h["id_off"][:k].view(np.uint64),
                 addr_off=h["addr_off"][:k], addr_len=h["addr_len"][:k], err=h["err"][:n],
-                checksum=u32(h["checksum"])[:n], source=u32(h["source"])[:n], source_inc=h["source_inc"][:n])
+                checksum=u32(h["checksum"])[:n], source=u32(h["source"])[:n], source_inc=h["source_inc"][:n],
+                target=u32(h["target"])[:n], ping_status=h["ping_status"][:n])

@@ -3,17 +3,24 @@
 // Encoder: one message = one list of change records, written as the bytes JSON.stringify
 // produces for
 //   issueAs records      {id, source, sourceIncarnationNumber, address, status, incarnationNumber}
-//                        (lib/gossip/dissemination.js:163-170; `id` dropped when absent, as
-//                        JSON.stringify drops an undefined member)
+//                        (lib/gossip/dissemination.js:163-170; JSON.stringify drops an undefined
+//                        member: per record, an id row starting with NUL, a source of NULL_ID or a
+//                        sourceIncarnationNumber of INT64_MIN is left out)
 //   fullSync records     {source, address, status, incarnationNumber} (dissemination.js:64-73)
-// wrapped as a bare array, a ping request body {checksum, changes, source, sourceIncarnationNumber}
-// (lib/gossip/ping-sender.js:71-76) or a ping response body {changes} (server/protocol/ping.js:45-48).
+// wrapped as a body (RP_WIRE_BODY_*): a bare array; a ping request {checksum, changes, source,
+// sourceIncarnationNumber} (lib/gossip/ping-sender.js:71-76); a ping response {changes}
+// (server/protocol/ping.js:45-48); a ping-req request {checksum, changes, source,
+// sourceIncarnationNumber, target} (lib/gossip/ping-req-sender.js:75-81); a ping-req response
+// {changes, pingStatus, target} (server/protocol/ping-req.js:61-65); a join response {app,
+// coordinator, membership, membershipChecksum} (server/protocol/join.js:128-133; membership =
+// fullSync records). Ids and offsets are validated on the device before anything is written.
 // Three passes over thread-per-record / thread-per-message grids: record lengths -> scans ->
 // records written at their final offsets (the same emit routine measures and writes, so
 // lengths and bytes cannot disagree).
 //
-// Decoder: one thread per message parses a changes array, or a body object whose `changes`
-// member is that array (other members skipped; checksum / source / sourceIncarnationNumber
+// Decoder: one thread per message parses a changes array, or a body object whose `changes` (or a
+// join response's `membership`) member is that array (other members skipped; checksum /
+// membershipChecksum, source / coordinator, sourceIncarnationNumber, target, pingStatus
 // captured), into per-record columns with addresses interned against the members' name table
 // by binary search over its byte-ordered ids. Strings with escapes are rejected (addresses and
 // uuids never hold one), numbers must be integral. Count pass -> scan -> fill pass.
@@ -69,6 +76,11 @@ struct Sink {
             for (uint32_t i = 0; i < k; i++) out[n + i] = status_char(s, i);
         n += k;
     }
+    __device__ void str(const Names& nm, uint32_t id) {  // "name"
+        lit("\"");
+        name(nm, id);
+        lit("\"");
+    }
 };
 
 struct Recs {
@@ -82,23 +94,29 @@ struct Recs {
 };
 
 __device__ void emit_record(Sink& s, const Names& nm, const Recs& R, uint64_t r) {
+    s.lit("{");
     if (R.form == 0) {
-        if (R.ids) {
-            s.lit("{\"id\":\"");
+        if (R.ids && R.ids[r * 36] != 0) {
+            s.lit("\"id\":\"");
             s.bytes(R.ids + r * 36, 36);
-            s.lit("\",\"source\":\"");
-        } else {
-            s.lit("{\"source\":\"");
+            s.lit("\",");
         }
-        s.name(nm, R.src[r]);
-        s.lit("\",\"sourceIncarnationNumber\":");
-        s.num(R.src_inc[r]);
-        s.lit(",\"address\":\"");
-    } else {
-        s.lit("{\"source\":\"");
-        s.name(nm, R.src[r]);
-        s.lit("\",\"address\":\"");
+        if (R.src[r] != NULL_ID) {
+            s.lit("\"source\":");
+            s.str(nm, R.src[r]);
+            s.lit(",");
+        }
+        if (R.src_inc && R.src_inc[r] != LLONG_MIN) {
+            s.lit("\"sourceIncarnationNumber\":");
+            s.num(R.src_inc[r]);
+            s.lit(",");
+        }
+    } else if (R.src[r] != NULL_ID) {
+        s.lit("\"source\":");
+        s.str(nm, R.src[r]);
+        s.lit(",");
     }
+    s.lit("\"address\":\"");
     s.name(nm, R.addr[r]);
     s.lit("\",\"status\":\"");
     s.status(R.status[r]);
@@ -107,37 +125,96 @@ __device__ void emit_record(Sink& s, const Names& nm, const Recs& R, uint64_t r)
     s.lit("}");
 }
 
+enum Body : int { B_ARRAY = 0, B_PING = 1, B_PING_RESP = 2, B_PINGREQ = 3, B_PINGREQ_RESP = 4, B_JOIN_RESP = 5 };
+
 struct Msgs {
     const uint32_t* rec_off;  // n+1
-    const uint32_t* checksum;
-    const uint32_t* source;
-    const int64_t* source_inc;
-    int body;  // 0 array, 1 ping request, 2 ping response
+    const uint32_t* checksum;     // ping, ping-req: checksum; join response: membershipChecksum
+    const uint32_t* source;       // ping, ping-req: source; join response: coordinator
+    const int64_t* source_inc;    // ping, ping-req: sourceIncarnationNumber
+    const uint32_t* target;       // ping-req request / response: target
+    const uint8_t* ping_status;   // ping-req response: pingStatus
+    const uint8_t* app;           // join response: the app name (one for the batch)
+    uint32_t app_len;
+    int body;
 };
 
-__device__ void emit_head(Sink& s, const Msgs& M, uint32_t m) {
-    if (M.body == 1) {
+__device__ void emit_head(Sink& s, const Names& nm, const Msgs& M, uint32_t m) {
+    switch (M.body) {
+    case B_PING:
+    case B_PINGREQ:
         s.lit("{\"checksum\":");
         s.num((int64_t)M.checksum[m]);
         s.lit(",\"changes\":[");
-    } else if (M.body == 2) {
+        break;
+    case B_PING_RESP:
+    case B_PINGREQ_RESP:
         s.lit("{\"changes\":[");
-    } else {
+        break;
+    case B_JOIN_RESP:
+        s.lit("{\"app\":\"");
+        s.bytes(M.app, M.app_len);
+        s.lit("\",\"coordinator\":");
+        s.str(nm, M.source[m]);
+        s.lit(",\"membership\":[");
+        break;
+    default:
         s.lit("[");
     }
 }
 
 __device__ void emit_tail(Sink& s, const Names& nm, const Msgs& M, uint32_t m) {
-    if (M.body == 1) {
-        s.lit("],\"source\":\"");
-        s.name(nm, M.source[m]);
-        s.lit("\",\"sourceIncarnationNumber\":");
+    switch (M.body) {
+    case B_PING:
+    case B_PINGREQ:
+        s.lit("],\"source\":");
+        s.str(nm, M.source[m]);
+        s.lit(",\"sourceIncarnationNumber\":");
         s.num(M.source_inc[m]);
+        if (M.body == B_PINGREQ) {
+            s.lit(",\"target\":");
+            s.str(nm, M.target[m]);
+        }
         s.lit("}");
-    } else if (M.body == 2) {
+        break;
+    case B_PING_RESP:
         s.lit("]}");
-    } else {
+        break;
+    case B_PINGREQ_RESP:
+        s.lit("],\"pingStatus\":");
+        s.lit(M.ping_status[m] ? "true" : "false");
+        s.lit(",\"target\":");
+        s.str(nm, M.target[m]);
+        s.lit("}");
+        break;
+    case B_JOIN_RESP:
+        s.lit("],\"membershipChecksum\":");
+        s.num((int64_t)M.checksum[m]);
+        s.lit("}");
+        break;
+    default:
         s.lit("]");
+    }
+}
+
+// Everything the encoder indexes with, checked before it writes: *bad = 1 + the first failing
+// kind (1 offsets, 2 record address, 3 record source, 4 status, 5 message source / coordinator,
+// 6 target).
+__global__ void k_validate(Names nm, Recs R, Msgs M, uint32_t n_msgs, uint64_t n_rec, uint32_t* bad) {
+    const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x, gs = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t m = g; m <= n_msgs; m += gs) {
+        const bool ok = m == 0 ? M.rec_off[0] == 0
+                               : M.rec_off[m] >= M.rec_off[m - 1] && (m < n_msgs || M.rec_off[m] == n_rec);
+        if (!ok) atomicMin(bad, 2u);
+        if (m == n_msgs) continue;
+        const bool src_used = M.body == B_PING || M.body == B_PINGREQ || M.body == B_JOIN_RESP;
+        if (src_used && M.source[m] >= nm.n) atomicMin(bad, 6u);
+        if ((M.body == B_PINGREQ || M.body == B_PINGREQ_RESP) && M.target[m] >= nm.n) atomicMin(bad, 7u);
+    }
+    for (uint64_t r = g; r < n_rec; r += gs) {
+        if (R.addr[r] >= nm.n) atomicMin(bad, 3u);
+        if (R.src[r] >= nm.n && R.src[r] != NULL_ID) atomicMin(bad, 4u);
+        if (R.status[r] > 3) atomicMin(bad, 5u);
     }
 }
 
@@ -163,7 +240,7 @@ __global__ void k_rec_len(Names nm, Recs R, Msgs M, uint32_t n_msgs, uint64_t n_
 __global__ void k_msg_len(Names nm, Msgs M, uint32_t n_msgs, const uint32_t* rec_scan, uint32_t* mlen) {
     for (uint32_t m = blockIdx.x * blockDim.x + threadIdx.x; m < n_msgs; m += gridDim.x * blockDim.x) {
         Sink s{nullptr};
-        emit_head(s, M, m);
+        emit_head(s, nm, M, m);
         emit_tail(s, nm, M, m);
         mlen[m] = s.n + rec_scan[M.rec_off[m + 1]] - rec_scan[M.rec_off[m]];
     }
@@ -175,7 +252,7 @@ __global__ void k_msg_write(Names nm, Msgs M, uint32_t n_msgs, const uint32_t* m
         out_off[m] = moff[m];
         if (m == n_msgs || !out) continue;
         Sink h{out + moff[m]};
-        emit_head(h, M, m);
+        emit_head(h, nm, M, m);
         Sink t{out + moff[m] + h.n + rec_scan[M.rec_off[m + 1]] - rec_scan[M.rec_off[m]]};
         emit_tail(t, nm, M, m);
     }
@@ -186,7 +263,7 @@ __global__ void k_rec_write(Names nm, Recs R, Msgs M, uint32_t n_msgs, uint64_t 
     for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n_rec; r += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t m = msg_of(M.rec_off, n_msgs, r);
         Sink h{nullptr};
-        emit_head(h, M, m);
+        emit_head(h, nm, M, m);
         uint8_t* p = out + moff[m] + h.n + (rec_scan[r] - rec_scan[M.rec_off[m]]);
         Sink s{p};
         emit_record(s, nm, R, r);
@@ -214,7 +291,7 @@ __global__ __launch_bounds__(kWrThreads) void k_rec_write_lds(Names nm, Recs R, 
         if (r < n_rec) {
             const uint32_t m = msg_of(M.rec_off, n_msgs, r);
             Sink h{nullptr};
-            emit_head(h, M, m);
+            emit_head(h, nm, M, m);
             dst = moff[m] + h.n + (rec_scan[r] - rec_scan[M.rec_off[m]]);
             const uint32_t full = rec_scan[r + 1] - rec_scan[r];
             const bool comma = r + 1 < M.rec_off[m + 1];
@@ -258,6 +335,8 @@ struct Out {
     uint32_t* m_checksum;
     uint32_t* m_source;
     int64_t* m_source_inc;
+    uint32_t* m_target;
+    uint8_t* m_ping_status;  // 0 false, 1 true, 0xFF absent
 };
 
 __device__ int name_cmp(const Names& nm, const uint8_t* s, uint32_t len, uint32_t id) {
@@ -326,6 +405,20 @@ struct Parser {
         if (i >= end) { fail(); len = 0; return; }
         len = (uint32_t)(i - s0);
         i++;
+    }
+    // true / false (1 / 0)
+    __device__ uint8_t boolean() {
+        ws();
+        if (i + 4 <= end && p[i] == 't' && p[i + 1] == 'r' && p[i + 2] == 'u' && p[i + 3] == 'e') {
+            i += 4;
+            return 1;
+        }
+        if (i + 5 <= end && p[i] == 'f' && p[i + 1] == 'a' && p[i + 2] == 'l' && p[i + 3] == 's' && p[i + 4] == 'e') {
+            i += 5;
+            return 0;
+        }
+        fail();
+        return 0;
     }
     __device__ int64_t integer() {
         ws();
@@ -467,8 +560,9 @@ __global__ void k_decode(In I, Names nm, Out O, uint32_t n_msgs) {
         const uint64_t kend = FILL ? O.rec_off[m + 1] : 0;
         uint32_t n = 0;
         bool seen = false;
-        uint32_t ck = 0, msrc = NULL_ID;
+        uint32_t ck = 0, msrc = NULL_ID, mtgt = NULL_ID;
         int64_t msinc = LLONG_MIN;
+        uint8_t pst = 0xFF;
         if (P.peek('[')) {
             n = parse_changes<FILL>(P, nm, O, k0, kend);
             seen = true;
@@ -482,17 +576,23 @@ __global__ void k_decode(In I, Names nm, Out O, uint32_t n_msgs) {
                     P.expect(':');
                     if (P.bad) break;
                     const uint8_t* key = P.p + ks;
-                    if (key_is(key, kl, "changes")) {
+                    if (key_is(key, kl, "changes") || key_is(key, kl, "membership")) {
                         n = parse_changes<FILL>(P, nm, O, k0, kend);
                         seen = true;
-                    } else if (key_is(key, kl, "checksum")) {
+                    } else if (key_is(key, kl, "checksum") || key_is(key, kl, "membershipChecksum")) {
                         ck = (uint32_t)P.integer();
-                    } else if (key_is(key, kl, "source")) {
+                    } else if (key_is(key, kl, "source") || key_is(key, kl, "coordinator")) {
                         uint64_t so; uint32_t sl;
                         P.str(so, sl);
                         if (FILL && !P.bad) msrc = name_find(nm, P.p + so, sl);
                     } else if (key_is(key, kl, "sourceIncarnationNumber")) {
                         msinc = P.integer();
+                    } else if (key_is(key, kl, "target")) {
+                        uint64_t so; uint32_t sl;
+                        P.str(so, sl);
+                        if (FILL && !P.bad) mtgt = name_find(nm, P.p + so, sl);
+                    } else if (key_is(key, kl, "pingStatus")) {
+                        pst = P.boolean();
                     } else {
                         P.skip_value();
                     }
@@ -512,6 +612,8 @@ __global__ void k_decode(In I, Names nm, Out O, uint32_t n_msgs) {
             if (O.m_checksum) O.m_checksum[m] = ck;
             if (O.m_source) O.m_source[m] = msrc;
             if (O.m_source_inc) O.m_source_inc[m] = msinc;
+            if (O.m_target) O.m_target[m] = mtgt;
+            if (O.m_ping_status) O.m_ping_status[m] = pst;
         }
     }
 }
@@ -530,33 +632,61 @@ Names names_of(NameTable& nt, hipStream_t st, Scratch& ws) {
 
 using rp::guard;
 
+namespace {
+const char* const kBad[] = {"", "message record offsets must start at 0, not decrease and end at n_rec",
+                            "a record's address is not an interned id", "a record's source is not an interned id",
+                            "a record's status is not 0..3", "a message's source / coordinator is not an interned id",
+                            "a message's target is not an interned id"};
+}  // namespace
+
 extern "C" {
 
-int rp_wire_encode_changes_dev(rp_members* m, uint32_t n_msgs, const uint32_t* d_msg_rec_off, uint64_t n_rec,
-                               const uint32_t* d_addr, const uint32_t* d_src, const uint8_t* d_status,
-                               const int64_t* d_inc, const int64_t* d_src_inc, const uint8_t* d_ids, int form,
-                               int body, const uint32_t* d_msg_checksum, const uint32_t* d_msg_source,
-                               const int64_t* d_msg_source_inc, uint8_t* d_out, uint64_t* d_out_off, void* stream) {
+int rp_wire_encode_dev(rp_members* m, uint32_t n_msgs, const uint32_t* d_msg_rec_off, uint64_t n_rec,
+                       const rp_wire_records* recs, int form, int body, const rp_wire_headers* hdr, uint8_t* d_out,
+                       uint64_t* d_out_off, void* stream) {
     return guard([&] {
         RP_REQUIRE(m, "null members handle");
         RP_REQUIRE(form == 0 || form == 1, "form must be 0 (issueAs) or 1 (fullSync)");
-        RP_REQUIRE(body >= 0 && body <= 2, "body must be 0 (array), 1 (ping request) or 2 (ping response)");
+        RP_REQUIRE(body >= RP_WIRE_BODY_ARRAY && body <= RP_WIRE_BODY_JOIN_RESPONSE, "unknown body");
         RP_REQUIRE(d_msg_rec_off && d_out_off, "null offsets");
-        RP_REQUIRE(n_rec == 0 || (d_addr && d_src && d_status && d_inc), "null record column");
-        RP_REQUIRE(n_rec == 0 || form == 1 || d_src_inc, "issueAs records need sourceIncarnationNumber");
-        RP_REQUIRE(body != 1 || (d_msg_checksum && d_msg_source && d_msg_source_inc), "ping body needs header columns");
+        const rp_wire_records R0 = recs ? *recs : rp_wire_records{};
+        const rp_wire_headers H0 = hdr ? *hdr : rp_wire_headers{};
+        RP_REQUIRE(n_rec == 0 || (R0.addr && R0.src && R0.status && R0.inc), "null record column");
+        const bool need_src = body == RP_WIRE_BODY_PING || body == RP_WIRE_BODY_PINGREQ ||
+                              body == RP_WIRE_BODY_JOIN_RESPONSE;
+        RP_REQUIRE(n_msgs == 0 || !need_src || (H0.source && H0.checksum), "this body needs source and checksum columns");
+        RP_REQUIRE(n_msgs == 0 || !(body == RP_WIRE_BODY_PING || body == RP_WIRE_BODY_PINGREQ) || H0.source_inc,
+                   "this body needs the sourceIncarnationNumber column");
+        RP_REQUIRE(n_msgs == 0 || !(body == RP_WIRE_BODY_PINGREQ || body == RP_WIRE_BODY_PINGREQ_RESPONSE) || H0.target,
+                   "this body needs the target column");
+        RP_REQUIRE(n_msgs == 0 || body != RP_WIRE_BODY_PINGREQ_RESPONSE || H0.ping_status,
+                   "the ping-req response needs the pingStatus column");
+        RP_REQUIRE(body != RP_WIRE_BODY_JOIN_RESPONSE || H0.app || H0.app_len == 0, "null app");
         hipStream_t hst;
         rp::Scratch* ws;
         rp::NameTable& nt = rp::members_names(m, &hst, &ws);
         hipStream_t st = stream ? rp::as_stream(stream) : hst;
         // every byte offset fits u32: bound the worst case on the host
         const uint64_t rec_max = 180 + 2ull * nt.max_len;
-        RP_REQUIRE(n_rec * rec_max + (uint64_t)n_msgs * (80 + nt.max_len) < 0xFFFFFFFFull,
+        RP_REQUIRE(n_rec * rec_max + (uint64_t)n_msgs * (120 + 2ull * nt.max_len + H0.app_len) < 0xFFFFFFFFull,
                    "encoded batch may exceed 4 GiB: split it");
         rp::Names nm = rp::names_of(nt, st, *ws);
-        rp::Recs R{d_addr, d_src, d_status, d_inc, d_src_inc, d_ids, form};
-        rp::Msgs M{d_msg_rec_off, d_msg_checksum, d_msg_source, d_msg_source_inc, body};
-        rp::DevBuf<uint32_t> rscan, mscan;
+        rp::DevBuf<uint8_t> app;
+        app.reserve(H0.app_len + 1);
+        if (H0.app_len) RP_HIP(hipMemcpyAsync(app.p, H0.app, H0.app_len, hipMemcpyHostToDevice, st));
+        rp::Recs R{R0.addr, R0.src, R0.status, R0.inc, R0.src_inc, R0.ids, form};
+        rp::Msgs M{d_msg_rec_off, H0.checksum, H0.source, H0.source_inc, H0.target, H0.ping_status, app.p,
+                   H0.app_len, body};
+        rp::DevBuf<uint32_t> rscan, mscan, bad;
+        bad.reserve(1);
+        RP_HIP(hipMemsetAsync(bad.p, 0xFF, 4, st));
+        hipLaunchKernelGGL(rp::k_validate, dim3(rp::grid_for(std::max<uint64_t>(n_rec, (uint64_t)n_msgs + 1), 256, 4096)),
+                           dim3(256), 0, st, nm, R, M, n_msgs, n_rec, bad.p);
+        RP_HIP(hipGetLastError());
+        uint32_t b = 0;
+        RP_HIP(hipMemcpyAsync(&b, bad.p, 4, hipMemcpyDeviceToHost, st));
+        RP_HIP(hipStreamSynchronize(st));
+        if (b != 0xFFFFFFFFu) throw rp::Error(rp::RP_EINVAL, std::string("wire encode: ") + kBad[b - 1]);
         rscan.reserve(n_rec + 1);
         mscan.reserve((uint64_t)n_msgs + 1);
         if (n_rec) {
@@ -583,24 +713,23 @@ int rp_wire_encode_changes_dev(rp_members* m, uint32_t n_msgs, const uint32_t* d
     });
 }
 
-int rp_wire_decode_changes_dev(rp_members* m, const uint8_t* d_buf, const uint64_t* d_msg_off, uint32_t n_msgs,
-                               uint32_t* d_msg_rec_off, uint32_t rec_cap, uint32_t* d_addr, uint32_t* d_src,
-                               uint8_t* d_status, int64_t* d_inc, int64_t* d_src_inc, uint64_t* d_id_off,
-                               uint64_t* d_addr_off, uint32_t* d_addr_len, uint64_t* d_err,
-                               uint32_t* d_msg_checksum, uint32_t* d_msg_source, int64_t* d_msg_source_inc,
-                               void* stream) {
+int rp_wire_decode_dev(rp_members* m, const uint8_t* d_buf, const uint64_t* d_msg_off, uint32_t n_msgs,
+                       uint32_t* d_msg_rec_off, uint32_t rec_cap, const rp_wire_records_out* recs,
+                       const rp_wire_headers_out* hdr, uint64_t* d_err, void* stream) {
     return guard([&] {
         RP_REQUIRE(m, "null members handle");
         RP_REQUIRE(d_msg_off && d_msg_rec_off && d_err, "null message offsets / errors");
-        RP_REQUIRE(rec_cap == 0 || (d_addr && d_status && d_inc), "null record column");
+        const rp_wire_records_out R = recs ? *recs : rp_wire_records_out{};
+        const rp_wire_headers_out H = hdr ? *hdr : rp_wire_headers_out{};
+        RP_REQUIRE(rec_cap == 0 || (R.addr && R.status && R.inc), "null record column");
         hipStream_t hst;
         rp::Scratch* ws;
         rp::NameTable& nt = rp::members_names(m, &hst, &ws);
         hipStream_t st = stream ? rp::as_stream(stream) : hst;
         rp::Names nm = rp::names_of(nt, st, *ws);
         rp::In I{d_buf, d_msg_off};
-        rp::Out O{d_msg_rec_off, d_msg_rec_off, rec_cap, d_addr, d_src, d_status, d_inc, d_src_inc, d_id_off,
-                  d_addr_off, d_addr_len, d_err, d_msg_checksum, d_msg_source, d_msg_source_inc};
+        rp::Out O{d_msg_rec_off, d_msg_rec_off, rec_cap, R.addr, R.src, R.status, R.inc, R.src_inc, R.id_off,
+                  R.addr_off, R.addr_len, d_err, H.checksum, H.source, H.source_inc, H.target, H.ping_status};
         if (n_msgs) {
             hipLaunchKernelGGL(rp::k_decode<false>, dim3(rp::grid_for(n_msgs, 64)), dim3(64), 0, st, I, nm, O,
                                n_msgs);
@@ -618,11 +747,37 @@ int rp_wire_decode_changes_dev(rp_members* m, const uint8_t* d_buf, const uint64
     });
 }
 
+// The first-round entry points, as thin forms of the two above.
+int rp_wire_encode_changes_dev(rp_members* m, uint32_t n_msgs, const uint32_t* d_msg_rec_off, uint64_t n_rec,
+                               const uint32_t* d_addr, const uint32_t* d_src, const uint8_t* d_status,
+                               const int64_t* d_inc, const int64_t* d_src_inc, const uint8_t* d_ids, int form,
+                               int body, const uint32_t* d_msg_checksum, const uint32_t* d_msg_source,
+                               const int64_t* d_msg_source_inc, uint8_t* d_out, uint64_t* d_out_off, void* stream) {
+    if (body < 0 || body > 2) {
+        rp::set_error("rp_wire_encode_changes_dev: body must be 0..2 (rp_wire_encode_dev takes every body)");
+        return rp::RP_EINVAL;
+    }
+    const rp_wire_records R{d_addr, d_src, d_status, d_inc, d_src_inc, d_ids};
+    const rp_wire_headers H{d_msg_checksum, d_msg_source, d_msg_source_inc, nullptr, nullptr, nullptr, 0};
+    return rp_wire_encode_dev(m, n_msgs, d_msg_rec_off, n_rec, &R, form, body, &H, d_out, d_out_off, stream);
+}
+
+int rp_wire_decode_changes_dev(rp_members* m, const uint8_t* d_buf, const uint64_t* d_msg_off, uint32_t n_msgs,
+                               uint32_t* d_msg_rec_off, uint32_t rec_cap, uint32_t* d_addr, uint32_t* d_src,
+                               uint8_t* d_status, int64_t* d_inc, int64_t* d_src_inc, uint64_t* d_id_off,
+                               uint64_t* d_addr_off, uint32_t* d_addr_len, uint64_t* d_err,
+                               uint32_t* d_msg_checksum, uint32_t* d_msg_source, int64_t* d_msg_source_inc,
+                               void* stream) {
+    const rp_wire_records_out R{d_addr, d_src, d_status, d_inc, d_src_inc, d_id_off, d_addr_off, d_addr_len};
+    const rp_wire_headers_out H{d_msg_checksum, d_msg_source, d_msg_source_inc, nullptr, nullptr};
+    return rp_wire_decode_dev(m, d_buf, d_msg_off, n_msgs, d_msg_rec_off, rec_cap, &R, &H, d_err, stream);
+}
+
 }  // extern "C"
 
 // ------------------------------------------------------------------ host-buffer forms
 // For callers holding host memory (the N-API addon, ctypes): stage through the handle's
-// device, run the _dev form on the handle's stream, copy back. PCIe-bound.
+// device, run the device form on the handle's stream, copy back. PCIe-bound.
 namespace {
 template <class T>
 T* stage(rp::DevBuf<T>& d, const T* h, uint64_t n, hipStream_t st) {
@@ -631,35 +786,47 @@ T* stage(rp::DevBuf<T>& d, const T* h, uint64_t n, hipStream_t st) {
     if (n) RP_HIP(hipMemcpyAsync(d.p, h, sizeof(T) * n, hipMemcpyHostToDevice, st));
     return d.p;
 }
+template <class T>
+void fetch(T* h, const rp::DevBuf<T>& d, uint64_t n) {
+    if (h && n) RP_HIP(hipMemcpy(h, d.p, sizeof(T) * n, hipMemcpyDeviceToHost));
+}
 }  // namespace
 
 extern "C" {
 
-int rp_wire_encode_changes(rp_members* m, uint32_t n_msgs, const uint32_t* msg_rec_off, const uint32_t* addr,
-                           const uint32_t* src, const uint8_t* status, const int64_t* inc, const int64_t* src_inc,
-                           const uint8_t* ids, int form, int body, const uint32_t* msg_checksum,
-                           const uint32_t* msg_source, const int64_t* msg_source_inc, uint8_t* out, uint64_t cap,
-                           uint64_t* out_off) {
+int rp_wire_encode(rp_members* m, uint32_t n_msgs, const uint32_t* msg_rec_off, const rp_wire_records* recs, int form,
+                   int body, const rp_wire_headers* hdr, uint8_t* out, uint64_t cap, uint64_t* out_off) {
     return guard([&] {
         RP_REQUIRE(m && msg_rec_off && out_off, "null handle / offsets");
+        RP_REQUIRE(msg_rec_off[0] == 0, "message record offsets must start at 0");
+        for (uint32_t j = 0; j < n_msgs; j++)
+            RP_REQUIRE(msg_rec_off[j + 1] >= msg_rec_off[j], "message record offsets must not decrease");
         hipStream_t st;
         rp::Scratch* ws;
-        rp::members_names(m, &st, &ws);
+        rp::NameTable& nt = rp::members_names(m, &st, &ws);
         const uint64_t n_rec = msg_rec_off[n_msgs];
-        rp::DevBuf<uint32_t> d_ro, d_a, d_s, d_ck, d_ms;
-        rp::DevBuf<uint8_t> d_st, d_ids, d_out;
+        const rp_wire_records R = recs ? *recs : rp_wire_records{};
+        const rp_wire_headers H = hdr ? *hdr : rp_wire_headers{};
+        RP_REQUIRE(n_rec == 0 || (R.addr && R.src && R.status && R.inc), "null record column");
+        const uint32_t nn = nt.size();
+        for (uint64_t r = 0; r < n_rec; r++) {  // the ids index the name table: check them here
+            RP_REQUIRE(R.addr[r] < nn, "wire encode: a record's address is not an interned id");
+            RP_REQUIRE(R.src[r] < nn || R.src[r] == RP_NULL_ID, "wire encode: a record's source is not an interned id");
+        }
+        rp::DevBuf<uint32_t> d_ro, d_a, d_s, d_ck, d_ms, d_tg;
+        rp::DevBuf<uint8_t> d_st, d_ids, d_out, d_ps;
         rp::DevBuf<int64_t> d_i, d_si, d_msi;
         rp::DevBuf<uint64_t> d_oo;
         stage(d_ro, msg_rec_off, (uint64_t)n_msgs + 1, st);
-        const bool ping = body == 1;
+        const rp_wire_records DR{stage(d_a, R.addr, n_rec, st), stage(d_s, R.src, n_rec, st),
+                                 stage(d_st, R.status, n_rec, st), stage(d_i, R.inc, n_rec, st),
+                                 stage(d_si, R.src_inc, n_rec, st), stage(d_ids, R.ids, n_rec * 36, st)};
+        const rp_wire_headers DH{stage(d_ck, H.checksum, n_msgs, st), stage(d_ms, H.source, n_msgs, st),
+                                 stage(d_msi, H.source_inc, n_msgs, st), stage(d_tg, H.target, n_msgs, st),
+                                 stage(d_ps, H.ping_status, n_msgs, st), H.app, H.app_len};
         d_oo.reserve((uint64_t)n_msgs + 1);
         auto run = [&](uint8_t* o) {
-            const int rc = rp_wire_encode_changes_dev(
-                m, n_msgs, d_ro.p, n_rec, stage(d_a, addr, n_rec, st), stage(d_s, src, n_rec, st),
-                stage(d_st, status, n_rec, st), stage(d_i, inc, n_rec, st), stage(d_si, src_inc, n_rec, st),
-                stage(d_ids, ids, n_rec * 36, st), form, body, ping ? stage(d_ck, msg_checksum, n_msgs, st) : nullptr,
-                ping ? stage(d_ms, msg_source, n_msgs, st) : nullptr,
-                ping ? stage(d_msi, msg_source_inc, n_msgs, st) : nullptr, o, d_oo.p, st);
+            const int rc = rp_wire_encode_dev(m, n_msgs, d_ro.p, n_rec, &DR, form, body, &DH, o, d_oo.p, st);
             if (rc) throw rp::Error(rc, rp_last_error());
         };
         run(nullptr);
@@ -673,42 +840,77 @@ int rp_wire_encode_changes(rp_members* m, uint32_t n_msgs, const uint32_t* msg_r
     });
 }
 
-int rp_wire_decode_changes(rp_members* m, const char* buf, const uint64_t* msg_off, uint32_t n_msgs,
-                           uint32_t* msg_rec_off, uint32_t rec_cap, uint32_t* addr, uint32_t* src, uint8_t* status,
-                           int64_t* inc, int64_t* src_inc, uint64_t* err) {
+int rp_wire_decode(rp_members* m, const char* buf, const uint64_t* msg_off, uint32_t n_msgs, uint32_t* msg_rec_off,
+                   uint32_t rec_cap, const rp_wire_records_out* recs, const rp_wire_headers_out* hdr, uint64_t* err) {
     return guard([&] {
         RP_REQUIRE(m && msg_off && msg_rec_off && err, "null handle / offsets / errors");
+        const uint64_t nb = msg_off[n_msgs];
+        RP_REQUIRE(buf || nb == 0, "null buffer with message bytes");
+        for (uint32_t j = 0; j < n_msgs; j++) RP_REQUIRE(msg_off[j + 1] >= msg_off[j], "message offsets must not decrease");
         hipStream_t st;
         rp::Scratch* ws;
         rp::members_names(m, &st, &ws);
-        const uint64_t nb = msg_off[n_msgs];
-        rp::DevBuf<uint8_t> d_buf, d_st;
-        rp::DevBuf<uint64_t> d_off, d_err;
-        rp::DevBuf<uint32_t> d_ro, d_a, d_s;
-        rp::DevBuf<int64_t> d_i, d_si;
+        const rp_wire_records_out R = recs ? *recs : rp_wire_records_out{};
+        const rp_wire_headers_out H = hdr ? *hdr : rp_wire_headers_out{};
+        rp::DevBuf<uint8_t> d_buf, d_st, d_ps;
+        rp::DevBuf<uint64_t> d_off, d_err, d_id, d_ao;
+        rp::DevBuf<uint32_t> d_ro, d_a, d_s, d_al, d_ck, d_ms, d_tg;
+        rp::DevBuf<int64_t> d_i, d_si, d_msi;
         stage(d_buf, reinterpret_cast<const uint8_t*>(buf), nb, st);
         if (!buf) d_buf.reserve(1);
         stage(d_off, msg_off, (uint64_t)n_msgs + 1, st);
         d_ro.reserve((uint64_t)n_msgs + 1);
-        d_err.reserve(n_msgs ? n_msgs : 1);
+        const uint64_t nm1 = n_msgs ? n_msgs : 1;
+        d_err.reserve(nm1);
         const uint64_t c = rec_cap ? rec_cap : 1;
-        d_a.reserve(c); d_s.reserve(c); d_st.reserve(c); d_i.reserve(c); d_si.reserve(c);
-        const int rc = rp_wire_decode_changes_dev(m, d_buf.p, d_off.p, n_msgs, d_ro.p, rec_cap, d_a.p, d_s.p, d_st.p,
-                                                  d_i.p, d_si.p, nullptr, nullptr, nullptr, d_err.p, nullptr, nullptr,
-                                                  nullptr, st);
+        d_a.reserve(c); d_st.reserve(c); d_i.reserve(c);
+        auto opt = [&](auto& d, const void* want, uint64_t n) { if (want) d.reserve(n); return want ? d.p : nullptr; };
+        const rp_wire_records_out DR{d_a.p, opt(d_s, R.src, c), d_st.p, d_i.p, opt(d_si, R.src_inc, c),
+                                     opt(d_id, R.id_off, c), opt(d_ao, R.addr_off, c), opt(d_al, R.addr_len, c)};
+        const rp_wire_headers_out DH{opt(d_ck, H.checksum, nm1), opt(d_ms, H.source, nm1),
+                                     opt(d_msi, H.source_inc, nm1), opt(d_tg, H.target, nm1),
+                                     opt(d_ps, H.ping_status, nm1)};
+        const int rc = rp_wire_decode_dev(m, d_buf.p, d_off.p, n_msgs, d_ro.p, rec_cap, &DR, &DH, d_err.p, st);
         if (rc) throw rp::Error(rc, rp_last_error());
         RP_HIP(hipStreamSynchronize(st));
         RP_HIP(hipMemcpy(msg_rec_off, d_ro.p, sizeof(uint32_t) * (n_msgs + 1), hipMemcpyDeviceToHost));
-        if (n_msgs) RP_HIP(hipMemcpy(err, d_err.p, sizeof(uint64_t) * n_msgs, hipMemcpyDeviceToHost));
+        fetch(err, d_err, n_msgs);
+        fetch(H.checksum, d_ck, n_msgs);
+        fetch(H.source, d_ms, n_msgs);
+        fetch(H.source_inc, d_msi, n_msgs);
+        fetch(H.target, d_tg, n_msgs);
+        fetch(H.ping_status, d_ps, n_msgs);
         const uint64_t k = std::min<uint64_t>(msg_rec_off[n_msgs], rec_cap);
-        if (k) {
-            if (addr) RP_HIP(hipMemcpy(addr, d_a.p, 4 * k, hipMemcpyDeviceToHost));
-            if (src) RP_HIP(hipMemcpy(src, d_s.p, 4 * k, hipMemcpyDeviceToHost));
-            if (status) RP_HIP(hipMemcpy(status, d_st.p, k, hipMemcpyDeviceToHost));
-            if (inc) RP_HIP(hipMemcpy(inc, d_i.p, 8 * k, hipMemcpyDeviceToHost));
-            if (src_inc) RP_HIP(hipMemcpy(src_inc, d_si.p, 8 * k, hipMemcpyDeviceToHost));
-        }
+        fetch(R.addr, d_a, k);
+        fetch(R.src, d_s, k);
+        fetch(R.status, d_st, k);
+        fetch(R.inc, d_i, k);
+        fetch(R.src_inc, d_si, k);
+        fetch(R.id_off, d_id, k);
+        fetch(R.addr_off, d_ao, k);
+        fetch(R.addr_len, d_al, k);
     });
+}
+
+int rp_wire_encode_changes(rp_members* m, uint32_t n_msgs, const uint32_t* msg_rec_off, const uint32_t* addr,
+                           const uint32_t* src, const uint8_t* status, const int64_t* inc, const int64_t* src_inc,
+                           const uint8_t* ids, int form, int body, const uint32_t* msg_checksum,
+                           const uint32_t* msg_source, const int64_t* msg_source_inc, uint8_t* out, uint64_t cap,
+                           uint64_t* out_off) {
+    if (body < 0 || body > 2) {
+        rp::set_error("rp_wire_encode_changes: body must be 0..2 (rp_wire_encode takes every body)");
+        return rp::RP_EINVAL;
+    }
+    const rp_wire_records R{addr, src, status, inc, src_inc, ids};
+    const rp_wire_headers H{msg_checksum, msg_source, msg_source_inc, nullptr, nullptr, nullptr, 0};
+    return rp_wire_encode(m, n_msgs, msg_rec_off, &R, form, body, &H, out, cap, out_off);
+}
+
+int rp_wire_decode_changes(rp_members* m, const char* buf, const uint64_t* msg_off, uint32_t n_msgs,
+                           uint32_t* msg_rec_off, uint32_t rec_cap, uint32_t* addr, uint32_t* src, uint8_t* status,
+                           int64_t* inc, int64_t* src_inc, uint64_t* err) {
+    const rp_wire_records_out R{addr, src, status, inc, src_inc, nullptr, nullptr, nullptr};
+    return rp_wire_decode(m, buf, msg_off, n_msgs, msg_rec_off, rec_cap, &R, nullptr, err);
 }
 
 }  // extern "C"

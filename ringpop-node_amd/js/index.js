@@ -173,6 +173,9 @@ HashRing.prototype.groupByOwner = function groupByOwner(keys, whoami) {
     return out;
 };
 
+// the name ringpop's handleOrProxyAll probes for (INTEGRATION.md): same function
+HashRing.prototype.groupBy = HashRing.prototype.groupByOwner;
+
 // RequestProxySend.lookupKeys (lib/request-proxy/send.js:171-179): distinct owners, first seen.
 HashRing.prototype.lookupKeys = function lookupKeys(keys, whoami) {
     var g = native.ringGroupKeys(this._h, this._customHash ? this._hashes(keys) : keys);

@@ -10,6 +10,7 @@
  * Built by ./Makefile (gcc, N-API v3+ headers of the node in this image, rpath to ..).
  */
 #include <node_api.h>
+#include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -813,6 +814,165 @@ static napi_value js_sim_stats(napi_env env, napi_callback_info info) {
 }
 
 /* ------------------------------------------------------------------ module */
+/* ------------------------------------------------------------------ wire bodies */
+/* the typed array at obj[key] (NULL when absent / null); *n its length */
+static void *prop_typed(napi_env env, napi_value obj, const char *key, napi_typedarray_type t, size_t *n) {
+    *n = 0;
+    if (is_nullish(env, obj)) return NULL;
+    napi_value v;
+    if (napi_get_named_property(env, obj, key, &v) != napi_ok || is_nullish(env, v)) return NULL;
+    return typed_data(env, v, t, n);
+}
+
+static int64_t *f64_to_i64(const double *d, size_t n, int nan_is_min) {
+    int64_t *o = (int64_t *)malloc(sizeof(int64_t) * (n ? n : 1));
+    for (size_t i = 0; i < n; i++) o[i] = (nan_is_min && d[i] != d[i]) ? INT64_MIN : (int64_t)d[i];
+    return o;
+}
+
+/* wireEncode(h, msgRecOff Uint32Array, recs {addr, src, status, inc, srcInc?, ids?}, form, body,
+ * hdr {checksum?, source?, sourceInc?, target?, pingStatus?, app?}) -> {bytes: Uint8Array,
+ * off: Float64Array}: JSON.stringify of the gossip bodies (dissemination.js:163-170, ping /
+ * ping-req / join bodies) on the device (rp_wire_encode). inc / srcInc are Float64Array (srcInc
+ * NaN = absent); src RP_NULL_ID = absent; an ids row starting with 0 = absent. */
+static napi_value js_wire_encode(napi_env env, napi_callback_info info) {
+    ARGS(6);
+    handle_t *h = get_handle(env, argv[0], 2);
+    if (!h) return NULL;
+    size_t nro = 0, na = 0, ns = 0, nst = 0, ni = 0, nsi = 0, nid = 0;
+    const uint32_t *ro = (const uint32_t *)typed_data(env, argv[1], napi_uint32_array, &nro);
+    if (!ro || nro < 1) {
+        napi_throw_type_error(env, NULL, "wireEncode expects msgRecOff Uint32Array(n_msgs + 1)");
+        return NULL;
+    }
+    const uint32_t n_msgs = (uint32_t)(nro - 1), n_rec = ro[n_msgs];
+    const uint32_t *addr = (const uint32_t *)prop_typed(env, argv[2], "addr", napi_uint32_array, &na);
+    const uint32_t *src = (const uint32_t *)prop_typed(env, argv[2], "src", napi_uint32_array, &ns);
+    const uint8_t *st = (const uint8_t *)prop_typed(env, argv[2], "status", napi_uint8_array, &nst);
+    const double *incd = (const double *)prop_typed(env, argv[2], "inc", napi_float64_array, &ni);
+    const double *sincd = (const double *)prop_typed(env, argv[2], "srcInc", napi_float64_array, &nsi);
+    const uint8_t *ids = (const uint8_t *)prop_typed(env, argv[2], "ids", napi_uint8_array, &nid);
+    if (na < n_rec || ns < n_rec || nst < n_rec || ni < n_rec || (sincd && nsi < n_rec) || (ids && nid < 36ull * n_rec)) {
+        napi_throw_type_error(env, NULL, "wireEncode: record columns shorter than msgRecOff says");
+        return NULL;
+    }
+    int32_t form = 0, body = 0;
+    NAPI_OK(napi_get_value_int32(env, argv[3], &form));
+    NAPI_OK(napi_get_value_int32(env, argv[4], &body));
+    size_t hck = 0, hs = 0, hsi = 0, ht = 0, hp = 0;
+    const uint32_t *ck = (const uint32_t *)prop_typed(env, argv[5], "checksum", napi_uint32_array, &hck);
+    const uint32_t *ms = (const uint32_t *)prop_typed(env, argv[5], "source", napi_uint32_array, &hs);
+    const double *msid = (const double *)prop_typed(env, argv[5], "sourceInc", napi_float64_array, &hsi);
+    const uint32_t *tg = (const uint32_t *)prop_typed(env, argv[5], "target", napi_uint32_array, &ht);
+    const uint8_t *ps = (const uint8_t *)prop_typed(env, argv[5], "pingStatus", napi_uint8_array, &hp);
+    if ((ck && hck < n_msgs) || (ms && hs < n_msgs) || (msid && hsi < n_msgs) || (tg && ht < n_msgs) ||
+        (ps && hp < n_msgs)) {
+        napi_throw_type_error(env, NULL, "wireEncode: header columns shorter than the message count");
+        return NULL;
+    }
+    char app[1024];
+    size_t app_len = 0;
+    if (!is_nullish(env, argv[5])) {
+        napi_value av;
+        if (napi_get_named_property(env, argv[5], "app", &av) == napi_ok && !is_nullish(env, av))
+            NAPI_OK(napi_get_value_string_utf8(env, av, app, sizeof app, &app_len));
+    }
+    int64_t *inc = f64_to_i64(incd, n_rec, 0), *sinc = sincd ? f64_to_i64(sincd, n_rec, 1) : NULL;
+    int64_t *msi = msid ? f64_to_i64(msid, n_msgs, 0) : NULL;
+    rp_wire_records R = {addr, src, st, inc, sinc, ids};
+    rp_wire_headers H = {ck, ms, msi, tg, ps, app_len ? app : NULL, (uint32_t)app_len};
+    void *od = NULL, *bd = NULL;
+    napi_value off = new_typed(env, napi_float64_array, n_msgs + 1, 8, &od);
+    uint64_t *o64 = (uint64_t *)malloc(sizeof(uint64_t) * (n_msgs + 1));
+    int rc = rp_wire_encode((rp_members *)h->p, n_msgs, ro, &R, form, body, &H, NULL, 0, o64);
+    napi_value bytes = NULL;
+    if (rc == 0) {
+        bytes = new_typed(env, napi_uint8_array, o64[n_msgs] ? o64[n_msgs] : 1, 1, &bd);
+        rc = rp_wire_encode((rp_members *)h->p, n_msgs, ro, &R, form, body, &H, (uint8_t *)bd, o64[n_msgs], o64);
+    }
+    for (uint32_t j = 0; rc == 0 && j <= n_msgs; j++) ((double *)od)[j] = (double)o64[j];
+    free(inc);
+    free(sinc);
+    free(msi);
+    free(o64);
+    RP_OK(rc);
+    napi_value out;
+    napi_create_object(env, &out);
+    napi_set_named_property(env, out, "bytes", bytes);
+    napi_set_named_property(env, out, "off", off);
+    return out;
+}
+
+/* wireDecode(h, bytes Uint8Array, msgOff Float64Array(n + 1), recCap) -> {recOff, addr, src, status,
+ * inc, srcInc (NaN absent), idOff, addrOff, addrLen, err, checksum, source, sourceInc (NaN absent),
+ * target, pingStatus}: safeParse + the bodies' members on the device (rp_wire_decode). */
+static napi_value js_wire_decode(napi_env env, napi_callback_info info) {
+    ARGS(4);
+    handle_t *h = get_handle(env, argv[0], 2);
+    if (!h) return NULL;
+    size_t nb = 0, no = 0;
+    const char *buf = (const char *)typed_data(env, argv[1], napi_uint8_array, &nb);
+    const double *offd = (const double *)typed_data(env, argv[2], napi_float64_array, &no);
+    uint32_t cap = 0;
+    NAPI_OK(napi_get_value_uint32(env, argv[3], &cap));
+    if (!offd || no < 1) {
+        napi_throw_type_error(env, NULL, "wireDecode expects msgOff Float64Array(n_msgs + 1)");
+        return NULL;
+    }
+    const uint32_t n = (uint32_t)(no - 1);
+    uint64_t *off = (uint64_t *)malloc(sizeof(uint64_t) * (n + 1));
+    for (uint32_t j = 0; j <= n; j++) off[j] = (uint64_t)offd[j];
+    if (off[n] > nb) {
+        free(off);
+        napi_throw_range_error(env, NULL, "wireDecode: msgOff past the buffer");
+        return NULL;
+    }
+    const size_t c = cap ? cap : 1, m1 = n ? n : 1;
+    void *p_ro, *p_a, *p_s, *p_st, *p_i, *p_si, *p_id, *p_ao, *p_al, *p_err, *p_ck, *p_ms, *p_msi, *p_tg, *p_ps;
+    napi_value ro = new_typed(env, napi_uint32_array, n + 1, 4, &p_ro);
+    napi_value a = new_typed(env, napi_uint32_array, c, 4, &p_a);
+    napi_value s2 = new_typed(env, napi_uint32_array, c, 4, &p_s);
+    napi_value st = new_typed(env, napi_uint8_array, c, 1, &p_st);
+    napi_value inc = new_typed(env, napi_float64_array, c, 8, &p_i);
+    napi_value sinc = new_typed(env, napi_float64_array, c, 8, &p_si);
+    napi_value idoff = new_typed(env, napi_float64_array, c, 8, &p_id);
+    napi_value aoff = new_typed(env, napi_float64_array, c, 8, &p_ao);
+    napi_value alen = new_typed(env, napi_uint32_array, c, 4, &p_al);
+    napi_value err = new_typed(env, napi_float64_array, m1, 8, &p_err);
+    napi_value ck = new_typed(env, napi_uint32_array, m1, 4, &p_ck);
+    napi_value ms = new_typed(env, napi_uint32_array, m1, 4, &p_ms);
+    napi_value msi = new_typed(env, napi_float64_array, m1, 8, &p_msi);
+    napi_value tg = new_typed(env, napi_uint32_array, m1, 4, &p_tg);
+    napi_value ps = new_typed(env, napi_uint8_array, m1, 1, &p_ps);
+    int64_t *i64 = (int64_t *)malloc(8 * c), *si64 = (int64_t *)malloc(8 * c), *msi64 = (int64_t *)malloc(8 * m1);
+    uint64_t *id64 = (uint64_t *)malloc(8 * c), *ao64 = (uint64_t *)malloc(8 * c), *e64 = (uint64_t *)malloc(8 * m1);
+    rp_wire_records_out R = {(uint32_t *)p_a, (uint32_t *)p_s, (uint8_t *)p_st, i64, si64, id64, ao64, (uint32_t *)p_al};
+    rp_wire_headers_out H = {(uint32_t *)p_ck, (uint32_t *)p_ms, msi64, (uint32_t *)p_tg, (uint8_t *)p_ps};
+    const int rc = rp_wire_decode((rp_members *)h->p, buf, off, n, (uint32_t *)p_ro, cap, &R, &H, e64);
+    if (rc == 0) {
+        const uint32_t k = ((uint32_t *)p_ro)[n] < cap ? ((uint32_t *)p_ro)[n] : cap;
+        for (uint32_t r = 0; r < k; r++) {
+            ((double *)p_i)[r] = (double)i64[r];
+            ((double *)p_si)[r] = si64[r] == INT64_MIN ? NAN : (double)si64[r];
+            ((double *)p_id)[r] = id64[r] == UINT64_MAX ? -1 : (double)id64[r];
+            ((double *)p_ao)[r] = (double)ao64[r];
+        }
+        for (uint32_t j = 0; j < n; j++) {
+            ((double *)p_err)[j] = (double)e64[j];
+            ((double *)p_msi)[j] = msi64[j] == INT64_MIN ? NAN : (double)msi64[j];
+        }
+    }
+    free(off); free(i64); free(si64); free(msi64); free(id64); free(ao64); free(e64);
+    RP_OK(rc);
+    napi_value out;
+    napi_create_object(env, &out);
+    const char *names[] = {"recOff", "addr", "src", "status", "inc", "srcInc", "idOff", "addrOff", "addrLen", "err",
+                           "checksum", "source", "sourceInc", "target", "pingStatus"};
+    napi_value vals[] = {ro, a, s2, st, inc, sinc, idoff, aoff, alen, err, ck, ms, msi, tg, ps};
+    for (size_t i = 0; i < sizeof(vals) / sizeof(vals[0]); i++) napi_set_named_property(env, out, names[i], vals[i]);
+    return out;
+}
+
 static napi_value init(napi_env env, napi_value exports) {
     static const struct {
         const char *name;
@@ -851,6 +1011,8 @@ static napi_value init(napi_env env, napi_value exports) {
         {"simView", js_sim_view},
         {"simConverged", js_sim_converged},
         {"simStats", js_sim_stats},
+        {"wireEncode", js_wire_encode},
+        {"wireDecode", js_wire_decode},
     };
     for (size_t i = 0; i < sizeof(fns) / sizeof(fns[0]); i++) {
         napi_value f;

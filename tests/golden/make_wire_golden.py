@@ -25,7 +25,8 @@ def make_cases():
     rng = random.Random(77)
     cases = []
     for name, n_members, n_changes, with_ids in [("empty", 3, 0, True), ("one", 4, 1, True), ("small", 40, 25, True),
-                                                 ("noid", 40, 30, False), ("wide", 600, 400, True)]:
+                                                 ("noid", 40, 30, False), ("wide", 600, 400, True),
+                                                 ("absent", 60, 45, "mixed")]:
         members = large[:n_members]
         whoami = members[0]
         incs = [0, 1, 1434401518824, 2 ** 53 - 1, 9, 10, 99, 100]
@@ -34,11 +35,17 @@ def make_cases():
         changes = []
         for a in rng.sample(members, n_changes):
             src = rng.choice(members)
-            changes.append([a, rng.choice(STATUSES), rng.choice([rng.choice(incs), 1434401500000 + rng.randrange(10 ** 7)]),
-                            src, 1434401500000 + rng.randrange(10 ** 7),
-                            str(uuid.UUID(int=rng.getrandbits(128), version=4)) if with_ids else None])
+            ch = [a, rng.choice(STATUSES), rng.choice([rng.choice(incs), 1434401500000 + rng.randrange(10 ** 7)]),
+                  src, 1434401500000 + rng.randrange(10 ** 7),
+                  str(uuid.UUID(int=rng.getrandbits(128), version=4)) if with_ids else None]
+            if with_ids == "mixed":  # JSON.stringify leaves undefined members out, per record
+                ch[3] = None if rng.random() < 0.3 else ch[3]
+                ch[4] = None if rng.random() < 0.3 else ch[4]
+                ch[5] = None if rng.random() < 0.4 else ch[5]
+            changes.append(ch)
         cases.append({"name": name, "whoami": whoami, "whoamiInc": 1434401518824 + rng.randrange(1000),
-                      "serverCount": n_members, "checksum": rng.getrandbits(32), "members": mem, "changes": changes})
+                      "serverCount": n_members, "checksum": rng.getrandbits(32), "members": mem, "changes": changes,
+                      "target": members[-1], "pingStatus": rng.random() < 0.5, "app": "ringpop-" + name})
     return cases
 
 

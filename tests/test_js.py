@@ -20,7 +20,7 @@ EXPORTS = ["version", "deviceCount", "hash32", "destroy", "ringCreate", "ringAdd
            "ringOwnerName", "ringLookup", "ringLookupN", "ringLookupNHashes", "ringGroupKeys", "membersCreate", "membersIntern",
            "membersSetLocal", "membersUpdate", "membersSet", "membersChecksum", "membersComputeChecksum",
            "membersChecksumString", "membersDump", "simCreate", "simStep", "simRound", "simChecksums",
-           "simView", "simConverged", "simStats"]
+           "simView", "simConverged", "simStats", "wireEncode", "wireDecode"]
 
 
 @pytest.fixture(scope="module")

@@ -48,3 +48,27 @@ def test_js_gossipsim_matches_reference_goldens(gpu, tmp_path):
         cases.append(dict(c, names=[S.c2_addr(i) for i in range(n)], inc0=[int(x) for x in S.c3_members(n)[2]]))
     res = run_node("sim_parity.js", {"cases": cases}, tmp_path)
     assert res["nfail"] == 0, res["fails"]
+
+
+def test_js_membership_dropin_matches_reference_goldens(gpu, tmp_path):
+    """The drop-in lib/membership module (ringpop-node_amd/js/membership.js), installed into the
+    module cache the way a ringpop deployment installs it, replays every membership golden: the
+    96 override rules (remote + local), random batches with repeated addresses and local
+    overrides, the 1332-member fixture, stash + set(), and the leave cases."""
+    import pyoracle
+    cases = gu.load("membership_golden.json")["cases"]
+    for c in cases:
+        n = 4000 if c["name"] == "fixture1332" else 2000
+        c["joinRands"] = [pyoracle.philox([k, 0, 0, 0], [c["joinSeed"], 0x4A4F494E])[0] for k in range(n)]
+    res = run_node("membership_parity.js", {"cases": cases}, tmp_path)
+    assert res["nfail"] == 0, res["fails"]
+    assert res["checks"] > 700
+
+
+def test_js_wire_bodies_match_reference_goldens(gpu, tmp_path):
+    """rpamd.node wireEncode / wireDecode (-> rp_wire_encode / rp_wire_decode): every golden body
+    — issueAs / fullSync arrays, ping, ping response, ping-req request, join response, with
+    per-record undefined members — byte for byte, and the bodies decoded back."""
+    res = run_node("wire_parity.js", {"cases": gu.load("wire_golden.json")["cases"]}, tmp_path)
+    assert res["nfail"] == 0, res["fails"]
+    assert res["checks"] > 100

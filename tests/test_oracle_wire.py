@@ -25,3 +25,9 @@ def test_oracle_matches_reference_wire_text():
         assert pywire.body(recs, "ping", c["checksum"], c["whoami"], c["whoamiInc"]) == o["ping"], c["name"]
         assert pywire.body(recs, "pingResponse") == o["pingResponse"], c["name"]
         assert pywire.decode(o["ping"]) == recs
+        assert pywire.body(recs, "pingReq", c["checksum"], c["whoami"], c["whoamiInc"],
+                           target=c["target"]) == o["pingReq"], c["name"]
+        assert pywire.body(recs, "pingReqResponse", target=c["target"], ping_status=c["pingStatus"]) == \
+            o["pingReqResponse"], c["name"]
+        assert pywire.body(fs, "joinResponse", c["checksum"], c["whoami"], app=c["app"]) == o["joinResponse"], c["name"]
+        assert pywire.decode(o["joinResponse"]) == fs

@@ -1,6 +1,8 @@
-"""GPU parity tests of the gossip wire codec through the C ABI (rp_wire_encode_changes_dev /
-rp_wire_decode_changes_dev): change records as dissemination.js:163-170 / 64-73 emit them,
-wrapped as ping-sender.js:71-76 and server/protocol/ping.js:45-48 bodies.
+"""GPU parity tests of the gossip wire codec through the C ABI (rp_wire_encode_dev /
+rp_wire_decode_dev and their host-buffer and first-round forms): change records as
+dissemination.js:163-170 / 64-73 emit them (undefined members left out per record), wrapped as
+the ping (ping-sender.js:71-76, ping.js:45-48), ping-req (ping-req-sender.js:75-81,
+ping-req.js:61-65) and join response (join.js:128-133) bodies.
 
 Oracle: tests/golden/wire_golden.json (the reference's Dissemination run in node) and
 oracle/pywire.py (pinned against it in tests/test_oracle_wire.py). Bit-exact bytes.
@@ -35,44 +37,80 @@ def split(blob, off):
     return [blob[int(off[j]):int(off[j + 1])].decode() for j in range(len(off) - 1)]
 
 
-def encode_cases(gpu, m, cases, form, body):
+def encode_cases(gpu, m, cases, form, body, app=None):
     rec_off, addr, src, st, inc, sinc, ids = [0], [], [], [], [], [], []
-    cks, msrc, msinc = [], [], []
+    cks, msrc, msinc, tgt, pst = [], [], [], [], []
     for c in cases:
         if form == "issueAs":
             rows = [(ch[0], ch[3], ch[1], ch[2], ch[4], ch[5]) for ch in c["changes"]]
         else:
-            rows = [(mm[0], c["whoami"], mm[1], mm[2], 0, None) for mm in c["members"]]
+            rows = [(mm[0], c["whoami"], mm[1], mm[2], None, None) for mm in c["members"]]
         for a, s_, status, i_, si, id_ in rows:
             addr.append(m.intern([a])[0])
-            src.append(m.intern([s_])[0])
+            src.append(NULL if s_ is None else m.intern([s_])[0])  # undefined source: left out
             st.append(ST[status])
             inc.append(i_)
-            sinc.append(si)
-            ids.append(np.frombuffer(id_.encode(), dtype=np.uint8) if id_ else None)
+            sinc.append(INT64_MIN if si is None else si)
+            ids.append(np.frombuffer(id_.encode(), dtype=np.uint8) if id_ else np.zeros(36, np.uint8))
         rec_off.append(len(addr))
         cks.append(c["checksum"])
         msrc.append(m.intern([c["whoami"]])[0])
         msinc.append(c["whoamiInc"])
-    have_ids = form == "issueAs" and all(x is not None for x in ids)
-    idarr = np.stack(ids) if have_ids and ids else None
+        tgt.append(m.intern([c["target"]])[0])
+        pst.append(1 if c["pingStatus"] else 0)
+    idarr = np.stack(ids) if form == "issueAs" and ids else None
     blob, off = gpu.wire_encode(m, np.array(rec_off), np.array(addr), np.array(src), np.array(st), np.array(inc),
                                 np.array(sinc), idarr, form=form, body=body, msg_checksum=cks, msg_source=msrc,
-                                msg_source_inc=msinc)
+                                msg_source_inc=msinc, msg_target=tgt, msg_ping_status=pst, app=app)
     return split(blob, off)
 
 
 def test_encode_matches_reference_golden(gpu):
     cases = golden()
     m = gpu.Membership()
-    with_ids = [c for c in cases if all(ch[5] for ch in c["changes"])]
-    no_ids = [c for c in cases if c not in with_ids]
-    assert no_ids  # the golden holds an id-less case
-    for group in (with_ids, no_ids):
-        assert encode_cases(gpu, m, group, "issueAs", "array") == [c["out"]["issueAs"] for c in group]
-        assert encode_cases(gpu, m, group, "issueAs", "ping") == [c["out"]["ping"] for c in group]
-        assert encode_cases(gpu, m, group, "issueAs", "pingResponse") == [c["out"]["pingResponse"] for c in group]
+    assert any(not ch[5] for c in cases for ch in c["changes"])  # id-less records
+    assert any(ch[3] is None or ch[4] is None for c in cases for ch in c["changes"])  # undefined members
+    assert encode_cases(gpu, m, cases, "issueAs", "array") == [c["out"]["issueAs"] for c in cases]
+    assert encode_cases(gpu, m, cases, "issueAs", "ping") == [c["out"]["ping"] for c in cases]
+    assert encode_cases(gpu, m, cases, "issueAs", "pingResponse") == [c["out"]["pingResponse"] for c in cases]
+    assert encode_cases(gpu, m, cases, "issueAs", "pingReq") == [c["out"]["pingReq"] for c in cases]
     assert encode_cases(gpu, m, cases, "fullSync", "array") == [c["out"]["fullSync"] for c in cases]
+    for c in cases:  # the app is one string per batch
+        assert encode_cases(gpu, m, [c], "fullSync", "joinResponse", app=c["app"]) == [c["out"]["joinResponse"]]
+
+
+def test_encode_pingreq_response_matches_reference_golden(gpu):
+    """{changes: issueAsReceiver(...), pingStatus, target} (ping-req.js:61-65): the records of the
+    reference's second issueAsReceiver call (piggyback counts moved on)."""
+    cases = golden()
+    m = gpu.Membership()
+    for c in cases:
+        want = c["out"]["pingReqResponse"]
+        recs = json.loads(want)["changes"]
+        sub = dict(c, changes=[[r["address"], r["status"], r["incarnationNumber"], r.get("source"),
+                                r.get("sourceIncarnationNumber"), r.get("id")] for r in recs])
+        assert encode_cases(gpu, m, [sub], "issueAs", "pingReqResponse") == [want]
+
+
+def test_encode_rejects_bad_ids_and_offsets(gpu):
+    """An id the name table does not hold (e.g. RP_NULL_ID from decoding an un-interned
+    address) or offsets that do not start at 0 / decrease are a clean RP_EINVAL, never a device
+    out-of-bounds read."""
+    m = gpu.Membership()
+    m.intern(["10.0.0.1:1", "10.0.0.2:2"])
+    ok = dict(src=np.array([0]), status=np.array([0]), inc=np.array([5]), src_inc=np.array([1]))
+    with pytest.raises(gpu.RingpopAmdError, match="address"):
+        gpu.wire_encode(m, np.array([0, 1]), np.array([NULL]), **ok)
+    with pytest.raises(gpu.RingpopAmdError, match="source"):
+        gpu.wire_encode(m, np.array([0, 1]), np.array([1]), np.array([7]), np.array([0]), np.array([5]))
+    with pytest.raises(gpu.RingpopAmdError, match="offsets"):
+        gpu.wire_encode(m, np.array([1, 1]), np.array([1]), **ok)
+    with pytest.raises(gpu.RingpopAmdError, match="target"):
+        gpu.wire_encode(m, np.array([0, 1]), np.array([1]), body="pingReqResponse", msg_target=[NULL],
+                        msg_ping_status=[1], **ok)
+    blob, _ = gpu.wire_encode(m, np.array([0, 1]), np.array([1]), **ok)
+    assert blob == b'[{"source":"10.0.0.1:1","sourceIncarnationNumber":1,"address":"10.0.0.2:2",' \
+                   b'"status":"alive","incarnationNumber":5}]'
 
 
 def test_decode_reference_golden(gpu):
@@ -80,9 +118,11 @@ def test_decode_reference_golden(gpu):
     m = gpu.Membership()
     for c in cases:
         m.intern([mm[0] for mm in c["members"]])
+    kinds = ["ping", "issueAs", "pingResponse", "fullSync", "pingReq", "pingReqResponse", "joinResponse"]
+    K = len(kinds)
     texts = []
     for c in cases:
-        texts += [c["out"]["ping"], c["out"]["issueAs"], c["out"]["pingResponse"], c["out"]["fullSync"]]
+        texts += [c["out"][x] for x in kinds]
     d = gpu.wire_decode(m, texts)
     assert (d["err"] == 0).all()
     for j, t in enumerate(texts):
@@ -92,7 +132,7 @@ def test_decode_reference_golden(gpu):
         raw = t.encode()
         for k, w in zip(range(a, b), want):
             assert m.address(int(d["addr"][k])) == w["address"]
-            assert m.address(int(d["src"][k])) == w["source"]
+            assert (m.address(int(d["src"][k])) if int(d["src"][k]) != NULL else None) == w.get("source")
             assert int(d["status"][k]) == ST[w["status"]]
             assert int(d["inc"][k]) == w["incarnationNumber"]
             assert int(d["src_inc"][k]) == w.get("sourceIncarnationNumber", INT64_MIN)
@@ -101,11 +141,18 @@ def test_decode_reference_golden(gpu):
                 assert raw[o:o + 36].decode() == w["id"]
             else:
                 assert int(d["id_off"][k]) == 2 ** 64 - 1
-    # ping headers (ping.js:27-36)
+    # body headers: ping (ping.js:27-36), ping-req request / response, join response
     for i, c in enumerate(cases):
-        assert int(d["checksum"][4 * i]) == c["checksum"]
-        assert m.address(int(d["source"][4 * i])) == c["whoami"]
-        assert int(d["source_inc"][4 * i]) == c["whoamiInc"]
+        j = K * i
+        assert int(d["checksum"][j]) == c["checksum"]
+        assert m.address(int(d["source"][j])) == c["whoami"]
+        assert int(d["source_inc"][j]) == c["whoamiInc"]
+        assert int(d["ping_status"][j]) == 0xFF and int(d["target"][j]) == NULL
+        assert m.address(int(d["target"][j + 4])) == c["target"] and int(d["source_inc"][j + 4]) == c["whoamiInc"]
+        assert int(d["ping_status"][j + 5]) == (1 if c["pingStatus"] else 0)
+        assert m.address(int(d["target"][j + 5])) == c["target"]
+        assert m.address(int(d["source"][j + 6])) == c["whoami"]  # coordinator
+        assert int(d["checksum"][j + 6]) == c["checksum"]  # membershipChecksum
 
 
 def test_decode_tolerates_json_layout_and_flags_errors(gpu):
@@ -214,3 +261,56 @@ def test_host_buffer_forms_match_device_forms(gpu):
     assert (si2[:k] == sinc).all()
     fs = pywire.decode(c["out"]["fullSync"])
     assert [m.address(int(x)) for x in a2[k:k + len(fs)]] == [r["address"] for r in fs]
+
+
+def test_host_buffer_full_api(gpu):
+    """rp_wire_encode / rp_wire_decode (host buffers, record + header structs): a ping-req
+    request round trip with an address that is not interned yet — the host decode hands back its
+    bytes (addr_off / addr_len) and every header column."""
+    import ctypes
+    m = gpu.Membership()
+    names = ["10.0.0.%d:1" % i for i in range(5)]
+    ids = np.array(m.intern(names), dtype=np.uint32)
+    L = gpu.lib()
+    ro = np.array([0, 2], dtype=np.uint32)
+    addr, src = ids[[1, 2]].copy(), np.array([ids[3], gpu.NULL_ID], dtype=np.uint32)
+    st, inc = np.array([1, 3], dtype=np.uint8), np.array([7, 9], dtype=np.int64)
+    sinc = np.array([11, gpu.INT64_MIN], dtype=np.int64)
+    ck, ms, msi, tg = (np.array([x], dtype=dt) for x, dt in ((99, np.uint32), (ids[0], np.uint32), (5, np.int64),
+                                                            (ids[4], np.uint32)))
+    P = lambda a: a.ctypes.data  # noqa: E731
+    recs = gpu.WireRecords(P(addr), P(src), P(st), P(inc), P(sinc), None)
+    hdr = gpu.WireHeaders(P(ck), P(ms), P(msi), P(tg), None, None, 0)
+    off = np.zeros(2, dtype=np.uint64)
+    gpu.check(L.rp_wire_encode(m._h, 1, P(ro), ctypes.byref(recs), 0, 3, ctypes.byref(hdr), None, 0, P(off)))
+    out = np.zeros(int(off[1]), dtype=np.uint8)
+    gpu.check(L.rp_wire_encode(m._h, 1, P(ro), ctypes.byref(recs), 0, 3, ctypes.byref(hdr), P(out), len(out), P(off)))
+    text = out.tobytes().decode()
+    assert json.loads(text) == {"checksum": 99, "changes": [
+        {"source": names[3], "sourceIncarnationNumber": 11, "address": names[1], "status": "suspect",
+         "incarnationNumber": 7},
+        {"address": names[2], "status": "leave", "incarnationNumber": 9}],
+        "source": names[0], "sourceIncarnationNumber": 5, "target": names[4]}
+    text2 = text.replace(names[2], "10.9.9.9:9")  # not interned
+    blob = text2.encode()
+    moff = np.array([0, len(blob)], dtype=np.uint64)
+    cap = 8
+    cols = dict(addr=np.zeros(cap, np.uint32), src=np.zeros(cap, np.uint32), status=np.zeros(cap, np.uint8),
+                inc=np.zeros(cap, np.int64), src_inc=np.zeros(cap, np.int64), id_off=np.zeros(cap, np.uint64),
+                addr_off=np.zeros(cap, np.uint64), addr_len=np.zeros(cap, np.uint32))
+    hcols = dict(checksum=np.zeros(1, np.uint32), source=np.zeros(1, np.uint32), source_inc=np.zeros(1, np.int64),
+                 target=np.zeros(1, np.uint32), ping_status=np.zeros(1, np.uint8))
+    ro2, err = np.zeros(2, np.uint32), np.zeros(1, np.uint64)
+    rout = gpu.WireRecordsOut(*[P(cols[k]) for k in ("addr", "src", "status", "inc", "src_inc", "id_off", "addr_off",
+                                                     "addr_len")])
+    hout = gpu.WireHeadersOut(*[P(hcols[k]) for k in ("checksum", "source", "source_inc", "target", "ping_status")])
+    gpu.check(L.rp_wire_decode(m._h, blob, P(moff), 1, P(ro2), cap, ctypes.byref(rout), ctypes.byref(hout), P(err)))
+    assert err[0] == 0 and ro2[1] == 2
+    assert cols["addr"][0] == ids[1] and cols["addr"][1] == gpu.NULL_ID
+    o, n = int(cols["addr_off"][1]), int(cols["addr_len"][1])
+    assert blob[o:o + n] == b"10.9.9.9:9"
+    assert cols["src"][1] == gpu.NULL_ID and cols["src_inc"][1] == gpu.INT64_MIN and cols["src_inc"][0] == 11
+    assert (hcols["checksum"][0], hcols["source"][0], hcols["source_inc"][0], hcols["target"][0],
+            hcols["ping_status"][0]) == (99, ids[0], 5, ids[4], 0xFF)
+    # host decode: null buffer with bytes is an error, not a read past a 1-byte buffer
+    assert L.rp_wire_decode(m._h, None, P(moff), 1, P(ro2), cap, ctypes.byref(rout), None, P(err)) != 0
