@@ -179,6 +179,38 @@ int rp_members_checksum_string(rp_members *m, char *buf, uint64_t cap, uint64_t 
 int rp_members_dump(rp_members *m, uint8_t *exists, uint8_t *status, int64_t *inc, uint32_t cap);
 int rp_members_count(rp_members *m, uint32_t *n_names);
 
+/* ---- flap-damping scores ----
+ * Member.dampScore / lastUpdateDampScore / lastUpdateTimestamp (lib/membership/member.js:28-41)
+ * kept on the device by member id. Once configured, every update() applies _applyUpdatePenalty
+ * (member.js:98-107, 133-153: decay, + penalty, clamp, suppress-limit check) to each applied
+ * update of another member at now_ms, stamps lastUpdateTimestamp on every applied update, and
+ * gives created members (update() or set()) the initial score; rp_members_damp_decay is
+ * Membership._decayMembersDampScore (lib/membership/index.js:374-383) over every member. The
+ * fields mirror config.js:60-71; the defaults are {1, 0, 0, 10000, 500, 5000, 60}. The decay
+ * factor is V8's Math.pow (fdlibm) restated bit for bit. */
+typedef struct rp_damp_config {
+    int enabled;            /* dampScoringEnabled: penalize applied updates */
+    double initial;         /* dampScoringInitial */
+    double min;             /* dampScoringMin */
+    double max;             /* dampScoringMax */
+    double penalty;         /* dampScoringPenalty */
+    double suppress_limit;  /* dampScoringSuppressLimit */
+    double half_life;       /* dampScoringHalfLife, seconds (> 0) */
+} rp_damp_config;
+
+/* Turn tracking on (first call: every id starts at `initial`, null timestamp) or change the
+ * config. Call it where the reference constructs Membership (initMembership, index.js:399-418). */
+int rp_members_damp_configure(rp_members *m, const rp_damp_config *cfg);
+/* The last update batch, per change in batch order: the member's dampScore after the change and
+ * whether 'suppressLimitExceeded' fired (member.js:141-152). k <= that batch's size. */
+int rp_members_damp_last(rp_members *m, double *score, uint8_t *exceeded, uint32_t k);
+/* The decayer tick at Date.now() = now_ms (host form syncs; _dev is stream-ordered). */
+int rp_members_damp_decay(rp_members *m, int64_t now_ms);
+int rp_members_damp_decay_dev(rp_members *m, int64_t now_ms, void *stream);
+/* Per id (cap entries, nullable outputs): dampScore, lastUpdateDampScore, lastUpdateTimestamp
+ * (0 = null). */
+int rp_members_damp_dump(rp_members *m, double *score, double *last_score, int64_t *last_ts, uint32_t cap);
+
 /* ------------------------------------------------------------------ Gossip wire bodies
  * Change records as the JSON text ringpop sends (addresses are ids interned in the members
  * handle m). Replaces the per-message JSON.stringify / safeParse of:

@@ -98,6 +98,17 @@ def lib():
         L.orc_sim_event.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32]
         L.orc_sim_set_threads.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.orc_sim_piggyback.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_js_pow.restype = ctypes.c_double
+        L.orc_js_pow.argtypes = [ctypes.c_double, ctypes.c_double]
+        L.orc_js_round.restype = ctypes.c_double
+        L.orc_js_round.argtypes = [ctypes.c_double]
+        L.orc_damp_decayed.restype = ctypes.c_double
+        L.orc_damp_decayed.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_int64, ctypes.c_int64]
+        L.orc_damp_penalized.restype = ctypes.c_double
+        L.orc_damp_penalized.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_int64, ctypes.c_int64,
+                                         ctypes.POINTER(ctypes.c_int)]
+        L.orc_damp_decay_all.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_uint32, ctypes.c_int64, ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -363,3 +374,46 @@ class Sim:
         out = np.zeros(4, dtype=np.uint64)
         lib().orc_sim_stats(self.h, out.ctypes.data)
         return dict(zip(["pings", "pingreqs", "fullsyncs", "applied"], (int(x) for x in out)))
+
+
+class DampCfg(ctypes.Structure):
+    """orc_damp_cfg (config.js:60-71 damp fields)."""
+    _fields_ = [("enabled", ctypes.c_int), ("initial", ctypes.c_double), ("min", ctypes.c_double),
+                ("max", ctypes.c_double), ("penalty", ctypes.c_double), ("suppress_limit", ctypes.c_double),
+                ("half_life", ctypes.c_double)]
+
+
+DAMP_DEFAULTS = {"dampScoringEnabled": True, "dampScoringInitial": 0, "dampScoringMin": 0, "dampScoringMax": 10000,
+                 "dampScoringPenalty": 500, "dampScoringSuppressLimit": 5000, "dampScoringHalfLife": 60}
+
+
+def damp_cfg(config=None):
+    """A DampCfg from reference config keys (missing keys take config.js's defaults)."""
+    c = dict(DAMP_DEFAULTS, **(config or {}))
+    return DampCfg(int(bool(c["dampScoringEnabled"])), c["dampScoringInitial"], c["dampScoringMin"],
+                   c["dampScoringMax"], c["dampScoringPenalty"], c["dampScoringSuppressLimit"],
+                   c["dampScoringHalfLife"])
+
+
+def js_pow(x, y):
+    return lib().orc_js_pow(x, y)
+
+
+def js_round(x):
+    return lib().orc_js_round(x)
+
+
+def damp_decayed(cfg, last_score, last_ts, now):
+    return lib().orc_damp_decayed(ctypes.byref(cfg), last_score, int(last_ts), int(now))
+
+
+def damp_penalized(cfg, last_score, last_ts, now):
+    e = ctypes.c_int()
+    s = lib().orc_damp_penalized(ctypes.byref(cfg), last_score, int(last_ts), int(now), ctypes.byref(e))
+    return s, bool(e.value)
+
+
+def damp_decay_all(cfg, exists, last_score, last_ts, now, score):
+    """In place over numpy arrays (u8, f64, i64, f64)."""
+    lib().orc_damp_decay_all(ctypes.byref(cfg), exists.ctypes.data, last_score.ctypes.data, last_ts.ctypes.data,
+                             len(exists), int(now), score.ctypes.data)

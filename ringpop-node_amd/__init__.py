@@ -115,6 +115,11 @@ SIGNATURES = {
     "rp_wire_decode": (_INT, [_P, _P, _P, _U32, _P, _U32, _P, _P, _P]),
     "rp_sim_counters": (_INT, [_P, _P]),
     "rp_members_defer_checksum": (_INT, [_P, _INT]),
+    "rp_members_damp_configure": (_INT, [_P, _P]),
+    "rp_members_damp_last": (_INT, [_P, _P, _P, _U32]),
+    "rp_members_damp_decay": (_INT, [_P, ctypes.c_int64]),
+    "rp_members_damp_decay_dev": (_INT, [_P, ctypes.c_int64, _P]),
+    "rp_members_damp_dump": (_INT, [_P, _P, _P, _P, _U32]),
     "rp_copy": (_INT, [_P, _P, _U64, _P]),
 }
 
@@ -438,6 +443,17 @@ class HashRing:
         check(lib().rp_ring_lookup_dev(self._h, keys_ptr, off_ptr, stride, n, owners_ptr, stream))
 
 
+class DampConfig(ctypes.Structure):
+    """rp_damp_config (include/ringpop_amd.h)."""
+    _fields_ = [("enabled", ctypes.c_int), ("initial", ctypes.c_double), ("min", ctypes.c_double),
+                ("max", ctypes.c_double), ("penalty", ctypes.c_double), ("suppress_limit", ctypes.c_double),
+                ("half_life", ctypes.c_double)]
+
+
+DAMP_DEFAULTS = {"dampScoringEnabled": True, "dampScoringInitial": 0, "dampScoringMin": 0, "dampScoringMax": 10000,
+                 "dampScoringPenalty": 500, "dampScoringSuppressLimit": 5000, "dampScoringHalfLife": 60}
+
+
 class Membership:
     """Device member table behind Membership.update / computeChecksum
     (lib/membership/index.js:48-123, 249-324; rules: lib/membership/member.js:71-202).
@@ -582,6 +598,41 @@ class Membership:
                    d_n_applied=None, stream=None):
         check(lib().rp_members_update_dev(self._h, d_ids, d_status, d_inc, k, int(now_ms), d_applied, d_new_status,
                                           d_new_inc, d_n_applied, stream))
+
+    # ---- flap-damping scores (member.js:45-66,133-153; index.js:330-383) ----
+    def damp_configure(self, config=None):
+        """Track dampScore on the device with the reference's config keys (config.js:60-71;
+        missing keys take its defaults)."""
+        c = dict(DAMP_DEFAULTS, **(config or {}))
+        cfg = DampConfig(int(bool(c["dampScoringEnabled"])), c["dampScoringInitial"], c["dampScoringMin"],
+                         c["dampScoringMax"], c["dampScoringPenalty"], c["dampScoringSuppressLimit"],
+                         c["dampScoringHalfLife"])
+        check(lib().rp_members_damp_configure(self._h, ctypes.byref(cfg)))
+
+    def damp_last(self, k):
+        """(score after each change, suppressLimitExceeded flags) of the last update batch of k changes."""
+        sc = np.empty(max(k, 1), dtype=np.float64)
+        ex = np.empty(max(k, 1), dtype=np.uint8)
+        check(lib().rp_members_damp_last(self._h, sc.ctypes.data, ex.ctypes.data, k))
+        return sc[:k], ex[:k]
+
+    def damp_decay(self, now_ms=None):
+        """Membership._decayMembersDampScore at Date.now() = now_ms."""
+        check(lib().rp_members_damp_decay(self._h, int(self.now() if now_ms is None else now_ms)))
+
+    def damp_decay_dev(self, now_ms, stream=None):
+        check(lib().rp_members_damp_decay_dev(self._h, int(now_ms), stream))
+
+    def damp_dump(self):
+        """Per id: dampScore, lastUpdateDampScore, lastUpdateTimestamp (0 = null)."""
+        n = ctypes.c_uint32()
+        check(lib().rp_members_count(self._h, ctypes.byref(n)))
+        m = n.value
+        sc = np.empty(max(m, 1), dtype=np.float64)
+        ls = np.empty(max(m, 1), dtype=np.float64)
+        ts = np.empty(max(m, 1), dtype=np.int64)
+        check(lib().rp_members_damp_dump(self._h, sc.ctypes.data, ls.ctypes.data, ts.ctypes.data, m))
+        return sc[:m], ls[:m], ts[:m]
 
 
 SIM_EVENT = {"kill": 0, "revive": 1, "leave": 2}

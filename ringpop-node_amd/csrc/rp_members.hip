@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/ringpop_amd.h"
+#include "rp_damp.h"
 #include "rp_hashlong.h"
 #include "rp_names.h"
 #include "rp_swim.h"
@@ -31,15 +32,29 @@ __global__ void k_sort_init(const uint32_t* __restrict__ ids, uint32_t k, uint32
     }
 }
 
+// Damp-scoring state by member id (Member.dampScore / lastUpdateDampScore /
+// lastUpdateTimestamp, member.js:35-39) and the per-change outputs of the batch being folded.
+// score == nullptr: not tracked (rp_members_damp_configure never called).
+struct DampArgs {
+    damp::Config c;
+    double* score;
+    double* last;
+    int64_t* ts;    // 0 stands for a null lastUpdateTimestamp (JS `now - null` = now)
+    double* out;    // per change: the member's dampScore after it
+    uint8_t* exc;   // per change: 'suppressLimitExceeded' emitted (member.js:141-152)
+};
+
 // One lane per id segment of the (id, arrival)-sorted batch: the sequential fold of
 // Membership.update restricted to one address (lib/membership/index.js:272-304).
 // applied: 0 = not applied, 1 = applied to an existing member, 2 = created a new member.
+// With damp tracking on, an applied update to another member takes _applyUpdatePenalty
+// (member.js:98-107, 133-153) and every applied update stamps lastUpdateTimestamp (:115-118).
 __global__ void k_fold(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv, uint32_t k,
                        const uint8_t* __restrict__ ch_status, const int64_t* __restrict__ ch_inc,
                        uint8_t* __restrict__ exists, uint8_t* __restrict__ status, int64_t* __restrict__ inc,
                        uint32_t local_id, int64_t now_ms, uint8_t* __restrict__ applied,
                        uint8_t* __restrict__ new_status, int64_t* __restrict__ new_inc,
-                       uint32_t* __restrict__ n_applied) {
+                       uint32_t* __restrict__ n_applied, DampArgs da) {
     const uint32_t gstride = gridDim.x * blockDim.x;
     for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < k; p += gstride) {
         const uint32_t id = sk[p];
@@ -47,15 +62,25 @@ __global__ void k_fold(const uint32_t* __restrict__ sk, const uint32_t* __restri
         bool ex = exists[id] != 0;
         uint8_t st = status[id];
         int64_t in = inc[id];
+        double sc = 0.0, ls = 0.0;
+        int64_t lt = 0;
+        if (da.score) {
+            sc = da.score[id];
+            ls = da.last[id];
+            lt = da.ts[id];
+        }
         uint32_t napp = 0;
         for (uint32_t q = p; q < k && sk[q] == id; q++) {
             const uint32_t j = sv[q];
             uint8_t us = ch_status[j];
             int64_t ui = ch_inc[j];
             uint8_t a;
-            if (!ex) {  // _createMember verbatim (index.js:277-291)
+            bool exc = false;
+            if (!ex) {  // _createMember verbatim (index.js:277-291): a fresh Member (member.js:28-41)
                 ex = true;
                 a = 2;
+                sc = ls = da.c.initial;
+                lt = 0;
             } else {
                 a = evaluate_update(st, in, id == local_id, us, ui, now_ms) ? 1 : 0;
             }
@@ -64,15 +89,47 @@ __global__ void k_fold(const uint32_t* __restrict__ sk, const uint32_t* __restri
                 in = ui;
                 napp++;
             }
+            if (a == 1 && da.score) {
+                if (da.c.enabled && id != local_id) {
+                    sc = damp::penalized(da.c, ls, lt, now_ms, &exc);
+                    ls = sc;
+                }
+                lt = now_ms;
+            }
             if (applied) applied[j] = a;
             if (new_status) new_status[j] = us;
             if (new_inc) new_inc[j] = ui;
+            if (da.out) {
+                da.out[j] = sc;
+                da.exc[j] = exc ? 1 : 0;
+            }
         }
         exists[id] = ex ? 1 : 0;
         status[id] = st;
         inc[id] = in;
+        if (da.score) {
+            da.score[id] = sc;
+            da.last[id] = ls;
+            da.ts[id] = lt;
+        }
         if (napp) atomicAdd(n_applied, napp);
     }
+}
+
+// Membership._decayMembersDampScore (index.js:374-383): decayDampScore on every member
+// (member.js:45-66). Reads 17 B and writes 8 B per id.
+__global__ void k_damp_decay(const uint8_t* __restrict__ exists, uint32_t n, double* __restrict__ score,
+                             const double* __restrict__ last, const int64_t* __restrict__ ts, damp::Config c,
+                             int64_t now_ms) {
+    const uint32_t gstride = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gstride)
+        if (exists[i]) score[i] = damp::decayed(c, last[i], ts[i], now_ms);
+}
+
+template <class T>
+__global__ void k_copy_fill(const T* __restrict__ a, uint32_t na, T* __restrict__ b, uint32_t nb, T fill) {
+    const uint32_t gstride = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += gstride) b[i] = i < na ? a[i] : fill;
 }
 
 // mergeMembershipChangesets (lib/membership/merge.js:22-51) over the (id, arrival)-sorted
@@ -106,11 +163,12 @@ __global__ void k_flag_nonzero(const uint32_t* __restrict__ mark, uint32_t k, ui
 
 // Membership.set (index.js:208-247) for the picked changes, in first-seen order: an existing
 // member takes the change's status and incarnation verbatim, an unknown address is created.
+// Each picked change makes a new Member (index.js:237-241), so its damp state restarts.
 __global__ void k_set_apply(const uint32_t* __restrict__ mark, const uint32_t* __restrict__ pos, uint32_t k,
                             const uint32_t* __restrict__ ids, const uint8_t* __restrict__ chs,
                             const int64_t* __restrict__ chi, uint8_t* __restrict__ exists,
                             uint8_t* __restrict__ status, int64_t* __restrict__ inc, uint32_t* __restrict__ pick,
-                            uint32_t* __restrict__ npick) {
+                            uint32_t* __restrict__ npick, DampArgs da) {
     const uint32_t gstride = gridDim.x * blockDim.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < k; i += gstride) {
         if (i == 0 && npick) *npick = pos[k];
@@ -120,6 +178,10 @@ __global__ void k_set_apply(const uint32_t* __restrict__ mark, const uint32_t* _
         exists[id] = 1;
         status[id] = chs[j];
         inc[id] = chi[j];
+        if (da.score) {
+            da.score[id] = da.last[id] = da.c.initial;
+            da.ts[id] = 0;
+        }
         if (pick) pick[pos[i]] = j;
     }
 }
@@ -219,6 +281,40 @@ struct Members {
     DevBuf<uint8_t> io_st, io_app, io_nst;
     DevBuf<int64_t> io_inc, io_ninc;
     Scratch ws;
+    // damp scoring (rp_members_damp_configure): per id score / last score / last timestamp, and
+    // the per-change score + suppress flag of the last update batch
+    bool damp_on = false;
+    damp::Config dcfg{};
+    DevBuf<double> d_score, d_last, d_out;
+    DevBuf<int64_t> d_ts;
+    DevBuf<uint8_t> d_exc;
+    uint32_t d_out_k = 0;
+
+    DampArgs damp_args(bool outputs) {
+        DampArgs a{};
+        a.c = dcfg;
+        if (damp_on) {
+            a.score = d_score.p;
+            a.last = d_last.p;
+            a.ts = d_ts.p;
+            if (outputs) {
+                a.out = d_out.p;
+                a.exc = d_exc.p;
+            }
+        }
+        return a;
+    }
+
+    template <class T>
+    void grow_one(DevBuf<T>& b, uint32_t old_n, uint32_t new_n, T fill) {
+        DevBuf<T> b2;
+        b2.reserve(new_n);
+        hipLaunchKernelGGL(k_copy_fill<T>, dim3(grid_for(new_n, 256)), dim3(256), 0, st, b.p, old_n, b2.p, new_n,
+                           fill);
+        RP_HIP(hipGetLastError());
+        RP_HIP(hipStreamSynchronize(st));
+        b.swap(b2);
+    }
 
     void grow(uint32_t need) {
         if (need <= cap) return;
@@ -235,7 +331,27 @@ struct Members {
         exists.swap(e2);
         status.swap(s2);
         inc.swap(i2);
+        if (damp_on) {
+            grow_one<double>(d_score, cap, nc, dcfg.initial);
+            grow_one<double>(d_last, cap, nc, dcfg.initial);
+            grow_one<int64_t>(d_ts, cap, nc, 0);
+        }
         cap = nc;
+    }
+
+    // rp_members_damp_configure: every member (present or not yet created) starts as a fresh
+    // Member would (member.js:35-39)
+    void damp_configure(const damp::Config& c) {
+        dcfg = c;
+        if (!damp_on) {
+            damp_on = true;
+            d_score.release();
+            d_last.release();
+            d_ts.release();
+            grow_one<double>(d_score, 0, cap, c.initial);
+            grow_one<double>(d_last, 0, cap, c.initial);
+            grow_one<int64_t>(d_ts, 0, cap, 0);
+        }
     }
 
     // Everything below is stream-ordered on `s` and never syncs with the host.
@@ -250,8 +366,13 @@ struct Members {
             int bits = 8;
             while (bits < 32 && (1ull << bits) < nt.size()) bits += 8;
             radix_sort_pairs(sk.p, sv.p, k, 0, bits, s, ws);
+            if (damp_on) {
+                d_out.reserve(k);
+                d_exc.reserve(k);
+                d_out_k = k;
+            }
             hipLaunchKernelGGL(k_fold, dim3(grid_for(k, 256)), dim3(256), 0, s, sk.p, sv.p, k, chs, chi, exists.p,
-                               status.p, inc.p, local_id, now_ms, applied, nst, ninc, napplied.p);
+                               status.p, inc.p, local_id, now_ms, applied, nst, ninc, napplied.p, damp_args(true));
             RP_HIP(hipGetLastError());
             if (!defer_ck) checksum_dev(s, napplied.p);
         }
@@ -280,7 +401,7 @@ struct Members {
         hipLaunchKernelGGL(k_flag_nonzero, dim3(grid_for(k, 256)), dim3(256), 0, s, mk.p, k, mpos.p);
         scan_exclusive_u32(mpos.p, mpos.p, k, s, ws);
         hipLaunchKernelGGL(k_set_apply, dim3(grid_for(k, 256)), dim3(256), 0, s, mk.p, mpos.p, k, ids, chs, chi,
-                           exists.p, status.p, inc.p, pick, npick);
+                           exists.p, status.p, inc.p, pick, npick, damp_args(false));
         RP_HIP(hipGetLastError());
         checksum_dev(s, nullptr);
     }
@@ -559,6 +680,62 @@ int rp_members_dump(rp_members* h, uint8_t* exists, uint8_t* status, int64_t* in
 
 int rp_members_count(rp_members* h, uint32_t* n_names) {
     return guard([&] { *n_names = MB(h).nt.size(); });
+}
+
+int rp_members_damp_configure(rp_members* h, const rp_damp_config* cfg) {
+    return guard([&] {
+        rp::Members& m = MB(h);
+        RP_REQUIRE(cfg, "damp_configure: null config");
+        RP_REQUIRE(cfg->half_life > 0.0, "damp_configure: half_life must be > 0");
+        rp::damp::Config c{cfg->enabled, cfg->initial, cfg->min, cfg->max, cfg->penalty, cfg->suppress_limit,
+                           cfg->half_life};
+        m.damp_configure(c);
+    });
+}
+
+int rp_members_damp_last(rp_members* h, double* score, uint8_t* exceeded, uint32_t k) {
+    return guard([&] {
+        rp::Members& m = MB(h);
+        RP_REQUIRE(m.damp_on, "damp_last: damp scoring is not configured");
+        RP_REQUIRE(k <= m.d_out_k, "damp_last: more changes asked for than the last batch had");
+        if (k && score) RP_HIP(hipMemcpyAsync(score, m.d_out.p, 8ull * k, hipMemcpyDeviceToHost, m.st));
+        if (k && exceeded) RP_HIP(hipMemcpyAsync(exceeded, m.d_exc.p, k, hipMemcpyDeviceToHost, m.st));
+        RP_HIP(hipStreamSynchronize(m.st));
+    });
+}
+
+int rp_members_damp_decay_dev(rp_members* h, int64_t now_ms, void* stream) {
+    return guard([&] {
+        rp::Members& m = MB(h);
+        RP_REQUIRE(m.damp_on, "damp_decay: damp scoring is not configured");
+        hipStream_t s = rp::as_stream(stream);
+        if (s != m.st) RP_HIP(hipStreamSynchronize(m.st));
+        const uint32_t n = m.nt.size();
+        if (n)
+            hipLaunchKernelGGL(rp::k_damp_decay, dim3(rp::grid_for(n, 256)), dim3(256), 0, s, m.exists.p, n,
+                               m.d_score.p, m.d_last.p, m.d_ts.p, m.dcfg, now_ms);
+        RP_HIP(hipGetLastError());
+    });
+}
+
+int rp_members_damp_decay(rp_members* h, int64_t now_ms) {
+    int rc = rp_members_damp_decay_dev(h, now_ms, nullptr);
+    if (rc) return rc;
+    return guard([&] { RP_HIP(hipStreamSynchronize(MB(h).st)); });
+}
+
+int rp_members_damp_dump(rp_members* h, double* score, double* last_score, int64_t* last_ts, uint32_t cap) {
+    return guard([&] {
+        rp::Members& m = MB(h);
+        RP_REQUIRE(m.damp_on, "damp_dump: damp scoring is not configured");
+        const uint32_t n = std::min(cap, m.nt.size());
+        if (n) {
+            if (score) RP_HIP(hipMemcpyAsync(score, m.d_score.p, 8ull * n, hipMemcpyDeviceToHost, m.st));
+            if (last_score) RP_HIP(hipMemcpyAsync(last_score, m.d_last.p, 8ull * n, hipMemcpyDeviceToHost, m.st));
+            if (last_ts) RP_HIP(hipMemcpyAsync(last_ts, m.d_ts.p, 8ull * n, hipMemcpyDeviceToHost, m.st));
+        }
+        RP_HIP(hipStreamSynchronize(m.st));
+    });
 }
 
 }  // extern "C"
