@@ -122,6 +122,8 @@ struct SimDev {
     uint8_t* st;
     int64_t* inc;
     uint32_t* order;
+    uint32_t* opos;  // inverse of order (each member's members-array position), or null
+    uint32_t xcap;   // D1 non-candidate list capacity (<= kXCap; RP_SIM_D1_XCAP lowers it)
     uint32_t* slot;  // 0 = no change, else index + 1 into the node's change list
     uint32_t* dev;   // [lv][W] rows ever changed, by address rank
     // sparse per node
@@ -1359,15 +1361,19 @@ __device__ void cursor_chunk(const SimDev& S, const LaneView& V, LaneCursor& C, 
 // so this is what bounds a refresh when few waves share a SIMD (the sharded case).
 // NP producer waves (3: 256-thread blocks; 7: 512-thread blocks, two waves per SIMD), each
 // producing 4 chunks per epoch.
+// sel != null: only the nodes listed in sel[0..*nsel) (the ping-req senders of D1, whose
+// views phases B and C just changed), 64 per workgroup in list order.
 template <int NP>
-__global__ __launch_bounds__(64 * (NP + 1)) void k_ck_pc(SimDev S) {
+__global__ __launch_bounds__(64 * (NP + 1)) void k_ck_pc(SimDev S, const uint32_t* __restrict__ sel,
+                                                         const uint32_t* __restrict__ nsel) {
     constexpr int kEp = 4 * NP;  // chunks per epoch
     __shared__ __attribute__((aligned(16))) uint32_t ring[kRingW + 24];
     __shared__ __attribute__((aligned(16))) u32x4s stage[2][kEp][2][64];
     __shared__ uint32_t s_nd[64], s_iters[64];
     __shared__ int32_t s_red[4];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t lv = blockIdx.x * 64 + lane;
+    uint32_t lv = blockIdx.x * 64 + lane;
+    if (sel) lv = lv < *nsel ? sel[lv] : NONE;
     const bool act = lv < S.NL && !S.dead[S.v0 + lv] && S.dirty[lv];
     if (!__syncthreads_or(act ? 1 : 0)) return;
     const uint32_t N = S.N;
@@ -1734,7 +1740,8 @@ __device__ void block_make(const SimDev& S, uint32_t lv, uint32_t a, uint8_t st,
     block_apply(S, lv, tmp, 1, L, now);
 }
 
-__device__ void lane0_shuffle(const SimDev& S, uint32_t lv) {
+// inv: also rewrite the row's inverse (k_opos_build does it for the start-up shuffle)
+__device__ void lane0_shuffle(const SimDev& S, uint32_t lv, bool inv) {
     const uint64_t row = (uint64_t)lv * S.N;
     const uint32_t v = S.v0 + lv;
     const uint32_t sh = S.n_shuf[lv]++;
@@ -1745,6 +1752,8 @@ __device__ void lane0_shuffle(const SimDev& S, uint32_t lv) {
         S.order[row + i] = S.order[row + j];
         S.order[row + j] = t;
     }
+    if (inv && S.opos)
+        for (uint32_t k = 0; k < S.N; k++) S.opos[row + S.order[row + k]] = k;
 }
 
 __device__ __forceinline__ bool pingable(const SimDev& S, uint64_t row, uint32_t v, uint32_t m) {
@@ -1770,7 +1779,7 @@ __device__ int32_t lane0_iter_next(const SimDev& S, uint32_t lv, uint32_t* list,
                 for (uint32_t q = 0; q < steps; q++) bits[list[q] >> 5] |= 1u << (list[q] & 31);
                 wrapped = true;
             }
-            lane0_shuffle(S, lv);
+            lane0_shuffle(S, lv, true);
         }
         S.it_idx[lv] = idx;
         const uint32_t m = S.order[row + idx];
@@ -1883,12 +1892,36 @@ __global__ void k_d1_list(SimDev S, uint32_t* __restrict__ list, uint32_t* __res
     }
 }
 
-// D1: ping-req fan-out for senders whose target is dead (one workgroup per listed sender)
+constexpr uint32_t kXCap = 2048;  // non-candidates a D1 sender sorts in LDS (more: the scan path)
+
+// The k-th (0-based) members-array position outside the sorted position set xs[0..n): with
+// y_i = xs[i] - i (non-decreasing), it is k + #{i : y_i <= k}.
+__device__ __forceinline__ uint32_t d1_select(const uint32_t* xs, uint32_t n, uint32_t k) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (xs[mid] - mid <= k)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return k + lo;
+}
+
+// D1: ping-req fan-out for senders whose target is dead (one workgroup per listed sender).
+// getRandomPingableMembers(3, [target]) (index.js:141-150) is _.sample over the members array
+// minus the non-candidates: self, the target, and members whose status is faulty / leave. Only
+// members whose row ever changed can be faulty / leave, so the non-candidates come from the
+// view's deviation bitmap (N/32 words), their positions from the inverse permutation; sorted in
+// LDS they turn each index the partial Fisher-Yates draws into a position by a binary search.
+// The draws, the swaps and so the helpers are the scan path's (kept for views with more than
+// kXCap non-candidates, or when the inverse is not allocated).
 __global__ __launch_bounds__(kT) void k_phase_d1(SimDev S, const uint32_t* __restrict__ list,
                                                  const uint32_t* __restrict__ nlist) {
     __shared__ Lds L;
     __shared__ Rec tmp;
-    __shared__ uint32_t ncand;
+    __shared__ uint32_t ncand, nx;
+    __shared__ uint32_t xs[kXCap];
     const int64_t now = S.now0 + 200 * S.round;
     uint32_t* cand = S.cand + (uint64_t)blockIdx.x * S.N;
     const uint32_t nl = *nlist;
@@ -1898,37 +1931,113 @@ __global__ __launch_bounds__(kT) void k_phase_d1(SimDev S, const uint32_t* __res
         const int32_t t = S.target[lv];
         const uint64_t row = (uint64_t)lv * S.N;
         if (threadIdx.x == 0) atomicAdd(&S.stats[1], 1ull);
-        // candidates: members-array order, pingable, not the target (index.js:141-150)
-        uint32_t written = 0;
-        for (uint32_t base = 0; base < S.N; base += kT) {
-            const uint32_t k = base + threadIdx.x;
-            bool ok = false;
-            uint32_t m = 0;
-            if (k < S.N) {
-                m = S.order[row + k];
-                ok = m != (uint32_t)t && pingable(S, row, v, m);
+        bool fast = S.opos != nullptr;
+        if (fast) {
+            if (threadIdx.x == 0) {
+                xs[0] = S.opos[row + v];
+                xs[1] = S.opos[row + (uint32_t)t];
+                nx = 2;
             }
-            uint32_t tot;
-            const uint32_t p = block_scan(ok ? 1u : 0u, L.u, &tot);
-            if (ok) cand[written + p] = m;
-            written += tot;
+            __syncthreads();
+            const uint32_t* dv = S.dev + (uint64_t)lv * S.W;
+            for (uint32_t w = threadIdx.x; w < S.W; w += kT) {
+                uint32_t bits = dv[w];
+                while (bits) {
+                    const uint32_t m = S.sorted[w * 32u + (uint32_t)__builtin_ctz(bits)];
+                    bits &= bits - 1u;
+                    if (m != v && m != (uint32_t)t && !pingable(S, row, v, m)) {
+                        const uint32_t q = atomicAdd(&nx, 1u);
+                        if (q < S.xcap) xs[q] = S.opos[row + m];
+                    }
+                }
+            }
+            __syncthreads();
+            fast = nx <= S.xcap;
         }
-        if (threadIdx.x == 0) ncand = written;
-        __syncthreads();
-        __threadfence_block();
-        if (threadIdx.x == 0) {
-            const uint32_t len = ncand;
-            const uint32_t nh = len < 3 ? len : 3;
-            for (uint32_t i = 0; i < nh; i++) {  // _.sample -> partial Fisher-Yates (SAMP stream)
-                const uint32_t r = philox_u32(S.seed, TAG_SAMP, (uint32_t)S.round, i, v);
-                const uint32_t j = i + (uint32_t)(((uint64_t)r * (len - i)) >> 32);
-                const uint32_t x = cand[i];
-                cand[i] = cand[j];
-                cand[j] = x;
-                S.helpers[lv * 3 + i] = cand[i];
+        if (fast) {
+            const uint32_t n = nx;
+            uint32_t P = 1;
+            while (P < n) P <<= 1;
+            for (uint32_t i = n + threadIdx.x; i < P; i += kT) xs[i] = 0xFFFFFFFFu;
+            __syncthreads();
+            for (uint32_t size = 2; size <= P; size <<= 1) {  // bitonic sort, ascending
+                for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+                    for (uint32_t i = threadIdx.x; i < P; i += kT) {
+                        const uint32_t j = i ^ stride;
+                        if (j > i) {
+                            const uint32_t a = xs[i], b = xs[j];
+                            if ((a > b) == ((i & size) == 0)) {
+                                xs[i] = b;
+                                xs[j] = a;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                }
             }
-            S.nhelp[lv] = nh;
-            ncand = nh;
+            if (threadIdx.x == 0) {
+                const uint32_t len = S.N - n;
+                const uint32_t nh = len < 3 ? len : 3;
+                uint32_t key[6], val[6], nk = 0;  // the candidate slots the swaps have rewritten
+                auto get = [&](uint32_t q) -> uint32_t {
+                    for (uint32_t z = 0; z < nk; z++)
+                        if (key[z] == q) return val[z];
+                    return S.order[row + d1_select(xs, n, q)];
+                };
+                auto put = [&](uint32_t q, uint32_t x) {
+                    for (uint32_t z = 0; z < nk; z++)
+                        if (key[z] == q) {
+                            val[z] = x;
+                            return;
+                        }
+                    key[nk] = q;
+                    val[nk] = x;
+                    nk++;
+                };
+                for (uint32_t i = 0; i < nh; i++) {  // _.sample -> partial Fisher-Yates (SAMP stream)
+                    const uint32_t r = philox_u32(S.seed, TAG_SAMP, (uint32_t)S.round, i, v);
+                    const uint32_t j = i + (uint32_t)(((uint64_t)r * (len - i)) >> 32);
+                    const uint32_t a = get(i), b = get(j);
+                    put(i, b);
+                    put(j, a);
+                    S.helpers[lv * 3 + i] = b;
+                }
+                S.nhelp[lv] = nh;
+                ncand = nh;
+            }
+        } else {
+            // candidates: members-array order, pingable, not the target (index.js:141-150)
+            uint32_t written = 0;
+            for (uint32_t base = 0; base < S.N; base += kT) {
+                const uint32_t k = base + threadIdx.x;
+                bool ok = false;
+                uint32_t m = 0;
+                if (k < S.N) {
+                    m = S.order[row + k];
+                    ok = m != (uint32_t)t && pingable(S, row, v, m);
+                }
+                uint32_t tot;
+                const uint32_t p = block_scan(ok ? 1u : 0u, L.u, &tot);
+                if (ok) cand[written + p] = m;
+                written += tot;
+            }
+            if (threadIdx.x == 0) ncand = written;
+            __syncthreads();
+            __threadfence_block();
+            if (threadIdx.x == 0) {
+                const uint32_t len = ncand;
+                const uint32_t nh = len < 3 ? len : 3;
+                for (uint32_t i = 0; i < nh; i++) {  // _.sample -> partial Fisher-Yates (SAMP stream)
+                    const uint32_t r = philox_u32(S.seed, TAG_SAMP, (uint32_t)S.round, i, v);
+                    const uint32_t j = i + (uint32_t)(((uint64_t)r * (len - i)) >> 32);
+                    const uint32_t x = cand[i];
+                    cand[i] = cand[j];
+                    cand[j] = x;
+                    S.helpers[lv * 3 + i] = cand[i];
+                }
+                S.nhelp[lv] = nh;
+                ncand = nh;
+            }
         }
         __syncthreads();
         if (ncand == 0) {
@@ -2299,7 +2408,15 @@ __global__ void k_sim_init(SimDev S) {
 
 __global__ void k_sim_start(SimDev S) {  // gossip.start -> membership.shuffle() on live nodes
     for (uint32_t lv = blockIdx.x * blockDim.x + threadIdx.x; lv < S.NL; lv += gridDim.x * blockDim.x)
-        if (!S.dead[S.v0 + lv]) lane0_shuffle(S, lv);
+        if (!S.dead[S.v0 + lv]) lane0_shuffle(S, lv, false);
+}
+
+// opos = the inverse of every row of order (one workgroup per row)
+__global__ void k_opos_build(SimDev S) {
+    for (uint32_t lv = blockIdx.x; lv < S.NL; lv += gridDim.x) {
+        const uint64_t row = (uint64_t)lv * S.N;
+        for (uint32_t k = threadIdx.x; k < S.N; k += blockDim.x) S.opos[row + S.order[row + k]] = k;
+    }
 }
 
 // every node starts with the same view: hash it once, copy to all
@@ -2356,6 +2473,7 @@ struct Sim {
     DevBuf<int64_t> inc, it_idx, inc_snap, inc0;
     DevBuf<int32_t> target;
     DevBuf<uint32_t> slot;
+    DevBuf<uint32_t> opos;
     DevBuf<uint32_t> order, dev, n_chg, n_tim, n_shuf, ring_count, max_piggy, checksum, ck_snap, ping_n, leg_n,
         helpers, nhelp, leg_nk, cand, rank, err, bounds, want, conv, leave_list;
     DevBuf<uint32_t> okey, oval, ocnt, ooff, omoff;  // outbox build
@@ -2400,9 +2518,9 @@ struct Sim {
         const char* m = getenv("RP_SIM_CK");
         const bool pc = m ? strcmp(m, "lanes") != 0 : groups <= cus;
         if (pc && !(m && !strcmp(m, "pc3")))
-            hipLaunchKernelGGL(k_ck_pc<7>, dim3(groups), dim3(512), 0, st, d);
+            hipLaunchKernelGGL(k_ck_pc<7>, dim3(groups), dim3(512), 0, st, d, nullptr, nullptr);
         else if (pc)
-            hipLaunchKernelGGL(k_ck_pc<3>, dim3(groups), dim3(256), 0, st, d);
+            hipLaunchKernelGGL(k_ck_pc<3>, dim3(groups), dim3(256), 0, st, d, nullptr, nullptr);
         else
             hipLaunchKernelGGL(k_ck_lanes, dim3(grid_for(NL, 256, 1u << 20)), dim3(256), 0, st, d);
         RP_HIP(hipGetLastError());
@@ -2550,6 +2668,10 @@ struct Sim {
                 d1list.reserve(NL + 1);
                 RP_HIP(hipMemsetAsync(d1list.p + NL, 0, 4, st));
                 hipLaunchKernelGGL(k_d1_list, dim3(grid_for(NL, 256)), dim3(256), 0, st, d, d1list.p, d1list.p + NL);
+                // the senders' checksums (their ping-req bodies carry them) as side-by-side chains
+                // first, so D1's workgroups find their views clean
+                if (!getenv("RP_SIM_D1_BLOCKCK"))
+                    hipLaunchKernelGGL(k_ck_pc<7>, dim3((NL + 63) / 64), dim3(512), 0, st, d, d1list.p, d1list.p + NL);
                 hipLaunchKernelGGL(k_phase_d1, dim3(g), dim3(kT), 0, st, d, d1list.p, d1list.p + NL);
             }
             build_out(K_LEG);
@@ -2781,6 +2903,10 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
         S.bounds.reserve(nshards + 1);
         S.pool.reserve(2 * L1 * cap + arena);
         S.cand.reserve((uint64_t)S.grid * n);
+        // the inverse permutation that makes D1 sub-linear (RP_SIM_OPOS_BYTES = 0 turns it off:
+        // every ping-req sender then scans its members array)
+        const bool use_opos = NN * 4ull <= env_u64("RP_SIM_OPOS_BYTES", 64ull << 30);
+        if (use_opos) S.opos.reserve(NN + 1);
         // lane checksums list each view's deviated pieces (16 B each); a view with more than dcap
         // falls back to scanning its bitmap
         uint64_t dcap = std::min<uint64_t>(n, 2ull * ndead + 256);
@@ -2809,6 +2935,8 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
         d.seed = seed; d.susp = suspicion_rounds; d.now0 = now0;
         d.Cd = (uint32_t)cap; d.Ct = (uint32_t)cap; d.Cm = (uint32_t)cap;
         d.st = S.st_.p; d.inc = S.inc.p; d.order = S.order.p; d.slot = S.slot.p; d.dev = S.dev.p;
+        d.opos = use_opos ? S.opos.p : nullptr;
+        d.xcap = (uint32_t)std::max<uint64_t>(2, std::min<uint64_t>(rp::kXCap, env_u64("RP_SIM_D1_XCAP", rp::kXCap)));
         d.chg = S.chg.p; d.n_chg = S.n_chg.p; d.tim = S.tim.p; d.n_tim = S.n_tim.p;
         d.it_idx = S.it_idx.p; d.n_shuf = S.n_shuf.p; d.ring_count = S.ring_count.p; d.max_piggy = S.max_piggy.p;
         d.checksum = S.checksum.p; d.dirty = S.dirty.p; d.dead = S.dead.p; d.stopped = S.stopped.p;
@@ -2833,6 +2961,8 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
         hipLaunchKernelGGL(rp::k_sim_init, dim3(rp::grid_for(NN + 1, 256, 8192)), dim3(256), 0, S.st, d);
         if (NL) {
             hipLaunchKernelGGL(rp::k_sim_start, dim3(rp::grid_for(NL, 64)), dim3(64), 0, S.st, d);
+            if (d.opos)
+                hipLaunchKernelGGL(rp::k_opos_build, dim3(std::min<uint32_t>(NL, 4096)), dim3(256), 0, S.st, d);
             hipLaunchKernelGGL(rp::k_sim_first_checksum, dim3(1), dim3(64), 0, S.st, d);
             hipLaunchKernelGGL(rp::k_sim_bcast_checksum, dim3(rp::grid_for(NL, 256)), dim3(256), 0, S.st, d);
         }

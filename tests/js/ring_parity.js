@@ -62,6 +62,7 @@ input.cases.forEach(function (c) {
             (want[d] = want[d] || []).push(k);
         });
         eq(tag + ' groupByOwner', ring.groupByOwner(b.keys, 'self:0'), want);
+        eq(tag + ' groupBy (the documented handleOrProxyAll line)', ring.groupBy ? ring.groupBy(b.keys, 'self:0') : null, want);
         eq(tag + ' lookupKeys', ring.lookupKeys(b.keys, 'self:0'), Object.keys(want));
         // the single-key forms on a few keys
         for (var i = 0; i < Math.min(4, b.keys.length); i++) {

@@ -54,6 +54,25 @@ def test_sim_matches_reference_goldens(gpu, case_name):
     sim.close()
 
 
+@pytest.mark.parametrize("mode", ["scan", "xcap3"])
+def test_sim_d1_paths_match_reference_goldens(gpu, monkeypatch, mode):
+    """Phase D1's two ways of drawing ping-req helpers give the reference's helpers: the members-
+    array scan (RP_SIM_OPOS_BYTES=0: no inverse permutation) and the mixed run where views with
+    more than 3 non-candidates scan while the others select through the sorted non-candidate
+    positions (RP_SIM_D1_XCAP=3). The default run (the goldens above) selects everywhere."""
+    if mode == "scan":
+        monkeypatch.setenv("RP_SIM_OPOS_BYTES", "0")
+    else:
+        monkeypatch.setenv("RP_SIM_D1_XCAP", "3")
+    for case in gu.load("sim_golden.json")["cases"]:
+        names, sim = _golden_sim(gpu, case)
+        for r, want in enumerate(case["checksums"]):
+            sim.step()
+            assert sim.checksums().tolist() == want, (case["name"], r)
+        assert sim.stats()["fullsyncs"] == case["fullSyncs"]
+        sim.close()
+
+
 @pytest.mark.parametrize("case_name", ["n40-leave", "n24-revive", "n64-half-leave"])
 def test_sharded_sim_matches_reference_goldens(gpu, case_name):
     """The same scenario goldens through the sharded path (3 shard handles, message exchanges
