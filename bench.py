@@ -324,9 +324,10 @@ def sim_bench(rpa, torch, dist, local, n=10_000, kill_pct=1, seed=11, max_rounds
     while rounds < max_rounds and time.perf_counter() - t0 < max_seconds:
         a = time.perf_counter()
         sim.step(1)
+        c = sim.converged()  # syncs the round; collective when sharded (every rank leaves together)
         per_round.append(time.perf_counter() - a)
         rounds += 1
-        if sim.converged():  # collective when sharded: every rank leaves at the same round
+        if c:
             conv = True
             break
     torch.cuda.synchronize()

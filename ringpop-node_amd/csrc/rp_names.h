@@ -28,6 +28,10 @@ struct NameTable {
     DevBuf<uint32_t> sorted;
     uint32_t sorted_n = 0;
     DevBuf<uint32_t> tmp;
+    // open-addressing index over the device names: 2^hbits slots holding ids (0xFFFFFFFF empty),
+    // keyed by farmhash32 of the name, linear probing (the wire decoder's interning)
+    DevBuf<uint32_t> htab;
+    uint32_t htab_n = 0, hbits = 0;
 
     uint32_t size() const { return (uint32_t)names.size(); }
     uint32_t find(const char* s, uint32_t n) const;
@@ -36,6 +40,8 @@ struct NameTable {
     void sync(hipStream_t st);
     // (re)sort ids by name on the device if names were added
     void sort(hipStream_t st, Scratch& ws);
+    // (re)build htab if names were added
+    void hash_index(hipStream_t st);
 };
 
 }  // namespace rp

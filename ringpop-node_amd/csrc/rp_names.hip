@@ -1,6 +1,7 @@
 // rp_names.hip — interned address table: host map + device mirror + device byte-order sort.
 #include <algorithm>
 
+#include "rp_farmhash.h"
 #include "rp_names.h"
 
 namespace rp {
@@ -25,7 +26,33 @@ __global__ void k_name_chunk(const uint8_t* __restrict__ names, const uint64_t* 
     }
 }
 
+__global__ void k_name_hash_insert(const uint8_t* __restrict__ names, const uint64_t* __restrict__ noff, uint32_t n,
+                                   uint32_t* __restrict__ htab, uint32_t mask) {
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gstride) {
+        const uint64_t b = noff[i];
+        uint32_t slot = fh::hash32(fh::PtrSrc{names + b}, (uint32_t)(noff[i + 1] - b)) & mask;
+        while (atomicCAS(&htab[slot], 0xFFFFFFFFu, (uint32_t)i) != 0xFFFFFFFFu) slot = (slot + 1) & mask;
+    }
+}
+
 }  // namespace
+
+void NameTable::hash_index(hipStream_t st) {
+    const uint32_t n = (uint32_t)names.size();
+    if (htab_n == n && htab.p) return;
+    sync(st);
+    uint32_t b = 4;
+    while ((1ull << b) < 2ull * n) b++;  // load factor <= 1/2
+    htab.reserve(1ull << b);
+    RP_HIP(hipMemsetAsync(htab.p, 0xFF, 4ull << b, st));
+    if (n)
+        hipLaunchKernelGGL(k_name_hash_insert, dim3(grid_for(n, 256)), dim3(256), 0, st, d_bytes.p, d_noff.p, n,
+                           htab.p, (1u << b) - 1u);
+    RP_HIP(hipGetLastError());
+    hbits = b;
+    htab_n = n;
+}
 
 uint32_t NameTable::find(const char* s, uint32_t n) const {
     auto it = ids.find(std::string(s, n));

@@ -44,6 +44,8 @@ struct Names {
     const uint64_t* off;
     const uint32_t* sorted;
     uint32_t n;
+    const uint32_t* htab;  // NameTable::htab (hash index of the names)
+    uint32_t hmask;
 };
 
 // ------------------------------------------------------------------ encoder
@@ -350,15 +352,15 @@ __device__ int name_cmp(const Names& nm, const uint8_t* s, uint32_t len, uint32_
     return len == l2 ? 0 : (len < l2 ? -1 : 1);
 }
 
+// the interned id of the bytes s[0..len), or NULL_ID: one farmhash32 and, expected, about one
+// probe of the names' hash index
 __device__ uint32_t name_find(const Names& nm, const uint8_t* s, uint32_t len) {
-    uint32_t lo = 0, hi = nm.n;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        const int c = name_cmp(nm, s, len, nm.sorted[mid]);
-        if (c == 0) return nm.sorted[mid];
-        if (c < 0) hi = mid; else lo = mid + 1;
+    uint32_t slot = fh::hash32(fh::PtrSrc{s}, len) & nm.hmask;
+    while (true) {
+        const uint32_t id = nm.htab[slot];
+        if (id == NULL_ID || name_cmp(nm, s, len, id) == 0) return id;
+        slot = (slot + 1) & nm.hmask;
     }
-    return NULL_ID;
 }
 
 template <int N>
@@ -552,9 +554,11 @@ __device__ uint32_t parse_changes(Parser& P, const Names& nm, const Out& O, uint
     return n;
 }
 
+// slow != null: only the messages the wave kernel left (slow[m] != 0)
 template <bool FILL>
-__global__ void k_decode(In I, Names nm, Out O, uint32_t n_msgs) {
+__global__ void k_decode(In I, Names nm, Out O, uint32_t n_msgs, const uint8_t* __restrict__ slow) {
     for (uint32_t m = blockIdx.x * blockDim.x + threadIdx.x; m < n_msgs; m += gridDim.x * blockDim.x) {
+        if (slow && !slow[m]) continue;
         Parser P{I.buf, I.msg_off[m], I.msg_off[m + 1]};
         const uint64_t k0 = FILL ? O.rec_off[m] : 0;
         const uint64_t kend = FILL ? O.rec_off[m + 1] : 0;
@@ -618,13 +622,487 @@ __global__ void k_decode(In I, Names nm, Out O, uint32_t n_msgs) {
     }
 }
 
+// ---- the wave-per-message decoder
+//
+// One wave stages a message in LDS with coalesced loads, then classifies its bytes 64 at a
+// time: a ballot of quotes gives, by a prefix parity, which bytes lie inside strings (the
+// grammar has no escapes: any backslash or control byte sends the message to the thread
+// parser); the quotes and the structural characters outside strings become a compacted token
+// list, and a second ballot pass gives each token's nesting depth. The body object's keys are
+// walked wave-uniformly, the records of the changes array are found as the '{' tokens one
+// level inside it and parsed one lane per record. Anything the wave parser does not accept
+// exactly as the thread parser would (k_decode: its grammar and its error offsets) is left to
+// the thread parser: the wave kernel marks it in `slow` and k_decode picks only those up.
+constexpr uint32_t kWBuf = 8192;  // message bytes staged per wave (longer: the thread parser)
+constexpr uint32_t kWTok = 2048;  // quotes + structural characters per message
+constexpr uint32_t kWLvl = 1024;  // array-level tokens (records + separators)
+constexpr int kDecWaves = 4;
+
+struct WaveLds {
+    uint32_t buf[kWBuf / 4 + 2];
+    uint16_t pos[kWTok];   // token byte offset in the message
+    int16_t dep[kWTok];    // depth before the token ({ [ open, } ] close)
+    uint16_t lvl[kWLvl];   // the changes array's level tokens
+    uint64_t scal[kWBuf / 64 + 1];  // bytes outside strings that are neither tokens nor whitespace
+    uint16_t op1[32], cl2[32];      // openers at depth 1 / closers at depth 2, in order: the k-th pair
+};
+
+__device__ __forceinline__ bool wave_isws(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+__device__ __forceinline__ bool wave_isopen(uint8_t c) { return c == '{' || c == '['; }
+__device__ __forceinline__ bool wave_isclose(uint8_t c) { return c == '}' || c == ']'; }
+
+struct WaveMsg {
+    const WaveLds* W;
+    const uint8_t* b;  // message byte 0 in LDS
+    uint32_t len, ntok;
+    __device__ uint8_t at(uint32_t i) const { return b[i]; }
+    __device__ uint8_t tch(uint32_t t) const { return b[W->pos[t]]; }
+    // no scalar byte strictly between byte offsets lo and hi
+    __device__ bool clean(uint32_t lo, uint32_t hi) const {
+        for (uint32_t i = lo + 1; i < hi;) {
+            const uint64_t w = W->scal[i >> 6] >> (i & 63);
+            if (w == 0) {
+                i = (i | 63) + 1;
+                continue;
+            }
+            return (uint32_t)__builtin_ctzll(w) + i >= hi;
+        }
+        return true;
+    }
+    // the scalar strictly between tokens t and t + 1: [s, e) without surrounding whitespace;
+    // false when it is empty or holds whitespace inside
+    __device__ bool scalar(uint32_t t, uint32_t& s, uint32_t& e) const {
+        uint32_t lo = W->pos[t] + 1, hi = t + 1 < ntok ? W->pos[t + 1] : len;
+        while (lo < hi && wave_isws(at(lo))) lo++;
+        while (hi > lo && wave_isws(at(hi - 1))) hi--;
+        if (lo == hi) return false;
+        for (uint32_t i = lo; i < hi; i++)
+            if (wave_isws(at(i))) return false;
+        s = lo;
+        e = hi;
+        return true;
+    }
+    // Parser::integer over [s, e): -?[0-9]{1,18}
+    __device__ bool integer(uint32_t s, uint32_t e, int64_t& v) const {
+        bool neg = false;
+        if (s < e && at(s) == '-') {
+            neg = true;
+            s++;
+        }
+        if (s == e || e - s > 18) return false;
+        uint64_t x = 0;
+        for (uint32_t i = s; i < e; i++) {
+            const uint8_t c = at(i);
+            if (c < '0' || c > '9') return false;
+            x = x * 10 + (c - '0');
+        }
+        v = neg ? -(int64_t)x : (int64_t)x;
+        return true;
+    }
+    // the token closing the nested value opened at token t (same depth after it)
+    __device__ uint32_t match(uint32_t t) const {
+        const int16_t d = W->dep[t];
+        for (uint32_t u = t + 1; u < ntok; u++)
+            if (W->dep[u] == d + 1 && wave_isclose(tch(u))) return u;
+        return ntok;
+    }
+    // a value starting at token t (after ':' at token t - 1): returns the token after it, or
+    // ntok on anything the thread parser would not skip the same way
+    __device__ uint32_t skip(uint32_t t) const {
+        if (t >= ntok) return ntok;
+        const uint8_t c = tch(t);
+        if (c == '"') return clean(W->pos[t - 1], W->pos[t]) ? t + 2 : ntok;
+        if (wave_isopen(c)) {
+            if (!clean(W->pos[t - 1], W->pos[t])) return ntok;
+            const uint32_t u = match(t);
+            return u < ntok ? u + 1 : ntok;
+        }
+        uint32_t s, e;
+        return scalar(t - 1, s, e) ? t : ntok;  // t is the ',' / '}' after the scalar
+    }
+};
+
+template <int N>
+__device__ bool wave_key(const WaveMsg& M, uint32_t t, const char (&k)[N]) {
+    return key_is(M.b + M.W->pos[t] + 1, (uint32_t)(M.W->pos[t + 1] - M.W->pos[t] - 1), k);
+}
+
+// One record object, tokens [t0 = '{', t1 = its '}'], parsed by one lane. false: leave the
+// message to the thread parser.
+template <bool FILL>
+__device__ bool wave_record(const WaveMsg& M, const Names& nm, const Out& O, uint64_t base, uint32_t t0, uint32_t t1,
+                            uint64_t k, uint64_t kend) {
+    uint32_t addr = NULL_ID, src = NULL_ID, alen = 0;
+    uint64_t aoff = 0, idoff = ~0ull;
+    uint8_t st = 0xFF;
+    int64_t inc = 0, sinc = LLONG_MIN;
+    bool has_inc = false;
+    uint32_t t = t0 + 1;
+    if (t >= t1) return false;  // {} : no address
+    while (true) {
+        // "key" :
+        if (t + 2 >= t1 || M.tch(t) != '"' || M.tch(t + 1) != '"' || M.tch(t + 2) != ':') return false;
+        if (!M.clean(M.W->pos[t - 1], M.W->pos[t]) || !M.clean(M.W->pos[t + 1], M.W->pos[t + 2])) return false;
+        const uint32_t kt = t;
+        const uint32_t v = t + 3;
+        const uint8_t* kp = M.b + M.W->pos[kt] + 1;
+        const uint32_t kl = (uint32_t)(M.W->pos[kt + 1] - M.W->pos[kt] - 1);
+        // 1 address, 2 source, 3 status, 4 id, 5 incarnationNumber, 6 sourceIncarnationNumber
+        const int kind = key_is(kp, kl, "address") ? 1 : key_is(kp, kl, "source") ? 2 : key_is(kp, kl, "status") ? 3
+                       : key_is(kp, kl, "id") ? 4 : key_is(kp, kl, "incarnationNumber") ? 5
+                       : key_is(kp, kl, "sourceIncarnationNumber") ? 6 : 0;
+        uint32_t nx;
+        if (kind >= 1 && kind <= 4) {
+            if (v + 1 >= t1 || M.tch(v) != '"' || !M.clean(M.W->pos[v - 1], M.W->pos[v])) return false;
+            const uint32_t so = M.W->pos[v] + 1, sl = M.W->pos[v + 1] - so;
+            if (kind == 1) {
+                aoff = base + so;
+                alen = sl;
+                if (FILL) addr = name_find(nm, M.b + so, sl);
+            } else if (kind == 2) {
+                if (FILL) src = name_find(nm, M.b + so, sl);
+            } else if (kind == 3) {
+                st = status_code(M.b + so, sl);
+                if (st == 0xFF) return false;
+            } else {
+                idoff = base + so;
+            }
+            nx = v + 2;
+        } else if (kind >= 5) {
+            uint32_t s, e;
+            int64_t x;
+            if (v >= t1 + 1 || !M.scalar(kt + 2, s, e) || !M.integer(s, e, x)) return false;
+            if (kind == 5) {
+                inc = x;
+                has_inc = true;
+            } else {
+                sinc = x;
+            }
+            nx = v;
+        } else {
+            nx = M.skip(v);
+            if (nx > t1) return false;
+        }
+        // , or }
+        if (nx > t1) return false;
+        const uint8_t c = M.tch(nx);
+        if (!M.clean(M.W->pos[nx - 1], M.W->pos[nx]) && M.tch(nx - 1) != ':') return false;
+        if (nx == t1) {
+            if (c != '}') return false;
+            break;
+        }
+        if (c != ',') return false;
+        t = nx + 1;
+    }
+    if (alen == 0 || st == 0xFF || !has_inc) return false;
+    if (FILL && k < kend && k < O.rec_cap) {
+        O.addr[k] = addr;
+        O.status[k] = st;
+        O.inc[k] = inc;
+        if (O.src) O.src[k] = src;
+        if (O.src_inc) O.src_inc[k] = sinc;
+        if (O.id_off) O.id_off[k] = idoff;
+        if (O.addr_off) O.addr_off[k] = aoff;
+        if (O.addr_len) O.addr_len[k] = alen;
+    }
+    return true;
+}
+
+#ifdef RP_WIRE_PROF
+__device__ unsigned long long g_wprof[8];
+#define WPROF(k)                                                   \
+    do {                                                           \
+        const uint64_t t_ = clock64();                             \
+        if (lane == 0) atomicAdd(&g_wprof[k], t_ - tprof);         \
+        tprof = t_;                                                \
+    } while (0)
+#else
+#define WPROF(k) \
+    do {         \
+    } while (0)
+#endif
+
+template <bool FILL>
+__global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, Out O, uint32_t n_msgs,
+                                                                 uint64_t vb, uint64_t ve, uint8_t* __restrict__ slow) {
+    __shared__ WaveLds lds[kDecWaves];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    WaveLds& W = lds[wv];
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const uint32_t nwaves = gridDim.x * kDecWaves;
+    for (uint32_t m = blockIdx.x * kDecWaves + wv; m < n_msgs; m += nwaves) {
+        if (FILL && slow[m]) continue;
+#ifdef RP_WIRE_PROF
+        uint64_t tprof = clock64();
+#endif
+        const uint64_t b0 = I.msg_off[m], b1 = I.msg_off[m + 1];
+        const uint64_t len64 = b1 - b0;
+        bool ok = len64 > 0 && len64 <= kWBuf;
+        const uintptr_t p0 = reinterpret_cast<uintptr_t>(I.buf) + b0;
+        const uint32_t sh = (uint32_t)(p0 & 3u);
+        const uint32_t len = ok ? (uint32_t)len64 : 0u;
+        // stage: dwords wholly inside the batch's bytes [vb, ve), byte loads at the edges
+        if (ok) {  // all loads in flight before the first LDS store
+            constexpr int kIt = (kWBuf / 4 + 2 + 63) / 64;
+            const uintptr_t a0 = p0 - sh;
+            const uint32_t nd = (sh + len + 3) / 4;
+            uint32_t xs[kIt];
+#pragma unroll
+            for (int q = 0; q < kIt; q++) {
+                const uint32_t d = lane + 64u * q;
+                const uintptr_t a = a0 + 4ull * d;
+                xs[q] = 0;
+                if (d < nd) {
+                    if (a >= vb && a + 4 <= ve) {
+                        xs[q] = *reinterpret_cast<const uint32_t*>(a);
+                    } else {
+                        for (uint32_t j = 0; j < 4; j++)
+                            if (a + j >= p0 && a + j < p0 + len)
+                                xs[q] |= (uint32_t)(*reinterpret_cast<const uint8_t*>(a + j)) << (8 * j);
+                    }
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < kIt; q++)
+                if (lane + 64u * q < nd) W.buf[lane + 64u * q] = xs[q];
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        WPROF(0);
+        const uint8_t* B = reinterpret_cast<const uint8_t*>(W.buf) + sh;
+        // classify 64 bytes at a time
+        uint32_t ntok = 0, quotes = 0;
+        bool bad = false;
+        for (uint32_t c4 = 0; ok && c4 < len; c4 += 256) {
+          uint8_t chs[4];  // four chunks' bytes read together: one LDS latency per 256 bytes
+#pragma unroll
+          for (int u = 0; u < 4; u++) chs[u] = c4 + 64u * u + lane < len ? B[c4 + 64u * u + lane] : (uint8_t)' ';
+#pragma unroll
+          for (int u = 0; u < 4; u++) {
+            const uint32_t c0 = c4 + 64u * u;
+            if (c0 >= len) break;
+            const uint32_t i = c0 + lane;
+            const bool in = i < len;
+            const uint8_t ch = chs[u];
+            const bool q = ch == '"';
+            const uint64_t Q = __ballot(q);
+            const bool instr = ((quotes + __popcll(Q & (lt | (1ull << lane)))) & 1u) != 0;  // opening quote + body
+            const bool str_body = instr && !q;
+            const bool structural = !instr && !q &&
+                                    (ch == '{' || ch == '}' || ch == '[' || ch == ']' || ch == ':' || ch == ',');
+            const bool tok = in && (q || structural);
+            const bool ws = wave_isws(ch);
+            const bool ctrl = in && ((ch < 0x20 && !(ws && !str_body)) || ch == '\\');
+            const uint64_t T = __ballot(tok);
+            const uint64_t S = __ballot(in && !instr && !tok && !ws);
+            bad |= __ballot(ctrl) != 0;
+            const uint32_t idx = ntok + (uint32_t)__popcll(T & lt);
+            if (tok && idx < kWTok) W.pos[idx] = (uint16_t)i;
+            if (lane == 0) W.scal[c0 >> 6] = S;
+            ntok += (uint32_t)__popcll(T);
+            quotes += (uint32_t)__popcll(Q);
+          }
+        }
+        ok = ok && !bad && ntok <= kWTok && (quotes & 1u) == 0 && ntok > 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        WPROF(1);
+        // depth before every token
+        int32_t depth = 0;
+        bool neg = false;
+        uint32_t nop1 = 0, ncl2 = 0;
+        for (uint32_t t0 = 0; ok && t0 < ntok; t0 += 64) {
+            const uint32_t t = t0 + lane;
+            const uint8_t ch = t < ntok ? B[W.pos[t]] : (uint8_t)' ';
+            const uint64_t Op = __ballot(t < ntok && wave_isopen(ch));
+            const uint64_t Cl = __ballot(t < ntok && wave_isclose(ch));
+            const int32_t d = depth + __popcll(Op & lt) - __popcll(Cl & lt);
+            if (t < ntok) W.dep[t] = (int16_t)d;
+            neg |= __ballot(t < ntok && (d < 0 || d > 30000 || (wave_isclose(ch) && d < 1))) != 0;
+            const uint64_t O1 = __ballot(t < ntok && wave_isopen(ch) && d == 1);
+            const uint64_t C2 = __ballot(t < ntok && wave_isclose(ch) && d == 2);
+            const uint32_t io = nop1 + (uint32_t)__popcll(O1 & lt), ic = ncl2 + (uint32_t)__popcll(C2 & lt);
+            if (((O1 >> lane) & 1ull) && io < 32) W.op1[io] = (uint16_t)t;
+            if (((C2 >> lane) & 1ull) && ic < 32) W.cl2[ic] = (uint16_t)t;
+            nop1 += (uint32_t)__popcll(O1);
+            ncl2 += (uint32_t)__popcll(C2);
+            depth += __popcll(Op) - __popcll(Cl);
+        }
+        ok = ok && !neg && depth == 0 && nop1 <= 32 && nop1 == ncl2;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        WPROF(2);
+        WaveMsg M{&W, B, len, ntok};
+        // the top level, wave-uniformly: [records] or {key: value, ...}
+        uint32_t arr = ntok, arr_end = ntok;  // the changes array's '[' and ']'
+        uint32_t ck = 0, msrc = NULL_ID, mtgt = NULL_ID;
+        int64_t msinc = LLONG_MIN;
+        uint8_t pst = 0xFF;
+        if (ok) {
+            const uint8_t c = M.tch(0);
+            ok = M.clean(0xFFFFFFFFu, W.pos[0]);  // only whitespace before the first token
+            const uint32_t last = ntok - 1;
+            ok = ok && M.clean(W.pos[last], len) && wave_isclose(M.tch(last)) && W.dep[last] == 1;
+            if (ok && c == '[') {
+                ok = M.tch(last) == ']';
+                arr = 0;
+                arr_end = last;
+            } else if (ok && c == '{') {
+                ok = M.tch(last) == '}';
+                uint32_t t = 1, kop = 0;  // kop: the next depth-1 opener, in walk order
+                bool seen = false, closed = false;
+                while (ok) {
+                    if (t + 2 >= last || M.tch(t) != '"' || M.tch(t + 1) != '"' || M.tch(t + 2) != ':' ||
+                        !M.clean(W.pos[t - 1], W.pos[t]) || !M.clean(W.pos[t + 1], W.pos[t + 2])) {
+                        ok = false;
+                        break;
+                    }
+                    const uint32_t v = t + 3;
+                    uint32_t nx = ntok;
+                    if (wave_key(M, t, "changes") || wave_key(M, t, "membership")) {
+                        if (seen || v >= last || M.tch(v) != '[' || !M.clean(W.pos[v - 1], W.pos[v])) {
+                            ok = false;
+                            break;
+                        }
+                        seen = true;
+                        arr = v;
+                        ok = kop < nop1 && W.op1[kop] == v;  // its ']' is the matching depth-2 closer
+                        arr_end = ok ? W.cl2[kop++] : ntok;
+                        ok = ok && arr_end < last && M.tch(arr_end) == ']';
+                        nx = arr_end + 1;
+                    } else if (wave_key(M, t, "checksum") || wave_key(M, t, "membershipChecksum") ||
+                               wave_key(M, t, "sourceIncarnationNumber")) {
+                        uint32_t s0, e0;
+                        int64_t x;
+                        ok = M.scalar(t + 2, s0, e0) && M.integer(s0, e0, x);
+                        if (wave_key(M, t, "sourceIncarnationNumber"))
+                            msinc = x;
+                        else
+                            ck = (uint32_t)x;
+                        nx = v;
+                    } else if (wave_key(M, t, "pingStatus")) {
+                        uint32_t s0, e0;
+                        ok = M.scalar(t + 2, s0, e0);
+                        if (ok && e0 - s0 == 4 && B[s0] == 't' && B[s0 + 1] == 'r' && B[s0 + 2] == 'u' && B[s0 + 3] == 'e')
+                            pst = 1;
+                        else if (ok && e0 - s0 == 5 && B[s0] == 'f' && B[s0 + 1] == 'a' && B[s0 + 2] == 'l' &&
+                                 B[s0 + 3] == 's' && B[s0 + 4] == 'e')
+                            pst = 0;
+                        else
+                            ok = false;
+                        nx = v;
+                    } else if (wave_key(M, t, "source") || wave_key(M, t, "coordinator") || wave_key(M, t, "target")) {
+                        ok = v + 1 < last && M.tch(v) == '"' && M.clean(W.pos[v - 1], W.pos[v]);
+                        if (ok && FILL) {
+                            const uint32_t so = W.pos[v] + 1, sl = W.pos[v + 1] - so;
+                            const uint32_t id = lane == 0 ? name_find(nm, B + so, sl) : 0u;
+                            const uint32_t idb = __shfl(id, 0, 64);
+                            if (wave_key(M, t, "target"))
+                                mtgt = idb;
+                            else
+                                msrc = idb;
+                        }
+                        nx = v + 2;
+                    } else if (v < last && wave_isopen(M.tch(v))) {  // an unknown member's nested value
+                        ok = kop < nop1 && W.op1[kop] == v && M.clean(W.pos[v - 1], W.pos[v]);
+                        nx = ok ? W.cl2[kop++] + 1u : ntok;
+                    } else {
+                        nx = M.skip(v);
+                    }
+                    if (!ok || nx > last) {
+                        ok = false;
+                        break;
+                    }
+                    if (!M.clean(W.pos[nx - 1], W.pos[nx]) && M.tch(nx - 1) != ':') {
+                        ok = false;
+                        break;
+                    }
+                    if (nx == last) {
+                        closed = true;
+                        break;
+                    }
+                    if (M.tch(nx) != ',') {
+                        ok = false;
+                        break;
+                    }
+                    t = nx + 1;
+                }
+                ok = ok && seen && closed;
+            } else {
+                ok = false;
+            }
+        }
+        WPROF(3);
+        // the changes array: its level tokens are { , { , ... {
+        uint32_t nrec = 0;
+        if (ok) {
+            const int16_t d = W.dep[arr];
+            uint32_t nl = 0;
+            for (uint32_t t0 = arr + 1; t0 < arr_end; t0 += 64) {
+                const uint32_t t = t0 + lane;
+                const bool lv = t < arr_end && W.dep[t] == d + 1;
+                const uint64_t L = __ballot(lv);
+                const uint32_t idx = nl + (uint32_t)__popcll(L & lt);
+                if (lv && idx < kWLvl) W.lvl[idx] = (uint16_t)t;
+                nl += (uint32_t)__popcll(L);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            // n records give 2n - 1 level tokens; an empty array none
+            if (nl == 0)
+                ok = arr_end == arr + 1 && M.clean(W.pos[arr], W.pos[arr_end]);
+            else
+                ok = nl < kWLvl && (nl & 1u) == 1u;
+            bool pat = true;
+            for (uint32_t j = lane; ok && j < nl; j += 64) {
+                const uint32_t t = W.lvl[j];
+                const uint8_t c = M.tch(t);
+                pat &= (j & 1u) ? c == ',' : c == '{';
+                // a record's last token is its '}', right before the next level token
+                if (!(j & 1u)) {
+                    const uint32_t nxt = j + 1 < nl ? W.lvl[j + 1] : arr_end;
+                    pat &= M.tch(nxt - 1) == '}' && W.dep[nxt - 1] == d + 2 && M.clean(W.pos[nxt - 1], W.pos[nxt]);
+                    const uint32_t prv = j == 0 ? arr : W.lvl[j - 1];
+                    pat &= M.clean(W.pos[prv], W.pos[t]);
+                }
+            }
+            ok = ok && __ballot(!pat) == 0;
+            nrec = ok ? (nl + 1) / 2 : 0;
+        }
+        WPROF(4);
+        // the records, one lane each
+        const uint64_t k0 = FILL ? O.rec_off[m] : 0;
+        const uint64_t kend = FILL ? O.rec_off[m + 1] : 0;
+        bool rok = true;
+        for (uint32_t r = lane; ok && r < nrec; r += 64) {
+            const uint32_t t0 = W.lvl[2 * r];
+            const uint32_t t1 = (2 * r + 1 < (nrec * 2 - 1) ? W.lvl[2 * r + 1] : arr_end) - 1;
+            rok &= wave_record<FILL>(M, nm, O, b0, t0, t1, k0 + r, kend);
+        }
+        ok = ok && __ballot(!rok) == 0;
+        WPROF(5);
+        if (lane == 0) {
+            if (!FILL) {
+                slow[m] = ok ? 0 : 1;
+                if (ok) O.cnt[m] = nrec;
+            } else if (ok) {
+                O.err[m] = 0;
+                if (O.m_checksum) O.m_checksum[m] = ck;
+                if (O.m_source) O.m_source[m] = msrc;
+                if (O.m_source_inc) O.m_source_inc[m] = msinc;
+                if (O.m_target) O.m_target[m] = mtgt;
+                if (O.m_ping_status) O.m_ping_status[m] = pst;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 __global__ void k_zero_tail(uint32_t* p, uint32_t n) {
     if (threadIdx.x == 0 && blockIdx.x == 0) p[n] = 0;
 }
 
 Names names_of(NameTable& nt, hipStream_t st, Scratch& ws) {
     nt.sort(st, ws);
-    return Names{nt.d_bytes.p, nt.d_noff.p, nt.sorted.p, nt.size()};
+    nt.hash_index(st);
+    return Names{nt.d_bytes.p, nt.d_noff.p, nt.sorted.p, nt.size(), nt.htab.p, (1u << nt.hbits) - 1u};
 }
 
 }  // namespace
@@ -730,18 +1208,61 @@ int rp_wire_decode_dev(rp_members* m, const uint8_t* d_buf, const uint64_t* d_ms
         rp::In I{d_buf, d_msg_off};
         rp::Out O{d_msg_rec_off, d_msg_rec_off, rec_cap, R.addr, R.src, R.status, R.inc, R.src_inc, R.id_off,
                   R.addr_off, R.addr_len, d_err, H.checksum, H.source, H.source_inc, H.target, H.ping_status};
-        if (n_msgs) {
+        // a wave per message where it can (k_decode_wave), the thread parser for the rest
+        // (RP_WIRE_THREAD=1: the thread parser for every message)
+        const bool wave = !getenv("RP_WIRE_THREAD");
+        rp::DevBuf<uint8_t> slow;
+        if (n_msgs && wave) {
+            slow.reserve(n_msgs);
+            uint64_t vb = 0, ve = 0;
+            RP_HIP(hipMemcpyAsync(&vb, d_msg_off, 8, hipMemcpyDeviceToHost, st));
+            RP_HIP(hipMemcpyAsync(&ve, d_msg_off + n_msgs, 8, hipMemcpyDeviceToHost, st));
+            RP_HIP(hipStreamSynchronize(st));
+            vb += reinterpret_cast<uint64_t>(d_buf);
+            ve += reinterpret_cast<uint64_t>(d_buf);
+            const unsigned g = rp::grid_for(n_msgs, rp::kDecWaves, 8192);
+            hipLaunchKernelGGL(rp::k_decode_wave<false>, dim3(g), dim3(64 * rp::kDecWaves), 0, st, I, nm, O, n_msgs,
+                               vb, ve, slow.p);
             hipLaunchKernelGGL(rp::k_decode<false>, dim3(rp::grid_for(n_msgs, 64)), dim3(64), 0, st, I, nm, O,
-                               n_msgs);
+                               n_msgs, slow.p);
             RP_HIP(hipGetLastError());
+            rp::scan_exclusive_u32(d_msg_rec_off, d_msg_rec_off, n_msgs, st, *ws);
+            hipLaunchKernelGGL(rp::k_decode_wave<true>, dim3(g), dim3(64 * rp::kDecWaves), 0, st, I, nm, O, n_msgs,
+                               vb, ve, slow.p);
+            hipLaunchKernelGGL(rp::k_decode<true>, dim3(rp::grid_for(n_msgs, 64)), dim3(64), 0, st, I, nm, O, n_msgs,
+                               slow.p);
+            RP_HIP(hipGetLastError());
+            RP_HIP(hipStreamSynchronize(st));  // slow is local
+#ifdef RP_WIRE_PROF
+            {
+                unsigned long long h[8];
+                RP_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(rp::g_wprof), sizeof h));
+                fprintf(stderr, "[rp] wire wave cycles (sum over waves): stage %llu classify %llu depth %llu top %llu "
+                        "level %llu records %llu\n", h[0], h[1], h[2], h[3], h[4], h[5]);
+            }
+#endif
+            if (getenv("RP_WIRE_DEBUG")) {
+                std::vector<uint8_t> h(n_msgs);
+                RP_HIP(hipMemcpy(h.data(), slow.p, n_msgs, hipMemcpyDeviceToHost));
+                uint64_t ns = 0;
+                for (uint8_t x : h) ns += x;
+                fprintf(stderr, "[rp] wire decode: %llu of %u messages by waves\n",
+                        (unsigned long long)(n_msgs - ns), n_msgs);
+            }
         } else {
-            hipLaunchKernelGGL(rp::k_zero_tail, dim3(1), dim3(64), 0, st, d_msg_rec_off, 0u);
-        }
-        rp::scan_exclusive_u32(d_msg_rec_off, d_msg_rec_off, n_msgs, st, *ws);
-        if (n_msgs) {
-            hipLaunchKernelGGL(rp::k_decode<true>, dim3(rp::grid_for(n_msgs, 64)), dim3(64), 0, st, I, nm, O,
-                               n_msgs);
-            RP_HIP(hipGetLastError());
+            if (n_msgs) {
+                hipLaunchKernelGGL(rp::k_decode<false>, dim3(rp::grid_for(n_msgs, 64)), dim3(64), 0, st, I, nm, O,
+                                   n_msgs, nullptr);
+                RP_HIP(hipGetLastError());
+            } else {
+                hipLaunchKernelGGL(rp::k_zero_tail, dim3(1), dim3(64), 0, st, d_msg_rec_off, 0u);
+            }
+            rp::scan_exclusive_u32(d_msg_rec_off, d_msg_rec_off, n_msgs, st, *ws);
+            if (n_msgs) {
+                hipLaunchKernelGGL(rp::k_decode<true>, dim3(rp::grid_for(n_msgs, 64)), dim3(64), 0, st, I, nm, O,
+                                   n_msgs, nullptr);
+                RP_HIP(hipGetLastError());
+            }
         }
         if (!stream) RP_HIP(hipStreamSynchronize(st));
     });

@@ -314,3 +314,77 @@ def test_host_buffer_full_api(gpu):
             hcols["ping_status"][0]) == (99, ids[0], 5, ids[4], 0xFF)
     # host decode: null buffer with bytes is an error, not a read past a 1-byte buffer
     assert L.rp_wire_decode(m._h, None, P(moff), 1, P(ro2), cap, ctypes.byref(rout), None, P(err)) != 0
+
+
+def _fuzz_texts(cases, seed):
+    """The reference's bodies re-serialised with random layouts and unknown members, then a set of
+    single-character mutations (most of them invalid JSON)."""
+    rng = random.Random(seed)
+    kinds = ["ping", "issueAs", "pingResponse", "fullSync", "pingReq", "pingReqResponse", "joinResponse"]
+    base = [c["out"][k] for c in cases for k in kinds]
+    ws = [" ", "\n", "\t", "\r\n ", ""]
+
+    def shuffle(o):
+        if isinstance(o, dict):
+            items = [(k, shuffle(v)) for k, v in o.items()]
+            rng.shuffle(items)
+            if rng.random() < 0.3:
+                items.insert(rng.randrange(len(items) + 1), ("x%d" % rng.randrange(9), rng.choice(
+                    [None, True, False, -12, "s:t[r]{,}", [1, {"b": "]"}, []], {"a": {"c": [None]}}, 3.5e2])))
+            return dict(items)
+        if isinstance(o, list):
+            return [shuffle(v) for v in o]
+        return o
+
+    out = []
+    for t in base:
+        out.append(t)
+        o = json.loads(t)
+        for _ in range(2):
+            sep = (rng.choice(ws) + "," + rng.choice(ws), rng.choice(ws) + ":" + rng.choice(ws))
+            out.append(rng.choice(ws) + json.dumps(shuffle(o), separators=sep) + rng.choice(ws))
+    mutants = []
+    for t in rng.sample(out, min(len(out), 400)):
+        if not t:
+            continue
+        i = rng.randrange(len(t))
+        kind = rng.randrange(6)
+        if kind == 0:
+            mutants.append(t[:i] + t[i + 1:])  # delete
+        elif kind == 1:
+            mutants.append(t[:i] + rng.choice('{}[]:,"\\ \t0a-.e\x01') + t[i:])  # insert
+        elif kind == 2:
+            mutants.append(t[:i])  # truncate
+        elif kind == 3:
+            mutants.append(t.replace("}", ",}", 1))  # trailing comma
+        elif kind == 4:
+            mutants.append(t.replace('"status"', '"status":"alive","status"', 1))  # duplicate key
+        else:
+            mutants.append(t + rng.choice([" ", "x", "]", ",", "{}"]))  # trailing bytes
+    return out + mutants
+
+
+def test_wave_decoder_equals_thread_decoder(gpu, monkeypatch, capfd):
+    """The wave-per-message decoder (k_decode_wave) and the thread parser (RP_WIRE_THREAD=1)
+    return identical columns, offsets, headers and error offsets on the reference's bodies,
+    re-laid-out variants with unknown members, and single-character mutants; the waves take
+    every well-formed message."""
+    cases = golden()
+    m = gpu.Membership()
+    for c in cases:
+        m.intern([mm[0] for mm in c["members"]] + [c["target"]])
+    texts = _fuzz_texts(cases, 11)
+    monkeypatch.setenv("RP_WIRE_DEBUG", "1")
+    capfd.readouterr()
+    dw = gpu.wire_decode(m, texts)
+    err = capfd.readouterr().err
+    monkeypatch.setenv("RP_WIRE_THREAD", "1")
+    dt = gpu.wire_decode(m, texts)
+    for k in dt:
+        assert np.array_equal(dw[k], dt[k]), k
+    n_ok = int((dt["err"] == 0).sum())
+    assert n_ok > 120 and n_ok < len(texts)
+    line = [x for x in err.splitlines() if "by waves" in x][-1]
+    by_waves = int(line.split()[3])
+    big = sum(1 for t in texts if len(t.encode()) > 8192)
+    assert by_waves >= n_ok - big, line
