@@ -53,6 +53,8 @@ def main():
                   "FETCH_SIZE of the key stream doubled per the gfx950 correction, calibrated with the hash-only "
                   "ablation kernel whose FETCH_SIZE is exactly half of the 2.42 GB of keys.",
     }
+    # which kernel build the counters came from (bench.py reports it as traffic_measured_on)
+    out["measured_on"] = os.environ.get("PMC_MEASURED_ON") or None
     print(json.dumps(out, indent=1))
 
 
