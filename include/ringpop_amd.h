@@ -377,13 +377,22 @@ int rp_sim_converged_local(rp_sim *s, uint32_t *out4);
  *                  send it (benchmarks/convergence-time/scenarios/); its LocalMemberLeaveEvent
  *                  stops the node's gossip loop and suspicion (on_membership_event.js:32-40). A
  *                  node that is down, or left already, ignores it.
+ *   RP_SIM_JOIN    a fresh process for the node bootstraps into the running cluster
+ *                  (index.js:240-322): makeAlive(self, Date.now()); three live nodes (JOIN
+ *                  Philox stream over the live nodes in id order) answer the join
+ *                  (server/protocol/join.js:126-133: makeAlive(joiner), fullSync);
+ *                  mergeJoinResponses (join-response-merge.js:40-56) is stashed and set()
+ *                  (index.js:208-247) builds the view, the set handler
+ *                  (on_membership_event.js:42-67) fills the ring and the suspicion timers; the
+ *                  dissemination is cleared as at bootstrap, then gossip.start shuffles. Needs an
+ *                  unsharded handle and one live node besides the joiner.
  * Convergence then reads: every node that is up and has not left holds the same checksum, each
  * member that left is `leave` and each other member that is down `faulty` in those views.
  * dead[] = down from the start (never started gossip; gossip/index.js:97 never shuffled). */
 typedef struct rp_sim_event {
     uint32_t round, kind, node, reserved;
 } rp_sim_event;
-enum { RP_SIM_KILL = 0, RP_SIM_REVIVE = 1, RP_SIM_LEAVE = 2 };
+enum { RP_SIM_KILL = 0, RP_SIM_REVIVE = 1, RP_SIM_LEAVE = 2, RP_SIM_JOIN = 3 };
 int rp_sim_create_scenario(uint32_t n, const char *names, const uint32_t *off, const int64_t *inc0,
                            const uint8_t *dead, uint32_t seed, uint32_t suspicion_rounds, int64_t now0, int device,
                            const uint32_t *bounds, uint32_t nshards, uint32_t shard, const rp_sim_event *events,

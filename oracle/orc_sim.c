@@ -52,6 +52,7 @@
 
 #define TAG_SHUF 0x53485546u
 #define TAG_SAMP 0x53414d50u
+#define TAG_JOIN 0x4a4f494eu
 #define NONE 0xFFFFFFFFu
 #define WIN 1024u
 
@@ -94,6 +95,7 @@ typedef struct {
     int64_t it_idx;
     uint32_t n_shuffles;
     uint32_t *order; /* whole members array, or the window [w0, w0 + WIN) */
+    uint32_t *base;  /* the members array a join's set() built (NULL: the bootstrap one) */
     uint32_t w0;
     uint32_t checksum;
     uint8_t dirty;
@@ -293,7 +295,10 @@ static void perm_shuffle(const orc_sim *s, uint32_t v, uint32_t sh, uint32_t *o)
 /* the whole current members array of view v (pointer valid until the next call) */
 static const uint32_t *perm_full(const orc_sim *s, uint32_t v, const node *nd, wctx *c) {
     if (s->full_order) return nd->order;
-    perm_initial(s->N, v, c->perm);
+    if (nd->base)
+        memcpy(c->perm, nd->base, 4ull * s->N);
+    else
+        perm_initial(s->N, v, c->perm);
     for (uint32_t sh = 0; sh < nd->n_shuffles; sh++) perm_shuffle(s, v, sh, c->perm);
     return c->perm;
 }
@@ -689,7 +694,7 @@ void orc_sim_free(orc_sim *s) {
     if (!s) return;
     for (uint32_t v = 0; v < s->N; v++) {
         node *nd = &s->nodes[v];
-        free(nd->e); free(nd->ix); free(nd->order);
+        free(nd->e); free(nd->ix); free(nd->order); free(nd->base);
         free(s->ping[v].v); free(s->resp[v].v);
         for (int k = 0; k < 3; k++) { free(s->legs[v][k].v); free(s->lresp[v][k].v); }
     }
@@ -708,12 +713,99 @@ void orc_sim_free(orc_sim *s) {
     free(s);
 }
 
+/* A fresh process for node v bootstraps into the running cluster (index.js:240-322):
+ * makeAlive(self, Date.now()); three live nodes other than v (a partial Fisher-Yates over them
+ * in id order, JOIN stream) answer the join: each applies makeAlive(v, that incarnation)
+ * (server/protocol/join.js:126) and returns its fullSync; mergeJoinResponses
+ * (join-response-merge.js:40-56: the first response when every checksum agrees, else
+ * mergeMembershipChangesets; the same rows either way) is stashed and set() (index.js:208-247)
+ * builds the view: self first, then the others in the first response's members-array order,
+ * each at the greatest incarnation any response holds (the first on ties). The set handler
+ * (on_membership_event.js:42-67) adds alive / suspect members to the ring without a
+ * ringChanged (maxPiggybackCount stays at the one-server value of makeAlive(self)) and starts a
+ * suspicion timer per suspect member. The dissemination is cleared as at bootstrap; gossip.start
+ * shuffles. */
+static void node_join(orc_sim *s, uint32_t v, wctx *c) {
+    const uint32_t N = s->N;
+    const int64_t now = s->now0 + 200 * s->round;
+    uint32_t len = 0;
+    for (uint32_t u = 0; u < N; u++)
+        if (u != v && !s->down[u]) c->cand[len++] = u;
+    const uint32_t nj = len < 3 ? len : 3;
+    uint32_t resp[3];
+    for (uint32_t q = 0; q < nj; q++) {
+        uint32_t r = philox_u32(s->seed, TAG_JOIN, (uint32_t)s->round, q, v);
+        uint32_t j = q + (uint32_t)(((uint64_t)r * (len - q)) >> 32);
+        uint32_t t = c->cand[q]; c->cand[q] = c->cand[j]; c->cand[j] = t;
+        resp[q] = c->cand[q];
+    }
+    for (uint32_t q = 0; q < nj; q++) make_change(s, resp[q], v, 0, now, c);
+    node *nd = &s->nodes[v];
+    /* the members array: self, then the first response's order without self */
+    uint32_t *base = nd->base ? nd->base : (uint32_t *)malloc(4ull * N);
+    base[0] = v;
+    if (nj) {
+        const uint32_t *p0 = perm_full(s, resp[0], &s->nodes[resp[0]], c);
+        for (uint32_t k = 0, o = 1; k < N; k++)
+            if (p0[k] != v) base[o++] = p0[k];
+    } else {
+        for (uint32_t k = 0, o = 1; k < N; k++)
+            if (k != v) base[o++] = k;
+    }
+    /* the rows: a fresh sparse view, then every member some response holds off its base state */
+    nd->ne = 0;
+    if (nd->ixcap) memset(nd->ix, 0, 4ull * nd->ixcap);
+    uint32_t nrem = 0;
+    for (uint32_t q = 0; q < nj; q++) {
+        const node *rq = &s->nodes[resp[q]];
+        for (uint32_t i = 0; i < rq->ne; i++) {
+            const uint32_t a = rq->e[i].addr;
+            if (a == v || find(nd, a)) continue;
+            uint8_t st = 0;
+            int64_t inc = s->inc0[a];
+            for (uint32_t q2 = 0; q2 < nj; q2++) { /* greatest incarnation, the first on ties */
+                const ent *x = find(&s->nodes[resp[q2]], a);
+                const uint8_t st2 = x ? x->st : 0;
+                const int64_t in2 = x ? x->inc : s->inc0[a];
+                if (q2 == 0 || in2 > inc) { st = st2; inc = in2; }
+            }
+            ent *e = get(s, nd, a);
+            e->st = st;
+            e->inc = inc;
+            e->in_ring = st == 0 || st == 1;
+            if (!e->in_ring) nrem++;
+            if (st == 1) { e->t_on = 1; e->deadline = s->round + s->susp_rounds; e->s_inc = inc; }
+        }
+    }
+    ent *self = get(s, nd, v);
+    self->st = 0;
+    self->inc = now;
+    self->in_ring = 1;
+    nd->ring_count = N - nrem;
+    nd->max_piggy = 15u * (uint32_t)digits(1);
+    nd->it_idx = -1;
+    nd->n_shuffles = 0;
+    nd->dirty = 1;
+    if (s->full_order) {
+        memcpy(nd->order, base, 4ull * N);
+        free(base);
+        nd->base = NULL;
+    } else {
+        nd->base = base;
+    }
+    s->down[v] = 0;
+    s->stopped[v] = 0;
+    s->left[v] = 0;
+    node_shuffle(s, v, nd, c); /* gossip.start */
+}
+
 /* Scenario events, applied before the next round (see the header). */
 int orc_sim_event(orc_sim *s, int kind, uint32_t v) {
     if (v >= s->N) return -1;
     switch (kind) {
     case ORC_SIM_KILL: s->down[v] = 1; return 0;
     case ORC_SIM_REVIVE: s->down[v] = 0; return 0;
+    case ORC_SIM_JOIN: node_join(s, v, &s->ctx[0]); return 0;
     case ORC_SIM_LEAVE: {
         node *nd = &s->nodes[v];
         /* the admin handler refuses a redundant leave (server/admin/member.js:84-89); a node that

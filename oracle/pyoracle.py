@@ -306,7 +306,7 @@ class Members:
         return buf.raw[:n].decode()
 
 
-SIM_EVENT = {"kill": 0, "revive": 1, "leave": 2}
+SIM_EVENT = {"kill": 0, "revive": 1, "leave": 2, "join": 3}
 
 
 class Sim:

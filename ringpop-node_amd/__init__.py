@@ -635,7 +635,7 @@ class Membership:
         return sc[:m], ls[:m], ts[:m]
 
 
-SIM_EVENT = {"kill": 0, "revive": 1, "leave": 2}
+SIM_EVENT = {"kill": 0, "revive": 1, "leave": 2, "join": 3}
 
 
 def _events(events):

@@ -58,6 +58,7 @@ constexpr int kT = 256;            // threads per node-workgroup
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint32_t TAG_SHUF = 0x53485546u;
 constexpr uint32_t TAG_SAMP = 0x53414d50u;
+constexpr uint32_t TAG_JOIN = 0x4a4f494eu;
 constexpr int kHashWin = 512;      // LDS window of pre-mixed chunks for the block checksum chain
 constexpr uint8_t ST_MASK = 3, IN_RING = 0x80;
 constexpr uint32_t kMaxShards = 64;
@@ -2214,6 +2215,98 @@ __global__ __launch_bounds__(kT) void k_leave(SimDev S, const uint32_t* __restri
     }
 }
 
+// ---- a fresh process joining from join responses (RP_SIM_JOIN; one shard)
+//
+// index.js:240-322 for node v: makeAlive(self, Date.now()); each responder (chosen on the host)
+// answers the join with makeAlive(v, that incarnation) (server/protocol/join.js:126) and its
+// fullSync; mergeJoinResponses (join-response-merge.js:40-56) + set() (index.js:208-247) give
+// self first, then the first response's members-array order without self, each member at the
+// greatest incarnation any response holds (the first on ties); the set handler
+// (on_membership_event.js:42-67) puts alive / suspect members in the ring without a ringChanged
+// and starts a timer per suspect member. The dissemination is cleared as at bootstrap.
+
+// the responders' join handler
+__global__ __launch_bounds__(kT) void k_join_resp(SimDev S, uint32_t v, int64_t incv, uint32_t r0, uint32_t r1,
+                                                  uint32_t r2, uint32_t nj) {
+    __shared__ Lds L;
+    __shared__ Rec tmp;
+    const int64_t now = S.now0 + 200 * S.round;
+    for (uint32_t q = blockIdx.x; q < nj; q += gridDim.x) {
+        const uint32_t r = q == 0 ? r0 : q == 1 ? r1 : r2;
+        block_make(S, r - S.v0, v, ST_ALIVE, incv, L, now, &tmp);
+    }
+}
+
+// v's position in the first response's members array; the joiner's deviation words cleared
+__global__ void k_join_prep(SimDev S, uint32_t v, uint32_t r0, uint32_t* __restrict__ scratch) {
+    const uint64_t row0 = (uint64_t)(r0 - S.v0) * S.N, rowv = (uint64_t)(v - S.v0) * S.N;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < S.N; k += gridDim.x * blockDim.x)
+        if (S.order[row0 + k] == v) scratch[0] = k;
+    for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < S.W; w += gridDim.x * blockDim.x)
+        S.dev[(uint64_t)(v - S.v0) * S.W + w] = 0;
+    (void)rowv;
+}
+
+// the joiner's rows, members array, timers; scratch[0] = v's position in r0's array,
+// scratch[1] accumulates the members outside the ring
+__global__ void k_join_view(SimDev S, uint32_t v, int64_t incv, uint32_t r0, uint32_t r1, uint32_t r2, uint32_t nj,
+                            uint32_t* __restrict__ scratch) {
+    const uint32_t lv = v - S.v0;
+    const uint64_t row = (uint64_t)lv * S.N;
+    const uint64_t row0 = (uint64_t)(r0 - S.v0) * S.N;
+    const uint32_t pv = scratch[0];
+    Timer* tim = S.tim + (uint64_t)lv * S.Ct;
+    for (uint32_t m = blockIdx.x * blockDim.x + threadIdx.x; m < S.N; m += gridDim.x * blockDim.x) {
+        uint8_t st = ST_ALIVE;
+        int64_t inc = incv;
+        if (m != v) {
+            for (uint32_t q = 0; q < nj; q++) {
+                const uint64_t rq = (uint64_t)((q == 0 ? r0 : q == 1 ? r1 : r2) - S.v0) * S.N;
+                const uint8_t s2 = S.st[rq + m] & ST_MASK;
+                const int64_t i2 = S.inc[rq + m];
+                if (q == 0 || i2 > inc) {
+                    st = s2;
+                    inc = i2;
+                }
+            }
+        }
+        const bool ring = st == ST_ALIVE || st == ST_SUSPECT;
+        S.st[row + m] = st | (ring ? IN_RING : 0);
+        S.inc[row + m] = inc;
+        S.slot[row + m] = 0;
+        if (!ring) atomicAdd(&scratch[1], 1u);
+        if (st != ST_ALIVE || inc != S.inc0[m]) {
+            const uint32_t k = S.rank[m];
+            atomicOr(&S.dev[(uint64_t)lv * S.W + (k >> 5)], 1u << (k & 31));
+        }
+        if (st == ST_SUSPECT && m != v) {
+            const uint32_t q = atomicAdd(&S.n_tim[lv], 1u);
+            if (q < S.Ct) tim[q] = Timer{m, (int32_t)(S.round + S.susp), inc};
+            else set_err(S, ERR_TIMERS);
+        }
+        // members array: self, then r0's without self
+        if (m == 0) S.order[row] = v;
+        const uint32_t k = m;  // position k of r0's array goes to k + 1 (before v) or k (after)
+        const uint32_t a = S.order[row0 + k];
+        if (a != v) S.order[row + (k < pv ? k + 1 : k)] = a;
+    }
+}
+
+// the joiner's scalars, then gossip.start's shuffle (one lane)
+__global__ void k_join_finish(SimDev S, uint32_t v, uint32_t* __restrict__ scratch) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    const uint32_t lv = v - S.v0;
+    S.ring_count[lv] = S.N - scratch[1];
+    S.max_piggy[lv] = 15u * digits(1);  // makeAlive(self)'s ringChanged; set() emits none
+    S.n_chg[lv] = 0;
+    S.it_idx[lv] = -1;
+    S.n_shuf[lv] = 0;
+    S.stopped[lv] = 0;
+    S.dirty[lv] = 1;
+    S.target[lv] = -1;
+    lane0_shuffle(S, lv, true);
+}
+
 // ---- outboxes: messages grouped by destination shard
 
 // Candidate c of a message kind: its destination shard (G = none) and the sort value c.
@@ -2714,12 +2807,66 @@ struct Sim {
 
     // The scenario's events of this round, before phase A: a node goes down or comes back (every
     // shard keeps the global down flags), or leaves (on the shard that owns it).
+    DevBuf<uint32_t> join_scratch;
+
+    // leaves collected so far run before anything that reads the views (a join)
+    void flush_leaves(std::vector<uint32_t>& leaves) {
+        if (leaves.empty()) return;
+        leave_list.reserve(leaves.size());
+        RP_HIP(hipMemcpyAsync(leave_list.p, leaves.data(), 4 * leaves.size(), hipMemcpyHostToDevice, st));
+        d.round = round;
+        hipLaunchKernelGGL(k_leave, dim3((unsigned)std::min<size_t>(leaves.size(), 1024)), dim3(kT), 0, st, d,
+                           leave_list.p, (uint32_t)leaves.size());
+        RP_HIP(hipGetLastError());
+        RP_HIP(hipStreamSynchronize(st));  // the host vector is reused
+        leaves.clear();
+    }
+
+    void join(uint32_t v) {
+        RP_REQUIRE(G == 1, "sim: join events need an unsharded simulator (the joiner reads its responders' views)");
+        std::vector<uint32_t> cand;
+        for (uint32_t u = 0; u < N; u++)
+            if (u != v && !h_dead[u]) cand.push_back(u);
+        const uint32_t nj = (uint32_t)std::min<size_t>(3, cand.size());
+        RP_REQUIRE(nj > 0, "sim: a join needs at least one live node to answer it");
+        for (uint32_t q = 0; q < nj; q++) {  // partial Fisher-Yates, JOIN stream
+            const uint32_t r = philox4x32_10(U4{(uint32_t)round, q, v, 0u}, d.seed, TAG_JOIN).x;
+            const uint32_t j = q + (uint32_t)(((uint64_t)r * (cand.size() - q)) >> 32);
+            std::swap(cand[q], cand[j]);
+        }
+        const uint32_t r0 = cand[0], r1 = nj > 1 ? cand[1] : 0, r2 = nj > 2 ? cand[2] : 0;
+        const int64_t incv = d.now0 + 200 * round;
+        d.round = round;
+        join_scratch.reserve(2);
+        RP_HIP(hipMemsetAsync(join_scratch.p, 0, 8, st));
+        RP_HIP(hipMemsetAsync(n_tim.p + (v - v0), 0, 4, st));
+        hipLaunchKernelGGL(k_join_resp, dim3(nj), dim3(kT), 0, st, d, v, incv, r0, r1, r2, nj);
+        hipLaunchKernelGGL(k_join_prep, dim3(grid_for(std::max(N, d.W), 256)), dim3(256), 0, st, d, v, r0,
+                           join_scratch.p);
+        hipLaunchKernelGGL(k_join_view, dim3(grid_for(N, 256)), dim3(256), 0, st, d, v, incv, r0, r1, r2, nj,
+                           join_scratch.p);
+        hipLaunchKernelGGL(k_join_finish, dim3(1), dim3(64), 0, st, d, v, join_scratch.p);
+        RP_HIP(hipGetLastError());
+        h_dead[v] = 0;
+        h_left[v] = 0;
+        RP_HIP(hipMemcpyAsync(dead.p, h_dead.data(), N, hipMemcpyHostToDevice, st));
+        RP_HIP(hipStreamSynchronize(st));
+    }
+
     void apply_events() {
         bool down_changed = false;
         std::vector<uint32_t> leaves;
         while (next_event < events.size() && events[next_event].round <= (uint64_t)round) {
             const rp_sim_event& e = events[next_event++];
             if (e.round != (uint64_t)round) continue;
+            if (e.kind == RP_SIM_JOIN) {
+                flush_leaves(leaves);
+                if (down_changed) RP_HIP(hipMemcpyAsync(dead.p, h_dead.data(), N, hipMemcpyHostToDevice, st));
+                down_changed = false;
+                join(e.node);
+                conv_dirty = true;
+                continue;
+            }
             if (e.kind == RP_SIM_KILL || e.kind == RP_SIM_REVIVE) {
                 const uint8_t dv = e.kind == RP_SIM_KILL ? 1 : 0;
                 down_changed |= h_dead[e.node] != dv;
@@ -2731,15 +2878,8 @@ struct Sim {
             conv_dirty = true;
         }
         if (down_changed) RP_HIP(hipMemcpyAsync(dead.p, h_dead.data(), N, hipMemcpyHostToDevice, st));
-        if (!leaves.empty()) {
-            leave_list.reserve(leaves.size());
-            RP_HIP(hipMemcpyAsync(leave_list.p, leaves.data(), 4 * leaves.size(), hipMemcpyHostToDevice, st));
-            d.round = round;
-            hipLaunchKernelGGL(k_leave, dim3((unsigned)std::min<size_t>(leaves.size(), 1024)), dim3(kT), 0, st, d,
-                               leave_list.p, (uint32_t)leaves.size());
-            RP_HIP(hipGetLastError());
-        }
-        if (down_changed || !leaves.empty()) RP_HIP(hipStreamSynchronize(st));  // host vectors reused
+        flush_leaves(leaves);
+        if (down_changed) RP_HIP(hipStreamSynchronize(st));  // host vectors reused
     }
 
     // {live, min checksum, max checksum, some wanted member not at its wanted status}
@@ -2801,7 +2941,7 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
     RP_REQUIRE(out && n >= 2 && names && off && inc0 && dead, "sim_create: bad arguments");
     RP_REQUIRE(n_events == 0 || events, "sim_create: events missing");
     for (uint32_t i = 0; i < n_events; i++)
-        RP_REQUIRE(events[i].node < n && events[i].kind <= RP_SIM_LEAVE, "sim_create: bad event");
+        RP_REQUIRE(events[i].node < n && events[i].kind <= RP_SIM_JOIN, "sim_create: bad event");
     RP_REQUIRE(n < (1u << 23), "sim_create: at most 2^23 members");
     RP_REQUIRE(nshards >= 1 && nshards <= rp::kMaxShards && shard < nshards, "sim_create: bad shard");
     std::vector<uint32_t> bnd(nshards + 1);

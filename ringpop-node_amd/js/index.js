@@ -271,8 +271,17 @@ function GossipSim(names, options) {
     requireDevice(this.device);
     var inc0 = options.inc0 instanceof Float64Array ? options.inc0 : Float64Array.from(options.inc0);
     var dead = options.dead ? Uint8Array.from(options.dead) : new Uint8Array(this.n);
+    // options.events: [[round, 'kill' | 'revive' | 'leave' | 'join', node], ...] (rp_sim_create_scenario)
+    var kinds = {kill: 0, revive: 1, leave: 2, join: 3};
+    var evs = options.events || [];
+    var ev = new Uint32Array(3 * evs.length);
+    evs.forEach(function (e, i) {
+        ev[3 * i] = e[0];
+        ev[3 * i + 1] = typeof e[1] === 'string' ? kinds[e[1]] : e[1];
+        ev[3 * i + 2] = e[2];
+    });
     this._h = native.simCreate(names, inc0, dead, options.seed || 0, options.suspicionRounds || 25,
-        options.now0 || 0, this.device);
+        options.now0 || 0, this.device, ev);
 }
 
 GossipSim.prototype.destroy = function destroy() { native.destroy(this._h); };

@@ -703,8 +703,10 @@ static napi_value js_members_dump(napi_env env, napi_callback_info info) {
 
 /* ------------------------------------------------------------------ gossip simulator */
 /* simCreate(names[], inc0 Float64Array, dead Uint8Array, seed, suspicionRounds, now0, device) */
+// simCreate(names, inc0, dead, seed, suspicionRounds, now0, device[, events Uint32Array of
+// (round, kind, node) triples: RP_SIM_KILL / REVIVE / LEAVE / JOIN])
 static napi_value js_sim_create(napi_env env, napi_callback_info info) {
-    ARGS(7);
+    ARGS(8);
     strpack_t s;
     if (strpack_from_array(env, argv[0], &s)) return NULL;
     size_t n1 = 0, n2 = 0;
@@ -724,8 +726,29 @@ static napi_value js_sim_create(napi_env env, napi_callback_info info) {
     napi_get_value_int32(env, argv[6], &dev);
     int64_t *inc = (int64_t *)malloc(sizeof(int64_t) * (s.n ? s.n : 1));
     for (uint32_t i = 0; i < s.n; i++) inc[i] = (int64_t)incd[i];
+    size_t ne = 0;
+    const uint32_t *ev = NULL;
+    napi_valuetype et = napi_undefined;
+    if (argc > 7) napi_typeof(env, argv[7], &et);
+    if (et == napi_object) {
+        ev = (const uint32_t *)typed_data(env, argv[7], napi_uint32_array, &ne);
+        if (!ev || ne % 3) {
+            free(inc);
+            strpack_free(&s);
+            napi_throw_type_error(env, NULL, "simCreate events must be a Uint32Array of (round, kind, node) triples");
+            return NULL;
+        }
+    }
+    rp_sim_event *evs = (rp_sim_event *)calloc(ne / 3 + 1, sizeof(rp_sim_event));
+    for (size_t i = 0; i < ne / 3; i++) {
+        evs[i].round = ev[3 * i];
+        evs[i].kind = ev[3 * i + 1];
+        evs[i].node = ev[3 * i + 2];
+    }
     rp_sim *sim = NULL;
-    int rc = rp_sim_create(s.n, s.bytes, s.off32, inc, dead, seed, susp, (int64_t)now0, dev, &sim);
+    int rc = rp_sim_create_scenario(s.n, s.bytes, s.off32, inc, dead, seed, susp, (int64_t)now0, dev, NULL, 1, 0, evs,
+                                    (uint32_t)(ne / 3), &sim);
+    free(evs);
     free(inc);
     strpack_free(&s);
     RP_OK(rc);

@@ -280,18 +280,27 @@ def sim_cases():
     #  - n24-revive: a node down from round 0 comes back after every change about it expired:
     #    it is answered with a full sync (dissemination.js:100-114) and refutes its own faulty
     #    status (member.js:76-81); a second node is suspended briefly and refutes `suspect`
+    #  - n30-join / n70-join: fresh processes bootstrapping into the running cluster from join
+    #    responses (mergeJoinResponses -> set(), join-sender.js:253-256): crashed nodes come back
+    #    after they were declared faulty, a live node restarts, a node that left rejoins, and
+    #    several nodes join in one round (later joiners may be answered by earlier ones)
     ev = lambda *e: [list(x) for x in e]  # noqa: E731
     scen = [("n100k1-digits", 100, 1, 60, 25, 13, []),
             ("n40-leave", 40, 1, 70, 6, 17, ev((2, "leave", 3), (5, "kill", 9), (10, "leave", 7), (11, "leave", 7),
                                               (30, "leave", 20), (30, "kill", 21))),
             ("n64-half-leave", 64, 0, 60, 25, 19, ev(*[(1, "leave", v) for v in range(0, 64, 2)])),
             ("n24-revive", 24, 0, 110, 8, 23, ev((0, "kill", 4), (3, "kill", 6), (12, "revive", 6),
-                                                 (60, "revive", 4), (70, "kill", 11), (71, "leave", 12)))]
+                                                 (60, "revive", 4), (70, "kill", 11), (71, "leave", 12))),
+            ("n30-join", 30, 0, 95, 6, 29, ev((0, "kill", 4), (0, "kill", 9), (5, "leave", 8), (22, "join", 4),
+                                               (28, "join", 13), (30, "join", 8), (45, "join", 9), (46, "kill", 2))),
+            ("n70-join", 70, 0, 80, 7, 31, ev(*([(3, "kill", v) for v in range(10, 16)] +
+                                                [(33, "join", v) for v in range(10, 16)])))]
     for name, n, k, rounds, susp, seed, events in scen:
         cases.append({"name": name, "names": [S.c2_addr(i) for i in range(n)],
                       "inc0": [int(x) for x in S.c3_members(n)[2]],
                       "dead": [int(x) for x in S.kill_set(n, k, seed)] if k else [0] * n, "seed": seed,
-                      "suspRounds": susp, "now0": S.NOW0, "rounds": rounds, "views": [0, n - 1],
+                      "suspRounds": susp, "now0": S.NOW0, "rounds": rounds,
+                      "views": [0, n - 1] + sorted({e[2] for e in events if e[1] == "join"})[:2],
                       "events": events})
     return cases
 

@@ -13,6 +13,9 @@ replay the same configs on the device and compare round by round.
 Cases:
   c4   10,000 members, 1% (100) down from the start (Philox seed 11), suspicion 25 rounds
   c5   100,000 members, 1% (1,000) down, suspicion 25 rounds
+  c4j  10,000 members, 1% down from the start; 100 running nodes crash at round 5; at round 45
+       fresh processes for 50 of them and for 20 nodes down from the start join from join
+       responses (mergeJoinResponses -> set(), RP_SIM_JOIN)
   c4s  10,000 members, 1% down from the start, then: 100 nodes leave at round 2
        (half-cluster-failure.js-style admin leaves), 100 running nodes crash at round 5, 50 of
        those come back at round 45 (they refute `faulty` and are answered with full syncs)
@@ -42,6 +45,7 @@ def run(name, threads):
                        events=events, threads=threads)
     print("%s: created in %.1f s" % (name, time.time() - t0), flush=True)
     out = {"name": name, "digests": [], "piggyback": [], "stats": [], "converged_round": None}
+    last_ev = max((e[0] for e in events), default=0)  # convergence counts once every event ran
     for r in range(cfg["max_rounds"]):
         t = time.time()
         sim.step()
@@ -51,7 +55,7 @@ def run(name, threads):
         st = sim.stats()
         out["stats"].append([st["pings"], st["pingreqs"], st["fullsyncs"], st["applied"]])
         conv = sim.converged()
-        if conv and out["converged_round"] is None:
+        if conv and out["converged_round"] is None and r >= last_ev:
             out["converged_round"] = r
         print("%s round %d: %.1f s %s conv=%s" % (name, r, time.time() - t, st, conv), flush=True)
         if out["converged_round"] is not None and r >= out["converged_round"] + cfg.get("after", 2):

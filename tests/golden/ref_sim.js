@@ -9,7 +9,13 @@
 // 'kill' (the node stops: crash / SIGSTOP, scripts/tick-cluster.js:417-470), 'revive' (SIGCONT:
 // back with its state intact), 'leave' (the admin leave handler, server/admin/member.js:70-98:
 // makeLeave(whoami, localMember.incarnationNumber), as benchmarks/convergence-time/scenarios/
-// send it).
+// send it), 'join' (a fresh process for the node bootstraps into the running cluster, index.js:
+// 240-322: makeAlive(self, Date.now()); three live nodes chosen by the JOIN Philox stream answer
+// the join (server/protocol/join.js:126-133: makeAlive(joiner, its incarnation), then
+// {checksum, membership: fullSync()}); mergeJoinResponses (join-sender.js:253-256,
+// join-response-merge.js:40-56) -> update (stashed) -> set() -> the set handler
+// (on_membership_event.js:42-67) -> ready; the model clears the dissemination as at
+// bootstrap; gossip.start shuffles).
 //
 // Reference code doing the work per node: lib/membership (Membership, Member, merge),
 // lib/gossip/dissemination.js, lib/gossip/suspicion.js, lib/membership/iterator.js,
@@ -51,7 +57,7 @@ function philox(c, k) {
     var r = philox([0, 0, 0, 0], [0, 0]);
     if (r[0] !== 0x6627e8d5 || r[3] !== 0x9b00dbd8) { throw new Error('philox KAT failed'); }
 })();
-var TAG_SHUF = 0x53485546, TAG_SAMP = 0x53414d50;
+var TAG_SHUF = 0x53485546, TAG_SAMP = 0x53414d50, TAG_JOIN = 0x4a4f494e;
 function scaled(r, n) { return Math.floor((r / 4294967296) * n); }  // == (r*n)>>32 for n < 2^21
 
 // ---- virtual time
@@ -66,6 +72,7 @@ var Suspicion = R('lib/gossip/suspicion.js');
 var MembershipIterator = R('lib/membership/iterator.js');
 var HashRing = R('lib/ring/index.js');
 var onMembershipEvent = R('lib/on_membership_event.js');
+var mergeJoinResponses = R('lib/gossip/join-response-merge.js');
 
 function FakeRingpop(whoami) {
     EventEmitter.call(this);
@@ -92,7 +99,7 @@ input.cases.forEach(function (c) {
     var idOf = {};
     c.names.forEach(function (a, i) { idOf[a] = i; });
     var dead = c.dead;
-    var nodes = c.names.map(function (addr, v) {
+    function makeNode(addr, v) {
         var rp = new FakeRingpop(addr);
         rp.ring = new HashRing({replicaPoints: 1});
         rp.membership = initMembership(rp);
@@ -126,6 +133,11 @@ input.cases.forEach(function (c) {
             }
             return cands.slice(0, k);
         };
+        return rp;
+    }
+    var nodes = c.names.map(function (addr, v) {
+        var rp = makeNode(addr, v);
+        var m = rp.membership;
         // bootstrap (index.js:270-322): self alive, stash the rest, set(), ready
         m.makeAlive(addr, c.inc0[v]);
         m.update(c.names.map(function (a, i) {
@@ -147,6 +159,34 @@ input.cases.forEach(function (c) {
             var v = e[2];
             if (e[1] === 'kill') { down[v] = 1; }
             if (e[1] === 'revive') { down[v] = 0; }
+            if (e[1] === 'join') {
+                var addr = c.names[v], incv = Date.now();
+                var prev = nodes[v];
+                var rp = makeNode(addr, v);
+                rp.fullSyncs = prev.fullSyncs;
+                rp.membership.makeAlive(addr, incv);
+                // the responders: 3 live nodes other than v, partial Fisher-Yates over them in id
+                // order with the JOIN stream (join-sender.js selects from the bootstrap hosts)
+                var cands = [];
+                for (var u = 0; u < N; u++) { if (u !== v && live(u)) { cands.push(u); } }
+                var nj = Math.min(3, cands.length);
+                for (var q = 0; q < nj; q++) {
+                    var jj = q + scaled(philox([round, q, v, 0], [seed, TAG_JOIN])[0], cands.length - q);
+                    var tt = cands[q]; cands[q] = cands[jj]; cands[jj] = tt;
+                }
+                var responses = cands.slice(0, nj).map(function (u) {
+                    nodes[u].membership.makeAlive(addr, incv);  // join.js:126
+                    return wire({checksum: nodes[u].membership.checksum,
+                        members: nodes[u].dissemination.fullSync()});
+                });
+                rp.membership.update(mergeJoinResponses(rp, responses));  // stashed: not ready
+                rp.membership.set();
+                rp.isReady = true;
+                rp.dissemination.clearChanges();
+                rp.membership.shuffle();  // gossip.start
+                nodes[v] = rp;
+                down[v] = 0;
+            }
             if (e[1] === 'leave') {  // server/admin/member.js:76-93, while the node is up
                 var lm = nodes[v].membership.localMember;
                 if (live(v) && lm.status !== 'leave') {

@@ -11,7 +11,7 @@ var input = JSON.parse(fs.readFileSync(process.argv[2], 'utf8'));
 var fails = [], checks = 0;
 input.cases.forEach(function (c) {
     var sim = new amd.GossipSim(c.names, {inc0: c.inc0, dead: c.dead, seed: c.seed,
-        suspicionRounds: c.suspRounds, now0: c.now0});
+        suspicionRounds: c.suspRounds, now0: c.now0, events: c.events || []});
     c.checksums.forEach(function (want, r) {
         sim.step(1);
         var got = Array.from(sim.checksums());

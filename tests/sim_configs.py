@@ -22,6 +22,10 @@ CASES = {
     "c5": {"n": 100_000, "kill_pct": 1, "seed": 11, "susp": 25, "now0": NOW0, "max_rounds": 80},
     "c4s": {"n": 10_000, "kill_pct": 1, "seed": 11, "susp": 25, "now0": NOW0, "max_rounds": 140, "scenario": True,
             "after": 4},
+    # 100 running nodes crash at round 5; at round 45 fresh processes for 50 of them, and for 20
+    # of the nodes down from the start, bootstrap back in from join responses
+    "c4j": {"n": 10_000, "kill_pct": 1, "seed": 11, "susp": 25, "now0": NOW0, "max_rounds": 140, "scenario": "join",
+            "after": 4},
 }
 
 
@@ -34,7 +38,14 @@ def case_inputs(cfg):
     inc0 = S.c3_members(n)[2]
     dead = S.kill_set(n, k, cfg["seed"])
     events = []
-    if cfg.get("scenario"):
+    if cfg.get("scenario") == "join":
+        live = np.flatnonzero(dead == 0)
+        r = np.random.default_rng(cfg["seed"] + 1)
+        crashed = r.permutation(live)[:100]
+        events += [(5, "kill", int(v)) for v in sorted(crashed)]
+        events += [(45, "join", int(v)) for v in sorted(crashed[:50])]
+        events += [(45, "join", int(v)) for v in np.flatnonzero(dead)[:20]]
+    elif cfg.get("scenario"):
         live = np.flatnonzero(dead == 0)
         r = np.random.default_rng(cfg["seed"])
         pick = r.permutation(live)

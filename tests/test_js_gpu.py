@@ -43,7 +43,8 @@ def test_js_gossipsim_matches_reference_goldens(gpu, tmp_path):
     S = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(S)
     cases = []
-    for c in gu.load("sim_golden.json")["cases"][:2]:
+    golden = gu.load("sim_golden.json")["cases"]
+    for c in golden[:2] + [x for x in golden if x["name"] in ("n24-revive", "n30-join")]:
         n = c["n"]
         cases.append(dict(c, names=[S.c2_addr(i) for i in range(n)], inc0=[int(x) for x in S.c3_members(n)[2]]))
     res = run_node("sim_parity.js", {"cases": cases}, tmp_path)

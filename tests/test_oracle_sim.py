@@ -2,7 +2,8 @@
 every live node's membership checksum and maxPiggybackCount that the REFERENCE modules produced
 when driven through the same round model (tests/golden/ref_sim.js), plus the full syncs they
 sent and final member tables — for the kill-only cases and the scenario cases (leave, crash
-mid-run, revive with refutation and full sync, ring size crossing a power of ten)."""
+mid-run, revive with refutation and full sync, ring size crossing a power of ten, fresh
+processes joining from join responses)."""
 import importlib.util
 import os
 
@@ -52,7 +53,8 @@ def test_sim_oracle_windowed_order_matches_whole(orc, monkeypatch):
     names = [S.c2_addr(i) for i in range(n)]
     inc0 = S.c3_members(n)[2]
     dead = S.kill_set(n, k, seed)
-    ev = [(40, "revive", int(np.flatnonzero(dead)[0])), (5, "leave", 7)]
+    ev = [(40, "revive", int(np.flatnonzero(dead)[0])), (5, "leave", 7), (60, "join", int(np.flatnonzero(dead)[1])),
+          (90, "join", 7), (90, "join", 11)]
     whole = orc.Sim(names, inc0, dead, seed=seed, susp_rounds=3, events=ev)
     monkeypatch.setenv("ORC_SIM_ORDER_BYTES", "100")
     win = orc.Sim(names, inc0, dead, seed=seed, susp_rounds=3, events=ev, threads=3)

@@ -24,6 +24,7 @@ def _replay(gpu, name, G=None):
     kw = dict(seed=cfg["seed"], suspicion_rounds=cfg["susp"], now0=cfg["now0"], events=events)
     sim = gpu.ShardedGossipSim(names, inc0, dead, G, **kw) if G else gpu.GossipSim(names, inc0, dead, **kw)
     conv = None
+    last_ev = max((e[0] for e in events), default=0)
     try:
         for r in range(want["rounds"]):
             sim.step()
@@ -33,7 +34,7 @@ def _replay(gpu, name, G=None):
             assert hashlib.sha256(pb.astype("<u4").tobytes()).hexdigest() == want["piggyback"][r], "round %d" % r
             st = sim.stats()
             assert [st["pings"], st["pingreqs"], st["fullsyncs"], st["applied"]] == want["stats"][r], "round %d" % r
-            if conv is None and sim.converged():
+            if conv is None and r >= last_ev and sim.converged():
                 conv = r
         assert conv == want["converged_round"]
     finally:
@@ -50,6 +51,11 @@ def test_c4_scenario_full_size(gpu):
 
 def test_c4_scenario_sharded(gpu):
     _replay(gpu, "c4s", G=4)
+
+
+def test_c4_join_full_size(gpu):
+    """70 fresh processes bootstrapping into the 10k cluster from join responses."""
+    _replay(gpu, "c4j")
 
 
 def test_c5_full_size_one_gpu(gpu):

@@ -163,3 +163,14 @@ def test_sim_capacity_overflow_is_loud(gpu, monkeypatch):
         for _ in range(30):
             g.step()
     g.close()
+
+
+def test_sim_join_refused_when_sharded(gpu):
+    """A join reads its responders' views, which a sharded simulator spreads over handles: the
+    event is refused loudly there instead of being approximated."""
+    case = next(c for c in gu.load("sim_golden.json")["cases"] if c["name"] == "n30-join")
+    _, sim = _golden_sim(gpu, case, G=2)
+    with pytest.raises(gpu.RingpopAmdError, match="join"):
+        for _ in range(25):
+            sim.step()
+    sim.close()
