@@ -232,8 +232,9 @@ def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=64, warmup=3):
            "updates_per_s": k * batches / dt, "ms_per_batch": dt * 1e3 / batches,
            "gpu_ms_per_batch": e0.elapsed_time(e1) / batches, "checksum": ck,
            "note": "every batch applies most of its updates and its checksum string is built after it; the "
-                   "strings' serial farmhash chains run up to 32 side by side (one workgroup each) and the "
-                   "last batch's checksum is read inside the timed region"}
+                   "strings' serial farmhash chains run side by side (one workgroup each; up to 256 pending "
+                   "strings within a 1 GiB slot pool, RP_MEMBERS_CK_BYTES) and the last batch's checksum is "
+                   "read inside the timed region"}
     # the fold alone (sort + k_fold), HIP events per batch on the launch stream
     rpa.check(rpa.lib().rp_members_defer_checksum(m._h, 1))
     nf = 20

@@ -10,6 +10,7 @@
 // and hashed by the long-chain farmhash kernel; every step is gated on "anything applied" read
 // from device memory, so a batch never syncs with the host.
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -22,15 +23,6 @@
 namespace rp {
 
 namespace {
-
-__global__ void k_sort_init(const uint32_t* __restrict__ ids, uint32_t k, uint32_t* __restrict__ sk,
-                            uint32_t* __restrict__ sv) {
-    const uint32_t gstride = gridDim.x * blockDim.x;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < k; i += gstride) {
-        sk[i] = ids[i];
-        sv[i] = i;
-    }
-}
 
 // Damp-scoring state by member id (Member.dampScore / lastUpdateDampScore /
 // lastUpdateTimestamp, member.js:35-39) and the per-change outputs of the batch being folded.
@@ -264,13 +256,15 @@ struct Members {
     DevBuf<int64_t> inc;
     DevBuf<uint32_t> ck;        // [0] checksum, [1] is_set
     DevBuf<uint32_t> napplied;  // per-batch applied count (the checksum gate)
-    // Checksum strings wait in slots until read or until kSlots are pending, then one launch
-    // hashes them side by side (one serial chain per workgroup): a batched caller pays one
-    // chain's latency per group instead of per batch. Reads flush first.
-    static constexpr uint32_t kSlots = 32;
-    DevBuf<uint8_t> ck_buf;   // kSlots strings of slot_bytes
+    // Checksum strings wait in slots until read or until every slot is pending, then one launch
+    // hashes them side by side (one serial chain per workgroup, up to one per CU): a batched
+    // caller pays one chain's latency per group instead of per batch. Reads flush first. The
+    // slot count is what fits RP_MEMBERS_CK_BYTES (default 1 GiB of HBM), at most kMaxSlots.
+    static constexpr uint32_t kMaxSlots = 256;
+    uint32_t nslots = 1;
+    DevBuf<uint8_t> ck_buf;   // nslots strings of slot_bytes
     uint64_t slot_bytes = 0;
-    DevBuf<uint32_t> ck_meta;  // [kSlots][4]: total, gate, hash, done
+    DevBuf<uint32_t> ck_meta;  // [kMaxSlots][4]: total, gate, hash, done
     uint32_t npending = 0;
     hipStream_t pend_st = nullptr;  // the stream the pending strings were built on
     DevBuf<uint32_t> ck_len, ck_pos;
@@ -362,10 +356,9 @@ struct Members {
         if (k) {
             sk.reserve(k);
             sv.reserve(k);
-            hipLaunchKernelGGL(k_sort_init, dim3(grid_for(k, 256)), dim3(256), 0, s, ids, k, sk.p, sv.p);
             int bits = 8;
             while (bits < 32 && (1ull << bits) < nt.size()) bits += 8;
-            radix_sort_pairs(sk.p, sv.p, k, 0, bits, s, ws);
+            radix_sort_index(ids, sk.p, sv.p, k, 0, bits, s, ws);
             if (damp_on) {
                 d_out.reserve(k);
                 d_exc.reserve(k);
@@ -392,10 +385,9 @@ struct Members {
         sv.reserve(k);
         mk.reserve(k);
         mpos.reserve(k + 1);
-        hipLaunchKernelGGL(k_sort_init, dim3(grid_for(k, 256)), dim3(256), 0, s, ids, k, sk.p, sv.p);
         int bits = 8;
         while (bits < 32 && (1ull << bits) < nt.size()) bits += 8;
-        radix_sort_pairs(sk.p, sv.p, k, 0, bits, s, ws);
+        radix_sort_index(ids, sk.p, sv.p, k, 0, bits, s, ws);
         RP_HIP(hipMemsetAsync(mk.p, 0, 4ull * k, s));
         hipLaunchKernelGGL(k_merge_pick, dim3(grid_for(k, 256)), dim3(256), 0, s, sk.p, sv.p, k, chi, local_id, mk.p);
         hipLaunchKernelGGL(k_flag_nonzero, dim3(grid_for(k, 256)), dim3(256), 0, s, mk.p, k, mpos.p);
@@ -422,12 +414,15 @@ struct Members {
         }
         if (need > slot_bytes) {
             ck_buf.release();
-            ck_buf.reserve(need * kSlots);
+            const char* e = getenv("RP_MEMBERS_CK_BYTES");
+            const uint64_t budget = e && *e ? strtoull(e, nullptr, 10) : (1ull << 30);
+            nslots = (uint32_t)std::min<uint64_t>(kMaxSlots, std::max<uint64_t>(1, budget / need));
+            ck_buf.reserve(need * nslots);
             slot_bytes = need;
         }
-        if (npending == kSlots) flush_checksums();
+        if (npending == nslots) flush_checksums();
         pend_st = s;
-        ck_meta.reserve(4 * kSlots);
+        ck_meta.reserve(4 * kMaxSlots);
         uint8_t* buf = ck_buf.p + slot_bytes * npending;
         hipLaunchKernelGGL(k_mck_len, dim3(grid_for(n, 256)), dim3(256), 0, s, nt.sorted.p, n, exists.p, status.p,
                            inc.p, nt.d_noff.p, gate, ck_len.p);
