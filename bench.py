@@ -185,11 +185,11 @@ def sim_cpu_baseline(n, kill_pct=1, seed=11, min_seconds=15.0, max_rounds=60, th
 
 # ------------------------------------------------------------------ device legs
 
-def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=64, warmup=3):
-    """C3 (BASELINE.json configs[2]): 100k-member table, batches of 100k updates (1% repeated
-    addresses), Membership.update fold + one checksum per batch, inputs resident in HBM. Also:
-    the fold alone (checksum deferred) against the HBM roofline at 49 B/update, the checksum
-    chain alone, and the fold at a batch large enough not to be launch-bound."""
+def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=512, warmup=3):
+    """C3 (BASELINE.json configs[2]): 100k-member table, a stream of batches of 100k updates (1%
+    repeated addresses), Membership.update fold + one checksum per batch, inputs resident in HBM.
+    Also: the fold alone (checksum deferred) against the HBM roofline at 49 B/update, the
+    checksum chain alone, and the fold at a batch large enough not to be launch-bound."""
     S = _synth()
     names, st0, inc0 = S.c3_members(n)
     m = rpa.Membership(whoami=names[0], capacity=n, device=local)
@@ -198,12 +198,17 @@ def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=64, warmup=3):
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
     # fresh batches (incarnations +3 per batch: most updates apply, every batch pays the
-    # checksum), all resident in HBM before the timed region
-    bufs = []
-    for b in range(warmup + batches + 20):
-        ids, us, ui = S.c3_updates(n, k, seed=100 + b, base_inc=inc0 + 3 * b)
-        bufs.append((torch.from_numpy(ids.view(np.int32)).cuda(), torch.from_numpy(us).cuda(),
+    # checksum), all resident in HBM before the timed region: 64 id/status sets, batch b takes
+    # set b % 64 with its incarnations raised by 192 per lap (= inc0 + 3b + {-1, 0, +1}, as a
+    # fresh c3_updates batch would have)
+    nsets = 64
+    sets = []
+    for q in range(nsets):
+        ids, us, ui = S.c3_updates(n, k, seed=100 + q, base_inc=inc0 + 3 * q)
+        sets.append((torch.from_numpy(ids.view(np.int32)).cuda(), torch.from_numpy(us).cuda(),
                      torch.from_numpy(ui).cuda()))
+    bufs = [(sets[b % nsets][0], sets[b % nsets][1], sets[b % nsets][2] + 3 * nsets * (b // nsets))
+            for b in range(warmup + batches + 20)]
     app = torch.empty(k, dtype=torch.uint8, device="cuda")
     nst = torch.empty(k, dtype=torch.uint8, device="cuda")
     ninc = torch.empty(k, dtype=torch.int64, device="cuda")
@@ -232,9 +237,10 @@ def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=64, warmup=3):
            "updates_per_s": k * batches / dt, "ms_per_batch": dt * 1e3 / batches,
            "gpu_ms_per_batch": e0.elapsed_time(e1) / batches, "checksum": ck,
            "note": "every batch applies most of its updates and its checksum string is built after it; the "
-                   "strings' serial farmhash chains run side by side (one workgroup each; up to 256 pending "
-                   "strings within a 1 GiB slot pool, RP_MEMBERS_CK_BYTES) and the last batch's checksum is "
-                   "read inside the timed region"}
+                   "strings' serial farmhash chains run in groups of 64 side by side (one workgroup each) on a "
+                   "side stream, overlapping the next batches' folds (256 slots within a 1 GiB pool, "
+                   "RP_MEMBERS_CK_BYTES); the last batch's checksum is read inside the timed region, so "
+                   "the final group's chains are in the time"}
     # the fold alone (sort + k_fold), HIP events per batch on the launch stream
     rpa.check(rpa.lib().rp_members_defer_checksum(m._h, 1))
     nf = 20

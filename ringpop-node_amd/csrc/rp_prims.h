@@ -33,9 +33,14 @@ void radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint64_t n, int begin_bit,
                       hipStream_t st, Scratch& ws);
 
 // Stable sort of the pairs (keys_in[i], i): sorted keys to keys_out, original indices to
-// idx_out (keys_in is not modified; no copy of it or iota is made).
+// idx_out (keys_in is not modified; no copy of it or iota is made). run_if (device word, may be
+// null): the launches do nothing unless *run_if != 0 when they run; only with
+// single_pass_sort(n).
 void radix_sort_index(const uint32_t* keys_in, uint32_t* keys_out, uint32_t* idx_out, uint64_t n, int begin_bit,
-                      int end_bit, hipStream_t st, Scratch& ws);
+                      int end_bit, hipStream_t st, Scratch& ws, const uint32_t* run_if = nullptr);
+
+// Whether radix sorts of n elements take the single-pass path.
+bool single_pass_sort(uint64_t n);
 
 // RP_PRIMS_MULTIPASS=1 selects the earlier multi-launch scan and sort (A/B and cross-checks).
 bool prims_multipass();

@@ -244,7 +244,9 @@ __device__ uint32_t lookback_thread(const uint64_t* lb, uint32_t tile, uint32_t 
 // turns them into digit bases (exclusive scan per pass) and zeroes them for the next sort.
 // dig: [0, 1024) histograms, [1024, 2048) bases, [2048] finished-workgroup counter.
 __global__ __launch_bounds__(kThreads) void k_os_hist(const uint32_t* __restrict__ keys, uint32_t n, int begin,
-                                                      int npass, uint32_t* __restrict__ dig) {
+                                                      int npass, uint32_t* __restrict__ dig,
+                                                      const uint32_t* __restrict__ run_if) {
+    if (run_if && *run_if == 0) return;  // (every workgroup: the finish counter is untouched)
     __shared__ uint32_t h[4][256];
     __shared__ uint32_t lds[kThreads + 1];
     __shared__ bool last;
@@ -301,7 +303,8 @@ __global__ __launch_bounds__(kThreads) void k_os_scatter(const uint32_t* __restr
                                                          uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                          uint32_t n, int shift, const uint32_t* __restrict__ dbase,
                                                          uint64_t* __restrict__ lb, unsigned long long* ctr,
-                                                         unsigned long long tbase, uint64_t tag) {
+                                                         unsigned long long tbase, uint64_t tag,
+                                                         const uint32_t* __restrict__ run_if) {
     constexpr int kOsTile = kThreads * kOsItems;
     constexpr int kOsWave = kOsTile / (kThreads / 64);
     __shared__ uint32_t wcnt[kThreads / 64][256];
@@ -313,7 +316,8 @@ __global__ __launch_bounds__(kThreads) void k_os_scatter(const uint32_t* __restr
     const bool has_v = IOTA || vin != nullptr;
 #pragma unroll
     for (int w = 0; w < kThreads / 64; w++) wcnt[w][tid] = 0;
-    const uint32_t tile = take_ticket(ctr, tbase);  // (syncs)
+    const uint32_t tile = take_ticket(ctr, tbase);  // (syncs; taken even when skipping)
+    if (run_if && *run_if == 0) return;
     const uint32_t t0 = tile * (uint32_t)kOsTile;
     const uint32_t w0 = t0 + (uint32_t)(wave * kOsWave);
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -489,7 +493,7 @@ uint64_t lb_begin(Scratch& ws, uint64_t tiles, uint32_t cols, hipStream_t st, un
 }
 
 void os_sort(const uint32_t* kin0, const uint32_t* vin0, bool iota, uint32_t* keys, uint32_t* vals, uint64_t n,
-             int begin_bit, int end_bit, hipStream_t st, Scratch& ws) {
+             int begin_bit, int end_bit, hipStream_t st, Scratch& ws, const uint32_t* run_if = nullptr) {
     const int npass = (end_bit - begin_bit + 7) / 8;
     RP_REQUIRE(npass >= 1 && npass <= 4, "radix sort: bit range");
     // 16 elements per thread (4096-element tiles) for large sorts; 8 below 2^20 elements, where
@@ -507,7 +511,7 @@ void os_sort(const uint32_t* kin0, const uint32_t* vin0, bool iota, uint32_t* ke
     }
     const uint32_t hist_blocks = (uint32_t)std::min<uint64_t>((n + 1023) / 1024, 1024);
     hipLaunchKernelGGL(k_os_hist, dim3(hist_blocks), dim3(kThreads), 0, st, kin0, (uint32_t)n, begin_bit, npass,
-                       ws.dig.p);
+                       ws.dig.p, run_if);
     RP_HIP(hipGetLastError());
     const bool has_v = iota || vin0 != nullptr;
     ws.a.reserve(n);
@@ -542,7 +546,8 @@ void os_sort(const uint32_t* kin0, const uint32_t* vin0, bool iota, uint32_t* ke
         auto kern = io ? (items == 16 ? k_os_scatter<true, 16> : k_os_scatter<true, 8>)
                        : (items == 16 ? k_os_scatter<false, 16> : k_os_scatter<false, 8>);
         hipLaunchKernelGGL(kern, dim3(tiles), dim3(kThreads), 0, st, kin, io ? nullptr : vin, dk[p], dv[p],
-                           (uint32_t)n, begin_bit + 8 * p, ws.dig.p + 1024 + 256 * p, ws.lb.p, ws.ticket.p, tb, tag);
+                           (uint32_t)n, begin_bit + 8 * p, ws.dig.p + 1024 + 256 * p, ws.lb.p, ws.ticket.p, tb, tag,
+                           run_if);
         RP_HIP(hipGetLastError());
         kin = dk[p];
         vin = dv[p];
@@ -582,17 +587,23 @@ void scan_exclusive_u32(const uint32_t* in, uint32_t* out, uint64_t n, hipStream
 }
 
 void radix_sort_index(const uint32_t* keys_in, uint32_t* keys_out, uint32_t* idx_out, uint64_t n, int begin_bit,
-                      int end_bit, hipStream_t st, Scratch& ws) {
+                      int end_bit, hipStream_t st, Scratch& ws, const uint32_t* run_if) {
     if (n == 0) return;
     RP_REQUIRE(n < (1ull << 32), "radix_sort_index: n must be < 2^32");
     RP_REQUIRE(keys_in != keys_out, "radix_sort_index: keys_in must not be keys_out");
-    if (!single_pass_sort(n) || n == 1) {
+    if (n == 1) {  // (run regardless of run_if: harmless)
+        RP_HIP(hipMemcpyAsync(keys_out, keys_in, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+        iota_u32(idx_out, 1, st);
+        return;
+    }
+    if (!single_pass_sort(n)) {
+        RP_REQUIRE(!run_if, "radix_sort_index: run_if needs the single-pass sort (single_pass_sort(n))");
         RP_HIP(hipMemcpyAsync(keys_out, keys_in, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
         iota_u32(idx_out, n, st);
         radix_sort_pairs(keys_out, idx_out, n, begin_bit, end_bit, st, ws);
         return;
     }
-    os_sort(keys_in, nullptr, true, keys_out, idx_out, n, begin_bit, end_bit, st, ws);
+    os_sort(keys_in, nullptr, true, keys_out, idx_out, n, begin_bit, end_bit, st, ws, run_if);
 }
 
 void radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint64_t n, int begin_bit, int end_bit,

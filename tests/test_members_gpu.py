@@ -186,7 +186,8 @@ def test_bootstrap_set_vs_oracle(gpu, orc):
 @pytest.mark.parametrize("nbatches,tail_noops", [(5, 0), (37, 3), (70, 0)])
 def test_grouped_checksums_across_unread_batches(gpu, orc, nbatches, tail_noops):
     """Device batches whose checksums are never read in between: their strings wait in slots and
-    are hashed side by side (32 per launch). A read after the last batch must equal the oracle's
+    are hashed side by side (groups of up to 64 per launch, on a side stream). A read after the
+    last batch must equal the oracle's
     checksum after the same sequence — including when the last batches applied nothing (the
     checksum is then the last applying batch's), and across several full groups."""
     S = synth()
@@ -209,4 +210,75 @@ def test_grouped_checksums_across_unread_batches(gpu, orc, nbatches, tail_noops)
         o.update_ids(ids, us, ui, False, 1434500000000 + b)
     torch.cuda.synchronize()
     assert m.checksum == o.checksum
+    assert m.generate_checksum_string() == o.checksum_string()
+
+
+@pytest.mark.parametrize("budget", [None, "3"], ids=["default-pool", "three-slots"])
+def test_checksum_groups_wrap_with_reads(gpu, orc, budget, monkeypatch):
+    """300 unread batches cycle through every slot group more than once (a group is rebuilt only
+    after its previous chains finished), with checksum reads at scattered points in between: each
+    read equals the oracle's checksum after the same prefix. RP_MEMBERS_CK_BYTES=3 leaves three
+    one-string slots (groups of one)."""
+    if budget:
+        monkeypatch.setenv("RP_MEMBERS_CK_BYTES", str(int(budget) * 200_000))
+    S = synth()
+    n = k = 4000
+    names, st0, inc0 = S.c3_members(n)
+    m = gpu.Membership(whoami=names[0], capacity=n)
+    o = orc.Members(names, local=names[0], join_seed=0)
+    ids0 = np.asarray(m.intern(names), dtype=np.uint32)
+    m.update_ids(ids0, st0, inc0, now_ms=1)
+    o.update_ids(ids0, st0, inc0, False, 1)
+    stream = torch.cuda.current_stream()
+    app = torch.empty(k, dtype=torch.uint8, device="cuda")
+    na = torch.zeros(1, dtype=torch.int32, device="cuda")
+    reads = {17, 64, 65, 130, 199, 257}
+    keep = []
+    for b in range(300):
+        ids, us, ui = S.c3_updates(n, k, seed=900 + b, base_inc=inc0 + 3 * b)
+        d = [torch.from_numpy(ids.view(np.int32)).cuda(), torch.from_numpy(us).cuda(), torch.from_numpy(ui).cuda()]
+        keep.append(d)
+        m.update_dev(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), k, 1434500000000 + b, app.data_ptr(),
+                     None, None, na.data_ptr(), stream.cuda_stream)
+        o.update_ids(ids, us, ui, False, 1434500000000 + b)
+        if b in reads:
+            assert m.checksum == o.checksum, b
+    torch.cuda.synchronize()
+    assert m.checksum == o.checksum
+
+
+@pytest.mark.parametrize("sorted_fold", [False, True], ids=["grouped", "sorted"])
+def test_hot_addresses_take_the_sorted_path(gpu, orc, sorted_fold, monkeypatch):
+    """The grouped fold handles up to 16 changes per address in a batch; a batch where one
+    address has more (here 17 and 60, next to addresses with exactly 16 and 15) takes the sorted
+    path. Every batch - before, during and after the overflow - must match the oracle, and the
+    grouped fold's per-address state must be clean again after an overflowing batch."""
+    if sorted_fold:
+        monkeypatch.setenv("RP_MEMBERS_SORTED_FOLD", "1")
+    S = synth()
+    n = 3000
+    names, st0, inc0 = S.c3_members(n)
+    m = gpu.Membership(whoami=names[0], capacity=n)
+    o = orc.Members(names, local=names[0], join_seed=0)
+    ids0 = np.asarray(m.intern(names), dtype=np.uint32)
+    m.update_ids(ids0, st0, inc0, now_ms=1)
+    o.update_ids(ids0, st0, inc0, False, 1)
+    rng = np.random.default_rng(5)
+    for b, hot in enumerate([{7: 16, 8: 15}, {7: 17, 9: 60, 10: 16}, {11: 3}, {12: 40}, {}]):
+        ids, us, ui = S.c3_updates(n, 2000, seed=300 + b, base_inc=inc0 + 3 * b)
+        ids, us, ui = list(ids), list(us), list(ui)
+        for a, c in hot.items():
+            for _ in range(c):
+                p = int(rng.integers(0, len(ids) + 1))
+                ids.insert(p, a)
+                us.insert(p, int(rng.integers(0, 4)))
+                ui.insert(p, int(inc0[a]) + 3 * b + int(rng.integers(-2, 3)))
+        ids = np.asarray(ids, np.uint32)
+        us = np.asarray(us, np.uint8)
+        ui = np.asarray(ui, np.int64)
+        ga, gs, gi, gna = m.update_ids(ids, us, ui, now_ms=1434500000000 + b)
+        oa, os_, oi, ona = o.update_ids(ids, us, ui, False, 1434500000000 + b)
+        assert gna == ona, b
+        assert np.array_equal(ga > 0, oa > 0), b
+        assert m.checksum == o.checksum, b
     assert m.generate_checksum_string() == o.checksum_string()
