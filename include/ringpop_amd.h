@@ -367,6 +367,19 @@ int rp_sim_outbox(rp_sim *s, uint64_t *nmsg, uint64_t *nrec, void **buf);
 int rp_sim_inbox(rp_sim *s, const uint64_t *nmsg, const uint64_t *nrec, void **buf);
 int rp_sim_exchange_local(rp_sim *const *shards, uint32_t nshards);
 int rp_sim_converged_local(rp_sim *s, uint32_t *out4);
+/* JOIN events on a sharded simulator (a joiner reads its responders' views, which other shards
+ * may hold). Before rp_sim_stage(s, 0) of every round, on every shard, repeat until *has == 0:
+ * rp_sim_join_export applies the round's events up to its next join, runs the join handler of
+ * the responders this shard owns and returns a device buffer of *bytes bytes holding their
+ * rows (zeros elsewhere; every byte has exactly one writing shard). The caller combines the
+ * shards' buffers into each shard's own buffer by a byte-wise sum (an RCCL / gloo all-reduce of
+ * uint8, or rp_sim_join_exchange_local for handles in one process), then calls
+ * rp_sim_join_import, which builds the joiner's view on its shard. (Replaces the responders'
+ * join handler + the joiner's mergeJoinResponses / set(): server/protocol/join.js:126,
+ * join-response-merge.js:40-56, membership/index.js:208-247.) */
+int rp_sim_join_export(rp_sim *s, int *has, void **buf, uint64_t *bytes);
+int rp_sim_join_import(rp_sim *s);
+int rp_sim_join_exchange_local(rp_sim *const *shards, uint32_t nshards);
 
 /* ---- Scenarios. Events run before phase A of their round, in the order given:
  *   RP_SIM_KILL    the node goes down (crash / SIGSTOP, scripts/tick-cluster.js:417-470): it

@@ -105,6 +105,9 @@ SIGNATURES = {
     "rp_sim_outbox": (_INT, [_P, _P, _P, _P]),
     "rp_sim_inbox": (_INT, [_P, _P, _P, _P]),
     "rp_sim_exchange_local": (_INT, [_P, _U32]),
+    "rp_sim_join_export": (_INT, [_P, _P, _P, _P]),
+    "rp_sim_join_import": (_INT, [_P]),
+    "rp_sim_join_exchange_local": (_INT, [_P, _U32]),
     "rp_sim_converged_local": (_INT, [_P, _P]),
     "rp_sim_create_scenario": (_INT, [_U32, _P, _P, _P, _P, _U32, _U32, ctypes.c_int64, _INT, _P, _U32, _U32, _P, _U32,
                                       _P]),
@@ -774,6 +777,18 @@ class SimShard:
     def stage(self, k):
         check(lib().rp_sim_stage(self._h, k))
 
+    def join_export(self):
+        """The round's events up to its next join (rp_sim_join_export): (has, device buffer,
+        bytes) with this shard's responders' rows; the caller sums the shards' buffers."""
+        has = ctypes.c_int()
+        bp = ctypes.c_void_p()
+        nb = ctypes.c_uint64()
+        check(lib().rp_sim_join_export(self._h, ctypes.byref(has), ctypes.byref(bp), ctypes.byref(nb)))
+        return bool(has.value), bp.value or 0, nb.value
+
+    def join_import(self):
+        check(lib().rp_sim_join_import(self._h))
+
     def outbox(self):
         """(nmsg[G], nrec[G], device buffer): per destination in shard order, a segment of
         nmsg[g] 40-byte headers then nrec[g] 24-byte records."""
@@ -865,8 +880,19 @@ class ShardedGossipSim:
         for s in self.shards:
             s.close()
 
+    def _joins(self):
+        """The round's join events (rp_sim_join_export / exchange / import, before stage 0)."""
+        while True:
+            has = [s.join_export()[0] for s in self.shards]
+            if not any(has):
+                return
+            check(lib().rp_sim_join_exchange_local(self._arr, self.G))
+            for s in self.shards:
+                s.join_import()
+
     def step(self, rounds=1):
         for _ in range(rounds):
+            self._joins()
             for k in range(SIM_STAGES):
                 for s in self.shards:
                     s.stage(k)
@@ -978,6 +1004,20 @@ class MessageExchange:
             self.copy(in_buf, recv.data_ptr(), tot_in)
         return in_nmsg, in_nrec
 
+    def sum_bytes(self, buf, nbytes):
+        """Byte-wise sum of every rank's device buffer into each rank's (the join exchange)."""
+        torch, dist = self.torch, self.dist
+        if self.on_device:
+            t = torch.as_tensor(_DeviceBytes(buf, nbytes), device=self.device)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            torch.cuda.current_stream().synchronize()
+        else:
+            h = self._staging("join", nbytes)
+            self.copy(h.data_ptr(), buf, nbytes)
+            v = h[:nbytes]
+            dist.all_reduce(v, op=dist.ReduceOp.SUM, group=self.group)
+            self.copy(buf, h.data_ptr(), nbytes)
+
 
 class DistGossipSim:
     """One shard of the simulator per torch.distributed rank (C5 over 1/2/4/8 GPUs: views
@@ -1000,6 +1040,12 @@ class DistGossipSim:
     def step(self, rounds=1):
         sh = self.shard
         for _ in range(rounds):
+            while True:  # the round's joins: every rank exports, the buffers are summed, then import
+                has, buf, nb = sh.join_export()
+                if not has:
+                    break
+                self.xchg.sum_bytes(buf, nb)
+                sh.join_import()
             for k in range(SIM_STAGES):
                 sh.stage(k)
                 if k < SIM_STAGES - 1:

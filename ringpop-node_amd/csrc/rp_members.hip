@@ -58,8 +58,10 @@ struct FoldArgs {
 // 2 = created a new member. With damp tracking on, an applied update to another member takes
 // _applyUpdatePenalty (member.js:98-107, 133-153) and every applied update stamps
 // lastUpdateTimestamp (:115-118).
+// Returns the number of changes applied (the caller sums them per wave: one atomic per wave,
+// not per address, on the batch's applied counter).
 template <class Change>
-__device__ __forceinline__ void fold_address(const FoldArgs& A, uint32_t id, uint32_t c, Change change) {
+__device__ __forceinline__ uint32_t fold_address(const FoldArgs& A, uint32_t id, uint32_t c, Change change) {
     const DampArgs& da = A.da;
     bool ex = A.exists[id] != 0;
     uint8_t st = A.status[id];
@@ -114,7 +116,14 @@ __device__ __forceinline__ void fold_address(const FoldArgs& A, uint32_t id, uin
         da.last[id] = ls;
         da.ts[id] = lt;
     }
-    if (napp) atomicAdd(A.n_applied, napp);
+    return napp;
+}
+
+// Adds every lane's v to *p with one atomic per wave; called by all lanes of the wave.
+__device__ __forceinline__ void wave_atomic_add(uint32_t* p, uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(p, v);
 }
 
 // Sorted path: one lane per id segment of the (id, arrival)-sorted batch. run_if (may be null):
@@ -123,13 +132,15 @@ __global__ void k_fold(const uint32_t* __restrict__ sk, const uint32_t* __restri
                        const uint32_t* __restrict__ run_if) {
     if (run_if && *run_if == 0) return;
     const uint32_t gstride = gridDim.x * blockDim.x;
+    uint32_t napp = 0;
     for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < k; p += gstride) {
         const uint32_t id = sk[p];
         if (p > 0 && sk[p - 1] == id) continue;  // not a segment head
         uint32_t c = 1;
         while (p + c < k && sk[p + c] == id) c++;
-        fold_address(A, id, c, [&](uint32_t q) { return sv[p + q]; });
+        napp += fold_address(A, id, c, [&](uint32_t q) { return sv[p + q]; });
     }
+    wave_atomic_add(A.n_applied, napp);
 }
 
 // Grouped path (no sort): every change links itself into its address's list (arbitrary order)
@@ -162,11 +173,12 @@ __global__ void k_fold_grouped(const uint32_t* __restrict__ ids, uint32_t k, uin
                                const uint32_t* __restrict__ overflow, FoldArgs A) {
     if (*overflow) return;
     const uint32_t gstride = gridDim.x * blockDim.x;
+    uint32_t napp = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < k; i += gstride) {
         const uint32_t id = ids[i];
         const uint32_t c = cnt[id];
         if (c == 1) {
-            fold_address(A, id, 1, [&](uint32_t) { return i; });
+            napp += fold_address(A, id, 1, [&](uint32_t) { return i; });
             cnt[id] = 0;
             head[id] = kGroupEmpty;
             continue;
@@ -183,10 +195,11 @@ __global__ void k_fold_grouped(const uint32_t* __restrict__ ids, uint32_t k, uin
             idx[r] = x;
             j = nxt[j];
         }
-        fold_address(A, id, c, [&](uint32_t q) { return idx[q]; });
+        napp += fold_address(A, id, c, [&](uint32_t q) { return idx[q]; });
         cnt[id] = 0;
         head[id] = kGroupEmpty;
     }
+    wave_atomic_add(A.n_applied, napp);
 }
 
 // After an overflowing batch took the sorted path: reset the entries its changes linked.

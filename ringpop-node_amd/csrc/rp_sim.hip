@@ -2215,7 +2215,7 @@ __global__ __launch_bounds__(kT) void k_leave(SimDev S, const uint32_t* __restri
     }
 }
 
-// ---- a fresh process joining from join responses (RP_SIM_JOIN; one shard)
+// ---- a fresh process joining from join responses (RP_SIM_JOIN)
 //
 // index.js:240-322 for node v: makeAlive(self, Date.now()); each responder (chosen on the host)
 // answers the join with makeAlive(v, that incarnation) (server/protocol/join.js:126) and its
@@ -2225,35 +2225,74 @@ __global__ __launch_bounds__(kT) void k_leave(SimDev S, const uint32_t* __restri
 // (on_membership_event.js:42-67) puts alive / suspect members in the ring without a ringChanged
 // and starts a timer per suspect member. The dissemination is cleared as at bootstrap.
 
-// the responders' join handler
+// Where the joiner reads its responders' rows: the shard's own view rows when every responder
+// is local (one shard), else a join exchange buffer (JoinBuf layout) that the shards filled with
+// their responders' rows.
+struct JoinSrc {
+    const uint8_t* st[3];   // status (masked or not: read through ST_MASK)
+    const int64_t* inc[3];
+    const uint32_t* order0;  // the first responder's members array
+};
+
+// Join exchange buffer: [3][N] statuses, [3][N] incarnations (16-B aligned), [N] order of r0.
+struct JoinBuf {
+    uint64_t o_inc, o_ord, bytes;
+    explicit JoinBuf(uint32_t N) {
+        o_inc = (3ull * N + 15) & ~15ull;
+        o_ord = o_inc + 24ull * N;
+        bytes = o_ord + 4ull * N;
+    }
+    JoinSrc src(const uint8_t* b, uint32_t N) const {
+        JoinSrc j{};
+        for (int q = 0; q < 3; q++) {
+            j.st[q] = b + (uint64_t)q * N;
+            j.inc[q] = reinterpret_cast<const int64_t*>(b + o_inc) + (uint64_t)q * N;
+        }
+        j.order0 = reinterpret_cast<const uint32_t*>(b + o_ord);
+        return j;
+    }
+};
+
+// the responders' join handler, on the shard that owns each (bit q of `local`)
 __global__ __launch_bounds__(kT) void k_join_resp(SimDev S, uint32_t v, int64_t incv, uint32_t r0, uint32_t r1,
-                                                  uint32_t r2, uint32_t nj) {
+                                                  uint32_t r2, uint32_t nj, uint32_t local) {
     __shared__ Lds L;
     __shared__ Rec tmp;
     const int64_t now = S.now0 + 200 * S.round;
     for (uint32_t q = blockIdx.x; q < nj; q += gridDim.x) {
+        if (!((local >> q) & 1u)) continue;
         const uint32_t r = q == 0 ? r0 : q == 1 ? r1 : r2;
         block_make(S, r - S.v0, v, ST_ALIVE, incv, L, now, &tmp);
     }
 }
 
+// this shard's responders' rows into the (zeroed) join exchange buffer
+__global__ void k_join_export(SimDev S, uint32_t r0, uint32_t r1, uint32_t r2, uint32_t nj, uint32_t local,
+                              uint8_t* __restrict__ jst, int64_t* __restrict__ jinc, uint32_t* __restrict__ jord) {
+    for (uint32_t m = blockIdx.x * blockDim.x + threadIdx.x; m < S.N; m += gridDim.x * blockDim.x)
+        for (uint32_t q = 0; q < nj; q++) {
+            if (!((local >> q) & 1u)) continue;
+            const uint64_t row = (uint64_t)((q == 0 ? r0 : q == 1 ? r1 : r2) - S.v0) * S.N;
+            jst[(uint64_t)q * S.N + m] = S.st[row + m] & ST_MASK;
+            jinc[(uint64_t)q * S.N + m] = S.inc[row + m];
+            if (q == 0) jord[m] = S.order[row + m];
+        }
+}
+
 // v's position in the first response's members array; the joiner's deviation words cleared
-__global__ void k_join_prep(SimDev S, uint32_t v, uint32_t r0, uint32_t* __restrict__ scratch) {
-    const uint64_t row0 = (uint64_t)(r0 - S.v0) * S.N, rowv = (uint64_t)(v - S.v0) * S.N;
+__global__ void k_join_prep(SimDev S, uint32_t v, JoinSrc J, uint32_t* __restrict__ scratch) {
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < S.N; k += gridDim.x * blockDim.x)
-        if (S.order[row0 + k] == v) scratch[0] = k;
+        if (J.order0[k] == v) scratch[0] = k;
     for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < S.W; w += gridDim.x * blockDim.x)
         S.dev[(uint64_t)(v - S.v0) * S.W + w] = 0;
-    (void)rowv;
 }
 
 // the joiner's rows, members array, timers; scratch[0] = v's position in r0's array,
 // scratch[1] accumulates the members outside the ring
-__global__ void k_join_view(SimDev S, uint32_t v, int64_t incv, uint32_t r0, uint32_t r1, uint32_t r2, uint32_t nj,
+__global__ void k_join_view(SimDev S, uint32_t v, int64_t incv, uint32_t nj, JoinSrc J,
                             uint32_t* __restrict__ scratch) {
     const uint32_t lv = v - S.v0;
     const uint64_t row = (uint64_t)lv * S.N;
-    const uint64_t row0 = (uint64_t)(r0 - S.v0) * S.N;
     const uint32_t pv = scratch[0];
     Timer* tim = S.tim + (uint64_t)lv * S.Ct;
     for (uint32_t m = blockIdx.x * blockDim.x + threadIdx.x; m < S.N; m += gridDim.x * blockDim.x) {
@@ -2261,9 +2300,8 @@ __global__ void k_join_view(SimDev S, uint32_t v, int64_t incv, uint32_t r0, uin
         int64_t inc = incv;
         if (m != v) {
             for (uint32_t q = 0; q < nj; q++) {
-                const uint64_t rq = (uint64_t)((q == 0 ? r0 : q == 1 ? r1 : r2) - S.v0) * S.N;
-                const uint8_t s2 = S.st[rq + m] & ST_MASK;
-                const int64_t i2 = S.inc[rq + m];
+                const uint8_t s2 = J.st[q][m] & ST_MASK;
+                const int64_t i2 = J.inc[q][m];
                 if (q == 0 || i2 > inc) {
                     st = s2;
                     inc = i2;
@@ -2287,7 +2325,7 @@ __global__ void k_join_view(SimDev S, uint32_t v, int64_t incv, uint32_t r0, uin
         // members array: self, then r0's without self
         if (m == 0) S.order[row] = v;
         const uint32_t k = m;  // position k of r0's array goes to k + 1 (before v) or k (after)
-        const uint32_t a = S.order[row0 + k];
+        const uint32_t a = J.order0[k];
         if (a != v) S.order[row + (k < pv ? k + 1 : k)] = a;
     }
 }
@@ -2822,8 +2860,18 @@ struct Sim {
         leaves.clear();
     }
 
-    void join(uint32_t v) {
-        RP_REQUIRE(G == 1, "sim: join events need an unsharded simulator (the joiner reads its responders' views)");
+    // A join in progress: the joiner, its responders (host-chosen, identical on every shard)
+    // and the incarnation its responders give it.
+    struct Join {
+        uint32_t v = 0, r[3] = {0, 0, 0}, nj = 0;
+        int64_t incv = 0;
+        bool active = false;
+    } pj;
+    DevBuf<uint8_t> jx;  // join exchange buffer (JoinBuf layout)
+
+    bool local_node(uint32_t u) const { return u >= v0 && u < v0 + NL; }
+
+    void join_begin(uint32_t v) {
         std::vector<uint32_t> cand;
         for (uint32_t u = 0; u < N; u++)
             if (u != v && !h_dead[u]) cand.push_back(u);
@@ -2834,39 +2882,85 @@ struct Sim {
             const uint32_t j = q + (uint32_t)(((uint64_t)r * (cand.size() - q)) >> 32);
             std::swap(cand[q], cand[j]);
         }
-        const uint32_t r0 = cand[0], r1 = nj > 1 ? cand[1] : 0, r2 = nj > 2 ? cand[2] : 0;
-        const int64_t incv = d.now0 + 200 * round;
+        pj.v = v;
+        pj.nj = nj;
+        for (uint32_t q = 0; q < 3; q++) pj.r[q] = q < nj ? cand[q] : 0;
+        pj.incv = d.now0 + 200 * round;
+        pj.active = true;
         d.round = round;
-        join_scratch.reserve(2);
-        RP_HIP(hipMemsetAsync(join_scratch.p, 0, 8, st));
-        RP_HIP(hipMemsetAsync(n_tim.p + (v - v0), 0, 4, st));
-        hipLaunchKernelGGL(k_join_resp, dim3(nj), dim3(kT), 0, st, d, v, incv, r0, r1, r2, nj);
-        hipLaunchKernelGGL(k_join_prep, dim3(grid_for(std::max(N, d.W), 256)), dim3(256), 0, st, d, v, r0,
-                           join_scratch.p);
-        hipLaunchKernelGGL(k_join_view, dim3(grid_for(N, 256)), dim3(256), 0, st, d, v, incv, r0, r1, r2, nj,
-                           join_scratch.p);
-        hipLaunchKernelGGL(k_join_finish, dim3(1), dim3(64), 0, st, d, v, join_scratch.p);
+        uint32_t local = 0;
+        for (uint32_t q = 0; q < nj; q++) local |= (local_node(pj.r[q]) ? 1u : 0u) << q;
+        if (local)
+            hipLaunchKernelGGL(k_join_resp, dim3(nj), dim3(kT), 0, st, d, v, pj.incv, pj.r[0], pj.r[1], pj.r[2], nj,
+                               local);
         RP_HIP(hipGetLastError());
+    }
+
+    // the joiner's view from its responders' rows (on the joiner's shard), then the global flags
+    void join_finish(const JoinSrc& J) {
+        const uint32_t v = pj.v;
+        if (local_node(v)) {
+            join_scratch.reserve(2);
+            RP_HIP(hipMemsetAsync(join_scratch.p, 0, 8, st));
+            RP_HIP(hipMemsetAsync(n_tim.p + (v - v0), 0, 4, st));
+            hipLaunchKernelGGL(k_join_prep, dim3(grid_for(std::max(N, d.W), 256)), dim3(256), 0, st, d, v, J,
+                               join_scratch.p);
+            hipLaunchKernelGGL(k_join_view, dim3(grid_for(N, 256)), dim3(256), 0, st, d, v, pj.incv, pj.nj, J,
+                               join_scratch.p);
+            hipLaunchKernelGGL(k_join_finish, dim3(1), dim3(64), 0, st, d, v, join_scratch.p);
+            RP_HIP(hipGetLastError());
+        }
         h_dead[v] = 0;
         h_left[v] = 0;
         RP_HIP(hipMemcpyAsync(dead.p, h_dead.data(), N, hipMemcpyHostToDevice, st));
         RP_HIP(hipStreamSynchronize(st));
+        pj.active = false;
+        conv_dirty = true;
     }
 
-    void apply_events() {
+    // one shard holding every responder: the joiner reads their rows in place
+    void join(uint32_t v) {
+        join_begin(v);
+        JoinSrc J{};
+        for (uint32_t q = 0; q < 3; q++) {
+            const uint64_t row = (uint64_t)((q < pj.nj ? pj.r[q] : pj.r[0]) - v0) * N;
+            J.st[q] = d.st + row;
+            J.inc[q] = d.inc + row;
+        }
+        J.order0 = d.order + (uint64_t)(pj.r[0] - v0) * N;
+        join_finish(J);
+    }
+
+    // The round's events up to the next join: kills, revives and leaves are applied; a join is
+    // applied in place when this handle holds every node (stop_at_join false), else it is
+    // begun (responders answer) and left for the join exchange. Returns true at such a join.
+    bool apply_events_until_join(bool stop_at_join) {
         bool down_changed = false;
         std::vector<uint32_t> leaves;
+        bool stopped = false;
         while (next_event < events.size() && events[next_event].round <= (uint64_t)round) {
-            const rp_sim_event& e = events[next_event++];
-            if (e.round != (uint64_t)round) continue;
+            const rp_sim_event& e = events[next_event];
+            if (e.round != (uint64_t)round) {
+                next_event++;
+                continue;
+            }
             if (e.kind == RP_SIM_JOIN) {
                 flush_leaves(leaves);
                 if (down_changed) RP_HIP(hipMemcpyAsync(dead.p, h_dead.data(), N, hipMemcpyHostToDevice, st));
                 down_changed = false;
+                if (stop_at_join) {
+                    next_event++;
+                    join_begin(e.node);
+                    stopped = true;
+                    break;
+                }
+                RP_REQUIRE(G == 1, "sim: a sharded simulator takes join events through rp_sim_join_export / "
+                                   "rp_sim_join_import before stage 0 (the joiner reads its responders' views)");
+                next_event++;
                 join(e.node);
-                conv_dirty = true;
                 continue;
             }
+            next_event++;
             if (e.kind == RP_SIM_KILL || e.kind == RP_SIM_REVIVE) {
                 const uint8_t dv = e.kind == RP_SIM_KILL ? 1 : 0;
                 down_changed |= h_dead[e.node] != dv;
@@ -2880,6 +2974,34 @@ struct Sim {
         if (down_changed) RP_HIP(hipMemcpyAsync(dead.p, h_dead.data(), N, hipMemcpyHostToDevice, st));
         flush_leaves(leaves);
         if (down_changed) RP_HIP(hipStreamSynchronize(st));  // host vectors reused
+        return stopped;
+    }
+    void apply_events() { apply_events_until_join(false); }
+
+    // rp_sim_join_export: up to the next join of this round; its responders' rows on this shard
+    // go into jx (zeros elsewhere)
+    bool join_export() {
+        RP_REQUIRE(next_stage == 0, "sim_join_export: call before stage 0 of a round");
+        RP_REQUIRE(!pj.active, "sim_join_export: the previous join was not imported");
+        if (!apply_events_until_join(true)) return false;
+        const JoinBuf B(N);
+        jx.reserve(B.bytes);
+        RP_HIP(hipMemsetAsync(jx.p, 0, B.bytes, st));
+        uint32_t local = 0;
+        for (uint32_t q = 0; q < pj.nj; q++) local |= (local_node(pj.r[q]) ? 1u : 0u) << q;
+        if (local)
+            hipLaunchKernelGGL(k_join_export, dim3(grid_for(N, 256)), dim3(256), 0, st, d, pj.r[0], pj.r[1], pj.r[2],
+                               pj.nj, local, jx.p, reinterpret_cast<int64_t*>(jx.p + B.o_inc),
+                               reinterpret_cast<uint32_t*>(jx.p + B.o_ord));
+        RP_HIP(hipGetLastError());
+        RP_HIP(hipStreamSynchronize(st));
+        return true;
+    }
+    // rp_sim_join_import: jx now holds every responder's rows
+    void join_import() {
+        RP_REQUIRE(pj.active, "sim_join_import: no join exported");
+        const JoinBuf B(N);
+        join_finish(B.src(jx.p, N));
     }
 
     // {live, min checksum, max checksum, some wanted member not at its wanted status}
@@ -3262,6 +3384,51 @@ int rp_sim_exchange_local(rp_sim* const* shards, uint32_t nshards) {
                 if (b)
                     RP_HIP(hipMemcpyAsync(D.in.buf.p + D.in.seg_off(src), Sx.out.buf.p + Sx.out.seg_off(dst), b,
                                           hipMemcpyDeviceToDevice, D.st));
+            }
+        }
+        for (uint32_t i = 0; i < nshards; i++) RP_HIP(hipStreamSynchronize(shards[i]->impl.st));
+    });
+}
+
+int rp_sim_join_export(rp_sim* s, int* has, void** buf, uint64_t* bytes) {
+    return guard([&] {
+        rp::Sim& S = SM(s);
+        const bool h = S.join_export();
+        if (has) *has = h ? 1 : 0;
+        if (buf) *buf = h ? S.jx.p : nullptr;
+        if (bytes) *bytes = h ? rp::JoinBuf(S.N).bytes : 0;
+    });
+}
+
+int rp_sim_join_import(rp_sim* s) {
+    return guard([&] { SM(s).join_import(); });
+}
+
+int rp_sim_join_exchange_local(rp_sim* const* shards, uint32_t nshards) {
+    return guard([&] {
+        RP_REQUIRE(shards && nshards >= 1, "sim_join_exchange_local: bad arguments");
+        for (uint32_t i = 0; i < nshards; i++) {
+            RP_REQUIRE(shards[i] && shards[i]->impl.G == nshards && shards[i]->impl.shard == i,
+                       "sim_join_exchange_local: handles must be shards 0..G-1 of one partition");
+            RP_REQUIRE(shards[i]->impl.pj.active, "sim_join_exchange_local: every shard must have exported the join");
+            RP_HIP(hipSetDevice(shards[i]->impl.device));
+            RP_HIP(hipStreamSynchronize(shards[i]->impl.st));
+        }
+        const rp::Sim& S0 = shards[0]->impl;
+        const rp::JoinBuf B(S0.N);
+        const uint64_t N = S0.N;
+        for (uint32_t q = 0; q < S0.pj.nj; q++) {
+            uint32_t o = 0;  // the shard owning responder q wrote its rows
+            while (o < nshards && !shards[o]->impl.local_node(S0.pj.r[q])) o++;
+            RP_REQUIRE(o < nshards, "sim_join_exchange_local: a responder belongs to no shard");
+            const uint8_t* src = shards[o]->impl.jx.p;
+            for (uint32_t g = 0; g < nshards; g++) {
+                if (g == o) continue;
+                rp::Sim& D = shards[g]->impl;
+                RP_HIP(hipMemcpyAsync(D.jx.p + q * N, src + q * N, N, hipMemcpyDefault, D.st));
+                RP_HIP(hipMemcpyAsync(D.jx.p + B.o_inc + 8 * q * N, src + B.o_inc + 8 * q * N, 8 * N, hipMemcpyDefault,
+                                      D.st));
+                if (q == 0) RP_HIP(hipMemcpyAsync(D.jx.p + B.o_ord, src + B.o_ord, 4 * N, hipMemcpyDefault, D.st));
             }
         }
         for (uint32_t i = 0; i < nshards; i++) RP_HIP(hipStreamSynchronize(shards[i]->impl.st));

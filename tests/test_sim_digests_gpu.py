@@ -58,6 +58,11 @@ def test_c4_join_full_size(gpu):
     _replay(gpu, "c4j")
 
 
+def test_c4_join_sharded(gpu):
+    """The same joins over 4 shard handles: responders and joiners on different shards."""
+    _replay(gpu, "c4j", G=4)
+
+
 def test_c5_full_size_one_gpu(gpu):
     _replay(gpu, "c5")
 

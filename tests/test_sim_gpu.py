@@ -165,12 +165,33 @@ def test_sim_capacity_overflow_is_loud(gpu, monkeypatch):
     g.close()
 
 
-def test_sim_join_refused_when_sharded(gpu):
-    """A join reads its responders' views, which a sharded simulator spreads over handles: the
-    event is refused loudly there instead of being approximated."""
+@pytest.mark.parametrize("case_name", ["n30-join", "n70-join"])
+@pytest.mark.parametrize("G", [2, 3])
+def test_sharded_sim_join_matches_reference_goldens(gpu, case_name, G):
+    """Join events on the sharded path: every shard exports the rows of the responders it owns
+    (rp_sim_join_export), the buffers are combined (rp_sim_join_exchange_local) and the joiner's
+    shard builds its view (rp_sim_join_import). Same checksums and piggyback counts every round
+    as the reference goldens."""
+    case = next(c for c in gu.load("sim_golden.json")["cases"] if c["name"] == case_name)
+    _, sim = _golden_sim(gpu, case, G=G)
+    for r, want in enumerate(case["checksums"]):
+        sim.step()
+        assert sim.checksums().tolist() == want, "round %d" % r
+        assert sim.piggyback().tolist() == case["maxPiggyback"][r], "round %d" % r
+    assert sim.stats()["fullsyncs"] == case["fullSyncs"]
+    sim.close()
+
+
+def test_sharded_join_without_exchange_is_refused(gpu):
+    """Stepping shard handles directly (no join export / import) into a join event is refused
+    loudly instead of being approximated."""
     case = next(c for c in gu.load("sim_golden.json")["cases"] if c["name"] == "n30-join")
     _, sim = _golden_sim(gpu, case, G=2)
     with pytest.raises(gpu.RingpopAmdError, match="join"):
         for _ in range(25):
-            sim.step()
+            for k in range(gpu.SIM_STAGES):
+                for s in sim.shards:
+                    s.stage(k)
+                if k < gpu.SIM_STAGES - 1:
+                    gpu.check(gpu.lib().rp_sim_exchange_local(sim._arr, sim.G))
     sim.close()

@@ -63,7 +63,16 @@ def _free_port():
     return p
 
 
-def _run_dist(gpu, tmp_path, G, backend, n=400, k=6, seed=7, susp=25, rounds=45):
+def _join_events(n, k, seed):
+    """The dist worker's "join" scenario (tests/workers/dist_sim_worker.py)."""
+    _, _, dead = _case(n, k, seed)
+    live = np.flatnonzero(dead == 0)
+    crashed = np.random.default_rng(seed).permutation(live)[:12]
+    ev = [(3, "kill", int(v)) for v in sorted(crashed)]
+    return ev + [(9, "join", int(v)) for v in sorted(crashed[:6])] + [(9, "join", int(v)) for v in np.flatnonzero(dead)[:2]]
+
+
+def _run_dist(gpu, tmp_path, G, backend, n=400, k=6, seed=7, susp=25, rounds=45, scenario=None):
     out = str(tmp_path / "dist.npz")
     port = _free_port()
     worker = os.path.join(REPO, "tests", "workers", "dist_sim_worker.py")
@@ -72,12 +81,13 @@ def _run_dist(gpu, tmp_path, G, backend, n=400, k=6, seed=7, susp=25, rounds=45)
         env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(G), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, worker, str(n), str(k), str(seed), str(susp), str(rounds),
-                                       out, backend], env=env))
+                                       out, backend] + ([scenario] if scenario else []), env=env))
     rcs = [p.wait(timeout=100) for p in procs]
     assert rcs == [0] * G
     d = np.load(out)
     names, inc0, dead = _case(n, k, seed)
-    ref = gpu.GossipSim(names, inc0, dead, seed=seed, suspicion_rounds=susp)
+    ref = gpu.GossipSim(names, inc0, dead, seed=seed, suspicion_rounds=susp,
+                        events=_join_events(n, k, seed) if scenario == "join" else ())
     conv = -1
     for r in range(rounds):
         ref.step()
@@ -97,3 +107,8 @@ def test_dist_one_rank_nccl_matches_unsharded(gpu, tmp_path):
     """The RCCL transport (device tensors, rp_copy on torch's stream, all_to_all_single over
     nccl) on the one GPU of the box; a multi-GPU node runs the same code with G ranks."""
     _run_dist(gpu, tmp_path, 1, "nccl")
+
+
+def test_dist_two_ranks_gloo_joins_match_unsharded(gpu, tmp_path):
+    """Join events across ranks: the join exchange buffer is summed over torch.distributed."""
+    _run_dist(gpu, tmp_path, 2, "gloo", scenario="join")

@@ -2,7 +2,7 @@
 processes on the same box). Rank 0 writes every round's gathered checksums, the convergence
 round and the stats to OUT (npz).
 
-    RANK=r WORLD_SIZE=g MASTER_ADDR=127.0.0.1 MASTER_PORT=p python dist_sim_worker.py n k seed susp rounds out backend
+    RANK=r WORLD_SIZE=g MASTER_ADDR=127.0.0.1 MASTER_PORT=p python dist_sim_worker.py n k seed susp rounds out backend [join]
 """
 import importlib.util
 import os
@@ -37,7 +37,13 @@ def main():
     names = [S.c2_addr(i) for i in range(n)]
     inc0 = S.c3_members(n)[2]
     dead = S.kill_set(n, k, seed)
-    sim = rpa.DistGossipSim(names, inc0, dead, seed=seed, suspicion_rounds=susp, device=local)
+    events = ()
+    if len(sys.argv) > 8 and sys.argv[8] == "join":  # kills at round 3, some rejoin at 9 (+ 2 never-up nodes)
+        live = np.flatnonzero(dead == 0)
+        crashed = np.random.default_rng(seed).permutation(live)[:12]
+        events = [(3, "kill", int(v)) for v in sorted(crashed)]
+        events += [(9, "join", int(v)) for v in sorted(crashed[:6])] + [(9, "join", int(v)) for v in np.flatnonzero(dead)[:2]]
+    sim = rpa.DistGossipSim(names, inc0, dead, seed=seed, suspicion_rounds=susp, device=local, events=events)
     cks, conv = [], -1
     for r in range(rounds):
         sim.step()

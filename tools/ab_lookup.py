@@ -48,6 +48,7 @@ def main():
         variants = {k: v for k, v in variants.items() if k in a.only.split(",")}
     knobs = ("RP_LOOKUP_KPL", "RP_RING_LAYOUT", "RP_LOOKUP_ABLATE", "RP_RING_WIDE")
     times = {k: [] for k in variants}
+    digests = {}
     for r in range(a.rounds + 1):
         for name, (env, n) in variants.items():
             for kn in knobs:
@@ -63,11 +64,14 @@ def main():
             torch.cuda.synchronize()
             if r:
                 times[name].append(e0.elapsed_time(e1))
+            else:  # output digest per variant (lookupN(3) variants must agree)
+                o = out[: B * n].long()
+                digests[name] = int(torch.sum(o * (torch.arange(B * n, device="cuda") % 1009 + 1)).item())
     res = {}
     for name, t in times.items():
         med = float(np.median(t))
         res[name] = {"median_ms": med, "min_ms": float(np.min(t)), "Glookups_s": B / med / 1e6,
-                     "alg_GBs": (48 if variants[name][1] == 3 else 40) * B / med / 1e6}
+                     "alg_GBs": (48 if variants[name][1] == 3 else 40) * B / med / 1e6, "digest": digests[name]}
     print(json.dumps(res, indent=1))
 
 
