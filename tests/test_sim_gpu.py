@@ -73,6 +73,20 @@ def test_sim_d1_paths_match_reference_goldens(gpu, monkeypatch, mode):
         sim.close()
 
 
+@pytest.mark.parametrize("kernel", ["pc", "lanes"])
+def test_sim_twins_match_reference_goldens(gpu, monkeypatch, kernel):
+    """Every scenario golden with the twin-view pass forced on (RP_SIM_TWINS=1) on both chain
+    kernels: late rounds have many equal views, each takes its representative's checksum."""
+    monkeypatch.setenv("RP_SIM_TWINS", "1")
+    monkeypatch.setenv("RP_SIM_CK", kernel)
+    for case in gu.load("sim_golden.json")["cases"]:
+        names, sim = _golden_sim(gpu, case)
+        for r, want in enumerate(case["checksums"]):
+            sim.step()
+            assert sim.checksums().tolist() == want, (case["name"], r)
+        sim.close()
+
+
 @pytest.mark.parametrize("case_name", ["n40-leave", "n24-revive", "n64-half-leave"])
 def test_sharded_sim_matches_reference_goldens(gpu, case_name):
     """The same scenario goldens through the sharded path (3 shard handles, message exchanges
@@ -114,11 +128,14 @@ def test_sim_vs_oracle(gpu, orc, n, k, seed, susp):
         assert np.array_equal(gs, os_) and np.array_equal(gi, oi)
 
 
+@pytest.mark.parametrize("twins", ["0", "1"])
 @pytest.mark.parametrize("kernel", ["pc", "lanes"])
-def test_sim_checksum_kernels_vs_oracle(gpu, orc, monkeypatch, kernel):
+def test_sim_checksum_kernels_vs_oracle(gpu, orc, monkeypatch, kernel, twins):
     """Both lane-checksum kernels (k_ck_pc: chain wave + producer waves; k_ck_lanes: one wave per
-    64 nodes), forced through RP_SIM_CK, against the oracle on a case with many deviations."""
+    64 nodes), forced through RP_SIM_CK, against the oracle on a case with many deviations; with
+    and without the twin-view pass (equal views hash once, compacted view lists)."""
     monkeypatch.setenv("RP_SIM_CK", kernel)
+    monkeypatch.setenv("RP_SIM_TWINS", twins)
     S = synth()
     n, k, seed, susp = 900, 60, 5, 6
     names = [S.c2_addr(i) for i in range(n)]
