@@ -149,8 +149,8 @@ __global__ void k_fold(const uint32_t* __restrict__ sk, const uint32_t* __restri
 // (each fold resets the entries it used).
 constexpr uint32_t kGroupMax = 16;
 // Batches up to here take the grouped fold: below it the sorted fold is launch-bound (1e5
-// changes: 0.067 vs 0.096 ms per batch); above it the grouped fold's scattered per-address
-// atomics and table accesses cost more than the sort saves (4M changes: 1.54 vs 1.13 ms).
+// changes: 0.054 vs 0.096 ms per batch); above it the grouped fold's scattered per-address
+// atomics and table accesses cost more than the sort saves (4M changes: 1.03 vs 0.68 ms).
 constexpr uint32_t kGroupedMaxBatch = 1u << 19;
 constexpr uint32_t kGroupEmpty = 0xFFFFFFFFu;
 
@@ -390,6 +390,10 @@ struct Members {
     }();
     DevBuf<uint32_t> g_cnt, g_head, g_nxt;
     uint32_t g_cap = 0;
+    uint32_t grouped_max = [] {  // RP_MEMBERS_GROUPED_MAX overrides kGroupedMaxBatch (A/B)
+        const char* e = getenv("RP_MEMBERS_GROUPED_MAX");
+        return e && *e ? (uint32_t)strtoul(e, nullptr, 10) : kGroupedMaxBatch;
+    }();
     DevBuf<uint32_t> mk, mpos;  // set: merge marks and their positions
     // host-buffer staging
     DevBuf<uint32_t> io_ids, io_pick;
@@ -488,7 +492,7 @@ struct Members {
             sk.reserve(k);
             sv.reserve(k);
             const unsigned g = grid_for(k, 256);
-            if (grouped_fold && k < kGroupedMaxBatch && single_pass_sort(k)) {
+            if (grouped_fold && k < grouped_max && single_pass_sort(k)) {
                 // no sort unless some address has more than kGroupMax changes in the batch; then
                 // the sorted path runs instead (its launches are gated on the overflow word)
                 if (g_cap < cap) {
