@@ -45,6 +45,65 @@ bool single_pass_sort(uint64_t n);
 // RP_PRIMS_MULTIPASS=1 selects the earlier multi-launch scan and sort (A/B and cross-checks).
 bool prims_multipass();
 
+// ---- decoupled look-back (shared by the single-pass scan / sort and other one-launch
+// prefix computations). Units (tiles, messages) take tickets in launch order, so every unit a
+// unit waits on is already running; a unit publishes its own count (flag A) at once, sums its
+// predecessors' words back to the nearest inclusive prefix (flag P), then publishes its P. A
+// word is [epoch:30 | flag:2 | value:32]; agent-scope atomics bypass the per-XCD L2s; words of
+// an earlier launch carry another epoch and read as "not ready", so nothing is cleared.
+constexpr uint64_t kLbA = 1ull << 32, kLbP = 2ull << 32, kLbFlags = 3ull << 32;
+constexpr int kLbEpochShift = 34;
+constexpr int kLbWin = 16;  // predecessor words in flight per per-thread look-back step
+// A waiting unit gives up after this many polls (seconds): a broken ordering then shows up as a
+// wrong result instead of a hung device.
+constexpr uint32_t kLbSpinCap = 1u << 24;
+
+struct LookBack {
+    uint64_t* words;  // one per unit
+    unsigned long long* ticket;
+    unsigned long long tbase;
+    uint64_t tag;
+};
+// State for one launch over `units` (> 0) units with one word each (uses ws.lb / ws.ticket).
+// The launch must take exactly units + extra_tickets tickets from `ticket` (e.g. a persistent
+// grid whose every wave ends on one ticket past the last unit): later launches on the same
+// Scratch find their tiles from the host's count of tickets taken.
+LookBack lookback_prepare(Scratch& ws, uint64_t units, uint64_t extra_tickets, hipStream_t st);
+
+__device__ __forceinline__ uint64_t lb_load(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool lb_ready(uint64_t v, uint64_t tag) {
+    return (v >> kLbEpochShift) == (tag >> kLbEpochShift) && (v & kLbFlags) != 0;
+}
+
+// The exclusive prefix of unit `u` over one word per unit, by all 64 lanes of one wave: 64
+// predecessor words per step, back to the nearest P.
+__device__ __forceinline__ uint32_t lookback_wave(const uint64_t* lb, uint32_t u, uint64_t tag) {
+    const int lane = threadIdx.x & 63;
+    uint32_t excl = 0;
+    int64_t t = (int64_t)u - 1 - lane;
+    while (u > 0) {
+        uint64_t w = t >= 0 ? lb_load(lb + t) : (tag | kLbP);
+        for (uint32_t spin = 0; !__all(lb_ready(w, tag)) && spin < kLbSpinCap; spin++) {
+            __builtin_amdgcn_s_sleep(1);
+            if (!lb_ready(w, tag)) w = lb_load(lb + t);
+        }
+        const uint64_t pm = __ballot((w & kLbP) != 0);
+        uint32_t x = (uint32_t)w;
+        if (pm && lane > __ffsll((long long)pm) - 1) x = 0;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+        excl += x;
+        if (pm) break;
+        t -= 64;
+    }
+    return excl;
+}
+
 // out[i] = i for i < n
 void iota_u32(uint32_t* out, uint64_t n, hipStream_t st);
 

@@ -186,22 +186,6 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(const uint32_t* __re
 // prefix (flag P), then publish their own P. A look-back word is
 // [epoch:30 | flag:2 | value:32]; agent-scope atomics bypass the per-XCD L2s. Words from an
 // earlier launch carry another epoch and read as "not ready", so the array is never cleared.
-constexpr uint64_t kLbA = 1ull << 32, kLbP = 2ull << 32, kLbFlags = 3ull << 32;
-constexpr int kLbEpochShift = 34;
-constexpr int kLbWin = 16;  // predecessor words in flight per look-back step
-// A waiting tile gives up after this many polls (seconds): a broken ordering then shows up as a
-// wrong result instead of a hung device.
-constexpr uint32_t kLbSpinCap = 1u << 24;
-
-__device__ __forceinline__ uint64_t lb_load(const uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void lb_store(uint64_t* p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ bool lb_ready(uint64_t v, uint64_t tag) {
-    return (v >> kLbEpochShift) == (tag >> kLbEpochShift) && (v & kLbFlags) != 0;
-}
 __device__ __forceinline__ uint32_t take_ticket(unsigned long long* ctr, unsigned long long base) {
     __shared__ uint32_t s_t;
     if (threadIdx.x == 0) s_t = (uint32_t)(atomicAdd(ctr, 1ull) - base);
@@ -318,6 +302,7 @@ __global__ __launch_bounds__(kThreads) void k_os_scatter(const uint32_t* __restr
     for (int w = 0; w < kThreads / 64; w++) wcnt[w][tid] = 0;
     const uint32_t tile = take_ticket(ctr, tbase);  // (syncs; taken even when skipping)
     if (run_if && *run_if == 0) return;
+    if ((uint64_t)tile * kOsTile >= n) return;  // a ticket count out of step: never write out of bounds
     const uint32_t t0 = tile * (uint32_t)kOsTile;
     const uint32_t w0 = t0 + (uint32_t)(wave * kOsWave);
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -392,8 +377,9 @@ __global__ __launch_bounds__(kThreads) void k_os_scan(const uint32_t* in, uint32
                                                       unsigned long long tbase, uint64_t tag, uint32_t ntiles) {
     __shared__ uint32_t lds[kThreads + 1];
     __shared__ uint32_t s_excl;
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int tid = threadIdx.x;
     const uint32_t tile = take_ticket(ctr, tbase);
+    if (tile >= ntiles) return;  // a ticket count out of step: never write out of bounds
     const uint64_t base = (uint64_t)tile * kTile + (uint64_t)tid * kItems;
     uint32_t v[kItems];
     uint32_t s = 0;
@@ -407,23 +393,7 @@ __global__ __launch_bounds__(kThreads) void k_os_scan(const uint32_t* in, uint32
     uint32_t ex = block_exclusive_scan(s, lds, &total);
     if (tid == 0) lb_store(lb + tile, tag | (tile == 0 ? kLbP : kLbA) | total);
     if (tid < 64) {
-        uint32_t excl = 0;
-        int64_t t = (int64_t)tile - 1 - lane;
-        while (tile > 0) {
-            uint64_t w = t >= 0 ? lb_load(lb + t) : (tag | kLbP);
-            for (uint32_t spin = 0; !__all(lb_ready(w, tag)) && spin < kLbSpinCap; spin++) {
-                __builtin_amdgcn_s_sleep(1);
-                if (!lb_ready(w, tag)) w = lb_load(lb + t);
-            }
-            const uint64_t pm = __ballot((w & kLbP) != 0);
-            uint32_t x = (uint32_t)w;
-            if (pm && lane > __ffsll((long long)pm) - 1) x = 0;
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
-            excl += x;
-            if (pm) break;
-            t -= 64;
-        }
+        const uint32_t excl = lookback_wave(lb, tile, tag);
         if (tid == 0) {
             if (tile > 0) lb_store(lb + tile, tag | kLbP | (excl + total));
             s_excl = excl;
@@ -467,6 +437,8 @@ bool prims_multipass() {
 
 namespace {
 
+}  // namespace
+
 // Look-back state for one single-pass launch of `tiles` tiles with `cols` words each: returns
 // the launch's epoch tag and the ticket base, and advances the host mirrors.
 uint64_t lb_begin(Scratch& ws, uint64_t tiles, uint32_t cols, hipStream_t st, unsigned long long* tbase) {
@@ -491,6 +463,18 @@ uint64_t lb_begin(Scratch& ws, uint64_t tiles, uint32_t cols, hipStream_t st, un
     ws.tickets += tiles;
     return (uint64_t)ws.epoch << kLbEpochShift;
 }
+
+LookBack lookback_prepare(Scratch& ws, uint64_t units, uint64_t extra_tickets, hipStream_t st) {
+    LookBack L{};
+    RP_REQUIRE(units > 0, "lookback_prepare: no units");
+    L.tag = lb_begin(ws, units, 1, st, &L.tbase);
+    ws.tickets += extra_tickets;  // tickets the launch takes beyond one per unit
+    L.words = ws.lb.p;
+    L.ticket = ws.ticket.p;
+    return L;
+}
+
+namespace {
 
 void os_sort(const uint32_t* kin0, const uint32_t* vin0, bool iota, uint32_t* keys, uint32_t* vals, uint64_t n,
              int begin_bit, int end_bit, hipStream_t st, Scratch& ws, const uint32_t* run_if = nullptr) {

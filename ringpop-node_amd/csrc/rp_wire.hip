@@ -554,71 +554,79 @@ __device__ uint32_t parse_changes(Parser& P, const Names& nm, const Out& O, uint
     return n;
 }
 
+// The thread parser over message m. !FILL: returns its record count (0 when it does not
+// parse) and writes nothing; FILL: writes its records k0.. (below kend, the count it had) and
+// the message's error and header outputs.
+template <bool FILL>
+__device__ uint32_t thread_parse(const In& I, const Names& nm, const Out& O, uint32_t m, uint64_t k0, uint64_t kend) {
+    Parser P{I.buf, I.msg_off[m], I.msg_off[m + 1]};
+    uint32_t n = 0;
+    bool seen = false;
+    uint32_t ck = 0, msrc = NULL_ID, mtgt = NULL_ID;
+    int64_t msinc = LLONG_MIN;
+    uint8_t pst = 0xFF;
+    if (P.peek('[')) {
+        n = parse_changes<FILL>(P, nm, O, k0, kend);
+        seen = true;
+    } else {
+        P.expect('{');
+        if (P.peek('}')) P.i++;
+        else
+            while (!P.bad) {
+                uint64_t ks; uint32_t kl;
+                P.str(ks, kl);
+                P.expect(':');
+                if (P.bad) break;
+                const uint8_t* key = P.p + ks;
+                if (key_is(key, kl, "changes") || key_is(key, kl, "membership")) {
+                    n = parse_changes<FILL>(P, nm, O, k0, kend);
+                    seen = true;
+                } else if (key_is(key, kl, "checksum") || key_is(key, kl, "membershipChecksum")) {
+                    ck = (uint32_t)P.integer();
+                } else if (key_is(key, kl, "source") || key_is(key, kl, "coordinator")) {
+                    uint64_t so; uint32_t sl;
+                    P.str(so, sl);
+                    if (FILL && !P.bad) msrc = name_find(nm, P.p + so, sl);
+                } else if (key_is(key, kl, "sourceIncarnationNumber")) {
+                    msinc = P.integer();
+                } else if (key_is(key, kl, "target")) {
+                    uint64_t so; uint32_t sl;
+                    P.str(so, sl);
+                    if (FILL && !P.bad) mtgt = name_find(nm, P.p + so, sl);
+                } else if (key_is(key, kl, "pingStatus")) {
+                    pst = P.boolean();
+                } else {
+                    P.skip_value();
+                }
+                if (P.peek(',')) { P.i++; continue; }
+                P.expect('}');
+                break;
+            }
+    }
+    P.ws();
+    if (!P.bad && P.i != P.end) P.fail();
+    if (!P.bad && !seen) P.fail();
+    if (P.bad) n = 0;
+    if (FILL) {
+        O.err[m] = P.bad ? P.bad_at - I.msg_off[m] + 1 : 0;
+        if (O.m_checksum) O.m_checksum[m] = ck;
+        if (O.m_source) O.m_source[m] = msrc;
+        if (O.m_source_inc) O.m_source_inc[m] = msinc;
+        if (O.m_target) O.m_target[m] = mtgt;
+        if (O.m_ping_status) O.m_ping_status[m] = pst;
+    }
+    return n;
+}
+
 // slow != null: only the messages the wave kernel left (slow[m] != 0)
 template <bool FILL>
 __global__ void k_decode(In I, Names nm, Out O, uint32_t n_msgs, const uint8_t* __restrict__ slow) {
     for (uint32_t m = blockIdx.x * blockDim.x + threadIdx.x; m < n_msgs; m += gridDim.x * blockDim.x) {
         if (slow && !slow[m]) continue;
-        Parser P{I.buf, I.msg_off[m], I.msg_off[m + 1]};
         const uint64_t k0 = FILL ? O.rec_off[m] : 0;
         const uint64_t kend = FILL ? O.rec_off[m + 1] : 0;
-        uint32_t n = 0;
-        bool seen = false;
-        uint32_t ck = 0, msrc = NULL_ID, mtgt = NULL_ID;
-        int64_t msinc = LLONG_MIN;
-        uint8_t pst = 0xFF;
-        if (P.peek('[')) {
-            n = parse_changes<FILL>(P, nm, O, k0, kend);
-            seen = true;
-        } else {
-            P.expect('{');
-            if (P.peek('}')) P.i++;
-            else
-                while (!P.bad) {
-                    uint64_t ks; uint32_t kl;
-                    P.str(ks, kl);
-                    P.expect(':');
-                    if (P.bad) break;
-                    const uint8_t* key = P.p + ks;
-                    if (key_is(key, kl, "changes") || key_is(key, kl, "membership")) {
-                        n = parse_changes<FILL>(P, nm, O, k0, kend);
-                        seen = true;
-                    } else if (key_is(key, kl, "checksum") || key_is(key, kl, "membershipChecksum")) {
-                        ck = (uint32_t)P.integer();
-                    } else if (key_is(key, kl, "source") || key_is(key, kl, "coordinator")) {
-                        uint64_t so; uint32_t sl;
-                        P.str(so, sl);
-                        if (FILL && !P.bad) msrc = name_find(nm, P.p + so, sl);
-                    } else if (key_is(key, kl, "sourceIncarnationNumber")) {
-                        msinc = P.integer();
-                    } else if (key_is(key, kl, "target")) {
-                        uint64_t so; uint32_t sl;
-                        P.str(so, sl);
-                        if (FILL && !P.bad) mtgt = name_find(nm, P.p + so, sl);
-                    } else if (key_is(key, kl, "pingStatus")) {
-                        pst = P.boolean();
-                    } else {
-                        P.skip_value();
-                    }
-                    if (P.peek(',')) { P.i++; continue; }
-                    P.expect('}');
-                    break;
-                }
-        }
-        P.ws();
-        if (!P.bad && P.i != P.end) P.fail();
-        if (!P.bad && !seen) P.fail();
-        if (P.bad) n = 0;
-        if (!FILL) {
-            O.cnt[m] = n;
-        } else {
-            O.err[m] = P.bad ? P.bad_at - I.msg_off[m] + 1 : 0;
-            if (O.m_checksum) O.m_checksum[m] = ck;
-            if (O.m_source) O.m_source[m] = msrc;
-            if (O.m_source_inc) O.m_source_inc[m] = msinc;
-            if (O.m_target) O.m_target[m] = mtgt;
-            if (O.m_ping_status) O.m_ping_status[m] = pst;
-        }
+        const uint32_t n = thread_parse<FILL>(I, nm, O, m, k0, kend);
+        if (!FILL) O.cnt[m] = n;
     }
 }
 
@@ -727,15 +735,25 @@ __device__ bool wave_key(const WaveMsg& M, uint32_t t, const char (&k)[N]) {
     return key_is(M.b + M.W->pos[t] + 1, (uint32_t)(M.W->pos[t + 1] - M.W->pos[t] - 1), k);
 }
 
-// One record object, tokens [t0 = '{', t1 = its '}'], parsed by one lane. false: leave the
-// message to the thread parser.
-template <bool FILL>
-__device__ bool wave_record(const WaveMsg& M, const Names& nm, const Out& O, uint64_t base, uint32_t t0, uint32_t t1,
-                            uint64_t k, uint64_t kend) {
-    uint32_t addr = NULL_ID, src = NULL_ID, alen = 0;
-    uint64_t aoff = 0, idoff = ~0ull;
-    uint8_t st = 0xFF;
-    int64_t inc = 0, sinc = LLONG_MIN;
+// One record's fields as parsed.
+struct RecF {
+    uint32_t addr, src, alen;
+    uint64_t aoff, idoff;
+    uint8_t st;
+    int64_t inc, sinc;
+};
+
+// One record object, tokens [t0 = '{', t1 = its '}'], parsed by one lane (addresses resolved).
+// false: leave the message to the thread parser.
+__device__ bool wave_record(const WaveMsg& M, const Names& nm, uint64_t base, uint32_t t0, uint32_t t1, RecF& f) {
+    f.addr = NULL_ID;
+    f.src = NULL_ID;
+    f.alen = 0;
+    f.aoff = 0;
+    f.idoff = ~0ull;
+    f.st = 0xFF;
+    f.inc = 0;
+    f.sinc = LLONG_MIN;
     bool has_inc = false;
     uint32_t t = t0 + 1;
     if (t >= t1) return false;  // {} : no address
@@ -756,16 +774,16 @@ __device__ bool wave_record(const WaveMsg& M, const Names& nm, const Out& O, uin
             if (v + 1 >= t1 || M.tch(v) != '"' || !M.clean(M.W->pos[v - 1], M.W->pos[v])) return false;
             const uint32_t so = M.W->pos[v] + 1, sl = M.W->pos[v + 1] - so;
             if (kind == 1) {
-                aoff = base + so;
-                alen = sl;
-                if (FILL) addr = name_find(nm, M.b + so, sl);
+                f.aoff = base + so;
+                f.alen = sl;
+                f.addr = name_find(nm, M.b + so, sl);
             } else if (kind == 2) {
-                if (FILL) src = name_find(nm, M.b + so, sl);
+                f.src = name_find(nm, M.b + so, sl);
             } else if (kind == 3) {
-                st = status_code(M.b + so, sl);
-                if (st == 0xFF) return false;
+                f.st = status_code(M.b + so, sl);
+                if (f.st == 0xFF) return false;
             } else {
-                idoff = base + so;
+                f.idoff = base + so;
             }
             nx = v + 2;
         } else if (kind >= 5) {
@@ -773,10 +791,10 @@ __device__ bool wave_record(const WaveMsg& M, const Names& nm, const Out& O, uin
             int64_t x;
             if (v >= t1 + 1 || !M.scalar(kt + 2, s, e) || !M.integer(s, e, x)) return false;
             if (kind == 5) {
-                inc = x;
+                f.inc = x;
                 has_inc = true;
             } else {
-                sinc = x;
+                f.sinc = x;
             }
             nx = v;
         } else {
@@ -794,18 +812,28 @@ __device__ bool wave_record(const WaveMsg& M, const Names& nm, const Out& O, uin
         if (c != ',') return false;
         t = nx + 1;
     }
-    if (alen == 0 || st == 0xFF || !has_inc) return false;
-    if (FILL && k < kend && k < O.rec_cap) {
-        O.addr[k] = addr;
-        O.status[k] = st;
-        O.inc[k] = inc;
-        if (O.src) O.src[k] = src;
-        if (O.src_inc) O.src_inc[k] = sinc;
-        if (O.id_off) O.id_off[k] = idoff;
-        if (O.addr_off) O.addr_off[k] = aoff;
-        if (O.addr_len) O.addr_len[k] = alen;
+    return f.alen != 0 && f.st != 0xFF && has_inc;
+}
+
+// Stash slots of message m: [stash_slot(m), stash_slot(m + 1)). An accepted record is at least
+// kMinRec bytes ({"address":"x","status":"alive","incarnationNumber":0} is 55), so a message of
+// L bytes holds at most L / kMinRec records and floor(off / kMinRec) + m leaves room for them.
+constexpr uint64_t kMinRec = 48;
+__device__ __forceinline__ uint64_t stash_slot(const In& I, uint32_t m) {
+    return (I.msg_off[m] - I.msg_off[0]) / kMinRec + m;
+}
+
+__device__ __forceinline__ void rec_write(const Out& O, uint64_t k, uint64_t kend, const RecF& f) {
+    if (k < kend && k < O.rec_cap) {
+        O.addr[k] = f.addr;
+        O.status[k] = f.st;
+        O.inc[k] = f.inc;
+        if (O.src) O.src[k] = f.src;
+        if (O.src_inc) O.src_inc[k] = f.sinc;
+        if (O.id_off) O.id_off[k] = f.idoff;
+        if (O.addr_off) O.addr_off[k] = f.aoff;
+        if (O.addr_len) O.addr_len[k] = f.alen;
     }
-    return true;
 }
 
 #ifdef RP_WIRE_PROF
@@ -822,16 +850,22 @@ __device__ unsigned long long g_wprof[8];
     } while (0)
 #endif
 
-template <bool FILL>
+// One parse per message: a wave parses a message, resolves its addresses and leaves its
+// records in the message's stash slots (slots are laid out from the message byte offsets, so no
+// count is needed first) and its count; a scan of the counts gives the record offsets and
+// k_decode_place moves the records to them. A message the wave parser does not accept is
+// counted by the wave's lane 0 with the thread parser and marked slow; k_decode fills those.
 __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, Out O, uint32_t n_msgs,
-                                                                 uint64_t vb, uint64_t ve, uint8_t* __restrict__ slow) {
+                                                                 uint64_t vb, uint64_t ve, RecF* __restrict__ stash,
+                                                                 uint8_t* __restrict__ slow,
+                                                                 uint32_t* __restrict__ n_by_waves) {
     __shared__ WaveLds lds[kDecWaves];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     WaveLds& W = lds[wv];
     const uint64_t lt = (1ull << lane) - 1ull;
+    uint32_t nwave = 0;  // messages this wave parsed itself (RP_WIRE_DEBUG)
     const uint32_t nwaves = gridDim.x * kDecWaves;
     for (uint32_t m = blockIdx.x * kDecWaves + wv; m < n_msgs; m += nwaves) {
-        if (FILL && slow[m]) continue;
 #ifdef RP_WIRE_PROF
         uint64_t tprof = clock64();
 #endif
@@ -991,7 +1025,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
                         nx = v;
                     } else if (wave_key(M, t, "source") || wave_key(M, t, "coordinator") || wave_key(M, t, "target")) {
                         ok = v + 1 < last && M.tch(v) == '"' && M.clean(W.pos[v - 1], W.pos[v]);
-                        if (ok && FILL) {
+                        if (ok) {
                             const uint32_t so = W.pos[v] + 1, sl = W.pos[v + 1] - so;
                             const uint32_t id = lane == 0 ? name_find(nm, B + so, sl) : 0u;
                             const uint32_t idb = __shfl(id, 0, 64);
@@ -1067,22 +1101,26 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
             nrec = ok ? (nl + 1) / 2 : 0;
         }
         WPROF(4);
-        // the records, one lane each
-        const uint64_t k0 = FILL ? O.rec_off[m] : 0;
-        const uint64_t kend = FILL ? O.rec_off[m + 1] : 0;
+        // the records, one lane each, parsed into this message's stash slots (its byte range
+        // bounds its record count: an accepted record is at least kMinRec bytes)
+        const uint64_t s0 = stash_slot(I, m), s1 = stash_slot(I, m + 1);
+        ok = ok && nrec <= s1 - s0;
         bool rok = true;
         for (uint32_t r = lane; ok && r < nrec; r += 64) {
             const uint32_t t0 = W.lvl[2 * r];
             const uint32_t t1 = (2 * r + 1 < (nrec * 2 - 1) ? W.lvl[2 * r + 1] : arr_end) - 1;
-            rok &= wave_record<FILL>(M, nm, O, b0, t0, t1, k0 + r, kend);
+            RecF f;
+            rok &= wave_record(M, nm, b0, t0, t1, f);
+            stash[s0 + r] = f;
         }
         ok = ok && __ballot(!rok) == 0;
         WPROF(5);
+        nwave += ok ? 1u : 0u;
         if (lane == 0) {
-            if (!FILL) {
-                slow[m] = ok ? 0 : 1;
-                if (ok) O.cnt[m] = nrec;
-            } else if (ok) {
+            slow[m] = ok ? 0 : 1;
+            // the record count (the thread parser's, 0 when the message does not parse)
+            O.cnt[m] = ok ? nrec : thread_parse<false>(I, nm, O, m, 0, 0);
+            if (ok) {
                 O.err[m] = 0;
                 if (O.m_checksum) O.m_checksum[m] = ck;
                 if (O.m_source) O.m_source[m] = msrc;
@@ -1091,7 +1129,23 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
                 if (O.m_ping_status) O.m_ping_status[m] = pst;
             }
         }
+        WPROF(6);
         __builtin_amdgcn_wave_barrier();
+    }
+    if (n_by_waves && lane == 0 && nwave) atomicAdd(n_by_waves, nwave);
+}
+
+// After the scan of the counts: the wave-parsed messages' records from their stash slots to
+// their places (a wave per message, a lane per record); the thread parser fills the rest.
+__global__ void k_decode_place(In I, Out O, uint32_t n_msgs, const RecF* __restrict__ stash,
+                               const uint8_t* __restrict__ slow) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t m = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; m < n_msgs; m += nw) {
+        if (slow[m]) continue;
+        const uint64_t k0 = O.rec_off[m], kend = O.rec_off[m + 1];
+        const uint64_t s0 = stash_slot(I, m);
+        for (uint64_t r = lane; k0 + r < kend; r += 64) rec_write(O, k0 + r, kend, stash[s0 + r]);
     }
 }
 
@@ -1208,12 +1262,10 @@ int rp_wire_decode_dev(rp_members* m, const uint8_t* d_buf, const uint64_t* d_ms
         rp::In I{d_buf, d_msg_off};
         rp::Out O{d_msg_rec_off, d_msg_rec_off, rec_cap, R.addr, R.src, R.status, R.inc, R.src_inc, R.id_off,
                   R.addr_off, R.addr_len, d_err, H.checksum, H.source, H.source_inc, H.target, H.ping_status};
-        // a wave per message where it can (k_decode_wave), the thread parser for the rest
-        // (RP_WIRE_THREAD=1: the thread parser for every message)
+        // a wave per message (k_decode_wave: one launch, the thread parser inside it for the
+        // messages the wave parser leaves); RP_WIRE_THREAD=1: the thread parser for every message
         const bool wave = !getenv("RP_WIRE_THREAD");
-        rp::DevBuf<uint8_t> slow;
         if (n_msgs && wave) {
-            slow.reserve(n_msgs);
             uint64_t vb = 0, ve = 0;
             RP_HIP(hipMemcpyAsync(&vb, d_msg_off, 8, hipMemcpyDeviceToHost, st));
             RP_HIP(hipMemcpyAsync(&ve, d_msg_off + n_msgs, 8, hipMemcpyDeviceToHost, st));
@@ -1221,34 +1273,41 @@ int rp_wire_decode_dev(rp_members* m, const uint8_t* d_buf, const uint64_t* d_ms
             vb += reinterpret_cast<uint64_t>(d_buf);
             ve += reinterpret_cast<uint64_t>(d_buf);
             const unsigned g = rp::grid_for(n_msgs, rp::kDecWaves, 8192);
-            hipLaunchKernelGGL(rp::k_decode_wave<false>, dim3(g), dim3(64 * rp::kDecWaves), 0, st, I, nm, O, n_msgs,
-                               vb, ve, slow.p);
-            hipLaunchKernelGGL(rp::k_decode<false>, dim3(rp::grid_for(n_msgs, 64)), dim3(64), 0, st, I, nm, O,
-                               n_msgs, slow.p);
+            const uint64_t nslots = (ve - vb) / rp::kMinRec + n_msgs + 1;
+            rp::DevBuf<rp::RecF> stash;
+            rp::DevBuf<uint8_t> slow;
+            stash.reserve(nslots);
+            slow.reserve(n_msgs);
+            const bool dbg = getenv("RP_WIRE_DEBUG") != nullptr;
+            rp::DevBuf<uint32_t> nbw;
+            if (dbg) {
+                nbw.reserve(1);
+                RP_HIP(hipMemsetAsync(nbw.p, 0, 4, st));
+            }
+            hipLaunchKernelGGL(rp::k_decode_wave, dim3(g), dim3(64 * rp::kDecWaves), 0, st, I, nm, O, n_msgs, vb, ve,
+                               stash.p, slow.p, dbg ? nbw.p : nullptr);
             RP_HIP(hipGetLastError());
             rp::scan_exclusive_u32(d_msg_rec_off, d_msg_rec_off, n_msgs, st, *ws);
-            hipLaunchKernelGGL(rp::k_decode_wave<true>, dim3(g), dim3(64 * rp::kDecWaves), 0, st, I, nm, O, n_msgs,
-                               vb, ve, slow.p);
+            hipLaunchKernelGGL(rp::k_decode_place, dim3(rp::grid_for((uint64_t)n_msgs * 64, 256, 8192)), dim3(256), 0,
+                               st, I, O, n_msgs, stash.p, slow.p);
             hipLaunchKernelGGL(rp::k_decode<true>, dim3(rp::grid_for(n_msgs, 64)), dim3(64), 0, st, I, nm, O, n_msgs,
                                slow.p);
             RP_HIP(hipGetLastError());
-            RP_HIP(hipStreamSynchronize(st));  // slow is local
+            RP_HIP(hipStreamSynchronize(st));  // stash and slow are local
+            if (dbg) {
+                uint32_t h = 0;
+                RP_HIP(hipMemcpy(&h, nbw.p, 4, hipMemcpyDeviceToHost));
+                fprintf(stderr, "[rp] wire decode: %u of %u messages by waves\n", h, n_msgs);
+            }
 #ifdef RP_WIRE_PROF
             {
+                RP_HIP(hipStreamSynchronize(st));
                 unsigned long long h[8];
                 RP_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(rp::g_wprof), sizeof h));
                 fprintf(stderr, "[rp] wire wave cycles (sum over waves): stage %llu classify %llu depth %llu top %llu "
-                        "level %llu records %llu\n", h[0], h[1], h[2], h[3], h[4], h[5]);
+                        "level %llu records %llu publish+fill %llu\n", h[0], h[1], h[2], h[3], h[4], h[5], h[6]);
             }
 #endif
-            if (getenv("RP_WIRE_DEBUG")) {
-                std::vector<uint8_t> h(n_msgs);
-                RP_HIP(hipMemcpy(h.data(), slow.p, n_msgs, hipMemcpyDeviceToHost));
-                uint64_t ns = 0;
-                for (uint8_t x : h) ns += x;
-                fprintf(stderr, "[rp] wire decode: %llu of %u messages by waves\n",
-                        (unsigned long long)(n_msgs - ns), n_msgs);
-            }
         } else {
             if (n_msgs) {
                 hipLaunchKernelGGL(rp::k_decode<false>, dim3(rp::grid_for(n_msgs, 64)), dim3(64), 0, st, I, nm, O,
