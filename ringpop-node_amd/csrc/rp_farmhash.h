@@ -155,6 +155,26 @@ RP_HD uint32_t hash32(const S& s, uint32_t len) {
     return h;
 }
 
+// h * 5 + 0xe6546b64 as a shift-add: hipcc otherwise emits v_mad_u64_u32 (a 64-bit
+// multiply-add at a fraction of the VALU rate) for the 32-bit result. Device only.
+RP_HD uint32_t m5c(uint32_t h) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    asm volatile("v_lshl_add_u32 %0, %1, 2, %1" : "=v"(r) : "v"(h));
+    return r + 0xe6546b64u;
+#else
+    return h * 5 + 0xe6546b64u;
+#endif
+}
+
+RP_HD uint32_t mur_w(uint32_t a, uint32_t h) {
+    a *= kC1;
+    a = rotr(a, 17);
+    a *= kC2;
+    h ^= a;
+    return m5c(rotr(h, 19));
+}
+
 // Fixed-length key (LEN % 4 == 0, LEN > 24) held as LEN/4 little-endian words: every fetch
 // offset is a compile-time multiple of 4, so the whole hash runs out of registers.
 template <uint32_t LEN>
@@ -167,13 +187,13 @@ RP_HD uint32_t hash32_words(const uint32_t* w) {
     uint32_t a3 = rotr(w[(LEN - 12) / 4] * kC1, 17) * kC2;
     uint32_t a4 = rotr(w[(LEN - 20) / 4] * kC1, 17) * kC2;
     h ^= a0;
-    h = rotr(h, 19) * 5 + 0xe6546b64u;
+    h = m5c(rotr(h, 19));
     h ^= a2;
-    h = rotr(h, 19) * 5 + 0xe6546b64u;
+    h = m5c(rotr(h, 19));
     g ^= a1;
-    g = rotr(g, 19) * 5 + 0xe6546b64u;
+    g = m5c(rotr(g, 19));
     g ^= a3;
-    g = rotr(g, 19) * 5 + 0xe6546b64u;
+    g = m5c(rotr(g, 19));
     f += a4;
     f = rotr(f, 19) + 113;
     constexpr uint32_t iters = (LEN - 1) / 20;
@@ -186,9 +206,9 @@ RP_HD uint32_t hash32_words(const uint32_t* w) {
         h += a;
         g += b;
         f += c;
-        h = mur(d, h) + e;
-        g = mur(c, g) + a;
-        f = mur(b + e * kC1, f) + d;
+        h = mur_w(d, h) + e;
+        g = mur_w(c, g) + a;
+        f = mur_w(b + e * kC1, f) + d;
         f += g;
         g += f;
     }
@@ -196,11 +216,9 @@ RP_HD uint32_t hash32_words(const uint32_t* w) {
     g = rotr(g, 17) * kC1;
     f = rotr(f, 11) * kC1;
     f = rotr(f, 17) * kC1;
-    h = rotr(h + g, 19);
-    h = h * 5 + 0xe6546b64u;
+    h = m5c(rotr(h + g, 19));
     h = rotr(h, 17) * kC1;
-    h = rotr(h + f, 19);
-    h = h * 5 + 0xe6546b64u;
+    h = m5c(rotr(h + f, 19));
     h = rotr(h, 17) * kC1;
     return h;
 }

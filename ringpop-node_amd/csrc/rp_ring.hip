@@ -100,6 +100,8 @@ struct CompactView {
     uint32_t fsh;  // fingerprint = (low 32 - cb bits of the hash) >> fsh
     uint32_t exact;  // fsh == 0: fingerprints are the whole residual
     uint32_t ablate;  // diagnostics only (RP_LOOKUP_ABLATE): 1 = no second windows, 2 = aligned windows
+    uint32_t ent_bytes;  // allocated bytes of ent / idx (buffer-descriptor ranges of the lean kernel)
+    uint32_t idx_bytes;
 };
 
 // Exact view for the compact kernel's deferred keys: the bucket start comes from the compact
@@ -631,6 +633,194 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_compact(const uint8_t* _
     }
 }
 
+// The C2 hot kernel, lean form (round 2): the same layout, loads and results as
+// k_lookupn_compact, with fewer vector instructions per key (the SQ counters put that kernel at
+// ~2.9x the VALU issue of the hash-only ablation).
+//   - The index record and the window come through buffer descriptors with 32-bit offsets (no
+//     64-bit address arithmetic); the nibble sum is two v_sad_u8.
+//   - Window 1 resolves a key in one straight-line pass when its position is at most 5 - NEED
+//     entries into the window and the NEED owners there are distinct: the fingerprint tests
+//     compare whole entries against kfp << ob, the owners are picked by the position.
+//   - The ~8 % of keys that need a second window (the position lies further, a long bucket, or
+//     a repeated owner) are appended to a per-wave list (ballot + mbcnt, 64 slots in LDS); the
+//     wave then finishes them one key per lane, so the second-window code runs once per wave
+//     instead of once per key slot. Keys past the list go to the exact fix path, like ties and
+//     positions near the ring end.
+template <int KPL, int NEED>
+__global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __restrict__ keys, uint64_t ntiles,
+                                                             CompactView cv, uint32_t* __restrict__ out,
+                                                             uint8_t* __restrict__ counts,
+                                                             uint32_t* __restrict__ slow_list,
+                                                             uint32_t* __restrict__ slow_cnt) {
+    constexpr int LEN = 36, W4 = LEN / 4;
+    constexpr int TK = kLkThreads * KPL;
+    constexpr int V4 = TK * W4 / 4;
+    constexpr int PER = (V4 + kLkThreads - 1) / kLkThreads;
+    constexpr int NW = kLkThreads / 64;
+    constexpr uint32_t SPAN = 5 - NEED;  // last window-1 position that still holds NEED entries
+    static_assert((TK * W4) % 4 == 0 && (TK * NEED) % 4 == 0 && NEED >= 1 && NEED <= 4, "tile shape");
+    constexpr int SK = TK * W4, SO = TK * NEED;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[SK > SO ? SK : SO];
+    __shared__ uint32_t ag[NW][3][64];  // per-wave second-window list: start, K, kk | bc << 12 | search << 16
+    __shared__ uint32_t nslow_tile;
+    uint32_t* const sk = lds;
+    uint32_t* const so = lds;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t omask = (1u << cv.ob) - 1u, obit = 1u << cv.ob;
+    const uint32_t bsh = 32u - cv.cb;
+    const uint32_t rmask = (1u << bsh) - 1u;
+    const __amdgpu_buffer_rsrc_t ent_r =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(cv.ent), 0, (int)cv.ent_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t idx_r =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(cv.idx), 0, (int)cv.idx_bytes, 0x00020000);
+    auto load16 = [&](uint32_t pos) {
+        return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ent_r, (int)(3u * pos), 0, 0));
+    };
+    auto ent5v = [&](const u32x4 v, uint32_t (&e)[5]) {
+        e[0] = v.x & 0xFFFFFFu;
+        e[1] = (v.x >> 24) | ((v.y & 0xFFFFu) << 8);
+        e[2] = (v.y >> 16) | ((v.z & 0xFFu) << 16);
+        e[3] = v.z >> 8;
+        e[4] = v.w & 0xFFFFFFu;
+    };
+    // a listed key's second window (held by one lane): finish it, write its row into `row`
+    auto finish2 = [&](const u32x4 win, uint32_t K, uint32_t w2, uint32_t* row, uint8_t* cnt, uint32_t* nsl,
+                       uint32_t* slist) {
+        const uint32_t kk = w2 & 0xFFFu, bck = (w2 >> 12) & 15u;
+        uint32_t e2[5];
+        ent5v(win, e2);
+        uint32_t off = 0;
+        bool slow = false;
+        if ((w2 >> 16) & 1u) {  // window 2 holds bucket entries 5..9
+            bool tie = false;
+#pragma unroll
+            for (int j = 0; j < 5; j++) {
+                const bool inb = (uint32_t)j + 5u < bck;
+                off += (inb && e2[j] < K);
+                tie |= (inb && e2[j] - K < obit);
+            }
+            slow = (tie && !cv.exact) | (off == 5u && bck > 10u);
+        }
+        uint32_t res[4] = {NIL, NIL, NIL, NIL};
+        const uint32_t rc = dedupe5(e2, off, omask, NEED, res);
+        slow |= rc < (uint32_t)NEED;
+        if (slow) {
+            const uint32_t sp = atomicAdd(nsl, 1u);
+            if (sp < kSlowPerTile) slist[sp] = kk;
+        }
+#pragma unroll
+        for (int q = 0; q < NEED; q++) row[kk * NEED + q] = res[q];
+        if (cnt) cnt[kk] = (uint8_t)rc;
+    };
+    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint64_t base = t * TK;
+        {
+            const u32x4* s4 = reinterpret_cast<const u32x4*>(keys + base * LEN);
+            u32x4 pre[PER];
+#pragma unroll
+            for (int q = 0; q < PER; q++) {
+                const int k = tid + q * kLkThreads;
+                if (k < V4) pre[q] = __builtin_nontemporal_load(s4 + k);
+            }
+#pragma unroll
+            for (int q = 0; q < PER; q++) {
+                const int k = tid + q * kLkThreads;
+                if (k < V4) reinterpret_cast<u32x4*>(sk)[k] = pre[q];
+            }
+        }
+        if (tid == 0) nslow_tile = 0;
+        __syncthreads();
+        uint32_t h[KPL];
+#pragma unroll
+        for (int k = 0; k < KPL; k++) {
+            uint32_t w[W4];
+#pragma unroll
+            for (int j = 0; j < W4; j++) w[j] = sk[(tid + k * kLkThreads) * W4 + j];
+            h[k] = fh::hash32_words<LEN>(w);
+        }
+        __syncthreads();  // sk is reused as so below
+        u32x2 rec[KPL];
+#pragma unroll
+        for (int k = 0; k < KPL; k++)
+            rec[k] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(idx_r, (int)((h[k] >> (bsh + 3u)) * 8u), 0, 0));
+        uint32_t lo[KPL], bc[KPL];
+        u32x4 win[KPL];
+#pragma unroll
+        for (int k = 0; k < KPL; k++) {
+            const uint32_t s4 = ((h[k] >> bsh) & 7u) * 4u;
+            const uint32_t below = rec[k].y & ((1u << s4) - 1u);
+            lo[k] = rec[k].x + __builtin_amdgcn_sad_u8(below & 0x0F0F0F0Fu, 0u,
+                                                       __builtin_amdgcn_sad_u8((below >> 4) & 0x0F0F0F0Fu, 0u, 0u));
+            bc[k] = (rec[k].y >> s4) & 15u;
+            win[k] = load16(lo[k]);
+        }
+        uint32_t nag = 0;  // wave-uniform length of this wave's list
+#pragma unroll
+        for (int k = 0; k < KPL; k++) {
+            uint32_t e[5];
+            ent5v(win[k], e);
+            const uint32_t K = ((h[k] & rmask) >> cv.fsh) << cv.ob;
+            uint32_t lt = 0;
+            bool tie = false;
+#pragma unroll
+            for (int j = 0; j < 5; j++) {
+                const bool inb = (uint32_t)j < bc[k];
+                lt += (inb && e[j] < K);
+                tie |= (inb && e[j] - K < obit);
+            }
+            uint32_t r[NEED];
+#pragma unroll
+            for (int q = 0; q < NEED; q++) {
+                uint32_t v = e[q] & omask;
+#pragma unroll
+                for (uint32_t d = 1; d <= SPAN; d++) v = lt == d ? (e[q + d] & omask) : v;
+                r[q] = v;
+            }
+            bool dup = false;
+#pragma unroll
+            for (int a = 0; a < NEED; a++)
+#pragma unroll
+                for (int b = a + 1; b < NEED; b++) dup |= r[a] == r[b];
+            const uint32_t kk = tid + k * kLkThreads;
+            bool slow = (tie && !cv.exact) | (lo[k] + 10u > cv.M);
+            const bool again = !slow && (lt > SPAN || dup);
+            const uint64_t m = __ballot(again);
+            const uint32_t pos = nag + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            nag += (uint32_t)__popcll(m);
+            if (again) {
+                if (pos < 64) {
+                    const bool search = lt == 5u && bc[k] > 5u;
+                    ag[wv][0][pos] = search ? lo[k] + 5u : lo[k] + lt;
+                    ag[wv][1][pos] = K;
+                    ag[wv][2][pos] = kk | (bc[k] << 12) | ((uint32_t)search << 16);
+                } else {
+                    slow = true;
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < NEED; q++) so[kk * NEED + q] = r[q];
+                if (counts) counts[base + kk] = (uint8_t)NEED;
+            }
+            if (slow) {
+                const uint32_t sp = atomicAdd(&nslow_tile, 1u);
+                if (sp < kSlowPerTile) slow_list[t * kSlowPerTile + sp] = kk;
+            }
+        }
+        // second windows, one listed key per lane (the list is this wave's own LDS rows)
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if ((uint32_t)lane < (nag < 64u ? nag : 64u))
+            finish2(load16(ag[wv][0][lane]), ag[wv][1][lane], ag[wv][2][lane], so, counts ? counts + base : nullptr,
+                    &nslow_tile, slow_list + t * kSlowPerTile);
+        __syncthreads();
+        if (tid == 0) slow_cnt[t] = nslow_tile;
+        u32x4* d4 = reinterpret_cast<u32x4*>(out + base * NEED);
+        const u32x4* s4 = reinterpret_cast<const u32x4*>(so);
+#pragma unroll
+        for (int k = tid; k < TK * NEED / 4; k += kLkThreads) __builtin_nontemporal_store(s4[k], d4 + k);
+        __syncthreads();
+    }
+}
+
 // Exact completion of the keys k_lookupn_compact deferred: one thread per tile redoes the keys
 // on its list (a tile whose list overflowed is redone whole).
 template <class View>
@@ -994,7 +1184,8 @@ struct Ring {
     PackedView pview() const { return PackedView{ent.p, pbstart.p, M, pbits}; }
     CompactView cview() const {
         const char* a = getenv("RP_LOOKUP_ABLATE");
-        return CompactView{cent.p, cidx.p, M, ccb, cob, cfsh, cfsh == 0, a ? (uint32_t)atoi(a) : 0u};
+        return CompactView{cent.p, cidx.p, M, ccb, cob, cfsh, cfsh == 0, a ? (uint32_t)atoi(a) : 0u,
+                           (uint32_t)(3ull * ((uint64_t)M + kEnt3Pad + 6) + 16), (uint32_t)(8ull << (ccb - 3))};
     }
 };
 
@@ -1230,15 +1421,23 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
     if (use_compact && fixed36 && aligned16 && (uint32_t)need == W && W <= 4 && n >= (uint64_t)kLkThreads * 4) {
         RP_REQUIRE(n < (1ull << 32), "lookupn: at most 2^32-1 keys per call");
         const CompactView cv = r.cview();
-        const int kpl = getenv("RP_LOOKUP_KPL") ? atoi(getenv("RP_LOOKUP_KPL")) : 4;
-        const uint64_t TK = (uint64_t)kLkThreads * (kpl == 1 ? 1 : kpl == 2 ? 2 : kpl == 8 ? 8 : 4);
+        int kpl = getenv("RP_LOOKUP_KPL") ? atoi(getenv("RP_LOOKUP_KPL")) : 4;
+        if (kpl != 1 && kpl != 2 && !((kpl == 3 || kpl == 8) && need == 3)) kpl = 4;  // the instantiated tiles
+        const uint64_t TK = (uint64_t)kLkThreads * kpl;
         const uint64_t ntiles = n / TK, done = ntiles * TK;
         r.slow.reserve(ntiles * kSlowPerTile + 1);
         r.nslow.reserve(ntiles + 1);
         const unsigned g = grid_for(ntiles, 1, 256 * 8);
-#define RP_COMPACT(KPL, NEED)                                                                               \
-    hipLaunchKernelGGL((k_lookupn_compact<KPL, NEED>), dim3(g), dim3(kLkThreads), 0, st, keys, ntiles, cv, out,  \
-                       counts, r.slow.p, r.nslow.p)
+        const bool lean = !(getenv("RP_LOOKUP_LEAN") && !strcmp(getenv("RP_LOOKUP_LEAN"), "0"));  // A/B: 0 = round-1 kernel
+#define RP_COMPACT(KPL, NEED)                                                                                  \
+    do {                                                                                                        \
+        if (lean)                                                                                               \
+            hipLaunchKernelGGL((k_lookupn_lean<KPL, NEED>), dim3(g), dim3(kLkThreads), 0, st, keys, ntiles, cv,  \
+                               out, counts, r.slow.p, r.nslow.p);                                               \
+        else                                                                                                    \
+            hipLaunchKernelGGL((k_lookupn_compact<KPL, NEED>), dim3(g), dim3(kLkThreads), 0, st, keys, ntiles,   \
+                               cv, out, counts, r.slow.p, r.nslow.p);                                           \
+    } while (0)
 #define RP_COMPACT_N(KPL)         \
     switch (need) {               \
         case 1: RP_COMPACT(KPL, 1); break; \
@@ -1252,6 +1451,8 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
             RP_COMPACT_N(2);
         } else if (kpl == 8 && need == 3) {
             RP_COMPACT(8, 3);
+        } else if (kpl == 3 && need == 3) {
+            RP_COMPACT(3, 3);
         } else {
             RP_COMPACT_N(4);
         }

@@ -105,12 +105,16 @@ def _random_history(orc, gpu, seed, pool_size, R, nbatches):
     return ring, oracle
 
 
-# lookup layouts/kernels (rp_ring.hip): compact = the default C2 hot path (k_lookupn_compact);
-# window = the packed probe kernel; packed / wide = the generic kernels over those layouts.
+# lookup layouts/kernels (rp_ring.hip): compact = the default C2 hot path (k_lookupn_lean);
+# round1 = k_lookupn_compact over the same layout; window = the packed probe kernel; packed / wide = the generic kernels over those layouts.
 LAYOUTS = {
     "compact": {},
     "compact-kpl1": {"RP_LOOKUP_KPL": "1"},
     "compact-kpl2": {"RP_LOOKUP_KPL": "2"},
+    "compact-kpl3": {"RP_LOOKUP_KPL": "3"},
+    "compact-kpl8": {"RP_LOOKUP_KPL": "8"},
+    "round1": {"RP_LOOKUP_LEAN": "0"},
+    "round1-kpl1": {"RP_LOOKUP_LEAN": "0", "RP_LOOKUP_KPL": "1"},
     "window": {"RP_RING_LAYOUT": "packed"},
     "packed": {"RP_RING_LAYOUT": "packed", "RP_RING_NOWINDOW": "1"},
     "wide": {"RP_RING_WIDE": "1"},
@@ -118,7 +122,7 @@ LAYOUTS = {
 
 
 def set_layout(monkeypatch, layout):
-    for k in ("RP_RING_WIDE", "RP_RING_NOWINDOW", "RP_RING_LAYOUT", "RP_LOOKUP_KPL"):
+    for k in ("RP_RING_WIDE", "RP_RING_NOWINDOW", "RP_RING_LAYOUT", "RP_LOOKUP_KPL", "RP_LOOKUP_LEAN"):
         monkeypatch.delenv(k, raising=False)
     for k, v in LAYOUTS[layout].items():
         monkeypatch.setenv(k, v)
@@ -204,7 +208,9 @@ def test_device_resident_lookupn_c1_vs_oracle(gpu, orc, layout, monkeypatch):
     assert np.array_equal(d_l.cpu().numpy().view(np.uint32), w[:, 0])
 
 
-def test_c2_full_size_properties(gpu, orc):
+@pytest.mark.parametrize("layout", ["compact", "round1"])
+def test_c2_full_size_properties(gpu, orc, layout, monkeypatch):
+    set_layout(monkeypatch, layout)
     # C2: 10k servers x 100 points (~1M tokens); 2^24 keys on device; size-independent
     # properties at full size + an exact oracle check on a strided sample.
     servers = c2_servers(orc, 10000)
@@ -251,7 +257,8 @@ def test_edge_cases(gpu):
     assert len(ids) == 0 and len(cnt) == 0
 
 
-@pytest.mark.parametrize("layout", ["compact", "compact-kpl1", "window"])
+@pytest.mark.parametrize("layout", ["compact", "compact-kpl1", "compact-kpl3", "compact-kpl8", "round1",
+                                    "round1-kpl1", "window"])
 @pytest.mark.parametrize("nserv,R", [(1, 100), (2, 2000), (3, 700), (5, 5), (40, 1), (64, 3)])
 def test_window_kernel_slow_paths_vs_oracle(gpu, orc, nserv, R, layout, monkeypatch):
     """Rings that force the window kernels' exact fallbacks: long buckets, runs of one owner,

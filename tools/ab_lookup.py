@@ -2,7 +2,8 @@
 
     python tools/ab_lookup.py [--servers 10000] [--log2 26] [--rounds 7]
 
-Variants: the compact layout (default) at 1/2/4 keys per lane, the packed probe kernel
+Variants: the compact layout through the lean kernel (default) and the round-1 kernel
+(RP_LOOKUP_LEAN=0) at 1/2/3/4/8 keys per lane, the packed probe kernel
 (RP_RING_LAYOUT=packed), the wide binary-search kernel (RP_RING_WIDE=1), and the hash-only
 ablation, for lookup and lookupN(3). Prints median/min ms and lookups/s per variant.
 """
@@ -35,18 +36,24 @@ def main():
     out = torch.empty(B * 3, dtype=torch.int32, device="cuda")
     # name -> (environment, n): compact = the default layout; packed = RP_RING_LAYOUT=packed
     variants = {
-        "compact-kpl4/lookupN3": ({"RP_LOOKUP_KPL": "4"}, 3),
-        "compact-kpl2/lookupN3": ({"RP_LOOKUP_KPL": "2"}, 3),
-        "compact-kpl1/lookupN3": ({"RP_LOOKUP_KPL": "1"}, 3),
-        "compact-kpl4/lookup": ({"RP_LOOKUP_KPL": "4"}, 1),
-        "compact-kpl2/lookup": ({"RP_LOOKUP_KPL": "2"}, 1),
+        "compact-kpl4/lookupN3": ({"RP_LOOKUP_LEAN": "0", "RP_LOOKUP_KPL": "4"}, 3),
+        "compact-kpl2/lookupN3": ({"RP_LOOKUP_LEAN": "0", "RP_LOOKUP_KPL": "2"}, 3),
+        "compact-kpl1/lookupN3": ({"RP_LOOKUP_LEAN": "0", "RP_LOOKUP_KPL": "1"}, 3),
+        "lean-kpl4/lookupN3": ({"RP_LOOKUP_LEAN": "1", "RP_LOOKUP_KPL": "4"}, 3),
+        "lean-kpl2/lookupN3": ({"RP_LOOKUP_LEAN": "1", "RP_LOOKUP_KPL": "2"}, 3),
+        "lean-kpl3/lookupN3": ({"RP_LOOKUP_LEAN": "1", "RP_LOOKUP_KPL": "3"}, 3),
+        "compact-kpl3/lookupN3": ({"RP_LOOKUP_LEAN": "0", "RP_LOOKUP_KPL": "3"}, 3),
+        "lean-kpl8/lookupN3": ({"RP_LOOKUP_LEAN": "1", "RP_LOOKUP_KPL": "8"}, 3),
+        "compact-kpl4/lookup": ({"RP_LOOKUP_LEAN": "0", "RP_LOOKUP_KPL": "4"}, 1),
+        "lean-kpl4/lookup": ({"RP_LOOKUP_LEAN": "1", "RP_LOOKUP_KPL": "4"}, 1),
+        "compact-kpl2/lookup": ({"RP_LOOKUP_LEAN": "0", "RP_LOOKUP_KPL": "2"}, 1),
         "probe/lookupN3": ({"RP_RING_LAYOUT": "packed", "RP_LOOKUP_KPL": "2"}, 3),
         "probe/ablate-hash-only": ({"RP_RING_LAYOUT": "packed", "RP_LOOKUP_ABLATE": "1"}, 3),
         "wide/lookupN3": ({"RP_RING_WIDE": "1"}, 3),
     }
     if a.only:
         variants = {k: v for k, v in variants.items() if k in a.only.split(",")}
-    knobs = ("RP_LOOKUP_KPL", "RP_RING_LAYOUT", "RP_LOOKUP_ABLATE", "RP_RING_WIDE")
+    knobs = ("RP_LOOKUP_LEAN", "RP_LOOKUP_KPL", "RP_RING_LAYOUT", "RP_LOOKUP_ABLATE", "RP_RING_WIDE")
     times = {k: [] for k in variants}
     digests = {}
     for r in range(a.rounds + 1):
