@@ -95,12 +95,17 @@ struct Msg {
 static_assert(sizeof(Msg) == 40, "Msg layout is part of the exchange format");
 static_assert(sizeof(Rec) == 24, "Rec layout is part of the exchange format");
 
-struct Change {  // an entry of dissemination's changes map
+// An entry of dissemination's changes map. It also carries the member's current status and
+// incarnation: every row update goes through block_apply, which records the change in the same
+// step (on_membership_event.js:86-134 -> recordChange), so an issue reads the records it sends
+// sequentially from the list instead of at random from the view's rows.
+struct Change {
     uint32_t addr;
     uint32_t cnt;  // piggybackCount
     uint32_t src;
-    uint32_t pad;
+    uint32_t st;   // the member's status (ST_MASK bits)
     int64_t srcinc;
+    int64_t inc;   // the member's incarnation
 };
 
 struct Timer {  // a suspicion timer (suspicion.js:55-84)
@@ -1617,11 +1622,13 @@ __device__ uint32_t block_apply(const SimDev& S, uint32_t lv, const Rec* recs, u
                 Change& c = chg[slot - 1];
                 c.cnt = 0;
                 c.src = r.src;
+                c.st = us;
                 c.srcinc = r.srcinc;
+                c.inc = ui;
             } else {
                 const uint32_t idx = nc + cpos;
                 if (idx < S.Cd) {
-                    chg[idx] = Change{a, 0u, r.src, 0u, r.srcinc};
+                    chg[idx] = Change{a, 0u, r.src, us, r.srcinc, ui};
                     S.slot[row + a] = idx + 1;
                 } else {
                     set_err(S, ERR_CHANGES);
@@ -1689,14 +1696,11 @@ __device__ uint32_t block_issue(const SimDev& S, uint32_t lv, uint32_t sender, i
         if (j < nc) {
             if (keep) {
                 chg[kept + kpos] = c;
-                S.slot[row + c.addr] = kept + kpos + 1;
+                if (kept + kpos != j) S.slot[row + c.addr] = kept + kpos + 1;  // moved up
             } else {
                 S.slot[row + c.addr] = 0;
             }
-            if (emit && out) {
-                const uint8_t st = S.st[row + c.addr] & ST_MASK;
-                out[emitted + epos] = Rec{rec_w0(c.addr, st, 0), c.src, S.inc[row + c.addr], c.srcinc};
-            }
+            if (emit && out) out[emitted + epos] = Rec{rec_w0(c.addr, (uint8_t)c.st, 0), c.src, c.inc, c.srcinc};
         }
         kept += ktot;
         emitted += etot;
@@ -1987,8 +1991,15 @@ __global__ __launch_bounds__(kT) void k_phase_b(SimDev S) {
     }
 }
 
-// C: each sender with a live target applies the response (ping-sender.js:38; the second
-// application at gossip/index.js:165 is idempotent: see DESIGN.md)
+// C: each sender with a live target applies the response (ping-sender.js:38). The reference
+// applies it a second time (gossip/index.js:165); that pass changes no state, so it is not run.
+// The records have distinct addresses, evaluate_update of a record depends only on its own
+// address's row, and every rule applies only a strictly newer incarnation or a strictly higher
+// status at the same incarnation, so after the first pass a record meets a row that it does
+// not override. The one exception is a suspect/faulty record about the local member: the local
+// override (member.js:76-81) applies it again, as alive at the same Date.now(), which rewrites
+// the same row and change values and only counts one more applied update; that count is added
+// here. The oracle keeps both passes, so the parity tests check this.
 __global__ __launch_bounds__(kT) void k_phase_c(SimDev S) {
     __shared__ Lds L;
     const int64_t now = S.now0 + 200 * S.round;
@@ -1999,7 +2010,11 @@ __global__ __launch_bounds__(kT) void k_phase_c(SimDev S) {
         if (m.n == NONE) continue;  // the target's arena overflowed (reported)
         const Rec* r = msg_recs(S, m);
         block_apply(S, lv, r, m.n, L, now);
-        block_apply(S, lv, r, m.n, L, now);
+        const uint32_t v = S.v0 + lv;
+        for (uint32_t k = threadIdx.x; k < m.n; k += kT) {
+            const uint8_t us = rec_st(r[k]);
+            if (rec_addr(r[k]) == v && (us == ST_SUSPECT || us == ST_FAULTY)) atomicAdd(&S.stats[3], 1ull);
+        }
     }
 }
 
@@ -2203,13 +2218,11 @@ __global__ __launch_bounds__(kT) void k_phase_d1(SimDev S, const uint32_t* __res
             if (j < nc) {
                 if (keep) {
                     chg[kept + kpos] = c;
-                    S.slot[row + c.addr] = kept + kpos + 1;
+                    if (kept + kpos != j) S.slot[row + c.addr] = kept + kpos + 1;  // moved up
                 } else {
                     S.slot[row + c.addr] = 0;
                 }
-                if (emit)
-                    leg[written2 + p] = Rec{rec_w0(c.addr, S.st[row + c.addr] & ST_MASK, c1), c.src,
-                                            S.inc[row + c.addr], c.srcinc};
+                if (emit) leg[written2 + p] = Rec{rec_w0(c.addr, (uint8_t)c.st, c1), c.src, c.inc, c.srcinc};
             }
             written2 += etot;
             kept += ktot;
