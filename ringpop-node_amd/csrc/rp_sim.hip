@@ -1371,10 +1371,12 @@ __device__ void cursor_chunk(const SimDev& S, const LaneView& V, LaneCursor& C, 
 // producing 4 chunks per epoch.
 // sel != null: only the nodes listed in sel[0..*nsel) (the ping-req senders of D1, whose
 // views phases B and C just changed), 64 per workgroup in list order.
-template <int NP>
+// CP chunks per producer per epoch: the LDS stage is 4 KB x NP x CP, so a smaller epoch lets
+// several groups share a CU (C5 on one GPU: ~635 dirty groups for 256 CUs).
+template <int NP, int CP = 4>
 __global__ __launch_bounds__(64 * (NP + 1)) void k_ck_pc(SimDev S, const uint32_t* __restrict__ sel,
                                                          const uint32_t* __restrict__ nsel) {
-    constexpr int kEp = 4 * NP;  // chunks per epoch
+    constexpr int kEp = CP * NP;  // chunks per epoch
     __shared__ __attribute__((aligned(16))) uint32_t ring[kRingW + 24];
     __shared__ __attribute__((aligned(16))) u32x4s stage[2][kEp][2][64];
     __shared__ uint32_t s_nd[64], s_iters[64];
@@ -1438,23 +1440,23 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_ck_pc(SimDev S, const uint32_
             R.ensure(S.sbase, lead, lane);  // epochs 0 and 1
         }
     }
-    // producer p (1..3) owns chunks [e*kEp + 4(p-1), +4) of epoch e
+    // producer p (1..NP) owns chunks [e*kEp + CP(p-1), +CP) of epoch e
     auto produce = [&](uint32_t e) {
-        const uint32_t c0 = e * kEp + 4 * (wv - 1);
-        const uint32_t ng = c0 >= iters ? 0u : (iters - c0 < 4 ? iters - c0 : 4u);
+        const uint32_t c0 = e * kEp + CP * (wv - 1);
+        const uint32_t ng = c0 >= iters ? 0u : (iters - c0 < (uint32_t)CP ? iters - c0 : (uint32_t)CP);
         if (!ng) return;
         const uint32_t q = c0 * 20;
         while (q >= C.pend && C.cur.w < N) C.advance(S, V);
-        uint32_t w4[4][5];
+        uint32_t w4[CP][5];
         {
             const uint32_t o = (uint32_t)((int32_t)q - C.delta);
             const uint32_t* p = R.ring + ((o >> 2) & (kRingW - 1));
             const uint32_t sh = o & 3;
-            uint32_t x[21];
+            uint32_t x[5 * CP + 1];
 #pragma unroll
-            for (int i = 0; i < 21; i++) x[i] = p[i];
+            for (int i = 0; i < 5 * CP + 1; i++) x[i] = p[i];
 #pragma unroll
-            for (int j = 0; j < 4; j++)
+            for (int j = 0; j < CP; j++)
 #pragma unroll
                 for (int i = 0; i < 5; i++) w4[j][i] = __builtin_amdgcn_alignbyte(x[5 * j + i + 1], x[5 * j + i], sh);
         }
@@ -1464,7 +1466,7 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_ck_pc(SimDev S, const uint32_
                 uint32_t w[5];
                 cursor_chunk(S, V, C, R, q + 20 * j, w);
 #pragma unroll
-                for (int jj = 0; jj < 4; jj++)
+                for (int jj = 0; jj < CP; jj++)
                     if ((uint32_t)jj == j)
 #pragma unroll
                         for (int i = 0; i < 5; i++) w4[jj][i] = w[i];
@@ -1472,8 +1474,8 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_ck_pc(SimDev S, const uint32_
         }
         const int b = e & 1;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int slot = 4 * (wv - 1) + j;
+        for (int j = 0; j < CP; j++) {
+            const int slot = CP * (wv - 1) + j;
             stage[b][slot][0][lane] = u32x4s{w4[j][0], w4[j][1], w4[j][2], w4[j][3]};
             stage[b][slot][1][lane] = u32x4s{w4[j][4], premix(w4[j][3]), premix(w4[j][2]),
                                              premix(w4[j][1] + w4[j][4] * fh::kC1)};
@@ -1506,9 +1508,9 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_ck_pc(SimDev S, const uint32_
                 if (__ballot(c0 + kEp > iters) == 0) {
                     // every lane takes the whole epoch: loads issued a 4-chunk group ahead, no
                     // branches
-                    u32x4s x[2][4][2];
+                    u32x4s x[2][CP][2];
 #pragma unroll
-                    for (int j = 0; j < 4; j++) {
+                    for (int j = 0; j < CP; j++) {
                         x[0][j][0] = stage[b][j][0][lane];
                         x[0][j][1] = stage[b][j][1][lane];
                     }
@@ -1516,13 +1518,13 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_ck_pc(SimDev S, const uint32_
                     for (int q = 0; q < NP; q++) {
                         if (q + 1 < NP) {
 #pragma unroll
-                            for (int j = 0; j < 4; j++) {
-                                x[(q + 1) & 1][j][0] = stage[b][4 * (q + 1) + j][0][lane];
-                                x[(q + 1) & 1][j][1] = stage[b][4 * (q + 1) + j][1][lane];
+                            for (int j = 0; j < CP; j++) {
+                                x[(q + 1) & 1][j][0] = stage[b][CP * (q + 1) + j][0][lane];
+                                x[(q + 1) & 1][j][1] = stage[b][CP * (q + 1) + j][1][lane];
                             }
                         }
 #pragma unroll
-                        for (int j = 0; j < 4; j++) step(x[q & 1][j][0], x[q & 1][j][1]);
+                        for (int j = 0; j < CP; j++) step(x[q & 1][j][0], x[q & 1][j][1]);
                     }
                 } else {
 #pragma unroll
@@ -2823,7 +2825,21 @@ struct Sim {
             sel = twin_list.p;
             nsel = twin_list.p + NL;
         }
-        if (pc && !(m && !strcmp(m, "pc3")))
+        // pc32 (3 producers x 2 chunks per epoch, 41 KB of LDS) puts 3 groups on a CU. On the
+        // lane path it takes the rounds whose compacted dirty views fill at most 3 groups per CU
+        // (C5 on one GPU: median round 64 against 68 ms); the peak rounds, where nearly every
+        // view is dirty and the machine is issue-bound, stay on k_ck_lanes (pc32 there: 111
+        // against 96 ms). Choosing reads the dirty count back (one small copy per round).
+        bool use32 = m && !strcmp(m, "pc32");
+        if (!m && !pc && sel) {
+            uint32_t nd = 0;
+            RP_HIP(hipMemcpyAsync(&nd, nsel, 4, hipMemcpyDeviceToHost, st));
+            RP_HIP(hipStreamSynchronize(st));
+            use32 = (nd + 63) / 64 <= 3 * cus;
+        }
+        if (use32)
+            hipLaunchKernelGGL((k_ck_pc<3, 2>), dim3(groups), dim3(256), 0, st, d, sel, nsel);
+        else if (pc && !(m && !strcmp(m, "pc3")))
             hipLaunchKernelGGL(k_ck_pc<7>, dim3(groups), dim3(512), 0, st, d, sel, nsel);
         else if (pc)
             hipLaunchKernelGGL(k_ck_pc<3>, dim3(groups), dim3(256), 0, st, d, sel, nsel);

@@ -73,7 +73,7 @@ def test_sim_d1_paths_match_reference_goldens(gpu, monkeypatch, mode):
         sim.close()
 
 
-@pytest.mark.parametrize("kernel", ["pc", "lanes"])
+@pytest.mark.parametrize("kernel", ["pc", "lanes", "pc32"])
 def test_sim_twins_match_reference_goldens(gpu, monkeypatch, kernel):
     """Every scenario golden with the twin-view pass forced on (RP_SIM_TWINS=1) on both chain
     kernels: late rounds have many equal views, each takes its representative's checksum."""
@@ -129,7 +129,7 @@ def test_sim_vs_oracle(gpu, orc, n, k, seed, susp):
 
 
 @pytest.mark.parametrize("twins", ["0", "1"])
-@pytest.mark.parametrize("kernel", ["pc", "lanes"])
+@pytest.mark.parametrize("kernel", ["pc", "lanes", "pc3", "pc32"])
 def test_sim_checksum_kernels_vs_oracle(gpu, orc, monkeypatch, kernel, twins):
     """Both lane-checksum kernels (k_ck_pc: chain wave + producer waves; k_ck_lanes: one wave per
     64 nodes), forced through RP_SIM_CK, against the oracle on a case with many deviations; with
