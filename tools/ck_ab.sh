@@ -1,17 +1,25 @@
 #!/bin/bash
-# GPU box: C5 (one GPU) round time per lane-checksum kernel choice (RP_SIM_CK; "auto" = the
-# default choice), bench.py's C5 leg only. Usage (repo root): tools/ck_ab.sh TAG "auto lanes pc32"
+# GPU box: C4 and C5 (one GPU) round times per checksum-kernel choice, bench.py's sim legs only.
+# Variants: auto (defaults), hw0 (RP_SIM_HW=0), lanes / pc32 / pc (RP_SIM_CK, twins on).
+# Usage (repo root): tools/ck_ab.sh TAG "auto hw0"
 set -u
 TAG=${1:-ckab}
 OUT=$PWD/gpurun_out/$TAG
 mkdir -p "$OUT"
-for v in ${2:-auto lanes pc32}; do
-  if [ "$v" = auto ]; then unset RP_SIM_CK; unset RP_SIM_TWINS; else export RP_SIM_CK=$v RP_SIM_TWINS=1; fi
-  timeout -k 10 240 python3 -u bench.py --no-cpu --no-merge --no-wire --sim-n 0 \
+for v in ${2:-auto hw0}; do
+  unset RP_SIM_CK RP_SIM_TWINS RP_SIM_HW
+  case $v in
+    auto) ;;
+    hw0) export RP_SIM_HW=0 ;;
+    *) export RP_SIM_CK=$v RP_SIM_TWINS=1 ;;
+  esac
+  timeout -k 10 240 python3 -u bench.py --no-cpu --no-merge --no-wire \
       --batch-log2 20 --steps 2 --warmup 1 > "$OUT/$v.json" 2> "$OUT/$v.err" || { echo "$v rc=$?"; tail -3 "$OUT/$v.err"; exit 1; }
   python3 - "$OUT/$v.json" "$v" <<'PY'
 import json, sys
-d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])["sim_c5"]
-print(sys.argv[2], round(d["ms_per_round"], 2), d["rounds_to_convergence"], d["round_ms"])
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+for k in ("sim", "sim_c5"):
+    s = d[k]
+    print(sys.argv[2], k, round(s["ms_per_round"], 3), s["rounds_to_convergence"], {q: round(x, 1) if isinstance(x, float) else x for q, x in s["round_ms"].items()})
 PY
 done
