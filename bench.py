@@ -237,7 +237,7 @@ def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=512, warmup=3):
            "updates_per_s": k * batches / dt, "ms_per_batch": dt * 1e3 / batches,
            "gpu_ms_per_batch": e0.elapsed_time(e1) / batches, "checksum": ck,
            "note": "every batch applies most of its updates and its checksum string is built after it; the "
-                   "strings' serial farmhash chains run in groups of 64 side by side (one workgroup each) on a "
+                   "strings' serial farmhash chains run in groups of 128 side by side (one workgroup each) on a "
                    "side stream, overlapping the next batches' folds (256 slots within a 1 GiB pool, "
                    "RP_MEMBERS_CK_BYTES); the last batch's checksum is read inside the timed region, so "
                    "the final group's chains are in the time"}

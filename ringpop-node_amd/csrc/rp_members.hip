@@ -367,8 +367,11 @@ struct Members {
     // of group_slots; a full group is hashed on a side stream (ck_st) while the next batches
     // fold and build their strings into the next group, so up to ngroups - 1 groups of chains
     // overlap the folds. Reads flush and wait. The slot count is what fits
-    // RP_MEMBERS_CK_BYTES (default 1 GiB of HBM), at most kMaxSlots.
-    static constexpr uint32_t kMaxSlots = 256, kGroupSlots = 64, kMaxGroups = 4;
+    // RP_MEMBERS_CK_BYTES (default 1 GiB of HBM), at most kMaxSlots. Groups of 128: a launch of
+    // 128 chains (one workgroup each) takes about as long as one of 64, and the folds and string
+    // builds of the next 128 batches take about as long (C3: 1.00-1.07 G updates/s against 0.86
+    // with groups of 64, 0.44 with 32; RP_MEMBERS_GROUP_SLOTS overrides).
+    static constexpr uint32_t kMaxSlots = 256, kGroupSlots = 128, kMaxGroups = 4;
     uint32_t nslots = 1, group_slots = 1, ngroups = 1;
     DevBuf<uint8_t> ck_buf;   // nslots strings of slot_bytes
     uint64_t slot_bytes = 0;
@@ -576,7 +579,9 @@ struct Members {
             const char* e = getenv("RP_MEMBERS_CK_BYTES");
             const uint64_t budget = e && *e ? strtoull(e, nullptr, 10) : (1ull << 30);
             nslots = (uint32_t)std::min<uint64_t>(kMaxSlots, std::max<uint64_t>(1, budget / need));
-            group_slots = std::max<uint32_t>(1, std::min<uint32_t>(kGroupSlots, nslots / 2));
+            const char* gs = getenv("RP_MEMBERS_GROUP_SLOTS");  // A/B: chains per group launch
+            const uint32_t gmax = gs && *gs ? (uint32_t)strtoul(gs, nullptr, 10) : kGroupSlots;
+            group_slots = std::max<uint32_t>(1, std::min<uint32_t>(gmax, nslots / 2));
             ngroups = std::max<uint32_t>(1, std::min<uint32_t>(kMaxGroups, nslots / group_slots));
             ck_buf.reserve(need * (uint64_t)group_slots * ngroups);
             slot_bytes = need;
