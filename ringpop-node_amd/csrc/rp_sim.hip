@@ -158,6 +158,7 @@ struct SimDev {
     Rec* pool;  // [2][NL][Cm] fixed slots (ping, leg) + arena
     uint64_t arena0, arena_cap;
     unsigned long long* cursor;  // arena bump pointer (reset every round)
+    uint32_t* work;              // [8] per-phase node counters (dynamic node order, reset every round)
     uint32_t *ping_n, *leg_n;
     uint32_t* helpers;  // [NL*3] (global ids)
     uint32_t* nhelp;    // [NL]
@@ -1809,6 +1810,29 @@ __device__ int32_t lane0_iter_next(const SimDev& S, uint32_t lv, uint32_t* list,
 
 __global__ void k_round_begin(SimDev S) {
     if (blockIdx.x == 0 && threadIdx.x == 0) *S.cursor = 0;
+    if (blockIdx.x == 0 && threadIdx.x < 8) S.work[threadIdx.x] = 0;
+}
+
+// Phases A, B and D2 take their local nodes from a counter, kNodeChunk at a time, instead of a
+// fixed stride: a node whose answer needs a checksum chain (block_checksum) holds its
+// workgroup for milliseconds, and a fixed assignment left the workgroups that drew several of
+// them running long after the rest (C5, early rounds: phase B 41-49 -> 14-18 ms). One atomic
+// per node cost ~1 ms per phase on one counter, hence the chunks; the cheap phases keep the
+// stride. Every node's work in a phase is independent of the others', so the order does not
+// matter (only where the arena places a response, never its content).
+constexpr uint32_t kNodeChunk = 4;
+struct NodeIter {
+    uint32_t cur = 0, end = 0;
+};
+__device__ __forceinline__ uint32_t next_node(const SimDev& S, int ph, uint32_t* slot, NodeIter& it) {
+    if (it.cur == it.end) {
+        __syncthreads();  // every thread has read the previous chunk's base
+        if (threadIdx.x == 0) *slot = atomicAdd(&S.work[ph], kNodeChunk);
+        __syncthreads();
+        it.cur = *slot;
+        it.end = it.cur + kNodeChunk;
+    }
+    return it.cur++;
 }
 
 // views the batch refresh is about to hash (stats[4])
@@ -1943,7 +1967,9 @@ __global__ void k_twin_copy(SimDev S, uint32_t* __restrict__ twin_of) {
 __global__ __launch_bounds__(kT) void k_phase_a(SimDev S) {
     __shared__ Lds L;
     __shared__ int32_t tgt;
-    for (uint32_t lv = blockIdx.x; lv < S.NL; lv += gridDim.x) {
+    __shared__ uint32_t s_w;
+    NodeIter it;
+    for (uint32_t lv = next_node(S, 0, &s_w, it); lv < S.NL; lv = next_node(S, 0, &s_w, it)) {
         const uint32_t v = S.v0 + lv;
         if (S.dead[v] || S.stopped[lv]) {  // down, or its gossip loop stopped by a leave
             if (threadIdx.x == 0) S.target[lv] = -1;
@@ -1976,7 +2002,9 @@ __global__ __launch_bounds__(kT) void k_phase_a(SimDev S) {
 __global__ __launch_bounds__(kT) void k_phase_b(SimDev S) {
     __shared__ Lds L;
     const int64_t now = S.now0 + 200 * S.round;
-    for (uint32_t lj = blockIdx.x; lj < S.NL; lj += gridDim.x) {
+    __shared__ uint32_t s_w;
+    NodeIter it;
+    for (uint32_t lj = next_node(S, 1, &s_w, it); lj < S.NL; lj = next_node(S, 1, &s_w, it)) {
         const uint32_t b = S.ib_off[lj], e = S.ib_off[lj + 1];
         for (uint32_t q = b; q < e; q++) {
             const uint32_t i = S.ib_idx[q];
@@ -2247,7 +2275,9 @@ __global__ __launch_bounds__(kT) void k_phase_d1(SimDev S, const uint32_t* __res
 __global__ __launch_bounds__(kT) void k_phase_d2(SimDev S) {
     __shared__ Lds L;
     const int64_t now = S.now0 + 200 * S.round;
-    for (uint32_t lh = blockIdx.x; lh < S.NL; lh += gridDim.x) {
+    __shared__ uint32_t s_w;
+    NodeIter it;
+    for (uint32_t lh = next_node(S, 3, &s_w, it); lh < S.NL; lh = next_node(S, 3, &s_w, it)) {
         const uint32_t b = S.ib_off[lh], e = S.ib_off[lh + 1];
         for (uint32_t q = b; q < e; q++) {
             const uint32_t i = S.ib_idx[q];
@@ -3376,7 +3406,7 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
         // iterator's scratch)
         const uint64_t strcap = std::max<uint64_t>(S.nt.h_bytes.size() + 29ull * n + 64, 5ull * n + 64);
         S.strbuf.reserve((uint64_t)S.grid * ((strcap + 255) & ~255ull));
-        S.stats.reserve(8); S.cursor.reserve(1); S.err.reserve(1);
+        S.stats.reserve(8); S.cursor.reserve(1 + 4); S.err.reserve(1);
         S.base_len = boff[n];
         S.inc0.reserve(n); S.rank.reserve(n); S.boff.reserve(n + 1ull); S.sbase.reserve(base.size());
         RP_HIP(hipMemcpyAsync(S.inc0.p, inc0, 8ull * n, hipMemcpyHostToDevice, S.st));
@@ -3402,7 +3432,7 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
         d.sorted = S.nt.sorted.p; d.rank = S.rank.p; d.names = S.nt.d_bytes.p; d.noff = S.nt.d_noff.p;
         d.sbase = S.sbase.p; d.boff = S.boff.p; d.inc0 = S.inc0.p;
         d.target = S.target.p; d.ck_snap = S.ck_snap.p; d.inc_snap = S.inc_snap.p;
-        d.pool = S.pool.p; d.arena0 = 2ull * L1 * cap; d.arena_cap = arena; d.cursor = S.cursor.p;
+        d.pool = S.pool.p; d.arena0 = 2ull * L1 * cap; d.arena_cap = arena; d.cursor = S.cursor.p; d.work = reinterpret_cast<uint32_t*>(S.cursor.p + 1);
         d.ping_n = S.ping_n.p; d.leg_n = S.leg_n.p; d.helpers = S.helpers.p; d.nhelp = S.nhelp.p;
         d.leg_nk = S.leg_nk.p; d.cand = S.cand.p;
         d.strbuf = S.strbuf.p; d.strcap = (strcap + 255) & ~255ull;
