@@ -1999,7 +1999,7 @@ __global__ __launch_bounds__(kT) void k_phase_a(SimDev S) {
 }
 
 // B: each live local target applies its pings in sender order and answers each one
-__global__ __launch_bounds__(kT) void k_phase_b(SimDev S) {
+__global__ __launch_bounds__(kT, 4) void k_phase_b(SimDev S) {
     __shared__ Lds L;
     const int64_t now = S.now0 + 200 * S.round;
     __shared__ uint32_t s_w;
@@ -2272,7 +2272,7 @@ __global__ __launch_bounds__(kT) void k_phase_d1(SimDev S, const uint32_t* __res
 
 // D2: local helpers handle their ping-req legs in (sender, leg) order (ping-req.js:26-68). The
 // legs to dead helpers were never sent (the sender sees a network error).
-__global__ __launch_bounds__(kT) void k_phase_d2(SimDev S) {
+__global__ __launch_bounds__(kT, 4) void k_phase_d2(SimDev S) {
     __shared__ Lds L;
     const int64_t now = S.now0 + 200 * S.round;
     __shared__ uint32_t s_w;
