@@ -900,7 +900,12 @@ int rp_members_damp_decay_dev(rp_members* h, int64_t now_ms, void* stream) {
 }
 
 int rp_members_damp_decay(rp_members* h, int64_t now_ms) {
-    int rc = rp_members_damp_decay_dev(h, now_ms, nullptr);
+    // on the handle's own stream: it is non-blocking, so a launch on the null stream would not
+    // be ordered before the reads (damp_dump, the next fold) that run on it
+    hipStream_t st = nullptr;
+    int rc = guard([&] { st = MB(h).st; });
+    if (rc) return rc;
+    rc = rp_members_damp_decay_dev(h, now_ms, st);
     if (rc) return rc;
     return guard([&] { RP_HIP(hipStreamSynchronize(MB(h).st)); });
 }
