@@ -17,7 +17,7 @@ a = ap.parse_args()
 rpa = bench.load_pkg()
 servers = [bench.c2_addr(i) for i in range(a.servers)]
 rings = {}
-for d in ("0",):
+for d in os.environ.get("AB_CB_DELTAS", "0").split(","):
     os.environ["RP_COMPACT_CB_DELTA"] = d
     r = rpa.HashRing()
     r.addRemoveServers(servers)
@@ -32,7 +32,7 @@ ref = None
 times = {}
 for rd in range(a.rounds + 1):
     for d, r in rings.items():
-        for kpl in ("4", "2"):
+        for kpl in os.environ.get("AB_CB_KPL", "4,2").split(","):
             os.environ["RP_LOOKUP_KPL"] = kpl[0]
             os.environ["RP_LOOKUP_ABLATE"] = kpl[2:] if "a" in kpl else "0"
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

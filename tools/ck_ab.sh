@@ -1,16 +1,18 @@
 #!/bin/bash
 # GPU box: C4 and C5 (one GPU) round times per checksum-kernel choice, bench.py's sim legs only.
-# Variants: auto (defaults), hw0 (RP_SIM_HW=0), lanes / pc32 / pc (RP_SIM_CK, twins on).
+# Variants: auto (defaults), d1blk (RP_SIM_D1_BLOCKCK=1: ping-req senders' checksums by one
+# workgroup each inside D1), lanes / pc32 / pc (RP_SIM_CK, twins on).
 # Usage (repo root): tools/ck_ab.sh TAG "auto hw0"
 set -u
 TAG=${1:-ckab}
 OUT=$PWD/gpurun_out/$TAG
 mkdir -p "$OUT"
 for v in ${2:-auto hw0}; do
-  unset RP_SIM_CK RP_SIM_TWINS RP_SIM_HW
+  unset RP_SIM_CK RP_SIM_TWINS RP_SIM_HW RP_SIM_D1_BLOCKCK
   case $v in
     auto) ;;
     hw0) export RP_SIM_HW=0 ;;
+    d1blk) export RP_SIM_D1_BLOCKCK=1 ;;
     *) export RP_SIM_CK=$v RP_SIM_TWINS=1 ;;
   esac
   timeout -k 10 240 python3 -u bench.py --no-cpu --no-merge --no-wire \
