@@ -646,7 +646,9 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_compact(const uint8_t* _
 //     wave then finishes them one key per lane, so the second-window code runs once per wave
 //     instead of once per key slot. Keys past the list go to the exact fix path, like ties and
 //     positions near the ring end.
-template <int KPL, int NEED>
+// HS: the tile's keys pass through LDS in HS slices (all loads issued first, held in registers),
+// so the key stage takes 1/HS of the LDS and more workgroups fit a CU (A/B).
+template <int KPL, int NEED, int HS = 1>
 __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __restrict__ keys, uint64_t ntiles,
                                                              CompactView cv, uint32_t* __restrict__ out,
                                                              uint8_t* __restrict__ counts,
@@ -659,9 +661,12 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
     constexpr int NW = kLkThreads / 64;
     constexpr uint32_t SPAN = 5 - NEED;  // last window-1 position that still holds NEED entries
     static_assert((TK * W4) % 4 == 0 && (TK * NEED) % 4 == 0 && NEED >= 1 && NEED <= 4, "tile shape");
-    constexpr int SK = TK * W4, SO = TK * NEED;
+    static_assert(KPL % HS == 0 && V4 % HS == 0, "slices of whole keys");
+    constexpr int SK = TK * W4 / HS, SO = TK * NEED;
+    constexpr int VS = V4 / HS;  // 16-B vectors per slice
     __shared__ __attribute__((aligned(16))) uint32_t lds[SK > SO ? SK : SO];
-    __shared__ uint32_t ag[NW][3][64];  // per-wave second-window list: start, K, kk | bc << 12 | search << 16
+    constexpr uint32_t AG = 64;  // list slots per wave (8 % of 64 * KPL keys: ~41 at KPL 8)
+    __shared__ uint32_t ag[NW][3][AG];  // per-wave second-window list: start, K, kk | bc << 12 | search << 16
     __shared__ uint32_t nslow_tile;
     uint32_t* const sk = lds;
     uint32_t* const so = lds;
@@ -714,6 +719,7 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
     };
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint64_t base = t * TK;
+        uint32_t h[KPL];
         {
             const u32x4* s4 = reinterpret_cast<const u32x4*>(keys + base * LEN);
             u32x4 pre[PER];
@@ -722,21 +728,24 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
                 const int k = tid + q * kLkThreads;
                 if (k < V4) pre[q] = __builtin_nontemporal_load(s4 + k);
             }
+            if (tid == 0) nslow_tile = 0;
 #pragma unroll
-            for (int q = 0; q < PER; q++) {
-                const int k = tid + q * kLkThreads;
-                if (k < V4) reinterpret_cast<u32x4*>(sk)[k] = pre[q];
+            for (int hs = 0; hs < HS; hs++) {
+                if (hs) __syncthreads();  // the previous slice is hashed
+#pragma unroll
+                for (int q = 0; q < PER; q++) {
+                    const int k = tid + q * kLkThreads;
+                    if (k >= hs * VS && k < (hs + 1) * VS) reinterpret_cast<u32x4*>(sk)[k - hs * VS] = pre[q];
+                }
+                __syncthreads();
+#pragma unroll
+                for (int k = hs * (KPL / HS); k < (hs + 1) * (KPL / HS); k++) {
+                    uint32_t w[W4];
+#pragma unroll
+                    for (int j = 0; j < W4; j++) w[j] = sk[(tid + (k - hs * (KPL / HS)) * kLkThreads) * W4 + j];
+                    h[k] = fh::hash32_words<LEN>(w);
+                }
             }
-        }
-        if (tid == 0) nslow_tile = 0;
-        __syncthreads();
-        uint32_t h[KPL];
-#pragma unroll
-        for (int k = 0; k < KPL; k++) {
-            uint32_t w[W4];
-#pragma unroll
-            for (int j = 0; j < W4; j++) w[j] = sk[(tid + k * kLkThreads) * W4 + j];
-            h[k] = fh::hash32_words<LEN>(w);
         }
         __syncthreads();  // sk is reused as so below
         u32x2 rec[KPL];
@@ -788,7 +797,7 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
             const uint32_t pos = nag + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             nag += (uint32_t)__popcll(m);
             if (again) {
-                if (pos < 64) {
+                if (pos < AG) {
                     const bool search = lt == 5u && bc[k] > 5u;
                     ag[wv][0][pos] = search ? lo[k] + 5u : lo[k] + lt;
                     ag[wv][1][pos] = K;
@@ -808,8 +817,8 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
         }
         // second windows, one listed key per lane (the list is this wave's own LDS rows)
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if ((uint32_t)lane < (nag < 64u ? nag : 64u))
-            finish2(load16(ag[wv][0][lane]), ag[wv][1][lane], ag[wv][2][lane], so, counts ? counts + base : nullptr,
+        for (uint32_t j = lane; j < (nag < AG ? nag : AG); j += 64)
+            finish2(load16(ag[wv][0][j]), ag[wv][1][j], ag[wv][2][j], so, counts ? counts + base : nullptr,
                     &nslow_tile, slow_list + t * kSlowPerTile);
         __syncthreads();
         if (tid == 0) slow_cnt[t] = nslow_tile;
@@ -1424,17 +1433,28 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
     if (use_compact && fixed36 && aligned16 && (uint32_t)need == W && W <= 4 && n >= (uint64_t)kLkThreads * 4) {
         RP_REQUIRE(n < (1ull << 32), "lookupn: at most 2^32-1 keys per call");
         const CompactView cv = r.cview();
-        int kpl = getenv("RP_LOOKUP_KPL") ? atoi(getenv("RP_LOOKUP_KPL")) : 4;
+        // lookupN(3) (the C2 bench): 8 keys per lane, staged through LDS in two slices (0.926-0.930
+        // against 0.962-0.970 ms for 4 keys per lane, profiles/r02/ab_lookup_lean.json); the other
+        // widths 4 keys per lane. RP_LOOKUP_KPL / RP_LOOKUP_HALF override (A/B).
+        int kpl = getenv("RP_LOOKUP_KPL") ? atoi(getenv("RP_LOOKUP_KPL")) : (need == 3 ? 8 : 4);
         if (kpl != 1 && kpl != 2 && !((kpl == 3 || kpl == 8) && need == 3)) kpl = 4;  // the instantiated tiles
+        if (n < (uint64_t)kLkThreads * kpl) kpl = 4;  // at least one whole tile
         const uint64_t TK = (uint64_t)kLkThreads * kpl;
         const uint64_t ntiles = n / TK, done = ntiles * TK;
         r.slow.reserve(ntiles * kSlowPerTile + 1);
         r.nslow.reserve(ntiles + 1);
         const unsigned g = grid_for(ntiles, 1, 256 * 8);
         const bool lean = !(getenv("RP_LOOKUP_LEAN") && !strcmp(getenv("RP_LOOKUP_LEAN"), "0"));  // A/B: 0 = round-1 kernel
+        const int half = getenv("RP_LOOKUP_HALF") ? atoi(getenv("RP_LOOKUP_HALF")) : (kpl == 8 ? 2 : 0);
 #define RP_COMPACT(KPL, NEED)                                                                                  \
     do {                                                                                                        \
-        if (lean)                                                                                               \
+        if (lean && half == 4 && KPL % 4 == 0)                                                                  \
+            hipLaunchKernelGGL((k_lookupn_lean<KPL, NEED, (KPL % 4 == 0 ? 4 : 1)>), dim3(g), dim3(kLkThreads), 0, \
+                               st, keys, ntiles, cv, out, counts, r.slow.p, r.nslow.p);                          \
+        else if (lean && half == 2 && KPL % 2 == 0)                                                             \
+            hipLaunchKernelGGL((k_lookupn_lean<KPL, NEED, (KPL % 2 == 0 ? 2 : 1)>), dim3(g), dim3(kLkThreads), 0, \
+                               st, keys, ntiles, cv, out, counts, r.slow.p, r.nslow.p);                          \
+        else if (lean)                                                                                          \
             hipLaunchKernelGGL((k_lookupn_lean<KPL, NEED>), dim3(g), dim3(kLkThreads), 0, st, keys, ntiles, cv,  \
                                out, counts, r.slow.p, r.nslow.p);                                               \
         else                                                                                                    \
@@ -1456,6 +1476,7 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
             RP_COMPACT(8, 3);
         } else if (kpl == 3 && need == 3) {
             RP_COMPACT(3, 3);
+
         } else {
             RP_COMPACT_N(4);
         }

@@ -105,7 +105,8 @@ def _random_history(orc, gpu, seed, pool_size, R, nbatches):
     return ring, oracle
 
 
-# lookup layouts/kernels (rp_ring.hip): compact = the default C2 hot path (k_lookupn_lean);
+# lookup layouts/kernels (rp_ring.hip): compact = the default C2 hot path (k_lookupn_lean, 8 keys
+# per lane staged in two slices for lookupN(3));
 # round1 = k_lookupn_compact over the same layout; window = the packed probe kernel; packed / wide = the generic kernels over those layouts.
 LAYOUTS = {
     "compact": {},
@@ -113,6 +114,11 @@ LAYOUTS = {
     "compact-kpl2": {"RP_LOOKUP_KPL": "2"},
     "compact-kpl3": {"RP_LOOKUP_KPL": "3"},
     "compact-kpl8": {"RP_LOOKUP_KPL": "8"},
+    "half": {"RP_LOOKUP_HALF": "2"},
+    "half-kpl2": {"RP_LOOKUP_HALF": "2", "RP_LOOKUP_KPL": "2"},
+    "half-kpl8": {"RP_LOOKUP_HALF": "2", "RP_LOOKUP_KPL": "8"},
+    "quarter-kpl8": {"RP_LOOKUP_HALF": "4", "RP_LOOKUP_KPL": "8"},
+    "lean-kpl4": {"RP_LOOKUP_HALF": "0", "RP_LOOKUP_KPL": "4"},
     "round1": {"RP_LOOKUP_LEAN": "0"},
     "round1-kpl1": {"RP_LOOKUP_LEAN": "0", "RP_LOOKUP_KPL": "1"},
     "window": {"RP_RING_LAYOUT": "packed"},
@@ -122,7 +128,7 @@ LAYOUTS = {
 
 
 def set_layout(monkeypatch, layout):
-    for k in ("RP_RING_WIDE", "RP_RING_NOWINDOW", "RP_RING_LAYOUT", "RP_LOOKUP_KPL", "RP_LOOKUP_LEAN"):
+    for k in ("RP_RING_WIDE", "RP_RING_NOWINDOW", "RP_RING_LAYOUT", "RP_LOOKUP_KPL", "RP_LOOKUP_LEAN", "RP_LOOKUP_HALF"):
         monkeypatch.delenv(k, raising=False)
     for k, v in LAYOUTS[layout].items():
         monkeypatch.setenv(k, v)
@@ -208,7 +214,7 @@ def test_device_resident_lookupn_c1_vs_oracle(gpu, orc, layout, monkeypatch):
     assert np.array_equal(d_l.cpu().numpy().view(np.uint32), w[:, 0])
 
 
-@pytest.mark.parametrize("layout", ["compact", "round1"])
+@pytest.mark.parametrize("layout", ["compact", "round1", "lean-kpl4", "quarter-kpl8"])
 def test_c2_full_size_properties(gpu, orc, layout, monkeypatch):
     set_layout(monkeypatch, layout)
     # C2: 10k servers x 100 points (~1M tokens); 2^24 keys on device; size-independent
@@ -258,7 +264,7 @@ def test_edge_cases(gpu):
 
 
 @pytest.mark.parametrize("layout", ["compact", "compact-kpl1", "compact-kpl3", "compact-kpl8", "round1",
-                                    "round1-kpl1", "window"])
+                                    "round1-kpl1", "half", "half-kpl2", "half-kpl8", "quarter-kpl8", "lean-kpl4", "window"])
 @pytest.mark.parametrize("nserv,R", [(1, 100), (2, 2000), (3, 700), (5, 5), (40, 1), (64, 3)])
 def test_window_kernel_slow_paths_vs_oracle(gpu, orc, nserv, R, layout, monkeypatch):
     """Rings that force the window kernels' exact fallbacks: long buckets, runs of one owner,

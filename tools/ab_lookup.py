@@ -39,11 +39,17 @@ def main():
         "compact-kpl4/lookupN3": ({"RP_LOOKUP_LEAN": "0", "RP_LOOKUP_KPL": "4"}, 3),
         "compact-kpl2/lookupN3": ({"RP_LOOKUP_LEAN": "0", "RP_LOOKUP_KPL": "2"}, 3),
         "compact-kpl1/lookupN3": ({"RP_LOOKUP_LEAN": "0", "RP_LOOKUP_KPL": "1"}, 3),
-        "lean-kpl4/lookupN3": ({"RP_LOOKUP_LEAN": "1", "RP_LOOKUP_KPL": "4"}, 3),
+        "lean-kpl4/lookupN3": ({"RP_LOOKUP_HALF": "0", "RP_LOOKUP_KPL": "4"}, 3),
+        "default/lookupN3": ({}, 3),
         "lean-kpl2/lookupN3": ({"RP_LOOKUP_LEAN": "1", "RP_LOOKUP_KPL": "2"}, 3),
+        "half-kpl4/lookupN3": ({"RP_LOOKUP_HALF": "2", "RP_LOOKUP_KPL": "4"}, 3),
+        "half-kpl8/lookupN3": ({"RP_LOOKUP_HALF": "2", "RP_LOOKUP_KPL": "8"}, 3),
+        "quarter-kpl8/lookupN3": ({"RP_LOOKUP_HALF": "4", "RP_LOOKUP_KPL": "8"}, 3),
+        "quarter-kpl4/lookupN3": ({"RP_LOOKUP_HALF": "4", "RP_LOOKUP_KPL": "4"}, 3),
+        "half-kpl2/lookupN3": ({"RP_LOOKUP_HALF": "2", "RP_LOOKUP_KPL": "2"}, 3),
         "lean-kpl3/lookupN3": ({"RP_LOOKUP_LEAN": "1", "RP_LOOKUP_KPL": "3"}, 3),
         "compact-kpl3/lookupN3": ({"RP_LOOKUP_LEAN": "0", "RP_LOOKUP_KPL": "3"}, 3),
-        "lean-kpl8/lookupN3": ({"RP_LOOKUP_LEAN": "1", "RP_LOOKUP_KPL": "8"}, 3),
+        "lean-kpl8/lookupN3": ({"RP_LOOKUP_HALF": "1", "RP_LOOKUP_KPL": "8"}, 3),
         "compact-kpl4/lookup": ({"RP_LOOKUP_LEAN": "0", "RP_LOOKUP_KPL": "4"}, 1),
         "lean-kpl4/lookup": ({"RP_LOOKUP_LEAN": "1", "RP_LOOKUP_KPL": "4"}, 1),
         "compact-kpl2/lookup": ({"RP_LOOKUP_LEAN": "0", "RP_LOOKUP_KPL": "2"}, 1),
@@ -53,7 +59,7 @@ def main():
     }
     if a.only:
         variants = {k: v for k, v in variants.items() if k in a.only.split(",")}
-    knobs = ("RP_LOOKUP_LEAN", "RP_LOOKUP_KPL", "RP_RING_LAYOUT", "RP_LOOKUP_ABLATE", "RP_RING_WIDE")
+    knobs = ("RP_LOOKUP_HALF", "RP_LOOKUP_LEAN", "RP_LOOKUP_KPL", "RP_RING_LAYOUT", "RP_LOOKUP_ABLATE", "RP_RING_WIDE")
     times = {k: [] for k in variants}
     digests = {}
     for r in range(a.rounds + 1):
