@@ -582,7 +582,7 @@ def main():
                        "keys_per_step": B, "total_keys": total, "parallelism": "keys sharded, ring replicated"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_measured_on": traffic_src,
-                         "kernel": "k_lookupn_lean<8,3,2> (+ k_lookupn_fix_tiles for deferred keys)",
+                         "kernel": "k_lookupn_lean<8,3,4> (+ k_lookupn_fix_tiles for deferred keys)",
                          "kernel_ms": kern_ms,
                          "bytes_per_unit": BYTES_PER_LOOKUPN3},
             "ring_build_ms": build_ms,

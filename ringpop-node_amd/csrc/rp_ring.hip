@@ -1433,9 +1433,10 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
     if (use_compact && fixed36 && aligned16 && (uint32_t)need == W && W <= 4 && n >= (uint64_t)kLkThreads * 4) {
         RP_REQUIRE(n < (1ull << 32), "lookupn: at most 2^32-1 keys per call");
         const CompactView cv = r.cview();
-        // lookupN(3) (the C2 bench): 8 keys per lane, staged through LDS in two slices (0.926-0.930
-        // against 0.962-0.970 ms for 4 keys per lane, profiles/r02/ab_lookup_lean.json); the other
-        // widths 4 keys per lane. RP_LOOKUP_KPL / RP_LOOKUP_HALF override (A/B).
+        // lookupN(3) (the C2 bench): 8 keys per lane, staged through LDS in four slices (0.925-0.926
+        // against 0.962-0.970 ms for 4 keys per lane; two slices 0.926-0.932; 6 keys per lane
+        // 0.956-0.959; profiles/r02/ab_lookup_lean.json); the other widths 4 keys per lane.
+        // RP_LOOKUP_KPL / RP_LOOKUP_HALF (slices: 2, 4) override (A/B).
         int kpl = getenv("RP_LOOKUP_KPL") ? atoi(getenv("RP_LOOKUP_KPL")) : (need == 3 ? 8 : 4);
         if (kpl != 1 && kpl != 2 && !((kpl == 3 || kpl == 8) && need == 3)) kpl = 4;  // the instantiated tiles
         if (n < (uint64_t)kLkThreads * kpl) kpl = 4;  // at least one whole tile
@@ -1445,7 +1446,7 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
         r.nslow.reserve(ntiles + 1);
         const unsigned g = grid_for(ntiles, 1, 256 * 8);
         const bool lean = !(getenv("RP_LOOKUP_LEAN") && !strcmp(getenv("RP_LOOKUP_LEAN"), "0"));  // A/B: 0 = round-1 kernel
-        const int half = getenv("RP_LOOKUP_HALF") ? atoi(getenv("RP_LOOKUP_HALF")) : (kpl == 8 ? 2 : 0);
+        const int half = getenv("RP_LOOKUP_HALF") ? atoi(getenv("RP_LOOKUP_HALF")) : (kpl == 8 ? 4 : 0);
 #define RP_COMPACT(KPL, NEED)                                                                                  \
     do {                                                                                                        \
         if (lean && half == 4 && KPL % 4 == 0)                                                                  \
@@ -1476,6 +1477,7 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
             RP_COMPACT(8, 3);
         } else if (kpl == 3 && need == 3) {
             RP_COMPACT(3, 3);
+
 
         } else {
             RP_COMPACT_N(4);

@@ -106,7 +106,7 @@ def _random_history(orc, gpu, seed, pool_size, R, nbatches):
 
 
 # lookup layouts/kernels (rp_ring.hip): compact = the default C2 hot path (k_lookupn_lean, 8 keys
-# per lane staged in two slices for lookupN(3));
+# per lane staged in four slices for lookupN(3));
 # round1 = k_lookupn_compact over the same layout; window = the packed probe kernel; packed / wide = the generic kernels over those layouts.
 LAYOUTS = {
     "compact": {},
@@ -214,7 +214,7 @@ def test_device_resident_lookupn_c1_vs_oracle(gpu, orc, layout, monkeypatch):
     assert np.array_equal(d_l.cpu().numpy().view(np.uint32), w[:, 0])
 
 
-@pytest.mark.parametrize("layout", ["compact", "round1", "lean-kpl4", "quarter-kpl8"])
+@pytest.mark.parametrize("layout", ["compact", "round1", "lean-kpl4", "half-kpl8"])
 def test_c2_full_size_properties(gpu, orc, layout, monkeypatch):
     set_layout(monkeypatch, layout)
     # C2: 10k servers x 100 points (~1M tokens); 2^24 keys on device; size-independent

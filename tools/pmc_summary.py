@@ -20,7 +20,7 @@ def main():
     for f in glob.glob(os.path.join(d, "*", "run_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
-            if "k_lookupn_lean<8, 3, 2>" in k or "k_lookupn_leanILi8ELi3ELi2E" in k:
+            if "k_lookupn_lean<8, 3, 4>" in k or "k_lookupn_leanILi8ELi3ELi4E" in k:
                 kk = "compact"
             elif "k_lookupn_probe<36, 2, 1>" in k:
                 kk = "hashonly"
@@ -37,7 +37,7 @@ def main():
     writes = c["WRITE_SIZE"] * 1024
     fixb = (fx.get("FETCH_SIZE", 0) + fx.get("WRITE_SIZE", 0)) * 1024
     out = {
-        "kernel": "k_lookupn_lean<8,3,2> (+ k_lookupn_fix_tiles)",
+        "kernel": "k_lookupn_lean<8,3,4> (+ k_lookupn_fix_tiles)",
         "keys_per_launch": keys,
         "counters_per_launch": avg,
         "key_stream_bytes": stream,
