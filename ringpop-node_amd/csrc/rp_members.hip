@@ -319,6 +319,104 @@ __global__ void k_mck_write(const uint32_t* __restrict__ order, uint32_t n, cons
     }
 }
 
+// The checksum string in one launch (round 2): a tile of 256 x kMckItems members in address
+// order computes its pieces' lengths, finds its byte offset by decoupled look-back over the
+// tiles (rp_prims.h), and writes its pieces; the last tile records the slot's meta. This
+// replaces k_mck_len + the scan + k_mck_write + k_slot_meta (four launches per checksummed
+// batch). Gated off (*gate == 0), every workgroup still takes its ticket and tile 0 records
+// the meta.
+
+static bool getenv_on(const char* name) {
+    const char* v = getenv(name);
+    return v && *v && *v != '0';
+}
+template <int kMckItems>
+__global__ __launch_bounds__(256) void k_mck_build(const uint32_t* __restrict__ order, uint32_t n,
+                                                   const uint8_t* __restrict__ exists, const uint8_t* __restrict__ status,
+                                                   const int64_t* __restrict__ inc, const uint8_t* __restrict__ names,
+                                                   const uint64_t* __restrict__ noff, const uint32_t* __restrict__ gate,
+                                                   uint8_t* __restrict__ buf, uint32_t* __restrict__ meta, uint64_t* lb,
+                                                   unsigned long long* ctr, unsigned long long tbase, uint64_t tag,
+                                                   uint32_t ntiles) {
+    __shared__ uint32_t s_tile, s_gate, s_excl;
+    __shared__ uint32_t s_wsum[4];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid == 0) {
+        s_tile = (uint32_t)(atomicAdd(ctr, 1ull) - tbase);
+        s_gate = gate ? *gate : 1u;
+    }
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    if (tile >= ntiles) return;  // a ticket count out of step: never write out of bounds
+    if (!s_gate) {
+        if (tile == 0 && tid == 0) {
+            meta[0] = 0;
+            meta[1] = 0;
+            meta[3] = 0;
+        }
+        return;
+    }
+    const uint32_t i0 = tile * (256u * kMckItems) + (uint32_t)tid * kMckItems;
+    uint32_t ids[kMckItems], len[kMckItems];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < kMckItems; j++) {
+        const uint32_t i = i0 + j;
+        ids[j] = i < n ? order[i] : 0u;
+        len[j] = (i < n && exists[ids[j]])
+                     ? (uint32_t)(noff[ids[j] + 1] - noff[ids[j]]) + status_len(status[ids[j]]) + dec_len(inc[ids[j]]) + 1u
+                     : 0u;
+        sum += len[j];
+    }
+    // exclusive scan of the threads' sums
+    uint32_t x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_wsum[wv] = x;
+    __syncthreads();
+    uint32_t wbase = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        wbase += w < wv ? s_wsum[w] : 0u;
+        total += s_wsum[w];
+    }
+    if (tid == 0) lb_store(lb + tile, tag | (tile == 0 ? kLbP : kLbA) | total);
+    if (tid < 64) {
+        const uint32_t excl = lookback_wave(lb, tile, tag);
+        if (tid == 0) {
+            if (tile > 0) lb_store(lb + tile, tag | kLbP | (excl + total));
+            s_excl = excl;
+            if (tile == ntiles - 1) {
+                meta[0] = excl + total;
+                meta[1] = 1;
+                meta[3] = 0;
+            }
+        }
+    }
+    __syncthreads();
+    uint32_t pos = s_excl + wbase + x - sum;
+#pragma unroll
+    for (int j = 0; j < kMckItems; j++) {
+        if (len[j]) {
+            const uint32_t id = ids[j];
+            uint8_t* o = buf + pos;
+            const uint64_t b = noff[id];
+            const uint32_t L = (uint32_t)(noff[id + 1] - b);
+            for (uint32_t q = 0; q < L; q++) *o++ = names[b + q];
+            const uint8_t st = status[id];
+            const uint32_t sl = status_len(st);
+            for (uint32_t q = 0; q < sl; q++) *o++ = status_char(st, q);
+            const uint32_t dl = dec_len(inc[id]);
+            dec_write(inc[id], o, dl);
+            o[dl] = ';';
+        }
+        pos += len[j];
+    }
+}
+
 // a pending checksum slot's total (string length + 1) and gate value, captured at build time
 __global__ void k_slot_meta(const uint32_t* __restrict__ total, const uint32_t* __restrict__ gate,
                             uint32_t* __restrict__ meta) {
@@ -594,14 +692,33 @@ struct Members {
         pend_st = s;
         ck_meta.reserve(4 * kMaxSlots);
         uint8_t* buf = ck_buf.p + slot_bytes * slot_index(npending);
-        hipLaunchKernelGGL(k_mck_len, dim3(grid_for(n, 256)), dim3(256), 0, s, nt.sorted.p, n, exists.p, status.p,
-                           inc.p, nt.d_noff.p, gate, ck_len.p);
-        RP_HIP(hipGetLastError());
-        scan_exclusive_u32(ck_len.p, ck_pos.p, n, s, ws);
-        hipLaunchKernelGGL(k_mck_write, dim3(grid_for(n, 256)), dim3(256), 0, s, nt.sorted.p, n, exists.p, status.p,
-                           inc.p, nt.d_bytes.p, nt.d_noff.p, ck_pos.p, gate, buf);
-        hipLaunchKernelGGL(k_slot_meta, dim3(1), dim3(1), 0, s, ck_pos.p + n, gate,
-                           ck_meta.p + 4ull * slot_index(npending));
+        if (getenv_on("RP_MEMBERS_CK3")) {  // A/B: the three-launch build (lengths, scan, write)
+            hipLaunchKernelGGL(k_mck_len, dim3(grid_for(n, 256)), dim3(256), 0, s, nt.sorted.p, n, exists.p,
+                               status.p, inc.p, nt.d_noff.p, gate, ck_len.p);
+            RP_HIP(hipGetLastError());
+            scan_exclusive_u32(ck_len.p, ck_pos.p, n, s, ws);
+            hipLaunchKernelGGL(k_mck_write, dim3(grid_for(n, 256)), dim3(256), 0, s, nt.sorted.p, n, exists.p,
+                               status.p, inc.p, nt.d_bytes.p, nt.d_noff.p, ck_pos.p, gate, buf);
+            hipLaunchKernelGGL(k_slot_meta, dim3(1), dim3(1), 0, s, ck_pos.p + n, gate,
+                               ck_meta.p + 4ull * slot_index(npending));
+        } else {
+            const char* it = getenv("RP_MEMBERS_CK_ITEMS");  // A/B: members per thread
+            const int items = it && *it ? atoi(it) : 1;
+            const uint32_t per = 256u * (items == 2 ? 2u : items == 4 ? 4u : 1u);
+            const uint32_t ntl = (uint32_t)((n + per - 1) / per);
+            const LookBack L = lookback_prepare(ws, ntl, 0, s);
+#define RP_MCK(I)                                                                                               \
+    hipLaunchKernelGGL((k_mck_build<I>), dim3(ntl), dim3(256), 0, s, nt.sorted.p, n, exists.p, status.p, inc.p, \
+                       nt.d_bytes.p, nt.d_noff.p, gate, buf, ck_meta.p + 4ull * slot_index(npending), L.words,   \
+                       L.ticket, L.tbase, L.tag, ntl)
+            if (items == 2)
+                RP_MCK(2);
+            else if (items == 4)
+                RP_MCK(4);
+            else
+                RP_MCK(1);
+#undef RP_MCK
+        }
         RP_HIP(hipGetLastError());
         npending++;
     }
@@ -832,7 +949,8 @@ int rp_members_checksum_string(rp_members* h, char* buf, uint64_t cap, uint64_t*
         if (n) {
             m.checksum_dev(m.st, nullptr);
             str = m.ck_buf.p + m.slot_bytes * m.slot_index(m.npending - 1);
-            RP_HIP(hipMemcpyAsync(&total, m.ck_pos.p + n, 4, hipMemcpyDeviceToHost, m.st));
+            RP_HIP(hipMemcpyAsync(&total, m.ck_meta.p + 4ull * m.slot_index(m.npending - 1), 4,
+                                  hipMemcpyDeviceToHost, m.st));
             RP_HIP(hipStreamSynchronize(m.st));
         }
         const uint64_t L = total ? total - 1 : 0;
