@@ -128,13 +128,21 @@ __device__ __forceinline__ void wave_atomic_add(uint32_t* p, uint32_t v) {
 
 // Sorted path: one lane per id segment of the (id, arrival)-sorted batch. run_if (may be null):
 // skip unless *run_if != 0.
+// g_cnt / g_head (non-null after a grouped attempt that overflowed): every id of the batch gets
+// its grouped-path entries reset here as well (they are only read by the grouped path), which
+// saves the batch a launch.
 __global__ void k_fold(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv, uint32_t k, FoldArgs A,
-                       const uint32_t* __restrict__ run_if) {
+                       const uint32_t* __restrict__ run_if, uint32_t* __restrict__ g_cnt = nullptr,
+                       uint32_t* __restrict__ g_head = nullptr) {
     if (run_if && *run_if == 0) return;
     const uint32_t gstride = gridDim.x * blockDim.x;
     uint32_t napp = 0;
     for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < k; p += gstride) {
         const uint32_t id = sk[p];
+        if (g_cnt) {
+            g_cnt[id] = 0;
+            g_head[id] = 0xFFFFFFFFu;
+        }
         if (p > 0 && sk[p - 1] == id) continue;  // not a segment head
         uint32_t c = 1;
         while (p + c < k && sk[p + c] == id) c++;
@@ -200,17 +208,6 @@ __global__ void k_fold_grouped(const uint32_t* __restrict__ ids, uint32_t k, uin
         head[id] = kGroupEmpty;
     }
     wave_atomic_add(A.n_applied, napp);
-}
-
-// After an overflowing batch took the sorted path: reset the entries its changes linked.
-__global__ void k_group_reset(const uint32_t* __restrict__ ids, uint32_t k, uint32_t* __restrict__ cnt,
-                              uint32_t* __restrict__ head, const uint32_t* __restrict__ overflow) {
-    if (*overflow == 0) return;
-    const uint32_t gstride = gridDim.x * blockDim.x;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < k; i += gstride) {
-        cnt[ids[i]] = 0;
-        head[ids[i]] = kGroupEmpty;
-    }
 }
 
 // Membership._decayMembersDampScore (index.js:374-383): decayDampScore on every member
@@ -612,8 +609,7 @@ struct Members {
                                    A);
                 RP_HIP(hipGetLastError());
                 radix_sort_index(ids, sk.p, sv.p, k, 0, bits, s, ws, ovf);
-                hipLaunchKernelGGL(k_fold, dim3(g), dim3(256), 0, s, sk.p, sv.p, k, A, ovf);
-                hipLaunchKernelGGL(k_group_reset, dim3(g), dim3(256), 0, s, ids, k, g_cnt.p, g_head.p, ovf);
+                hipLaunchKernelGGL(k_fold, dim3(g), dim3(256), 0, s, sk.p, sv.p, k, A, ovf, g_cnt.p, g_head.p);
             } else {
                 radix_sort_index(ids, sk.p, sv.p, k, 0, bits, s, ws);
                 hipLaunchKernelGGL(k_fold, dim3(g), dim3(256), 0, s, sk.p, sv.p, k, A, nullptr);
