@@ -2865,7 +2865,11 @@ struct Sim {
             uint32_t nd = 0;
             RP_HIP(hipMemcpyAsync(&nd, nsel, 4, hipMemcpyDeviceToHost, st));
             RP_HIP(hipStreamSynchronize(st));
-            use32 = (nd + 63) / 64 <= 3 * cus;
+            static const uint32_t per_cu = [] {  // A/B: RP_SIM_PC32_PER_CU
+                const char* e = getenv("RP_SIM_PC32_PER_CU");
+                return e && *e ? (uint32_t)atoi(e) : 3u;
+            }();
+            use32 = (nd + 63) / 64 <= per_cu * cus;
         }
         if (use32)
             hipLaunchKernelGGL((k_ck_pc<3, 2>), dim3(groups), dim3(256), 0, st, d, sel, nsel);

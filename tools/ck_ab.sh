@@ -8,11 +8,14 @@ TAG=${1:-ckab}
 OUT=$PWD/gpurun_out/$TAG
 mkdir -p "$OUT"
 for v in ${2:-auto hw0}; do
-  unset RP_SIM_CK RP_SIM_TWINS RP_SIM_HW RP_SIM_D1_BLOCKCK
+  unset RP_SIM_CK RP_SIM_TWINS RP_SIM_HW RP_SIM_D1_BLOCKCK RP_SIM_PC32_PER_CU
   case $v in
     auto) ;;
     hw0) export RP_SIM_HW=0 ;;
     d1blk) export RP_SIM_D1_BLOCKCK=1 ;;
+    cu2) export RP_SIM_PC32_PER_CU=2 ;;
+    cu4) export RP_SIM_PC32_PER_CU=4 ;;
+    cu6) export RP_SIM_PC32_PER_CU=6 ;;
     *) export RP_SIM_CK=$v RP_SIM_TWINS=1 ;;
   esac
   timeout -k 10 240 python3 -u bench.py --no-cpu --no-merge --no-wire \
