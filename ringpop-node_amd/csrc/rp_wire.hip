@@ -363,12 +363,18 @@ __device__ uint32_t name_find(const Names& nm, const uint8_t* s, uint32_t len) {
     }
 }
 
+// s[0..N-1) == k, every byte compared (no early exit), so the loads issue together
+template <int N>
+__device__ __forceinline__ bool key_eq(const uint8_t* s, const char (&k)[N]) {
+    uint32_t d = 0;
+#pragma unroll
+    for (int i = 0; i < N - 1; i++) d |= (uint32_t)(s[i] ^ (uint8_t)k[i]);
+    return d == 0;
+}
+
 template <int N>
 __device__ bool key_is(const uint8_t* s, uint32_t len, const char (&k)[N]) {
-    if (len != N - 1) return false;
-    for (int i = 0; i < N - 1; i++)
-        if (s[i] != (uint8_t)k[i]) return false;
-    return true;
+    return len == N - 1 && key_eq(s, k);
 }
 
 struct Parser {
@@ -469,10 +475,9 @@ struct Parser {
 };
 
 __device__ uint8_t status_code(const uint8_t* s, uint32_t len) {
-    if (key_is(s, len, "alive")) return ST_ALIVE;
-    if (key_is(s, len, "suspect")) return ST_SUSPECT;
-    if (key_is(s, len, "faulty")) return ST_FAULTY;
-    if (key_is(s, len, "leave")) return ST_LEAVE;
+    if (len == 5) return key_eq(s, "alive") ? ST_ALIVE : key_eq(s, "leave") ? ST_LEAVE : 0xFF;
+    if (len == 7) return key_eq(s, "suspect") ? ST_SUSPECT : 0xFF;
+    if (len == 6) return key_eq(s, "faulty") ? ST_FAULTY : 0xFF;
     return 0xFF;
 }
 
@@ -649,12 +654,23 @@ constexpr int kDecWaves = 4;
 struct WaveLds {
     uint32_t buf[kWBuf / 4 + 2];
     uint16_t pos[kWTok];   // token byte offset in the message
-    int16_t dep[kWTok];    // depth before the token ({ [ open, } ] close)
-    uint16_t lvl[kWLvl];   // the changes array's level tokens
-    uint64_t scal[kWBuf / 64 + 1];  // bytes outside strings that are neither tokens nor whitespace
+    int8_t dep[kWTok];     // depth before the token ({ [ open, } ] close)
+    uint8_t tc[kWTok];     // the token's character
+    alignas(16) uint16_t lvl[kWLvl];  // the changes array's level tokens (the classifier's scratch before)
+    uint64_t scal[kWBuf / 64 + 4];  // buffer bytes outside strings that are neither tokens nor
+                                    // whitespace (bit sh + i: message byte i)
     uint16_t op1[32], cl2[32];      // openers at depth 1 / closers at depth 2, in order: the k-th pair
 };
 
+// SWAR over the four bytes of a dword: bit 7 of byte j set where byte j == c
+__device__ __forceinline__ uint32_t swar_eq(uint32_t x, uint8_t c) {
+    const uint32_t t = x ^ (0x01010101u * c);
+    return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+}
+// bit 7 of bytes 0..3 → bits 0..3
+__device__ __forceinline__ uint32_t swar_bits(uint32_t m) {
+    return ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u);
+}
 __device__ __forceinline__ bool wave_isws(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
 __device__ __forceinline__ bool wave_isopen(uint8_t c) { return c == '{' || c == '['; }
 __device__ __forceinline__ bool wave_isclose(uint8_t c) { return c == '}' || c == ']'; }
@@ -663,14 +679,16 @@ struct WaveMsg {
     const WaveLds* W;
     const uint8_t* b;  // message byte 0 in LDS
     uint32_t len, ntok;
+    uint32_t sh;       // byte 0's offset in the staged dwords
     __device__ uint8_t at(uint32_t i) const { return b[i]; }
-    __device__ uint8_t tch(uint32_t t) const { return b[W->pos[t]]; }
+    __device__ uint8_t tch(uint32_t t) const { return W->tc[t]; }
     // no scalar byte strictly between byte offsets lo and hi
     __device__ bool clean(uint32_t lo, uint32_t hi) const {
         for (uint32_t i = lo + 1; i < hi;) {
-            const uint64_t w = W->scal[i >> 6] >> (i & 63);
+            const uint32_t ib = i + sh;
+            const uint64_t w = W->scal[ib >> 6] >> (ib & 63);
             if (w == 0) {
-                i = (i | 63) + 1;
+                i += 64u - (ib & 63u);
                 continue;
             }
             return (uint32_t)__builtin_ctzll(w) + i >= hi;
@@ -707,9 +725,36 @@ struct WaveMsg {
         v = neg ? -(int64_t)x : (int64_t)x;
         return true;
     }
+    // The integer strictly between tokens t and t + 1 (Parser::integer after the scalar's
+    // whitespace trim). JSON.stringify's form (no whitespace at either end) is read with all
+    // its bytes loaded at once; anything else takes scalar() + integer().
+    __device__ bool int_tok(uint32_t t, int64_t& v) const {
+        const uint32_t lo = W->pos[t] + 1, hi = t + 1 < ntok ? W->pos[t + 1] : len;
+        if (hi <= lo || hi - lo > 19 || wave_isws(at(lo)) || wave_isws(at(hi - 1))) {
+            uint32_t s, e;
+            return scalar(t, s, e) && integer(s, e, v);
+        }
+        uint8_t c[19];  // up to 19 bytes past the buffer's end stay inside this wave's WaveLds
+#pragma unroll
+        for (int i = 0; i < 19; i++) c[i] = at(lo + i);
+        const uint32_t n = hi - lo;
+        const bool neg = c[0] == '-';
+        if (n - (neg ? 1u : 0u) == 0 || n - (neg ? 1u : 0u) > 18) return false;
+        uint64_t x = 0;
+        bool ok = true;
+#pragma unroll
+        for (uint32_t i = 0; i < 19; i++) {
+            const uint32_t d = (uint32_t)c[i] - '0';
+            const bool in = i < n && !(i == 0 && neg);
+            ok &= !in || d <= 9;
+            x = in ? x * 10 + d : x;
+        }
+        v = neg ? -(int64_t)x : (int64_t)x;
+        return ok;
+    }
     // the token closing the nested value opened at token t (same depth after it)
     __device__ uint32_t match(uint32_t t) const {
-        const int16_t d = W->dep[t];
+        const int32_t d = W->dep[t];
         for (uint32_t u = t + 1; u < ntok; u++)
             if (W->dep[u] == d + 1 && wave_isclose(tch(u))) return u;
         return ntok;
@@ -766,9 +811,12 @@ __device__ bool wave_record(const WaveMsg& M, const Names& nm, uint64_t base, ui
         const uint8_t* kp = M.b + M.W->pos[kt] + 1;
         const uint32_t kl = (uint32_t)(M.W->pos[kt + 1] - M.W->pos[kt] - 1);
         // 1 address, 2 source, 3 status, 4 id, 5 incarnationNumber, 6 sourceIncarnationNumber
-        const int kind = key_is(kp, kl, "address") ? 1 : key_is(kp, kl, "source") ? 2 : key_is(kp, kl, "status") ? 3
-                       : key_is(kp, kl, "id") ? 4 : key_is(kp, kl, "incarnationNumber") ? 5
-                       : key_is(kp, kl, "sourceIncarnationNumber") ? 6 : 0;
+        // (dispatched on the length: one compare)
+        const int kind = kl == 7 ? (key_eq(kp, "address") ? 1 : 0)
+                       : kl == 6 ? (key_eq(kp, "source") ? 2 : key_eq(kp, "status") ? 3 : 0)
+                       : kl == 2 ? (key_eq(kp, "id") ? 4 : 0)
+                       : kl == 17 ? (key_eq(kp, "incarnationNumber") ? 5 : 0)
+                       : kl == 23 ? (key_eq(kp, "sourceIncarnationNumber") ? 6 : 0) : 0;
         uint32_t nx;
         if (kind >= 1 && kind <= 4) {
             if (v + 1 >= t1 || M.tch(v) != '"' || !M.clean(M.W->pos[v - 1], M.W->pos[v])) return false;
@@ -787,9 +835,8 @@ __device__ bool wave_record(const WaveMsg& M, const Names& nm, uint64_t base, ui
             }
             nx = v + 2;
         } else if (kind >= 5) {
-            uint32_t s, e;
             int64_t x;
-            if (v >= t1 + 1 || !M.scalar(kt + 2, s, e) || !M.integer(s, e, x)) return false;
+            if (v >= t1 + 1 || !M.int_tok(kt + 2, x)) return false;
             if (kind == 5) {
                 f.inc = x;
                 has_inc = true;
@@ -904,38 +951,74 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         WPROF(0);
         const uint8_t* B = reinterpret_cast<const uint8_t*>(W.buf) + sh;
-        // classify 64 bytes at a time
+        // classify 256 bytes per step, a staged dword per lane, in buffer coordinates (buffer
+        // byte sh + i is message byte i): a quote's string parity from the lane's own quotes and
+        // a ballot of the lanes with an odd count; the tokens (quotes and structural characters
+        // outside strings) compacted by a prefix of the lanes' token counts (three ballots); the
+        // scalar bitmap packed from the lanes' nibbles through LDS
         uint32_t ntok = 0, quotes = 0;
         bool bad = false;
-        for (uint32_t c4 = 0; ok && c4 < len; c4 += 256) {
-          uint8_t chs[4];  // four chunks' bytes read together: one LDS latency per 256 bytes
-#pragma unroll
-          for (int u = 0; u < 4; u++) chs[u] = c4 + 64u * u + lane < len ? B[c4 + 64u * u + lane] : (uint8_t)' ';
-#pragma unroll
-          for (int u = 0; u < 4; u++) {
-            const uint32_t c0 = c4 + 64u * u;
-            if (c0 >= len) break;
-            const uint32_t i = c0 + lane;
-            const bool in = i < len;
-            const uint8_t ch = chs[u];
-            const bool q = ch == '"';
-            const uint64_t Q = __ballot(q);
-            const bool instr = ((quotes + __popcll(Q & (lt | (1ull << lane)))) & 1u) != 0;  // opening quote + body
-            const bool str_body = instr && !q;
-            const bool structural = !instr && !q &&
-                                    (ch == '{' || ch == '}' || ch == '[' || ch == ']' || ch == ':' || ch == ',');
-            const bool tok = in && (q || structural);
-            const bool ws = wave_isws(ch);
-            const bool ctrl = in && ((ch < 0x20 && !(ws && !str_body)) || ch == '\\');
-            const uint64_t T = __ballot(tok);
-            const uint64_t S = __ballot(in && !instr && !tok && !ws);
+        const uint32_t nbd = (sh + len + 3) / 4;
+        uint8_t* nib = reinterpret_cast<uint8_t*>(W.lvl);
+        for (uint32_t d0 = 0; ok && d0 < nbd; d0 += 64) {
+            const uint32_t dw = d0 + lane;
+            uint32_t x = dw < nbd ? W.buf[dw] : 0x20202020u;
+            // the message's bytes of this dword (a neighbour's bytes at either end read as blanks)
+            const int lo = min(max((int)sh - (int)(4 * dw), 0), 4);
+            const int hi = min(max((int)(sh + len) - (int)(4 * dw), 0), 4);
+            const uint32_t m_in = (uint32_t)((0x80808080ull << (8 * lo)) & (0x80808080ull >> (8 * (4 - hi))));
+            const uint32_t bm = (m_in >> 7) * 0xFFu;
+            x = (x & bm) | (0x20202020u & ~bm);
+            // bytes as bit 7 of each byte lane (SWAR)
+            const uint32_t Q = swar_eq(x, '"');
+            uint32_t p = Q ^ (Q << 8);
+            p ^= p << 16;  // bit 7 of byte j: odd number of the lane's quotes up to byte j
+            const uint64_t Po = __ballot((p >> 31) & 1u);
+            const uint32_t pre = (quotes + (uint32_t)__popcll(Po & lt)) & 1u;
+            const uint32_t instr = p ^ (pre ? 0x80808080u : 0u);  // opening quote + body
+            const uint32_t xd = x & 0xDFDFDFDFu;                  // { [ → 0x5B, } ] → 0x5D
+            const uint32_t structural = (swar_eq(xd, 0x5B) | swar_eq(xd, 0x5D) | swar_eq(x, ':') | swar_eq(x, ',')) &
+                                        ~instr & ~Q;
+            const uint32_t tokb = Q | structural;
+            const uint32_t ws = swar_eq(x, ' ') | swar_eq(x, '\t') | swar_eq(x, '\n') | swar_eq(x, '\r');
+            const uint32_t lt20 = ~(((x & 0x7F7F7F7Fu) + 0x60606060u) | x) & 0x80808080u;
+            const uint32_t str_body = instr & ~Q;
+            const uint32_t ctrlb = (lt20 & ~(ws & ~str_body)) | swar_eq(x, '\\');
+            const uint32_t sb = ~instr & ~tokb & ~ws & 0x80808080u;
+            const uint32_t tm = swar_bits(tokb), sm = swar_bits(sb);
+            const bool ctrl = ctrlb != 0;
             bad |= __ballot(ctrl) != 0;
-            const uint32_t idx = ntok + (uint32_t)__popcll(T & lt);
-            if (tok && idx < kWTok) W.pos[idx] = (uint16_t)i;
-            if (lane == 0) W.scal[c0 >> 6] = S;
-            ntok += (uint32_t)__popcll(T);
-            quotes += (uint32_t)__popcll(Q);
-          }
+            const uint32_t k = (uint32_t)__builtin_popcount(tm);
+            const uint64_t K0 = __ballot(k & 1u), K1 = __ballot(k & 2u), K2 = __ballot(k & 4u);
+            uint32_t idx = ntok + (uint32_t)__popcll(K0 & lt) + 2u * (uint32_t)__popcll(K1 & lt) +
+                           4u * (uint32_t)__popcll(K2 & lt);
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if ((tm >> j) & 1u) {
+                    if (idx < kWTok) {
+                        W.pos[idx] = (uint16_t)(4 * dw + j - sh);
+                        W.tc[idx] = (uint8_t)(x >> (8 * j));
+                    }
+                    idx++;
+                }
+            nib[lane] = (uint8_t)sm;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if (lane < 4) {  // 16 lanes' nibbles → the bitmap word of 64 buffer bytes
+                const uint4 v = *reinterpret_cast<const uint4*>(nib + 16 * lane);
+                uint64_t a = (uint64_t)v.x | ((uint64_t)v.y << 32), c = (uint64_t)v.z | ((uint64_t)v.w << 32);
+                a = (a | (a >> 4)) & 0x00FF00FF00FF00FFull;
+                a = (a | (a >> 8)) & 0x0000FFFF0000FFFFull;
+                a = (a | (a >> 16)) & 0xFFFFFFFFull;
+                c = (c | (c >> 4)) & 0x00FF00FF00FF00FFull;
+                c = (c | (c >> 8)) & 0x0000FFFF0000FFFFull;
+                c = (c | (c >> 16)) & 0xFFFFFFFFull;
+                W.scal[d0 / 16 + lane] = a | (c << 32);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            ntok += (uint32_t)__popcll(K0) + 2u * (uint32_t)__popcll(K1) + 4u * (uint32_t)__popcll(K2);
+            quotes += (uint32_t)__popcll(Po);
         }
         ok = ok && !bad && ntok <= kWTok && (quotes & 1u) == 0 && ntok > 0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -946,12 +1029,12 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
         uint32_t nop1 = 0, ncl2 = 0;
         for (uint32_t t0 = 0; ok && t0 < ntok; t0 += 64) {
             const uint32_t t = t0 + lane;
-            const uint8_t ch = t < ntok ? B[W.pos[t]] : (uint8_t)' ';
+            const uint8_t ch = t < ntok ? W.tc[t] : (uint8_t)' ';
             const uint64_t Op = __ballot(t < ntok && wave_isopen(ch));
             const uint64_t Cl = __ballot(t < ntok && wave_isclose(ch));
             const int32_t d = depth + __popcll(Op & lt) - __popcll(Cl & lt);
-            if (t < ntok) W.dep[t] = (int16_t)d;
-            neg |= __ballot(t < ntok && (d < 0 || d > 30000 || (wave_isclose(ch) && d < 1))) != 0;
+            if (t < ntok) W.dep[t] = (int8_t)d;
+            neg |= __ballot(t < ntok && (d < 0 || d > 120 || (wave_isclose(ch) && d < 1))) != 0;
             const uint64_t O1 = __ballot(t < ntok && wave_isopen(ch) && d == 1);
             const uint64_t C2 = __ballot(t < ntok && wave_isclose(ch) && d == 2);
             const uint32_t io = nop1 + (uint32_t)__popcll(O1 & lt), ic = ncl2 + (uint32_t)__popcll(C2 & lt);
@@ -964,7 +1047,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
         ok = ok && !neg && depth == 0 && nop1 <= 32 && nop1 == ncl2;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         WPROF(2);
-        WaveMsg M{&W, B, len, ntok};
+        WaveMsg M{&W, B, len, ntok, sh};
         // the top level, wave-uniformly: [records] or {key: value, ...}
         uint32_t arr = ntok, arr_end = ntok;  // the changes array's '[' and ']'
         uint32_t ck = 0, msrc = NULL_ID, mtgt = NULL_ID;
@@ -1004,9 +1087,8 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
                         nx = arr_end + 1;
                     } else if (wave_key(M, t, "checksum") || wave_key(M, t, "membershipChecksum") ||
                                wave_key(M, t, "sourceIncarnationNumber")) {
-                        uint32_t s0, e0;
                         int64_t x;
-                        ok = M.scalar(t + 2, s0, e0) && M.integer(s0, e0, x);
+                        ok = M.int_tok(t + 2, x);
                         if (wave_key(M, t, "sourceIncarnationNumber"))
                             msinc = x;
                         else
@@ -1068,7 +1150,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
         // the changes array: its level tokens are { , { , ... {
         uint32_t nrec = 0;
         if (ok) {
-            const int16_t d = W.dep[arr];
+            const int32_t d = W.dep[arr];
             uint32_t nl = 0;
             for (uint32_t t0 = arr + 1; t0 < arr_end; t0 += 64) {
                 const uint32_t t = t0 + lane;
