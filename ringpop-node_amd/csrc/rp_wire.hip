@@ -341,15 +341,20 @@ struct Out {
     uint8_t* m_ping_status;  // 0 false, 1 true, 0xFF absent
 };
 
-__device__ int name_cmp(const Names& nm, const uint8_t* s, uint32_t len, uint32_t id) {
-    const uint64_t a = nm.off[id], b = nm.off[id + 1];
-    const uint32_t l2 = (uint32_t)(b - a);
-    const uint32_t k = len < l2 ? len : l2;
-    for (uint32_t i = 0; i < k; i++) {
-        const uint8_t x = s[i], y = nm.bytes[a + i];
-        if (x != y) return x < y ? -1 : 1;
+// name id's bytes == s[0..len): 16 bytes per step, all loads of a step issued together
+__device__ bool name_eq(const Names& nm, const uint8_t* s, uint32_t len, uint32_t id) {
+    const uint64_t a = nm.off[id];
+    if (nm.off[id + 1] - a != len) return false;
+    for (uint32_t i = 0; i < len; i += 16) {
+        uint32_t d = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 16; j++) {
+            const uint32_t k = min(i + j, len - 1);
+            d |= (uint32_t)(s[k] ^ nm.bytes[a + k]);
+        }
+        if (d) return false;
     }
-    return len == l2 ? 0 : (len < l2 ? -1 : 1);
+    return true;
 }
 
 // the interned id of the bytes s[0..len), or NULL_ID: one farmhash32 and, expected, about one
@@ -358,7 +363,7 @@ __device__ uint32_t name_find(const Names& nm, const uint8_t* s, uint32_t len) {
     uint32_t slot = fh::hash32(fh::PtrSrc{s}, len) & nm.hmask;
     while (true) {
         const uint32_t id = nm.htab[slot];
-        if (id == NULL_ID || name_cmp(nm, s, len, id) == 0) return id;
+        if (id == NULL_ID || name_eq(nm, s, len, id)) return id;
         slot = (slot + 1) & nm.hmask;
     }
 }
@@ -775,9 +780,19 @@ struct WaveMsg {
     }
 };
 
-template <int N>
-__device__ bool wave_key(const WaveMsg& M, uint32_t t, const char (&k)[N]) {
-    return key_is(M.b + M.W->pos[t] + 1, (uint32_t)(M.W->pos[t + 1] - M.W->pos[t] - 1), k);
+// A body member's key: 1 changes / membership, 2 checksum / membershipChecksum,
+// 3 sourceIncarnationNumber, 4 pingStatus, 5 source / coordinator, 6 target, 0 any other
+__device__ int top_kind(const uint8_t* kp, uint32_t kl) {
+    switch (kl) {
+        case 7: return key_eq(kp, "changes") ? 1 : 0;
+        case 10: return key_eq(kp, "membership") ? 1 : key_eq(kp, "pingStatus") ? 4 : 0;
+        case 8: return key_eq(kp, "checksum") ? 2 : 0;
+        case 18: return key_eq(kp, "membershipChecksum") ? 2 : 0;
+        case 23: return key_eq(kp, "sourceIncarnationNumber") ? 3 : 0;
+        case 6: return key_eq(kp, "source") ? 5 : key_eq(kp, "target") ? 6 : 0;
+        case 11: return key_eq(kp, "coordinator") ? 5 : 0;
+        default: return 0;
+    }
 }
 
 // One record's fields as parsed.
@@ -789,7 +804,9 @@ struct RecF {
 };
 
 // One record object, tokens [t0 = '{', t1 = its '}'], parsed by one lane (addresses resolved).
-// false: leave the message to the thread parser.
+// false: leave the message to the thread parser. Each member's tokens (key, ':', value and
+// the separator after it) are read from LDS together, so a member costs about three dependent
+// LDS trips: its tokens, then its key's and value's bytes, then the name lookups.
 __device__ bool wave_record(const WaveMsg& M, const Names& nm, uint64_t base, uint32_t t0, uint32_t t1, RecF& f) {
     f.addr = NULL_ID;
     f.src = NULL_ID;
@@ -800,16 +817,20 @@ __device__ bool wave_record(const WaveMsg& M, const Names& nm, uint64_t base, ui
     f.inc = 0;
     f.sinc = LLONG_MIN;
     bool has_inc = false;
+    const uint16_t* P = M.W->pos;
+    const uint8_t* TC = M.W->tc;
     uint32_t t = t0 + 1;
     if (t >= t1) return false;  // {} : no address
     while (true) {
-        // "key" :
-        if (t + 2 >= t1 || M.tch(t) != '"' || M.tch(t + 1) != '"' || M.tch(t + 2) != ':') return false;
-        if (!M.clean(M.W->pos[t - 1], M.W->pos[t]) || !M.clean(M.W->pos[t + 1], M.W->pos[t + 2])) return false;
-        const uint32_t kt = t;
-        const uint32_t v = t + 3;
-        const uint8_t* kp = M.b + M.W->pos[kt] + 1;
-        const uint32_t kl = (uint32_t)(M.W->pos[kt + 1] - M.W->pos[kt] - 1);
+        // "key" : value (,|}) — tokens t .. t + 5 (indices past t1 are read but not used:
+        // they stay inside this wave's WaveLds)
+        if (t + 2 >= t1) return false;
+        const uint32_t pm = P[t - 1], p0 = P[t], p1 = P[t + 1], p2 = P[t + 2], p3 = P[t + 3], p4 = P[t + 4],
+                       p5 = P[t + 5];
+        const uint8_t c0 = TC[t], c1 = TC[t + 1], c2 = TC[t + 2], c3 = TC[t + 3], c4 = TC[t + 4], c5 = TC[t + 5];
+        if (!((c0 == '"') & (c1 == '"') & (c2 == ':')) || !M.clean(pm, p0) || !M.clean(p1, p2)) return false;
+        const uint8_t* kp = M.b + p0 + 1;
+        const uint32_t kl = p1 - p0 - 1;
         // 1 address, 2 source, 3 status, 4 id, 5 incarnationNumber, 6 sourceIncarnationNumber
         // (dispatched on the length: one compare)
         const int kind = kl == 7 ? (key_eq(kp, "address") ? 1 : 0)
@@ -818,9 +839,12 @@ __device__ bool wave_record(const WaveMsg& M, const Names& nm, uint64_t base, ui
                        : kl == 17 ? (key_eq(kp, "incarnationNumber") ? 5 : 0)
                        : kl == 23 ? (key_eq(kp, "sourceIncarnationNumber") ? 6 : 0) : 0;
         uint32_t nx;
+        uint8_t cn, cb;  // the separator token's character and the one before it
+        uint32_t pb, pn;  // their positions
         if (kind >= 1 && kind <= 4) {
-            if (v + 1 >= t1 || M.tch(v) != '"' || !M.clean(M.W->pos[v - 1], M.W->pos[v])) return false;
-            const uint32_t so = M.W->pos[v] + 1, sl = M.W->pos[v + 1] - so;
+            // a string value: tokens t + 3, t + 4; the separator t + 5
+            if (t + 4 >= t1 || c3 != '"' || !M.clean(p2, p3)) return false;
+            const uint32_t so = p3 + 1, sl = p4 - so;
             if (kind == 1) {
                 f.aoff = base + so;
                 f.alen = sl;
@@ -833,30 +857,42 @@ __device__ bool wave_record(const WaveMsg& M, const Names& nm, uint64_t base, ui
             } else {
                 f.idoff = base + so;
             }
-            nx = v + 2;
+            nx = t + 5;
+            cn = c5;
+            cb = c4;
+            pb = p4;
+            pn = p5;
         } else if (kind >= 5) {
+            // an integer between tokens t + 2 and t + 3 (the separator)
             int64_t x;
-            if (v >= t1 + 1 || !M.int_tok(kt + 2, x)) return false;
+            if (!M.int_tok(t + 2, x)) return false;
             if (kind == 5) {
                 f.inc = x;
                 has_inc = true;
             } else {
                 f.sinc = x;
             }
-            nx = v;
+            nx = t + 3;
+            cn = c3;
+            cb = c2;
+            pb = p2;
+            pn = p3;
         } else {
-            nx = M.skip(v);
+            nx = M.skip(t + 3);
             if (nx > t1) return false;
+            cn = M.tch(nx);
+            cb = M.tch(nx - 1);
+            pb = P[nx - 1];
+            pn = P[nx];
         }
         // , or }
         if (nx > t1) return false;
-        const uint8_t c = M.tch(nx);
-        if (!M.clean(M.W->pos[nx - 1], M.W->pos[nx]) && M.tch(nx - 1) != ':') return false;
+        if (cb != ':' && !M.clean(pb, pn)) return false;
         if (nx == t1) {
-            if (c != '}') return false;
+            if (cn != '}') return false;
             break;
         }
-        if (c != ',') return false;
+        if (cn != ',') return false;
         t = nx + 1;
     }
     return f.alen != 0 && f.st != 0xFF && has_inc;
@@ -1067,14 +1103,16 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
                 uint32_t t = 1, kop = 0;  // kop: the next depth-1 opener, in walk order
                 bool seen = false, closed = false;
                 while (ok) {
-                    if (t + 2 >= last || M.tch(t) != '"' || M.tch(t + 1) != '"' || M.tch(t + 2) != ':' ||
+                    const uint8_t c0 = M.tch(t), c1 = M.tch(t + 1), c2 = M.tch(t + 2);
+                    if (t + 2 >= last || !((c0 == '"') & (c1 == '"') & (c2 == ':')) ||
                         !M.clean(W.pos[t - 1], W.pos[t]) || !M.clean(W.pos[t + 1], W.pos[t + 2])) {
                         ok = false;
                         break;
                     }
                     const uint32_t v = t + 3;
                     uint32_t nx = ntok;
-                    if (wave_key(M, t, "changes") || wave_key(M, t, "membership")) {
+                    const int kind = top_kind(B + W.pos[t] + 1, (uint32_t)(W.pos[t + 1] - W.pos[t] - 1));
+                    if (kind == 1) {
                         if (seen || v >= last || M.tch(v) != '[' || !M.clean(W.pos[v - 1], W.pos[v])) {
                             ok = false;
                             break;
@@ -1085,16 +1123,15 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
                         arr_end = ok ? W.cl2[kop++] : ntok;
                         ok = ok && arr_end < last && M.tch(arr_end) == ']';
                         nx = arr_end + 1;
-                    } else if (wave_key(M, t, "checksum") || wave_key(M, t, "membershipChecksum") ||
-                               wave_key(M, t, "sourceIncarnationNumber")) {
+                    } else if (kind == 2 || kind == 3) {
                         int64_t x;
                         ok = M.int_tok(t + 2, x);
-                        if (wave_key(M, t, "sourceIncarnationNumber"))
+                        if (kind == 3)
                             msinc = x;
                         else
                             ck = (uint32_t)x;
                         nx = v;
-                    } else if (wave_key(M, t, "pingStatus")) {
+                    } else if (kind == 4) {
                         uint32_t s0, e0;
                         ok = M.scalar(t + 2, s0, e0);
                         if (ok && e0 - s0 == 4 && B[s0] == 't' && B[s0 + 1] == 'r' && B[s0 + 2] == 'u' && B[s0 + 3] == 'e')
@@ -1105,13 +1142,13 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
                         else
                             ok = false;
                         nx = v;
-                    } else if (wave_key(M, t, "source") || wave_key(M, t, "coordinator") || wave_key(M, t, "target")) {
+                    } else if (kind == 5 || kind == 6) {
                         ok = v + 1 < last && M.tch(v) == '"' && M.clean(W.pos[v - 1], W.pos[v]);
                         if (ok) {
                             const uint32_t so = W.pos[v] + 1, sl = W.pos[v + 1] - so;
                             const uint32_t id = lane == 0 ? name_find(nm, B + so, sl) : 0u;
                             const uint32_t idb = __shfl(id, 0, 64);
-                            if (wave_key(M, t, "target"))
+                            if (kind == 6)
                                 mtgt = idb;
                             else
                                 msrc = idb;
