@@ -375,7 +375,8 @@ def sim_bench(rpa, torch, dist, local, n=10_000, kill_pct=1, seed=11, max_rounds
 def wire_bench(rpa, torch, dev, n_msgs=100_000, recs=32, reps=5):
     """Gossip wire bodies (rp_wire_*): n_msgs ping request bodies (ping-sender.js:71-76), each
     carrying `recs` issueAs change records (dissemination.js:163-170) over the C5 address set,
-    encoded to JSON and decoded back on the device. Reported as records/s and JSON GB/s (the
+    encoded to JSON and decoded back on the device (records and the body headers a ping
+    receiver reads: checksum, source, sourceIncarnationNumber). Reported as records/s and JSON GB/s (the
     bytes written by the encoder / read by the decoder; both are bounded by HBM)."""
     S = _synth()
     n = 100_000
@@ -404,6 +405,9 @@ def wire_bench(rpa, torch, dev, n_msgs=100_000, recs=32, reps=5):
     e = lambda dt: torch.empty(k, dtype=dt, device="cuda")  # noqa: E731
     cols = [e(torch.int32), e(torch.int32), e(torch.uint8), e(torch.int64), e(torch.int64)]
     err = torch.empty(n_msgs, dtype=torch.int64, device="cuda")
+    # the body headers a ping receiver reads (ping.js: checksum, source, sourceIncarnationNumber)
+    h_ck, h_src = (torch.empty(n_msgs, dtype=torch.int32, device="cuda") for _ in range(2))
+    h_sinc = torch.empty(n_msgs, dtype=torch.int64, device="cuda")
 
     def enc():
         rpa.check(L.rp_wire_encode_changes_dev(*args, out.data_ptr(), out_off.data_ptr(), sp))
@@ -411,7 +415,7 @@ def wire_bench(rpa, torch, dev, n_msgs=100_000, recs=32, reps=5):
     def dec():
         rpa.check(L.rp_wire_decode_changes_dev(m._h, out.data_ptr(), out_off.data_ptr(), n_msgs, rec_off2.data_ptr(),
                                                k, *[c.data_ptr() for c in cols], None, None, None, err.data_ptr(),
-                                               None, None, None, sp))
+                                               h_ck.data_ptr(), h_src.data_ptr(), h_sinc.data_ptr(), sp))
         torch.cuda.synchronize()
 
     res = {}
@@ -425,6 +429,7 @@ def wire_bench(rpa, torch, dev, n_msgs=100_000, recs=32, reps=5):
         dt = (time.perf_counter() - t0) / reps
         res[name] = {"ms": dt * 1e3, "records_per_s": k / dt, "json_GBps": total / dt / 1e9}
     ok = bool((err == 0).all().item()) and bool(torch.equal(cols[0], addr)) and bool(torch.equal(cols[3], inc))
+    ok = ok and bool(torch.equal(h_ck, ck)) and bool(torch.equal(h_src, msrc)) and bool(torch.equal(h_sinc, msinc))
     m.close()
     return {"workload": "%d ping request bodies x %d issueAs change records (C5 addresses), JSON encode + decode"
                         % (n_msgs, recs), "json_bytes": total, "round_trip_ok": ok, **res}
