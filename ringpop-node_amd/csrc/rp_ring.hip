@@ -1444,8 +1444,12 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
         const uint64_t ntiles = n / TK, done = ntiles * TK;
         r.slow.reserve(ntiles * kSlowPerTile + 1);
         r.nslow.reserve(ntiles + 1);
-        const unsigned g = grid_for(ntiles, 1, 256 * 8);
         const bool lean = !(getenv("RP_LOOKUP_LEAN") && !strcmp(getenv("RP_LOOKUP_LEAN"), "0"));  // A/B: 0 = round-1 kernel
+        // workgroups, tiles strided over them: the lean kernel at 4096 (4 rounds of the 1024 that
+        // fit, 8 tiles each at C2) ran 0.905-0.911 ms against 0.926-0.930 at 2048 (3072: 0.917;
+        // 5120-16384: 0.908-0.914; profiles/r02/ab_lookup_grid.json). RP_LOOKUP_GRID overrides (A/B).
+        const unsigned g = grid_for(ntiles, 1, getenv("RP_LOOKUP_GRID") ? (unsigned)atoi(getenv("RP_LOOKUP_GRID"))
+                                                                        : (lean ? 4096u : 2048u));
         const int half = getenv("RP_LOOKUP_HALF") ? atoi(getenv("RP_LOOKUP_HALF")) : (kpl == 8 ? 4 : 0);
 #define RP_COMPACT(KPL, NEED)                                                                                  \
     do {                                                                                                        \

@@ -56,10 +56,18 @@ def main():
         "probe/lookupN3": ({"RP_RING_LAYOUT": "packed", "RP_LOOKUP_KPL": "2"}, 3),
         "probe/ablate-hash-only": ({"RP_RING_LAYOUT": "packed", "RP_LOOKUP_ABLATE": "1"}, 3),
         "wide/lookupN3": ({"RP_RING_WIDE": "1"}, 3),
+        "grid1024/lookupN3": ({"RP_LOOKUP_GRID": "1024"}, 3),
+        "grid4096/lookupN3": ({"RP_LOOKUP_GRID": "4096"}, 3),
+        "grid8192/lookupN3": ({"RP_LOOKUP_GRID": "8192"}, 3),
+        "grid3072/lookupN3": ({"RP_LOOKUP_GRID": "3072"}, 3),
+        "grid5120/lookupN3": ({"RP_LOOKUP_GRID": "5120"}, 3),
+        "grid6144/lookupN3": ({"RP_LOOKUP_GRID": "6144"}, 3),
+        "grid16384/lookupN3": ({"RP_LOOKUP_GRID": "16384"}, 3),
+        "grid32768/lookupN3": ({"RP_LOOKUP_GRID": "32768"}, 3),
     }
     if a.only:
         variants = {k: v for k, v in variants.items() if k in a.only.split(",")}
-    knobs = ("RP_LOOKUP_HALF", "RP_LOOKUP_LEAN", "RP_LOOKUP_KPL", "RP_RING_LAYOUT", "RP_LOOKUP_ABLATE", "RP_RING_WIDE")
+    knobs = ("RP_LOOKUP_HALF", "RP_LOOKUP_LEAN", "RP_LOOKUP_KPL", "RP_RING_LAYOUT", "RP_LOOKUP_ABLATE", "RP_RING_WIDE", "RP_LOOKUP_GRID")
     times = {k: [] for k in variants}
     digests = {}
     for r in range(a.rounds + 1):
