@@ -1391,7 +1391,10 @@ int rp_wire_decode_dev(rp_members* m, const uint8_t* d_buf, const uint64_t* d_ms
             RP_HIP(hipStreamSynchronize(st));
             vb += reinterpret_cast<uint64_t>(d_buf);
             ve += reinterpret_cast<uint64_t>(d_buf);
-            const unsigned g = rp::grid_for(n_msgs, rp::kDecWaves, 8192);
+            // a wave per message (3.73 ms at 100 k messages against 3.75-3.86 with 512-8192
+            // workgroups striding; tools/wire_grid.sh); RP_WIRE_GRID caps it (A/B)
+            const unsigned g = rp::grid_for(n_msgs, rp::kDecWaves,
+                                            getenv("RP_WIRE_GRID") ? (unsigned)atoi(getenv("RP_WIRE_GRID")) : 1u << 20);
             const uint64_t nslots = (ve - vb) / rp::kMinRec + n_msgs + 1;
             rp::DevBuf<rp::RecF> stash;
             rp::DevBuf<uint8_t> slow;
