@@ -1356,7 +1356,9 @@ int rp_wire_encode_dev(rp_members* m, uint32_t n_msgs, const uint32_t* d_msg_rec
                            n_msgs, mscan.p, rscan.p, d_out, d_out_off);
         RP_HIP(hipGetLastError());
         if (d_out && n_rec) {
-            hipLaunchKernelGGL(rp::k_rec_write_lds, dim3(rp::grid_for(n_rec, rp::kWrThreads, 4096)),
+            hipLaunchKernelGGL(rp::k_rec_write_lds,
+                               dim3(rp::grid_for(n_rec, rp::kWrThreads,
+                                                 getenv("RP_WIRE_WGRID") ? (unsigned)atoi(getenv("RP_WIRE_WGRID")) : 4096u)),
                                dim3(rp::kWrThreads), 0, st, nm, R, M, n_msgs, n_rec, mscan.p, rscan.p, d_out);
             RP_HIP(hipGetLastError());
         }
