@@ -118,6 +118,8 @@ LAYOUTS = {
     "half-kpl2": {"RP_LOOKUP_HALF": "2", "RP_LOOKUP_KPL": "2"},
     "half-kpl8": {"RP_LOOKUP_HALF": "2", "RP_LOOKUP_KPL": "8"},
     "quarter-kpl8": {"RP_LOOKUP_HALF": "4", "RP_LOOKUP_KPL": "8"},
+    # three workgroups striding over every tile (RP_LOOKUP_GRID): LDS lists and counters reused
+    "quarter-kpl8-grid3": {"RP_LOOKUP_HALF": "4", "RP_LOOKUP_KPL": "8", "RP_LOOKUP_GRID": "3"},
     "lean-kpl4": {"RP_LOOKUP_HALF": "0", "RP_LOOKUP_KPL": "4"},
     "round1": {"RP_LOOKUP_LEAN": "0"},
     "round1-kpl1": {"RP_LOOKUP_LEAN": "0", "RP_LOOKUP_KPL": "1"},
@@ -128,7 +130,8 @@ LAYOUTS = {
 
 
 def set_layout(monkeypatch, layout):
-    for k in ("RP_RING_WIDE", "RP_RING_NOWINDOW", "RP_RING_LAYOUT", "RP_LOOKUP_KPL", "RP_LOOKUP_LEAN", "RP_LOOKUP_HALF"):
+    for k in ("RP_RING_WIDE", "RP_RING_NOWINDOW", "RP_RING_LAYOUT", "RP_LOOKUP_KPL", "RP_LOOKUP_LEAN", "RP_LOOKUP_HALF",
+              "RP_LOOKUP_GRID"):
         monkeypatch.delenv(k, raising=False)
     for k, v in LAYOUTS[layout].items():
         monkeypatch.setenv(k, v)

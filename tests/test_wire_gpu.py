@@ -364,16 +364,20 @@ def _fuzz_texts(cases, seed):
     return out + mutants
 
 
-def test_wave_decoder_equals_thread_decoder(gpu, monkeypatch, capfd):
+@pytest.mark.parametrize("grid", [None, "3"], ids=["wave-per-message", "waves-stride-messages"])
+def test_wave_decoder_equals_thread_decoder(gpu, monkeypatch, capfd, grid):
     """The wave-per-message decoder (k_decode_wave) and the thread parser (RP_WIRE_THREAD=1)
     return identical columns, offsets, headers and error offsets on the reference's bodies,
     re-laid-out variants with unknown members, and single-character mutants; the waves take
-    every well-formed message."""
+    every well-formed message. grid "3": three workgroups, so every wave parses many messages
+    one after another in the same LDS (RP_WIRE_GRID)."""
     cases = golden()
     m = gpu.Membership()
     for c in cases:
         m.intern([mm[0] for mm in c["members"]] + [c["target"]])
     texts = _fuzz_texts(cases, 11)
+    if grid:
+        monkeypatch.setenv("RP_WIRE_GRID", grid)
     monkeypatch.setenv("RP_WIRE_DEBUG", "1")
     capfd.readouterr()
     dw = gpu.wire_decode(m, texts)
