@@ -120,7 +120,8 @@ def cpu_baseline(servers, nkeys, threads, min_seconds=10.0):
 def merge_cpu_baseline(n, k, threads):
     """C3 on the host: the oracle's Membership.update (oracle/orc_members.c: sequential fold +
     one checksum per batch, as lib/membership/index.js:249-324 runs) on one thread, and the fold
-    sharded by id over `threads` threads (checksum still one serial hash)."""
+    sharded by id over `threads` threads with the checksum string formatted by all of them (the
+    hash itself is one serial chain). `value` is the better of the two."""
     pyoracle = _oracle()
     S = _synth()
     names, st0, inc0 = S.c3_members(n)
@@ -150,8 +151,9 @@ def merge_cpu_baseline(n, k, threads):
             b += 1
         dt = time.perf_counter() - t0
         res[label] = (done / dt, b - b0, dt)
-    return {"value": res["all"][0], "unit": "updates/s", "cores": threads, "kind": "port",
-            "value_1thread": res["1thread"][0],
+    best = "all" if res["all"][0] >= res["1thread"][0] else "1thread"
+    return {"value": res[best][0], "unit": "updates/s", "cores": threads if best == "all" else 1, "kind": "port",
+            "value_1thread": res["1thread"][0], "value_all_threads": res["all"][0], "best_of": best,
             "sample": "C3 batches of %d updates over %d members incl. one checksum per batch: %d batches on 1 "
                       "thread (oracle/orc_members.c sequential fold) in %.1f s; %d batches with the fold sharded "
                       "by id over %d threads in %.1f s" % (k, n, res["1thread"][1], res["1thread"][2],

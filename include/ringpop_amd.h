@@ -8,7 +8,12 @@
  *   - every function returns 0 on success or a negative status; rp_last_error() gives the
  *     thread-local message. Empty results are NOT errors (reference returns null / []).
  *   - host pointers are borrowed for the duration of the call; *_dev variants take device
- *     pointers and a HIP stream (void*; NULL = default stream) and are stream-ordered.
+ *     pointers and a HIP stream (void*; NULL = the null stream, except rp_wire_decode*_dev,
+ *     where NULL = the members handle's own stream) and are stream-ordered. A handle's device
+ *     scratch is ordered across streams: a call on another stream than the handle's previous
+ *     one first waits for the work queued on that stream. Device-side ordering faults (a
+ *     look-back wait that gave up) are reported as RP_EDEVICE at the next host-synchronizing
+ *     call on the handle.
  *   - owner ids are interned server ids (stable for the life of a ring); 0xFFFFFFFF = null.
  *   - strings are byte ranges (UTF-8): `bytes` + `off[n+1]` (uint32 offsets) or a fixed
  *     `stride`. Handles are not thread-safe (one HIP stream per handle).

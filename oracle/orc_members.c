@@ -44,6 +44,10 @@ struct orc_members {
     uint32_t *sorted; /* ids sorted by address */
     char *buf;
     uint64_t buf_cap;
+    /* compute_checksum_mt: per-thread segment buffers, kept across calls (fresh pages per call
+       would serialise the threads on page faults) */
+    char *tbuf[256];
+    uint64_t tcap[256];
 };
 
 static int cmp_addr(const orc_members *m, uint32_t a, uint32_t b) {
@@ -84,6 +88,7 @@ void orc_members_free(orc_members *m) {
     free(m->nb); free(m->noff); free(m->exists); free(m->status); free(m->inc); free(m->order);
     free(m->st_id); free(m->st_status); free(m->st_inc); free(m->st_batch_end);
     free(m->sorted); free(m->buf);
+    for (int t = 0; t < 256; t++) free(m->tbuf[t]);
     free(m);
 }
 
@@ -121,7 +126,40 @@ static int other_override(uint8_t cur, int64_t cur_inc, uint8_t st, int64_t inc)
     return 0;
 }
 
-static void compute_checksum(orc_members *m) {
+/* String(inc) for an integral Number (decimal, '-' for negatives); returns the length. */
+static uint32_t fmt_i64(char *o, int64_t v) {
+    char t[24];
+    uint32_t n = 0;
+    uint64_t u = v < 0 ? (uint64_t)(-(v + 1)) + 1 : (uint64_t)v;
+    do {
+        t[n++] = (char)('0' + (u % 10));
+        u /= 10;
+    } while (u);
+    uint32_t w = 0;
+    if (v < 0) o[w++] = '-';
+    while (n) o[w++] = t[--n];
+    return w;
+}
+
+/* generateChecksumString's pieces (index.js:115-120) of the members sorted[k0..k1), each
+ * followed by ';' (the caller drops the string's last ';'). Returns the bytes written. */
+static uint64_t format_pieces(const orc_members *m, uint32_t k0, uint32_t k1, char *o) {
+    uint64_t w = 0;
+    for (uint32_t k = k0; k < k1; k++) {
+        uint32_t id = m->sorted[k];
+        if (!m->exists[id]) continue;
+        uint64_t ln = m->noff[id + 1] - m->noff[id];
+        memcpy(o + w, m->nb + m->noff[id], ln);
+        w += ln;
+        memcpy(o + w, STATUS_STR[m->status[id]], STATUS_LEN[m->status[id]]);
+        w += STATUS_LEN[m->status[id]];
+        w += fmt_i64(o + w, m->inc[id]);
+        o[w++] = ';';
+    }
+    return w;
+}
+
+static void ensure_buf(orc_members *m) {
     uint64_t need = 0;
     for (uint32_t i = 0; i < m->n_names; i++)
         if (m->exists[i]) need += (m->noff[i + 1] - m->noff[i]) + 7 + 21 + 1;
@@ -129,20 +167,70 @@ static void compute_checksum(orc_members *m) {
         m->buf_cap = need + 64;
         m->buf = (char *)realloc(m->buf, m->buf_cap);
     }
-    uint64_t o = 0;
-    int first = 1;
-    for (uint32_t k = 0; k < m->n_names; k++) {
-        uint32_t id = m->sorted[k];
-        if (!m->exists[id]) continue;
-        if (!first) m->buf[o++] = ';';
-        first = 0;
-        uint64_t ln = m->noff[id + 1] - m->noff[id];
-        memcpy(m->buf + o, m->nb + m->noff[id], ln);
-        o += ln;
-        memcpy(m->buf + o, STATUS_STR[m->status[id]], STATUS_LEN[m->status[id]]);
-        o += STATUS_LEN[m->status[id]];
-        o += (uint64_t)sprintf(m->buf + o, "%lld", (long long)m->inc[id]);
+}
+
+static void compute_checksum(orc_members *m) {
+    ensure_buf(m);
+    uint64_t o = format_pieces(m, 0, m->n_names, m->buf);
+    if (o) o--; /* the joined string has no trailing ';' */
+    m->checksum = orc_hash32((const uint8_t *)m->buf, o);
+    m->has_checksum = 1;
+}
+
+/* The same checksum with the string formatted by T threads (segments of the address order in
+ * private buffers, then copied into place); the hash itself is one serial chain. */
+typedef struct {
+    const orc_members *m;
+    uint32_t k0, k1;
+    char *tmp;
+    uint64_t len, off;
+    char *dst;
+} fmt_job;
+
+static void *fmt_worker(void *p) {
+    fmt_job *j = (fmt_job *)p;
+    j->len = format_pieces(j->m, j->k0, j->k1, j->tmp);
+    return NULL;
+}
+
+static void *copy_worker(void *p) {
+    fmt_job *j = (fmt_job *)p;
+    memcpy(j->dst + j->off, j->tmp, j->len);
+    return NULL;
+}
+
+static void compute_checksum_mt(orc_members *m, int T) {
+    if (T <= 1 || m->n_names < 4096) {
+        compute_checksum(m);
+        return;
     }
+    ensure_buf(m);
+    pthread_t th[256];
+    fmt_job jobs[256];
+    const uint32_t per = (m->n_names + T - 1) / T;
+    for (int t = 0; t < T; t++) {
+        uint32_t k0 = (uint32_t)t * per, k1 = k0 + per;
+        if (k0 > m->n_names) k0 = m->n_names;
+        if (k1 > m->n_names) k1 = m->n_names;
+        uint64_t cap = 0;
+        for (uint32_t k = k0; k < k1; k++) cap += (m->noff[m->sorted[k] + 1] - m->noff[m->sorted[k]]) + 7 + 21 + 1;
+        if (cap + 1 > m->tcap[t]) {
+            free(m->tbuf[t]);
+            m->tcap[t] = cap + 1;
+            m->tbuf[t] = (char *)malloc(m->tcap[t]);
+        }
+        jobs[t] = (fmt_job){m, k0, k1, m->tbuf[t], 0, 0, m->buf};
+        pthread_create(&th[t], NULL, fmt_worker, &jobs[t]);
+    }
+    uint64_t o = 0;
+    for (int t = 0; t < T; t++) {
+        pthread_join(th[t], NULL);
+        jobs[t].off = o;
+        o += jobs[t].len;
+    }
+    for (int t = 0; t < T; t++) pthread_create(&th[t], NULL, copy_worker, &jobs[t]);
+    for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
+    if (o) o--;
     m->checksum = orc_hash32((const uint8_t *)m->buf, o);
     m->has_checksum = 1;
 }
@@ -222,7 +310,7 @@ static void *fold_worker(void *p) {
     orc_members *m = j->m;
     for (uint32_t i = 0; i < j->k; i++) {
         uint32_t id = j->ids[i];
-        if (id % j->T != j->t) continue;
+        if ((uint32_t)(((uint64_t)id * j->T) / m->n_names) != j->t) continue; /* contiguous id ranges: no false sharing */
         uint8_t st = j->status[i];
         int64_t in = j->inc[i];
         int applied = 0;
@@ -260,7 +348,7 @@ uint32_t orc_members_update_mt(orc_members *m, const uint32_t *ids, const uint8_
         pthread_join(th[t], NULL);
         napplied += jobs[t].napplied;
     }
-    if (napplied) compute_checksum(m);
+    if (napplied) compute_checksum_mt(m, threads);
     return napplied;
 }
 
@@ -326,3 +414,6 @@ uint64_t orc_members_checksum_string(orc_members *m, char *buf, uint64_t cap) {
     if (buf) memcpy(buf, m->buf, n < cap ? n : cap);
     return n;
 }
+
+/* Membership.computeChecksum on T threads (bench.py's CPU baseline probes it). */
+void orc_members_compute_checksum_mt(orc_members *m, int threads) { compute_checksum_mt(m, threads); }

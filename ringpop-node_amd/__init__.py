@@ -204,6 +204,9 @@ class HashRing:
         check(lib().rp_ring_create(self.replicaPoints, device, ctypes.byref(h)))
         self._h = h
         self._names = {}
+        # servers (lib/ring/index.js:32): name -> True in insertion order (Object.keys order),
+        # kept from the same add / remove decisions the device makes and checked against it
+        self._servers = {}
 
     def close(self):
         if getattr(self, "_h", None):
@@ -244,6 +247,18 @@ class HashRing:
         changed = ctypes.c_int()
         check(lib().rp_ring_add_remove(self._h, ab, ao.ctypes.data, len(add), _ptr(at),
                                        rb, ro.ctypes.data, len(rem), _ptr(rt), ctypes.byref(changed)))
+        mine = False
+        for a in add:
+            if a not in self._servers:
+                self._servers[a] = True
+                mine = True
+        for r in rem:
+            if r in self._servers:
+                del self._servers[r]
+                mine = True
+        if mine != bool(changed.value):
+            raise RingpopAmdError("device ring and servers map disagree (ringChanged %s vs %s)"
+                                  % (bool(changed.value), mine))
         if changed.value:
             self.emit("checksumComputed")
         return bool(changed.value)
@@ -307,10 +322,12 @@ class HashRing:
 
     @property
     def servers(self):
-        return {self.name(i): True for i in self.server_ids()}
+        """lib/ring/index.js:32 (a copy)"""
+        return dict(self._servers)
 
     def getStats(self):
-        return {"checksum": self.checksum, "servers": [self.name(i) for i in self.server_ids()]}
+        """lib/ring/index.js:111-116"""
+        return {"checksum": self.checksum, "servers": list(self._servers)}
 
     def name(self, sid):
         sid = int(sid)

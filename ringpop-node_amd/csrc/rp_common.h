@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <stdexcept>
 #include <string>
@@ -58,6 +59,17 @@ int guard(F&& f) {
 }
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// A positive integer from the environment (A/B knobs: grid caps, group sizes); `dflt` when the
+// variable is unset, empty, not a number, or not positive, so no knob can ask for a 0-workgroup
+// launch.
+inline uint64_t env_pos(const char* name, uint64_t dflt) {
+    const char* e = getenv(name);
+    if (!e || !*e) return dflt;
+    char* end = nullptr;
+    const unsigned long long v = strtoull(e, &end, 10);
+    return (end && *end == 0 && v > 0) ? (uint64_t)v : dflt;
+}
 
 inline unsigned grid_for(uint64_t items, unsigned per_block, unsigned cap = 2048) {
     uint64_t g = (items + per_block - 1) / per_block;

@@ -36,13 +36,42 @@ struct DampArgs {
     uint8_t* exc;   // per change: 'suppressLimitExceeded' emitted (member.js:141-152)
 };
 
+// One member row in HBM (16 B, one aligned load / store per member): incarnation, status,
+// exists, and the grouped fold's per-batch change counter (0 between batches).
+struct alignas(16) MRow {
+    int64_t inc;
+    uint8_t status;
+    uint8_t exists;
+    uint16_t pad;
+    uint32_t cnt;
+};
+static_assert(sizeof(MRow) == 16, "MRow is one 16-byte load");
+
+// One dwordx4 load / store per row (a struct copy would be split into per-field accesses).
+__device__ __forceinline__ MRow row_load(const MRow* p) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    MRow r;
+    r.inc = (int64_t)(((uint64_t)v.y << 32) | v.x);
+    r.status = (uint8_t)(v.z & 0xFFu);
+    r.exists = (uint8_t)((v.z >> 8) & 0xFFu);
+    r.pad = 0;
+    r.cnt = v.w;
+    return r;
+}
+__device__ __forceinline__ void row_store(MRow* p, int64_t inc, uint8_t status, uint8_t exists) {
+    uint4 v;
+    v.x = (uint32_t)(uint64_t)inc;
+    v.y = (uint32_t)((uint64_t)inc >> 32);
+    v.z = (uint32_t)status | ((uint32_t)exists << 8);
+    v.w = 0;  // the grouped fold's change counter, cleared
+    *reinterpret_cast<uint4*>(p) = v;
+}
+
 // The batch and table operands of one Membership.update fold.
 struct FoldArgs {
     const uint8_t* ch_status;
     const int64_t* ch_inc;
-    uint8_t* exists;
-    uint8_t* status;
-    int64_t* inc;
+    MRow* rows;
     uint32_t local_id;
     int64_t now_ms;
     uint8_t* applied;
@@ -57,15 +86,16 @@ struct FoldArgs {
 // of the address's q-th change. applied: 0 = not applied, 1 = applied to an existing member,
 // 2 = created a new member. With damp tracking on, an applied update to another member takes
 // _applyUpdatePenalty (member.js:98-107, 133-153) and every applied update stamps
-// lastUpdateTimestamp (:115-118).
+// lastUpdateTimestamp (:115-118). `row` is the member's row as loaded; it is written back once
+// with its change counter cleared.
 // Returns the number of changes applied (the caller sums them per wave: one atomic per wave,
 // not per address, on the batch's applied counter).
 template <class Change>
-__device__ __forceinline__ uint32_t fold_address(const FoldArgs& A, uint32_t id, uint32_t c, Change change) {
+__device__ __forceinline__ uint32_t fold_address(const FoldArgs& A, uint32_t id, MRow row, uint32_t c, Change change) {
     const DampArgs& da = A.da;
-    bool ex = A.exists[id] != 0;
-    uint8_t st = A.status[id];
-    int64_t in = A.inc[id];
+    bool ex = row.exists != 0;
+    uint8_t st = row.status;
+    int64_t in = row.inc;
     double sc = 0.0, ls = 0.0;
     int64_t lt = 0;
     if (da.score) {
@@ -108,9 +138,7 @@ __device__ __forceinline__ uint32_t fold_address(const FoldArgs& A, uint32_t id,
             da.exc[j] = exc ? 1 : 0;
         }
     }
-    A.exists[id] = ex ? 1 : 0;
-    A.status[id] = st;
-    A.inc[id] = in;
+    row_store(A.rows + id, in, st, ex ? 1 : 0);
     if (da.score) {
         da.score[id] = sc;
         da.last[id] = ls;
@@ -119,105 +147,142 @@ __device__ __forceinline__ uint32_t fold_address(const FoldArgs& A, uint32_t id,
     return napp;
 }
 
-// Adds every lane's v to *p with one atomic per wave; called by all lanes of the wave.
-__device__ __forceinline__ void wave_atomic_add(uint32_t* p, uint32_t v) {
+// The sum of every thread's v over the workgroup (256 threads), valid in thread 0; called by
+// all threads. (One atomic per wave on a single counter serialises: MI355X retires about 88
+// same-address atomics per µs, so 1,563 waves of a C3 batch cost 18 µs and 65,536 waves of a
+// 2^22 batch 0.75 ms. The fold kernels reduce per workgroup instead.)
+__device__ __forceinline__ uint32_t block_sum256(uint32_t v) {
+    __shared__ uint32_t s_w[4];
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    if ((threadIdx.x & 63) == 0 && v) atomicAdd(p, v);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+// The last workgroup of a launch to get here (done: a counter that is 0 before the launch and is
+// left 0 after it) publishes the batch's applied count to *out and, when reset is non-null,
+// clears *reset (the gate word this launch ran under). Called by every thread of every
+// workgroup after its atomics. Every workgroup pays an agent-scope release fence here (an L2
+// write-back on gfx950), so only the rare sorted fold uses it; the grouped path hands the
+// count on through the next launch instead (k_fold gated off).
+__device__ __forceinline__ void last_block_publish(uint32_t* done, const uint32_t* napplied, uint32_t* out,
+                                                   uint32_t* reset) {
+    __shared__ bool s_last;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!s_last || threadIdx.x != 0) return;
+    __threadfence();
+    if (out) *out = __hip_atomic_load(napplied, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (reset) __hip_atomic_store(reset, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Sorted path: one lane per id segment of the (id, arrival)-sorted batch. run_if (may be null):
-// skip unless *run_if != 0.
-// g_cnt / g_head (non-null after a grouped attempt that overflowed): every id of the batch gets
-// its grouped-path entries reset here as well (they are only read by the grouped path), which
-// saves the batch a launch.
-__global__ void k_fold(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv, uint32_t k, FoldArgs A,
-                       const uint32_t* __restrict__ run_if, uint32_t* __restrict__ g_cnt = nullptr,
-                       uint32_t* __restrict__ g_head = nullptr) {
-    if (run_if && *run_if == 0) return;
+// skip unless *run_if != 0; the last workgroup then clears *run_if. done / out: see
+// last_block_publish (out may be null). Every id of the batch gets its row written (counter
+// cleared), so a grouped attempt that overflowed leaves no counts behind. Gated off, the
+// grouped fold ran before it in the stream: workgroup 0 sums that fold's per-workgroup applied
+// counts (part[0..nparts)) into *A.n_applied (the checksum gate) and *out.
+__global__ __launch_bounds__(256) void k_fold(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
+                                              uint32_t k, FoldArgs A, uint32_t* __restrict__ run_if,
+                                              uint32_t* __restrict__ done, uint32_t* __restrict__ out,
+                                              const uint32_t* __restrict__ part, uint32_t nparts) {
+    if (run_if && *run_if == 0) {
+        if (blockIdx.x != 0) return;
+        uint32_t v = 0;
+        for (uint32_t b = threadIdx.x; b < nparts; b += 256) v += part[b];
+        v = block_sum256(v);
+        if (threadIdx.x == 0) {
+            *A.n_applied = v;
+            if (out) *out = v;
+        }
+        return;
+    }
     const uint32_t gstride = gridDim.x * blockDim.x;
     uint32_t napp = 0;
     for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < k; p += gstride) {
         const uint32_t id = sk[p];
-        if (g_cnt) {
-            g_cnt[id] = 0;
-            g_head[id] = 0xFFFFFFFFu;
-        }
         if (p > 0 && sk[p - 1] == id) continue;  // not a segment head
         uint32_t c = 1;
         while (p + c < k && sk[p + c] == id) c++;
-        napp += fold_address(A, id, c, [&](uint32_t q) { return sv[p + q]; });
+        napp += fold_address(A, id, row_load(A.rows + id), c, [&](uint32_t q) { return sv[p + q]; });
     }
-    wave_atomic_add(A.n_applied, napp);
+    napp = block_sum256(napp);
+    if (threadIdx.x == 0 && napp) atomicAdd(A.n_applied, napp);
+    last_block_publish(done, A.n_applied, out, run_if);
 }
 
-// Grouped path (no sort): every change links itself into its address's list (arbitrary order)
-// and counts it; an address with more than kGroupMax changes in the batch sets *overflow and
-// the batch takes the sorted path instead. cnt / head are all-zero / all-EMPTY between batches
-// (each fold resets the entries it used).
-constexpr uint32_t kGroupMax = 16;
-// Batches up to here take the grouped fold: below it the sorted fold is launch-bound (1e5
-// changes: 0.054 vs 0.096 ms per batch); above it the grouped fold's scattered per-address
-// atomics and table accesses cost more than the sort saves (4M changes: 1.03 vs 0.68 ms).
-constexpr uint32_t kGroupedMaxBatch = 1u << 19;
-constexpr uint32_t kGroupEmpty = 0xFFFFFFFFu;
+// Grouped path (no sort, round 3): two launches per batch.
+//   k_link: every change takes its rank among its address's changes from an atomic on the
+//   address's row counter (arbitrary order), keeps it (rk), and a change of rank 1..kSlots
+//   writes its batch index into the address's inline slot array. Rank kSlots + 1 (an address
+//   with more than kSlots + 1 changes) sets *ovf, and the sorted path folds the batch instead.
+//   k_fold_fast: the rank-0 change of every address loads the row (count included) and, for a
+//   repeated address, its slots (contiguous, no dependent list walk), puts the indices in
+//   arrival order in registers and folds them.
+// Each address costs one atomic, one 16-B row load and one 16-B row store; the batch's applied
+// counter is cleared by k_link, so the batch needs no memset.
+constexpr uint32_t kSlots = 15;  // changes per address on the grouped path: kSlots + 1
+constexpr uint32_t kDoneWords = 4;  // [0] k_fold_fast, [1] k_fold, [2] k_mck? (spare)
 
-__global__ void k_group_link(const uint32_t* __restrict__ ids, uint32_t k, uint32_t* __restrict__ cnt,
-                             uint32_t* __restrict__ head, uint32_t* __restrict__ nxt, uint32_t* __restrict__ overflow) {
-    const uint32_t gstride = gridDim.x * blockDim.x;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < k; i += gstride) {
-        const uint32_t id = ids[i];
-        const uint32_t c = atomicAdd(&cnt[id], 1u);
-        nxt[i] = atomicExch(&head[id], i);
-        if (c == kGroupMax) *overflow = 1u;
-    }
+__global__ void k_link(const uint32_t* __restrict__ ids, uint32_t k, MRow* __restrict__ rows,
+                       uint32_t* __restrict__ slots, uint8_t* __restrict__ rk, uint32_t* __restrict__ ovf,
+                       uint32_t* __restrict__ napplied) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) *napplied = 0;
+    if (i >= k) return;
+    const uint32_t id = ids[i];
+    const uint32_t r = atomicAdd(&rows[id].cnt, 1u);
+    rk[i] = r < 255u ? (uint8_t)r : (uint8_t)255;
+    if (r >= 1u && r <= kSlots) slots[(uint64_t)id * kSlots + (r - 1u)] = i;
+    if (r == kSlots + 1u) *ovf = 1u;
 }
 
-// One lane per address: the lane of the address's last-linked change (head) gathers the list,
-// puts it in arrival order (insertion sort of at most kGroupMax indices) and folds it; a
-// single change folds directly. Then the address's cnt / head entries are reset.
-__global__ void k_fold_grouped(const uint32_t* __restrict__ ids, uint32_t k, uint32_t* __restrict__ cnt,
-                               uint32_t* __restrict__ head, const uint32_t* __restrict__ nxt,
-                               const uint32_t* __restrict__ overflow, FoldArgs A) {
-    if (*overflow) return;
-    const uint32_t gstride = gridDim.x * blockDim.x;
+// The workgroup's applied count goes to part[blockIdx.x] (summed by the gated-off k_fold).
+__global__ __launch_bounds__(256) void k_fold_fast(const uint32_t* __restrict__ ids, uint32_t k,
+                                                   const uint8_t* __restrict__ rk, const uint32_t* __restrict__ slots,
+                                                   const uint32_t* __restrict__ ovf, FoldArgs A,
+                                                   uint32_t* __restrict__ part) {
+    if (*ovf) return;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t napp = 0;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < k; i += gstride) {
+    if (i < k && rk[i] == 0) {
         const uint32_t id = ids[i];
-        const uint32_t c = cnt[id];
-        if (c == 1) {
-            napp += fold_address(A, id, 1, [&](uint32_t) { return i; });
-            cnt[id] = 0;
-            head[id] = kGroupEmpty;
-            continue;
-        }
-        if (c == 0 || head[id] != i) continue;  // another lane owns this address
-        uint32_t idx[kGroupMax];
-        uint32_t j = i;
-        for (uint32_t q = 0; q < c; q++) {
-            uint32_t x = j, r = q;
-            while (r > 0 && idx[r - 1] > x) {
-                idx[r] = idx[r - 1];
-                r--;
+        const MRow row = row_load(A.rows + id);
+        const uint32_t c = row.cnt;
+        if (c <= 1) {
+            napp = fold_address(A, id, row, 1, [&](uint32_t) { return i; });
+        } else {
+            uint32_t idx[kSlots + 1];
+            idx[0] = i;
+            const uint32_t* sl = slots + (uint64_t)id * kSlots;
+            for (uint32_t q = 1; q < c; q++) {
+                const uint32_t x = sl[q - 1];
+                uint32_t r = q;
+                while (r > 0 && idx[r - 1] > x) {
+                    idx[r] = idx[r - 1];
+                    r--;
+                }
+                idx[r] = x;
             }
-            idx[r] = x;
-            j = nxt[j];
+            napp = fold_address(A, id, row, c, [&](uint32_t q) { return idx[q]; });
         }
-        napp += fold_address(A, id, c, [&](uint32_t q) { return idx[q]; });
-        cnt[id] = 0;
-        head[id] = kGroupEmpty;
     }
-    wave_atomic_add(A.n_applied, napp);
+    napp = block_sum256(napp);
+    if (threadIdx.x == 0) part[blockIdx.x] = napp;
 }
 
 // Membership._decayMembersDampScore (index.js:374-383): decayDampScore on every member
 // (member.js:45-66). Reads 17 B and writes 8 B per id.
-__global__ void k_damp_decay(const uint8_t* __restrict__ exists, uint32_t n, double* __restrict__ score,
+__global__ void k_damp_decay(const MRow* __restrict__ rows, uint32_t n, double* __restrict__ score,
                              const double* __restrict__ last, const int64_t* __restrict__ ts, damp::Config c,
                              int64_t now_ms) {
     const uint32_t gstride = gridDim.x * blockDim.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gstride)
-        if (exists[i]) score[i] = damp::decayed(c, last[i], ts[i], now_ms);
+        if (rows[i].exists) score[i] = damp::decayed(c, last[i], ts[i], now_ms);
 }
 
 template <class T>
@@ -260,8 +325,7 @@ __global__ void k_flag_nonzero(const uint32_t* __restrict__ mark, uint32_t k, ui
 // Each picked change makes a new Member (index.js:237-241), so its damp state restarts.
 __global__ void k_set_apply(const uint32_t* __restrict__ mark, const uint32_t* __restrict__ pos, uint32_t k,
                             const uint32_t* __restrict__ ids, const uint8_t* __restrict__ chs,
-                            const int64_t* __restrict__ chi, uint8_t* __restrict__ exists,
-                            uint8_t* __restrict__ status, int64_t* __restrict__ inc, uint32_t* __restrict__ pick,
+                            const int64_t* __restrict__ chi, MRow* __restrict__ rows, uint32_t* __restrict__ pick,
                             uint32_t* __restrict__ npick, DampArgs da) {
     const uint32_t gstride = gridDim.x * blockDim.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < k; i += gstride) {
@@ -269,9 +333,7 @@ __global__ void k_set_apply(const uint32_t* __restrict__ mark, const uint32_t* _
         const uint32_t m = mark[i];
         if (!m) continue;
         const uint32_t j = m - 1u, id = ids[j];
-        exists[id] = 1;
-        status[id] = chs[j];
-        inc[id] = chi[j];
+        row_store(rows + id, chi[j], chs[j], 1);
         if (da.score) {
             da.score[id] = da.last[id] = da.c.initial;
             da.ts[id] = 0;
@@ -281,41 +343,6 @@ __global__ void k_set_apply(const uint32_t* __restrict__ mark, const uint32_t* _
 }
 
 // generateChecksumString pieces (index.js:115-120): address + status + incarnation + ';'
-__global__ void k_mck_len(const uint32_t* __restrict__ order, uint32_t n, const uint8_t* __restrict__ exists,
-                          const uint8_t* __restrict__ status, const int64_t* __restrict__ inc,
-                          const uint64_t* __restrict__ noff, const uint32_t* __restrict__ gate,
-                          uint32_t* __restrict__ len) {
-    if (gate && *gate == 0) return;
-    const uint32_t gstride = gridDim.x * blockDim.x;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gstride) {
-        const uint32_t id = order[i];
-        len[i] = exists[id] ? (uint32_t)(noff[id + 1] - noff[id]) + status_len(status[id]) + dec_len(inc[id]) + 1u : 0u;
-    }
-}
-
-__global__ void k_mck_write(const uint32_t* __restrict__ order, uint32_t n, const uint8_t* __restrict__ exists,
-                            const uint8_t* __restrict__ status, const int64_t* __restrict__ inc,
-                            const uint8_t* __restrict__ names, const uint64_t* __restrict__ noff,
-                            const uint32_t* __restrict__ pos, const uint32_t* __restrict__ gate,
-                            uint8_t* __restrict__ buf) {
-    if (gate && *gate == 0) return;
-    const uint32_t gstride = gridDim.x * blockDim.x;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gstride) {
-        const uint32_t id = order[i];
-        if (!exists[id]) continue;
-        uint8_t* o = buf + pos[i];
-        const uint64_t b = noff[id];
-        const uint32_t L = (uint32_t)(noff[id + 1] - b);
-        for (uint32_t q = 0; q < L; q++) *o++ = names[b + q];
-        const uint8_t st = status[id];
-        const uint32_t sl = status_len(st);
-        for (uint32_t q = 0; q < sl; q++) *o++ = status_char(st, q);
-        const uint32_t dl = dec_len(inc[id]);
-        dec_write(inc[id], o, dl);
-        o[dl] = ';';
-    }
-}
-
 // The checksum string in one launch (round 2): a tile of 256 x kMckItems members in address
 // order computes its pieces' lengths, finds its byte offset by decoupled look-back over the
 // tiles (rp_prims.h), and writes its pieces; the last tile records the slot's meta. This
@@ -329,22 +356,17 @@ static bool getenv_on(const char* name) {
 }
 template <int kMckItems>
 __global__ __launch_bounds__(256) void k_mck_build(const uint32_t* __restrict__ order, uint32_t n,
-                                                   const uint8_t* __restrict__ exists, const uint8_t* __restrict__ status,
-                                                   const int64_t* __restrict__ inc, const uint8_t* __restrict__ names,
+                                                   const MRow* __restrict__ rows, const uint8_t* __restrict__ names,
                                                    const uint64_t* __restrict__ noff, const uint32_t* __restrict__ gate,
                                                    uint8_t* __restrict__ buf, uint32_t* __restrict__ meta, uint64_t* lb,
-                                                   unsigned long long* ctr, unsigned long long tbase, uint64_t tag,
-                                                   uint32_t ntiles) {
-    __shared__ uint32_t s_tile, s_gate, s_excl;
+                                                   unsigned long long* ctr, uint64_t tag, uint32_t ntiles,
+                                                   uint32_t* err) {
+    __shared__ uint32_t s_gate, s_excl;
     __shared__ uint32_t s_wsum[4];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    if (tid == 0) {
-        s_tile = (uint32_t)(atomicAdd(ctr, 1ull) - tbase);
-        s_gate = gate ? *gate : 1u;
-    }
-    __syncthreads();
-    const uint32_t tile = s_tile;
-    if (tile >= ntiles) return;  // a ticket count out of step: never write out of bounds
+    if (tid == 0) s_gate = gate ? *gate : 1u;
+    const uint32_t tile = take_unit(ctr, ntiles, err);  // (syncs)
+    if (tile >= ntiles) return;  // a ticket count out of step (reported): never write out of bounds
     if (!s_gate) {
         if (tile == 0 && tid == 0) {
             meta[0] = 0;
@@ -355,13 +377,15 @@ __global__ __launch_bounds__(256) void k_mck_build(const uint32_t* __restrict__ 
     }
     const uint32_t i0 = tile * (256u * kMckItems) + (uint32_t)tid * kMckItems;
     uint32_t ids[kMckItems], len[kMckItems];
+    MRow row[kMckItems];
     uint32_t sum = 0;
 #pragma unroll
     for (int j = 0; j < kMckItems; j++) {
         const uint32_t i = i0 + j;
         ids[j] = i < n ? order[i] : 0u;
-        len[j] = (i < n && exists[ids[j]])
-                     ? (uint32_t)(noff[ids[j] + 1] - noff[ids[j]]) + status_len(status[ids[j]]) + dec_len(inc[ids[j]]) + 1u
+        row[j] = row_load(rows + ids[j]);
+        len[j] = (i < n && row[j].exists)
+                     ? (uint32_t)(noff[ids[j] + 1] - noff[ids[j]]) + status_len(row[j].status) + dec_len(row[j].inc) + 1u
                      : 0u;
         sum += len[j];
     }
@@ -382,7 +406,7 @@ __global__ __launch_bounds__(256) void k_mck_build(const uint32_t* __restrict__ 
     }
     if (tid == 0) lb_store(lb + tile, tag | (tile == 0 ? kLbP : kLbA) | total);
     if (tid < 64) {
-        const uint32_t excl = lookback_wave(lb, tile, tag);
+        const uint32_t excl = lookback_wave(lb, tile, tag, err);
         if (tid == 0) {
             if (tile > 0) lb_store(lb + tile, tag | kLbP | (excl + total));
             s_excl = excl;
@@ -403,24 +427,15 @@ __global__ __launch_bounds__(256) void k_mck_build(const uint32_t* __restrict__ 
             const uint64_t b = noff[id];
             const uint32_t L = (uint32_t)(noff[id + 1] - b);
             for (uint32_t q = 0; q < L; q++) *o++ = names[b + q];
-            const uint8_t st = status[id];
+            const uint8_t st = row[j].status;
             const uint32_t sl = status_len(st);
             for (uint32_t q = 0; q < sl; q++) *o++ = status_char(st, q);
-            const uint32_t dl = dec_len(inc[id]);
-            dec_write(inc[id], o, dl);
+            const uint32_t dl = dec_len(row[j].inc);
+            dec_write(row[j].inc, o, dl);
             o[dl] = ';';
         }
         pos += len[j];
     }
-}
-
-// a pending checksum slot's total (string length + 1) and gate value, captured at build time
-__global__ void k_slot_meta(const uint32_t* __restrict__ total, const uint32_t* __restrict__ gate,
-                            uint32_t* __restrict__ meta) {
-    const uint32_t g = gate ? *gate : 1u;
-    meta[0] = g ? *total : 0u;
-    meta[1] = g;
-    meta[3] = 0;
 }
 
 // the group's results in batch order: the membership checksum is the last gated batch's hash
@@ -432,14 +447,15 @@ __global__ void k_ck_commit(const uint32_t* __restrict__ meta, uint32_t n, uint3
         }
 }
 
-__global__ void k_copy_grow(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b,
-                            const int64_t* __restrict__ c, uint32_t n, uint8_t* __restrict__ a2,
-                            uint8_t* __restrict__ b2, int64_t* __restrict__ c2, uint32_t n2) {
+// the table's rows as the host API returns them (rp_members_dump): exists, status, incarnation
+__global__ void k_rows_split(const MRow* __restrict__ rows, uint32_t n, uint8_t* __restrict__ ex,
+                             uint8_t* __restrict__ st, int64_t* __restrict__ inc) {
     const uint32_t gstride = gridDim.x * blockDim.x;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += gstride) {
-        a2[i] = i < n ? a[i] : 0;
-        b2[i] = i < n ? b[i] : 0;
-        c2[i] = i < n ? c[i] : 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gstride) {
+        const MRow r = row_load(rows + i);
+        ex[i] = r.exists;
+        st[i] = r.status;
+        inc[i] = r.inc;
     }
 }
 
@@ -452,10 +468,11 @@ struct Members {
     uint32_t local_id = 0xFFFFFFFFu;
     uint32_t cap = 0;
     bool defer_ck = false;  // rp_members_defer_checksum
-    DevBuf<uint8_t> exists, status;
-    DevBuf<int64_t> inc;
+    DevBuf<MRow> rows;          // the member table, one 16-B row per id
     DevBuf<uint32_t> ck;        // [0] checksum, [1] is_set
-    DevBuf<uint32_t> napplied;  // per-batch applied count (the checksum gate)
+    // [0] per-batch applied count (the checksum gate), [1] the grouped path overflowed (cleared
+    // by the sorted fold that then runs), [2..) the launches' last-workgroup counters
+    DevBuf<uint32_t> napplied;
     // Checksum strings wait in slots until read or until a group of slots is pending, then one
     // launch hashes the group side by side (one serial chain per workgroup): a batched caller
     // pays one chain's latency per group instead of per batch. The slots form ngroups groups
@@ -480,18 +497,12 @@ struct Members {
     uint32_t slot_index(uint32_t j) const { return cur_group * group_slots + j; }
     DevBuf<uint32_t> ck_len, ck_pos;
     DevBuf<uint32_t> sk, sv;
-    // the grouped (sort-free) fold: per id change count and list head, per change list link
-    // (RP_MEMBERS_SORTED_FOLD=1 always sorts)
-    bool grouped_fold = [] {
-        const char* e = getenv("RP_MEMBERS_SORTED_FOLD");
-        return !(e && *e && *e != '0');
-    }();
-    DevBuf<uint32_t> g_cnt, g_head, g_nxt;
-    uint32_t g_cap = 0;
-    uint32_t grouped_max = [] {  // RP_MEMBERS_GROUPED_MAX overrides kGroupedMaxBatch (A/B)
-        const char* e = getenv("RP_MEMBERS_GROUPED_MAX");
-        return e && *e ? (uint32_t)strtoul(e, nullptr, 10) : kGroupedMaxBatch;
-    }();
+    // the grouped (sort-free) fold: per id inline slots for repeated addresses, per change its
+    // rank among its address's changes (RP_MEMBERS_SORTED_FOLD=1 always sorts)
+    bool grouped_fold = !getenv_on("RP_MEMBERS_SORTED_FOLD");
+    DevBuf<uint32_t> g_slots;
+    DevBuf<uint8_t> g_rk;
+    DevBuf<uint32_t> g_part;  // per-workgroup applied counts of k_fold_fast
     DevBuf<uint32_t> mk, mpos;  // set: merge marks and their positions
     // host-buffer staging
     DevBuf<uint32_t> io_ids, io_pick;
@@ -536,18 +547,7 @@ struct Members {
     void grow(uint32_t need) {
         if (need <= cap) return;
         uint32_t nc = std::max<uint32_t>(need, cap ? cap * 2 : 1024);
-        DevBuf<uint8_t> e2, s2;
-        DevBuf<int64_t> i2;
-        e2.reserve(nc);
-        s2.reserve(nc);
-        i2.reserve(nc);
-        hipLaunchKernelGGL(k_copy_grow, dim3(grid_for(nc, 256)), dim3(256), 0, st, exists.p, status.p, inc.p, cap,
-                           e2.p, s2.p, i2.p, nc);
-        RP_HIP(hipGetLastError());
-        RP_HIP(hipStreamSynchronize(st));
-        exists.swap(e2);
-        status.swap(s2);
-        inc.swap(i2);
+        grow_one<MRow>(rows, cap, nc, MRow{0, 0, 0, 0, 0});
         if (damp_on) {
             grow_one<double>(d_score, cap, nc, dcfg.initial);
             grow_one<double>(d_last, cap, nc, dcfg.initial);
@@ -572,53 +572,50 @@ struct Members {
     }
 
     // Everything below is stream-ordered on `s` and never syncs with the host.
+    // Grouped path (every batch size): k_link + k_fold_fast; then the sorted path's launches,
+    // gated on the overflow word on the device (they exit at once unless an address had more
+    // than kSlots + 1 changes). The applied count goes to n_applied_out from the last workgroup
+    // of whichever fold ran.
     void update_dev(const uint32_t* ids, const uint8_t* chs, const int64_t* chi, uint32_t k, int64_t now_ms,
                     uint8_t* applied, uint8_t* nst, int64_t* ninc, uint32_t* n_applied_out, hipStream_t s) {
         if (s != st) RP_HIP(hipStreamSynchronize(st));
-        // napplied[0]: applied count (the checksum gate); [1]: the grouped path overflowed
-        RP_HIP(hipMemsetAsync(napplied.p, 0, 2 * sizeof(uint32_t), s));
-        if (k) {
-            if (damp_on) {
-                d_out.reserve(k);
-                d_exc.reserve(k);
-                d_out_k = k;
-            }
-            const FoldArgs A{chs, chi, exists.p, status.p, inc.p, local_id, now_ms, applied, nst, ninc, napplied.p,
-                             damp_args(true)};
-            int bits = 8;
-            while (bits < 32 && (1ull << bits) < nt.size()) bits += 8;
-            sk.reserve(k);
-            sv.reserve(k);
-            const unsigned g = grid_for(k, 256);
-            if (grouped_fold && k < grouped_max && single_pass_sort(k)) {
-                // no sort unless some address has more than kGroupMax changes in the batch; then
-                // the sorted path runs instead (its launches are gated on the overflow word)
-                if (g_cap < cap) {
-                    g_cnt.release();
-                    g_head.release();
-                    g_cnt.reserve(cap);
-                    g_head.reserve(cap);
-                    RP_HIP(hipMemsetAsync(g_cnt.p, 0, 4ull * cap, s));
-                    RP_HIP(hipMemsetAsync(g_head.p, 0xFF, 4ull * cap, s));
-                    g_cap = cap;
-                }
-                g_nxt.reserve(k);
-                uint32_t* ovf = napplied.p + 1;
-                hipLaunchKernelGGL(k_group_link, dim3(g), dim3(256), 0, s, ids, k, g_cnt.p, g_head.p, g_nxt.p, ovf);
-                hipLaunchKernelGGL(k_fold_grouped, dim3(g), dim3(256), 0, s, ids, k, g_cnt.p, g_head.p, g_nxt.p, ovf,
-                                   A);
-                RP_HIP(hipGetLastError());
-                radix_sort_index(ids, sk.p, sv.p, k, 0, bits, s, ws, ovf);
-                hipLaunchKernelGGL(k_fold, dim3(g), dim3(256), 0, s, sk.p, sv.p, k, A, ovf, g_cnt.p, g_head.p);
-            } else {
-                radix_sort_index(ids, sk.p, sv.p, k, 0, bits, s, ws);
-                hipLaunchKernelGGL(k_fold, dim3(g), dim3(256), 0, s, sk.p, sv.p, k, A, nullptr);
-            }
-            RP_HIP(hipGetLastError());
-            if (!defer_ck) checksum_dev(s, napplied.p);
+        if (!k) {
+            RP_HIP(hipMemsetAsync(napplied.p, 0, sizeof(uint32_t), s));
+            if (n_applied_out) RP_HIP(hipMemsetAsync(n_applied_out, 0, sizeof(uint32_t), s));
+            return;
         }
-        if (n_applied_out)
-            RP_HIP(hipMemcpyAsync(n_applied_out, napplied.p, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+        if (damp_on) {
+            d_out.reserve(k);
+            d_exc.reserve(k);
+            d_out_k = k;
+        }
+        const FoldArgs A{chs, chi, rows.p, local_id, now_ms, applied, nst, ninc, napplied.p, damp_args(true)};
+        int bits = 8;
+        while (bits < 32 && (1ull << bits) < nt.size()) bits += 8;
+        sk.reserve(k);
+        sv.reserve(k);
+        uint32_t* ovf = napplied.p + 1;
+        uint32_t* done = napplied.p + 2;
+        const unsigned g = grid_for(k, 256);
+        if (grouped_fold) {
+            g_slots.reserve((uint64_t)cap * kSlots);
+            g_rk.reserve(k);
+            const unsigned g1 = (unsigned)((k + 255) / 256);
+            g_part.reserve(g1);
+            hipLaunchKernelGGL(k_link, dim3(g1), dim3(256), 0, s, ids, k, rows.p, g_slots.p, g_rk.p, ovf, napplied.p);
+            hipLaunchKernelGGL(k_fold_fast, dim3(g1), dim3(256), 0, s, ids, k, g_rk.p, g_slots.p, ovf, A, g_part.p);
+            RP_HIP(hipGetLastError());
+            radix_sort_index(ids, sk.p, sv.p, k, 0, bits, s, ws, ovf);
+            hipLaunchKernelGGL(k_fold, dim3(g), dim3(256), 0, s, sk.p, sv.p, k, A, ovf, done + 1, n_applied_out,
+                               g_part.p, g1);
+        } else {
+            RP_HIP(hipMemsetAsync(napplied.p, 0, sizeof(uint32_t), s));
+            radix_sort_index(ids, sk.p, sv.p, k, 0, bits, s, ws);
+            hipLaunchKernelGGL(k_fold, dim3(g), dim3(256), 0, s, sk.p, sv.p, k, A, nullptr, done + 1, n_applied_out,
+                               nullptr, 0u);
+        }
+        RP_HIP(hipGetLastError());
+        if (!defer_ck) checksum_dev(s, napplied.p);
     }
 
     // Membership.set over a stash of k changes (arrival order): merge, set, checksum once.
@@ -641,7 +638,7 @@ struct Members {
         hipLaunchKernelGGL(k_flag_nonzero, dim3(grid_for(k, 256)), dim3(256), 0, s, mk.p, k, mpos.p);
         scan_exclusive_u32(mpos.p, mpos.p, k, s, ws);
         hipLaunchKernelGGL(k_set_apply, dim3(grid_for(k, 256)), dim3(256), 0, s, mk.p, mpos.p, k, ids, chs, chi,
-                           exists.p, status.p, inc.p, pick, npick, damp_args(false));
+                           rows.p, pick, npick, damp_args(false));
         RP_HIP(hipGetLastError());
         checksum_dev(s, nullptr);
     }
@@ -670,11 +667,9 @@ struct Members {
             for (auto& b : group_busy) b = false;
             cur_group = 0;
             ck_buf.release();
-            const char* e = getenv("RP_MEMBERS_CK_BYTES");
-            const uint64_t budget = e && *e ? strtoull(e, nullptr, 10) : (1ull << 30);
+            const uint64_t budget = env_pos("RP_MEMBERS_CK_BYTES", 1ull << 30);
             nslots = (uint32_t)std::min<uint64_t>(kMaxSlots, std::max<uint64_t>(1, budget / need));
-            const char* gs = getenv("RP_MEMBERS_GROUP_SLOTS");  // A/B: chains per group launch
-            const uint32_t gmax = gs && *gs ? (uint32_t)strtoul(gs, nullptr, 10) : kGroupSlots;
+            const uint32_t gmax = (uint32_t)env_pos("RP_MEMBERS_GROUP_SLOTS", kGroupSlots);  // A/B: chains per launch
             group_slots = std::max<uint32_t>(1, std::min<uint32_t>(gmax, nslots / 2));
             ngroups = std::max<uint32_t>(1, std::min<uint32_t>(kMaxGroups, nslots / group_slots));
             ck_buf.reserve(need * (uint64_t)group_slots * ngroups);
@@ -688,25 +683,16 @@ struct Members {
         pend_st = s;
         ck_meta.reserve(4 * kMaxSlots);
         uint8_t* buf = ck_buf.p + slot_bytes * slot_index(npending);
-        if (getenv_on("RP_MEMBERS_CK3")) {  // A/B: the three-launch build (lengths, scan, write)
-            hipLaunchKernelGGL(k_mck_len, dim3(grid_for(n, 256)), dim3(256), 0, s, nt.sorted.p, n, exists.p,
-                               status.p, inc.p, nt.d_noff.p, gate, ck_len.p);
-            RP_HIP(hipGetLastError());
-            scan_exclusive_u32(ck_len.p, ck_pos.p, n, s, ws);
-            hipLaunchKernelGGL(k_mck_write, dim3(grid_for(n, 256)), dim3(256), 0, s, nt.sorted.p, n, exists.p,
-                               status.p, inc.p, nt.d_bytes.p, nt.d_noff.p, ck_pos.p, gate, buf);
-            hipLaunchKernelGGL(k_slot_meta, dim3(1), dim3(1), 0, s, ck_pos.p + n, gate,
-                               ck_meta.p + 4ull * slot_index(npending));
-        } else {
+        {
             const char* it = getenv("RP_MEMBERS_CK_ITEMS");  // A/B: members per thread
             const int items = it && *it ? atoi(it) : 1;
             const uint32_t per = 256u * (items == 2 ? 2u : items == 4 ? 4u : 1u);
             const uint32_t ntl = (uint32_t)((n + per - 1) / per);
-            const LookBack L = lookback_prepare(ws, ntl, 0, s);
-#define RP_MCK(I)                                                                                               \
-    hipLaunchKernelGGL((k_mck_build<I>), dim3(ntl), dim3(256), 0, s, nt.sorted.p, n, exists.p, status.p, inc.p, \
-                       nt.d_bytes.p, nt.d_noff.p, gate, buf, ck_meta.p + 4ull * slot_index(npending), L.words,   \
-                       L.ticket, L.tbase, L.tag, ntl)
+            const LookBack L = lookback_prepare(ws, ntl, s);
+#define RP_MCK(I)                                                                                              \
+    hipLaunchKernelGGL((k_mck_build<I>), dim3(ntl), dim3(256), 0, s, nt.sorted.p, n, rows.p, nt.d_bytes.p,     \
+                       nt.d_noff.p, gate, buf, ck_meta.p + 4ull * slot_index(npending), L.words, L.ticket, L.tag,  \
+                       ntl, L.err)
             if (items == 2)
                 RP_MCK(2);
             else if (items == 4)
@@ -797,8 +783,9 @@ int rp_members_create(uint32_t capacity, int device, rp_members** out) {
             throw rp::Error(rp::RP_EDEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(e));
         }
         m.ck.reserve(2);
-        m.napplied.reserve(2);
+        m.napplied.reserve(2 + rp::kDoneWords);
         RP_HIP(hipMemsetAsync(m.ck.p, 0, 2 * sizeof(uint32_t), m.st));
+        RP_HIP(hipMemsetAsync(m.napplied.p, 0, (2 + rp::kDoneWords) * sizeof(uint32_t), m.st));
         m.grow(capacity ? capacity : 1024);
         RP_HIP(hipStreamSynchronize(m.st));
         *out = h;
@@ -874,6 +861,7 @@ int rp_members_update(rp_members* h, const uint32_t* ids, const uint8_t* status,
         uint32_t na = 0;
         RP_HIP(hipMemcpyAsync(&na, m.napplied.p, 4, hipMemcpyDeviceToHost, m.st));
         RP_HIP(hipStreamSynchronize(m.st));
+        rp::scratch_check(m.ws, m.st);
         if (n_applied) *n_applied = na;
     });
 }
@@ -907,6 +895,7 @@ int rp_members_set(rp_members* h, const uint32_t* ids, const uint8_t* status, co
         uint32_t np = 0;
         RP_HIP(hipMemcpyAsync(&np, m.io_pick.p + kk, 4, hipMemcpyDeviceToHost, m.st));
         RP_HIP(hipStreamSynchronize(m.st));
+        rp::scratch_check(m.ws, m.st);
         if (pick && np) RP_HIP(hipMemcpy(pick, m.io_pick.p, 4ull * np, hipMemcpyDeviceToHost));
         if (npick) *npick = np;
     });
@@ -919,6 +908,7 @@ int rp_members_checksum(rp_members* h, uint32_t* out, int* is_set) {
         uint32_t v[2];
         RP_HIP(hipMemcpyAsync(v, m.ck.p, sizeof v, hipMemcpyDeviceToHost, m.st));
         RP_HIP(hipStreamSynchronize(m.st));
+        rp::scratch_check(m.ws, m.st);
         if (out) *out = v[0];
         if (is_set) *is_set = v[1] ? 1 : 0;
     });
@@ -965,9 +955,18 @@ int rp_members_dump(rp_members* h, uint8_t* exists, uint8_t* status, int64_t* in
         rp::Members& m = MB(h);
         const uint32_t n = std::min(cap, m.nt.size());
         if (n) {
-            if (exists) RP_HIP(hipMemcpyAsync(exists, m.exists.p, n, hipMemcpyDeviceToHost, m.st));
-            if (status) RP_HIP(hipMemcpyAsync(status, m.status.p, n, hipMemcpyDeviceToHost, m.st));
-            if (inc) RP_HIP(hipMemcpyAsync(inc, m.inc.p, 8ull * n, hipMemcpyDeviceToHost, m.st));
+            rp::DevBuf<uint8_t> de, ds;
+            rp::DevBuf<int64_t> di;
+            de.reserve(n);
+            ds.reserve(n);
+            di.reserve(n);
+            hipLaunchKernelGGL(rp::k_rows_split, dim3(rp::grid_for(n, 256)), dim3(256), 0, m.st, m.rows.p, n, de.p,
+                               ds.p, di.p);
+            RP_HIP(hipGetLastError());
+            if (exists) RP_HIP(hipMemcpyAsync(exists, de.p, n, hipMemcpyDeviceToHost, m.st));
+            if (status) RP_HIP(hipMemcpyAsync(status, ds.p, n, hipMemcpyDeviceToHost, m.st));
+            if (inc) RP_HIP(hipMemcpyAsync(inc, di.p, 8ull * n, hipMemcpyDeviceToHost, m.st));
+            RP_HIP(hipStreamSynchronize(m.st));
         }
         RP_HIP(hipStreamSynchronize(m.st));
     });
@@ -1007,7 +1006,7 @@ int rp_members_damp_decay_dev(rp_members* h, int64_t now_ms, void* stream) {
         if (s != m.st) RP_HIP(hipStreamSynchronize(m.st));
         const uint32_t n = m.nt.size();
         if (n)
-            hipLaunchKernelGGL(rp::k_damp_decay, dim3(rp::grid_for(n, 256)), dim3(256), 0, s, m.exists.p, n,
+            hipLaunchKernelGGL(rp::k_damp_decay, dim3(rp::grid_for(n, 256)), dim3(256), 0, s, m.rows.p, n,
                                m.d_score.p, m.d_last.p, m.d_ts.p, m.dcfg, now_ms);
         RP_HIP(hipGetLastError());
     });

@@ -186,17 +186,10 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(const uint32_t* __re
 // prefix (flag P), then publish their own P. A look-back word is
 // [epoch:30 | flag:2 | value:32]; agent-scope atomics bypass the per-XCD L2s. Words from an
 // earlier launch carry another epoch and read as "not ready", so the array is never cleared.
-__device__ __forceinline__ uint32_t take_ticket(unsigned long long* ctr, unsigned long long base) {
-    __shared__ uint32_t s_t;
-    if (threadIdx.x == 0) s_t = (uint32_t)(atomicAdd(ctr, 1ull) - base);
-    __syncthreads();
-    return s_t;
-}
-
 // The exclusive prefix of `tile` for the word column `col` (stride words per tile), by one
 // thread: kLbWin predecessor words per step, back to the nearest P.
 __device__ uint32_t lookback_thread(const uint64_t* lb, uint32_t tile, uint32_t stride, uint32_t col,
-                                    uint64_t tag) {
+                                    uint64_t tag, uint32_t* err) {
     uint32_t excl = 0;
     int64_t t = (int64_t)tile - 1;
     while (t >= 0) {
@@ -208,10 +201,12 @@ __device__ uint32_t lookback_thread(const uint64_t* lb, uint32_t tile, uint32_t 
         bool done = false;
         int q = 0;
         for (; q < m; q++) {
-            for (uint32_t spin = 0; !lb_ready(v[q], tag) && spin < kLbSpinCap; spin++) {
+            uint32_t spin = 0;
+            for (; !lb_ready(v[q], tag) && spin < kLbSpinCap; spin++) {
                 __builtin_amdgcn_s_sleep(1);
                 v[q] = lb_load(lb + (uint64_t)(t - q) * stride + col);
             }
+            if (spin == kLbSpinCap) atomicOr(err, kErrSpin);
             excl += (uint32_t)v[q];
             if (v[q] & kLbP) {
                 done = true;
@@ -287,7 +282,7 @@ __global__ __launch_bounds__(kThreads) void k_os_scatter(const uint32_t* __restr
                                                          uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                          uint32_t n, int shift, const uint32_t* __restrict__ dbase,
                                                          uint64_t* __restrict__ lb, unsigned long long* ctr,
-                                                         unsigned long long tbase, uint64_t tag,
+                                                         uint32_t ntiles, uint64_t tag, uint32_t* err,
                                                          const uint32_t* __restrict__ run_if) {
     constexpr int kOsTile = kThreads * kOsItems;
     constexpr int kOsWave = kOsTile / (kThreads / 64);
@@ -300,9 +295,9 @@ __global__ __launch_bounds__(kThreads) void k_os_scatter(const uint32_t* __restr
     const bool has_v = IOTA || vin != nullptr;
 #pragma unroll
     for (int w = 0; w < kThreads / 64; w++) wcnt[w][tid] = 0;
-    const uint32_t tile = take_ticket(ctr, tbase);  // (syncs; taken even when skipping)
-    if (run_if && *run_if == 0) return;
-    if ((uint64_t)tile * kOsTile >= n) return;  // a ticket count out of step: never write out of bounds
+    if (run_if && *run_if == 0) return;  // (the whole launch: no tickets taken)
+    const uint32_t tile = take_unit(ctr, ntiles, err);  // (syncs)
+    if (tile >= ntiles) return;  // a ticket count out of step (reported): never write out of bounds
     const uint32_t t0 = tile * (uint32_t)kOsTile;
     const uint32_t w0 = t0 + (uint32_t)(wave * kOsWave);
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -344,7 +339,7 @@ __global__ __launch_bounds__(kThreads) void k_os_scatter(const uint32_t* __restr
     uint32_t tot;
     lstart[tid] = block_exclusive_scan(cnt, lds, &tot);  // (syncs)
     if (tile > 0) {
-        const uint32_t excl = lookback_thread(lb, tile, 256, (uint32_t)tid, tag);
+        const uint32_t excl = lookback_thread(lb, tile, 256, (uint32_t)tid, tag, err);
         lb_store(mine, tag | kLbP | (excl + cnt));
         gbase[tid] = dbase[tid] + excl;
     } else {
@@ -374,12 +369,12 @@ __global__ __launch_bounds__(kThreads) void k_os_scatter(const uint32_t* __restr
 // prefixes by a wave-wide look-back (64 predecessor words per step).
 __global__ __launch_bounds__(kThreads) void k_os_scan(const uint32_t* in, uint32_t* out, uint32_t n,
                                                       uint64_t* __restrict__ lb, unsigned long long* ctr,
-                                                      unsigned long long tbase, uint64_t tag, uint32_t ntiles) {
+                                                      uint64_t tag, uint32_t ntiles, uint32_t* err) {
     __shared__ uint32_t lds[kThreads + 1];
     __shared__ uint32_t s_excl;
     const int tid = threadIdx.x;
-    const uint32_t tile = take_ticket(ctr, tbase);
-    if (tile >= ntiles) return;  // a ticket count out of step: never write out of bounds
+    const uint32_t tile = take_unit(ctr, ntiles, err);
+    if (tile >= ntiles) return;  // a ticket count out of step (reported): never write out of bounds
     const uint64_t base = (uint64_t)tile * kTile + (uint64_t)tid * kItems;
     uint32_t v[kItems];
     uint32_t s = 0;
@@ -393,7 +388,7 @@ __global__ __launch_bounds__(kThreads) void k_os_scan(const uint32_t* in, uint32
     uint32_t ex = block_exclusive_scan(s, lds, &total);
     if (tid == 0) lb_store(lb + tile, tag | (tile == 0 ? kLbP : kLbA) | total);
     if (tid < 64) {
-        const uint32_t excl = lookback_wave(lb, tile, tag);
+        const uint32_t excl = lookback_wave(lb, tile, tag, err);
         if (tid == 0) {
             if (tile > 0) lb_store(lb + tile, tag | kLbP | (excl + total));
             s_excl = excl;
@@ -440,12 +435,14 @@ namespace {
 }  // namespace
 
 // Look-back state for one single-pass launch of `tiles` tiles with `cols` words each: returns
-// the launch's epoch tag and the ticket base, and advances the host mirrors.
-uint64_t lb_begin(Scratch& ws, uint64_t tiles, uint32_t cols, hipStream_t st, unsigned long long* tbase) {
+// the launch's epoch tag (the ticket counter is 0 between launches).
+uint64_t lb_begin(Scratch& ws, uint64_t tiles, uint32_t cols, hipStream_t st) {
+    ws.use_on(st);
     if (!ws.ticket.p) {
         ws.ticket.reserve(1);
+        ws.err.reserve(1);
         RP_HIP(hipMemsetAsync(ws.ticket.p, 0, sizeof(unsigned long long), st));
-        ws.tickets = 0;
+        RP_HIP(hipMemsetAsync(ws.err.p, 0, sizeof(uint32_t), st));
     }
     const uint64_t words = tiles * cols;
     bool zero = false;
@@ -459,19 +456,33 @@ uint64_t lb_begin(Scratch& ws, uint64_t tiles, uint32_t cols, hipStream_t st, un
         zero = true;
     }
     if (zero) RP_HIP(hipMemsetAsync(ws.lb.p, 0, ws.lb.cap * sizeof(uint64_t), st));
-    *tbase = ws.tickets;
-    ws.tickets += tiles;
     return (uint64_t)ws.epoch << kLbEpochShift;
 }
 
-LookBack lookback_prepare(Scratch& ws, uint64_t units, uint64_t extra_tickets, hipStream_t st) {
+LookBack lookback_prepare(Scratch& ws, uint64_t units, hipStream_t st) {
     LookBack L{};
-    RP_REQUIRE(units > 0, "lookback_prepare: no units");
-    L.tag = lb_begin(ws, units, 1, st, &L.tbase);
-    ws.tickets += extra_tickets;  // tickets the launch takes beyond one per unit
+    RP_REQUIRE(units > 0 && units < (1ull << 32), "lookback_prepare: units");
+    L.tag = lb_begin(ws, units, 1, st);
     L.words = ws.lb.p;
     L.ticket = ws.ticket.p;
+    L.err = ws.err.p;
     return L;
+}
+
+void scratch_check(Scratch& ws, hipStream_t st) {
+    if (!ws.err.p) return;
+    uint32_t e = 0;
+    RP_HIP(hipMemcpyAsync(&e, ws.err.p, sizeof e, hipMemcpyDeviceToHost, st));
+    RP_HIP(hipStreamSynchronize(st));
+    if (e) {
+        RP_HIP(hipMemsetAsync(ws.err.p, 0, sizeof(uint32_t), st));
+        RP_HIP(hipStreamSynchronize(st));
+        throw Error(RP_EDEVICE, std::string("device primitive reported a broken ordering (") +
+                                    (e & kErrSpin ? "look-back wait gave up" : "") +
+                                    (e == (kErrSpin | kErrTicket) ? ", " : "") +
+                                    (e & kErrTicket ? "ticket past the launch's tiles" : "") +
+                                    "): results of the last calls on this handle are not valid");
+    }
 }
 
 namespace {
@@ -523,15 +534,14 @@ void os_sort(const uint32_t* kin0, const uint32_t* vin0, bool iota, uint32_t* ke
     const uint32_t* kin = kin0;
     const uint32_t* vin = vin0;
     for (int p = 0; p < npass; p++) {
-        unsigned long long tb;
-        const uint64_t tag = lb_begin(ws, tiles, 256, st, &tb);
+        const uint64_t tag = lb_begin(ws, tiles, 256, st);
         RP_REQUIRE(dk[p] != kin, "radix sort: pass writes its input");
         const bool io = p == 0 && iota;
         auto kern = io ? (items == 16 ? k_os_scatter<true, 16> : k_os_scatter<true, 8>)
                        : (items == 16 ? k_os_scatter<false, 16> : k_os_scatter<false, 8>);
         hipLaunchKernelGGL(kern, dim3(tiles), dim3(kThreads), 0, st, kin, io ? nullptr : vin, dk[p], dv[p],
-                           (uint32_t)n, begin_bit + 8 * p, ws.dig.p + 1024 + 256 * p, ws.lb.p, ws.ticket.p, tb, tag,
-                           run_if);
+                           (uint32_t)n, begin_bit + 8 * p, ws.dig.p + 1024 + 256 * p, ws.lb.p, ws.ticket.p, tiles, tag,
+                           ws.err.p, run_if);
         RP_HIP(hipGetLastError());
         kin = dk[p];
         vin = dv[p];
@@ -556,6 +566,7 @@ bool single_pass_sort(uint64_t n) {
 }
 
 void scan_exclusive_u32(const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t st, Scratch& ws) {
+    ws.use_on(st);
     if (prims_multipass() || n == 0) {
         DevBuf<uint32_t>* lv[3] = {&ws.s0, &ws.s1, &ws.s2};
         scan_level(in, out, n, st, lv, 0);
@@ -563,10 +574,9 @@ void scan_exclusive_u32(const uint32_t* in, uint32_t* out, uint64_t n, hipStream
     }
     RP_REQUIRE(n < (1ull << 32), "scan_exclusive_u32: n must be < 2^32");
     const uint32_t tiles = (uint32_t)((n + kTile - 1) / kTile);
-    unsigned long long tb;
-    const uint64_t tag = lb_begin(ws, tiles, 1, st, &tb);
-    hipLaunchKernelGGL(k_os_scan, dim3(tiles), dim3(kThreads), 0, st, in, out, (uint32_t)n, ws.lb.p, ws.ticket.p, tb,
-                       tag, tiles);
+    const uint64_t tag = lb_begin(ws, tiles, 1, st);
+    hipLaunchKernelGGL(k_os_scan, dim3(tiles), dim3(kThreads), 0, st, in, out, (uint32_t)n, ws.lb.p, ws.ticket.p,
+                       tag, tiles, ws.err.p);
     RP_HIP(hipGetLastError());
 }
 
@@ -574,14 +584,14 @@ void radix_sort_index(const uint32_t* keys_in, uint32_t* keys_out, uint32_t* idx
                       int end_bit, hipStream_t st, Scratch& ws, const uint32_t* run_if) {
     if (n == 0) return;
     RP_REQUIRE(n < (1ull << 32), "radix_sort_index: n must be < 2^32");
+    ws.use_on(st);
     RP_REQUIRE(keys_in != keys_out, "radix_sort_index: keys_in must not be keys_out");
     if (n == 1) {  // (run regardless of run_if: harmless)
         RP_HIP(hipMemcpyAsync(keys_out, keys_in, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
         iota_u32(idx_out, 1, st);
         return;
     }
-    if (!single_pass_sort(n)) {
-        RP_REQUIRE(!run_if, "radix_sort_index: run_if needs the single-pass sort (single_pass_sort(n))");
+    if (!single_pass_sort(n) && !run_if) {  // (a gated sort always takes the single-pass kernels)
         RP_HIP(hipMemcpyAsync(keys_out, keys_in, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
         iota_u32(idx_out, n, st);
         radix_sort_pairs(keys_out, idx_out, n, begin_bit, end_bit, st, ws);
@@ -594,6 +604,7 @@ void radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint64_t n, int begin_bit,
                       hipStream_t st, Scratch& ws) {
     if (n <= 1) return;
     RP_REQUIRE(n < (1ull << 32), "radix_sort_pairs: n must be < 2^32");
+    ws.use_on(st);
     if (single_pass_sort(n)) {
         os_sort(keys, vals, false, keys, vals, n, begin_bit, end_bit, st, ws);
         return;

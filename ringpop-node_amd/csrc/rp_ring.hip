@@ -1372,6 +1372,7 @@ static void ring_compute_checksum(Ring& r) {
     uint32_t v[2];
     RP_HIP(hipMemcpyAsync(v, r.ck_out.p, sizeof v, hipMemcpyDeviceToHost, r.st));
     RP_HIP(hipStreamSynchronize(r.st));
+    scratch_check(r.ws, r.st);
     r.checksum = v[0];
     r.has_checksum = true;
 }
@@ -1448,8 +1449,7 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
         // workgroups, tiles strided over them: the lean kernel at 4096 (4 rounds of the 1024 that
         // fit, 8 tiles each at C2) ran 0.905-0.911 ms against 0.926-0.930 at 2048 (3072: 0.917;
         // 5120-16384: 0.908-0.914; profiles/r02/ab_lookup_grid.json). RP_LOOKUP_GRID overrides (A/B).
-        const unsigned g = grid_for(ntiles, 1, getenv("RP_LOOKUP_GRID") ? (unsigned)atoi(getenv("RP_LOOKUP_GRID"))
-                                                                        : (lean ? 4096u : 2048u));
+        const unsigned g = grid_for(ntiles, 1, (unsigned)env_pos("RP_LOOKUP_GRID", lean ? 4096u : 2048u));
         const int half = getenv("RP_LOOKUP_HALF") ? atoi(getenv("RP_LOOKUP_HALF")) : (kpl == 8 ? 4 : 0);
 #define RP_COMPACT(KPL, NEED)                                                                                  \
     do {                                                                                                        \

@@ -1358,7 +1358,7 @@ int rp_wire_encode_dev(rp_members* m, uint32_t n_msgs, const uint32_t* d_msg_rec
         if (d_out && n_rec) {
             hipLaunchKernelGGL(rp::k_rec_write_lds,
                                dim3(rp::grid_for(n_rec, rp::kWrThreads,
-                                                 getenv("RP_WIRE_WGRID") ? (unsigned)atoi(getenv("RP_WIRE_WGRID")) : 4096u)),
+                                                 (unsigned)rp::env_pos("RP_WIRE_WGRID", 4096u))),
                                dim3(rp::kWrThreads), 0, st, nm, R, M, n_msgs, n_rec, mscan.p, rscan.p, d_out);
             RP_HIP(hipGetLastError());
         }
@@ -1396,7 +1396,7 @@ int rp_wire_decode_dev(rp_members* m, const uint8_t* d_buf, const uint64_t* d_ms
             // a wave per message (3.73 ms at 100 k messages against 3.75-3.86 with 512-8192
             // workgroups striding; tools/wire_grid.sh); RP_WIRE_GRID caps it (A/B)
             const unsigned g = rp::grid_for(n_msgs, rp::kDecWaves,
-                                            getenv("RP_WIRE_GRID") ? (unsigned)atoi(getenv("RP_WIRE_GRID")) : 1u << 20);
+                                            (unsigned)rp::env_pos("RP_WIRE_GRID", 1u << 20));
             const uint64_t nslots = (ve - vb) / rp::kMinRec + n_msgs + 1;
             rp::DevBuf<rp::RecF> stash;
             rp::DevBuf<uint8_t> slow;
@@ -1418,6 +1418,7 @@ int rp_wire_decode_dev(rp_members* m, const uint8_t* d_buf, const uint64_t* d_ms
                                slow.p);
             RP_HIP(hipGetLastError());
             RP_HIP(hipStreamSynchronize(st));  // stash and slow are local
+            rp::scratch_check(*ws, st);
             if (dbg) {
                 uint32_t h = 0;
                 RP_HIP(hipMemcpy(&h, nbw.p, 4, hipMemcpyDeviceToHost));

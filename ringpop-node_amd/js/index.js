@@ -44,6 +44,10 @@ function HashRing(options) {
     this.device = this.options.device || 0;
     requireDevice(this.device);
     this._h = native.ringCreate(this.replicaPoints, this.device);
+    // servers (index.js:32): name -> true in insertion order, as the reference keeps it (its
+    // Object.keys order is getStats().servers). Host bookkeeping of the same add / remove
+    // decisions the device makes; every change is checked against the device's answer.
+    this.servers = {};
     this.checksum = null;
 }
 util.inherits(HashRing, EventEmitter);
@@ -68,10 +72,27 @@ HashRing.prototype._refreshChecksum = function _refreshChecksum() {
     this.emit('checksumComputed');
 };
 
+// The servers map after a batch (index.js:60-94: adds in order, then removes in order), and
+// whether it changed; the device must agree.
+HashRing.prototype._applyServers = function _applyServers(add, remove, deviceChanged) {
+    var changed = false;
+    for (var i = 0; i < add.length; i++) {
+        if (!this.servers[add[i]]) { this.servers[add[i]] = true; changed = true; }
+    }
+    for (var j = 0; j < remove.length; j++) {
+        if (this.servers[remove[j]]) { delete this.servers[remove[j]]; changed = true; }
+    }
+    if (changed !== !!deviceChanged) {
+        throw new Error('ringpop_amd: device ring and servers map disagree (ringChanged ' +
+            deviceChanged + ' vs ' + changed + ')');
+    }
+    return changed;
+};
+
 // addServer(name) — index.js:39-48
 HashRing.prototype.addServer = function addServer(name) {
     if (this.hasServer(name)) { return; }
-    native.ringAddRemove(this._h, [name], null, this._replicaTokens([name]), null);
+    this._applyServers([name], [], native.ringAddRemove(this._h, [name], null, this._replicaTokens([name]), null));
     this._refreshChecksum();
     this.emit('added', name);
 };
@@ -79,7 +100,7 @@ HashRing.prototype.addServer = function addServer(name) {
 // removeServer(name) — index.js:124-133
 HashRing.prototype.removeServer = function removeServer(name) {
     if (!this.hasServer(name)) { return; }
-    native.ringAddRemove(this._h, null, [name], null, this._replicaTokens([name]));
+    this._applyServers([], [name], native.ringAddRemove(this._h, null, [name], null, this._replicaTokens([name])));
     this._refreshChecksum();
     this.emit('removed', name);
 };
@@ -89,8 +110,9 @@ HashRing.prototype.removeServer = function removeServer(name) {
 HashRing.prototype.addRemoveServers = function addRemoveServers(serversToAdd, serversToRemove) {
     serversToAdd = serversToAdd || [];
     serversToRemove = serversToRemove || [];
-    var changed = native.ringAddRemove(this._h, serversToAdd, serversToRemove,
-        this._replicaTokens(serversToAdd), this._replicaTokens(serversToRemove));
+    var changed = this._applyServers(serversToAdd, serversToRemove,
+        native.ringAddRemove(this._h, serversToAdd, serversToRemove,
+            this._replicaTokens(serversToAdd), this._replicaTokens(serversToRemove)));
     if (changed) { this._refreshChecksum(); }
     return changed;
 };
@@ -101,16 +123,23 @@ HashRing.prototype.computeChecksum = function computeChecksum() {
     this._refreshChecksum();
 };
 
+// getServerCount / getStats / hasServer — index.js:107-120, over the servers map as the
+// reference reads them (no device round trip).
 HashRing.prototype.getServerCount = function getServerCount() {
-    return native.ringServerCount(this._h);
+    return Object.keys(this.servers).length;
 };
 
 HashRing.prototype.getStats = function getStats() {
-    return {checksum: this.checksum, servers: native.ringServers(this._h)};
+    return {checksum: this.checksum, servers: Object.keys(this.servers)};
 };
 
 HashRing.prototype.hasServer = function hasServer(name) {
-    return native.ringHasServer(this._h, name);
+    return !!this.servers[name];
+};
+
+// the device's own count / names (tests: coherence with the servers map)
+HashRing.prototype.deviceServerCount = function deviceServerCount() {
+    return native.ringServerCount(this._h);
 };
 
 // lookup(key) — index.js:145-154 (a batch of one; use lookupBatch for throughput).

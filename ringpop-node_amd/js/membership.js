@@ -60,7 +60,9 @@ function LocalMemberLeaveEvent(member, oldStatus) {
 LocalMemberLeaveEvent.Name = 'localMemberLeave';
 
 // Member (lib/membership/member.js:28-41): the JS object the rest of ringpop holds. Its state
-// is written from the device's verdicts; damp scoring (member.js:45-66, 133-153) stays here.
+// is written from the device's verdicts. With dampScoringEnabled the damp scores are the
+// device's too (rp_members_damp_*: the penalty folded with each update batch, the decayer
+// sweep); otherwise only lastUpdateTimestamp moves, as in the reference.
 function Member(ringpop, update) {
     EventEmitter.call(this);
     this.ringpop = ringpop;
@@ -105,8 +107,10 @@ Member.prototype.getStats = function getStats() {
 
 // The device's verdict on an existing member, applied the way evaluateUpdate does after its
 // rules passed (member.js:86-121): status (a local leave emits LocalMemberLeaveEvent),
-// incarnation, damp penalty, 'updated'.
-Member.prototype._applyVerdict = function _applyVerdict(update) {
+// incarnation, damp penalty, 'updated'. damp (device damp scoring): {score, exceeded, now} of
+// this change from rp_members_damp_last — the score after _applyUpdatePenalty and whether it
+// passed the suppress limit.
+Member.prototype._applyVerdict = function _applyVerdict(update, damp) {
     var oldStatus = this.status;
     if (this.status !== update.status) {
         this.status = update.status;
@@ -116,11 +120,16 @@ Member.prototype._applyVerdict = function _applyVerdict(update) {
     }
     if (this.incarnationNumber !== update.incarnationNumber) { this.incarnationNumber = update.incarnationNumber; }
     if (cfg(this.ringpop, 'dampScoringEnabled', false) && update.address !== this.ringpop.whoami()) {
-        this._applyUpdatePenalty();
+        if (damp) {
+            this.dampScore = damp.score;
+            if (damp.exceeded) { this.emit('suppressLimitExceeded'); }
+        } else {
+            this._applyUpdatePenalty();
+        }
         this.lastUpdateDampScore = this.dampScore;
     }
     this.emit('updated', update);
-    this.lastUpdateTimestamp = this.Date.now();
+    this.lastUpdateTimestamp = damp ? damp.now : this.Date.now();
 };
 
 // Membership (lib/membership/index.js:34-46) over one rp_members handle.
@@ -141,6 +150,9 @@ function Membership(opts) {
     this._h = native.membersCreate(opts.capacity || 1024, this.device);
     this._ids = {};  // address -> interned id
     this._local = null;
+    // damp scoring on the device when the config enables it (decided at the first call that
+    // needs it: initMembership's ringpop has its config by then)
+    this._deviceDamp = null;
 }
 util.inherits(Membership, EventEmitter);
 
@@ -168,6 +180,26 @@ Membership.prototype._intern = function _intern(addresses) {
         native.membersSetLocal(this._h, this._intern([me])[0]);
     }
     return ids;
+};
+
+// Whether damp scores live on the device; the first call configures rp_members_damp_* from
+// ringpop's config (config.js:60-71 names and defaults).
+Membership.prototype._damp = function _damp() {
+    if (this._deviceDamp === null) {
+        this._deviceDamp = !!cfg(this.ringpop, 'dampScoringEnabled', false);
+        if (this._deviceDamp) {
+            native.membersDampConfigure(this._h, {
+                enabled: true,
+                initial: cfg(this.ringpop, 'dampScoringInitial', 0),
+                min: cfg(this.ringpop, 'dampScoringMin', 0),
+                max: cfg(this.ringpop, 'dampScoringMax', 10000),
+                penalty: cfg(this.ringpop, 'dampScoringPenalty', 500),
+                suppressLimit: cfg(this.ringpop, 'dampScoringSuppressLimit', 5000),
+                halfLife: cfg(this.ringpop, 'dampScoringHalfLife', 60)
+            });
+        }
+    }
+    return this._deviceDamp;
 };
 
 Membership.prototype._columns = function _columns(changes) {
@@ -297,7 +329,10 @@ Membership.prototype.update = function update(changes, isLocal) {
         return [];
     }
     var col = this._columns(changes);
-    var r = native.membersUpdate(this._h, col.ids, col.st, col.inc, Date.now());
+    var deviceDamp = this._damp();
+    var now = Date.now();
+    var r = native.membersUpdate(this._h, col.ids, col.st, col.inc, now);
+    var d = deviceDamp && r.nApplied > 0 ? native.membersDampLast(this._h, changes.length) : null;
     var updates = [];
     for (var i = 0; i < changes.length; i++) {
         var a = r.applied[i];
@@ -317,7 +352,8 @@ Membership.prototype.update = function update(changes, isLocal) {
             upd = {status: st, incarnationNumber: inc};
             for (var key in change) { if (!(key in upd)) { upd[key] = change[key]; } }
         }
-        this.membersByAddress[change.address]._applyVerdict(upd);
+        this.membersByAddress[change.address]._applyVerdict(upd,
+            d ? {score: d.score[i], exceeded: d.exceeded[i], now: now} : null);
         updates.push(upd);
     }
     if (updates.length > 0) {
@@ -368,8 +404,22 @@ Membership.prototype._createMember = function _createMember(update) {  // index.
     return member;
 };
 
+// _decayMembersDampScore (index.js:374-383): with device damp scoring one k_damp_decay sweep,
+// then every Member takes its score and emits 'dampScoreDecayed' (new, old) as decayDampScore
+// does (member.js:45-66).
 Membership.prototype._decayMembersDampScore = function _decayMembersDampScore() {
-    for (var i = 0; i < this.members.length; i++) { this.members[i].decayDampScore(); }
+    if (!this._damp()) {
+        for (var i = 0; i < this.members.length; i++) { this.members[i].decayDampScore(); }
+        return;
+    }
+    native.membersDampDecay(this._h, Date.now());
+    var dump = native.membersDampDump(this._h);
+    for (var j = 0; j < this.members.length; j++) {
+        var m = this.members[j];
+        var old = m.dampScore;
+        m.dampScore = dump.score[this._ids[m.address]];
+        if (old !== null && old !== undefined) { m.emit('dampScoreDecayed', m.dampScore, old); }
+    }
 };
 
 Membership.prototype._updateMember = function _updateMember(update, isLocal) {  // index.js:386-397

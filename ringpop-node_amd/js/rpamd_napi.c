@@ -11,6 +11,7 @@
  */
 #include <node_api.h>
 #include <math.h>
+#include <stdio.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -45,6 +46,8 @@
         napi_throw_type_error(env, NULL, "wrong number of arguments");     \
         return NULL;                                                       \
     }
+
+static int64_t *f64_to_i64(napi_env env, const double *d, size_t n, int nan_is_min, const char *what);
 
 static napi_value make_u32(napi_env env, uint32_t v) {
     napi_value out;
@@ -584,15 +587,22 @@ static napi_value js_members_update(napi_env env, napi_callback_info info) {
     }
     double now = 0;
     NAPI_OK(napi_get_value_double(env, argv[4], &now));
-    int64_t *inc = (int64_t *)malloc(sizeof(int64_t) * (k ? k : 1));
-    for (size_t i = 0; i < k; i++) inc[i] = (int64_t)incd[i];
+    int64_t now64 = 0;
+    {
+        int64_t *t = f64_to_i64(env, &now, 1, 0, "update: now");
+        if (!t) return NULL;
+        now64 = t[0];
+        free(t);
+    }
+    int64_t *inc = f64_to_i64(env, incd, k, 0, "update: incarnationNumber");
+    if (!inc) return NULL;
     void *ad = NULL, *sd = NULL, *id = NULL;
     napi_value applied = new_typed(env, napi_uint8_array, k, 1, &ad);
     napi_value nst = new_typed(env, napi_uint8_array, k, 1, &sd);
     napi_value ninc = new_typed(env, napi_float64_array, k, 8, &id);
     int64_t *ninc64 = (int64_t *)malloc(sizeof(int64_t) * (k ? k : 1));
     uint32_t napplied = 0;
-    int rc = k ? rp_members_update((rp_members *)h->p, ids, st, inc, (uint32_t)k, (int64_t)now, (uint8_t *)ad,
+    int rc = k ? rp_members_update((rp_members *)h->p, ids, st, inc, (uint32_t)k, now64, (uint8_t *)ad,
                                    (uint8_t *)sd, ninc64, &napplied)
                : 0;
     for (size_t i = 0; rc == 0 && i < k; i++) ((double *)id)[i] = (double)ninc64[i];
@@ -623,9 +633,9 @@ static napi_value js_members_set(napi_env env, napi_callback_info info) {
         napi_throw_type_error(env, NULL, "set expects Uint32Array ids, Uint8Array status, Float64Array inc of equal length");
         return NULL;
     }
-    int64_t *inc = (int64_t *)malloc(sizeof(int64_t) * (k ? k : 1));
+    int64_t *inc = f64_to_i64(env, incd, k, 0, "set: incarnationNumber");
+    if (!inc) return NULL;
     uint32_t *pick = (uint32_t *)malloc(sizeof(uint32_t) * (k ? k : 1));
-    for (size_t i = 0; i < k; i++) inc[i] = (int64_t)incd[i];
     uint32_t np = 0;
     int rc = rp_members_set((rp_members *)h->p, ids, st, inc, (uint32_t)k, pick, &np);
     free(inc);
@@ -701,6 +711,101 @@ static napi_value js_members_dump(napi_env env, napi_callback_info info) {
     return out;
 }
 
+/* ------------------------------------------------------------------ damp scoring
+ * Member damp scores on the device (rp_members_damp_*; member.js:45-66,133-153,
+ * membership/index.js:330-383), for the drop-in Membership (js/membership.js). */
+static double prop_double(napi_env env, napi_value obj, const char *key, double dflt) {
+    napi_value v;
+    double d = dflt;
+    if (is_nullish(env, obj) || napi_get_named_property(env, obj, key, &v) != napi_ok || is_nullish(env, v)) return dflt;
+    napi_valuetype t;
+    napi_typeof(env, v, &t);
+    if (t == napi_boolean) {
+        bool b = false;
+        napi_get_value_bool(env, v, &b);
+        return b ? 1.0 : 0.0;
+    }
+    if (napi_get_value_double(env, v, &d) != napi_ok) return dflt;
+    return d;
+}
+
+/* membersDampConfigure(h, {enabled, initial, min, max, penalty, suppressLimit, halfLife}) with
+ * ringpop's defaults (config.js:60-71) for absent keys. */
+static napi_value js_members_damp_configure(napi_env env, napi_callback_info info) {
+    ARGS(2);
+    handle_t *h = get_handle(env, argv[0], 2);
+    if (!h) return NULL;
+    rp_damp_config c;
+    c.enabled = prop_double(env, argv[1], "enabled", 1.0) != 0.0;
+    c.initial = prop_double(env, argv[1], "initial", 0.0);
+    c.min = prop_double(env, argv[1], "min", 0.0);
+    c.max = prop_double(env, argv[1], "max", 10000.0);
+    c.penalty = prop_double(env, argv[1], "penalty", 500.0);
+    c.suppress_limit = prop_double(env, argv[1], "suppressLimit", 5000.0);
+    c.half_life = prop_double(env, argv[1], "halfLife", 60.0);
+    RP_OK(rp_members_damp_configure((rp_members *)h->p, &c));
+    return make_null(env);
+}
+
+/* membersDampLast(h, k) -> {score: Float64Array(k), exceeded: Uint8Array(k)}: per change of the
+ * last update batch, the member's dampScore after it and whether suppressLimitExceeded fired. */
+static napi_value js_members_damp_last(napi_env env, napi_callback_info info) {
+    ARGS(2);
+    handle_t *h = get_handle(env, argv[0], 2);
+    if (!h) return NULL;
+    uint32_t k = 0;
+    NAPI_OK(napi_get_value_uint32(env, argv[1], &k));
+    void *sd = NULL, *ed = NULL;
+    napi_value sc = new_typed(env, napi_float64_array, k, 8, &sd);
+    napi_value ex = new_typed(env, napi_uint8_array, k, 1, &ed);
+    RP_OK(k ? rp_members_damp_last((rp_members *)h->p, (double *)sd, (uint8_t *)ed, k) : 0);
+    napi_value out;
+    napi_create_object(env, &out);
+    napi_set_named_property(env, out, "score", sc);
+    napi_set_named_property(env, out, "exceeded", ex);
+    return out;
+}
+
+/* membersDampDecay(h, now): _decayMembersDampScore (index.js:374-383) on the device. */
+static napi_value js_members_damp_decay(napi_env env, napi_callback_info info) {
+    ARGS(2);
+    handle_t *h = get_handle(env, argv[0], 2);
+    if (!h) return NULL;
+    double now = 0;
+    NAPI_OK(napi_get_value_double(env, argv[1], &now));
+    int64_t *t = f64_to_i64(env, &now, 1, 0, "membersDampDecay: now");
+    if (!t) return NULL;
+    const int64_t now64 = t[0];
+    free(t);
+    RP_OK(rp_members_damp_decay((rp_members *)h->p, now64));
+    return make_null(env);
+}
+
+/* membersDampDump(h) -> {score, last, ts: Float64Array (0 = null)} by member id. */
+static napi_value js_members_damp_dump(napi_env env, napi_callback_info info) {
+    ARGS(1);
+    handle_t *h = get_handle(env, argv[0], 2);
+    if (!h) return NULL;
+    rp_members *m = (rp_members *)h->p;
+    uint32_t n = 0;
+    RP_OK(rp_members_count(m, &n));
+    void *sd = NULL, *ld = NULL, *td = NULL;
+    napi_value sc = new_typed(env, napi_float64_array, n, 8, &sd);
+    napi_value ls = new_typed(env, napi_float64_array, n, 8, &ld);
+    napi_value ts = new_typed(env, napi_float64_array, n, 8, &td);
+    int64_t *t64 = (int64_t *)malloc(sizeof(int64_t) * (n ? n : 1));
+    int rc = n ? rp_members_damp_dump(m, (double *)sd, (double *)ld, t64, n) : 0;
+    for (uint32_t i = 0; rc == 0 && i < n; i++) ((double *)td)[i] = (double)t64[i];
+    free(t64);
+    RP_OK(rc);
+    napi_value out;
+    napi_create_object(env, &out);
+    napi_set_named_property(env, out, "score", sc);
+    napi_set_named_property(env, out, "last", ls);
+    napi_set_named_property(env, out, "ts", ts);
+    return out;
+}
+
 /* ------------------------------------------------------------------ gossip simulator */
 /* simCreate(names[], inc0 Float64Array, dead Uint8Array, seed, suspicionRounds, now0, device) */
 // simCreate(names, inc0, dead, seed, suspicionRounds, now0, device[, events Uint32Array of
@@ -724,8 +829,15 @@ static napi_value js_sim_create(napi_env env, napi_callback_info info) {
     napi_get_value_uint32(env, argv[4], &susp);
     napi_get_value_double(env, argv[5], &now0);
     napi_get_value_int32(env, argv[6], &dev);
-    int64_t *inc = (int64_t *)malloc(sizeof(int64_t) * (s.n ? s.n : 1));
-    for (uint32_t i = 0; i < s.n; i++) inc[i] = (int64_t)incd[i];
+    int64_t *inc = f64_to_i64(env, incd, s.n, 0, "simCreate: inc0");
+    int64_t *n0 = inc ? f64_to_i64(env, &now0, 1, 0, "simCreate: now0") : NULL;
+    if (!inc || !n0) {
+        free(inc);
+        strpack_free(&s);
+        return NULL;
+    }
+    const int64_t now64 = n0[0];
+    free(n0);
     size_t ne = 0;
     const uint32_t *ev = NULL;
     napi_valuetype et = napi_undefined;
@@ -746,7 +858,7 @@ static napi_value js_sim_create(napi_env env, napi_callback_info info) {
         evs[i].node = ev[3 * i + 2];
     }
     rp_sim *sim = NULL;
-    int rc = rp_sim_create_scenario(s.n, s.bytes, s.off32, inc, dead, seed, susp, (int64_t)now0, dev, NULL, 1, 0, evs,
+    int rc = rp_sim_create_scenario(s.n, s.bytes, s.off32, inc, dead, seed, susp, now64, dev, NULL, 1, 0, evs,
                                     (uint32_t)(ne / 3), &sim);
     free(evs);
     free(inc);
@@ -847,9 +959,25 @@ static void *prop_typed(napi_env env, napi_value obj, const char *key, napi_type
     return typed_data(env, v, t, n);
 }
 
-static int64_t *f64_to_i64(const double *d, size_t n, int nan_is_min) {
+/* Incarnation numbers arrive as doubles (JS Numbers). Converting NaN, +-Inf or a value outside
+ * int64 to int64_t is undefined behaviour in C, so those are rejected with a TypeError (NaN only
+ * where it stands for "absent": nan_is_min). Returns NULL with the exception pending. */
+static int64_t *f64_to_i64(napi_env env, const double *d, size_t n, int nan_is_min, const char *what) {
     int64_t *o = (int64_t *)malloc(sizeof(int64_t) * (n ? n : 1));
-    for (size_t i = 0; i < n; i++) o[i] = (nan_is_min && d[i] != d[i]) ? INT64_MIN : (int64_t)d[i];
+    for (size_t i = 0; i < n; i++) {
+        const double x = d[i];
+        if (nan_is_min && x != x) {
+            o[i] = INT64_MIN;
+        } else if (!(x >= -9223372036854775808.0 && x < 9223372036854775808.0)) { /* NaN, Inf, range */
+            char msg[160];
+            snprintf(msg, sizeof msg, "%s[%zu] is not a finite number within int64 range", what, i);
+            free(o);
+            napi_throw_type_error(env, NULL, msg);
+            return NULL;
+        } else {
+            o[i] = (int64_t)x;
+        }
+    }
     return o;
 }
 
@@ -893,15 +1021,29 @@ static napi_value js_wire_encode(napi_env env, napi_callback_info info) {
         napi_throw_type_error(env, NULL, "wireEncode: header columns shorter than the message count");
         return NULL;
     }
-    char app[1024];
+    /* the join response's app name, any length (its byte length first, then the bytes) */
+    char *app = NULL;
     size_t app_len = 0;
     if (!is_nullish(env, argv[5])) {
         napi_value av;
-        if (napi_get_named_property(env, argv[5], "app", &av) == napi_ok && !is_nullish(env, av))
-            NAPI_OK(napi_get_value_string_utf8(env, av, app, sizeof app, &app_len));
+        if (napi_get_named_property(env, argv[5], "app", &av) == napi_ok && !is_nullish(env, av)) {
+            NAPI_OK(napi_get_value_string_utf8(env, av, NULL, 0, &app_len));
+            app = (char *)malloc(app_len + 1);
+            size_t got = 0;
+            NAPI_OK(napi_get_value_string_utf8(env, av, app, app_len + 1, &got));
+            app_len = got;
+        }
     }
-    int64_t *inc = f64_to_i64(incd, n_rec, 0), *sinc = sincd ? f64_to_i64(sincd, n_rec, 1) : NULL;
-    int64_t *msi = msid ? f64_to_i64(msid, n_msgs, 0) : NULL;
+    int64_t *inc = f64_to_i64(env, incd, n_rec, 0, "wireEncode: inc");
+    int64_t *sinc = (inc && sincd) ? f64_to_i64(env, sincd, n_rec, 1, "wireEncode: srcInc") : NULL;
+    int64_t *msi = (inc && (!sincd || sinc) && msid) ? f64_to_i64(env, msid, n_msgs, 0, "wireEncode: sourceInc") : NULL;
+    if (!inc || (sincd && !sinc) || (msid && !msi)) {
+        free(inc);
+        free(sinc);
+        free(msi);
+        free(app);
+        return NULL;
+    }
     rp_wire_records R = {addr, src, st, inc, sinc, ids};
     rp_wire_headers H = {ck, ms, msi, tg, ps, app_len ? app : NULL, (uint32_t)app_len};
     void *od = NULL, *bd = NULL;
@@ -918,6 +1060,7 @@ static napi_value js_wire_encode(napi_env env, napi_callback_info info) {
     free(sinc);
     free(msi);
     free(o64);
+    free(app);
     RP_OK(rc);
     napi_value out;
     napi_create_object(env, &out);
@@ -1027,6 +1170,10 @@ static napi_value init(napi_env env, napi_value exports) {
         {"membersComputeChecksum", js_members_compute_checksum},
         {"membersChecksumString", js_members_checksum_string},
         {"membersDump", js_members_dump},
+        {"membersDampConfigure", js_members_damp_configure},
+        {"membersDampLast", js_members_damp_last},
+        {"membersDampDecay", js_members_damp_decay},
+        {"membersDampDump", js_members_damp_dump},
         {"simCreate", js_sim_create},
         {"simStep", js_sim_step},
         {"simRound", js_sim_round},

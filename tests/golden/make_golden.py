@@ -122,7 +122,8 @@ def make_ring():
               "replicaPoints": c.get("replicaPoints", 100), "names": names, "batches": []}
         for b, ob in zip(c["batches"], o["batches"]):
             fb = {"add": b["add"], "remove": b["remove"], "changed": ob["changed"],
-                  "checksum": ob["checksum"], "serverCount": ob["serverCount"], "size": ob["size"]}
+                  "checksum": ob["checksum"], "serverCount": ob["serverCount"], "size": ob["size"],
+                  "servers": ob["servers"]}  # Object.keys(ring.servers): insertion order
             tree = ob["tree"]
             fb["tree_sha256"] = tree_digest(tree)
             if len(tree["tokens"]) <= 4000:

@@ -52,6 +52,7 @@ input.cases.forEach(function (c) {
             changed: changed,
             checksum: ring.checksum,
             serverCount: ring.getServerCount(),
+            servers: Object.keys(ring.servers),
             size: ring.rbtree.size,
         };
         if (c.dump) { bo.tree = dumpTree(ring); }

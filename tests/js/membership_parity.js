@@ -86,4 +86,54 @@ input.cases.forEach(function (c) {
     eq(c.name + ' set events', ev.set, want.set);
     m.destroy();
 });
+// Damp scoring (tests/golden/damp_golden.json, the reference Membership / Member with damp
+// scoring on): with dampScoringEnabled the drop-in keeps the scores on the device
+// (rp_members_damp_*). Every member's dampScore, lastUpdateDampScore and lastUpdateTimestamp
+// after every op, and the order of memberSuppressLimitExceeded events, must equal the
+// reference's bit for bit.
+function DampRingpop(whoami, cfgOver) {
+    FakeRingpop.call(this, whoami);
+    var conf = {
+        dampScoringEnabled: true, dampScoringDecayEnabled: false, dampScoringDecayInterval: 1000,
+        dampScoringHalfLife: 60, dampScoringInitial: 0, dampScoringMax: 10000, dampScoringMin: 0,
+        dampScoringPenalty: 500, dampScoringReuseLimit: 2500, dampScoringSuppressLimit: 5000
+    };
+    Object.keys(cfgOver || {}).forEach(function (k) { conf[k] = cfgOver[k]; });
+    this.config = {get: function (k) { return conf[k]; }};
+}
+util.inherits(DampRingpop, FakeRingpop);
+
+(input.dampCases || []).forEach(function (c) {
+    var rp = new DampRingpop(c.local, c.config);
+    var m = initMembership(rp);
+    rp.membership = m;
+    m.getJoinPosition = function () { return this.members.length; };
+    var suppressed = [];
+    m.on('memberSuppressLimitExceeded', function (member) { suppressed.push(member.address); });
+    c.ops.forEach(function (op, j) {
+        clock = op.now;
+        suppressed.length = 0;
+        var tag = 'damp ' + c.name + ' op ' + j, o = c.out[j];
+        if (op.type === 'ready') {
+            rp.isReady = op.value;
+        } else if (op.type === 'set') {
+            m.set();
+        } else if (op.type === 'decay') {
+            m._decayMembersDampScore();
+        } else {
+            var changes = op.changes.map(function (ch, i) {
+                return {address: ch[0], status: ch[1], incarnationNumber: ch[2], _i: i};
+            });
+            var applied = m.update(changes, op.isLocal);
+            eq(tag + ' applied', applied.map(function (u) { return u._i; }), o.applied);
+        }
+        eq(tag + ' suppressed', suppressed, o.suppressed);
+        eq(tag + ' damp state', m.members.map(function (x) {
+            return [x.address, x.dampScore, x.lastUpdateDampScore, x.lastUpdateTimestamp];
+        }), o.members);
+    });
+    eq('damp ' + c.name + ' on the device', m._deviceDamp, !!rp.config.get('dampScoringEnabled'));
+    m.destroy();
+});
+
 console.log(JSON.stringify({nfail: fails.length, checks: checks, fails: fails.slice(0, 20)}));

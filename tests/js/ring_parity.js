@@ -46,6 +46,10 @@ input.cases.forEach(function (c) {
         eq(tag + ' changed', ring.addRemoveServers(b.add, b.remove), b.changed);
         eq(tag + ' event', events.checksumComputed - before, b.changed ? 1 : 0);
         eq(tag + ' serverCount', ring.getServerCount(), b.serverCount);
+        eq(tag + ' device serverCount', ring.deviceServerCount(), b.serverCount);
+        eq(tag + ' servers (Object.keys order)', Object.keys(ring.servers), b.servers);
+        eq(tag + ' getStats', ring.getStats(), {checksum: b.checksum, servers: b.servers});
+        eq(tag + ' replicaPoints', ring.replicaPoints, c.replicaPoints);
         eq(tag + ' checksum', ring.checksum, b.checksum);
         if (!b.keys) { return; }
         eq(tag + ' lookup', ring.lookupBatch(b.keys).map(toIdx), b.lookup);

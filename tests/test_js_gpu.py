@@ -55,15 +55,20 @@ def test_js_membership_dropin_matches_reference_goldens(gpu, tmp_path):
     """The drop-in lib/membership module (ringpop-node_amd/js/membership.js), installed into the
     module cache the way a ringpop deployment installs it, replays every membership golden: the
     96 override rules (remote + local), random batches with repeated addresses and local
-    overrides, the 1332-member fixture, stash + set(), and the leave cases."""
+    overrides, the 1332-member fixture, stash + set(), and the leave cases; then every damp
+    scoring golden (tests/golden/damp_golden.json) with the scores on the device."""
     import pyoracle
     cases = gu.load("membership_golden.json")["cases"]
     for c in cases:
         n = 4000 if c["name"] == "fixture1332" else 2000
         c["joinRands"] = [pyoracle.philox([k, 0, 0, 0], [c["joinSeed"], 0x4A4F494E])[0] for k in range(n)]
-    res = run_node("membership_parity.js", {"cases": cases}, tmp_path)
+    damp = gu.load("damp_golden.json")["cases"]
+    for c in damp:
+        for o in c["out"]:
+            o.pop("pow", None)
+    res = run_node("membership_parity.js", {"cases": cases, "dampCases": damp}, tmp_path)
     assert res["nfail"] == 0, res["fails"]
-    assert res["checks"] > 700
+    assert res["checks"] > 700 + 2 * sum(len(c["ops"]) for c in damp)
 
 
 def test_js_wire_bodies_match_reference_goldens(gpu, tmp_path):

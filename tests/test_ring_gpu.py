@@ -33,6 +33,9 @@ def test_ring_matches_reference_goldens(gpu, orc, case_name):
         changed = ring.addRemoveServers(b["add"], b["remove"])
         assert changed == b["changed"]
         assert ring.getServerCount() == b["serverCount"]
+        assert list(ring.servers) == b["servers"]  # Object.keys(ring.servers), insertion order
+        assert ring.getStats()["servers"] == b["servers"]
+        assert sorted(ring.name(i) for i in ring.server_ids()) == sorted(b["servers"])  # the device's set
         assert ring.size == b["size"]
         assert ring.checksum == b["checksum"]
         if "tree" in b:
