@@ -187,14 +187,22 @@ def sim_cpu_baseline(n, kill_pct=1, seed=11, min_seconds=15.0, max_rounds=60, th
 
 # ------------------------------------------------------------------ device legs
 
-def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=512, warmup=3):
+def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=512, warmup=3, world=1, dist=None,
+                reduce_max=None):
     """C3 (BASELINE.json configs[2]): 100k-member table, a stream of batches of 100k updates (1%
     repeated addresses), Membership.update fold + one checksum per batch, inputs resident in HBM.
     Also: the fold alone (checksum deferred) against the HBM roofline at 49 B/update, the
-    checksum chain alone, and the fold at a batch large enough not to be launch-bound."""
+    checksum chain alone, and the fold at a batch large enough not to be launch-bound.
+    world > 1: every rank folds the whole stream on its own replica
+    (DistMembership) and checksums the batches b % world == rank; the timed region is
+    barrier-bracketed and the slowest rank's time is reported (strong scaling: the stream is
+    fixed)."""
     S = _synth()
     names, st0, inc0 = S.c3_members(n)
-    m = rpa.Membership(whoami=names[0], capacity=n, device=local)
+    if world > 1:
+        m = rpa.DistMembership(whoami=names[0], capacity=n, device=local, history_cap=batches + warmup + 64)
+    else:
+        m = rpa.Membership(whoami=names[0], capacity=n, device=local)
     ids0 = np.asarray(m.intern(names), dtype=np.uint32)
     m.update_ids(ids0, st0, inc0, now_ms=1)
     stream = torch.cuda.current_stream()
@@ -226,16 +234,25 @@ def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=512, warmup=3):
     m.checksum
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     e0.record(stream)
     for b in range(batches):
         one(warmup + b)
-    ck = m.checksum  # reads the last batch's checksum: every pending chain runs inside the timed region
+    ck = m.checksum  # reads this replica's last checksum: every pending chain runs inside the timed region
     e1.record(stream)
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     dt = time.perf_counter() - t0
+    if world > 1:
+        dt = reduce_max([dt])[0]
+        ck = m.checksums()[-1]  # the last batch's checksum (gathered once, after the timed region)
     out = {"workload": "C3: %d-member table, %d updates/batch (1%% repeated addresses), fold + 1 checksum "
-                       "per batch" % (n, k),
+                       "per batch%s" % (n, k, ", %d replicas, batch-strided checksums" % world if world > 1 else ""),
+           "n_gpus": world, "scaling": "strong",
            "updates_per_s": k * batches / dt, "ms_per_batch": dt * 1e3 / batches,
            "gpu_ms_per_batch": e0.elapsed_time(e1) / batches, "checksum": ck,
            "note": "every batch applies most of its updates and its checksum string is built after it; the "
@@ -243,7 +260,11 @@ def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=512, warmup=3):
                    "side stream, overlapping the next batches' folds (256 slots within a 1 GiB pool, "
                    "RP_MEMBERS_CK_BYTES); the last batch's checksum is read inside the timed region, so "
                    "the final group's chains are in the time"}
-    # the fold alone (sort + k_fold), HIP events per batch on the launch stream
+    if world > 1:  # the fold-only and large-batch legs are per-replica: rank 0's one-GPU run reports them
+        m.close()
+        return out
+    # the fold alone (k_link + k_fold_fast + the gated sorted path), HIP events per batch on the
+    # launch stream
     rpa.check(rpa.lib().rp_members_defer_checksum(m._h, 1))
     nf = 20
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nf)]
@@ -264,8 +285,8 @@ def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=512, warmup=3):
     out["fold"] = {"ms_per_batch": fold_ms, "bytes_per_update": BYTES_PER_UPDATE,
                    "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                 "frac": ach / HBM_PEAK_GBS,
-                                "note": "k_sort_init + radix sort + k_fold per 100k-update batch (HIP events); "
-                                        "launch-bound at this batch size"}}
+                                "note": "k_link + k_fold_fast + the gated sorted path (7 launches) per "
+                                        "100k-update batch (HIP events); launch-bound at this batch size"}}
     out["checksum_chain"] = {"ms": ck_ms, "string_bytes": slen, "GBps": slen / (ck_ms * 1e-3) / 1e9,
                              "note": "one serial farmhash chain (not rooflined, SURVEY §8d)"}
     m.close()
@@ -437,6 +458,39 @@ def wire_bench(rpa, torch, dev, n_msgs=100_000, recs=32, reps=5):
                         % (n_msgs, recs), "json_bytes": total, "round_trip_ok": ok, **res}
 
 
+# The reference's own API per call on one core (tools/ref_node_bench.py): C2
+# lookup 0.300 M/s, C2 lookupN(key, 3) 593 /s, C3 Membership.update of 100k + checksum 495 ms,
+# computeChecksum alone at 100k members 200 ms.
+REF_NODE = {"lookup_us": 1e6 / 0.300e6, "lookupN3_us": 1e6 / 593, "update_100k_batch_ms": 495.0,
+            "computeChecksum_100k_ms": 200.0, "source": "BASELINE.md §3.1 (node v12, 1 core of the build container)"}
+
+
+def api_latency_bench(timeout=300):
+    """The drop-in JS API one call at a time, in node on this box (tools/api_latency.js):
+    HashRing.lookup / lookupN (RingPop.lookup, index.js:434-471), lookupNBatch at 1 / 64 / 4096
+    keys, and the drop-in Membership.update with 1 / 10 / 100 changes (the per-ping update,
+    server/protocol/ping.js:44) at 100k / 10k / 1332 members, next to the reference's per-call
+    times (REF_NODE)."""
+    import shutil
+    node = shutil.which("node")
+    addon = os.path.join(REPO, "ringpop-node_amd", "js", "rpamd.node")
+    if not node or not os.path.exists(addon):
+        return {"skipped": "node or rpamd.node not available"}
+    r = subprocess.run([node, os.path.join(REPO, "tools", "api_latency.js")], capture_output=True, text=True,
+                       timeout=timeout)
+    if r.returncode != 0:
+        return {"error": r.stderr[-800:]}
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    out["reference_node_1core"] = REF_NODE
+    b = out["lookupNBatch3"]
+    # per-key device cost of a batched call against the reference's per-call lookupN(3)
+    out["lookupN3_batch_where_device_wins"] = min((int(n) for n in b if b[n]["us_per_key"] < REF_NODE["lookupN3_us"]),
+                                                  default=None)
+    out["lookup_speedup_single_call"] = REF_NODE["lookup_us"] / out["lookup"]["median_us"]
+    out["lookupN3_speedup_single_call"] = REF_NODE["lookupN3_us"] / out["lookupN3"]["median_us"]
+    return out
+
+
 def pmc_traffic():
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
@@ -492,6 +546,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-merge", action="store_true")
     ap.add_argument("--no-wire", action="store_true")
+    ap.add_argument("--no-api", action="store_true", help="skip the node per-call latency leg")
     ap.add_argument("--sim-n", type=int, default=10000, help="C4 members, one GPU (0: skip)")
     ap.add_argument("--sim5-n", type=int, default=100000, help="C5 members, sharded over all ranks (0: skip)")
     ap.add_argument("--sim5-cpu", type=int, default=1, help="time the C5 oracle sample (rank 0, N=1)")
@@ -565,6 +620,9 @@ def main():
     total = B * args.steps * world
     del keys, owners
     torch.cuda.empty_cache()
+    merge = None
+    if not args.no_merge:
+        merge = merge_bench(rpa, torch, local, world=world, dist=dist, reduce_max=reduce_max)
     sim5 = sim_bench(rpa, torch, dist, local, n=args.sim5_n, world=world, reduce_max=reduce_max) \
         if args.sim5_n else None
     if rank == 0:
@@ -596,8 +654,8 @@ def main():
             "host": host_info(),
         }
         th = args.cpu_threads or host_cores()
-        if not args.no_merge:
-            out["merge"] = merge_bench(rpa, torch, local)
+        if merge is not None:
+            out["merge"] = merge
             if not args.no_cpu and world == 1:
                 out["merge"]["cpu_baseline"] = merge_cpu_baseline(100_000, 100_000, th)
         if args.sim_n and world == 1:
@@ -606,6 +664,8 @@ def main():
             out["sim_c5"] = sim5
         if not args.no_wire:
             out["wire"] = wire_bench(rpa, torch, local)
+        if not args.no_api and world == 1:
+            out["api_latency"] = api_latency_bench()
         if not args.no_cpu and world == 1:
             out["cpu_baseline"] = cpu_baseline(servers, args.cpu_keys, th)
             if args.sim_n and "sim" in out:

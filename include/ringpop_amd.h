@@ -178,6 +178,18 @@ int rp_members_compute_checksum(rp_members *m);
  * index.js:306-309); a caller folding many batches calls rp_members_compute_checksum once at the
  * end. Default off. */
 int rp_members_defer_checksum(rp_members *m, int defer);
+/* Batch-strided checksums over replicas (§8e membership merge on G GPUs: every replica folds
+ * every batch, so each holds the whole table; the checksum strings and their serial farmhash
+ * chains, index.js:48-75 / 306-309, are divided among the replicas). From this call on, update
+ * batch b (counting update calls with k > 0 from 0) builds and hashes its checksum only when
+ * b % nshards == shard. With history_cap > 0 each such batch's {checksum, applied-anything} is
+ * recorded in order (at most history_cap of them; rp_members_checksum_history reads them). A
+ * batch that applied nothing leaves the reference's checksum unchanged: a reader carries the
+ * previous batch's value forward. nshards = 1, shard = 0 restores the default. */
+int rp_members_checksum_shard(rp_members *m, uint32_t nshards, uint32_t shard, uint32_t history_cap);
+/* The recorded per-batch checksums (this shard's batches, in batch order): hash[i], applied[i]
+ * (0: the batch applied nothing; hash[i] is then 0), up to cap; *n = entries recorded. */
+int rp_members_checksum_history(rp_members *m, uint32_t *hash, uint8_t *applied, uint32_t cap, uint32_t *n);
 /* generateChecksumString() (writes up to cap bytes; *len = full length). */
 int rp_members_checksum_string(rp_members *m, char *buf, uint64_t cap, uint64_t *len);
 /* Member table by id (exists/status/incarnation), cap entries. */

@@ -118,6 +118,8 @@ SIGNATURES = {
     "rp_wire_decode": (_INT, [_P, _P, _P, _U32, _P, _U32, _P, _P, _P]),
     "rp_sim_counters": (_INT, [_P, _P]),
     "rp_members_defer_checksum": (_INT, [_P, _INT]),
+    "rp_members_checksum_shard": (_INT, [_P, _U32, _U32, _U32]),
+    "rp_members_checksum_history": (_INT, [_P, _P, _P, _U32, _P]),
     "rp_members_damp_configure": (_INT, [_P, _P]),
     "rp_members_damp_last": (_INT, [_P, _P, _P, _U32]),
     "rp_members_damp_decay": (_INT, [_P, ctypes.c_int64]),
@@ -619,6 +621,20 @@ class Membership:
         check(lib().rp_members_update_dev(self._h, d_ids, d_status, d_inc, k, int(now_ms), d_applied, d_new_status,
                                           d_new_inc, d_n_applied, stream))
 
+    def checksum_shard(self, nshards, shard, history_cap=0):
+        """From now on checksum only update batches b % nshards == shard (rp_members_checksum_shard),
+        recording each one's checksum when history_cap > 0."""
+        check(lib().rp_members_checksum_shard(self._h, nshards, shard, history_cap))
+
+    def checksum_history(self):
+        """This handle's recorded per-batch checksums: (hash uint32[], applied uint8[])."""
+        n = ctypes.c_uint32()
+        check(lib().rp_members_checksum_history(self._h, None, None, 0, ctypes.byref(n)))
+        h = np.empty(max(n.value, 1), dtype=np.uint32)
+        a = np.empty(max(n.value, 1), dtype=np.uint8)
+        check(lib().rp_members_checksum_history(self._h, h.ctypes.data, a.ctypes.data, n.value, ctypes.byref(n)))
+        return h[:n.value], a[:n.value]
+
     # ---- flap-damping scores (member.js:45-66,133-153; index.js:330-383) ----
     def damp_configure(self, config=None):
         """Track dampScore on the device with the reference's config keys (config.js:60-71;
@@ -653,6 +669,60 @@ class Membership:
         ts = np.empty(max(m, 1), dtype=np.int64)
         check(lib().rp_members_damp_dump(self._h, sc.ctypes.data, ls.ctypes.data, ts.ctypes.data, m))
         return sc[:m], ls[:m], ts[:m]
+
+
+class DistMembership(Membership):
+    """Membership.update over G GPUs (membership merge): one replica of the member
+    table per rank (one process per GPU). Every rank folds every batch (the fold is cheap and
+    keeps each replica whole: any rank answers member reads); the per-batch checksums, whose
+    string build and serial farmhash chain are most of a batch (index.js:48-75, 306-309), are
+    divided among the ranks: rank g computes those of batches b with b % G == g. No per-batch
+    collective: `checksums()` gathers the recorded per-batch values once (one all-gather).
+
+    The batch stream must be the same on every rank (as the reference's is the same for one
+    process)."""
+
+    def __init__(self, whoami=None, capacity=1024, device=0, history_cap=1 << 16, group=None):
+        import torch.distributed as dist
+        super().__init__(whoami=whoami, capacity=capacity, device=device)
+        self._dist = dist
+        self._group = group
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.checksum_shard(self.world, self.rank, history_cap)
+
+    def checksums(self):
+        """The checksum after every update batch since construction (None before the first
+        applied one), in batch order: every rank's recorded values gathered and interleaved, a
+        batch that applied nothing carrying the previous value forward (index.js:306-309)."""
+        import torch
+        h, a = self.checksum_history()
+        if self.world > 1:
+            # nccl (RCCL) gathers device tensors; gloo host tensors
+            dev = "cuda" if self._dist.get_backend(self._group) == "nccl" else "cpu"
+            n = torch.tensor([len(h)], dtype=torch.int64, device=dev)
+            ns = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(self.world)]
+            self._dist.all_gather(ns, n, group=self._group)
+            ns = [int(x.item()) for x in ns]
+            cap = max(ns)
+            mine = torch.zeros(cap, 2, dtype=torch.int64)
+            mine[:len(h), 0] = torch.from_numpy(h.astype(np.int64))
+            mine[:len(h), 1] = torch.from_numpy(a.astype(np.int64))
+            parts = [torch.zeros(cap, 2, dtype=torch.int64, device=dev) for _ in range(self.world)]
+            self._dist.all_gather(parts, mine.to(dev), group=self._group)
+            parts = [x.cpu() for x in parts]
+        else:
+            ns = [len(h)]
+            parts = [torch.from_numpy(np.stack([h.astype(np.int64), a.astype(np.int64)], axis=1))]
+        total = sum(ns)
+        out, cur = [], None
+        for b in range(total):
+            g, j = b % self.world, b // self.world
+            hv, av = int(parts[g][j, 0]), int(parts[g][j, 1])
+            if av:
+                cur = hv
+            out.append(cur)
+        return out
 
 
 SIM_EVENT = {"kill": 0, "revive": 1, "leave": 2, "join": 3}

@@ -438,6 +438,20 @@ __global__ __launch_bounds__(256) void k_mck_build(const uint32_t* __restrict__ 
     }
 }
 
+// the per-batch history (rp_members_checksum_shard): the group's update-batch slots (bit j of
+// mask) append {hash, gate} in slot order
+__global__ void k_ck_hist(const uint32_t* __restrict__ meta, uint32_t n, uint64_t mask_lo, uint64_t mask_hi,
+                          uint32_t* __restrict__ hist) {
+    uint32_t c = 0;
+    for (uint32_t j = 0; j < n; j++) {
+        const bool on = j < 64 ? (mask_lo >> j) & 1u : (mask_hi >> (j - 64)) & 1u;
+        if (!on) continue;
+        hist[2 * c] = meta[4 * j + 1] ? meta[4 * j + 2] : 0u;
+        hist[2 * c + 1] = meta[4 * j + 1];
+        c++;
+    }
+}
+
 // the group's results in batch order: the membership checksum is the last gated batch's hash
 __global__ void k_ck_commit(const uint32_t* __restrict__ meta, uint32_t n, uint32_t* __restrict__ ck) {
     for (uint32_t b = 0; b < n; b++)
@@ -489,6 +503,14 @@ struct Members {
     uint64_t slot_bytes = 0;
     DevBuf<uint32_t> ck_meta;  // [kMaxSlots][4]: total, gate, hash, done
     uint32_t npending = 0;     // pending strings in the current group
+    // Batch-strided checksums over replicas (rp_members_checksum_shard): every replica folds every
+    // batch; this one builds and hashes the strings of update batches b with b % ck_nsh == ck_sh
+    // only, and records each one's {hash, gate} in ck_hist (hist_cap entries, hist_n used).
+    uint32_t ck_nsh = 1, ck_sh = 0;
+    uint64_t batch_no = 0;  // update batches (k > 0) seen
+    DevBuf<uint32_t> ck_hist;
+    uint32_t hist_cap = 0, hist_n = 0;
+    uint64_t pend_mask[2] = {0, 0};  // pending slots that are update batches (history)
     uint32_t cur_group = 0;
     hipStream_t pend_st = nullptr;  // the stream the pending strings were built on
     hipStream_t ck_st = nullptr;    // the side stream the chains run on
@@ -615,7 +637,9 @@ struct Members {
                                nullptr, 0u);
         }
         RP_HIP(hipGetLastError());
-        if (!defer_ck) checksum_dev(s, napplied.p);
+        const bool mine = ck_nsh <= 1 || batch_no % ck_nsh == ck_sh;
+        batch_no++;
+        if (!defer_ck && mine) checksum_dev(s, napplied.p, true);
     }
 
     // Membership.set over a stash of k changes (arrival order): merge, set, checksum once.
@@ -646,7 +670,7 @@ struct Members {
     // Membership.computeChecksum (index.js:48-75) gated on *gate != 0 (null = always): the
     // string is built now (it reflects the table after this batch) into the next slot; its hash
     // lands in ck when the group is flushed.
-    void checksum_dev(hipStream_t s, const uint32_t* gate) {
+    void checksum_dev(hipStream_t s, const uint32_t* gate, bool is_batch = false) {
         const uint32_t n = nt.size();
         if (!n) return;
         ck_len.reserve(n + 1);
@@ -702,6 +726,7 @@ struct Members {
 #undef RP_MCK
         }
         RP_HIP(hipGetLastError());
+        if (is_batch && hist_cap) pend_mask[npending >> 6] |= 1ull << (npending & 63);
         npending++;
     }
 
@@ -715,6 +740,16 @@ struct Members {
         hash_long_multi(ck_buf.p + slot_bytes * first, slot_bytes, npending, ck_meta.p + 4 * first, ck_st);
         hipLaunchKernelGGL(k_ck_commit, dim3(1), dim3(1), 0, ck_st, ck_meta.p + 4 * first, npending, ck.p);
         RP_HIP(hipGetLastError());
+        const uint32_t nb = (uint32_t)(__builtin_popcountll(pend_mask[0]) + __builtin_popcountll(pend_mask[1]));
+        if (nb) {
+            if (hist_n + nb > hist_cap)
+                throw Error(RP_ESTATE, "checksum history full (rp_members_checksum_shard history_cap)");
+            hipLaunchKernelGGL(k_ck_hist, dim3(1), dim3(1), 0, ck_st, ck_meta.p + 4 * first, npending, pend_mask[0],
+                               pend_mask[1], ck_hist.p + 2ull * hist_n);
+            RP_HIP(hipGetLastError());
+            hist_n += nb;
+        }
+        pend_mask[0] = pend_mask[1] = 0;
         RP_HIP(hipEventRecord(ev_hashed[cur_group], ck_st));
         group_busy[cur_group] = true;
         cur_group = (cur_group + 1) % ngroups;
@@ -916,6 +951,37 @@ int rp_members_checksum(rp_members* h, uint32_t* out, int* is_set) {
 
 int rp_members_defer_checksum(rp_members* h, int defer) {
     return guard([&] { MB(h).defer_ck = defer != 0; });
+}
+
+int rp_members_checksum_shard(rp_members* h, uint32_t nshards, uint32_t shard, uint32_t history_cap) {
+    return guard([&] {
+        rp::Members& m = MB(h);
+        RP_REQUIRE(nshards >= 1 && shard < nshards, "checksum_shard: shard must be < nshards");
+        m.settle_checksums();  // pending strings keep the old numbering
+        m.ck_nsh = nshards;
+        m.ck_sh = shard;
+        m.batch_no = 0;
+        m.hist_n = 0;
+        m.hist_cap = history_cap;
+        if (history_cap) m.ck_hist.reserve(2ull * history_cap);
+    });
+}
+
+int rp_members_checksum_history(rp_members* h, uint32_t* hash, uint8_t* applied, uint32_t cap, uint32_t* n) {
+    return guard([&] {
+        rp::Members& m = MB(h);
+        m.settle_checksums();
+        const uint32_t c = std::min(cap, m.hist_n);
+        if (c && (hash || applied)) {
+            std::vector<uint32_t> v(2ull * c);
+            RP_HIP(hipMemcpy(v.data(), m.ck_hist.p, 8ull * c, hipMemcpyDeviceToHost));
+            for (uint32_t i = 0; i < c; i++) {
+                if (hash) hash[i] = v[2 * i];
+                if (applied) applied[i] = v[2 * i + 1] ? 1 : 0;
+            }
+        }
+        if (n) *n = m.hist_n;
+    });
 }
 
 int rp_members_compute_checksum(rp_members* h) {

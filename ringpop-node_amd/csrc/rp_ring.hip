@@ -648,6 +648,8 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_compact(const uint8_t* _
 //     positions near the ring end.
 // HS: the tile's keys pass through LDS in HS slices (all loads issued first, held in registers),
 // so the key stage takes 1/HS of the LDS and more workgroups fit a CU (A/B).
+// (Forcing 5 waves per SIMD with __launch_bounds__ spills 8 VGPRs and ran 1.05 against 0.91 ms,
+// profiles/r03/ab_lookup_occ.json: the 119 VGPRs and 4 waves per SIMD stay.)
 template <int KPL, int NEED, int HS = 1>
 __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __restrict__ keys, uint64_t ntiles,
                                                              CompactView cv, uint32_t* __restrict__ out,

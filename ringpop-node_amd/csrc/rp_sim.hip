@@ -1953,6 +1953,35 @@ __global__ void k_dirty_list(SimDev S, uint32_t* __restrict__ list, uint32_t* __
     }
 }
 
+// The early refresh's views (stage 2, beside the D1 sender chains): the live dirty views except
+// the round's ping-req senders (k_d1_list's predicate: their chains run in k_ck_pc over the D1
+// list, and phase D1 reads and may change those views meanwhile). The count goes to the
+// views-hashed counter (stats[4]) as k_count_dirty's would.
+__global__ void k_early_list(SimDev S, uint32_t* __restrict__ list, uint32_t* __restrict__ n) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    uint32_t cnt = 0;
+    for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < S.NL; i0 += stride) {
+        const uint32_t lv = i0 + threadIdx.x;
+        bool on = lv < S.NL && S.dirty[lv] && !S.dead[S.v0 + lv];
+        if (on) {
+            const int32_t t = S.target[lv];
+            on = !(t >= 0 && S.dead[t]);
+            // a view whose earliest suspicion timer is due fires it in phase E and changes again
+            // (timers are appended with due = round + susp, so tim[0] is the earliest)
+            if (on && S.n_tim[lv] && S.tim[(uint64_t)lv * S.Ct].due <= S.round) on = false;
+        }
+        const uint64_t m = __ballot(on);
+        if (!m) continue;
+        uint32_t base = 0;
+        if (lane == __ffsll((long long)m) - 1) base = atomicAdd(n, (uint32_t)__popcll(m));
+        base = __shfl(base, __ffsll((long long)m) - 1, 64);
+        if (on) list[base + __popcll(m & ((1ull << lane) - 1))] = lv;
+        cnt += lane == 0 ? (uint32_t)__popcll(m) : 0u;
+    }
+    if (lane == 0 && cnt) atomicAdd(&S.stats[4], (unsigned long long)cnt);
+}
+
 __global__ void k_twin_copy(SimDev S, uint32_t* __restrict__ twin_of) {
     for (uint32_t lv = blockIdx.x * blockDim.x + threadIdx.x; lv < S.NL; lv += gridDim.x * blockDim.x) {
         const uint32_t r = twin_of[lv];
@@ -2761,6 +2790,16 @@ struct MsgBuf {
 struct Sim {
     int device = 0;
     hipStream_t st = nullptr;
+    // the early refresh (stage 2): dirty views hashed on a side stream beside the D1 sender
+    // chains; stage 3 waits for it before phase D2 changes views again (RP_SIM_EARLY=1: on)
+    hipStream_t st2 = nullptr;
+    hipEvent_t ev_c = nullptr, ev_early = nullptr;
+    bool early_pending = false;
+    bool early_on = [] {
+        const char* e = getenv("RP_SIM_EARLY");
+        return e && *e == '1';
+    }();
+    DevBuf<uint32_t> elist;
     uint32_t N = 0, NL = 0, v0 = 0, G = 1, shard = 0;
     unsigned grid = 0;
     NameTable nt;
@@ -3030,16 +3069,49 @@ struct Sim {
                 d1list.reserve(NL + 1);
                 RP_HIP(hipMemsetAsync(d1list.p + NL, 0, 4, st));
                 hipLaunchKernelGGL(k_d1_list, dim3(grid_for(NL, 256)), dim3(256), 0, st, d, d1list.p, d1list.p + NL);
+                const bool early = early_on;
+                if (early) {  // this round's dirty views except the D1 senders, listed after C
+                    elist.reserve(NL + 1);
+                    RP_HIP(hipMemsetAsync(elist.p + NL, 0, 4, st));
+                    hipLaunchKernelGGL(k_early_list, dim3(grid_for(NL, 256, 1024)), dim3(256), 0, st, d, elist.p,
+                                       elist.p + NL);
+                    if (!st2) {
+                        RP_HIP(hipStreamCreateWithFlags(&st2, hipStreamNonBlocking));
+                        RP_HIP(hipEventCreateWithFlags(&ev_c, hipEventDisableTiming));
+                        RP_HIP(hipEventCreateWithFlags(&ev_early, hipEventDisableTiming));
+                    }
+                    RP_HIP(hipEventRecord(ev_c, st));
+                }
                 // the senders' checksums (their ping-req bodies carry them) as side-by-side chains
                 // first, so D1's workgroups find their views clean
                 if (!getenv("RP_SIM_D1_BLOCKCK"))
                     hipLaunchKernelGGL(k_ck_pc<7>, dim3((NL + 63) / 64), dim3(512), 0, st, d, d1list.p, d1list.p + NL);
                 hipLaunchKernelGGL(k_phase_d1, dim3(g), dim3(kT), 0, st, d, d1list.p, d1list.p + NL);
+                if (early) {
+                    // The D1 chains hold a few CUs for milliseconds (one 64-view group per CU);
+                    // the rest of the machine hashes the views B and C dirtied, which the next
+                    // round's refresh would otherwise hash after E. A view that D2, D3 or E
+                    // changes again is dirty again and is hashed again then.
+                    RP_HIP(hipStreamWaitEvent(st2, ev_c, 0));
+                    const uint32_t groups = (NL + 63) / 64;
+                    if (groups <= cus)
+                        hipLaunchKernelGGL(k_ck_pc<7>, dim3(groups), dim3(512), 0, st2, d, elist.p, elist.p + NL);
+                    else
+                        hipLaunchKernelGGL(k_ck_lanes, dim3(grid_for(NL, 256, 1u << 20)), dim3(256), 0, st2, d,
+                                           elist.p, elist.p + NL);
+                    RP_HIP(hipGetLastError());
+                    RP_HIP(hipEventRecord(ev_early, st2));
+                    early_pending = true;
+                }
             }
             build_out(K_LEG);
             break;
         case 3:
             import_in(K_LEG);
+            if (early_pending) {  // D2 changes helper views: the early refresh must be done
+                RP_HIP(hipStreamWaitEvent(st, ev_early, 0));
+                early_pending = false;
+            }
             if (NL) hipLaunchKernelGGL(k_phase_d2, dim3(g), dim3(kT), 0, st, d);
             build_out(K_LRESP);
             break;
@@ -3527,6 +3599,12 @@ int rp_sim_destroy(rp_sim* s) {
         if (s->impl.st) {
             (void)hipStreamSynchronize(s->impl.st);
             (void)hipStreamDestroy(s->impl.st);
+        }
+        if (s->impl.st2) {
+            (void)hipStreamSynchronize(s->impl.st2);
+            (void)hipStreamDestroy(s->impl.st2);
+            (void)hipEventDestroy(s->impl.ev_c);
+            (void)hipEventDestroy(s->impl.ev_early);
         }
         delete s;
     });

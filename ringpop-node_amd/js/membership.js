@@ -216,9 +216,16 @@ Membership.prototype._columns = function _columns(changes) {
 
 // computeChecksum (index.js:48-75): the device hashes the address-sorted checksum string
 Membership.prototype.computeChecksum = function computeChecksum() {
+    return this._takeChecksum(native.membersComputeChecksum);
+};
+
+// The checksum `read` returns, taken with computeChecksum's events and stats. update() passes
+// the read of the checksum its batch already built on the device (rp_members_update computes
+// it once per applied batch, index.js:306-309), so a batch hashes its string once.
+Membership.prototype._takeChecksum = function _takeChecksum(read) {
     var start = new Date();
     var prev = this.checksum;
-    this.checksum = native.membersComputeChecksum(this._h);
+    this.checksum = read(this._h);
     this.emit('checksumComputed');
     this.ringpop.stat('timing', 'compute-checksum', start);
     this.ringpop.stat('gauge', 'checksum', this.checksum);
@@ -357,7 +364,7 @@ Membership.prototype.update = function update(changes, isLocal) {
         updates.push(upd);
     }
     if (updates.length > 0) {
-        this.computeChecksum();
+        this._takeChecksum(native.membersChecksum);
         this.emit('updated', updates);
     }
     return updates;

@@ -45,3 +45,16 @@ def test_bench_one_gpu_schema(gpu):
     assert out["n_gpus"] == 1 and out["roofline"]["frac"] > 0
     assert out["sim_c5"]["round_ms"]["max"] >= out["sim_c5"]["round_ms"]["p50"]
     assert out["sim_c5"]["traffic"]["records"] > 0
+
+
+def test_bench_four_ranks_spawned_with_merge(gpu):
+    """`bench.py --gpus 4`: four ranks (gloo; they share the box's GPU), the C5-path simulator
+    sharded four ways and the C3 merge as four replicas with batch-strided checksums
+    (DistMembership); rank 0 reports n_gpus = 4 for both."""
+    small = [x for x in SMALL if x != "--no-merge"]
+    out = _bench(4, small, {"RP_BENCH_BACKEND": "gloo"})
+    assert out["n_gpus"] == 4
+    assert out["config"]["total_keys"] == 4 * 2 * (1 << 18)
+    assert out["sim_c5"]["n_gpus"] == 4 and out["sim_c5"]["converged"]
+    assert out["merge"]["n_gpus"] == 4 and out["merge"]["updates_per_s"] > 0
+    assert isinstance(out["merge"]["checksum"], int)

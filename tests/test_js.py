@@ -19,7 +19,8 @@ EXPORTS = ["version", "deviceCount", "hash32", "destroy", "ringCreate", "ringAdd
            "ringChecksumString", "ringServerCount", "ringTokenCount", "ringHasServer", "ringServers",
            "ringOwnerName", "ringLookup", "ringLookupN", "ringLookupNHashes", "ringGroupKeys", "membersCreate", "membersIntern",
            "membersSetLocal", "membersUpdate", "membersSet", "membersChecksum", "membersComputeChecksum",
-           "membersChecksumString", "membersDump", "simCreate", "simStep", "simRound", "simChecksums",
+           "membersChecksumString", "membersDump", "membersDampConfigure", "membersDampLast", "membersDampDecay",
+           "membersDampDump", "simCreate", "simStep", "simRound", "simChecksums",
            "simView", "simConverged", "simStats", "wireEncode", "wireDecode"]
 
 

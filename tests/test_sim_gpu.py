@@ -212,3 +212,11 @@ def test_sharded_join_without_exchange_is_refused(gpu):
                 if k < gpu.SIM_STAGES - 1:
                     gpu.check(gpu.lib().rp_sim_exchange_local(sim._arr, sim.G))
     sim.close()
+
+
+def test_sim_with_early_refresh_matches_reference_goldens(gpu, monkeypatch):
+    """RP_SIM_EARLY=1: the stage-2 refresh beside the D1 chains (off by default, DESIGN.md §4.4);
+    the goldens must hold either way."""
+    monkeypatch.setenv("RP_SIM_EARLY", "1")
+    test_sim_matches_reference_goldens(gpu, "n24-revive")
+    test_sim_matches_reference_goldens(gpu, "n30-join")

@@ -72,7 +72,7 @@ def _join_events(n, k, seed):
     return ev + [(9, "join", int(v)) for v in sorted(crashed[:6])] + [(9, "join", int(v)) for v in np.flatnonzero(dead)[:2]]
 
 
-def _run_dist(gpu, tmp_path, G, backend, n=400, k=6, seed=7, susp=25, rounds=45, scenario=None):
+def _run_dist(gpu, tmp_path, G, backend, n=400, k=6, seed=7, susp=25, rounds=45, scenario=None, timeout=100):
     out = str(tmp_path / "dist.npz")
     port = _free_port()
     worker = os.path.join(REPO, "tests", "workers", "dist_sim_worker.py")
@@ -82,7 +82,7 @@ def _run_dist(gpu, tmp_path, G, backend, n=400, k=6, seed=7, susp=25, rounds=45,
                    MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, worker, str(n), str(k), str(seed), str(susp), str(rounds),
                                        out, backend] + ([scenario] if scenario else []), env=env))
-    rcs = [p.wait(timeout=100) for p in procs]
+    rcs = [p.wait(timeout=timeout) for p in procs]
     assert rcs == [0] * G
     d = np.load(out)
     names, inc0, dead = _case(n, k, seed)
@@ -112,3 +112,10 @@ def test_dist_one_rank_nccl_matches_unsharded(gpu, tmp_path):
 def test_dist_two_ranks_gloo_joins_match_unsharded(gpu, tmp_path):
     """Join events across ranks: the join exchange buffer is summed over torch.distributed."""
     _run_dist(gpu, tmp_path, 2, "gloo", scenario="join")
+
+
+def test_dist_four_ranks_gloo_joins_match_unsharded(gpu, tmp_path):
+    """The 8-GPU run's shape across processes at a smaller scale: 4 ranks (sharing the box's GPU,
+    gloo transport), n = 2000 with crashes at round 3 and joins at round 9 (rp_sim_join_export /
+    import across all four shards), checked round by round against the unsharded simulator."""
+    _run_dist(gpu, tmp_path, 4, "gloo", n=2000, k=20, rounds=50, scenario="join", timeout=200)
