@@ -24,10 +24,23 @@ def load_pkg():
     return mod
 
 
+def _stale(lib_path):
+    """The library is missing or older than any of its sources (csrc/*, include/*.h): rebuild
+    rather than test a stale shipped .so."""
+    if not os.path.exists(lib_path):
+        return True
+    t = os.path.getmtime(lib_path)
+    srcs = [os.path.join(REPO, "include", "ringpop_amd.h")]
+    csrc = os.path.join(REPO, "ringpop-node_amd", "csrc")
+    srcs += [os.path.join(csrc, f) for f in os.listdir(csrc) if f.endswith((".hip", ".h")) or f == "Makefile"]
+    # (2 s of slack: a copy of the tree that does not keep modification times must not rebuild)
+    return any(os.path.getmtime(x) > t + 2.0 for x in srcs if os.path.exists(x))
+
+
 @pytest.fixture(scope="session")
 def rpa():
     mod = load_pkg()
-    if not os.path.exists(mod.LIB_PATH):
+    if _stale(mod.LIB_PATH) and not os.environ.get("RP_AMD_LIB"):
         mod.build()
     return mod
 
