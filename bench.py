@@ -188,7 +188,7 @@ def sim_cpu_baseline(n, kill_pct=1, seed=11, min_seconds=15.0, max_rounds=60, th
 # ------------------------------------------------------------------ device legs
 
 def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=512, warmup=3, world=1, dist=None,
-                reduce_max=None):
+                reduce_max=None, extras=True):
     """C3 (BASELINE.json configs[2]): 100k-member table, a stream of batches of 100k updates (1%
     repeated addresses), Membership.update fold + one checksum per batch, inputs resident in HBM.
     Also: the fold alone (checksum deferred) against the HBM roofline at 49 B/update, the
@@ -260,7 +260,7 @@ def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=512, warmup=3, 
                    "side stream, overlapping the next batches' folds (256 slots within a 1 GiB pool, "
                    "RP_MEMBERS_CK_BYTES); the last batch's checksum is read inside the timed region, so "
                    "the final group's chains are in the time"}
-    if world > 1:  # the fold-only and large-batch legs are per-replica: rank 0's one-GPU run reports them
+    if world > 1 or not extras:  # the fold-only and large-batch legs are per-replica: rank 0's one-GPU run
         m.close()
         return out
     # the fold alone (k_link + k_fold_fast + the gated sorted path), HIP events per batch on the

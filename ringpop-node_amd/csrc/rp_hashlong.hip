@@ -3,8 +3,8 @@
 // farmhashmk::Hash32 over a long string is a serial chain across 20-byte chunks, so one
 // string runs on one lane. Everything in a chunk that does not depend on the chain state
 // (the five words and the three Murmur pre-mixes rotr(x*c1,17)*c2 of d, c and b+e*c1) is
-// computed ahead by the other 192 lanes of the workgroup into a double-buffered LDS window;
-// the chain lane then does 5 dependent ops per chunk (the regrouping below). Per-view parallel checksums (the
+// computed ahead by 128 producer lanes of the workgroup into a double-buffered LDS window;
+// the chain lanes then do 5 dependent ops per chunk (the regrouping below). Per-view parallel checksums (the
 // simulator) use one lane per view instead.
 #include "rp_farmhash.h"
 #include "rp_hashlong.h"
@@ -48,9 +48,29 @@ __device__ __forceinline__ uint32_t mul5_add(uint32_t x, uint32_t c) {  // 5x + 
     return lshl_add<2>(x, x + c);
 }
 
+// The coupled (g, f) pair runs on two lanes of one wave, g on lane 0 and f on lane 1, so one
+// instruction advances both. With r = rotr(v ^ premix, 19) per lane and sh = 1 (g) or 0 (f):
+//   v' = 5 r_other + (5 (r_self << sh) + c_self)
+// (lane 0: 5 (r_f + 2 r_g) + c_g, lane 1: 5 (r_g + r_f) + c_f); the first term is a DPP quad
+// permute of 5 r folded into the final add. Six VALU ops per chunk for both words where the
+// single-lane form issued eleven, and no DPP wait states (5 r is written two ops before it is
+// read across lanes): a lone wave issues about one instruction per four cycles, so the chain's
+// rate is its instruction count. h (which never mixes with g and f before the finalisation)
+// runs on lane 64.
+__device__ __forceinline__ uint32_t lshl_add_v(uint32_t a, uint32_t sh, uint32_t b) {  // (a << sh) + b
+    uint32_t r;
+    asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(sh), "v"(b));
+    return r;
+}
+__device__ __forceinline__ uint32_t swap_pair(uint32_t v) {  // lanes 2i <-> 2i+1 (quad_perm 1,0,3,2)
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);
+}
+
 // One string's chain by the whole workgroup (see the kernels below).
 __device__ void hash_long_block(const uint8_t* __restrict__ s, uint64_t len, uint32_t* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) uint32_t win[2][kWin][8];
+    // per window, per chain lane (g, f, h), per chunk: {premix word, next-chunk addend}
+    __shared__ __attribute__((aligned(16))) uint2 win[2][3][kWin];
+    __shared__ uint32_t s_st[3];
     const int tid = threadIdx.x;
     if (len <= 24) {
         if (tid == 0) {
@@ -76,14 +96,12 @@ __device__ void hash_long_block(const uint8_t* __restrict__ s, uint64_t len, uin
                 b2 = word(o + 24);
                 c2 = word(o + 28);
             }
-            uint32_t* r = win[buf][j];
-            *reinterpret_cast<uint4*>(r) = uint4{premix(d), premix(cc), premix(b + e * fh::kC1), kK + e + a2};
-            *reinterpret_cast<uint2*>(r + 4) = uint2{2u * kK + a + d + c2, 3u * kK + 2u * a + d + b2};
+            win[buf][0][j] = uint2{premix(cc), 3u * kK + 2u * a + d + b2};
+            win[buf][1][j] = uint2{premix(b + e * fh::kC1), 2u * kK + a + d + c2};
+            win[buf][2][j] = uint2{premix(d), kK + e + a2};
         }
     };
-    // chain state (lane 0 only), pre-added with chunk 0's words
-    uint32_t hp = 0, gp = 0, fp = 0;
-    if (tid == 0) {
+    if (tid == 0) {  // chain state pre-added with chunk 0's words
         const uint32_t L = (uint32_t)len;
         uint32_t h = L, g = fh::kC1 * L, f = g;
         const uint32_t a0 = premix(ld32(s, len - 4)), a1 = premix(ld32(s, len - 8)), a2 = premix(ld32(s, len - 16)),
@@ -98,69 +116,68 @@ __device__ void hash_long_block(const uint8_t* __restrict__ s, uint64_t len, uin
         g = fh::rotr(g, 19) * 5 + kK;
         f += a4;
         f = fh::rotr(f, 19) + 113;
-        hp = h + word(0);
-        gp = g + word(4);
-        fp = f + word(8);
+        s_st[0] = g + word(4);
+        s_st[1] = f + word(8);
+        s_st[2] = h + word(0);
     }
-    __shared__ uint32_t s_h;
-    if (tid == 0) s_h = hp;  // the h chain runs on wave 1 (lane 64)
     fill(0, 0, tid, kHlThreads);
     __syncthreads();
-    if (tid == 64) hp = s_h;
+    // lane 0: g, lane 1: f (wave 0); lane 64: h (wave 1)
+    const int ln = tid < 2 ? tid : 2;
+    uint32_t v = (tid < 2 || tid == 64) ? s_st[ln] : 0u;
+    const uint32_t sh = tid == 0 ? 1u : 0u, sh2 = sh + 2u;
     const uint64_t nwin = (iters + kWin - 1) / kWin;
 #ifdef RP_CK_PROF
     uint64_t t_chain = 0;
     const uint64_t t_start = clock64();
 #endif
-    // One wave issues about one VALU op per 4 cycles, so a lone chain is issue-bound: h (which
-    // never mixes with g and f before the finalisation) runs on lane 64 while lane 0 runs the
-    // coupled (g, f) pair; waves 2-3 produce the next window.
-    auto step_gf = [&](const uint4 x, const uint2 y) {
-        const uint32_t rg = __builtin_amdgcn_alignbit(gp ^ x.y, gp ^ x.y, 19);
-        const uint32_t rf = __builtin_amdgcn_alignbit(fp ^ x.z, fp ^ x.z, 19);
-        fp = mul5_add(rf + rg, y.x);
-        gp = mul5_add(lshl_add<1>(rg, rf), y.y);
+    auto step_gf = [&](const uint2 x) {
+        const uint32_t y = v ^ x.x;
+        const uint32_t r = __builtin_amdgcn_alignbit(y, y, 19);
+        const uint32_t r5 = (r << 2) + r;
+        const uint32_t own = (r << sh2) + ((r << sh) + x.y);
+        v = swap_pair(r5) + own;
     };
-    auto step_h = [&](const uint4 x) {
-        const uint32_t rh = __builtin_amdgcn_alignbit(hp ^ x.x, hp ^ x.x, 19);
-        hp = mul5_add(rh, x.w);
+    auto step_h = [&](const uint2 x) {
+        const uint32_t y = v ^ x.x;
+        v = mul5_add(__builtin_amdgcn_alignbit(y, y, 19), x.y);
     };
     for (uint64_t w = 0; w < nwin; w++) {
         const int cur = (int)(w & 1);
         if (tid >= 128) {
             if (w + 1 < nwin) fill(cur ^ 1, (w + 1) * kWin, tid - 128, kHlThreads - 128);
-        } else if (tid == 0 || tid == 64) {
+        } else if (tid < 2 || tid == 64) {
 #ifdef RP_CK_PROF
             const uint64_t tc0 = clock64();
 #endif
             const uint64_t c0 = w * kWin;
             const int n = (int)((iters - c0) < (uint64_t)kWin ? (iters - c0) : kWin);
-            if (tid == 0) {
-                int j = 0;
+            const uint2* src = win[cur][ln];
+            int j = 0;
+            if (tid < 2) {
                 for (; j + 8 <= n; j += 8) {  // the LDS reads of 8 chunks issued ahead of their steps
-                    uint4 x[8];
-                    uint2 y[8];
+                    uint4 x[4];
 #pragma unroll
-                    for (int q = 0; q < 8; q++) {
-                        x[q] = *reinterpret_cast<const uint4*>(win[cur][j + q]);
-                        y[q] = *reinterpret_cast<const uint2*>(win[cur][j + q] + 4);
+                    for (int q = 0; q < 4; q++) x[q] = *reinterpret_cast<const uint4*>(src + j + 2 * q);
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        step_gf(uint2{x[q].x, x[q].y});
+                        step_gf(uint2{x[q].z, x[q].w});
                     }
-#pragma unroll
-                    for (int q = 0; q < 8; q++) step_gf(x[q], y[q]);
                 }
-                for (; j < n; j++)
-                    step_gf(*reinterpret_cast<const uint4*>(win[cur][j]),
-                            *reinterpret_cast<const uint2*>(win[cur][j] + 4));
+                for (; j < n; j++) step_gf(src[j]);
             } else {
-                int j = 0;
                 for (; j + 8 <= n; j += 8) {
-                    uint4 x[8];
+                    uint4 x[4];
 #pragma unroll
-                    for (int q = 0; q < 8; q++) x[q] = *reinterpret_cast<const uint4*>(win[cur][j + q]);
+                    for (int q = 0; q < 4; q++) x[q] = *reinterpret_cast<const uint4*>(src + j + 2 * q);
 #pragma unroll
-                    for (int q = 0; q < 8; q++) step_h(x[q]);
+                    for (int q = 0; q < 4; q++) {
+                        step_h(uint2{x[q].x, x[q].y});
+                        step_h(uint2{x[q].z, x[q].w});
+                    }
                 }
-                for (; j < n; j++) step_h(*reinterpret_cast<const uint4*>(win[cur][j]));
+                for (; j < n; j++) step_h(src[j]);
             }
 #ifdef RP_CK_PROF
             if (tid == 0) t_chain += clock64() - tc0;
@@ -168,10 +185,10 @@ __device__ void hash_long_block(const uint8_t* __restrict__ s, uint64_t len, uin
         }
         __syncthreads();
     }
-    if (tid == 64) s_h = hp;
+    if (tid < 2 || tid == 64) s_st[ln] = v;
     __syncthreads();
     if (tid == 0) {
-        uint32_t h = s_h, g = gp, f = fp;  // the last chunk's next-words were 0
+        uint32_t h = s_st[2], g = s_st[0], f = s_st[1];  // the last chunk's next-words were 0
         g = fh::rotr(g, 11) * fh::kC1;
         g = fh::rotr(g, 17) * fh::kC1;
         f = fh::rotr(f, 11) * fh::kC1;

@@ -58,12 +58,12 @@ __device__ __forceinline__ MRow row_load(const MRow* p) {
     r.cnt = v.w;
     return r;
 }
-__device__ __forceinline__ void row_store(MRow* p, int64_t inc, uint8_t status, uint8_t exists) {
+__device__ __forceinline__ void row_store(MRow* p, int64_t inc, uint8_t status, uint8_t exists, uint32_t cnt = 0) {
     uint4 v;
     v.x = (uint32_t)(uint64_t)inc;
     v.y = (uint32_t)((uint64_t)inc >> 32);
     v.z = (uint32_t)status | ((uint32_t)exists << 8);
-    v.w = 0;  // the grouped fold's change counter, cleared
+    v.w = cnt;  // the grouped fold's change counter, normally cleared
     *reinterpret_cast<uint4*>(p) = v;
 }
 
@@ -87,11 +87,12 @@ struct FoldArgs {
 // 2 = created a new member. With damp tracking on, an applied update to another member takes
 // _applyUpdatePenalty (member.js:98-107, 133-153) and every applied update stamps
 // lastUpdateTimestamp (:115-118). `row` is the member's row as loaded; it is written back once
-// with its change counter cleared.
+// with its change counter set to cnt_after (cleared, except by the overflow fold).
 // Returns the number of changes applied (the caller sums them per wave: one atomic per wave,
 // not per address, on the batch's applied counter).
 template <class Change>
-__device__ __forceinline__ uint32_t fold_address(const FoldArgs& A, uint32_t id, MRow row, uint32_t c, Change change) {
+__device__ __forceinline__ uint32_t fold_address(const FoldArgs& A, uint32_t id, MRow row, uint32_t c, Change change,
+                                                 uint32_t cnt_after = 0) {
     const DampArgs& da = A.da;
     bool ex = row.exists != 0;
     uint8_t st = row.status;
@@ -138,7 +139,7 @@ __device__ __forceinline__ uint32_t fold_address(const FoldArgs& A, uint32_t id,
             da.exc[j] = exc ? 1 : 0;
         }
     }
-    row_store(A.rows + id, in, st, ex ? 1 : 0);
+    row_store(A.rows + id, in, st, ex ? 1 : 0, cnt_after);
     if (da.score) {
         da.score[id] = sc;
         da.last[id] = ls;
@@ -219,14 +220,16 @@ __global__ __launch_bounds__(256) void k_fold(const uint32_t* __restrict__ sk, c
 //   k_link: every change takes its rank among its address's changes from an atomic on the
 //   address's row counter (arbitrary order), keeps it (rk), and a change of rank 1..kSlots
 //   writes its batch index into the address's inline slot array. Rank kSlots + 1 (an address
-//   with more than kSlots + 1 changes) sets *ovf, and the sorted path folds the batch instead.
+//   with more than kSlots + 1 changes) sets *ovf.
 //   k_fold_fast: the rank-0 change of every address loads the row (count included) and, for a
 //   repeated address, its slots (contiguous, no dependent list walk), puts the indices in
-//   arrival order in registers and folds them.
+//   arrival order in registers and folds them. An address with more changes is marked
+//   (counter = kOvfMark) and left to k_fold_ovf, one gated launch after it.
 // Each address costs one atomic, one 16-B row load and one 16-B row store; the batch's applied
 // counter is cleared by k_link, so the batch needs no memset.
 constexpr uint32_t kSlots = 15;  // changes per address on the grouped path: kSlots + 1
-constexpr uint32_t kDoneWords = 4;  // [0] k_fold_fast, [1] k_fold, [2] k_mck? (spare)
+constexpr uint32_t kOvfMark = 0xFFFFFFFFu;  // row counter of an address left to k_fold_ovf
+constexpr uint32_t kDoneWords = 4;  // [0] spare, [1] k_fold, [2] k_ovf_len's ticket, [3] spare
 
 __global__ void k_link(const uint32_t* __restrict__ ids, uint32_t k, MRow* __restrict__ rows,
                        uint32_t* __restrict__ slots, uint8_t* __restrict__ rk, uint32_t* __restrict__ ovf,
@@ -241,19 +244,19 @@ __global__ void k_link(const uint32_t* __restrict__ ids, uint32_t k, MRow* __res
     if (r == kSlots + 1u) *ovf = 1u;
 }
 
-// The workgroup's applied count goes to part[blockIdx.x] (summed by the gated-off k_fold).
+// The workgroup's applied count goes to part[blockIdx.x] (summed by k_ovf_len or k_fold_ovf).
 __global__ __launch_bounds__(256) void k_fold_fast(const uint32_t* __restrict__ ids, uint32_t k,
                                                    const uint8_t* __restrict__ rk, const uint32_t* __restrict__ slots,
-                                                   const uint32_t* __restrict__ ovf, FoldArgs A,
-                                                   uint32_t* __restrict__ part) {
-    if (*ovf) return;
+                                                   FoldArgs A, uint32_t* __restrict__ part) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t napp = 0;
     if (i < k && rk[i] == 0) {
         const uint32_t id = ids[i];
         const MRow row = row_load(A.rows + id);
         const uint32_t c = row.cnt;
-        if (c <= 1) {
+        if (c > kSlots + 1) {  // more changes than slots: marked for k_fold_ovf
+            A.rows[id].cnt = kOvfMark;
+        } else if (c <= 1) {
             napp = fold_address(A, id, row, 1, [&](uint32_t) { return i; });
         } else {
             uint32_t idx[kSlots + 1];
@@ -273,6 +276,102 @@ __global__ __launch_bounds__(256) void k_fold_fast(const uint32_t* __restrict__ 
     }
     napp = block_sum256(napp);
     if (threadIdx.x == 0) part[blockIdx.x] = napp;
+    if (threadIdx.x == 0 && blockIdx.x == 0) part[gridDim.x] = 0;  // the overflow fold's count (k_ovf_len)
+}
+
+// The grouped path's overflow fold: the addresses k_fold_fast marked (more than kSlots + 1
+// changes in the batch), folded by one workgroup of NT threads over the batch in NT-change
+// chunks in arrival order: a chunk's marked changes are compacted, sorted by (address,
+// arrival) in LDS and folded one lane per address segment, the rows keeping the mark until the
+// last chunk; then the marks are cleared. An address's changes are applied in arrival order, as
+// the sequential fold does. Returns this thread's applied count.
+template <int NT>
+__device__ uint32_t ovf_fold(const uint32_t* __restrict__ ids, uint32_t k, const FoldArgs& A) {
+    __shared__ uint64_t s_key[NT];
+    __shared__ uint32_t s_cnt[NT / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    uint32_t napp = 0;
+    for (uint32_t c0 = 0; c0 < k; c0 += NT) {
+        const uint32_t i = c0 + tid;
+        uint32_t id = 0;
+        bool f = false;
+        if (i < k) {
+            id = ids[i];
+            f = __hip_atomic_load(&A.rows[id].cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == kOvfMark;
+        }
+        const uint64_t bal = __ballot(f);
+        if (lane == 0) s_cnt[wv] = (uint32_t)__popcll(bal);
+        __syncthreads();
+        uint32_t base = 0, m = 0;
+        for (uint32_t w = 0; w < NT / 64; w++) {
+            base += w < wv ? s_cnt[w] : 0u;
+            m += s_cnt[w];
+        }
+        if (m == 0) {  // uniform
+            __syncthreads();
+            continue;
+        }
+        const uint32_t pos = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+        if (f) s_key[pos] = ((uint64_t)id << 32) | i;
+        uint32_t np = 1;
+        while (np < m) np <<= 1;
+        if (tid >= m && tid < np) s_key[tid] = ~0ull;
+        __syncthreads();
+        for (uint32_t k2 = 2; k2 <= np; k2 <<= 1)
+            for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
+                const uint32_t x = tid ^ j;
+                if (tid < np && x > tid) {
+                    const uint64_t a = s_key[tid], b = s_key[x];
+                    if ((a > b) == ((tid & k2) == 0)) {
+                        s_key[tid] = b;
+                        s_key[x] = a;
+                    }
+                }
+                __syncthreads();
+            }
+        if (tid < m) {
+            const uint32_t sid = (uint32_t)(s_key[tid] >> 32);
+            if (tid == 0 || (uint32_t)(s_key[tid - 1] >> 32) != sid) {
+                uint32_t c = 1;
+                while (tid + c < m && (uint32_t)(s_key[tid + c] >> 32) == sid) c++;
+                napp += fold_address(A, sid, row_load(A.rows + sid), c,
+                                     [&](uint32_t q) { return (uint32_t)s_key[tid + q]; }, kOvfMark);
+            }
+        }
+        __syncthreads();
+    }
+    for (uint32_t i = tid; i < k; i += NT) {
+        const uint32_t id = ids[i];
+        if (A.rows[id].cnt == kOvfMark) A.rows[id].cnt = 0;
+    }
+    return napp;
+}
+
+// The grouped path's third launch when the batch's checksum string is not built (deferred, or
+// another replica's batch): gated off (*ovf == 0, the normal case) it only sums the fold's
+// per-workgroup applied counts into *A.n_applied (the checksum gate) and *out; gated on, it
+// runs the overflow fold first and resets *ovf.
+__global__ __launch_bounds__(1024) void k_fold_ovf(const uint32_t* __restrict__ ids, uint32_t k,
+                                                   uint32_t* __restrict__ ovf, FoldArgs A,
+                                                   const uint32_t* __restrict__ part, uint32_t nparts,
+                                                   uint32_t* __restrict__ out) {
+    __shared__ uint32_t s_on, s_w[16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid == 0) s_on = *ovf;
+    __syncthreads();
+    uint32_t v = s_on ? ovf_fold<1024>(ids, k, A) : 0u;
+    for (uint32_t b = tid; b < nparts; b += 1024) v += part[b];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) s_w[wv] = v;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < 16; w++) t += s_w[w];
+        *A.n_applied = t;
+        if (out) *out = t;
+        if (s_on) *ovf = 0;
+    }
 }
 
 // Membership._decayMembersDampScore (index.js:374-383): decayDampScore on every member
@@ -342,32 +441,154 @@ __global__ void k_set_apply(const uint32_t* __restrict__ mark, const uint32_t* _
     }
 }
 
-// generateChecksumString pieces (index.js:115-120): address + status + incarnation + ';'
-// The checksum string in one launch (round 2): a tile of 256 x kMckItems members in address
-// order computes its pieces' lengths, finds its byte offset by decoupled look-back over the
-// tiles (rp_prims.h), and writes its pieces; the last tile records the slot's meta. This
-// replaces k_mck_len + the scan + k_mck_write + k_slot_meta (four launches per checksummed
-// batch). Gated off (*gate == 0), every workgroup still takes its ticket and tile 0 records
-// the meta.
+// generateChecksumString pieces (index.js:115-120): address + status + incarnation + ';' per
+// member in address order, in two launches after the fold (round 3; round 2's single launch
+// found each tile's offset by decoupled look-back behind a ticket counter, and its 391
+// same-address ticket atomics plus the look-back chain cost more than a second launch):
+//   k_ovf_len: the grouped fold's third step (the overflow fold when *ovf is set, and the
+//   batch's applied count into the checksum gate) and, per tile of 256 members, the sum of the
+//   pieces' lengths into tile_tot (always: it reflects the table after the fold).
+//   k_mck_write: each tile sums the totals of the tiles before it (a few hundred words read in
+//   parallel), scans its own lengths, assembles its pieces in LDS and stores them as aligned
+//   16-byte words; the last tile records the slot's meta. Gated off (*gate == 0), tile 0 only
+//   records the meta.
 
 static bool getenv_on(const char* name) {
     const char* v = getenv(name);
     return v && *v && *v != '0';
 }
-template <int kMckItems>
-__global__ __launch_bounds__(256) void k_mck_build(const uint32_t* __restrict__ order, uint32_t n,
+constexpr uint32_t kMckStage = 24576;  // LDS bytes a tile's pieces are assembled in
+
+// One member's piece: row, length and (for names of at most 28 bytes plus alignment) the
+// name's aligned dwords, loaded together before the tile's scan so their latency overlaps it.
+struct MckItem {
+    uint32_t id, len, nlen, sh;
+    MRow row;
+    uint64_t noff;
+    uint32_t w[8];
+};
+__device__ __forceinline__ void mck_load(uint32_t i, const uint32_t* __restrict__ order, uint32_t n,
+                                         const MRow* __restrict__ rows, const uint64_t* __restrict__ noff,
+                                         MckItem& t) {
+    t.id = i < n ? order[i] : 0u;
+    t.row = row_load(rows + t.id);
+    t.noff = noff[t.id];
+    t.nlen = (uint32_t)(noff[t.id + 1] - t.noff);
+    t.len = (i < n && t.row.exists) ? t.nlen + status_len(t.row.status) + dec_len(t.row.inc) + 1u : 0u;
+}
+__device__ __forceinline__ void mck_load_name(const uint8_t* __restrict__ names, MckItem& t) {
+    const uint8_t* src = names + t.noff;
+    t.sh = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 3u);
+    const uint32_t* a4 = reinterpret_cast<const uint32_t*>(src - t.sh);
+    const uint32_t nw = t.len && t.sh + t.nlen <= 32u ? (t.sh + t.nlen + 3u) >> 2 : 0u;
+#pragma unroll
+    for (int k = 0; k < 8; k++) t.w[k] = (uint32_t)k < nw ? a4[k] : 0u;
+}
+// address + status + incarnation + ';' at o (global or LDS)
+__device__ __forceinline__ void mck_emit(uint8_t* o, const uint8_t* __restrict__ names, const MckItem& t) {
+    const uint32_t L = t.nlen;
+    if (t.sh + L <= 32u) {
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+#pragma unroll
+            for (int bb = 0; bb < 4; bb++) {
+                const int q = 4 * k + bb - (int)t.sh;
+                if (q >= 0 && q < (int)L) o[q] = (uint8_t)(t.w[k] >> (8 * bb));
+            }
+    } else {
+        const uint8_t* src = names + t.noff;
+        for (uint32_t q = 0; q < L; q++) o[q] = src[q];
+    }
+    o += L;
+    const uint8_t stc = t.row.status;
+    const uint32_t sl = status_len(stc);
+    for (uint32_t q = 0; q < sl; q++) o[q] = status_char(stc, q);
+    o += sl;
+    const uint32_t dl = dec_len(t.row.inc);
+    dec_write(t.row.inc, o, dl);
+    o[dl] = ';';
+}
+
+// Grid: one workgroup per tile. When *ovf is set, the first workgroup to take a ticket runs the
+// overflow fold (its applied count to part[nparts]) and clears *ovf; the others wait for that
+// before reading rows (the ticket holder is running, so the wait ends). A workgroup that takes
+// ticket 0 after the fold finds *ovf clear and skips it; every ticket-0 holder resets the
+// counter when done, so it is 0 again after the launch. Workgroup 0 then sums the applied
+// counts into *A.n_applied and *out.
+__global__ __launch_bounds__(256) void k_ovf_len(const uint32_t* __restrict__ order, uint32_t n,
+                                                 const uint64_t* __restrict__ noff, uint32_t* __restrict__ tile_tot,
+                                                 const uint32_t* __restrict__ ids, uint32_t k, uint32_t* ovf, FoldArgs A,
+                                                 uint32_t* part, uint32_t nparts, uint32_t* __restrict__ out,
+                                                 uint32_t* tick, uint32_t* err) {
+    __shared__ uint32_t s_on, s_t, s_w[4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid == 0) s_on = __hip_atomic_load(ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (s_on) {  // rare: uniform per workgroup
+        if (tid == 0) s_t = atomicAdd(tick, 1u);
+        __syncthreads();
+        if (s_t == 0) {
+            if (tid == 0) s_on = __hip_atomic_load(ovf, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            if (s_on) {
+                const uint32_t v = block_sum256(ovf_fold<256>(ids, k, A));
+                if (tid == 0) {
+                    part[nparts] = v;
+                    __hip_atomic_store(ovf, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            if (tid == 0) __hip_atomic_store(tick, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (tid == 0) {
+            uint32_t spin = 0;
+            while (__hip_atomic_load(ovf, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+                if (++spin == kLbSpinCap) {
+                    atomicOr(err, kErrSpin);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        __syncthreads();
+    }
+    MckItem t;
+    mck_load(blockIdx.x * 256u + tid, order, n, A.rows, noff, t);
+    const uint32_t total = block_sum256(t.len);
+    if (tid == 0) tile_tot[blockIdx.x] = total;
+    if (blockIdx.x == 0) {
+        uint32_t v = 0;
+        for (uint32_t b = tid; b <= nparts; b += 256) v += part[b];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+        __syncthreads();
+        if (lane == 0) s_w[wv] = v;
+        __syncthreads();
+        if (tid == 0) {
+            const uint32_t a = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+            *A.n_applied = a;
+            if (out) *out = a;
+        }
+    }
+}
+
+// The sorted path and Membership.set: the tile lengths alone (ungated; the gate is already set).
+__global__ __launch_bounds__(256) void k_mck_len(const uint32_t* __restrict__ order, uint32_t n,
+                                                 const MRow* __restrict__ rows, const uint64_t* __restrict__ noff,
+                                                 uint32_t* __restrict__ tile_tot) {
+    MckItem t;
+    mck_load(blockIdx.x * 256u + threadIdx.x, order, n, rows, noff, t);
+    const uint32_t total = block_sum256(t.len);
+    if (threadIdx.x == 0) tile_tot[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(256) void k_mck_write(const uint32_t* __restrict__ order, uint32_t n,
                                                    const MRow* __restrict__ rows, const uint8_t* __restrict__ names,
                                                    const uint64_t* __restrict__ noff, const uint32_t* __restrict__ gate,
-                                                   uint8_t* __restrict__ buf, uint32_t* __restrict__ meta, uint64_t* lb,
-                                                   unsigned long long* ctr, uint64_t tag, uint32_t ntiles,
-                                                   uint32_t* err) {
-    __shared__ uint32_t s_gate, s_excl;
-    __shared__ uint32_t s_wsum[4];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    if (tid == 0) s_gate = gate ? *gate : 1u;
-    const uint32_t tile = take_unit(ctr, ntiles, err);  // (syncs)
-    if (tile >= ntiles) return;  // a ticket count out of step (reported): never write out of bounds
-    if (!s_gate) {
+                                                   const uint32_t* __restrict__ tile_tot, uint8_t* __restrict__ buf,
+                                                   uint32_t* __restrict__ meta) {
+    __shared__ uint32_t s_wsum[4], s_pre[4];
+    __shared__ uint32_t s_stage[kMckStage / 4 + 4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, tile = blockIdx.x;
+    if (gate && *gate == 0) {
         if (tile == 0 && tid == 0) {
             meta[0] = 0;
             meta[1] = 0;
@@ -375,77 +596,76 @@ __global__ __launch_bounds__(256) void k_mck_build(const uint32_t* __restrict__ 
         }
         return;
     }
-    const uint32_t i0 = tile * (256u * kMckItems) + (uint32_t)tid * kMckItems;
-    uint32_t ids[kMckItems], len[kMckItems];
-    MRow row[kMckItems];
-    uint32_t sum = 0;
-#pragma unroll
-    for (int j = 0; j < kMckItems; j++) {
-        const uint32_t i = i0 + j;
-        ids[j] = i < n ? order[i] : 0u;
-        row[j] = row_load(rows + ids[j]);
-        len[j] = (i < n && row[j].exists)
-                     ? (uint32_t)(noff[ids[j] + 1] - noff[ids[j]]) + status_len(row[j].status) + dec_len(row[j].inc) + 1u
-                     : 0u;
-        sum += len[j];
-    }
-    // exclusive scan of the threads' sums
-    uint32_t x = sum;
+    uint32_t pre = 0;  // this thread's share of the earlier tiles' totals
+    for (uint32_t q = tid; q < tile; q += 256) pre += tile_tot[q];
+    MckItem t;
+    mck_load(tile * 256u + tid, order, n, rows, noff, t);
+    mck_load_name(names, t);
+    // inclusive scan of the lengths within each wave; wave totals and prefix shares
+    uint32_t x = t.len;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
+        if ((int)lane >= o) x += y;
     }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) pre += __shfl_xor(pre, o, 64);
     if (lane == 63) s_wsum[wv] = x;
+    if (lane == 0) s_pre[wv] = pre;
     __syncthreads();
     uint32_t wbase = 0, total = 0;
 #pragma unroll
-    for (int w = 0; w < 4; w++) {
+    for (uint32_t w = 0; w < 4; w++) {
         wbase += w < wv ? s_wsum[w] : 0u;
         total += s_wsum[w];
     }
-    if (tid == 0) lb_store(lb + tile, tag | (tile == 0 ? kLbP : kLbA) | total);
-    if (tid < 64) {
-        const uint32_t excl = lookback_wave(lb, tile, tag, err);
-        if (tid == 0) {
-            if (tile > 0) lb_store(lb + tile, tag | kLbP | (excl + total));
-            s_excl = excl;
-            if (tile == ntiles - 1) {
-                meta[0] = excl + total;
-                meta[1] = 1;
-                meta[3] = 0;
-            }
-        }
+    const uint32_t g0 = s_pre[0] + s_pre[1] + s_pre[2] + s_pre[3];
+    if (tid == 0 && tile == gridDim.x - 1) {
+        meta[0] = g0 + total;
+        meta[1] = 1;
+        meta[3] = 0;
     }
+    const uint32_t pos = wbase + x - t.len;  // this thread's first byte, tile-relative
+    if (total > kMckStage) {  // a tile of long names: each thread writes its piece straight out
+        if (t.len) mck_emit(buf + g0 + pos, names, t);
+        return;
+    }
+    // Staged: the pieces are assembled in LDS (byte writes there are cheap), then the tile leaves
+    // as aligned 16-byte stores; the tile's first and last partial 16 bytes, which it shares
+    // with its neighbours, are written bytewise.
+    uint8_t* const st = reinterpret_cast<uint8_t*>(s_stage);
+    if (t.len) mck_emit(st + pos, names, t);
     __syncthreads();
-    uint32_t pos = s_excl + wbase + x - sum;
+    const uint32_t a0 = g0 & ~15u, nch = (g0 + total - a0 + 15u) >> 4;
+    for (uint32_t c = tid; c < nch; c += 256) {
+        const uint32_t a = a0 + 16u * c;
+        if (a >= g0 && a + 16u <= g0 + total) {
+            const uint32_t l = a - g0, d = l >> 2, r = (l & 3u) * 8u;
+            uint32_t w[5];
 #pragma unroll
-    for (int j = 0; j < kMckItems; j++) {
-        if (len[j]) {
-            const uint32_t id = ids[j];
-            uint8_t* o = buf + pos;
-            const uint64_t b = noff[id];
-            const uint32_t L = (uint32_t)(noff[id + 1] - b);
-            for (uint32_t q = 0; q < L; q++) *o++ = names[b + q];
-            const uint8_t st = row[j].status;
-            const uint32_t sl = status_len(st);
-            for (uint32_t q = 0; q < sl; q++) *o++ = status_char(st, q);
-            const uint32_t dl = dec_len(row[j].inc);
-            dec_write(row[j].inc, o, dl);
-            o[dl] = ';';
+            for (int q = 0; q < 5; q++) w[q] = s_stage[d + q];
+            uint4 o;
+            o.x = r ? __builtin_amdgcn_alignbit(w[1], w[0], r) : w[0];
+            o.y = r ? __builtin_amdgcn_alignbit(w[2], w[1], r) : w[1];
+            o.z = r ? __builtin_amdgcn_alignbit(w[3], w[2], r) : w[2];
+            o.w = r ? __builtin_amdgcn_alignbit(w[4], w[3], r) : w[3];
+            *reinterpret_cast<uint4*>(buf + a) = o;
+        } else {
+            const uint32_t lo = a > g0 ? a : g0, hi = a + 16u < g0 + total ? a + 16u : g0 + total;
+            for (uint32_t q = lo; q < hi; q++) buf[q] = st[q - g0];
         }
-        pos += len[j];
     }
 }
 
 // the per-batch history (rp_members_checksum_shard): the group's update-batch slots (bit j of
 // mask) append {hash, gate} in slot order
-__global__ void k_ck_hist(const uint32_t* __restrict__ meta, uint32_t n, uint64_t mask_lo, uint64_t mask_hi,
-                          uint32_t* __restrict__ hist) {
+struct SlotMask {
+    uint64_t w[1024 / 64];
+};
+__global__ void k_ck_hist(const uint32_t* __restrict__ meta, uint32_t n, SlotMask mask, uint32_t* __restrict__ hist) {
     uint32_t c = 0;
     for (uint32_t j = 0; j < n; j++) {
-        const bool on = j < 64 ? (mask_lo >> j) & 1u : (mask_hi >> (j - 64)) & 1u;
-        if (!on) continue;
+        if (!((mask.w[j >> 6] >> (j & 63)) & 1u)) continue;
         hist[2 * c] = meta[4 * j + 1] ? meta[4 * j + 2] : 0u;
         hist[2 * c + 1] = meta[4 * j + 1];
         c++;
@@ -497,11 +717,12 @@ struct Members {
     // 128 chains (one workgroup each) takes about as long as one of 64, and the folds and string
     // builds of the next 128 batches take about as long (C3: 1.00-1.07 G updates/s against 0.86
     // with groups of 64, 0.44 with 32; RP_MEMBERS_GROUP_SLOTS overrides).
-    static constexpr uint32_t kMaxSlots = 256, kGroupSlots = 128, kMaxGroups = 4;
+    static constexpr uint32_t kMaxSlots = 1024, kGroupSlots = 128, kMaxGroups = 4;
     uint32_t nslots = 1, group_slots = 1, ngroups = 1;
     DevBuf<uint8_t> ck_buf;   // nslots strings of slot_bytes
     uint64_t slot_bytes = 0;
     DevBuf<uint32_t> ck_meta;  // [kMaxSlots][4]: total, gate, hash, done
+    DevBuf<uint32_t> ck_tiles;  // the string build's per-tile byte totals
     uint32_t npending = 0;     // pending strings in the current group
     // Batch-strided checksums over replicas (rp_members_checksum_shard): every replica folds every
     // batch; this one builds and hashes the strings of update batches b with b % ck_nsh == ck_sh
@@ -510,7 +731,8 @@ struct Members {
     uint64_t batch_no = 0;  // update batches (k > 0) seen
     DevBuf<uint32_t> ck_hist;
     uint32_t hist_cap = 0, hist_n = 0;
-    uint64_t pend_mask[2] = {0, 0};  // pending slots that are update batches (history)
+    static_assert(kMaxSlots <= sizeof(SlotMask) * 8, "one mask bit per slot");
+    SlotMask pend_mask = {};  // pending slots that are update batches (history)
     uint32_t cur_group = 0;
     hipStream_t pend_st = nullptr;  // the stream the pending strings were built on
     hipStream_t ck_st = nullptr;    // the side stream the chains run on
@@ -594,10 +816,9 @@ struct Members {
     }
 
     // Everything below is stream-ordered on `s` and never syncs with the host.
-    // Grouped path (every batch size): k_link + k_fold_fast; then the sorted path's launches,
-    // gated on the overflow word on the device (they exit at once unless an address had more
-    // than kSlots + 1 changes). The applied count goes to n_applied_out from the last workgroup
-    // of whichever fold ran.
+    // Grouped path (every batch size): k_link + k_fold_fast + k_fold_ovf (gated on the overflow
+    // word on the device: it folds only addresses with more than kSlots + 1 changes, and sums
+    // the applied count into n_applied_out). RP_MEMBERS_SORTED_FOLD=1: radix sort + k_fold.
     void update_dev(const uint32_t* ids, const uint8_t* chs, const int64_t* chi, uint32_t k, int64_t now_ms,
                     uint8_t* applied, uint8_t* nst, int64_t* ninc, uint32_t* n_applied_out, hipStream_t s) {
         if (s != st) RP_HIP(hipStreamSynchronize(st));
@@ -619,17 +840,23 @@ struct Members {
         uint32_t* ovf = napplied.p + 1;
         uint32_t* done = napplied.p + 2;
         const unsigned g = grid_for(k, 256);
+        const bool mine = ck_nsh <= 1 || batch_no % ck_nsh == ck_sh;
+        batch_no++;
+        const bool build = !defer_ck && mine;
         if (grouped_fold) {
             g_slots.reserve((uint64_t)cap * kSlots);
             g_rk.reserve(k);
             const unsigned g1 = (unsigned)((k + 255) / 256);
-            g_part.reserve(g1);
+            g_part.reserve(g1 + 1);
             hipLaunchKernelGGL(k_link, dim3(g1), dim3(256), 0, s, ids, k, rows.p, g_slots.p, g_rk.p, ovf, napplied.p);
-            hipLaunchKernelGGL(k_fold_fast, dim3(g1), dim3(256), 0, s, ids, k, g_rk.p, g_slots.p, ovf, A, g_part.p);
+            hipLaunchKernelGGL(k_fold_fast, dim3(g1), dim3(256), 0, s, ids, k, g_rk.p, g_slots.p, A, g_part.p);
             RP_HIP(hipGetLastError());
-            radix_sort_index(ids, sk.p, sv.p, k, 0, bits, s, ws, ovf);
-            hipLaunchKernelGGL(k_fold, dim3(g), dim3(256), 0, s, sk.p, sv.p, k, A, ovf, done + 1, n_applied_out,
-                               g_part.p, g1);
+            if (build && nt.size()) {  // the overflow fold rides on the string build's length launch
+                const OvfArgs ov{ids, k, ovf, A, g_part.p, g1, n_applied_out};
+                checksum_dev(s, napplied.p, true, &ov);
+                return;
+            }
+            hipLaunchKernelGGL(k_fold_ovf, dim3(1), dim3(1024), 0, s, ids, k, ovf, A, g_part.p, g1, n_applied_out);
         } else {
             RP_HIP(hipMemsetAsync(napplied.p, 0, sizeof(uint32_t), s));
             radix_sort_index(ids, sk.p, sv.p, k, 0, bits, s, ws);
@@ -637,9 +864,7 @@ struct Members {
                                nullptr, 0u);
         }
         RP_HIP(hipGetLastError());
-        const bool mine = ck_nsh <= 1 || batch_no % ck_nsh == ck_sh;
-        batch_no++;
-        if (!defer_ck && mine) checksum_dev(s, napplied.p, true);
+        if (build) checksum_dev(s, napplied.p, true);
     }
 
     // Membership.set over a stash of k changes (arrival order): merge, set, checksum once.
@@ -670,7 +895,17 @@ struct Members {
     // Membership.computeChecksum (index.js:48-75) gated on *gate != 0 (null = always): the
     // string is built now (it reflects the table after this batch) into the next slot; its hash
     // lands in ck when the group is flushed.
-    void checksum_dev(hipStream_t s, const uint32_t* gate, bool is_batch = false) {
+    // ov: the grouped fold's overflow step, run by the length launch (k_ovf_len).
+    struct OvfArgs {
+        const uint32_t* ids;
+        uint32_t k;
+        uint32_t* ovf;
+        FoldArgs A;
+        uint32_t* part;
+        uint32_t nparts;
+        uint32_t* out;
+    };
+    void checksum_dev(hipStream_t s, const uint32_t* gate, bool is_batch = false, const OvfArgs* ov = nullptr) {
         const uint32_t n = nt.size();
         if (!n) return;
         ck_len.reserve(n + 1);
@@ -708,25 +943,26 @@ struct Members {
         ck_meta.reserve(4 * kMaxSlots);
         uint8_t* buf = ck_buf.p + slot_bytes * slot_index(npending);
         {
-            const char* it = getenv("RP_MEMBERS_CK_ITEMS");  // A/B: members per thread
-            const int items = it && *it ? atoi(it) : 1;
-            const uint32_t per = 256u * (items == 2 ? 2u : items == 4 ? 4u : 1u);
-            const uint32_t ntl = (uint32_t)((n + per - 1) / per);
-            const LookBack L = lookback_prepare(ws, ntl, s);
-#define RP_MCK(I)                                                                                              \
-    hipLaunchKernelGGL((k_mck_build<I>), dim3(ntl), dim3(256), 0, s, nt.sorted.p, n, rows.p, nt.d_bytes.p,     \
-                       nt.d_noff.p, gate, buf, ck_meta.p + 4ull * slot_index(npending), L.words, L.ticket, L.tag,  \
-                       ntl, L.err)
-            if (items == 2)
-                RP_MCK(2);
-            else if (items == 4)
-                RP_MCK(4);
-            else
-                RP_MCK(1);
-#undef RP_MCK
+            const uint32_t ntl = (n + 255) / 256;
+            ck_tiles.reserve(ntl);
+            uint32_t* meta = ck_meta.p + 4ull * slot_index(npending);
+            if (ov) {
+                if (!ws.err.p) {
+                    ws.err.reserve(1);
+                    RP_HIP(hipMemsetAsync(ws.err.p, 0, sizeof(uint32_t), s));
+                }
+                hipLaunchKernelGGL(k_ovf_len, dim3(ntl), dim3(256), 0, s, nt.sorted.p, n, nt.d_noff.p, ck_tiles.p,
+                                   ov->ids, ov->k, ov->ovf, ov->A, ov->part, ov->nparts, ov->out,
+                                   napplied.p + 2 + 2, ws.err.p);
+            } else {
+                hipLaunchKernelGGL(k_mck_len, dim3(ntl), dim3(256), 0, s, nt.sorted.p, n, rows.p, nt.d_noff.p,
+                                   ck_tiles.p);
+            }
+            hipLaunchKernelGGL(k_mck_write, dim3(ntl), dim3(256), 0, s, nt.sorted.p, n, rows.p, nt.d_bytes.p,
+                               nt.d_noff.p, gate, ck_tiles.p, buf, meta);
         }
         RP_HIP(hipGetLastError());
-        if (is_batch && hist_cap) pend_mask[npending >> 6] |= 1ull << (npending & 63);
+        if (is_batch && hist_cap) pend_mask.w[npending >> 6] |= 1ull << (npending & 63);
         npending++;
     }
 
@@ -740,16 +976,17 @@ struct Members {
         hash_long_multi(ck_buf.p + slot_bytes * first, slot_bytes, npending, ck_meta.p + 4 * first, ck_st);
         hipLaunchKernelGGL(k_ck_commit, dim3(1), dim3(1), 0, ck_st, ck_meta.p + 4 * first, npending, ck.p);
         RP_HIP(hipGetLastError());
-        const uint32_t nb = (uint32_t)(__builtin_popcountll(pend_mask[0]) + __builtin_popcountll(pend_mask[1]));
+        uint32_t nb = 0;
+        for (uint64_t w : pend_mask.w) nb += (uint32_t)__builtin_popcountll(w);
         if (nb) {
             if (hist_n + nb > hist_cap)
                 throw Error(RP_ESTATE, "checksum history full (rp_members_checksum_shard history_cap)");
-            hipLaunchKernelGGL(k_ck_hist, dim3(1), dim3(1), 0, ck_st, ck_meta.p + 4 * first, npending, pend_mask[0],
-                               pend_mask[1], ck_hist.p + 2ull * hist_n);
+            hipLaunchKernelGGL(k_ck_hist, dim3(1), dim3(1), 0, ck_st, ck_meta.p + 4 * first, npending, pend_mask,
+                               ck_hist.p + 2ull * hist_n);
             RP_HIP(hipGetLastError());
             hist_n += nb;
         }
-        pend_mask[0] = pend_mask[1] = 0;
+        pend_mask = {};
         RP_HIP(hipEventRecord(ev_hashed[cur_group], ck_st));
         group_busy[cur_group] = true;
         cur_group = (cur_group + 1) % ngroups;

@@ -958,30 +958,36 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
         const uintptr_t p0 = reinterpret_cast<uintptr_t>(I.buf) + b0;
         const uint32_t sh = (uint32_t)(p0 & 3u);
         const uint32_t len = ok ? (uint32_t)len64 : 0u;
-        // stage: dwords wholly inside the batch's bytes [vb, ve), byte loads at the edges
-        if (ok) {  // all loads in flight before the first LDS store
-            constexpr int kIt = (kWBuf / 4 + 2 + 63) / 64;
+        // stage: dwords wholly inside the batch's bytes [vb, ve) go global -> LDS directly
+        // (global_load_lds: no registers held per load, so every load of the message is in
+        // flight at once), the few at the batch's edges bytewise through registers
+        if (ok) {
             const uintptr_t a0 = p0 - sh;
             const uint32_t nd = (sh + len + 3) / 4;
-            uint32_t xs[kIt];
-#pragma unroll
-            for (int q = 0; q < kIt; q++) {
+            uint32_t edge = 0, edge_d = ~0u;
+            const int nq = (int)((nd + 63) / 64);
+            for (int q = 0; q < nq; q++) {  // not unrolled: no per-q address kept live
                 const uint32_t d = lane + 64u * q;
                 const uintptr_t a = a0 + 4ull * d;
-                xs[q] = 0;
                 if (d < nd) {
                     if (a >= vb && a + 4 <= ve) {
-                        xs[q] = *reinterpret_cast<const uint32_t*>(a);
-                    } else {
+                        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(a), &W.buf[64u * q], 4, 0, 0);
+                    } else {  // at most two dwords of the whole batch (its first and last)
+                        uint32_t x = 0;
                         for (uint32_t j = 0; j < 4; j++)
                             if (a + j >= p0 && a + j < p0 + len)
-                                xs[q] |= (uint32_t)(*reinterpret_cast<const uint8_t*>(a + j)) << (8 * j);
+                                x |= (uint32_t)(*reinterpret_cast<const uint8_t*>(a + j)) << (8 * j);
+                        if (edge_d == ~0u) {
+                            edge_d = d;
+                            edge = x;
+                        } else {
+                            W.buf[d] = x;
+                        }
                     }
                 }
             }
-#pragma unroll
-            for (int q = 0; q < kIt; q++)
-                if (lane + 64u * q < nd) W.buf[lane + 64u * q] = xs[q];
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (edge_d != ~0u) W.buf[edge_d] = edge;
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -248,11 +248,13 @@ def test_checksum_groups_wrap_with_reads(gpu, orc, budget, monkeypatch):
 
 
 @pytest.mark.parametrize("sorted_fold", [False, True], ids=["grouped", "sorted"])
-def test_hot_addresses_take_the_sorted_path(gpu, orc, sorted_fold, monkeypatch):
-    """The grouped fold handles up to 16 changes per address in a batch; a batch where one
-    address has more (here 17 and 60, next to addresses with exactly 16 and 15) takes the sorted
-    path. Every batch - before, during and after the overflow - must match the oracle, and the
-    grouped fold's per-address state must be clean again after an overflowing batch."""
+def test_hot_addresses_take_the_overflow_fold(gpu, orc, sorted_fold, monkeypatch):
+    """The grouped fold handles up to 16 changes per address in a batch; an address with more
+    (here 17 and 60, next to addresses with exactly 16 and 15; later 3000 and 500 changes, so
+    one address fills whole 1024-change chunks of k_fold_ovf and spans several) is folded by
+    the gated overflow launch. Every batch - before, during and after the overflow - must match
+    the oracle, and the grouped fold's per-address state must be clean again after an
+    overflowing batch."""
     if sorted_fold:
         monkeypatch.setenv("RP_MEMBERS_SORTED_FOLD", "1")
     S = synth()
@@ -264,7 +266,8 @@ def test_hot_addresses_take_the_sorted_path(gpu, orc, sorted_fold, monkeypatch):
     m.update_ids(ids0, st0, inc0, now_ms=1)
     o.update_ids(ids0, st0, inc0, False, 1)
     rng = np.random.default_rng(5)
-    for b, hot in enumerate([{7: 16, 8: 15}, {7: 17, 9: 60, 10: 16}, {11: 3}, {12: 40}, {}]):
+    for b, hot in enumerate([{7: 16, 8: 15}, {7: 17, 9: 60, 10: 16}, {11: 3}, {12: 40}, {13: 3000, 14: 500},
+                             {13: 2}, {}]):
         ids, us, ui = S.c3_updates(n, 2000, seed=300 + b, base_inc=inc0 + 3 * b)
         ids, us, ui = list(ids), list(us), list(ui)
         for a, c in hot.items():
