@@ -63,7 +63,7 @@ constexpr int kHashWin = 512;      // LDS window of pre-mixed chunks for the blo
 constexpr uint8_t ST_MASK = 3, IN_RING = 0x80;
 constexpr uint32_t kMaxShards = 64;
 // error flags (rp_sim_step reports them)
-constexpr uint32_t ERR_CHANGES = 1, ERR_TIMERS = 2, ERR_ARENA = 4;
+constexpr uint32_t ERR_CHANGES = 1, ERR_TIMERS = 2, ERR_ARENA = 4, ERR_TWINFP = 8;
 
 // One piggybacked change on the wire (dissemination.js:163-170): 24 bytes.
 // w0 = address (bits 0-22) | status (bits 23-24) | aux (bits 25-31: a ping-req leg record's
@@ -135,8 +135,10 @@ struct SimDev {
     // sparse per node
     Change* chg;  // [lv][Cd]
     uint32_t* n_chg;
-    Timer* tim;  // [lv][Ct]
+    Timer* tim;  // [lv][Ct] appended in due order; [t_head, n_tim) are pending
     uint32_t* n_tim;
+    uint32_t* t_head;  // first pending timer (the ones before it have fired or lapsed)
+    uint64_t* vfp;     // [NL] twin fingerprint of each view, kept by block_apply (see twin_mix)
     // per local node
     int64_t* it_idx;
     uint32_t *n_shuf, *ring_count, *max_piggy, *checksum;
@@ -281,6 +283,7 @@ __device__ __forceinline__ uint32_t ld32(const uint8_t* p, uint64_t o) {
 struct Lds {
     uint32_t u[16];
     uint64_t u64;
+    unsigned long long fpd;  // block_apply: the batch's twin-fingerprint delta
     uint32_t win[2][kHashWin][8] __attribute__((aligned(16)));
     uint32_t pad[8];  // the chain's one-chunk lookahead past win[1]
 };
@@ -575,6 +578,14 @@ __device__ __forceinline__ uint32_t lshl_add(uint32_t a, uint32_t b) {
     asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(SH), "v"(b));
     return r;
 }
+__device__ __forceinline__ uint32_t lshl_add_v(uint32_t a, uint32_t sh, uint32_t b) {  // (a << sh) + b
+    uint32_t r;
+    asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(sh), "v"(b));
+    return r;
+}
+__device__ __forceinline__ uint32_t swap_pair(uint32_t v) {  // lanes 2i <-> 2i+1 (quad_perm 1,0,3,2)
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);
+}
 
 // Membership.computeChecksum (index.js:48-75) of local node lv by one workgroup, without
 // materialising the string: the view's deviated pieces are listed in address order with their
@@ -714,9 +725,10 @@ __device__ void block_checksum(const SimDev& S, uint32_t lv, uint8_t* scratch, L
             f = fh::rotr(f, 19) + 113;
         }
         // The chain in pre-added form (as rp_hashlong.hip): the state enters chunk j as
-        // hp = h + a_j, gp = g + b_j, fp = f + c_j, and chunk j's record holds
-        // {premix(d), premix(c), premix(b + e c1), K + e + a', 2K + a + d + c', 3K + 2a + d + b'}
-        // with a', b', c' the next chunk's first words (0 after the last chunk).
+        // hp = h + a_j, gp = g + b_j, fp = f + c_j, and chunk j's record holds one {premix,
+        // addend} pair per chain word: h {premix(d), K + e + a'}, g {premix(c), 3K + 2a + d + b'},
+        // f {premix(b + e c1), 2K + a + d + c'}, with a', b', c' the next chunk's first words (0
+        // after the last chunk).
         constexpr uint32_t kK = 0xe6546b64u;
         // the 20 bytes of chunk c as words (TabCursor C is advanced to c)
         auto chunk_words = [&](TabCursor& C, uint64_t c, uint32_t (&wd)[5]) {
@@ -749,10 +761,10 @@ __device__ void block_checksum(const SimDev& S, uint32_t lv, uint8_t* scratch, L
                 uint32_t nx[5] = {0, 0, 0, 0, 0};
                 if (c0 + j + 1 < iters) chunk_words(C, c0 + j + 1, nx);
                 uint32_t* r = L.win[wb][j];
-                *reinterpret_cast<uint4*>(r) =
-                    uint4{premix(wd[3]), premix(wd[2]), premix(wd[1] + wd[4] * fh::kC1), kK + wd[4] + nx[0]};
+                *reinterpret_cast<uint2*>(r) = uint2{premix(wd[3]), kK + wd[4] + nx[0]};
+                *reinterpret_cast<uint2*>(r + 2) = uint2{premix(wd[2]), 3u * kK + 2u * wd[0] + wd[3] + nx[1]};
                 *reinterpret_cast<uint2*>(r + 4) =
-                    uint2{2u * kK + wd[0] + wd[3] + nx[2], 3u * kK + 2u * wd[0] + wd[3] + nx[1]};
+                    uint2{premix(wd[1] + wd[4] * fh::kC1), 2u * kK + wd[0] + wd[3] + nx[2]};
 #pragma unroll
                 for (int i = 0; i < 5; i++) wd[i] = nx[i];
             }
@@ -764,13 +776,17 @@ __device__ void block_checksum(const SimDev& S, uint32_t lv, uint8_t* scratch, L
             TabCursor C0{0, NONE, Piece{}};
             uint32_t w0[5];
             chunk_words(C0, 0, w0);
-            L.u[0] = h + w0[0];
-            g += w0[1];
-            f += w0[2];
+            L.u[0] = g + w0[1];
+            L.u[1] = f + w0[2];
+            L.u[2] = h + w0[0];
         }
         fill(0, 0, tid, kT);
         __syncthreads();
-        uint32_t hp = L.u[0], gp = g, fp = f;
+        // the coupled (g, f) pair on lanes 0 and 1 of wave 0 (one instruction advances both, as
+        // rp_hashlong.hip), h on lane 64
+        const int ln = tid < 2 ? tid : 2;
+        uint32_t cv = (tid < 2 || tid == 64) ? L.u[ln] : 0u;
+        const uint32_t sh = tid == 0 ? 1u : 0u, sh2 = sh + 2u;
         __syncthreads();
         const uint64_t nwin = (iters + kHashWin - 1) / kHashWin;
         for (uint64_t w = 0; w < nwin; w++) {
@@ -783,48 +799,48 @@ __device__ void block_checksum(const SimDev& S, uint32_t lv, uint8_t* scratch, L
 #ifdef RP_CK_PROF
                 bt_fill += clock64() - tf0;
 #endif
-            } else if (tid == 0 || tid == 64) {
+            } else if (tid < 2 || tid == 64) {
 #ifdef RP_CK_PROF
                 const uint64_t tc0 = clock64();
 #endif
                 const uint64_t c0 = w * kHashWin;
                 const int n = (int)((iters - c0) < (uint64_t)kHashWin ? (iters - c0) : kHashWin);
-                if (tid == 0) {  // (g, f): LDS reads 8 chunks ahead of their steps
-                    auto step = [&](const uint4 x, const uint2 y) {
-                        const uint32_t rg = fh::rotr(gp ^ x.y, 19), rf = fh::rotr(fp ^ x.z, 19);
-                        fp = lshl_add<2>(rf + rg, (rf + rg) + y.x);
-                        const uint32_t s2 = lshl_add<1>(rg, rf);
-                        gp = lshl_add<2>(s2, s2 + y.y);
+                // lane 0 (g) reads record words 2-3, lane 1 (f) words 4-5, lane 64 (h) words 0-1;
+                // the pair: v' = 5 r_other + (5 (r_self << sh) + addend); h: 5 r + addend. LDS
+                // reads 8 chunks ahead of their steps.
+                if (tid < 2) {
+                    const int wo = 2 + 2 * tid;
+                    auto step = [&](const uint2 x) {
+                        const uint32_t y = cv ^ x.x;
+                        const uint32_t r = __builtin_amdgcn_alignbit(y, y, 19);
+                        const uint32_t r5 = lshl_add<2>(r, r);
+                        const uint32_t own = lshl_add_v(r, sh2, lshl_add_v(r, sh, x.y));
+                        cv = swap_pair(r5) + own;
                     };
                     int j = 0;
                     for (; j + 8 <= n; j += 8) {
-                        uint4 x[8];
-                        uint2 y[8];
+                        uint2 x[8];
 #pragma unroll
-                        for (int q = 0; q < 8; q++) {
-                            x[q] = *reinterpret_cast<const uint4*>(L.win[cur][j + q]);
-                            y[q] = *reinterpret_cast<const uint2*>(L.win[cur][j + q] + 4);
-                        }
-#pragma unroll
-                        for (int q = 0; q < 8; q++) step(x[q], y[q]);
-                    }
-                    for (; j < n; j++)
-                        step(*reinterpret_cast<const uint4*>(L.win[cur][j]),
-                             *reinterpret_cast<const uint2*>(L.win[cur][j] + 4));
-                } else {  // h
-                    auto step = [&](const uint4 x) {
-                        const uint32_t rh = fh::rotr(hp ^ x.x, 19);
-                        hp = lshl_add<2>(rh, rh + x.w);
-                    };
-                    int j = 0;
-                    for (; j + 8 <= n; j += 8) {
-                        uint4 x[8];
-#pragma unroll
-                        for (int q = 0; q < 8; q++) x[q] = *reinterpret_cast<const uint4*>(L.win[cur][j + q]);
+                        for (int q = 0; q < 8; q++) x[q] = *reinterpret_cast<const uint2*>(L.win[cur][j + q] + wo);
 #pragma unroll
                         for (int q = 0; q < 8; q++) step(x[q]);
                     }
-                    for (; j < n; j++) step(*reinterpret_cast<const uint4*>(L.win[cur][j]));
+                    for (; j < n; j++) step(*reinterpret_cast<const uint2*>(L.win[cur][j] + wo));
+                } else {
+                    auto step = [&](const uint2 x) {
+                        const uint32_t y = cv ^ x.x;
+                        const uint32_t r = __builtin_amdgcn_alignbit(y, y, 19);
+                        cv = lshl_add<2>(r, r + x.y);
+                    };
+                    int j = 0;
+                    for (; j + 8 <= n; j += 8) {
+                        uint2 x[8];
+#pragma unroll
+                        for (int q = 0; q < 8; q++) x[q] = *reinterpret_cast<const uint2*>(L.win[cur][j + q]);
+#pragma unroll
+                        for (int q = 0; q < 8; q++) step(x[q]);
+                    }
+                    for (; j < n; j++) step(*reinterpret_cast<const uint2*>(L.win[cur][j]));
                 }
 #ifdef RP_CK_PROF
                 if (tid == 0) bt_chain += clock64() - tc0;
@@ -832,12 +848,12 @@ __device__ void block_checksum(const SimDev& S, uint32_t lv, uint8_t* scratch, L
             }
             __syncthreads();
         }
-        if (tid == 64) L.u[1] = hp;
+        if (tid < 2 || tid == 64) L.u[ln] = cv;
         __syncthreads();
         if (tid == 0) {
-            h = L.u[1];  // the last chunk's next-words were 0: plain h, g, f
-            g = gp;
-            f = fp;
+            g = L.u[0];  // the last chunk's next-words were 0: plain h, g, f
+            f = L.u[1];
+            h = L.u[2];
             g = fh::rotr(g, 11) * fh::kC1;
             g = fh::rotr(g, 17) * fh::kC1;
             f = fh::rotr(f, 11) * fh::kC1;
@@ -1024,6 +1040,88 @@ __device__ void lane_pass1(const SimDev& S, const LaneView& V, uint4* dl, int64_
             last = k;
         }
     }
+}
+
+// lane_pass1 by a segment of SEG lanes of one wave (lane sl of the segment; act and the view are
+// segment-uniform, every lane of the segment calls it). Each lane takes a contiguous run of
+// bitmap words; the record offsets and the running shift come from segment scans, so the list is
+// the one lane_pass1 writes (a piece too long for its record makes nd exceed dcap the same way).
+// One lane walking ~1,000 deviated members through their dependent loads took milliseconds (the
+// D1 senders at C5); SEG lanes take 1/SEG of it.
+template <int SEG>
+__device__ void seg_pass1(const SimDev& S, const LaneView& V, uint4* dl, bool act, uint32_t sl, int64_t& dtot,
+                          int64_t& dlo, int64_t& dhi, uint32_t& last, uint32_t& nd) {
+    const uint32_t per = (S.W + SEG - 1) / SEG;
+    const uint32_t w0 = min(S.W, sl * per), w1 = min(S.W, w0 + per);
+    uint32_t cnt = 0;
+    if (act)
+        for (uint32_t w = w0; w < w1; w++) cnt += __builtin_popcount(V.dev[w]);
+    // exclusive scan of the counts over the segment
+    uint32_t inc = cnt;
+#pragma unroll
+    for (int o = 1; o < SEG; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o, SEG);
+        if (sl >= (uint32_t)o) inc += t;
+    }
+    const uint32_t total = __shfl(inc, SEG - 1, SEG);
+    uint32_t idx = inc - cnt;
+    int64_t run = 0, lmin = 0, lmax = 0;
+    uint32_t llast = NONE;
+    bool big = false;
+    if (act) {
+        for (uint32_t w = w0; w < w1; w++) {
+            uint32_t bits = V.dev[w];
+            while (bits) {
+                const uint32_t k = (w << 5) + __builtin_ctz(bits);
+                bits &= bits - 1;
+                const uint32_t a = S.sorted[k];
+                const uint8_t st = V.strow[a] & ST_MASK;
+                const int64_t x = V.incrow[a], x0 = S.inc0[a];
+                int64_t d = (int64_t)status_len(st) - 5;
+                if (x != x0) d += (int64_t)dec_len(x) - (int64_t)dec_len(x0);
+                if (idx < S.dcap) {
+                    const uint32_t bpos = (uint32_t)S.boff[k];
+                    const uint32_t blen = (uint32_t)(S.boff[k + 1] - bpos);
+                    const uint32_t nl = (uint32_t)(S.noff[a + 1] - S.noff[a]);
+                    const uint32_t plen = (uint32_t)((int64_t)blen + d);
+                    if (plen > 0xFFu) big = true;
+                    dl[idx] = uint4{bpos, a, blen | (nl << 8) | ((uint32_t)st << 16) | ((x == x0 ? 1u : 0u) << 18) |
+                                                 (plen << 19),
+                                    k};
+                }
+                idx++;
+                run += d;
+                lmin = run < lmin ? run : lmin;
+                lmax = run > lmax ? run : lmax;
+                llast = k;
+            }
+        }
+    }
+    // the running shift: exclusive scan of the lanes' sums, then min / max over the segment
+    int64_t rin = run;
+#pragma unroll
+    for (int o = 1; o < SEG; o <<= 1) {
+        const int64_t t = __shfl_up(rin, o, SEG);
+        if (sl >= (uint32_t)o) rin += t;
+    }
+    const int64_t ex = rin - run;
+    int64_t mn = ex + lmin, mx = ex + lmax;
+    uint32_t lst = llast == NONE ? 0u : llast + 1u;
+    uint32_t bg = big ? 1u : 0u;
+#pragma unroll
+    for (int o = SEG / 2; o > 0; o >>= 1) {
+        const int64_t a = __shfl_xor(mn, o, SEG), b = __shfl_xor(mx, o, SEG);
+        mn = a < mn ? a : mn;
+        mx = b > mx ? b : mx;
+        const uint32_t c = __shfl_xor(lst, o, SEG);
+        lst = c > lst ? c : lst;
+        bg |= __shfl_xor(bg, o, SEG);
+    }
+    dtot = __shfl(rin, SEG - 1, SEG);
+    dlo = mn < 0 ? mn : 0;
+    dhi = mx > 0 ? mx : 0;
+    last = lst ? lst - 1u : NONE;
+    nd = bg && total <= S.dcap ? S.dcap + 1u : total;  // an oversize piece: the lane path's fallback
 }
 
 // Every live local node whose view changed: one node per lane, the wave's 64 chains in lockstep
@@ -1560,13 +1658,283 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_ck_pc(SimDev S, const uint32_
     }
 }
 
+// The chains of k_ck_pc for a short list of views (D1's ping-req senders, whose checksums their
+// ping-req bodies carry: ~1 % of the nodes, so a few groups on an idle machine and the refresh is
+// a latency bound). The coupled (g, f) pair runs on two lanes in the pre-added form of
+// rp_hashlong.hip (one instruction advances both: six VALU ops per chunk, four of them on the
+// dependent path, against k_ck_pc's one lane per view), so a workgroup holds VPG <= 32 views.
+// Waves: 0 = the pairs (lane 2i: g of view i, lane 2i + 1: f); 1 = the h chains (lane i < VPG;
+// also the chain init per view; pass 1 runs on every wave, SEG lanes per view: seg_pass1); 2..NP+1 = producers, lane = (view lane % VPG, part
+// lane / VPG): producer p's part hf makes chunks [e kEp + CP (NPART p + hf), + CP) of epoch e.
+// Producers are the bound when views carry many deviated pieces (a wave waits for its slowest
+// lane's piece overlay every call), so D1 takes 16 views per group: twice the chunks per epoch
+// for the same producer calls, and the chain waves set the pace. A chunk's
+// record per chain word: h {premix(d), K + e + a'}, g {premix(c), 3K + 2a + d + b'}, f
+// {premix(b + e c1), 2K + a + d + c'} with a', b', c' the next chunk's first words (0 after the
+// last), so a producer also reads the first words of the chunk after its run.
+template <int NP, int CP, int VPG>
+__global__ __launch_bounds__(64 * (NP + 2)) void k_ck_pair(SimDev S, const uint32_t* __restrict__ sel,
+                                                          const uint32_t* __restrict__ nsel) {
+    static_assert(VPG == 8 || VPG == 16 || VPG == 32, "views per group");
+    constexpr int NPART = 64 / VPG;       // producer lanes per view in a wave
+    constexpr int kEp = NPART * CP * NP;  // chunks per epoch
+    static_assert(kEp % 8 == 0, "the chain loads 8 records ahead");
+    constexpr uint32_t kK = 0xe6546b64u;
+    __shared__ __attribute__((aligned(16))) uint32_t ring[kRingW + 24];
+    __shared__ __attribute__((aligned(16))) uint2 stage[2][kEp][3][VPG];  // role 0: h, 1: g, 2: f
+    __shared__ uint32_t s_nd[VPG], s_iters[VPG], s_st[3][VPG], s_w0[3][VPG], s_last[VPG];
+    __shared__ int64_t s_dtot[VPG], s_dlo[VPG], s_dhi[VPG];
+    constexpr int SEG = 64 * (NP + 2) / VPG;  // lanes per view for pass 1
+    static_assert(SEG <= 64 && (SEG & (SEG - 1)) == 0, "pass-1 segments within a wave");
+    __shared__ int32_t s_red[4];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // the lane's view (wave 0: lanes >= 2 VPG idle; wave 1: lanes >= VPG idle)
+    const uint32_t vi = wv == 0 ? (uint32_t)lane >> 1 : wv == 1 ? (uint32_t)lane : (uint32_t)lane % VPG;
+    uint32_t lv = vi < VPG ? blockIdx.x * VPG + vi : NONE;
+    if (sel && lv != NONE) lv = lv < *nsel ? sel[lv] : NONE;
+    const bool act = lv < S.NL && !S.dead[S.v0 + lv] && S.dirty[lv];
+    if (!__syncthreads_or(act ? 1 : 0)) return;
+    const uint32_t N = S.N;
+    const uint64_t row = (uint64_t)(act ? lv : 0) * N;
+    const LaneView V{S, S.st + row, S.inc + row, S.dev + (uint64_t)(act ? lv : 0) * S.W};
+    uint4* dl = S.dlist + (uint64_t)(act ? lv : 0) * S.dcap;
+    {  // pass 1, SEG lanes per view
+        const uint32_t sv = threadIdx.x / SEG, sl = threadIdx.x % SEG;
+        uint32_t slv = blockIdx.x * VPG + sv;
+        if (sel) slv = slv < *nsel ? sel[slv] : NONE;
+        const bool sact = slv < S.NL && !S.dead[S.v0 + slv] && S.dirty[slv];
+        const uint64_t srow = (uint64_t)(sact ? slv : 0) * N;
+        const LaneView SV{S, S.st + srow, S.inc + srow, S.dev + (uint64_t)(sact ? slv : 0) * S.W};
+        int64_t dt, dlo1, dhi1;
+        uint32_t la, nd1;
+        seg_pass1<SEG>(S, SV, S.dlist + (uint64_t)(sact ? slv : 0) * S.dcap, sact, sl, dt, dlo1, dhi1, la, nd1);
+        if (sl == 0) {
+            s_dtot[sv] = dt;
+            s_dlo[sv] = dlo1;
+            s_dhi[sv] = dhi1;
+            s_last[sv] = la;
+            s_nd[sv] = nd1;
+        }
+    }
+    __syncthreads();
+    uint32_t hdone = 0;
+    if (wv == 1) {
+        int64_t dtot = 0, dlo = 0, dhi = 0;
+        uint32_t last = NONE, nd = 0;
+        if (act) {
+            dtot = s_dtot[lane];
+            dlo = s_dlo[lane];
+            dhi = s_dhi[lane];
+            last = s_last[lane];
+            nd = s_nd[lane];
+        }
+        const uint64_t len = (uint64_t)((int64_t)S.boff[N] + dtot);
+        const bool bad = act && (nd > S.dcap || len > 0x7FFFFFF0ull);
+        uint32_t iters = 0, h = 0, g = 0, f = 0;
+        bool done = false;
+        if (act && !bad) {
+            lane_chain_init(S, V, len, dtot, last, h, g, f, done);
+            iters = done ? 0u : (uint32_t)((len - 1) / 20);
+        }
+        hdone = h;
+        if (lane < VPG) {
+            s_iters[lane] = iters;
+            s_st[0][lane] = h;
+            s_st[1][lane] = g;
+            s_st[2][lane] = f;
+        }
+        const int64_t DLO = wave_min64(act ? dlo : 0), DHI = wave_max64(act ? dhi : 0);
+        const bool okw = __ballot(bad) == 0 && DHI - DLO <= (int64_t)(kRing - 3 * kSlice - 4 * kEp * 20 - 256);
+        const int64_t MX = wave_max64((int64_t)iters);
+        if (lane == 0) {
+            s_red[0] = okw ? 1 : 0;
+            s_red[1] = (int32_t)DLO;
+            s_red[2] = (int32_t)MX;
+        }
+    }
+    __syncthreads();
+    if (!s_red[0]) {  // block-uniform: too many deviations for the list or the ring
+        if (wv == 1 && act) {
+            S.checksum[lv] = lane_checksum(S, lv);
+            S.dirty[lv] = 0;
+        }
+        return;
+    }
+    const int32_t DLO = s_red[1];
+    const uint32_t maxit = (uint32_t)s_red[2];
+    const uint32_t nep = (maxit + kEp - 1) / kEp;
+    const uint32_t lead = (uint32_t)(2 * kEp * 20 + 64 - DLO) + kSlice;
+    const uint32_t iters = vi < VPG ? s_iters[vi] : 0u;
+    BaseRing R;
+    R.ring = ring;
+    R.hi = 0;
+    LaneCursor C;
+    const int pw = wv - 2, hf = lane / VPG;
+    if (wv >= 2) {
+        if (act && iters) C.init(S, V, dl, s_nd[vi]);
+        if (wv == 2) {
+            R.start(S.sbase, lane);
+            R.ensure(S.sbase, lead, lane);  // epochs 0 and 1
+        }
+    }
+    auto produce = [&](uint32_t e) {
+        const uint32_t c0 = e * kEp + CP * (NPART * pw + hf);
+        const uint32_t ng = c0 >= iters ? 0u : (iters - c0 < (uint32_t)CP ? iters - c0 : (uint32_t)CP);
+        if (!ng) return;
+        const uint32_t ngx = ng + (c0 + ng < iters ? 1u : 0u);  // + the next chunk, if any
+        const uint32_t q = c0 * 20;
+        while (q >= C.pend && C.cur.w < N) C.advance(S, V);
+        uint32_t w4[CP + 1][5];
+        {
+            const uint32_t o = (uint32_t)((int32_t)q - C.delta);
+            const uint32_t* p = R.ring + ((o >> 2) & (kRingW - 1));
+            const uint32_t sh = o & 3;
+            uint32_t x[5 * CP + 4];
+#pragma unroll
+            for (int i = 0; i < 5 * CP + 4; i++) x[i] = p[i];
+#pragma unroll
+            for (int j = 0; j < CP; j++)
+#pragma unroll
+                for (int i = 0; i < 5; i++) w4[j][i] = __builtin_amdgcn_alignbyte(x[5 * j + i + 1], x[5 * j + i], sh);
+#pragma unroll
+            for (int i = 0; i < 3; i++) w4[CP][i] = __builtin_amdgcn_alignbyte(x[5 * CP + i + 1], x[5 * CP + i], sh);
+            w4[CP][3] = w4[CP][4] = 0;
+        }
+        if (__builtin_expect(q + 20 * ngx > C.pos, 0)) {
+            const uint32_t j0 = C.pos > q ? (C.pos - q) / 20 : 0;
+            for (uint32_t j = j0; j < ngx; j++) {
+                uint32_t w[5];
+                cursor_chunk(S, V, C, R, q + 20 * j, w);
+#pragma unroll
+                for (int jj = 0; jj <= CP; jj++)
+                    if ((uint32_t)jj == j)
+#pragma unroll
+                        for (int i = 0; i < 5; i++) w4[jj][i] = w[i];
+            }
+        }
+        if (c0 == 0) {  // chunk 0's first words pre-add the chain state
+            s_w0[0][vi] = w4[0][0];
+            s_w0[1][vi] = w4[0][1];
+            s_w0[2][vi] = w4[0][2];
+        }
+        const int b = e & 1;
+#pragma unroll
+        for (int j = 0; j < CP; j++) {
+            if ((uint32_t)j < ng) {
+                const bool nx = (uint32_t)j + 1 < ngx;
+                const uint32_t a1 = nx ? w4[j + 1][0] : 0u, b1 = nx ? w4[j + 1][1] : 0u, c1 = nx ? w4[j + 1][2] : 0u;
+                const uint32_t a = w4[j][0], bb = w4[j][1], cc = w4[j][2], d = w4[j][3], ee = w4[j][4];
+                const int slot = CP * (NPART * pw + hf) + j;
+                stage[b][slot][0][vi] = uint2{premix(d), kK + ee + a1};
+                stage[b][slot][1][vi] = uint2{premix(cc), 3u * kK + 2u * a + d + b1};
+                stage[b][slot][2][vi] = uint2{premix(bb + ee * fh::kC1), 2u * kK + a + d + c1};
+            }
+        }
+    };
+    __syncthreads();  // the ring holds epochs 0 and 1
+    if (wv >= 2 && act) produce(0);
+    __syncthreads();
+    const uint32_t role = wv == 0 ? 1u + ((uint32_t)lane & 1u) : 0u;
+    const uint32_t sh = (wv == 0 && (lane & 1) == 0) ? 1u : 0u, sh2 = sh + 2u;
+    uint32_t cv = 0;
+    if ((wv == 0 || wv == 1) && act && iters) cv = s_st[role][vi] + s_w0[role][vi];
+    auto step_pair = [&](const uint2 x) {
+        const uint32_t y = cv ^ x.x;
+        const uint32_t r = __builtin_amdgcn_alignbit(y, y, 19);
+        const uint32_t r5 = lshl_add<2>(r, r);
+        const uint32_t own = lshl_add_v(r, sh2, lshl_add_v(r, sh, x.y));
+        cv = swap_pair(r5) + own;
+    };
+    auto step_h = [&](const uint2 x) {
+        const uint32_t y = cv ^ x.x;
+        const uint32_t r = __builtin_amdgcn_alignbit(y, y, 19);
+        cv = lshl_add<2>(r, r + x.y);
+    };
+    for (uint32_t e = 0; e < nep; e++) {
+        const int b = e & 1;
+        const uint32_t c0 = e * kEp;
+        if (wv <= 1) {
+            if (act) {
+                if (__ballot(c0 + kEp > iters) == 0) {  // every lane takes the whole epoch
+#pragma unroll
+                    for (int j = 0; j < kEp; j += 8) {
+                        uint2 x[8];
+#pragma unroll
+                        for (int q = 0; q < 8; q++) x[q] = stage[b][j + q][role][vi];
+                        if (wv == 0) {
+#pragma unroll
+                            for (int q = 0; q < 8; q++) step_pair(x[q]);
+                        } else {
+#pragma unroll
+                            for (int q = 0; q < 8; q++) step_h(x[q]);
+                        }
+                    }
+                } else {
+                    for (int j = 0; j < kEp; j++) {
+                        if (c0 + j < iters) {  // (a pair's lanes share the view: both or neither)
+                            if (wv == 0) step_pair(stage[b][j][role][vi]);
+                            else step_h(stage[b][j][role][vi]);
+                        }
+                    }
+                }
+            }
+        } else {
+            if (act && e + 1 < nep) produce(e + 1);
+            // the ring one epoch further ahead (the producers of the next iteration read it
+            // after the barrier; nobody reads the slices being replaced any more)
+            if (wv == 2) R.ensure(S.sbase, (e + 2) * kEp * 20 + lead, lane);
+        }
+        __syncthreads();
+    }
+    if (wv <= 1 && act) s_st[role][vi] = cv;
+    __syncthreads();
+    if (wv == 1 && act) {  // the last chunk's next-words were 0: plain h, g, f
+        S.checksum[lv] = iters == 0 ? hdone : chain_final(s_st[0][lane], s_st[1][lane], s_st[2][lane]);
+        S.dirty[lv] = 0;
+    }
+}
+
 // ---- membership / dissemination / suspicion on one node
+
+// A view's twin fingerprint: the sum over its deviated members (rank k; rows not at the base
+// values) of a 64-bit mix of (rank, status, incarnation). Order-free, so block_apply keeps it
+// per view as rows change (vfp) and the twin pass reads it instead of scanning the bitmap.
+__device__ __forceinline__ uint64_t twin_mix(uint32_t k, uint8_t st, int64_t inc) {
+    uint64_t x = ((uint64_t)k << 2 | st) * 0x9E3779B97F4A7C15ull ^ (uint64_t)inc * 0xC2B2AE3D27D4EB4Full;
+    x ^= x >> 29;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 32;
+    return x;
+}
+
+// the mix of a member's row, 0 at the base values (alive, the initial incarnation)
+__device__ __forceinline__ uint64_t twin_term(uint32_t k, uint8_t st, int64_t inc, int64_t inc0) {
+    return (st != ST_ALIVE || inc != inc0) ? twin_mix(k, st, inc) : 0ull;
+}
+
+// The node's change list as an LDS hash table (addr -> status, incarnation) for block_apply's
+// no-op test: a list entry always holds its member's row values (block_apply writes both in the
+// same step; an issue only deletes entries), so a record about a listed member is evaluated
+// without reading the view's row, which is a random HBM access per record. Overlays Lds::win.
+constexpr uint32_t kApHash = 2048;          // slots (a power of 2)
+constexpr uint32_t kApHashMax = 1536;       // list entries it takes (load <= 0.75)
+constexpr uint32_t kApHashMin = 64;         // records that pay for building it
+constexpr uint32_t kApEmpty = 0xFFFFFFFFu;  // key: addr | status << 30
+struct ApHash {
+    uint32_t key[kApHash];
+    int64_t inc[kApHash];
+};
+static_assert(sizeof(ApHash) <= sizeof(Lds::win), "the change-list hash overlays the checksum window");
+__device__ __forceinline__ uint32_t ap_slot(uint32_t a) { return (a * 0x9E3779B1u) >> (32 - 11); }
+static_assert(kApHash == 1u << 11, "ap_slot shift");
 
 // Membership.update(records) on local node lv + the 'updated' listeners
 // (on_membership_event.js:86-134): view row, recordChange (dissemination.js:56-72), suspicion
 // start (a suspect update about another member), ring add/remove -> maxPiggybackCount. Records
 // carry distinct addresses (one message), so lanes apply them independently. Returns the number
-// applied (block-uniform).
+// applied (block-uniform). A record about a member on the node's change list is tested against
+// the list entry first (ApHash); only the records that apply, or whose member is not listed,
+// read the view's row.
 __device__ uint32_t block_apply(const SimDev& S, uint32_t lv, const Rec* recs, uint32_t n, Lds& L, int64_t now) {
     const uint32_t v = S.v0 + lv;
     const uint64_t row = (uint64_t)lv * S.N;
@@ -1576,10 +1944,26 @@ __device__ uint32_t block_apply(const SimDev& S, uint32_t lv, const Rec* recs, u
     __syncthreads();
     uint32_t nc = S.n_chg[lv], nt = S.n_tim[lv];
     const bool stopped = S.stopped[lv] != 0;
+    ApHash& HT = *reinterpret_cast<ApHash*>(&L.win[0][0][0]);
+    if (threadIdx.x == 0) L.fpd = 0;  // (visible after the loop's first block_scan)
+    const bool hashed = n >= kApHashMin && nc > 0 && nc <= kApHashMax && S.N < (1u << 30);
+    if (hashed) {  // block-uniform
+        for (uint32_t q = threadIdx.x; q < kApHash; q += kT) HT.key[q] = kApEmpty;
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < nc; j += kT) {
+            const uint32_t a = chg[j].addr;
+            const uint32_t k = a | (chg[j].st << 30);
+            uint32_t q = ap_slot(a);
+            while (atomicCAS(&HT.key[q], kApEmpty, k) != kApEmpty) q = (q + 1) & (kApHash - 1);
+            HT.inc[q] = chg[j].inc;
+        }
+        __syncthreads();
+    }
     for (uint32_t base = 0; base < n; base += kT) {
         const uint32_t i = base + threadIdx.x;
         bool applied = false, need_timer = false, need_new = false;
         uint32_t a = 0, slot = 0;
+        uint64_t fpd = 0;
         uint8_t us = 0;
         int64_t ui = 0;
         Rec r{};
@@ -1588,8 +1972,19 @@ __device__ uint32_t block_apply(const SimDev& S, uint32_t lv, const Rec* recs, u
             a = rec_addr(r);
             us = rec_st(r);
             ui = r.inc;
-            const uint8_t cur = S.st[row + a];
-            if (evaluate_update(cur & ST_MASK, S.inc[row + a], a == v, us, ui, now)) {
+            bool noop = false;
+            if (hashed) {
+                uint32_t q = ap_slot(a), k;
+                while ((k = HT.key[q]) != kApEmpty && (k & 0x3FFFFFFFu) != a) q = (q + 1) & (kApHash - 1);
+                if (k != kApEmpty) {
+                    uint8_t s2 = us;
+                    int64_t i2 = ui;
+                    noop = !evaluate_update((uint8_t)(k >> 30), HT.inc[q], a == v, s2, i2, now);
+                }
+            }
+            const uint8_t cur = noop ? (uint8_t)0 : S.st[row + a];
+            const int64_t oi = noop ? 0 : S.inc[row + a];
+            if (!noop && evaluate_update(cur & ST_MASK, oi, a == v, us, ui, now)) {
                 applied = true;
                 napp++;
                 // createUpdatedHandlerForRing: alive -> add, faulty/leave -> remove
@@ -1605,6 +2000,7 @@ __device__ uint32_t block_apply(const SimDev& S, uint32_t lv, const Rec* recs, u
                 S.inc[row + a] = ui;
                 const uint32_t k = S.rank[a];
                 atomicOr(&S.dev[(uint64_t)lv * S.W + (k >> 5)], 1u << (k & 31));
+                fpd = twin_term(k, us, ui, S.inc0[a]) - twin_term(k, cur & ST_MASK, oi, S.inc0[a]);
                 need_timer = us == ST_SUSPECT && a != v && !stopped;
                 // the local member becoming `leave` (LocalMemberLeaveEvent, member.js:87-95)
                 if (a == v && us == ST_LEAVE && (cur & ST_MASK) != ST_LEAVE) nleave++;
@@ -1621,6 +2017,7 @@ __device__ uint32_t block_apply(const SimDev& S, uint32_t lv, const Rec* recs, u
             else set_err(S, ERR_TIMERS);
         }
         if (applied) {
+            if (fpd) atomicAdd(&L.fpd, (unsigned long long)fpd);
             if (!need_new) {
                 Change& c = chg[slot - 1];
                 c.cnt = 0;
@@ -1650,8 +2047,10 @@ __device__ uint32_t block_apply(const SimDev& S, uint32_t lv, const Rec* recs, u
         // gossip.stop() + suspicion.stopAll() (on_membership_event.js:32-40): every timer is
         // cleared, the ones this batch started included (they start after the event)
         S.n_tim[lv] = leaves ? 0u : nt;
+        if (leaves) S.t_head[lv] = 0;
         if (leaves) S.stopped[lv] = 1;
         if (tot) {
+            S.vfp[lv] += L.fpd;
             S.dirty[lv] = 1;
             atomicAdd(&S.stats[3], (unsigned long long)tot);
             if (adds || rems) {  // ringChanged -> adjustMaxPiggybackCount (dissemination.js:38-55)
@@ -1855,41 +2254,48 @@ __global__ void k_count_dirty(SimDev S) {
 // representative's member by member over the union of both bitmaps (exact: a fingerprint
 // collision only costs the verification), and an equal view is marked clean and takes the
 // representative's checksum after the chains.
-__device__ __forceinline__ uint64_t twin_mix(uint32_t k, uint8_t st, int64_t inc) {
-    uint64_t x = ((uint64_t)k << 2 | st) * 0x9E3779B97F4A7C15ull ^ (uint64_t)inc * 0xC2B2AE3D27D4EB4Full;
-    x ^= x >> 29;
-    x *= 0xBF58476D1CE4E5B9ull;
-    x ^= x >> 32;
-    return x;
-}
 
 constexpr unsigned long long kTwinEmpty = ~0ull;
 
 __device__ __forceinline__ uint32_t twin_slot(uint64_t f, uint32_t tmask) { return (uint32_t)(f ^ (f >> 32)) & tmask; }
 
-__global__ void k_twin_fp(SimDev S, uint64_t* __restrict__ fp, unsigned long long* __restrict__ tkey,
-                          uint32_t* __restrict__ trep, uint32_t tmask) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
-    for (uint32_t lv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; lv < S.NL; lv += nw) {
-        if (!S.dirty[lv] || S.dead[S.v0 + lv]) continue;  // wave-uniform
-        const uint64_t row = (uint64_t)lv * S.N;
-        const uint32_t* dv = S.dev + (uint64_t)lv * S.W;
-        uint64_t sum = 0;
-        for (uint32_t w = lane; w < S.W; w += 64) {
-            uint32_t bits = dv[w];
-            while (bits) {
-                const uint32_t k = (w << 5) + __builtin_ctz(bits);
-                bits &= bits - 1;
-                const uint32_t a = S.sorted[k];
-                const uint8_t st = S.st[row + a] & ST_MASK;
-                const int64_t inc = S.inc[row + a];
-                if (st != ST_ALIVE || inc != S.inc0[a]) sum += twin_mix(k, st, inc);
-            }
+// a view's fingerprint from its rows (one wave; the result in every lane)
+__device__ uint64_t view_fp_scan(const SimDev& S, uint32_t lv, int lane) {
+    const uint64_t row = (uint64_t)lv * S.N;
+    const uint32_t* dv = S.dev + (uint64_t)lv * S.W;
+    uint64_t sum = 0;
+    for (uint32_t w = lane; w < S.W; w += 64) {
+        uint32_t bits = dv[w];
+        while (bits) {
+            const uint32_t k = (w << 5) + __builtin_ctz(bits);
+            bits &= bits - 1;
+            const uint32_t a = S.sorted[k];
+            sum += twin_term(k, S.st[row + a] & ST_MASK, S.inc[row + a], S.inc0[a]);
         }
+    }
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
-        if (lane == 0) {
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    return sum;
+}
+
+// the kept fingerprint of a view whose rows were rewritten wholesale (a join)
+__global__ void k_vfp_view(SimDev S, uint32_t lv) {
+    const uint64_t f = view_fp_scan(S, lv, threadIdx.x & 63);
+    if (threadIdx.x == 0) S.vfp[lv] = f;
+}
+
+// Every dirty live view into the fingerprint table (one lane per view; verify: one wave per
+// view also recomputes it from the rows and flags a difference).
+__global__ void k_twin_fp(SimDev S, uint64_t* __restrict__ fp, unsigned long long* __restrict__ tkey,
+                          uint32_t* __restrict__ trep, uint32_t tmask, int verify) {
+    const int lane = threadIdx.x & 63;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (verify ? S.NL * 64u : S.NL);
+         i += gridDim.x * blockDim.x) {
+        const uint32_t lv = verify ? i >> 6 : i;
+        if (!S.dirty[lv] || S.dead[S.v0 + lv]) continue;  // (wave-uniform when verifying)
+        const uint64_t sum = S.vfp[lv];
+        if (verify && view_fp_scan(S, lv, lane) != sum && lane == 0) set_err(S, ERR_TWINFP);
+        if (!verify || lane == 0) {
             const uint64_t f = sum == kTwinEmpty ? 0x5bd1e995ull : sum;
             fp[lv] = f;
             for (uint32_t h = twin_slot(f, tmask);; h = (h + 1) & tmask) {
@@ -1968,8 +2374,9 @@ __global__ void k_early_list(SimDev S, uint32_t* __restrict__ list, uint32_t* __
             const int32_t t = S.target[lv];
             on = !(t >= 0 && S.dead[t]);
             // a view whose earliest suspicion timer is due fires it in phase E and changes again
-            // (timers are appended with due = round + susp, so tim[0] is the earliest)
-            if (on && S.n_tim[lv] && S.tim[(uint64_t)lv * S.Ct].due <= S.round) on = false;
+            // (timers are appended with due = round + susp, so the head timer is the earliest)
+            const uint32_t th = S.t_head[lv];
+            if (on && S.n_tim[lv] > th && S.tim[(uint64_t)lv * S.Ct + th].due <= S.round) on = false;
         }
         const uint64_t m = __ballot(on);
         if (!m) continue;
@@ -2353,38 +2760,61 @@ __global__ __launch_bounds__(kT) void k_phase_d3(SimDev S) {
 // is live while its member is still suspect at the captured incarnation (a newer suspicion
 // started a newer timer; any other status stopped it); the rest are dropped. The firings touch
 // distinct members, so they are applied together.
+// Timers are appended with due = round + susp, so a node's list is in due order and the timers
+// due this round are a prefix of its pending part [t_head, n_tim): only that prefix is read
+// (a lapsed timer that is not due yet waits in the list; at its due round it is dropped, as the
+// reference's cleared timeout never fires). A list past half its capacity is pruned whole and
+// compacted instead, so the appends of later rounds keep their room.
 __global__ __launch_bounds__(kT) void k_phase_e(SimDev S) {
     __shared__ Lds L;
     const int64_t now = S.now0 + 200 * S.round;
     for (uint32_t lv = blockIdx.x; lv < S.NL; lv += gridDim.x) {
         const uint32_t v = S.v0 + lv;
         if (S.dead[v] || S.stopped[lv]) continue;
+        const uint32_t nt = S.n_tim[lv], h0 = S.t_head[lv];
+        if (h0 >= nt) continue;  // nothing pending
         const uint64_t row = (uint64_t)lv * S.N;
         const int64_t srci = S.inc[row + v];
         Rec* stage = ping_slot(S, lv);  // free: the ping left in the exchange after phase A
         Timer* tim = S.tim + (uint64_t)lv * S.Ct;
-        const uint32_t nt = S.n_tim[lv];
-        uint32_t written = 0, kept = 0;
-        for (uint32_t base = 0; base < nt; base += kT) {
+        const bool whole = nt > S.Ct / 2;
+        uint32_t written = 0, kept = 0, h = h0;
+        for (uint32_t base = h0; base < nt; base += kT) {
             const uint32_t i = base + threadIdx.x;
-            bool keep = false, fire = false;
+            bool keep = false, fire = false, due = false;
             Timer t{};
             if (i < nt) {
                 t = tim[i];
-                const bool live = (S.st[row + t.addr] & ST_MASK) == ST_SUSPECT && S.inc[row + t.addr] == t.inc;
-                fire = live && t.due <= S.round;
-                keep = live && !fire;
+                due = t.due <= S.round;
+                if (due || whole) {
+                    const bool live = (S.st[row + t.addr] & ST_MASK) == ST_SUSPECT && S.inc[row + t.addr] == t.inc;
+                    fire = live && due;
+                    keep = live && !due;
+                }
             }
-            uint32_t ktot, ftot;
+            uint32_t ktot, ftot, dtot;
             const uint32_t kpos = block_scan(keep ? 1u : 0u, L.u, &ktot);
             const uint32_t fpos = block_scan(fire ? 1u : 0u, L.u, &ftot);
-            if (keep) tim[kept + kpos] = t;
+            block_scan(due ? 1u : 0u, L.u, &dtot);
+            if (whole && keep) tim[kept + kpos] = t;
             if (fire && written + fpos < S.Cm) stage[written + fpos] = Rec{rec_w0(t.addr, ST_FAULTY, 0), v, t.inc, srci};
             kept += ktot;
             written += ftot;
+            h += dtot;
             __syncthreads();
+            if (!whole && dtot < kT) break;  // the due prefix ended in this chunk (block-uniform)
         }
-        if (threadIdx.x == 0) S.n_tim[lv] = kept;
+        if (threadIdx.x == 0) {
+            if (whole) {
+                S.n_tim[lv] = kept;
+                S.t_head[lv] = 0;
+            } else if (h >= nt) {
+                S.n_tim[lv] = 0;
+                S.t_head[lv] = 0;
+            } else {
+                S.t_head[lv] = h;
+            }
+        }
         __threadfence_block();
         __syncthreads();
         if (written > S.Cm) {
@@ -2688,19 +3118,39 @@ __global__ void k_csr(const uint32_t* __restrict__ keys, uint32_t n, uint32_t N,
 // hostToAliveWorker): {count, min checksum, max checksum, some wanted member not at its wanted
 // status in one of those views}. want[i] = member | status << 24: a member that left must be
 // `leave`, any other member that is down `faulty`.
+// Two launches: the live count and checksum range (one atomic of each kind per wave), then the
+// wanted statuses, which the second launch reads only when this shard's live checksums are all
+// equal (otherwise the handle has not converged whatever they are: conv_reduce needs min == max).
+__global__ void k_conv_ck(SimDev S, const uint8_t* __restrict__ skip, uint32_t* __restrict__ out) {
+    uint32_t cnt = 0, lo = 0xFFFFFFFFu, hi = 0;
+    for (uint32_t lv = blockIdx.x * blockDim.x + threadIdx.x; lv < S.NL; lv += gridDim.x * blockDim.x) {
+        if (skip[S.v0 + lv]) continue;
+        const uint32_t c = S.checksum[lv];
+        cnt++;
+        lo = c < lo ? c : lo;
+        hi = c > hi ? c : hi;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        cnt += __shfl_xor(cnt, o, 64);
+        const uint32_t l2 = __shfl_xor(lo, o, 64), h2 = __shfl_xor(hi, o, 64);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+    }
+    if ((threadIdx.x & 63) == 0 && cnt) {
+        atomicAdd(&out[0], cnt);
+        atomicMin(&out[1], lo);
+        atomicMax(&out[2], hi);
+    }
+}
 __global__ void k_conv_local(SimDev S, const uint8_t* __restrict__ skip, const uint32_t* __restrict__ want,
                              uint32_t nk, uint32_t* __restrict__ out) {
+    if (out[0] == 0 || out[1] != out[2]) return;  // block-uniform
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (uint64_t)S.NL * nk;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t lv = (uint32_t)(i / nk), w = want[i % nk], a = w & 0xFFFFFFu;
         if (skip[S.v0 + lv]) continue;
         if ((S.st[(uint64_t)lv * S.N + a] & ST_MASK) != (w >> 24)) out[3] = 1;
-    }
-    for (uint32_t lv = blockIdx.x * blockDim.x + threadIdx.x; lv < S.NL; lv += gridDim.x * blockDim.x) {
-        if (skip[S.v0 + lv]) continue;
-        atomicAdd(&out[0], 1u);
-        atomicMin(&out[1], S.checksum[lv]);
-        atomicMax(&out[2], S.checksum[lv]);
     }
 }
 
@@ -2725,6 +3175,8 @@ __global__ void k_sim_init(SimDev S) {
         S.dirty[lv] = 1;  // first checksum by k_ck_lanes
         S.n_chg[lv] = 0;
         S.n_tim[lv] = 0;
+        S.t_head[lv] = 0;
+        S.vfp[lv] = 0;
         S.target[lv] = -1;
         S.nhelp[lv] = 0;
         S.stopped[lv] = 0;
@@ -2809,14 +3261,14 @@ struct Sim {
     DevBuf<int32_t> target;
     DevBuf<uint32_t> slot;
     DevBuf<uint32_t> opos;
-    DevBuf<uint32_t> order, dev, n_chg, n_tim, n_shuf, ring_count, max_piggy, checksum, ck_snap, ping_n, leg_n,
+    DevBuf<uint32_t> order, dev, n_chg, n_tim, t_head, n_shuf, ring_count, max_piggy, checksum, ck_snap, ping_n, leg_n,
         helpers, nhelp, leg_nk, cand, rank, err, bounds, want, conv, leave_list;
     DevBuf<uint32_t> okey, oval, ocnt, ooff, omoff;  // outbox build
     DevBuf<uint64_t> oseg;                           // outbox segment offsets
     DevBuf<Msg> imsg;                                // inbox headers, gathered
     DevBuf<uint32_t> ib_off, ib_idx, ikey;         // inbox build
     DevBuf<uint32_t> rsp_n, resp_idx, lresp_idx, d1list;
-    DevBuf<uint64_t> boff, rsp_off, ibase;
+    DevBuf<uint64_t> boff, rsp_off, ibase, vfp;
     DevBuf<Change> chg;
     DevBuf<Timer> tim;
     DevBuf<Rec> pool;
@@ -2877,7 +3329,11 @@ struct Sim {
             RP_HIP(hipMemsetAsync(twin_key.p, 0xFF, 8ull * T, st));
             RP_HIP(hipMemsetAsync(twin_rep.p, 0xFF, 4ull * T, st));
             const unsigned gw = grid_for((uint64_t)NL * 64, 256, 4096);
-            hipLaunchKernelGGL(k_twin_fp, dim3(gw), dim3(256), 0, st, d, twin_fp.p, twin_key.p, twin_rep.p, T - 1);
+            // RP_SIM_TWIN_VERIFY=1: recompute every fingerprint from the rows (a check of vfp)
+            const char* tv = getenv("RP_SIM_TWIN_VERIFY");
+            const int verify = tv && *tv && *tv != '0';
+            hipLaunchKernelGGL(k_twin_fp, dim3(verify ? gw : grid_for(NL, 256, 4096)), dim3(256), 0, st, d, twin_fp.p,
+                               twin_key.p, twin_rep.p, T - 1, verify);
             hipLaunchKernelGGL(k_twin_check, dim3(gw), dim3(256), 0, st, d, twin_fp.p, twin_key.p, twin_rep.p, T - 1,
                                twin_of.p, twin_cnt.p);
             RP_HIP(hipGetLastError());
@@ -2910,7 +3366,9 @@ struct Sim {
             }();
             use32 = (nd + 63) / 64 <= per_cu * cus;
         }
-        if (use32)
+        if (m && !strcmp(m, "pair"))  // A/B: the lane-pair chains, 32 views per workgroup
+            hipLaunchKernelGGL((k_ck_pair<6, 2, 32>), dim3((NL + 31) / 32), dim3(512), 0, st, d, sel, nsel);
+        else if (use32)
             hipLaunchKernelGGL((k_ck_pc<3, 2>), dim3(groups), dim3(256), 0, st, d, sel, nsel);
         else if (pc && !(m && !strcmp(m, "pc3")))
             hipLaunchKernelGGL(k_ck_pc<7>, dim3(groups), dim3(512), 0, st, d, sel, nsel);
@@ -3084,8 +3542,24 @@ struct Sim {
                 }
                 // the senders' checksums (their ping-req bodies carry them) as side-by-side chains
                 // first, so D1's workgroups find their views clean
-                if (!getenv("RP_SIM_D1_BLOCKCK"))
+                // (RP_SIM_D1_CK=pc: k_ck_pc's one lane per view; blockck: a workgroup per sender
+                // inside D1)
+                const char* d1ck = getenv("RP_SIM_D1_CK");
+                if (d1ck && !strcmp(d1ck, "pc"))
                     hipLaunchKernelGGL(k_ck_pc<7>, dim3((NL + 63) / 64), dim3(512), 0, st, d, d1list.p, d1list.p + NL);
+                else if (!(d1ck && !strcmp(d1ck, "blockck")) && !getenv("RP_SIM_D1_BLOCKCK"))
+                {
+                    static const int vpg = [] {  // A/B: RP_SIM_D1_VPG = 8 | 16
+                        const char* e = getenv("RP_SIM_D1_VPG");
+                        return e && *e ? atoi(e) : 8;
+                    }();
+                    if (vpg == 16)
+                        hipLaunchKernelGGL((k_ck_pair<6, 2, 16>), dim3((NL + 15) / 16), dim3(512), 0, st, d, d1list.p,
+                                           d1list.p + NL);
+                    else
+                        hipLaunchKernelGGL((k_ck_pair<6, 2, 8>), dim3((NL + 7) / 8), dim3(512), 0, st, d, d1list.p,
+                                           d1list.p + NL);
+                }
                 hipLaunchKernelGGL(k_phase_d1, dim3(g), dim3(kT), 0, st, d, d1list.p, d1list.p + NL);
                 if (early) {
                     // The D1 chains hold a few CUs for milliseconds (one 64-view group per CU);
@@ -3144,6 +3618,8 @@ struct Sim {
             throw Error(RP_ESTATE, "sim: a node's dissemination list exceeded its capacity (RP_SIM_CAP)");
         if (e & ERR_TIMERS) throw Error(RP_ESTATE, "sim: a node's suspicion timers exceeded their capacity (RP_SIM_CAP)");
         if (e & ERR_ARENA) throw Error(RP_ESTATE, "sim: the per-round message arena overflowed (RP_SIM_ARENA)");
+        if (e & ERR_TWINFP)
+            throw Error(RP_ESTATE, "sim: a view's kept twin fingerprint differs from its rows (RP_SIM_TWIN_VERIFY)");
     }
 
     // The scenario's events of this round, before phase A: a node goes down or comes back (every
@@ -3206,11 +3682,13 @@ struct Sim {
             join_scratch.reserve(2);
             RP_HIP(hipMemsetAsync(join_scratch.p, 0, 8, st));
             RP_HIP(hipMemsetAsync(n_tim.p + (v - v0), 0, 4, st));
+            RP_HIP(hipMemsetAsync(t_head.p + (v - v0), 0, 4, st));
             hipLaunchKernelGGL(k_join_prep, dim3(grid_for(std::max(N, d.W), 256)), dim3(256), 0, st, d, v, J,
                                join_scratch.p);
             hipLaunchKernelGGL(k_join_view, dim3(grid_for(N, 256)), dim3(256), 0, st, d, v, pj.incv, pj.nj, J,
                                join_scratch.p);
             hipLaunchKernelGGL(k_join_finish, dim3(1), dim3(64), 0, st, d, v, join_scratch.p);
+            hipLaunchKernelGGL(k_vfp_view, dim3(1), dim3(64), 0, st, d, v - v0);
             RP_HIP(hipGetLastError());
         }
         h_dead[v] = 0;
@@ -3328,9 +3806,12 @@ struct Sim {
         }
         const uint32_t init[4] = {0u, 0xFFFFFFFFu, 0u, 0u};
         RP_HIP(hipMemcpyAsync(conv.p, init, sizeof init, hipMemcpyHostToDevice, st));
-        if (NL)
-            hipLaunchKernelGGL(k_conv_local, dim3(grid_for((uint64_t)NL * std::max(nwant, 1u), 256, 8192)), dim3(256),
-                               0, st, d, cskip.p, want.p, nwant, conv.p);
+        if (NL) {
+            hipLaunchKernelGGL(k_conv_ck, dim3(grid_for(NL, 256, 1024)), dim3(256), 0, st, d, cskip.p, conv.p);
+            if (nwant)
+                hipLaunchKernelGGL(k_conv_local, dim3(grid_for((uint64_t)NL * nwant, 256, 8192)), dim3(256), 0, st, d,
+                                   cskip.p, want.p, nwant, conv.p);
+        }
         RP_HIP(hipGetLastError());
         RP_HIP(hipMemcpyAsync(out4, conv.p, 16, hipMemcpyDeviceToHost, st));
         RP_HIP(hipStreamSynchronize(st));
@@ -3456,7 +3937,7 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
         S.st_.reserve(NN + 1); S.inc.reserve(NN + 1); S.order.reserve(NN + 1); S.slot.reserve(NN + 1);
         S.dev.reserve(L1 * W);
         S.chg.reserve(L1 * cap); S.tim.reserve(L1 * cap);
-        S.n_chg.reserve(L1); S.n_tim.reserve(L1);
+        S.n_chg.reserve(L1); S.n_tim.reserve(L1); S.t_head.reserve(L1); S.vfp.reserve(L1);
         S.it_idx.reserve(L1); S.n_shuf.reserve(L1); S.ring_count.reserve(L1); S.max_piggy.reserve(L1);
         S.checksum.reserve(L1); S.dirty.reserve(L1); S.dead.reserve(n); S.target.reserve(L1); S.ck_snap.reserve(L1);
         S.inc_snap.reserve(L1); S.ping_n.reserve(L1); S.leg_n.reserve(L1);
@@ -3502,7 +3983,7 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
         d.st = S.st_.p; d.inc = S.inc.p; d.order = S.order.p; d.slot = S.slot.p; d.dev = S.dev.p;
         d.opos = use_opos ? S.opos.p : nullptr;
         d.xcap = (uint32_t)std::max<uint64_t>(2, std::min<uint64_t>(rp::kXCap, env_u64("RP_SIM_D1_XCAP", rp::kXCap)));
-        d.chg = S.chg.p; d.n_chg = S.n_chg.p; d.tim = S.tim.p; d.n_tim = S.n_tim.p;
+        d.chg = S.chg.p; d.n_chg = S.n_chg.p; d.tim = S.tim.p; d.n_tim = S.n_tim.p; d.t_head = S.t_head.p; d.vfp = S.vfp.p;
         d.it_idx = S.it_idx.p; d.n_shuf = S.n_shuf.p; d.ring_count = S.ring_count.p; d.max_piggy = S.max_piggy.p;
         d.checksum = S.checksum.p; d.dirty = S.dirty.p; d.dead = S.dead.p; d.stopped = S.stopped.p;
         d.sorted = S.nt.sorted.p; d.rank = S.rank.p; d.names = S.nt.d_bytes.p; d.noff = S.nt.d_noff.p;
@@ -3516,7 +3997,7 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
         d.resp_idx = S.resp_idx.p; d.lresp_idx = S.lresp_idx.p;
         d.stats = S.stats.p; d.err = S.err.p; d.round = 0;
         {
-            const void* ptrs[] = {d.st, d.inc, d.order, d.slot, d.dev, d.chg, d.n_chg, d.tim, d.n_tim, d.it_idx,
+            const void* ptrs[] = {d.st, d.inc, d.order, d.slot, d.dev, d.chg, d.n_chg, d.tim, d.n_tim, d.t_head, d.vfp, d.it_idx,
                                   d.n_shuf, d.ring_count, d.max_piggy, d.checksum, d.dirty, d.dead, d.sorted,
                                   d.rank, d.names, d.noff, d.sbase, d.boff, d.inc0, d.target, d.ck_snap,
                                   d.inc_snap, d.pool, d.cursor, d.ping_n, d.leg_n, d.helpers, d.nhelp, d.leg_nk,

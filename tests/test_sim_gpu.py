@@ -54,16 +54,20 @@ def test_sim_matches_reference_goldens(gpu, case_name):
     sim.close()
 
 
-@pytest.mark.parametrize("mode", ["scan", "xcap3"])
+@pytest.mark.parametrize("mode", ["scan", "xcap3", "ck_pc", "ck_block"])
 def test_sim_d1_paths_match_reference_goldens(gpu, monkeypatch, mode):
     """Phase D1's two ways of drawing ping-req helpers give the reference's helpers: the members-
     array scan (RP_SIM_OPOS_BYTES=0: no inverse permutation) and the mixed run where views with
     more than 3 non-candidates scan while the others select through the sorted non-candidate
-    positions (RP_SIM_D1_XCAP=3). The default run (the goldens above) selects everywhere."""
+    positions (RP_SIM_D1_XCAP=3). The default run (the goldens above) selects everywhere. The
+    senders' checksums (default: k_ck_pair, the lane-pair chains) also run through k_ck_pc
+    (RP_SIM_D1_CK=pc) and a workgroup per sender (blockck)."""
     if mode == "scan":
         monkeypatch.setenv("RP_SIM_OPOS_BYTES", "0")
-    else:
+    elif mode == "xcap3":
         monkeypatch.setenv("RP_SIM_D1_XCAP", "3")
+    else:
+        monkeypatch.setenv("RP_SIM_D1_CK", "pc" if mode == "ck_pc" else "blockck")
     for case in gu.load("sim_golden.json")["cases"]:
         names, sim = _golden_sim(gpu, case)
         for r, want in enumerate(case["checksums"]):
@@ -73,11 +77,14 @@ def test_sim_d1_paths_match_reference_goldens(gpu, monkeypatch, mode):
         sim.close()
 
 
-@pytest.mark.parametrize("kernel", ["pc", "lanes", "pc32"])
+@pytest.mark.parametrize("kernel", ["pc", "lanes", "pc32", "pair"])
 def test_sim_twins_match_reference_goldens(gpu, monkeypatch, kernel):
     """Every scenario golden with the twin-view pass forced on (RP_SIM_TWINS=1) on both chain
-    kernels: late rounds have many equal views, each takes its representative's checksum."""
+    kernels: late rounds have many equal views, each takes its representative's checksum. The
+    fingerprints block_apply keeps per view (joins recompute theirs) are checked against a scan of
+    every dirty view's rows each refresh (RP_SIM_TWIN_VERIFY=1: a difference raises)."""
     monkeypatch.setenv("RP_SIM_TWINS", "1")
+    monkeypatch.setenv("RP_SIM_TWIN_VERIFY", "1")
     monkeypatch.setenv("RP_SIM_CK", kernel)
     for case in gu.load("sim_golden.json")["cases"]:
         names, sim = _golden_sim(gpu, case)
@@ -129,13 +136,14 @@ def test_sim_vs_oracle(gpu, orc, n, k, seed, susp):
 
 
 @pytest.mark.parametrize("twins", ["0", "1"])
-@pytest.mark.parametrize("kernel", ["pc", "lanes", "pc3", "pc32"])
+@pytest.mark.parametrize("kernel", ["pc", "lanes", "pc3", "pc32", "pair"])
 def test_sim_checksum_kernels_vs_oracle(gpu, orc, monkeypatch, kernel, twins):
     """Both lane-checksum kernels (k_ck_pc: chain wave + producer waves; k_ck_lanes: one wave per
     64 nodes), forced through RP_SIM_CK, against the oracle on a case with many deviations; with
     and without the twin-view pass (equal views hash once, compacted view lists)."""
     monkeypatch.setenv("RP_SIM_CK", kernel)
     monkeypatch.setenv("RP_SIM_TWINS", twins)
+    monkeypatch.setenv("RP_SIM_TWIN_VERIFY", twins)
     S = synth()
     n, k, seed, susp = 900, 60, 5, 6
     names = [S.c2_addr(i) for i in range(n)]
@@ -212,6 +220,15 @@ def test_sharded_join_without_exchange_is_refused(gpu):
                 if k < gpu.SIM_STAGES - 1:
                     gpu.check(gpu.lib().rp_sim_exchange_local(sim._arr, sim.G))
     sim.close()
+
+
+@pytest.mark.parametrize("case_name", ["n30-join", "n70-join"])
+def test_sharded_join_twins_verified(gpu, monkeypatch, case_name):
+    """Joins rewrite the joiner's rows wholesale; its kept twin fingerprint is recomputed from the
+    rows (k_vfp_view) and checked by RP_SIM_TWIN_VERIFY with the twin pass forced on."""
+    monkeypatch.setenv("RP_SIM_TWINS", "1")
+    monkeypatch.setenv("RP_SIM_TWIN_VERIFY", "1")
+    test_sharded_sim_join_matches_reference_goldens(gpu, case_name, 2)
 
 
 def test_sim_with_early_refresh_matches_reference_goldens(gpu, monkeypatch):
