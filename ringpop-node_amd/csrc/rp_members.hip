@@ -374,6 +374,256 @@ __global__ __launch_bounds__(1024) void k_fold_ovf(const uint32_t* __restrict__ 
     }
 }
 
+// Bucket path (large batches, round 3): the batch is partitioned by id into buckets of kBk ids
+// (a stable-per-id order is not needed: an address's changes are put back in arrival order by
+// their batch index), then one workgroup folds one bucket with the bucket's 128 KB of rows
+// resident in its XCD's L2, so the row accesses and the rank counters stop being random HBM /
+// memory-side atomics (k_link's one atomic per change was half of a 2^22 batch). The per-change
+// outputs come back in batch order through the record positions (pos) and a 1-byte result per
+// record: a coalesced gather reads res, which fits L2.
+//   k_bk_count   per 4,096-change tile: the bucket histogram (bucket-major counts)
+//   scan         offsets of every (bucket, tile) run
+//   k_bk_scatter 16-B records {id, batch index | status << 30, incarnation} into bucket runs,
+//                pos[j] = the record's position
+//   k_bk_fold    a workgroup per bucket: LDS counters per id; single changes fold at once, an
+//                address's repeated changes are sorted by batch index in LDS and folded by one
+//                lane; an address with more than kSlots + 1 changes (or a bucket whose repeated
+//                changes overflow the LDS list) is marked for the overflow fold (k_fold_ovf /
+//                k_ovf_len, as on the grouped path)
+//   k_bk_gather  applied / new status / new incarnation per change in batch order
+constexpr uint32_t kBkBits = 13, kBk = 1u << kBkBits;  // ids per bucket (128 KB of rows)
+constexpr uint32_t kBkTile = 4096;                     // changes per count / scatter tile
+constexpr uint32_t kBkDup = 2048;                      // repeated-address changes a bucket sorts in LDS
+constexpr uint32_t kBkMaxBuckets = 1024;               // (LDS of the count / scatter tiles): 8M ids
+constexpr uint8_t kResLocal = 4;                       // res: the local override rewrote (status, inc)
+
+struct alignas(16) BRec {
+    uint32_t id;
+    uint32_t js;  // batch index | status << 30
+    int64_t inc;
+};
+
+__global__ __launch_bounds__(256) void k_bk_count(const uint32_t* __restrict__ ids, uint32_t k, uint32_t nb,
+                                                  uint32_t ntiles, uint32_t* __restrict__ counts) {
+    __shared__ uint32_t h[kBkMaxBuckets];
+    for (uint32_t b = threadIdx.x; b < nb; b += 256) h[b] = 0;
+    __syncthreads();
+    const uint32_t t = blockIdx.x, base = t * kBkTile;
+    for (uint32_t i = threadIdx.x; i < kBkTile; i += 256) {
+        const uint32_t j = base + i;
+        if (j < k) atomicAdd(&h[ids[j] >> kBkBits], 1u);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += 256) counts[(uint64_t)b * ntiles + t] = h[b];
+}
+
+// A tile's records go through LDS in bucket order, so each bucket's run leaves as consecutive
+// 16-B stores (a wave writes a few whole lines instead of 64 scattered records).
+__global__ __launch_bounds__(256) void k_bk_scatter(const uint32_t* __restrict__ ids, const uint8_t* __restrict__ chs,
+                                                    const int64_t* __restrict__ chi, uint32_t k, uint32_t nb,
+                                                    uint32_t ntiles, const uint32_t* __restrict__ offs,
+                                                    BRec* __restrict__ recs, uint32_t* __restrict__ pos) {
+    __shared__ uint32_t h[kBkMaxBuckets], ls[kBkMaxBuckets], gs[kBkMaxBuckets], s_w[4];
+    __shared__ uint4 stage[kBkTile];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t t = blockIdx.x, base = t * kBkTile;
+    const uint32_t n = k - base < kBkTile ? k - base : kBkTile;
+    for (uint32_t b = tid; b < nb; b += 256) {
+        h[b] = 0;
+        gs[b] = offs[(uint64_t)b * ntiles + t];
+    }
+    __syncthreads();
+    constexpr uint32_t PER = kBkTile / 256;
+    uint32_t rk[PER], idv[PER];
+#pragma unroll
+    for (uint32_t q = 0; q < PER; q++) {
+        const uint32_t i = tid + q * 256;
+        idv[q] = i < n ? ids[base + i] : 0u;
+        rk[q] = i < n ? atomicAdd(&h[idv[q] >> kBkBits], 1u) : 0u;
+    }
+    __syncthreads();
+    // exclusive scan of h over the buckets (contiguous runs per thread, then across threads)
+    const uint32_t per = (nb + 255) / 256, b0 = min(nb, tid * per), b1 = min(nb, b0 + per);
+    uint32_t run = 0;
+    for (uint32_t b = b0; b < b1; b++) run += h[b];
+    uint32_t inc = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t x = __shfl_up(inc, o, 64);
+        if (lane >= (uint32_t)o) inc += x;
+    }
+    if (lane == 63) s_w[wv] = inc;
+    __syncthreads();
+    uint32_t ex = inc - run;
+    for (uint32_t w = 0; w < wv; w++) ex += s_w[w];
+    for (uint32_t b = b0; b < b1; b++) {
+        ls[b] = ex;
+        ex += h[b];
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < PER; q++) {
+        const uint32_t i = tid + q * 256;
+        if (i < n) {
+            const uint32_t j = base + i, b = idv[q] >> kBkBits;
+            const int64_t inc8 = chi[j];
+            stage[ls[b] + rk[q]] = uint4{idv[q], j | ((uint32_t)(chs[j] & 3u) << 30), (uint32_t)(uint64_t)inc8,
+                                         (uint32_t)((uint64_t)inc8 >> 32)};
+            pos[j] = gs[b] + rk[q];
+        }
+    }
+    __syncthreads();
+    for (uint32_t q = tid; q < n; q += 256) {
+        const uint4 v = stage[q];
+        const uint32_t b = v.x >> kBkBits;
+        *reinterpret_cast<uint4*>(recs + gs[b] + (q - ls[b])) = v;
+    }
+}
+
+// One change on a member row (the step of fold_address without damp scoring): returns applied
+// (0, 1 existing, 2 created) | kResLocal when the local override rewrote the change.
+__device__ __forceinline__ uint8_t bk_step(const FoldArgs& A, uint32_t id, bool& ex, uint8_t& st, int64_t& in,
+                                          uint8_t us, int64_t ui) {
+    uint8_t a, loc = 0;
+    if (!ex) {
+        ex = true;
+        a = 2;
+    } else {
+        const uint8_t us0 = us;
+        const int64_t ui0 = ui;
+        a = evaluate_update(st, in, id == A.local_id, us, ui, A.now_ms) ? 1 : 0;
+        loc = (us != us0 || ui != ui0) ? kResLocal : 0;
+    }
+    if (a) {
+        st = us;
+        in = ui;
+    }
+    return a | loc;
+}
+
+// A workgroup per bucket: per-id change counters and each id's (last) record in LDS; then the
+// bucket's ids in id order, so the rows move as whole lines: a single change folds at once,
+// repeated changes go to the sorted LDS list (one lane per address, in batch order), more than
+// kSlots + 1 changes (or a list that would overflow) to the overflow fold.
+__global__ __launch_bounds__(1024) void k_bk_fold(const BRec* __restrict__ recs, const uint32_t* __restrict__ offs,
+                                                  uint32_t ntiles, uint32_t nb, FoldArgs A,
+                                                  const uint32_t* __restrict__ pos, uint8_t* __restrict__ res,
+                                                  uint32_t* __restrict__ ovf, uint32_t* __restrict__ part) {
+    __shared__ uint32_t cnt[kBk], map[kBk];
+    __shared__ uint64_t dk[kBkDup];
+    __shared__ uint32_t s_nd, s_w[16];
+    const uint32_t tid = threadIdx.x, b = blockIdx.x, id0 = b << kBkBits;
+    const uint32_t r0 = offs[(uint64_t)b * ntiles], r1 = offs[(uint64_t)(b + 1) * ntiles];
+    for (uint32_t q = tid; q < kBk; q += 1024) cnt[q] = 0;
+    if (tid == 0) s_nd = 0;
+    __syncthreads();
+    for (uint32_t p = r0 + tid; p < r1; p += 1024) {
+        const uint32_t il = recs[p].id - id0;
+        atomicAdd(&cnt[il], 1u);
+        map[il] = p;
+    }
+    __syncthreads();
+    {  // the repeated changes the LDS list would take
+        uint32_t v = 0;
+        for (uint32_t q = tid; q < kBk; q += 1024) {
+            const uint32_t c = cnt[q];
+            v += (c > 1 && c <= kSlots + 1) ? c : 0u;
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+        if ((tid & 63) == 0 && v) atomicAdd(&s_nd, v);
+    }
+    __syncthreads();
+    const uint32_t nd = s_nd;
+    const bool listed = nd <= kBkDup;  // block-uniform
+    uint32_t napp = 0;
+    for (uint32_t q = tid; q < kBk; q += 1024) {  // ids in order: coalesced rows
+        const uint32_t c = cnt[q], id = id0 + q;
+        if (c == 1) {
+            const uint32_t p = map[q];
+            const uint4 v = *reinterpret_cast<const uint4*>(recs + p);
+            const MRow row = row_load(A.rows + id);
+            bool ex = row.exists != 0;
+            uint8_t st = row.status;
+            int64_t in = row.inc;
+            const uint8_t r = bk_step(A, id, ex, st, in, (uint8_t)(v.y >> 30), (int64_t)(((uint64_t)v.w << 32) | v.z));
+            row_store(A.rows + id, in, st, 1);
+            res[p] = r;
+            napp += (r & 3u) ? 1u : 0u;
+        } else if (c > kSlots + 1 || (c > 1 && !listed)) {  // the overflow fold takes the address
+            A.rows[id].cnt = kOvfMark;
+            *ovf = 1u;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) s_nd = 0;
+    __syncthreads();
+    if (listed && nd) {  // repeated addresses: list, sort by (address, batch index), fold per address
+        for (uint32_t p = r0 + tid; p < r1; p += 1024) {
+            const uint2 v = *reinterpret_cast<const uint2*>(recs + p);
+            const uint32_t c = cnt[v.x - id0];
+            if (c > 1 && c <= kSlots + 1) dk[atomicAdd(&s_nd, 1u)] = ((uint64_t)(v.x - id0) << 32) | (v.y & 0x3FFFFFFFu);
+        }
+        __syncthreads();
+        uint32_t np = 1;
+        while (np < nd) np <<= 1;
+        for (uint32_t q = nd + tid; q < np; q += 1024) dk[q] = ~0ull;
+        __syncthreads();
+        for (uint32_t k2 = 2; k2 <= np; k2 <<= 1)
+            for (uint32_t jj = k2 >> 1; jj > 0; jj >>= 1) {
+                for (uint32_t t = tid; t < np; t += 1024) {
+                    const uint32_t x = t ^ jj;
+                    if (x > t) {
+                        const uint64_t a = dk[t], c = dk[x];
+                        if ((a > c) == ((t & k2) == 0)) {
+                            dk[t] = c;
+                            dk[x] = a;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        for (uint32_t q = tid; q < nd; q += 1024) {
+            const uint32_t il = (uint32_t)(dk[q] >> 32);
+            if (q > 0 && (uint32_t)(dk[q - 1] >> 32) == il) continue;  // not a segment head
+            const uint32_t id = id0 + il;
+            const MRow row = row_load(A.rows + id);
+            bool ex = row.exists != 0;
+            uint8_t st = row.status;
+            int64_t in = row.inc;
+            for (uint32_t e = q; e < nd && (uint32_t)(dk[e] >> 32) == il; e++) {
+                const uint32_t j = (uint32_t)dk[e];
+                const uint8_t r = bk_step(A, id, ex, st, in, A.ch_status[j] & 3u, A.ch_inc[j]);
+                res[pos[j]] = r;
+                napp += (r & 3u) ? 1u : 0u;
+            }
+            row_store(A.rows + id, in, st, ex ? 1 : 0);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) napp += __shfl_xor(napp, o, 64);
+    if ((tid & 63) == 0) s_w[tid >> 6] = napp;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < 16; w++) t += s_w[w];
+        part[b] = t;
+        if (b == 0) part[nb] = 0;  // the overflow fold's count (k_ovf_len)
+    }
+}
+
+__global__ void k_bk_gather(const uint32_t* __restrict__ pos, const uint8_t* __restrict__ res,
+                            const uint8_t* __restrict__ chs, const int64_t* __restrict__ chi, uint32_t k, int64_t now_ms,
+                            uint8_t* __restrict__ applied, uint8_t* __restrict__ nst, int64_t* __restrict__ ninc) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= k) return;
+    const uint8_t r = res[pos[j]];
+    const bool loc = (r & kResLocal) != 0;  // suspect / faulty about the local member: alive at now
+    if (applied) applied[j] = r & 3u;
+    if (nst) nst[j] = loc ? (uint8_t)ST_ALIVE : chs[j];
+    if (ninc) ninc[j] = loc ? now_ms : chi[j];
+}
+
 // Membership._decayMembersDampScore (index.js:374-383): decayDampScore on every member
 // (member.js:45-66). Reads 17 B and writes 8 B per id.
 __global__ void k_damp_decay(const MRow* __restrict__ rows, uint32_t n, double* __restrict__ score,
@@ -746,7 +996,19 @@ struct Members {
     bool grouped_fold = !getenv_on("RP_MEMBERS_SORTED_FOLD");
     DevBuf<uint32_t> g_slots;
     DevBuf<uint8_t> g_rk;
-    DevBuf<uint32_t> g_part;  // per-workgroup applied counts of k_fold_fast
+    DevBuf<uint32_t> g_part;  // per-workgroup applied counts of k_fold_fast (per bucket: k_bk_fold)
+    // the bucket path (batches of kBkMin changes or more without damp scoring; RP_MEMBERS_BUCKET_FOLD
+    // = 0 | 1 overrides the size rule)
+    DevBuf<uint32_t> bk_counts, bk_pos;
+    DevBuf<BRec> bk_recs;
+    DevBuf<uint8_t> bk_res;
+    static constexpr uint32_t kBkMin = 1u << 19;
+    bool use_bucket_fold(uint32_t k, uint32_t nb) const {
+        if (damp_on || nb > kBkMaxBuckets || k >= (1u << 30) || !grouped_fold) return false;
+        const char* e = getenv("RP_MEMBERS_BUCKET_FOLD");
+        if (e && *e) return *e != '0';
+        return k >= kBkMin;
+    }
     DevBuf<uint32_t> mk, mpos;  // set: merge marks and their positions
     // host-buffer staging
     DevBuf<uint32_t> io_ids, io_pick;
@@ -843,7 +1105,32 @@ struct Members {
         const bool mine = ck_nsh <= 1 || batch_no % ck_nsh == ck_sh;
         batch_no++;
         const bool build = !defer_ck && mine;
-        if (grouped_fold) {
+        const uint32_t nb = (cap + kBk - 1) / kBk;
+        if (use_bucket_fold(k, nb)) {
+            const uint32_t ntiles = (k + kBkTile - 1) / kBkTile;
+            const uint64_t nc = (uint64_t)nb * ntiles;
+            bk_counts.reserve(nc + 1);
+            bk_recs.reserve(k);
+            bk_pos.reserve(k);
+            bk_res.reserve(k);
+            g_part.reserve(nb + 1);
+            hipLaunchKernelGGL(k_bk_count, dim3(ntiles), dim3(256), 0, s, ids, k, nb, ntiles, bk_counts.p);
+            scan_exclusive_u32(bk_counts.p, bk_counts.p, nc, s, ws);
+            hipLaunchKernelGGL(k_bk_scatter, dim3(ntiles), dim3(256), 0, s, ids, chs, chi, k, nb, ntiles, bk_counts.p,
+                               bk_recs.p, bk_pos.p);
+            hipLaunchKernelGGL(k_bk_fold, dim3(nb), dim3(1024), 0, s, bk_recs.p, bk_counts.p, ntiles, nb, A, bk_pos.p,
+                               bk_res.p, ovf, g_part.p);
+            if (applied || nst || ninc)
+                hipLaunchKernelGGL(k_bk_gather, dim3(grid_for(k, 256, 1u << 30)), dim3(256), 0, s, bk_pos.p, bk_res.p,
+                                   chs, chi, k, now_ms, applied, nst, ninc);
+            RP_HIP(hipGetLastError());
+            if (build && nt.size()) {
+                const OvfArgs ov{ids, k, ovf, A, g_part.p, nb, n_applied_out};
+                checksum_dev(s, napplied.p, true, &ov);
+                return;
+            }
+            hipLaunchKernelGGL(k_fold_ovf, dim3(1), dim3(1024), 0, s, ids, k, ovf, A, g_part.p, nb, n_applied_out);
+        } else if (grouped_fold) {
             g_slots.reserve((uint64_t)cap * kSlots);
             g_rk.reserve(k);
             const unsigned g1 = (unsigned)((k + 255) / 256);

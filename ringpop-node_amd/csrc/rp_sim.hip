@@ -108,6 +108,11 @@ struct Change {
     int64_t inc;   // the member's incarnation
 };
 
+struct P1 {  // a view's pass-1 results (lane_pass1 / seg_pass1)
+    int64_t dtot, dlo, dhi;
+    uint32_t last, nd;
+};
+
 struct Timer {  // a suspicion timer (suspicion.js:55-84)
     uint32_t addr;
     int32_t due;  // round at whose end it fires
@@ -170,6 +175,10 @@ struct SimDev {
     uint64_t strcap;
     uint4* dlist;       // [NL][dcap] a lane checksum's deviated pieces, address order
     uint32_t dcap;
+    P1* p1;              // [NL] pass-1 results k_pass1 left for the refresh kernel
+    uint32_t p1_pre;     // 1: the lane kernels read p1 instead of running lane_pass1
+    uint32_t ck_ablate;  // timing ablations of k_ck_lanes (RP_SIM_CK_ABLATE; results are wrong): 1 no
+                         // fixups, 2 also no word production
     // inbound messages of the current stage
     const Msg* in_msg;      // headers, gathered in arrival order
     const uint8_t* in_buf;  // the inbox: per source shard [headers | records]
@@ -1124,6 +1133,25 @@ __device__ void seg_pass1(const SimDev& S, const LaneView& V, uint4* dl, bool ac
     nd = bg && total <= S.dcap ? S.dcap + 1u : total;  // an oversize piece: the lane path's fallback
 }
 
+// Pass 1 of the refresh's views ahead of the lane kernels, one wave per view (seg_pass1<64>):
+// a lane walking its own view's bitmap (3,125 words at C5) and ~1,000 deviated members through
+// dependent loads spent milliseconds before its chain started; 64 lanes take 1/64 of that.
+__global__ __launch_bounds__(256) void k_pass1(SimDev S, const uint32_t* __restrict__ sel,
+                                               const uint32_t* __restrict__ nsel) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t nw = gridDim.x * blockDim.x / 64;
+    const uint32_t n = sel ? *nsel : S.NL;
+    for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) / 64; i < n; i += nw) {
+        const uint32_t lv = sel ? sel[i] : i;
+        if (lv >= S.NL || S.dead[S.v0 + lv] || !S.dirty[lv]) continue;  // wave-uniform
+        const uint64_t row = (uint64_t)lv * S.N;
+        const LaneView V{S, S.st + row, S.inc + row, S.dev + (uint64_t)lv * S.W};
+        P1 r;
+        seg_pass1<64>(S, V, S.dlist + (uint64_t)lv * S.dcap, true, (uint32_t)lane, r.dtot, r.dlo, r.dhi, r.last, r.nd);
+        if (lane == 0) S.p1[lv] = r;
+    }
+}
+
 // Every live local node whose view changed: one node per lane, the wave's 64 chains in lockstep
 // over a shared LDS ring of the base string. A view with more deviated pieces than its list holds,
 // or a wave whose lanes drift further apart than the ring allows, uses the L2 path
@@ -1145,7 +1173,18 @@ __global__ __launch_bounds__(256) void k_ck_lanes(SimDev S, const uint32_t* __re
     int64_t dtot = 0, dlo = 0, dhi = 0;
     uint32_t last = NONE, nd = 0;
     uint4* dl = S.dlist + (uint64_t)(act ? lv : 0) * S.dcap;
-    if (act) lane_pass1(S, V, dl, dtot, dlo, dhi, last, nd);
+    if (act) {
+        if (S.p1_pre) {
+            const P1 r = S.p1[lv];
+            dtot = r.dtot;
+            dlo = r.dlo;
+            dhi = r.dhi;
+            last = r.last;
+            nd = r.nd;
+        } else {
+            lane_pass1(S, V, dl, dtot, dlo, dhi, last, nd);
+        }
+    }
     const uint64_t len = (uint64_t)((int64_t)S.boff[N] + dtot);
     const bool ring_ok = __ballot(act && (nd > S.dcap || len > 0x7FFFFFF0ull)) == 0 &&
                          wave_max64(act ? dhi : 0) - wave_min64(act ? dlo : 0) <= (int64_t)(kRing - 2 * kSlice - 256);
@@ -1306,7 +1345,18 @@ __global__ __launch_bounds__(256) void k_ck_lanes(SimDev S, const uint32_t* __re
             while (__builtin_expect(q1 >= C.pend, 0) && C.cur.w < N) C.advance(S, V);
         }
         // one basic block: the next group's words + pre-mixes beside this group's chain
-        produce(q1, nw, n5, n6, n7);
+        if (S.ck_ablate < 2) {
+            produce(q1, nw, n5, n6, n7);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+#pragma unroll
+                for (int i = 0; i < 5; i++) nw[j][i] = wd[j][i] + 1u;
+                n5[j] = p5[j] ^ 3u;
+                n6[j] = p6[j] ^ 5u;
+                n7[j] = p7[j] ^ 7u;
+            }
+        }
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             if ((uint32_t)j < ng) {
@@ -1320,7 +1370,7 @@ __global__ __launch_bounds__(256) void k_ck_lanes(SimDev S, const uint32_t* __re
                 g += f;
             }
         }
-        if (__builtin_expect(ng1 && q1 + 20 * ng1 > C.pos, 0)) fixup(q1, ng1, nw, n5, n6, n7);
+        if (__builtin_expect(ng1 && q1 + 20 * ng1 > C.pos, 0) && S.ck_ablate == 0) fixup(q1, ng1, nw, n5, n6, n7);
 #pragma unroll
         for (int j = 0; j < 4; j++) {
 #pragma unroll
@@ -1495,7 +1545,18 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_ck_pc(SimDev S, const uint32_
     if (wv == 0) {
         int64_t dtot = 0, dlo = 0, dhi = 0;
         uint32_t last = NONE, nd = 0;
-        if (act) lane_pass1(S, V, dl, dtot, dlo, dhi, last, nd);
+        if (act) {
+            if (S.p1_pre) {
+                const P1 r = S.p1[lv];
+                dtot = r.dtot;
+                dlo = r.dlo;
+                dhi = r.dhi;
+                last = r.last;
+                nd = r.nd;
+            } else {
+                lane_pass1(S, V, dl, dtot, dlo, dhi, last, nd);
+            }
+        }
         len = (uint64_t)((int64_t)S.boff[N] + dtot);
         const bool bad = act && (nd > S.dcap || len > 0x7FFFFFF0ull);
         uint32_t iters = 0;
@@ -3273,6 +3334,7 @@ struct Sim {
     DevBuf<Timer> tim;
     DevBuf<Rec> pool;
     DevBuf<uint4> dlist;
+    DevBuf<P1> p1buf;
     DevBuf<unsigned long long> stats, cursor;
     MsgBuf out, in;
     Scratch ws;
@@ -3301,6 +3363,10 @@ struct Sim {
             cus = (uint32_t)(n > 0 ? n : 1);
         }
         const uint32_t groups = (NL + 63) / 64;
+        {
+            const char* ab = getenv("RP_SIM_CK_ABLATE");
+            d.ck_ablate = ab && *ab ? (uint32_t)atoi(ab) : 0u;
+        }
         hipLaunchKernelGGL(k_count_dirty, dim3(grid_for(NL, 256, 1024)), dim3(256), 0, st, d);
         const char* m = getenv("RP_SIM_CK");
         const bool pc = m ? strcmp(m, "lanes") != 0 : groups <= cus;
@@ -3366,6 +3432,18 @@ struct Sim {
             }();
             use32 = (nd + 63) / 64 <= per_cu * cus;
         }
+        // Pass 1 of every view to hash, a wave per view, ahead of the producer/consumer kernels,
+        // whose chain wave otherwise walks its 64 views' bitmaps and deviated members before any
+        // chunk is produced (C5: k_ck_pc<3, 2> 375 -> 324 ms over a run for 13 ms of k_pass1).
+        // k_ck_lanes hides its own lane walks behind other waves: there k_pass1 costs more than
+        // it saves (153 against 49 ms), so it stays in the kernel (RP_SIM_PASS1=0|1 overrides).
+        const bool lanes_path = !use32 && !pc && !(m && !strcmp(m, "pair"));
+        const char* p1e = getenv("RP_SIM_PASS1");
+        const bool pre1 = p1e && *p1e ? *p1e != '0' : !lanes_path;
+        if (pre1 && !(m && !strcmp(m, "pair"))) {
+            hipLaunchKernelGGL(k_pass1, dim3(grid_for((uint64_t)NL * 64, 256, 4096)), dim3(256), 0, st, d, sel, nsel);
+            d.p1_pre = 1;
+        }
         if (m && !strcmp(m, "pair"))  // A/B: the lane-pair chains, 32 views per workgroup
             hipLaunchKernelGGL((k_ck_pair<6, 2, 32>), dim3((NL + 31) / 32), dim3(512), 0, st, d, sel, nsel);
         else if (use32)
@@ -3376,6 +3454,7 @@ struct Sim {
             hipLaunchKernelGGL(k_ck_pc<3>, dim3(groups), dim3(256), 0, st, d, sel, nsel);
         else
             hipLaunchKernelGGL(k_ck_lanes, dim3(grid_for(NL, 256, 1u << 20)), dim3(256), 0, st, d, sel, nsel);
+        d.p1_pre = 0;
         if (twins) hipLaunchKernelGGL(k_twin_copy, dim3(grid_for(NL, 256)), dim3(256), 0, st, d, twin_of.p);
         RP_HIP(hipGetLastError());
     }
@@ -3937,7 +4016,7 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
         S.st_.reserve(NN + 1); S.inc.reserve(NN + 1); S.order.reserve(NN + 1); S.slot.reserve(NN + 1);
         S.dev.reserve(L1 * W);
         S.chg.reserve(L1 * cap); S.tim.reserve(L1 * cap);
-        S.n_chg.reserve(L1); S.n_tim.reserve(L1); S.t_head.reserve(L1); S.vfp.reserve(L1);
+        S.n_chg.reserve(L1); S.n_tim.reserve(L1); S.t_head.reserve(L1); S.vfp.reserve(L1); S.p1buf.reserve(L1);
         S.it_idx.reserve(L1); S.n_shuf.reserve(L1); S.ring_count.reserve(L1); S.max_piggy.reserve(L1);
         S.checksum.reserve(L1); S.dirty.reserve(L1); S.dead.reserve(n); S.target.reserve(L1); S.ck_snap.reserve(L1);
         S.inc_snap.reserve(L1); S.ping_n.reserve(L1); S.leg_n.reserve(L1);
@@ -3983,7 +4062,7 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
         d.st = S.st_.p; d.inc = S.inc.p; d.order = S.order.p; d.slot = S.slot.p; d.dev = S.dev.p;
         d.opos = use_opos ? S.opos.p : nullptr;
         d.xcap = (uint32_t)std::max<uint64_t>(2, std::min<uint64_t>(rp::kXCap, env_u64("RP_SIM_D1_XCAP", rp::kXCap)));
-        d.chg = S.chg.p; d.n_chg = S.n_chg.p; d.tim = S.tim.p; d.n_tim = S.n_tim.p; d.t_head = S.t_head.p; d.vfp = S.vfp.p;
+        d.chg = S.chg.p; d.n_chg = S.n_chg.p; d.tim = S.tim.p; d.n_tim = S.n_tim.p; d.t_head = S.t_head.p; d.vfp = S.vfp.p; d.p1 = S.p1buf.p; d.p1_pre = 0;
         d.it_idx = S.it_idx.p; d.n_shuf = S.n_shuf.p; d.ring_count = S.ring_count.p; d.max_piggy = S.max_piggy.p;
         d.checksum = S.checksum.p; d.dirty = S.dirty.p; d.dead = S.dead.p; d.stopped = S.stopped.p;
         d.sorted = S.nt.sorted.p; d.rank = S.rank.p; d.names = S.nt.d_bytes.p; d.noff = S.nt.d_noff.p;

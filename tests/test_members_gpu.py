@@ -31,8 +31,13 @@ def device_state(m, names):
     return {a: (int(st[i]), int(inc[i])) for a, i in zip(names, ids) if ex[i]}
 
 
+@pytest.mark.parametrize("fold", ["default", "bucket"])
 @pytest.mark.parametrize("case_name", ["random", "fixture1332", "leave", "rules"])
-def test_members_match_reference_goldens(gpu, case_name):
+def test_members_match_reference_goldens(gpu, case_name, fold, monkeypatch):
+    """Every membership golden; "bucket" forces the large-batch bucket fold
+    (RP_MEMBERS_BUCKET_FOLD=1) at the goldens' small batch sizes."""
+    if fold == "bucket":
+        monkeypatch.setenv("RP_MEMBERS_BUCKET_FOLD", "1")
     cases = gu.load("membership_golden.json")["cases"]
     sel = [c for c in cases if c["name"].startswith("rule/")] if case_name == "rules" else \
         [c for c in cases if c["name"] == case_name]
@@ -54,8 +59,12 @@ def test_members_match_reference_goldens(gpu, case_name):
                 assert m.generate_checksum_string() == op["checksumString"]
 
 
-def test_c3_merge_vs_oracle(gpu, orc):
-    """C3 at full size: 100k members, 100k updates with 1% duplicated addresses."""
+@pytest.mark.parametrize("fold", ["default", "bucket"])
+def test_c3_merge_vs_oracle(gpu, orc, fold, monkeypatch):
+    """C3 at full size: 100k members, 100k updates with 1% duplicated addresses (13 buckets of
+    8,192 ids on the bucket path)."""
+    if fold == "bucket":
+        monkeypatch.setenv("RP_MEMBERS_BUCKET_FOLD", "1")
     S = synth()
     n = k = 100_000
     names, st0, inc0 = S.c3_members(n)
@@ -247,7 +256,7 @@ def test_checksum_groups_wrap_with_reads(gpu, orc, budget, monkeypatch):
     assert m.checksum == o.checksum
 
 
-@pytest.mark.parametrize("sorted_fold", [False, True], ids=["grouped", "sorted"])
+@pytest.mark.parametrize("sorted_fold", [False, True, "bucket"], ids=["grouped", "sorted", "bucket"])
 def test_hot_addresses_take_the_overflow_fold(gpu, orc, sorted_fold, monkeypatch):
     """The grouped fold handles up to 16 changes per address in a batch; an address with more
     (here 17 and 60, next to addresses with exactly 16 and 15; later 3000 and 500 changes, so
@@ -255,7 +264,9 @@ def test_hot_addresses_take_the_overflow_fold(gpu, orc, sorted_fold, monkeypatch
     the gated overflow launch. Every batch - before, during and after the overflow - must match
     the oracle, and the grouped fold's per-address state must be clean again after an
     overflowing batch."""
-    if sorted_fold:
+    if sorted_fold == "bucket":
+        monkeypatch.setenv("RP_MEMBERS_BUCKET_FOLD", "1")
+    elif sorted_fold:
         monkeypatch.setenv("RP_MEMBERS_SORTED_FOLD", "1")
     S = synth()
     n = 3000
@@ -285,3 +296,40 @@ def test_hot_addresses_take_the_overflow_fold(gpu, orc, sorted_fold, monkeypatch
         assert np.array_equal(ga > 0, oa > 0), b
         assert m.checksum == o.checksum, b
     assert m.generate_checksum_string() == o.checksum_string()
+
+
+def test_bucket_fold_repeats_overflow_and_large_batch(gpu, orc, monkeypatch):
+    """The bucket fold (batches of 2^19+ changes by default) against the oracle: a 2^20-change
+    batch over 2^20 members (128 buckets; its applied flags, rewritten updates and checksum), and
+    a batch whose first two buckets hold 6,000 addresses with two changes each (12,000 repeated
+    changes: more than a bucket's LDS list of 2,048, so the buckets' repeated addresses
+    take the overflow fold); the local member's repeated suspect / faulty changes take the local
+    override."""
+    S = synth()
+    n = 1 << 20
+    names, st0, inc0 = S.c3_members(n)
+    m = gpu.Membership(whoami=names[0], capacity=n)
+    o = orc.Members(names, local=names[0], join_seed=0)
+    ids0 = np.asarray(m.intern(names), dtype=np.uint32)
+    assert (ids0 == np.arange(n)).all()  # device ids are the oracle's positions
+    m.update_ids(ids0, st0, inc0, now_ms=1)
+    o.update_ids(ids0, st0, inc0, False, 1)
+    ids, us, ui = S.c3_updates(n, n, seed=41, base_inc=inc0)
+    ga, gs, gi, gna = m.update_ids(ids, us, ui, now_ms=1434500000007)
+    oa, os_, oi, ona = o.update_ids(ids, us, ui, False, 1434500000007)
+    assert gna == ona
+    assert np.array_equal(ga > 0, oa > 0)
+    assert np.array_equal(gs[oa > 0], os_[oa > 0]) and np.array_equal(gi[oa > 0], oi[oa > 0])
+    assert m.checksum == o.checksum
+    monkeypatch.setenv("RP_MEMBERS_BUCKET_FOLD", "1")
+    rng = np.random.default_rng(9)
+    rep = rng.permutation(16384)[:6000].astype(np.uint32)
+    ids = np.concatenate([rep, rng.integers(0, n, 20000).astype(np.uint32), rep[::-1], [0, 0, 0]]).astype(np.uint32)
+    us = rng.integers(0, 4, len(ids)).astype(np.uint8)
+    ui = (inc0[ids] + rng.integers(-1, 3, len(ids))).astype(np.int64)
+    ga, gs, gi, gna = m.update_ids(ids, us, ui, now_ms=1434500000009)
+    oa, os_, oi, ona = o.update_ids(ids, us, ui, False, 1434500000009)
+    assert gna == ona
+    assert np.array_equal(ga > 0, oa > 0)
+    assert np.array_equal(gs[oa > 0], os_[oa > 0]) and np.array_equal(gi[oa > 0], oi[oa > 0])
+    assert m.checksum == o.checksum

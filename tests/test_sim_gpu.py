@@ -136,11 +136,16 @@ def test_sim_vs_oracle(gpu, orc, n, k, seed, susp):
 
 
 @pytest.mark.parametrize("twins", ["0", "1"])
-@pytest.mark.parametrize("kernel", ["pc", "lanes", "pc3", "pc32", "pair"])
+@pytest.mark.parametrize("kernel", ["pc", "lanes", "pc3", "pc32", "pair", "lanes-p1", "pc32-p1", "lanes+p1"])
 def test_sim_checksum_kernels_vs_oracle(gpu, orc, monkeypatch, kernel, twins):
     """Both lane-checksum kernels (k_ck_pc: chain wave + producer waves; k_ck_lanes: one wave per
     64 nodes), forced through RP_SIM_CK, against the oracle on a case with many deviations; with
-    and without the twin-view pass (equal views hash once, compacted view lists)."""
+    and without the twin-view pass (equal views hash once, compacted view lists). "-p1": each lane
+    walks its own view's pass 1 (RP_SIM_PASS1=0) instead of k_pass1's wave per view, "+p1" the
+    other way round (k_ck_lanes defaults to its own walks)."""
+    if kernel[-3:] in ("-p1", "+p1"):
+        monkeypatch.setenv("RP_SIM_PASS1", "0" if kernel[-3] == "-" else "1")
+        kernel = kernel[:-3]
     monkeypatch.setenv("RP_SIM_CK", kernel)
     monkeypatch.setenv("RP_SIM_TWINS", twins)
     monkeypatch.setenv("RP_SIM_TWIN_VERIFY", twins)
