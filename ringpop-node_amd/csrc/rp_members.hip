@@ -393,7 +393,7 @@ __global__ __launch_bounds__(1024) void k_fold_ovf(const uint32_t* __restrict__ 
 //   k_bk_gather  applied / new status / new incarnation per change in batch order
 constexpr uint32_t kBkBits = 13, kBk = 1u << kBkBits;  // ids per bucket (128 KB of rows)
 constexpr uint32_t kBkTile = 4096;                     // changes per count / scatter tile
-constexpr uint32_t kBkDup = 2048;                      // repeated-address changes a bucket sorts in LDS
+constexpr uint32_t kBkDup = 1024;  // repeated-address changes a bucket sorts in LDS (72 KB in all: two workgroups per CU)
 constexpr uint32_t kBkMaxBuckets = 1024;               // (LDS of the count / scatter tiles): 8M ids
 constexpr uint8_t kResLocal = 4;                       // res: the local override rewrote (status, inc)
 
@@ -409,10 +409,16 @@ __global__ __launch_bounds__(256) void k_bk_count(const uint32_t* __restrict__ i
     for (uint32_t b = threadIdx.x; b < nb; b += 256) h[b] = 0;
     __syncthreads();
     const uint32_t t = blockIdx.x, base = t * kBkTile;
-    for (uint32_t i = threadIdx.x; i < kBkTile; i += 256) {
-        const uint32_t j = base + i;
-        if (j < k) atomicAdd(&h[ids[j] >> kBkBits], 1u);
+    constexpr uint32_t PER = kBkTile / 256;
+    uint32_t idv[PER];
+#pragma unroll
+    for (uint32_t q = 0; q < PER; q++) {  // every load in flight before the first atomic
+        const uint32_t j = base + threadIdx.x + q * 256;
+        idv[q] = j < k ? ids[j] : 0xFFFFFFFFu;
     }
+#pragma unroll
+    for (uint32_t q = 0; q < PER; q++)
+        if (idv[q] != 0xFFFFFFFFu) atomicAdd(&h[idv[q] >> kBkBits], 1u);
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < nb; b += 256) counts[(uint64_t)b * ntiles + t] = h[b];
 }
@@ -422,7 +428,8 @@ __global__ __launch_bounds__(256) void k_bk_count(const uint32_t* __restrict__ i
 __global__ __launch_bounds__(256) void k_bk_scatter(const uint32_t* __restrict__ ids, const uint8_t* __restrict__ chs,
                                                     const int64_t* __restrict__ chi, uint32_t k, uint32_t nb,
                                                     uint32_t ntiles, const uint32_t* __restrict__ offs,
-                                                    BRec* __restrict__ recs, uint32_t* __restrict__ pos) {
+                                                    BRec* __restrict__ recs, uint32_t* __restrict__ bid,
+                                                    uint32_t* __restrict__ pos) {
     __shared__ uint32_t h[kBkMaxBuckets], ls[kBkMaxBuckets], gs[kBkMaxBuckets], s_w[4];
     __shared__ uint4 stage[kBkTile];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -435,12 +442,17 @@ __global__ __launch_bounds__(256) void k_bk_scatter(const uint32_t* __restrict__
     __syncthreads();
     constexpr uint32_t PER = kBkTile / 256;
     uint32_t rk[PER], idv[PER];
+    uint8_t stv[PER];
+    int64_t incv[PER];
 #pragma unroll
-    for (uint32_t q = 0; q < PER; q++) {
+    for (uint32_t q = 0; q < PER; q++) {  // every load in flight before the first atomic
         const uint32_t i = tid + q * 256;
         idv[q] = i < n ? ids[base + i] : 0u;
-        rk[q] = i < n ? atomicAdd(&h[idv[q] >> kBkBits], 1u) : 0u;
+        stv[q] = i < n ? chs[base + i] : (uint8_t)0;
+        incv[q] = i < n ? chi[base + i] : 0;
     }
+#pragma unroll
+    for (uint32_t q = 0; q < PER; q++) rk[q] = tid + q * 256 < n ? atomicAdd(&h[idv[q] >> kBkBits], 1u) : 0u;
     __syncthreads();
     // exclusive scan of h over the buckets (contiguous runs per thread, then across threads)
     const uint32_t per = (nb + 255) / 256, b0 = min(nb, tid * per), b1 = min(nb, b0 + per);
@@ -466,8 +478,8 @@ __global__ __launch_bounds__(256) void k_bk_scatter(const uint32_t* __restrict__
         const uint32_t i = tid + q * 256;
         if (i < n) {
             const uint32_t j = base + i, b = idv[q] >> kBkBits;
-            const int64_t inc8 = chi[j];
-            stage[ls[b] + rk[q]] = uint4{idv[q], j | ((uint32_t)(chs[j] & 3u) << 30), (uint32_t)(uint64_t)inc8,
+            const int64_t inc8 = incv[q];
+            stage[ls[b] + rk[q]] = uint4{idv[q], j | ((uint32_t)(stv[q] & 3u) << 30), (uint32_t)(uint64_t)inc8,
                                          (uint32_t)((uint64_t)inc8 >> 32)};
             pos[j] = gs[b] + rk[q];
         }
@@ -475,8 +487,9 @@ __global__ __launch_bounds__(256) void k_bk_scatter(const uint32_t* __restrict__
     __syncthreads();
     for (uint32_t q = tid; q < n; q += 256) {
         const uint4 v = stage[q];
-        const uint32_t b = v.x >> kBkBits;
-        *reinterpret_cast<uint4*>(recs + gs[b] + (q - ls[b])) = v;
+        const uint32_t b = v.x >> kBkBits, d = gs[b] + (q - ls[b]);
+        *reinterpret_cast<uint4*>(recs + d) = v;
+        bid[d] = v.x;  // the ids alone, for the fold's counter pass
     }
 }
 
@@ -505,7 +518,8 @@ __device__ __forceinline__ uint8_t bk_step(const FoldArgs& A, uint32_t id, bool&
 // bucket's ids in id order, so the rows move as whole lines: a single change folds at once,
 // repeated changes go to the sorted LDS list (one lane per address, in batch order), more than
 // kSlots + 1 changes (or a list that would overflow) to the overflow fold.
-__global__ __launch_bounds__(1024) void k_bk_fold(const BRec* __restrict__ recs, const uint32_t* __restrict__ offs,
+__global__ __launch_bounds__(1024) void k_bk_fold(const BRec* __restrict__ recs, const uint32_t* __restrict__ bid,
+                                                  const uint32_t* __restrict__ offs,
                                                   uint32_t ntiles, uint32_t nb, FoldArgs A,
                                                   const uint32_t* __restrict__ pos, uint8_t* __restrict__ res,
                                                   uint32_t* __restrict__ ovf, uint32_t* __restrict__ part) {
@@ -517,32 +531,61 @@ __global__ __launch_bounds__(1024) void k_bk_fold(const BRec* __restrict__ recs,
     for (uint32_t q = tid; q < kBk; q += 1024) cnt[q] = 0;
     if (tid == 0) s_nd = 0;
     __syncthreads();
-    for (uint32_t p = r0 + tid; p < r1; p += 1024) {
-        const uint32_t il = recs[p].id - id0;
-        atomicAdd(&cnt[il], 1u);
-        map[il] = p;
-    }
-    __syncthreads();
-    {  // the repeated changes the LDS list would take
-        uint32_t v = 0;
-        for (uint32_t q = tid; q < kBk; q += 1024) {
-            const uint32_t c = cnt[q];
-            v += (c > 1 && c <= kSlots + 1) ? c : 0u;
+    // counters; a change that finds its address already counted goes straight to the repeated
+    // list (the first change is added from map below), so no pass re-reads the records for it
+    for (uint32_t p0 = r0 + tid; p0 < r1; p0 += 8 * 1024) {  // 8 id loads in flight per lane
+        uint32_t il[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const uint32_t p = p0 + q * 1024;
+            il[q] = p < r1 ? bid[p] - id0 : 0xFFFFFFFFu;
         }
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-        if ((tid & 63) == 0 && v) atomicAdd(&s_nd, v);
+        for (int q = 0; q < 8; q++)
+            if (il[q] != 0xFFFFFFFFu) {
+                const uint32_t p = p0 + q * 1024;
+                const uint32_t old = atomicAdd(&cnt[il[q]], 1u);
+                if (old == 0) {
+                    map[il[q]] = p;
+                } else {
+                    const uint32_t e = atomicAdd(&s_nd, 1u);
+                    if (e < kBkDup) dk[e] = ((uint64_t)il[q] << 32) | (recs[p].js & 0x3FFFFFFFu);
+                }
+            }
     }
+    __syncthreads();
+    // + the first change of every repeated address
+    for (uint32_t q = tid; q < kBk; q += 1024)
+        if (cnt[q] > 1) {
+            const uint32_t e = atomicAdd(&s_nd, 1u);
+            if (e < kBkDup) dk[e] = ((uint64_t)q << 32) | (recs[map[q]].js & 0x3FFFFFFFu);
+        }
     __syncthreads();
     const uint32_t nd = s_nd;
     const bool listed = nd <= kBkDup;  // block-uniform
     uint32_t napp = 0;
-    for (uint32_t q = tid; q < kBk; q += 1024) {  // ids in order: coalesced rows
+    constexpr uint32_t PI = kBk / 1024;  // ids per lane
+    uint4 rv[PI];
+    uint4 wv4[PI];
+#pragma unroll
+    for (uint32_t u = 0; u < PI; u++) {  // each lane's records and rows in flight together
+        const uint32_t q = tid + u * 1024;
+        if (cnt[q] == 1) {
+            rv[u] = *reinterpret_cast<const uint4*>(recs + map[q]);
+            wv4[u] = *reinterpret_cast<const uint4*>(A.rows + id0 + q);
+        }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < PI; u++) {  // ids in order: coalesced rows
+        const uint32_t q = tid + u * 1024;
         const uint32_t c = cnt[q], id = id0 + q;
         if (c == 1) {
             const uint32_t p = map[q];
-            const uint4 v = *reinterpret_cast<const uint4*>(recs + p);
-            const MRow row = row_load(A.rows + id);
+            const uint4 v = rv[u];
+            MRow row;
+            row.inc = (int64_t)(((uint64_t)wv4[u].y << 32) | wv4[u].x);
+            row.status = (uint8_t)(wv4[u].z & 0xFFu);
+            row.exists = (uint8_t)((wv4[u].z >> 8) & 0xFFu);
             bool ex = row.exists != 0;
             uint8_t st = row.status;
             int64_t in = row.inc;
@@ -556,15 +599,7 @@ __global__ __launch_bounds__(1024) void k_bk_fold(const BRec* __restrict__ recs,
         }
     }
     __syncthreads();
-    if (tid == 0) s_nd = 0;
-    __syncthreads();
-    if (listed && nd) {  // repeated addresses: list, sort by (address, batch index), fold per address
-        for (uint32_t p = r0 + tid; p < r1; p += 1024) {
-            const uint2 v = *reinterpret_cast<const uint2*>(recs + p);
-            const uint32_t c = cnt[v.x - id0];
-            if (c > 1 && c <= kSlots + 1) dk[atomicAdd(&s_nd, 1u)] = ((uint64_t)(v.x - id0) << 32) | (v.y & 0x3FFFFFFFu);
-        }
-        __syncthreads();
+    if (listed && nd) {  // repeated addresses: sort by (address, batch index), fold per address
         uint32_t np = 1;
         while (np < nd) np <<= 1;
         for (uint32_t q = nd + tid; q < np; q += 1024) dk[q] = ~0ull;
@@ -586,6 +621,7 @@ __global__ __launch_bounds__(1024) void k_bk_fold(const BRec* __restrict__ recs,
         for (uint32_t q = tid; q < nd; q += 1024) {
             const uint32_t il = (uint32_t)(dk[q] >> 32);
             if (q > 0 && (uint32_t)(dk[q - 1] >> 32) == il) continue;  // not a segment head
+            if (cnt[il] > kSlots + 1) continue;                         // the overflow fold's
             const uint32_t id = id0 + il;
             const MRow row = row_load(A.rows + id);
             bool ex = row.exists != 0;
@@ -999,7 +1035,7 @@ struct Members {
     DevBuf<uint32_t> g_part;  // per-workgroup applied counts of k_fold_fast (per bucket: k_bk_fold)
     // the bucket path (batches of kBkMin changes or more without damp scoring; RP_MEMBERS_BUCKET_FOLD
     // = 0 | 1 overrides the size rule)
-    DevBuf<uint32_t> bk_counts, bk_pos;
+    DevBuf<uint32_t> bk_counts, bk_pos, bk_bid;
     DevBuf<BRec> bk_recs;
     DevBuf<uint8_t> bk_res;
     static constexpr uint32_t kBkMin = 1u << 19;
@@ -1111,14 +1147,16 @@ struct Members {
             const uint64_t nc = (uint64_t)nb * ntiles;
             bk_counts.reserve(nc + 1);
             bk_recs.reserve(k);
+            bk_bid.reserve(k);
             bk_pos.reserve(k);
             bk_res.reserve(k);
             g_part.reserve(nb + 1);
             hipLaunchKernelGGL(k_bk_count, dim3(ntiles), dim3(256), 0, s, ids, k, nb, ntiles, bk_counts.p);
             scan_exclusive_u32(bk_counts.p, bk_counts.p, nc, s, ws);
             hipLaunchKernelGGL(k_bk_scatter, dim3(ntiles), dim3(256), 0, s, ids, chs, chi, k, nb, ntiles, bk_counts.p,
-                               bk_recs.p, bk_pos.p);
-            hipLaunchKernelGGL(k_bk_fold, dim3(nb), dim3(1024), 0, s, bk_recs.p, bk_counts.p, ntiles, nb, A, bk_pos.p,
+                               bk_recs.p, bk_bid.p, bk_pos.p);
+            hipLaunchKernelGGL(k_bk_fold, dim3(nb), dim3(1024), 0, s, bk_recs.p, bk_bid.p, bk_counts.p, ntiles, nb, A,
+                               bk_pos.p,
                                bk_res.p, ovf, g_part.p);
             if (applied || nst || ninc)
                 hipLaunchKernelGGL(k_bk_gather, dim3(grid_for(k, 256, 1u << 30)), dim3(256), 0, s, bk_pos.p, bk_res.p,

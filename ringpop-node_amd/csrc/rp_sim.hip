@@ -3287,7 +3287,7 @@ struct MsgBuf {
     uint64_t bytes() const { return sizeof(Msg) * tot_msg + sizeof(Rec) * tot_rec; }
     void size_for(uint64_t b) {
         if (b + 8 > buf.cap) {
-            const uint64_t c = std::max<uint64_t>(b + 8, buf.cap + buf.cap / 2);
+            const uint64_t c = std::max<uint64_t>(b + 8, 2 * buf.cap);
             buf.reserve(c);
         }
     }
@@ -4027,6 +4027,15 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
         S.stopped.reserve(L1);
         S.bounds.reserve(nshards + 1);
         S.pool.reserve(2 * L1 * cap + arena);
+        // The message buffers up front for a stage where every local node sends a full change list
+        // (C5: 5.4 GB each): growing them mid-run (a hipFree + hipMalloc of gigabytes) stalled a
+        // peak round by 0.1 s. RP_SIM_MSG_BYTES caps the reservation (they still grow past it).
+        {
+            const uint64_t want = (uint64_t)L1 * (sizeof(rp::Msg) + sizeof(rp::Rec) * cap) + 4096;
+            const uint64_t lim = env_u64("RP_SIM_MSG_BYTES", 16ull << 30);
+            S.out.size_for(std::min(want, lim));
+            S.in.size_for(std::min(want, lim));
+        }
         S.cand.reserve((uint64_t)S.grid * n);
         // the inverse permutation that makes D1 sub-linear (RP_SIM_OPOS_BYTES = 0 turns it off:
         // every ping-req sender then scans its members array)

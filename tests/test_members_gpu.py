@@ -302,7 +302,7 @@ def test_bucket_fold_repeats_overflow_and_large_batch(gpu, orc, monkeypatch):
     """The bucket fold (batches of 2^19+ changes by default) against the oracle: a 2^20-change
     batch over 2^20 members (128 buckets; its applied flags, rewritten updates and checksum), and
     a batch whose first two buckets hold 6,000 addresses with two changes each (12,000 repeated
-    changes: more than a bucket's LDS list of 2,048, so the buckets' repeated addresses
+    changes: more than a bucket's LDS list of 1,024, so the buckets' repeated addresses
     take the overflow fold); the local member's repeated suspect / faulty changes take the local
     override."""
     S = synth()
