@@ -946,6 +946,31 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_generic(const uint8_t* _
     }
 }
 
+// Small host batches (the drop-in's one-key lookup / lookupN calls, index.js:434-471): the keys
+// travel in the kernel arguments and the rows go straight to pinned host memory, so a call is
+// one launch and one stream sync instead of two copies each way (host_lookup).
+constexpr uint32_t kSmallKeys = 64, kSmallBytes = 3072, kSmallW = 16;
+struct SmallKeys {
+    uint32_t n;
+    uint16_t off[kSmallKeys + 1];
+    uint8_t b[kSmallBytes];
+};
+template <int MAXN, class View>
+__global__ __launch_bounds__(64) void k_lookupn_small(const SmallKeys sk, View rv, int np, uint32_t W,
+                                                      uint32_t* __restrict__ out, uint8_t* __restrict__ counts) {
+    __shared__ uint8_t kb[kSmallBytes];
+    const uint32_t k = threadIdx.x, nb = sk.off[sk.n];
+    for (uint32_t i = k; i < nb; i += 64) kb[i] = sk.b[i];
+    __syncthreads();
+    if (k >= sk.n) return;
+    const uint32_t b = sk.off[k], e = sk.off[k + 1];
+    const uint32_t i = rv.find(fh::hash32(fh::PtrSrc{kb + b}, e - b));
+    uint32_t res[MAXN];
+    const int c = ring_walk<MAXN>(rv, i, np, res);
+    for (uint32_t q = 0; q < W; q++) out[k * W + q] = q < (uint32_t)MAXN ? res[q] : NIL;
+    if (counts) counts[k] = (uint8_t)(c > 255 ? 255 : c);
+}
+
 // ---- build kernels ----
 
 // tokens[a*R + i] = farmhash32(name(ids[a]) + String(i)); owners likewise = ids[a].
@@ -1187,6 +1212,11 @@ struct Ring {
     DevBuf<uint32_t> scalar;
     DevBuf<uint32_t> io_a, io_b;
     DevBuf<uint8_t> io_keys, io_cnt;
+    // pinned, device-mapped rows / counts of the small host path (k_lookupn_small)
+    uint32_t* pin_out = nullptr;
+    uint8_t* pin_cnt = nullptr;
+    uint32_t* pin_out_dev = nullptr;
+    uint8_t* pin_cnt_dev = nullptr;
     DevBuf<uint64_t> io_off;
     // group keys by owner (handleOrProxyAll)
     DevBuf<uint32_t> grp_own, grp_key, grp_first, grp_dk, grp_dv, grp_rank;
@@ -1708,6 +1738,8 @@ int rp_ring_destroy(rp_ring* r) {
             (void)hipStreamSynchronize(r->impl.st);
             (void)hipStreamDestroy(r->impl.st);
         }
+        if (r->impl.pin_out) (void)hipHostFree(r->impl.pin_out);
+        if (r->impl.pin_cnt) (void)hipHostFree(r->impl.pin_cnt);
         delete r;
     });
 }
@@ -1882,9 +1914,46 @@ int rp_ring_lookupn_hashes_dev(rp_ring* h, const uint32_t* d_hashes, uint64_t n,
 }
 
 // host-buffer forms: stage through the handle's device buffers on its stream
+// The small path: at most kSmallKeys keys of kSmallBytes in all, rows of at most kSmallW owners,
+// on the wide view (binary search + the reference walk). RP_RING_SMALL=0 turns it off (A/B).
+static bool host_lookup_small(rp::Ring& r, const char* keys, const uint64_t* off, uint32_t stride, uint64_t n, int np,
+                              uint32_t W, uint32_t* owners, uint8_t* counts) {
+    using namespace rp;
+    const char* se = getenv("RP_RING_SMALL");
+    const bool on = !(se && !strcmp(se, "0"));
+    const int need = np <= 0 ? 1 : np;
+    if (!on || n > kSmallKeys || W > kSmallW || need > 8 || r.M == 0) return false;
+    const uint64_t bytes = stride ? n * stride : off[n] - off[0];
+    if (bytes > kSmallBytes) return false;
+    SmallKeys sk;
+    sk.n = (uint32_t)n;
+    for (uint64_t k = 0; k <= n; k++) sk.off[k] = (uint16_t)(stride ? k * stride : off[k] - off[0]);
+    memcpy(sk.b, keys + (stride ? 0 : off[0]), bytes);
+    if (!r.pin_out) {
+        RP_HIP(hipHostMalloc(reinterpret_cast<void**>(&r.pin_out), 4ull * kSmallKeys * kSmallW, hipHostMallocMapped));
+        RP_HIP(hipHostMalloc(reinterpret_cast<void**>(&r.pin_cnt), kSmallKeys, hipHostMallocMapped));
+        RP_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&r.pin_out_dev), r.pin_out, 0));
+        RP_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&r.pin_cnt_dev), r.pin_cnt, 0));
+    }
+    const auto rv = r.view();
+    uint8_t* cd = counts ? r.pin_cnt_dev : nullptr;
+    if (need == 1)
+        hipLaunchKernelGGL((k_lookupn_small<1, decltype(rv)>), dim3(1), dim3(64), 0, r.st, sk, rv, np, W, r.pin_out_dev, cd);
+    else if (need <= 4)
+        hipLaunchKernelGGL((k_lookupn_small<4, decltype(rv)>), dim3(1), dim3(64), 0, r.st, sk, rv, np, W, r.pin_out_dev, cd);
+    else
+        hipLaunchKernelGGL((k_lookupn_small<8, decltype(rv)>), dim3(1), dim3(64), 0, r.st, sk, rv, np, W, r.pin_out_dev, cd);
+    RP_HIP(hipGetLastError());
+    RP_HIP(hipStreamSynchronize(r.st));
+    memcpy(owners, r.pin_out, 4ull * n * W);
+    if (counts) memcpy(counts, r.pin_cnt, n);
+    return true;
+}
+
 static void host_lookup(rp::Ring& r, const char* keys, const uint64_t* off, uint32_t stride, const uint32_t* hashes,
                         uint64_t n, int np, uint32_t W, uint32_t* owners, uint8_t* counts) {
     if (n == 0) return;
+    if (!hashes && host_lookup_small(r, keys, off, stride, n, np, W, owners, counts)) return;
     const uint8_t* dk = nullptr;
     const uint64_t* doff = nullptr;
     const uint32_t* dh = nullptr;

@@ -171,6 +171,31 @@ def test_variable_length_keys_vs_oracle(gpu, orc):
         assert [ring.name(x) for x in row[:c]] == [oracle.name(x) for x in oracle.lookupn_hash(hs[k], 3)]
 
 
+@pytest.mark.parametrize("nkeys", [1, 7, 64, 65])
+def test_small_host_batches_vs_oracle(gpu, orc, nkeys, monkeypatch):
+    """The one-call drop-in path: host batches of at most 64 keys (3 KB) and 16 owners per row
+    go through the kernel arguments and pinned memory (k_lookupn_small); 65 keys, a 3,100-byte
+    key or wider rows take the staged path. Both against the oracle, lookup and lookupN(n) for
+    n = 0..20."""
+    ring, oracle = _random_history(orc, gpu, 8, 50, 100, 3)
+    rng = random.Random(nkeys)
+    keys = ["".join(rng.choice("abcdef0123456789:-./") for _ in range(rng.randint(0, 45))) for _ in range(nkeys)]
+    if nkeys == 7:
+        keys[3] = "y" * 3100  # past the inline bytes: the staged path
+    hs = [orc.hash32(k) for k in keys]
+    got = ring.lookup_ids(keys)
+    assert [ring.name(x) for x in got] == [oracle.name(oracle.lookup_hash(h)) for h in hs]
+    for n in (0, 1, 2, 3, 8, 9, 16, 17, 20):
+        g, gc = ring.lookupn_ids(keys, n)
+        for k, (row, c) in enumerate(zip(g, gc)):
+            assert [ring.name(x) for x in row[:c]] == [oracle.name(x) for x in oracle.lookupn_hash(hs[k], n)], (n, k)
+    monkeypatch.setenv("RP_RING_SMALL", "0")
+    g0, c0 = ring.lookupn_ids(keys, 3)
+    monkeypatch.delenv("RP_RING_SMALL")
+    g1, c1 = ring.lookupn_ids(keys, 3)
+    assert np.array_equal(g0, g1) and np.array_equal(c0, c1)
+
+
 def test_device_farmhash_and_keygen(gpu, orc):
     rng = random.Random(2)
     strs = [bytes(rng.randrange(256) for _ in range(n)) for n in list(range(0, 80)) * 3 + [500, 4096]]
