@@ -378,24 +378,46 @@ __global__ __launch_bounds__(1024) void k_fold_ovf(const uint32_t* __restrict__ 
 // (a stable-per-id order is not needed: an address's changes are put back in arrival order by
 // their batch index), then one workgroup folds one bucket with the bucket's 128 KB of rows
 // resident in its XCD's L2, so the row accesses and the rank counters stop being random HBM /
-// memory-side atomics (k_link's one atomic per change was half of a 2^22 batch). The per-change
-// outputs come back in batch order through the record positions (pos) and a 1-byte result per
-// record: a coalesced gather reads res, which fits L2.
-//   k_bk_count   per 4,096-change tile: the bucket histogram (bucket-major counts)
-//   scan         offsets of every (bucket, tile) run
-//   k_bk_scatter 16-B records {id, batch index | status << 30, incarnation} into bucket runs,
-//                pos[j] = the record's position
-//   k_bk_fold    a workgroup per bucket: LDS counters per id; single changes fold at once, an
-//                address's repeated changes are sorted by batch index in LDS and folded by one
-//                lane; an address with more than kSlots + 1 changes (or a bucket whose repeated
-//                changes overflow the LDS list) is marked for the overflow fold (k_fold_ovf /
-//                k_ovf_len, as on the grouped path)
-//   k_bk_gather  applied / new status / new incarnation per change in batch order
-constexpr uint32_t kBkBits = 13, kBk = 1u << kBkBits;  // ids per bucket (128 KB of rows)
-constexpr uint32_t kBkTile = 4096;                     // changes per count / scatter tile
-constexpr uint32_t kBkDup = 1024;  // repeated-address changes a bucket sorts in LDS (72 KB in all: two workgroups per CU)
-constexpr uint32_t kBkMaxBuckets = 1024;               // (LDS of the count / scatter tiles): 8M ids
-constexpr uint8_t kResLocal = 4;                       // res: the local override rewrote (status, inc)
+// memory-side atomics (k_link's one atomic per change was half of a 2^22 batch). Three launches:
+//   k_bk_scatter a 4,096-change tile sorts its 16-B records {id, batch index | status << 30,
+//                incarnation} by bucket in LDS and stores them as one contiguous run at
+//                recs + tile * kBkTile (whole lines); seg[bucket][tile] = the bucket's segment
+//                of that run (start << 16 | length). No global count pass or scan: the fold
+//                walks a bucket's segments of every tile.
+//   k_bk_fold    a workgroup per bucket: reads the bucket's segments once, in order, keeping
+//                per id the change count and the first change (batch index, status,
+//                incarnation) in LDS; then the bucket's ids in id order (rows as whole lines):
+//                a single change folds from LDS, an address's repeated changes are sorted by
+//                batch index in LDS and folded by one lane; an address with more than kSlots + 1
+//                changes (or a bucket whose repeated changes overflow the LDS list) is marked
+//                for the overflow fold (k_fold_ovf / k_ovf_len, as on the grouped path). The
+//                1-B result goes to resid[id] (coalesced), or to resj[batch index] for an
+//                address with repeated changes (resid holds kResRep)
+//   k_bk_gather  applied per change in batch order, from resid[ids[j]] (4 MB, L2-resident),
+//                four changes per lane (the new status / incarnation outputs are copied from the
+//                input by k_bk_scatter; the fold rewrites the local overrides)
+#ifndef RP_BK_BITS
+#define RP_BK_BITS 12
+#endif
+#ifndef RP_BK_FT
+#define RP_BK_FT 512
+#endif
+constexpr uint32_t kBkBits = RP_BK_BITS, kBk = 1u << kBkBits;  // ids per bucket (4,096: 64 KB of rows)
+constexpr uint32_t kBkTile = 4096;                             // changes per scatter tile
+constexpr uint32_t kBkST = 1024;                               // threads per scatter tile
+constexpr uint32_t kBkFT = RP_BK_FT;                           // threads per fold workgroup
+constexpr uint32_t kBkDup = kBkFT;                             // repeated-address changes a bucket sorts in LDS
+static_assert(kBkDup <= 1024, "k_bk_fold: one repeated change per thread, 10-bit entry in the key");
+static_assert(kBk % kBkFT == 0 && kBkFT % 64 == 0, "k_bk_fold: whole ids per lane");
+constexpr uint32_t kBkMaxBuckets = 2048;               // (LDS of the scatter tiles): 8M ids
+constexpr uint8_t kResLocal = 4;                       // result: the local override rewrote (status, inc)
+constexpr uint8_t kResRep = 8;                         // resid: repeated changes, results in resj
+
+// seg layout: groups of 16 buckets, then tile, then bucket (one 64-B line per (group, tile)), so
+// a scatter tile writes whole lines and the 16 buckets that share a line fold on one XCD
+__host__ __device__ __forceinline__ uint64_t seg_at(uint32_t b, uint32_t t, uint32_t ntiles) {
+    return ((uint64_t)(b >> 4) * ntiles + t) * 16 + (b & 15u);
+}
 
 struct alignas(16) BRec {
     uint32_t id;
@@ -403,59 +425,43 @@ struct alignas(16) BRec {
     int64_t inc;
 };
 
-__global__ __launch_bounds__(256) void k_bk_count(const uint32_t* __restrict__ ids, uint32_t k, uint32_t nb,
-                                                  uint32_t ntiles, uint32_t* __restrict__ counts) {
-    __shared__ uint32_t h[kBkMaxBuckets];
-    for (uint32_t b = threadIdx.x; b < nb; b += 256) h[b] = 0;
-    __syncthreads();
-    const uint32_t t = blockIdx.x, base = t * kBkTile;
-    constexpr uint32_t PER = kBkTile / 256;
-    uint32_t idv[PER];
-#pragma unroll
-    for (uint32_t q = 0; q < PER; q++) {  // every load in flight before the first atomic
-        const uint32_t j = base + threadIdx.x + q * 256;
-        idv[q] = j < k ? ids[j] : 0xFFFFFFFFu;
-    }
-#pragma unroll
-    for (uint32_t q = 0; q < PER; q++)
-        if (idv[q] != 0xFFFFFFFFu) atomicAdd(&h[idv[q] >> kBkBits], 1u);
-    __syncthreads();
-    for (uint32_t b = threadIdx.x; b < nb; b += 256) counts[(uint64_t)b * ntiles + t] = h[b];
-}
-
-// A tile's records go through LDS in bucket order, so each bucket's run leaves as consecutive
-// 16-B stores (a wave writes a few whole lines instead of 64 scattered records).
-__global__ __launch_bounds__(256) void k_bk_scatter(const uint32_t* __restrict__ ids, const uint8_t* __restrict__ chs,
+__global__ __launch_bounds__(kBkST) void k_bk_scatter(const uint32_t* __restrict__ ids, const uint8_t* __restrict__ chs,
                                                     const int64_t* __restrict__ chi, uint32_t k, uint32_t nb,
-                                                    uint32_t ntiles, const uint32_t* __restrict__ offs,
-                                                    BRec* __restrict__ recs, uint32_t* __restrict__ bid,
-                                                    uint32_t* __restrict__ pos) {
-    __shared__ uint32_t h[kBkMaxBuckets], ls[kBkMaxBuckets], gs[kBkMaxBuckets], s_w[4];
+                                                    uint32_t ntiles, BRec* __restrict__ recs,
+                                                    uint32_t* __restrict__ seg, uint8_t* __restrict__ nst,
+                                                    int64_t* __restrict__ ninc) {
     __shared__ uint4 stage[kBkTile];
+    __shared__ uint32_t h[kBkMaxBuckets], s_w[kBkST / 64];
+    __shared__ uint16_t ls[kBkMaxBuckets];  // <= 4,096 (76 KB in all: two tiles per CU)
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t t = blockIdx.x, base = t * kBkTile;
     const uint32_t n = k - base < kBkTile ? k - base : kBkTile;
-    for (uint32_t b = tid; b < nb; b += 256) {
-        h[b] = 0;
-        gs[b] = offs[(uint64_t)b * ntiles + t];
-    }
+    for (uint32_t b = tid; b < nb; b += kBkST) h[b] = 0;
     __syncthreads();
-    constexpr uint32_t PER = kBkTile / 256;
+    constexpr uint32_t PER = kBkTile / kBkST;
     uint32_t rk[PER], idv[PER];
     uint8_t stv[PER];
     int64_t incv[PER];
 #pragma unroll
     for (uint32_t q = 0; q < PER; q++) {  // every load in flight before the first atomic
-        const uint32_t i = tid + q * 256;
+        const uint32_t i = tid + q * kBkST;
         idv[q] = i < n ? ids[base + i] : 0u;
         stv[q] = i < n ? chs[base + i] : (uint8_t)0;
         incv[q] = i < n ? chi[base + i] : 0;
     }
 #pragma unroll
-    for (uint32_t q = 0; q < PER; q++) rk[q] = tid + q * 256 < n ? atomicAdd(&h[idv[q] >> kBkBits], 1u) : 0u;
+    for (uint32_t q = 0; q < PER; q++) {  // the outputs start as copies; the fold rewrites local overrides
+        const uint32_t i = tid + q * kBkST;
+        if (i < n) {
+            if (nst) nst[base + i] = stv[q];
+            if (ninc) ninc[base + i] = incv[q];
+        }
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < PER; q++) rk[q] = tid + q * kBkST < n ? atomicAdd(&h[idv[q] >> kBkBits], 1u) : 0u;
     __syncthreads();
     // exclusive scan of h over the buckets (contiguous runs per thread, then across threads)
-    const uint32_t per = (nb + 255) / 256, b0 = min(nb, tid * per), b1 = min(nb, b0 + per);
+    const uint32_t per = (nb + kBkST - 1) / kBkST, b0 = min(nb, tid * per), b1 = min(nb, b0 + per);
     uint32_t run = 0;
     for (uint32_t b = b0; b < b1; b++) run += h[b];
     uint32_t inc = run;
@@ -470,27 +476,22 @@ __global__ __launch_bounds__(256) void k_bk_scatter(const uint32_t* __restrict__
     for (uint32_t w = 0; w < wv; w++) ex += s_w[w];
     for (uint32_t b = b0; b < b1; b++) {
         ls[b] = ex;
+        seg[seg_at(b, t, ntiles)] = (ex << 16) | h[b];  // start <= 4,096, length <= 4,096
         ex += h[b];
     }
     __syncthreads();
 #pragma unroll
     for (uint32_t q = 0; q < PER; q++) {
-        const uint32_t i = tid + q * 256;
+        const uint32_t i = tid + q * kBkST;
         if (i < n) {
             const uint32_t j = base + i, b = idv[q] >> kBkBits;
             const int64_t inc8 = incv[q];
             stage[ls[b] + rk[q]] = uint4{idv[q], j | ((uint32_t)(stv[q] & 3u) << 30), (uint32_t)(uint64_t)inc8,
                                          (uint32_t)((uint64_t)inc8 >> 32)};
-            pos[j] = gs[b] + rk[q];
         }
     }
     __syncthreads();
-    for (uint32_t q = tid; q < n; q += 256) {
-        const uint4 v = stage[q];
-        const uint32_t b = v.x >> kBkBits, d = gs[b] + (q - ls[b]);
-        *reinterpret_cast<uint4*>(recs + d) = v;
-        bid[d] = v.x;  // the ids alone, for the fold's counter pass
-    }
+    for (uint32_t q = tid; q < n; q += kBkST) *reinterpret_cast<uint4*>(recs + base + q) = stage[q];
 }
 
 // One change on a member row (the step of fold_address without damp scoring): returns applied
@@ -514,123 +515,135 @@ __device__ __forceinline__ uint8_t bk_step(const FoldArgs& A, uint32_t id, bool&
     return a | loc;
 }
 
-// A workgroup per bucket: per-id change counters and each id's (last) record in LDS; then the
-// bucket's ids in id order, so the rows move as whole lines: a single change folds at once,
-// repeated changes go to the sorted LDS list (one lane per address, in batch order), more than
-// kSlots + 1 changes (or a list that would overflow) to the overflow fold.
-__global__ __launch_bounds__(1024) void k_bk_fold(const BRec* __restrict__ recs, const uint32_t* __restrict__ bid,
-                                                  const uint32_t* __restrict__ offs,
+// A change about the local member that the override rewrote (suspect / faulty: alive at now):
+// its outputs, copied from the input by k_bk_scatter
+__device__ __forceinline__ void bk_local(const FoldArgs& A, uint32_t j) {
+    if (A.new_status) A.new_status[j] = ST_ALIVE;
+    if (A.new_inc) A.new_inc[j] = A.now_ms;
+}
+
+// A workgroup per bucket (72.5 KB of LDS: two per CU): per id the change count and the first
+// change, read from the bucket's segments in record order; then the bucket's ids in id order,
+// so the rows move as whole lines: a single change folds at once, repeated changes go to the
+// sorted LDS list (one lane per address, in batch order), more than kSlots + 1 changes (or a
+// list that would overflow) to the overflow fold.
+__global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs, const uint32_t* __restrict__ seg,
                                                   uint32_t ntiles, uint32_t nb, FoldArgs A,
-                                                  const uint32_t* __restrict__ pos, uint8_t* __restrict__ res,
+                                                  uint8_t* __restrict__ resid, uint8_t* __restrict__ resj,
                                                   uint32_t* __restrict__ ovf, uint32_t* __restrict__ part) {
-    __shared__ uint32_t cnt[kBk], map[kBk];
+    __shared__ uint32_t cnt[kBk], fjs[kBk];
+    __shared__ int64_t finc[kBk];
+    // repeated changes: key (address << 40 | batch index << 10 | entry), the entry's status and
+    // incarnation beside it, so the per-address fold reads only LDS
     __shared__ uint64_t dk[kBkDup];
-    __shared__ uint32_t s_nd, s_w[16];
-    const uint32_t tid = threadIdx.x, b = blockIdx.x, id0 = b << kBkBits;
-    const uint32_t r0 = offs[(uint64_t)b * ntiles], r1 = offs[(uint64_t)(b + 1) * ntiles];
-    for (uint32_t q = tid; q < kBk; q += 1024) cnt[q] = 0;
+    __shared__ int64_t dinc[kBkDup];
+    __shared__ uint8_t dst[kBkDup];
+    __shared__ uint32_t s_nd, s_w[kBkFT / 64];
+    // XCD-aware: blocks are dealt round-robin over the 8 XCDs, so block i's XCD folds the
+    // contiguous bucket range (i % 8) * per ...: neighbouring buckets, whose segments share record
+    // lines in every tile run, fold at the same time in one L2
+    const uint32_t per = (nb + 7) / 8, b = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+    if (b >= nb) return;
+    const uint32_t tid = threadIdx.x, id0 = b << kBkBits;
+    auto dput = [&](uint32_t d, uint32_t il, uint32_t js, int64_t in) {
+        dk[d] = ((uint64_t)il << 40) | ((uint64_t)(js & 0x3FFFFFFFu) << 10) | d;
+        dst[d] = (uint8_t)(js >> 30);
+        dinc[d] = in;
+    };
+    for (uint32_t q = tid; q < kBk; q += kBkFT) cnt[q] = 0;
     if (tid == 0) s_nd = 0;
     __syncthreads();
-    // counters; a change that finds its address already counted goes straight to the repeated
-    // list (the first change is added from map below), so no pass re-reads the records for it
-    for (uint32_t p0 = r0 + tid; p0 < r1; p0 += 8 * 1024) {  // 8 id loads in flight per lane
-        uint32_t il[8];
+    // a lane per tile segment, up to 8 records in flight; a change that finds its address
+    // already counted goes straight to the repeated list (the first change is added below)
+    for (uint32_t t = tid; t < ntiles; t += kBkFT) {
+        const uint32_t e = seg[seg_at(b, t, ntiles)], n = e & 0xFFFFu;
+        const BRec* r = recs + (uint64_t)t * kBkTile + (e >> 16);
+        for (uint32_t i0 = 0; i0 < n; i0 += 8) {
+            uint4 v[8];
 #pragma unroll
-        for (int q = 0; q < 8; q++) {
-            const uint32_t p = p0 + q * 1024;
-            il[q] = p < r1 ? bid[p] - id0 : 0xFFFFFFFFu;
-        }
+            for (uint32_t q = 0; q < 8; q++)
+                v[q] = i0 + q < n ? *reinterpret_cast<const uint4*>(r + i0 + q) : uint4{0, 0, 0, 0};
 #pragma unroll
-        for (int q = 0; q < 8; q++)
-            if (il[q] != 0xFFFFFFFFu) {
-                const uint32_t p = p0 + q * 1024;
-                const uint32_t old = atomicAdd(&cnt[il[q]], 1u);
-                if (old == 0) {
-                    map[il[q]] = p;
-                } else {
-                    const uint32_t e = atomicAdd(&s_nd, 1u);
-                    if (e < kBkDup) dk[e] = ((uint64_t)il[q] << 32) | (recs[p].js & 0x3FFFFFFFu);
+            for (uint32_t q = 0; q < 8; q++)
+                if (i0 + q < n) {
+                    const uint32_t il = v[q].x - id0;
+                    const int64_t in = (int64_t)(((uint64_t)v[q].w << 32) | v[q].z);
+                    const uint32_t old = atomicAdd(&cnt[il], 1u);
+                    if (old == 0) {
+                        fjs[il] = v[q].y;
+                        finc[il] = in;
+                    } else {
+                        const uint32_t d = atomicAdd(&s_nd, 1u);
+                        if (d < kBkDup) dput(d, il, v[q].y, in);
+                    }
                 }
-            }
+        }
     }
     __syncthreads();
     // + the first change of every repeated address
-    for (uint32_t q = tid; q < kBk; q += 1024)
+    for (uint32_t q = tid; q < kBk; q += kBkFT)
         if (cnt[q] > 1) {
-            const uint32_t e = atomicAdd(&s_nd, 1u);
-            if (e < kBkDup) dk[e] = ((uint64_t)q << 32) | (recs[map[q]].js & 0x3FFFFFFFu);
+            const uint32_t d = atomicAdd(&s_nd, 1u);
+            if (d < kBkDup) dput(d, q, fjs[q], finc[q]);
         }
     __syncthreads();
     const uint32_t nd = s_nd;
     const bool listed = nd <= kBkDup;  // block-uniform
     uint32_t napp = 0;
-    constexpr uint32_t PI = kBk / 1024;  // ids per lane
-    uint4 rv[PI];
+    constexpr uint32_t PI = kBk / kBkFT;  // ids per lane
     uint4 wv4[PI];
 #pragma unroll
-    for (uint32_t u = 0; u < PI; u++) {  // each lane's records and rows in flight together
-        const uint32_t q = tid + u * 1024;
-        if (cnt[q] == 1) {
-            rv[u] = *reinterpret_cast<const uint4*>(recs + map[q]);
-            wv4[u] = *reinterpret_cast<const uint4*>(A.rows + id0 + q);
-        }
+    for (uint32_t u = 0; u < PI; u++) {  // each lane's rows in flight together
+        const uint32_t q = tid + u * kBkFT;
+        if (cnt[q] == 1) wv4[u] = *reinterpret_cast<const uint4*>(A.rows + id0 + q);
     }
 #pragma unroll
-    for (uint32_t u = 0; u < PI; u++) {  // ids in order: coalesced rows
-        const uint32_t q = tid + u * 1024;
+    for (uint32_t u = 0; u < PI; u++) {  // ids in order: coalesced rows and results
+        const uint32_t q = tid + u * kBkFT;
         const uint32_t c = cnt[q], id = id0 + q;
+        uint8_t r = 0;
         if (c == 1) {
-            const uint32_t p = map[q];
-            const uint4 v = rv[u];
-            MRow row;
-            row.inc = (int64_t)(((uint64_t)wv4[u].y << 32) | wv4[u].x);
-            row.status = (uint8_t)(wv4[u].z & 0xFFu);
-            row.exists = (uint8_t)((wv4[u].z >> 8) & 0xFFu);
-            bool ex = row.exists != 0;
-            uint8_t st = row.status;
-            int64_t in = row.inc;
-            const uint8_t r = bk_step(A, id, ex, st, in, (uint8_t)(v.y >> 30), (int64_t)(((uint64_t)v.w << 32) | v.z));
+            bool ex = ((wv4[u].z >> 8) & 0xFFu) != 0;
+            uint8_t st = (uint8_t)(wv4[u].z & 0xFFu);
+            int64_t in = (int64_t)(((uint64_t)wv4[u].y << 32) | wv4[u].x);
+            r = bk_step(A, id, ex, st, in, (uint8_t)(fjs[q] >> 30), finc[q]);
             row_store(A.rows + id, in, st, 1);
-            res[p] = r;
+            if (r & kResLocal) bk_local(A, fjs[q] & 0x3FFFFFFFu);
             napp += (r & 3u) ? 1u : 0u;
-        } else if (c > kSlots + 1 || (c > 1 && !listed)) {  // the overflow fold takes the address
-            A.rows[id].cnt = kOvfMark;
-            *ovf = 1u;
+        } else if (c > 1) {
+            r = kResRep;
+            if (c > kSlots + 1 || !listed) {  // the overflow fold takes the address
+                A.rows[id].cnt = kOvfMark;
+                *ovf = 1u;
+            }
         }
+        resid[id] = r;
     }
     __syncthreads();
     if (listed && nd) {  // repeated addresses: sort by (address, batch index), fold per address
-        uint32_t np = 1;
-        while (np < nd) np <<= 1;
-        for (uint32_t q = nd + tid; q < np; q += 1024) dk[q] = ~0ull;
+        // rank sort (nd <= kBkDup <= kBkFT: one key per thread; the wave reads each key as a broadcast)
+        const uint64_t my = tid < nd ? dk[tid] : 0;
+        uint32_t rk = 0;
+        if (tid < nd)
+            for (uint32_t f = 0; f < nd; f++) rk += dk[f] < my ? 1u : 0u;
         __syncthreads();
-        for (uint32_t k2 = 2; k2 <= np; k2 <<= 1)
-            for (uint32_t jj = k2 >> 1; jj > 0; jj >>= 1) {
-                for (uint32_t t = tid; t < np; t += 1024) {
-                    const uint32_t x = t ^ jj;
-                    if (x > t) {
-                        const uint64_t a = dk[t], c = dk[x];
-                        if ((a > c) == ((t & k2) == 0)) {
-                            dk[t] = c;
-                            dk[x] = a;
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-        for (uint32_t q = tid; q < nd; q += 1024) {
-            const uint32_t il = (uint32_t)(dk[q] >> 32);
-            if (q > 0 && (uint32_t)(dk[q - 1] >> 32) == il) continue;  // not a segment head
+        if (tid < nd) dk[rk] = my;
+        __syncthreads();
+        for (uint32_t q = tid; q < nd; q += kBkFT) {
+            const uint32_t il = (uint32_t)(dk[q] >> 40);
+            if (q > 0 && (uint32_t)(dk[q - 1] >> 40) == il) continue;  // not a segment head
             if (cnt[il] > kSlots + 1) continue;                         // the overflow fold's
             const uint32_t id = id0 + il;
             const MRow row = row_load(A.rows + id);
             bool ex = row.exists != 0;
             uint8_t st = row.status;
             int64_t in = row.inc;
-            for (uint32_t e = q; e < nd && (uint32_t)(dk[e] >> 32) == il; e++) {
-                const uint32_t j = (uint32_t)dk[e];
-                const uint8_t r = bk_step(A, id, ex, st, in, A.ch_status[j] & 3u, A.ch_inc[j]);
-                res[pos[j]] = r;
+            for (uint32_t e = q; e < nd && (uint32_t)(dk[e] >> 40) == il; e++) {
+                const uint64_t key = dk[e];
+                const uint32_t j = (uint32_t)(key >> 10) & 0x3FFFFFFFu, x = (uint32_t)key & (kBkDup - 1);
+                const uint8_t r = bk_step(A, id, ex, st, in, dst[x] & 3u, dinc[x]);
+                resj[j] = r;
+                if (r & kResLocal) bk_local(A, j);
                 napp += (r & 3u) ? 1u : 0u;
             }
             row_store(A.rows + id, in, st, ex ? 1 : 0);
@@ -642,22 +655,31 @@ __global__ __launch_bounds__(1024) void k_bk_fold(const BRec* __restrict__ recs,
     __syncthreads();
     if (tid == 0) {
         uint32_t t = 0;
-        for (int w = 0; w < 16; w++) t += s_w[w];
+        for (int w = 0; w < (int)(kBkFT / 64); w++) t += s_w[w];
         part[b] = t;
         if (b == 0) part[nb] = 0;  // the overflow fold's count (k_ovf_len)
     }
 }
 
-__global__ void k_bk_gather(const uint32_t* __restrict__ pos, const uint8_t* __restrict__ res,
-                            const uint8_t* __restrict__ chs, const int64_t* __restrict__ chi, uint32_t k, int64_t now_ms,
-                            uint8_t* __restrict__ applied, uint8_t* __restrict__ nst, int64_t* __restrict__ ninc) {
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= k) return;
-    const uint8_t r = res[pos[j]];
-    const bool loc = (r & kResLocal) != 0;  // suspect / faulty about the local member: alive at now
-    if (applied) applied[j] = r & 3u;
-    if (nst) nst[j] = loc ? (uint8_t)ST_ALIVE : chs[j];
-    if (ninc) ninc[j] = loc ? now_ms : chi[j];
+// applied per change in batch order from resid[ids[j]] (4 MB, L2-resident) or resj[j]. V = 4:
+// four consecutive changes per lane (16-B id loads, 4-B stores; the host checks the alignment).
+template <uint32_t V>
+__global__ __launch_bounds__(256) void k_bk_gather(const uint32_t* __restrict__ ids, const uint8_t* __restrict__ resid,
+                                                   const uint8_t* __restrict__ resj, uint32_t k,
+                                                   uint8_t* __restrict__ applied) {
+    const uint32_t j0 = (blockIdx.x * blockDim.x + threadIdx.x) * V;
+    if (j0 >= k) return;
+    auto one = [&](uint32_t j, uint32_t id) -> uint32_t {
+        const uint8_t r = resid[id];
+        return (r == kResRep ? resj[j] : r) & 3u;
+    };
+    if (V == 4 && j0 + 4 <= k) {
+        const uint4 iv = *reinterpret_cast<const uint4*>(ids + j0);
+        *reinterpret_cast<uint32_t*>(applied + j0) =
+            one(j0, iv.x) | (one(j0 + 1, iv.y) << 8) | (one(j0 + 2, iv.z) << 16) | (one(j0 + 3, iv.w) << 24);
+        return;
+    }
+    for (uint32_t j = j0; j < j0 + V && j < k; j++) applied[j] = (uint8_t)one(j, ids[j]);
 }
 
 // Membership._decayMembersDampScore (index.js:374-383): decayDampScore on every member
@@ -1035,9 +1057,9 @@ struct Members {
     DevBuf<uint32_t> g_part;  // per-workgroup applied counts of k_fold_fast (per bucket: k_bk_fold)
     // the bucket path (batches of kBkMin changes or more without damp scoring; RP_MEMBERS_BUCKET_FOLD
     // = 0 | 1 overrides the size rule)
-    DevBuf<uint32_t> bk_counts, bk_pos, bk_bid;
+    DevBuf<uint32_t> bk_seg;
     DevBuf<BRec> bk_recs;
-    DevBuf<uint8_t> bk_res;
+    DevBuf<uint8_t> bk_resid, bk_resj;
     static constexpr uint32_t kBkMin = 1u << 19;
     bool use_bucket_fold(uint32_t k, uint32_t nb) const {
         if (damp_on || nb > kBkMaxBuckets || k >= (1u << 30) || !grouped_fold) return false;
@@ -1144,23 +1166,24 @@ struct Members {
         const uint32_t nb = (cap + kBk - 1) / kBk;
         if (use_bucket_fold(k, nb)) {
             const uint32_t ntiles = (k + kBkTile - 1) / kBkTile;
-            const uint64_t nc = (uint64_t)nb * ntiles;
-            bk_counts.reserve(nc + 1);
-            bk_recs.reserve(k);
-            bk_bid.reserve(k);
-            bk_pos.reserve(k);
-            bk_res.reserve(k);
+            bk_seg.reserve((uint64_t)((nb + 15) / 16) * 16 * ntiles);
+            bk_recs.reserve((uint64_t)ntiles * kBkTile);
+            bk_resid.reserve((uint64_t)nb * kBk);
+            bk_resj.reserve(k);
             g_part.reserve(nb + 1);
-            hipLaunchKernelGGL(k_bk_count, dim3(ntiles), dim3(256), 0, s, ids, k, nb, ntiles, bk_counts.p);
-            scan_exclusive_u32(bk_counts.p, bk_counts.p, nc, s, ws);
-            hipLaunchKernelGGL(k_bk_scatter, dim3(ntiles), dim3(256), 0, s, ids, chs, chi, k, nb, ntiles, bk_counts.p,
-                               bk_recs.p, bk_bid.p, bk_pos.p);
-            hipLaunchKernelGGL(k_bk_fold, dim3(nb), dim3(1024), 0, s, bk_recs.p, bk_bid.p, bk_counts.p, ntiles, nb, A,
-                               bk_pos.p,
-                               bk_res.p, ovf, g_part.p);
-            if (applied || nst || ninc)
-                hipLaunchKernelGGL(k_bk_gather, dim3(grid_for(k, 256, 1u << 30)), dim3(256), 0, s, bk_pos.p, bk_res.p,
-                                   chs, chi, k, now_ms, applied, nst, ninc);
+            hipLaunchKernelGGL(k_bk_scatter, dim3(ntiles), dim3(kBkST), 0, s, ids, chs, chi, k, nb, ntiles, bk_recs.p,
+                               bk_seg.p, nst, ninc);
+            hipLaunchKernelGGL(k_bk_fold, dim3((nb + 7) / 8 * 8), dim3(kBkFT), 0, s, bk_recs.p, bk_seg.p, ntiles, nb, A,
+                               bk_resid.p, bk_resj.p, ovf, g_part.p);
+            if (applied) {
+                const bool v4 = ((uintptr_t)ids & 15) == 0 && ((uintptr_t)applied & 3) == 0;
+                if (v4)
+                    hipLaunchKernelGGL(k_bk_gather<4>, dim3(grid_for((k + 3) / 4, 256, 1u << 30)), dim3(256), 0, s,
+                                       ids, bk_resid.p, bk_resj.p, k, applied);
+                else
+                    hipLaunchKernelGGL(k_bk_gather<1>, dim3(grid_for(k, 256, 1u << 30)), dim3(256), 0, s, ids,
+                                       bk_resid.p, bk_resj.p, k, applied);
+            }
             RP_HIP(hipGetLastError());
             if (build && nt.size()) {
                 const OvfArgs ov{ids, k, ovf, A, g_part.p, nb, n_applied_out};
