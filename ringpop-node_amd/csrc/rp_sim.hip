@@ -177,8 +177,8 @@ struct SimDev {
     uint32_t dcap;
     P1* p1;              // [NL] pass-1 results k_pass1 left for the refresh kernel
     uint32_t p1_pre;     // 1: the lane kernels read p1 instead of running lane_pass1
-    uint32_t ck_ablate;  // timing ablations of k_ck_lanes (RP_SIM_CK_ABLATE; results are wrong): 1 no
-                         // fixups, 2 also no word production
+    uint32_t ck_ablate;  // timing ablation of k_ck_lanes (RP_SIM_CK_ABLATE=1; results are wrong): no
+                         // piece fixups
     // inbound messages of the current stage
     const Msg* in_msg;      // headers, gathered in arrival order
     const uint8_t* in_buf;  // the inbox: per source shard [headers | records]
@@ -591,6 +591,12 @@ __device__ __forceinline__ uint32_t lshl_add_v(uint32_t a, uint32_t sh, uint32_t
     uint32_t r;
     asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(sh), "v"(b));
     return r;
+}
+// a * c + b with a 32-bit v_mul_lo_u32 (hipcc fuses `a * c + b` into a 64-bit v_mad_u64_u32)
+__device__ __forceinline__ uint32_t mul_lo_add(uint32_t a, uint32_t c, uint32_t b) {
+    uint32_t r;
+    asm("v_mul_lo_u32 %0, %1, %2" : "=v"(r) : "v"(a), "s"(c));
+    return r + b;
 }
 __device__ __forceinline__ uint32_t swap_pair(uint32_t v) {  // lanes 2i <-> 2i+1 (quad_perm 1,0,3,2)
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);
@@ -1276,7 +1282,7 @@ __global__ __launch_bounds__(256) void k_ck_lanes(SimDev S, const uint32_t* __re
             for (int i = 0; i < 5; i++) w[j][i] = __builtin_amdgcn_alignbyte(x[5 * j + i + 1], x[5 * j + i], sh);
             a5[j] = premix(w[j][3]);
             a6[j] = premix(w[j][2]);
-            a7[j] = premix(w[j][1] + w[j][4] * fh::kC1);
+            a7[j] = premix(mul_lo_add(w[j][4], fh::kC1, w[j][1]));
         }
     };
     // redo the chunks of the group at q that touch the piece under the cursor (and later ones)
@@ -1344,31 +1350,42 @@ __global__ __launch_bounds__(256) void k_ck_lanes(SimDev S, const uint32_t* __re
         if (ng1) {
             while (__builtin_expect(q1 >= C.pend, 0) && C.cur.w < N) C.advance(S, V);
         }
-        // one basic block: the next group's words + pre-mixes beside this group's chain
-        if (S.ck_ablate < 2) {
+        // one chunk of the chain (5 r as one v_lshl_add_u32)
+        auto chunk = [&](int j) {
+            h += wd[j][0];
+            g += wd[j][1];
+            f += wd[j][2];
+            const uint32_t rh = fh::rotr(h ^ p5[j], 19), rg = fh::rotr(g ^ p6[j], 19), rf = fh::rotr(f ^ p7[j], 19);
+            h = lshl_add<2>(rh, rh) + 0xe6546b64u + wd[j][4];
+            g = lshl_add<2>(rg, rg) + 0xe6546b64u + wd[j][0];
+            f = lshl_add<2>(rf, rf) + 0xe6546b64u + wd[j][3];
+            f += g;
+            g += f;
+        };
+        // one basic block: the next group's words + pre-mixes beside this group's chain. The arms
+        // differ only in masking; each holds its own copy of produce (a block boundary between
+        // the two streams would serialise them; without the compiler barriers hipcc hoists the
+        // common copy out of the arms). Every live lane takes a whole group except in
+        // its last one.
+        // (the pins keep the pre-mixes computed in the arm: hipcc would sink the arms' common
+        // multiplies into the join block)
+        auto pin = [&]() {
+#pragma unroll
+            for (int j = 0; j < 4; j++) asm volatile("" : "+v"(n5[j]), "+v"(n6[j]), "+v"(n7[j]));
+        };
+        if (__ballot(act && ng < 4) == 0) {
+            asm volatile("" ::: "memory");  // keeps the arm's ring reads (and all that uses them) in the arm
             produce(q1, nw, n5, n6, n7);
+#pragma unroll
+            for (int j = 0; j < 4; j++) chunk(j);
+            pin();
         } else {
+            asm volatile("" ::: "memory");
+            produce(q1, nw, n5, n6, n7);
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-#pragma unroll
-                for (int i = 0; i < 5; i++) nw[j][i] = wd[j][i] + 1u;
-                n5[j] = p5[j] ^ 3u;
-                n6[j] = p6[j] ^ 5u;
-                n7[j] = p7[j] ^ 7u;
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            if ((uint32_t)j < ng) {
-                h += wd[j][0];
-                g += wd[j][1];
-                f += wd[j][2];
-                h = fh::rotr(h ^ p5[j], 19) * 5 + 0xe6546b64u + wd[j][4];
-                g = fh::rotr(g ^ p6[j], 19) * 5 + 0xe6546b64u + wd[j][0];
-                f = fh::rotr(f ^ p7[j], 19) * 5 + 0xe6546b64u + wd[j][3];
-                f += g;
-                g += f;
-            }
+            for (int j = 0; j < 4; j++)
+                if ((uint32_t)j < ng) chunk(j);
+            pin();
         }
         if (__builtin_expect(ng1 && q1 + 20 * ng1 > C.pos, 0) && S.ck_ablate == 0) fixup(q1, ng1, nw, n5, n6, n7);
 #pragma unroll
