@@ -769,6 +769,8 @@ constexpr uint32_t kMckStage = 24576;  // LDS bytes a tile's pieces are assemble
 
 // One member's piece: row, length and (for names of at most 28 bytes plus alignment) the
 // name's aligned dwords, loaded together before the tile's scan so their latency overlaps it.
+// Names come by rank from the table's address-ordered copy (NameTable::sort_bytes: soff / sbytes),
+// so a tile's names are one contiguous run; only the row is a random access.
 struct MckItem {
     uint32_t id, len, nlen, sh;
     MRow row;
@@ -776,12 +778,12 @@ struct MckItem {
     uint32_t w[8];
 };
 __device__ __forceinline__ void mck_load(uint32_t i, const uint32_t* __restrict__ order, uint32_t n,
-                                         const MRow* __restrict__ rows, const uint64_t* __restrict__ noff,
+                                         const MRow* __restrict__ rows, const uint32_t* __restrict__ soff,
                                          MckItem& t) {
     t.id = i < n ? order[i] : 0u;
     t.row = row_load(rows + t.id);
-    t.noff = noff[t.id];
-    t.nlen = (uint32_t)(noff[t.id + 1] - t.noff);
+    t.noff = i < n ? soff[i] : 0u;
+    t.nlen = i < n ? soff[i + 1] - (uint32_t)t.noff : 0u;
     t.len = (i < n && t.row.exists) ? t.nlen + status_len(t.row.status) + dec_len(t.row.inc) + 1u : 0u;
 }
 __device__ __forceinline__ void mck_load_name(const uint8_t* __restrict__ names, MckItem& t) {
@@ -824,7 +826,7 @@ __device__ __forceinline__ void mck_emit(uint8_t* o, const uint8_t* __restrict__
 // counter when done, so it is 0 again after the launch. Workgroup 0 then sums the applied
 // counts into *A.n_applied and *out.
 __global__ __launch_bounds__(256) void k_ovf_len(const uint32_t* __restrict__ order, uint32_t n,
-                                                 const uint64_t* __restrict__ noff, uint32_t* __restrict__ tile_tot,
+                                                 const uint32_t* __restrict__ soff, uint32_t* __restrict__ tile_tot,
                                                  const uint32_t* __restrict__ ids, uint32_t k, uint32_t* ovf, FoldArgs A,
                                                  uint32_t* part, uint32_t nparts, uint32_t* __restrict__ out,
                                                  uint32_t* tick, uint32_t* err) {
@@ -859,7 +861,7 @@ __global__ __launch_bounds__(256) void k_ovf_len(const uint32_t* __restrict__ or
         __syncthreads();
     }
     MckItem t;
-    mck_load(blockIdx.x * 256u + tid, order, n, A.rows, noff, t);
+    mck_load(blockIdx.x * 256u + tid, order, n, A.rows, soff, t);
     const uint32_t total = block_sum256(t.len);
     if (tid == 0) tile_tot[blockIdx.x] = total;
     if (blockIdx.x == 0) {
@@ -880,17 +882,17 @@ __global__ __launch_bounds__(256) void k_ovf_len(const uint32_t* __restrict__ or
 
 // The sorted path and Membership.set: the tile lengths alone (ungated; the gate is already set).
 __global__ __launch_bounds__(256) void k_mck_len(const uint32_t* __restrict__ order, uint32_t n,
-                                                 const MRow* __restrict__ rows, const uint64_t* __restrict__ noff,
+                                                 const MRow* __restrict__ rows, const uint32_t* __restrict__ soff,
                                                  uint32_t* __restrict__ tile_tot) {
     MckItem t;
-    mck_load(blockIdx.x * 256u + threadIdx.x, order, n, rows, noff, t);
+    mck_load(blockIdx.x * 256u + threadIdx.x, order, n, rows, soff, t);
     const uint32_t total = block_sum256(t.len);
     if (threadIdx.x == 0) tile_tot[blockIdx.x] = total;
 }
 
 __global__ __launch_bounds__(256) void k_mck_write(const uint32_t* __restrict__ order, uint32_t n,
                                                    const MRow* __restrict__ rows, const uint8_t* __restrict__ names,
-                                                   const uint64_t* __restrict__ noff, const uint32_t* __restrict__ gate,
+                                                   const uint32_t* __restrict__ soff, const uint32_t* __restrict__ gate,
                                                    const uint32_t* __restrict__ tile_tot, uint8_t* __restrict__ buf,
                                                    uint32_t* __restrict__ meta) {
     __shared__ uint32_t s_wsum[4], s_pre[4];
@@ -907,7 +909,7 @@ __global__ __launch_bounds__(256) void k_mck_write(const uint32_t* __restrict__ 
     uint32_t pre = 0;  // this thread's share of the earlier tiles' totals
     for (uint32_t q = tid; q < tile; q += 256) pre += tile_tot[q];
     MckItem t;
-    mck_load(tile * 256u + tid, order, n, rows, noff, t);
+    mck_load(tile * 256u + tid, order, n, rows, soff, t);
     mck_load_name(names, t);
     // inclusive scan of the lengths within each wave; wave totals and prefix shares
     uint32_t x = t.len;
@@ -1299,15 +1301,15 @@ struct Members {
                     ws.err.reserve(1);
                     RP_HIP(hipMemsetAsync(ws.err.p, 0, sizeof(uint32_t), s));
                 }
-                hipLaunchKernelGGL(k_ovf_len, dim3(ntl), dim3(256), 0, s, nt.sorted.p, n, nt.d_noff.p, ck_tiles.p,
+                hipLaunchKernelGGL(k_ovf_len, dim3(ntl), dim3(256), 0, s, nt.sorted.p, n, nt.soff.p, ck_tiles.p,
                                    ov->ids, ov->k, ov->ovf, ov->A, ov->part, ov->nparts, ov->out,
                                    napplied.p + 2 + 2, ws.err.p);
             } else {
-                hipLaunchKernelGGL(k_mck_len, dim3(ntl), dim3(256), 0, s, nt.sorted.p, n, rows.p, nt.d_noff.p,
+                hipLaunchKernelGGL(k_mck_len, dim3(ntl), dim3(256), 0, s, nt.sorted.p, n, rows.p, nt.soff.p,
                                    ck_tiles.p);
             }
-            hipLaunchKernelGGL(k_mck_write, dim3(ntl), dim3(256), 0, s, nt.sorted.p, n, rows.p, nt.d_bytes.p,
-                               nt.d_noff.p, gate, ck_tiles.p, buf, meta);
+            hipLaunchKernelGGL(k_mck_write, dim3(ntl), dim3(256), 0, s, nt.sorted.p, n, rows.p, nt.sbytes.p,
+                               nt.soff.p, gate, ck_tiles.p, buf, meta);
         }
         RP_HIP(hipGetLastError());
         if (is_batch && hist_cap) pend_mask.w[npending >> 6] |= 1ull << (npending & 63);
@@ -1434,7 +1436,7 @@ int rp_members_intern(rp_members* h, const char* bytes, const uint32_t* off, uin
             if (ids_out) ids_out[i] = id;
         }
         m.grow(m.nt.size());
-        m.nt.sort(m.st, m.ws);  // address order for checksums (also uploads the names)
+        m.nt.sort_bytes(m.st, m.ws);  // address order for checksums (also uploads the names)
         RP_HIP(hipStreamSynchronize(m.st));
     });
 }

@@ -28,6 +28,11 @@ struct NameTable {
     DevBuf<uint32_t> sorted;
     uint32_t sorted_n = 0;
     DevBuf<uint32_t> tmp;
+    // the names concatenated in byte order (sbytes, padded by 32 bytes) and their offsets by
+    // rank (soff[n] = the total): the membership checksum string reads its names in order
+    DevBuf<uint8_t> sbytes;
+    DevBuf<uint32_t> soff;
+    uint32_t sbytes_n = 0;
     // open-addressing index over the device names: 2^hbits slots holding ids (0xFFFFFFFF empty),
     // keyed by farmhash32 of the name, linear probing (the wire decoder's interning)
     DevBuf<uint32_t> htab;
@@ -40,6 +45,8 @@ struct NameTable {
     void sync(hipStream_t st);
     // (re)sort ids by name on the device if names were added
     void sort(hipStream_t st, Scratch& ws);
+    // sort(), then (re)build sbytes / soff if names were added
+    void sort_bytes(hipStream_t st, Scratch& ws);
     // (re)build htab if names were added
     void hash_index(hipStream_t st);
 };

@@ -36,7 +36,46 @@ __global__ void k_name_hash_insert(const uint8_t* __restrict__ names, const uint
     }
 }
 
+// soff[i] = the length of the i-th name in byte order (soff[n] = 0, for the exclusive scan)
+__global__ void k_name_sorted_len(const uint64_t* __restrict__ noff, const uint32_t* __restrict__ sorted, uint32_t n,
+                                  uint32_t* __restrict__ len) {
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += gstride)
+        len[i] = i < n ? (uint32_t)(noff[sorted[i] + 1] - noff[sorted[i]]) : 0u;
+}
+
+__global__ void k_name_sorted_copy(const uint8_t* __restrict__ names, const uint64_t* __restrict__ noff,
+                                   const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ soff, uint32_t n,
+                                   uint8_t* __restrict__ sbytes) {
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gstride) {
+        const uint8_t* src = names + noff[sorted[i]];
+        uint8_t* dst = sbytes + soff[i];
+        const uint32_t L = soff[i + 1] - soff[i];
+        for (uint32_t q = 0; q < L; q++) dst[q] = src[q];
+    }
+}
+
 }  // namespace
+
+void NameTable::sort_bytes(hipStream_t st, Scratch& ws) {
+    sort(st, ws);
+    const uint32_t n = (uint32_t)names.size();
+    if (sbytes_n == n && soff.p) return;
+    if (h_bytes.size() > 0xFFFFFF00ull) throw Error(RP_EINVAL, "names past 4 GB of bytes (32-bit sorted offsets)");
+    soff.reserve((uint64_t)n + 1);
+    sbytes.reserve(h_bytes.size() + 32);
+    RP_HIP(hipMemsetAsync(sbytes.p, 0, h_bytes.size() + 32, st));
+    hipLaunchKernelGGL(k_name_sorted_len, dim3(grid_for((uint64_t)n + 1, 256)), dim3(256), 0, st, d_noff.p, sorted.p, n,
+                       soff.p);
+    RP_HIP(hipGetLastError());
+    scan_exclusive_u32(soff.p, soff.p, (uint64_t)n + 1, st, ws);
+    if (n)
+        hipLaunchKernelGGL(k_name_sorted_copy, dim3(grid_for(n, 256)), dim3(256), 0, st, d_bytes.p, d_noff.p,
+                           sorted.p, soff.p, n, sbytes.p);
+    RP_HIP(hipGetLastError());
+    sbytes_n = n;
+}
 
 void NameTable::hash_index(hipStream_t st) {
     const uint32_t n = (uint32_t)names.size();
