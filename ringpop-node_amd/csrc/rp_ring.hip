@@ -633,6 +633,25 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_compact(const uint8_t* _
     }
 }
 
+// One deferred key redone exactly: hash, exact position, the reference walk; its row and count
+// overwrite what the compact kernel stored.
+template <class View>
+__device__ __forceinline__ void lookupn_redo(const uint8_t* __restrict__ keys, const View& rv, int np, uint32_t W,
+                                             uint32_t* __restrict__ out, uint8_t* __restrict__ counts, uint64_t k) {
+    uint32_t w[9];
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(keys + k * 36);
+#pragma unroll
+    for (int j = 0; j < 9; j++) w[j] = src[j];
+    const uint32_t h = fh::hash32_words<36>(w);
+    uint32_t res[4];
+    const int cnt = ring_walk<4>(rv, rv.find(h), np, res);
+    uint32_t* row = out + k * W;
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+        if ((uint32_t)q < W) row[q] = res[q];
+    if (counts) counts[k] = (uint8_t)cnt;
+}
+
 // The C2 hot kernel, lean form (round 2): the same layout, loads and results as
 // k_lookupn_compact, with fewer vector instructions per key (the SQ counters put that kernel at
 // ~2.9x the VALU issue of the hash-only ablation).
@@ -650,12 +669,15 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_compact(const uint8_t* _
 // so the key stage takes 1/HS of the LDS and more workgroups fit a CU (A/B).
 // (Forcing 5 waves per SIMD with __launch_bounds__ spills 8 VGPRs and ran 1.05 against 0.91 ms,
 // profiles/r03/ab_lookup_occ.json: the 119 VGPRs and 4 waves per SIMD stay.)
-template <int KPL, int NEED, int HS = 1>
+// FUSE: the workgroup finishes its own tiles' deferred keys after its last tile (one thread per
+// list slot, 8 tiles at a time) instead of k_lookupn_fix_tiles (A/B: RP_LOOKUP_FUSEFIX).
+template <int KPL, int NEED, int HS = 1, bool FUSE = false>
 __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __restrict__ keys, uint64_t ntiles,
                                                              CompactView cv, uint32_t* __restrict__ out,
                                                              uint8_t* __restrict__ counts,
                                                              uint32_t* __restrict__ slow_list,
-                                                             uint32_t* __restrict__ slow_cnt) {
+                                                             uint32_t* __restrict__ slow_cnt, CompactFixView fv,
+                                                             int np) {
     constexpr int LEN = 36, W4 = LEN / 4;
     constexpr int TK = kLkThreads * KPL;
     constexpr int V4 = TK * W4 / 4;
@@ -830,6 +852,25 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
         for (int k = tid; k < TK * NEED / 4; k += kLkThreads) __builtin_nontemporal_store(s4[k], d4 + k);
         __syncthreads();
     }
+    if constexpr (FUSE) {
+        // this workgroup's tiles t = blockIdx.x + i * gridDim.x; their rows are stored (the barrier
+        // above orders the overwrites after them)
+        constexpr uint32_t TPP = kLkThreads / kSlowPerTile;
+        const uint64_t nt = ntiles > blockIdx.x ? (ntiles - blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
+        for (uint64_t i0 = 0; i0 < nt; i0 += TPP) {
+            const uint64_t i = i0 + (uint32_t)tid / kSlowPerTile;
+            const uint32_t q = (uint32_t)tid % kSlowPerTile;
+            if (i < nt) {
+                const uint64_t t = blockIdx.x + i * gridDim.x;
+                const uint32_t c = slow_cnt[t];
+                if (c <= kSlowPerTile) {
+                    if (q < c) lookupn_redo(keys, fv, np, (uint32_t)NEED, out, counts, t * TK + slow_list[t * kSlowPerTile + q]);
+                } else {
+                    for (uint32_t k = q; k < (uint32_t)TK; k += kSlowPerTile) lookupn_redo(keys, fv, np, (uint32_t)NEED, out, counts, t * TK + k);
+                }
+            }
+        }
+    }
 }
 
 // Exact completion of the keys the compact kernels deferred: one thread per list slot
@@ -848,20 +889,7 @@ __global__ __launch_bounds__(256) void k_lookupn_fix_tiles(const uint8_t* __rest
     if (t >= ntiles) return;
     const uint32_t c = slow_cnt[t];
     if (c == 0) return;
-    auto redo = [&](uint64_t k) {
-        uint32_t w[9];
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(keys + k * 36);
-#pragma unroll
-        for (int j = 0; j < 9; j++) w[j] = src[j];
-        const uint32_t h = fh::hash32_words<36>(w);
-        uint32_t res[4];
-        const int cnt = ring_walk<4>(rv, rv.find(h), np, res);
-        uint32_t* row = out + k * W;
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-            if ((uint32_t)q < W) row[q] = res[q];
-        if (counts) counts[k] = (uint8_t)cnt;
-    };
+    auto redo = [&](uint64_t k) { lookupn_redo(keys, rv, np, W, out, counts, k); };
     if (c <= kSlowPerTile) {
         if (q < c) redo(t * TK + slow_list[t * kSlowPerTile + q]);
     } else {
@@ -1483,17 +1511,23 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
         // 5120-16384: 0.908-0.914; profiles/r02/ab_lookup_grid.json). RP_LOOKUP_GRID overrides (A/B).
         const unsigned g = grid_for(ntiles, 1, (unsigned)env_pos("RP_LOOKUP_GRID", lean ? 4096u : 2048u));
         const int half = getenv("RP_LOOKUP_HALF") ? atoi(getenv("RP_LOOKUP_HALF")) : (kpl == 8 ? 4 : 0);
+        const CompactFixView fv{r.tok.p, r.own.p, r.cidx.p, r.view(), r.M, r.ccb};
+        // deferred keys finished by the lean kernel's own workgroups (A/B): only <8, 3, 4>
+        const bool fuse = getenv_flag("RP_LOOKUP_FUSEFIX") && lean && half == 4 && kpl == 8 && need == 3 && cv.ablate != 3;
 #define RP_COMPACT(KPL, NEED)                                                                                  \
     do {                                                                                                        \
-        if (lean && half == 4 && KPL % 4 == 0)                                                                  \
+        if (lean && half == 4 && KPL % 4 == 0 && fuse)                                                          \
+            hipLaunchKernelGGL((k_lookupn_lean<KPL, NEED, (KPL % 4 == 0 ? 4 : 1), true>), dim3(g), dim3(kLkThreads), \
+                               0, st, keys, ntiles, cv, out, counts, r.slow.p, r.nslow.p, fv, np);               \
+        else if (lean && half == 4 && KPL % 4 == 0)                                                             \
             hipLaunchKernelGGL((k_lookupn_lean<KPL, NEED, (KPL % 4 == 0 ? 4 : 1)>), dim3(g), dim3(kLkThreads), 0, \
-                               st, keys, ntiles, cv, out, counts, r.slow.p, r.nslow.p);                          \
+                               st, keys, ntiles, cv, out, counts, r.slow.p, r.nslow.p, fv, np);                  \
         else if (lean && half == 2 && KPL % 2 == 0)                                                             \
             hipLaunchKernelGGL((k_lookupn_lean<KPL, NEED, (KPL % 2 == 0 ? 2 : 1)>), dim3(g), dim3(kLkThreads), 0, \
-                               st, keys, ntiles, cv, out, counts, r.slow.p, r.nslow.p);                          \
+                               st, keys, ntiles, cv, out, counts, r.slow.p, r.nslow.p, fv, np);                  \
         else if (lean)                                                                                          \
             hipLaunchKernelGGL((k_lookupn_lean<KPL, NEED>), dim3(g), dim3(kLkThreads), 0, st, keys, ntiles, cv,  \
-                               out, counts, r.slow.p, r.nslow.p);                                               \
+                               out, counts, r.slow.p, r.nslow.p, fv, np);                                       \
         else                                                                                                    \
             hipLaunchKernelGGL((k_lookupn_compact<KPL, NEED>), dim3(g), dim3(kLkThreads), 0, st, keys, ntiles,   \
                                cv, out, counts, r.slow.p, r.nslow.p);                                           \
@@ -1521,8 +1555,7 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
 #undef RP_COMPACT_N
 #undef RP_COMPACT
         const uint64_t fthreads = ntiles * kSlowPerTile;
-        const CompactFixView fv{r.tok.p, r.own.p, r.cidx.p, r.view(), r.M, r.ccb};
-        if (cv.ablate != 3)
+        if (cv.ablate != 3 && !fuse)
             hipLaunchKernelGGL((k_lookupn_fix_tiles<CompactFixView>), dim3((unsigned)((fthreads + 255) / 256)),
                                dim3(256), 0, st, keys, fv, np, W, out, counts, r.slow.p, r.nslow.p, ntiles,
                                (uint32_t)TK);
