@@ -633,6 +633,66 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_compact(const uint8_t* _
     }
 }
 
+// The exact position and walk of a deferred key on the compact layout with the dependent trips
+// cut: the bucket's tokens are compared four at a time (one vector load for a bucket of <= 4) and
+// the next 8 owners come in two vector loads; the result equals ring_walk's (the general walk
+// takes over when 8 entries do not hold np distinct owners or the ring end is near).
+__device__ __forceinline__ int compact_fix_walk(const CompactFixView& fv, uint32_t h, int np, uint32_t (&res)[4]) {
+    if (np < 1 || np > 4) return ring_walk<4>(fv, fv.find(h), np, res);
+    const uint32_t bsh = 32u - fv.cb;
+    const uint32_t g = h >> (bsh + 3u), s4 = ((h >> bsh) & 7u) * 4u;
+    const u32x2 rec = *reinterpret_cast<const u32x2*>(fv.idx + 2ull * g);
+    const uint32_t bc = (rec.y >> s4) & 15u;
+    uint32_t i;
+    if (bc == 15u) {
+        i = fv.wide.find(h);
+    } else {
+        const uint32_t below = rec.y & ((1u << s4) - 1u);
+        const uint32_t x = (below & 0x0F0F0F0Fu) + ((below >> 4) & 0x0F0F0F0Fu);
+        i = rec.x + ((x * 0x01010101u) >> 24);
+        uint32_t lt = 0;
+        for (uint32_t j = 0; j < bc; j += 4) {
+            if (i + j + 4 <= fv.M) {
+                const u32x4_a1 v = *reinterpret_cast<const u32x4_a1*>(fv.tok + i + j);
+                lt += (j < bc && v.x < h) + (j + 1 < bc && v.y < h) + (j + 2 < bc && v.z < h) + (j + 3 < bc && v.w < h);
+            } else {
+                for (uint32_t q = j; q < bc && q < j + 4; q++) lt += fv.tok[i + q] < h;
+            }
+        }
+        i += lt;  // tokens are sorted: the count below h is the position
+    }
+    const uint32_t p = (i == fv.M) ? 0u : i;
+    if (p + 8 <= fv.M) {
+        const u32x4_a1 a = *reinterpret_cast<const u32x4_a1*>(fv.own + p);
+        const u32x4_a1 b = *reinterpret_cast<const u32x4_a1*>(fv.own + p + 4);
+        const uint32_t o[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int q = 0; q < 4; q++) res[q] = NIL;
+        int cnt = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            bool dup = false;
+#pragma unroll
+            for (int q = 0; q < 4; q++) dup |= (q < cnt) & (res[q] == o[j]);
+            if (!dup && cnt < np) {
+#pragma unroll
+                for (int q = 0; q < 4; q++) res[q] = (q == cnt) ? o[j] : res[q];
+                cnt++;
+            }
+        }
+        if (cnt >= np) return cnt;
+    }
+    return ring_walk<4>(fv, i, np, res);
+}
+
+template <class View>
+__device__ __forceinline__ int fix_walk(const View& rv, uint32_t h, int np, uint32_t (&res)[4]) {
+    if constexpr (std::is_same<View, CompactFixView>::value)
+        return compact_fix_walk(rv, h, np, res);
+    else
+        return ring_walk<4>(rv, rv.find(h), np, res);
+}
+
 // One deferred key redone exactly: hash, exact position, the reference walk; its row and count
 // overwrite what the compact kernel stored.
 template <class View>
@@ -644,7 +704,7 @@ __device__ __forceinline__ void lookupn_redo(const uint8_t* __restrict__ keys, c
     for (int j = 0; j < 9; j++) w[j] = src[j];
     const uint32_t h = fh::hash32_words<36>(w);
     uint32_t res[4];
-    const int cnt = ring_walk<4>(rv, rv.find(h), np, res);
+    const int cnt = fix_walk(rv, h, np, res);
     uint32_t* row = out + k * W;
 #pragma unroll
     for (int q = 0; q < 4; q++)
@@ -887,11 +947,13 @@ __global__ __launch_bounds__(256) void k_lookupn_fix_tiles(const uint8_t* __rest
     const uint64_t t = gid / kSlowPerTile;
     const uint32_t q = (uint32_t)(gid % kSlowPerTile);
     if (t >= ntiles) return;
+    // the count and the slot are independent loads (one trip); the slot is used only when q < count
     const uint32_t c = slow_cnt[t];
+    const uint32_t kq = slow_list[t * kSlowPerTile + q];
     if (c == 0) return;
     auto redo = [&](uint64_t k) { lookupn_redo(keys, rv, np, W, out, counts, k); };
     if (c <= kSlowPerTile) {
-        if (q < c) redo(t * TK + slow_list[t * kSlowPerTile + q]);
+        if (q < c) lookupn_redo(keys, rv, np, W, out, counts, t * TK + kq);
     } else {
         for (uint32_t k = q; k < TK; k += kSlowPerTile) redo(t * TK + k);
     }
