@@ -268,6 +268,10 @@ def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=512, warmup=3, 
     rpa.check(rpa.lib().rp_members_defer_checksum(m._h, 1))
     nf = 20
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nf)]
+    # a spin kernel ahead of the batches, so the host has enqueued them all before the GPU reaches
+    # them: the events then time the device, not the host's launch rate (7 launches per batch take
+    # the host longer than the GPU's 0.02 ms; without it the figure flips between 0.021 and 0.034)
+    torch.cuda._sleep(4_000_000)
     for b in range(nf):
         evs[b][0].record(stream)
         one(warmup + batches + b)
@@ -306,6 +310,7 @@ def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=512, warmup=3, 
     one(0, mb, big, nb)
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(6)]
+    torch.cuda._sleep(4_000_000)  # (as for the C3 fold above)
     for b in range(6):
         evs[b][0].record(stream)
         one(b + 1, mb, big, nb)
