@@ -102,6 +102,8 @@ struct CompactView {
     uint32_t ablate;  // diagnostics only (RP_LOOKUP_ABLATE): 1 = no second windows, 2 = aligned windows
     uint32_t ent_bytes;  // allocated bytes of ent / idx (buffer-descriptor ranges of the lean kernel)
     uint32_t idx_bytes;
+    uint32_t wpred;  // lean kernel: window 1 starts where the key's hash falls in its bucket (A/B:
+                     // RP_LOOKUP_WPRED=0 starts it at the bucket start)
 };
 
 // Exact view for the compact kernel's deferred keys: the bucket start comes from the compact
@@ -772,23 +774,33 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
         e[3] = v.z >> 8;
         e[4] = v.w & 0xFFFFFFu;
     };
+    // Window 1's first entry within the bucket (round 3): the key's position in a bucket of bc
+    // tokens is about bc times its place in the bucket's hash range (r), so the window starts at
+    // max(0, floor(r bc) - 1). A window at w > 0 resolves positions w+1..w+2 (entry w below the key
+    // is the guard), one at 0 positions 0..2: 3.6 % of keys need a second window instead of 9.9 %
+    // (Poisson buckets of 1.9 tokens). Long buckets (> 10) keep w = 0.
+    auto wstart = [&](uint32_t hk, uint32_t bck) -> uint32_t {
+        const uint32_t fl = (((hk << cv.cb) >> 24) * bck) >> 8;
+        return (cv.wpred && bck <= 10u && fl > 1u) ? fl - 1u : 0u;
+    };
     // a listed key's second window (held by one lane): finish it, write its row into `row`
     auto finish2 = [&](const u32x4 win, uint32_t K, uint32_t w2, uint32_t* row, uint8_t* cnt, uint32_t* nsl,
                        uint32_t* slist) {
-        const uint32_t kk = w2 & 0xFFFu, bck = (w2 >> 12) & 15u;
+        const uint32_t kk = w2 & 0xFFFu, bck = (w2 >> 12) & 15u, b0 = (w2 >> 17) & 15u;
         uint32_t e2[5];
         ent5v(win, e2);
         uint32_t off = 0;
         bool slow = false;
-        if ((w2 >> 16) & 1u) {  // window 2 holds bucket entries 5..9
+        if ((w2 >> 16) & 1u) {  // window 2 holds bucket entries b0..b0+4: search it
             bool tie = false;
 #pragma unroll
             for (int j = 0; j < 5; j++) {
-                const bool inb = (uint32_t)j + 5u < bck;
+                const bool inb = (uint32_t)j + b0 < bck;
                 off += (inb && e2[j] < K);
                 tie |= (inb && e2[j] - K < obit);
             }
-            slow = (tie && !cv.exact) | (off == 5u && bck > 10u);
+            // past this window too; or (guard) the key may lie before entry b0
+            slow = (tie && !cv.exact) | (off == 5u && bck > b0 + 5u) | (((w2 >> 21) & 1u) && off == 0u);
         }
         uint32_t res[4] = {NIL, NIL, NIL, NIL};
         const uint32_t rc = dedupe5(e2, off, omask, NEED, res);
@@ -845,7 +857,7 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
             lo[k] = rec[k].x + __builtin_amdgcn_sad_u8(below & 0x0F0F0F0Fu, 0u,
                                                        __builtin_amdgcn_sad_u8((below >> 4) & 0x0F0F0F0Fu, 0u, 0u));
             bc[k] = (rec[k].y >> s4) & 15u;
-            win[k] = load16(lo[k]);
+            win[k] = load16(lo[k] + wstart(h[k], bc[k]));
         }
         uint32_t nag = 0;  // wave-uniform length of this wave's list
 #pragma unroll
@@ -853,11 +865,12 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
             uint32_t e[5];
             ent5v(win[k], e);
             const uint32_t K = ((h[k] & rmask) >> cv.fsh) << cv.ob;
-            uint32_t lt = 0;
+            const uint32_t w = wstart(h[k], bc[k]);
+            uint32_t lt = 0;  // in-bucket window entries below the key: the position is lo + w + lt
             bool tie = false;
 #pragma unroll
             for (int j = 0; j < 5; j++) {
-                const bool inb = (uint32_t)j < bc[k];
+                const bool inb = (uint32_t)j + w < bc[k];
                 lt += (inb && e[j] < K);
                 tie |= (inb && e[j] - K < obit);
             }
@@ -875,17 +888,22 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
 #pragma unroll
                 for (int b = a + 1; b < NEED; b++) dup |= r[a] == r[b];
             const uint32_t kk = tid + k * kLkThreads;
-            bool slow = (tie && !cv.exact) | (lo[k] + 10u > cv.M);
-            const bool again = !slow && (lt > SPAN || dup);
+            bool slow = (tie && !cv.exact) | (lo[k] + 20u > cv.M);
+            const bool under = w > 0u && lt == 0u;  // the key lies before window 1's first entry
+            const bool again = !slow && (lt > SPAN || dup || under);
             const uint64_t m = __ballot(again);
             const uint32_t pos = nag + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             nag += (uint32_t)__popcll(m);
             if (again) {
                 if (pos < AG) {
-                    const bool search = lt == 5u && bc[k] > 5u;
-                    ag[wv][0][pos] = search ? lo[k] + 5u : lo[k] + lt;
+                    // under: search from w - 2 (the position is at most w), guarded when > 0; past
+                    // window 1 inside the bucket: search on from w + 5; else the position is known
+                    const uint32_t b0 = under ? (w > 2u ? w - 2u : 0u) : w + 5u;
+                    const bool search = under || (lt == 5u && bc[k] > w + 5u);
+                    ag[wv][0][pos] = lo[k] + (search ? b0 : w + lt);
                     ag[wv][1][pos] = K;
-                    ag[wv][2][pos] = kk | (bc[k] << 12) | ((uint32_t)search << 16);
+                    ag[wv][2][pos] = kk | (bc[k] << 12) | ((uint32_t)search << 16) | ((search ? b0 : 0u) << 17) |
+                                     ((uint32_t)(under && b0 > 0u) << 21);
                 } else {
                     slow = true;
                 }
@@ -1319,7 +1337,8 @@ struct Ring {
     CompactView cview() const {
         const char* a = getenv("RP_LOOKUP_ABLATE");
         return CompactView{cent.p, cidx.p, M, ccb, cob, cfsh, cfsh == 0, a ? (uint32_t)atoi(a) : 0u,
-                           (uint32_t)(3ull * ((uint64_t)M + kEnt3Pad + 6) + 16), (uint32_t)(8ull << (ccb - 3))};
+                           (uint32_t)(3ull * ((uint64_t)M + kEnt3Pad + 6) + 16), (uint32_t)(8ull << (ccb - 3)),
+                           getenv("RP_LOOKUP_WPRED") && !strcmp(getenv("RP_LOOKUP_WPRED"), "0") ? 0u : 1u};
     }
 };
 
