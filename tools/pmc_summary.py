@@ -20,7 +20,7 @@ def main():
     for f in glob.glob(os.path.join(d, "*", "run_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
-            if "k_lookupn_lean<8, 3, 4>" in k or "k_lookupn_leanILi8ELi3ELi4E" in k:
+            if "k_lookupn_lean<8, 3, 4" in k or "k_lookupn_leanILi8ELi3ELi4E" in k:
                 kk = "compact"
             elif "k_lookupn_probe<36, 2, 1>" in k:
                 kk = "hashonly"
