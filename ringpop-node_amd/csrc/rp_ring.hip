@@ -730,7 +730,7 @@ __device__ __forceinline__ void lookupn_redo(const uint8_t* __restrict__ keys, c
 // HS: the tile's keys pass through LDS in HS slices (all loads issued first, held in registers),
 // so the key stage takes 1/HS of the LDS and more workgroups fit a CU (A/B).
 // (Forcing 5 waves per SIMD with __launch_bounds__ spills 8 VGPRs and ran 1.05 against 0.91 ms,
-// profiles/r03/ab_lookup_occ.json: the 119 VGPRs and 4 waves per SIMD stay.)
+// profiles/r03/ab_lookup_occ.json: the 119-121 VGPRs and 4 waves per SIMD stay.)
 // FUSE: the workgroup finishes its own tiles' deferred keys after its last tile (one thread per
 // list slot, 8 tiles at a time) instead of k_lookupn_fix_tiles (A/B: RP_LOOKUP_FUSEFIX).
 template <int KPL, int NEED, int HS = 1, bool FUSE = false>
