@@ -778,10 +778,12 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
     // tokens is about bc times its place in the bucket's hash range (r), so the window starts at
     // max(0, floor(r bc) - 1). A window at w > 0 resolves positions w+1..w+2 (entry w below the key
     // is the guard), one at 0 positions 0..2: 3.6 % of keys need a second window instead of 9.9 %
-    // (Poisson buckets of 1.9 tokens). Long buckets (> 10) keep w = 0.
+    // (Poisson buckets of 1.9 tokens; lookupN(2): 3.3 % -> 1.6 %). Long buckets (> 10) keep w = 0,
+    // and so does lookup (NEED 1), whose window at 0 already resolves positions 0..4 (0.9 % of keys
+    // past it against 1.5 % with the predicted start).
     auto wstart = [&](uint32_t hk, uint32_t bck) -> uint32_t {
         const uint32_t fl = (((hk << cv.cb) >> 24) * bck) >> 8;
-        return (cv.wpred && bck <= 10u && fl > 1u) ? fl - 1u : 0u;
+        return (NEED >= 2 && cv.wpred && bck <= 10u && fl > 1u) ? fl - 1u : 0u;
     };
     // a listed key's second window (held by one lane): finish it, write its row into `row`
     auto finish2 = [&](const u32x4 win, uint32_t K, uint32_t w2, uint32_t* row, uint8_t* cnt, uint32_t* nsl,
