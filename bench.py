@@ -373,6 +373,7 @@ def sim_bench(rpa, torch, dist, local, n=10_000, kill_pct=1, seed=11, max_rounds
     if world > 1:
         pr = np.asarray(reduce_max(list(pr)))  # round r's time = the slowest rank's
     dt, create_s = reduce_max([dt, create_s]) if world > 1 else (dt, create_s)
+    ex_s, ex_dev = reduce_max([sim.exchange_s, sim.xchg.device_ms()]) if world > 1 else (0.0, 0.0)
     st = sim.stats()
     cnt = sim.counters()
     msg_bytes = 40 * cnt["messages"] + 24 * cnt["records"] + BYTES_PER_UPDATE * cnt["applied"]
@@ -396,6 +397,11 @@ def sim_bench(rpa, torch, dist, local, n=10_000, kill_pct=1, seed=11, max_rounds
                                "checksum string (serial chains: throughput, not a roofline)" % cnt["base_len"]}}
     if world > 1:
         out["exchange_bytes_per_round_rank0"] = sim.exchange_bytes / max(rounds, 1)
+        # host time inside the message exchanges (counts all-to-all, inbox sizing, the byte
+        # all-to-all-v queued on RCCL, join sums), the slowest rank's, per round
+        out["exchange_ms_per_round"] = ex_s * 1e3 / max(rounds, 1)
+        # the byte all-to-all-v kernels' own time on the device (RCCL; HIP events around each)
+        out["exchange_device_ms_per_round"] = ex_dev / max(rounds, 1)
     sim.close()
     return out
 

@@ -190,6 +190,10 @@ int rp_members_checksum_shard(rp_members *m, uint32_t nshards, uint32_t shard, u
 /* The recorded per-batch checksums (this shard's batches, in batch order): hash[i], applied[i]
  * (0: the batch applied nothing; hash[i] is then 0), up to cap; *n = entries recorded. */
 int rp_members_checksum_history(rp_members *m, uint32_t *hash, uint8_t *applied, uint32_t cap, uint32_t *n);
+/* Drop the first `count` recorded entries (after reading them), so a long-running replica keeps
+ * recording: update refuses a batch with RP_ESTATE, before applying anything, when its entry
+ * would not fit history_cap. */
+int rp_members_checksum_history_drain(rp_members *m, uint32_t count);
 /* generateChecksumString() (writes up to cap bytes; *len = full length). */
 int rp_members_checksum_string(rp_members *m, char *buf, uint64_t cap, uint64_t *len);
 /* Member table by id (exists/status/incarnation), cap entries. */
@@ -382,6 +386,10 @@ int rp_sim_shard_info(rp_sim *s, uint32_t *v0, uint32_t *nl, uint32_t *nshards, 
 int rp_sim_stage(rp_sim *s, int stage);
 int rp_sim_outbox(rp_sim *s, uint64_t *nmsg, uint64_t *nrec, void **buf);
 int rp_sim_inbox(rp_sim *s, const uint64_t *nmsg, const uint64_t *nrec, void **buf);
+/* The handle's next stage waits (on the device, no host sync) for the work queued so far on
+ * `stream`: a caller that moved the inbox bytes with a collective on its own stream (RCCL on
+ * torch's stream) orders the import after it this way. */
+int rp_sim_wait_stream(rp_sim *s, void *stream);
 int rp_sim_exchange_local(rp_sim *const *shards, uint32_t nshards);
 int rp_sim_converged_local(rp_sim *s, uint32_t *out4);
 /* JOIN events on a sharded simulator (a joiner reads its responders' views, which other shards

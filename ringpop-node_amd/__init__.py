@@ -105,6 +105,7 @@ SIGNATURES = {
     "rp_sim_outbox": (_INT, [_P, _P, _P, _P]),
     "rp_sim_inbox": (_INT, [_P, _P, _P, _P]),
     "rp_sim_exchange_local": (_INT, [_P, _U32]),
+    "rp_sim_wait_stream": (_INT, [_P, _P]),
     "rp_sim_join_export": (_INT, [_P, _P, _P, _P]),
     "rp_sim_join_import": (_INT, [_P]),
     "rp_sim_join_exchange_local": (_INT, [_P, _U32]),
@@ -120,6 +121,7 @@ SIGNATURES = {
     "rp_members_defer_checksum": (_INT, [_P, _INT]),
     "rp_members_checksum_shard": (_INT, [_P, _U32, _U32, _U32]),
     "rp_members_checksum_history": (_INT, [_P, _P, _P, _U32, _P]),
+    "rp_members_checksum_history_drain": (_INT, [_P, _U32]),
     "rp_members_damp_configure": (_INT, [_P, _P]),
     "rp_members_damp_last": (_INT, [_P, _P, _P, _U32]),
     "rp_members_damp_decay": (_INT, [_P, ctypes.c_int64]),
@@ -153,6 +155,12 @@ def lib():
             fn.argtypes = args
         _lib = L
     return _lib
+
+
+def _is_array_index(k):
+    """A property name JS orders first in Object.keys: the canonical decimal of an integer in
+    [0, 2^32 - 2]."""
+    return k.isdigit() and k.isascii() and (k == "0" or k[0] != "0") and int(k) < 0xFFFFFFFF
 
 
 def check(rc):
@@ -239,31 +247,34 @@ class HashRing:
                         dtype=np.uint32)
 
     def addRemoveServers(self, serversToAdd=None, serversToRemove=None):
-        """lib/ring/index.js:60-94; returns ringChanged."""
-        add = list(serversToAdd or [])
-        rem = list(serversToRemove or [])
+        """lib/ring/index.js:60-94; returns ringChanged. The reference's per-name decisions (adds in
+        order, then removes, each against the servers map) are made first; only the names that
+        change go to the device, and the map is committed after the device call succeeded."""
+        over = {}
+        add, rem = [], []
+        for a in serversToAdd or []:
+            if not over.get(a, a in self._servers):
+                over[a] = True
+                add.append(a)
+        for r in serversToRemove or []:
+            if over.get(r, r in self._servers):
+                over[r] = False
+                rem.append(r)
+        if not add and not rem:
+            return False
         ab, ao = _pack(add)
         rb, ro = _pack(rem)
-        at = self._tokens(add)
-        rt = self._tokens(rem)
         changed = ctypes.c_int()
-        check(lib().rp_ring_add_remove(self._h, ab, ao.ctypes.data, len(add), _ptr(at),
-                                       rb, ro.ctypes.data, len(rem), _ptr(rt), ctypes.byref(changed)))
-        mine = False
+        check(lib().rp_ring_add_remove(self._h, ab, ao.ctypes.data, len(add), _ptr(self._tokens(add)),
+                                       rb, ro.ctypes.data, len(rem), _ptr(self._tokens(rem)), ctypes.byref(changed)))
+        if not changed.value:
+            raise RingpopAmdError("the device ring did not change for add %r remove %r" % (add, rem))
         for a in add:
-            if a not in self._servers:
-                self._servers[a] = True
-                mine = True
+            self._servers[a] = True
         for r in rem:
-            if r in self._servers:
-                del self._servers[r]
-                mine = True
-        if mine != bool(changed.value):
-            raise RingpopAmdError("device ring and servers map disagree (ringChanged %s vs %s)"
-                                  % (bool(changed.value), mine))
-        if changed.value:
-            self.emit("checksumComputed")
-        return bool(changed.value)
+            del self._servers[r]
+        self.emit("checksumComputed")
+        return True
 
     def addServer(self, name):
         """lib/ring/index.js:39-48"""
@@ -328,8 +339,11 @@ class HashRing:
         return dict(self._servers)
 
     def getStats(self):
-        """lib/ring/index.js:111-116"""
-        return {"checksum": self.checksum, "servers": list(self._servers)}
+        """lib/ring/index.js:111-116 (servers in Object.keys order: array-index names ascending,
+        then the others in insertion order)"""
+        idx = sorted((int(k), k) for k in self._servers if _is_array_index(k))
+        return {"checksum": self.checksum,
+                "servers": [k for _, k in idx] + [k for k in self._servers if not _is_array_index(k)]}
 
     def name(self, sid):
         sid = int(sid)
@@ -680,7 +694,9 @@ class DistMembership(Membership):
     collective: `checksums()` gathers the recorded per-batch values once (one all-gather).
 
     The batch stream must be the same on every rank (as the reference's is the same for one
-    process)."""
+    process). The device records at most `history_cap` of this rank's batches between two
+    `checksums()` calls (an update past that fails with nothing applied); `checksums()` moves the
+    record to the host and drains it, so a long-running replica keeps going."""
 
     def __init__(self, whoami=None, capacity=1024, device=0, history_cap=1 << 16, group=None):
         import torch.distributed as dist
@@ -689,14 +705,37 @@ class DistMembership(Membership):
         self._group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self._hist_h = np.zeros(0, dtype=np.uint32)  # this rank's drained record
+        self._hist_a = np.zeros(0, dtype=np.uint8)
         self.checksum_shard(self.world, self.rank, history_cap)
+
+    @property
+    def checksum(self):
+        """Membership.checksum after the last batch. Rank g hashes only batches b % G == g, so the
+        latest value lives on one rank: with G > 1 this is a collective (every rank must read it,
+        as with checksums()); with G = 1 it is the device's own value."""
+        if self.world == 1:
+            return Membership.checksum.fget(self)
+        cs = self.checksums()
+        return cs[-1] if cs else Membership.checksum.fget(self)
+
+    def compute_checksum(self):
+        """computeChecksum() of this rank's replica, which is the whole table: local, no collective."""
+        check(lib().rp_members_compute_checksum(self._h))
+        return Membership.checksum.fget(self)
 
     def checksums(self):
         """The checksum after every update batch since construction (None before the first
         applied one), in batch order: every rank's recorded values gathered and interleaved, a
-        batch that applied nothing carrying the previous value forward (index.js:306-309)."""
+        batch that applied nothing carrying the previous value forward (index.js:306-309).
+        A collective: every rank calls it."""
         import torch
         h, a = self.checksum_history()
+        if len(h):
+            check(lib().rp_members_checksum_history_drain(self._h, len(h)))
+            self._hist_h = np.concatenate([self._hist_h, h])
+            self._hist_a = np.concatenate([self._hist_a, a])
+        h, a = self._hist_h, self._hist_a
         if self.world > 1:
             # nccl (RCCL) gathers device tensors; gloo host tensors
             dev = "cuda" if self._dist.get_backend(self._group) == "nccl" else "cpu"
@@ -1045,6 +1084,16 @@ class MessageExchange:
         self._cnt = torch.zeros(2 * self.G, dtype=torch.int64, device=self.device)
         self._rcnt = torch.zeros(2 * self.G, dtype=torch.int64, device=self.device)
         self._host = {}  # gloo staging buffers, kept across rounds
+        self._events = []  # (start, end) of every byte collective queued on the device
+
+    def device_ms(self):
+        """Device time of the byte collectives queued since the last call (nccl; 0 with gloo)."""
+        if not self._events:
+            return 0.0
+        self._events[-1][1].synchronize()
+        ms = sum(a.elapsed_time(b) for a, b in self._events)
+        self._events = []
+        return ms
 
     def copy(self, dst, src, nbytes):
         if nbytes:
@@ -1061,10 +1110,14 @@ class MessageExchange:
             self._host[key] = t
         return t
 
-    def exchange(self, out_nmsg, out_nrec, out_buf, alloc_in):
+    def exchange(self, out_nmsg, out_nrec, out_buf, alloc_in, after=None):
         """out_*: this rank's outbox (counts per destination, its packed buffer's address).
         alloc_in(in_nmsg, in_nrec) -> the inbox's address, which receives every source's segment
-        for this rank in source order."""
+        for this rank in source order. after(stream): with the nccl backend, called with torch's
+        stream once the byte collective is queued on it, so the consumer orders its next work
+        after it on the device (rp_sim_wait_stream); without it the host waits for the stream.
+        The per-peer counts do cross to the host once per exchange: torch's all_to_all_single
+        takes its split sizes as host integers, and the inbox is sized from them."""
         torch, dist, G = self.torch, self.dist, self.G
         self._cnt.copy_(torch.from_numpy(np.stack([out_nmsg, out_nrec], axis=1).astype(np.int64).reshape(-1)))
         dist.all_to_all_single(self._rcnt, self._cnt, group=self.group)
@@ -1079,9 +1132,16 @@ class MessageExchange:
                 torch.empty(0, dtype=torch.uint8, device=self.device)
             recv = torch.as_tensor(_DeviceBytes(in_buf, tot_in), device=self.device) if tot_in else \
                 torch.empty(0, dtype=torch.uint8, device=self.device)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
             dist.all_to_all_single(recv, send, output_split_sizes=seg_in, input_split_sizes=seg_out,
                                    group=self.group)
-            torch.cuda.current_stream().synchronize()
+            e1.record()
+            self._events.append((e0, e1))
+            if after is not None:
+                after(torch.cuda.current_stream().cuda_stream)
+            else:
+                torch.cuda.current_stream().synchronize()
         else:
             send = self._staging("send", tot_out)
             recv = self._staging("recv", tot_in)
@@ -1120,25 +1180,34 @@ class DistGossipSim:
         self.shard = SimShard(names, inc0, dead, self.G, self.rank, seed, suspicion_rounds, now0, device,
                               events=events)
         self.exchange_bytes = 0
+        # host wall time inside the exchanges (count all-to-all + its host read, inbox sizing, the
+        # byte all-to-all-v queued, and the join sums): what the message transport adds to a round
+        self.exchange_s = 0.0
 
     def close(self):
         self.shard.close()
 
     def step(self, rounds=1):
+        import time
         sh = self.shard
+        wait = lambda stream: check(lib().rp_sim_wait_stream(sh._h, stream))  # noqa: E731
         for _ in range(rounds):
             while True:  # the round's joins: every rank exports, the buffers are summed, then import
                 has, buf, nb = sh.join_export()
                 if not has:
                     break
+                t = time.perf_counter()
                 self.xchg.sum_bytes(buf, nb)
+                self.exchange_s += time.perf_counter() - t
                 sh.join_import()
             for k in range(SIM_STAGES):
                 sh.stage(k)
                 if k < SIM_STAGES - 1:
                     nm, nr, buf = sh.outbox()
                     self.exchange_bytes += int(nm.sum()) * MSG_BYTES + int(nr.sum()) * REC_BYTES
-                    self.xchg.exchange(nm, nr, buf, sh.inbox)
+                    t = time.perf_counter()
+                    self.xchg.exchange(nm, nr, buf, sh.inbox, after=wait)
+                    self.exchange_s += time.perf_counter() - t
 
     @property
     def round(self):

@@ -1163,8 +1163,15 @@ struct Members {
         uint32_t* done = napplied.p + 2;
         const unsigned g = grid_for(k, 256);
         const bool mine = ck_nsh <= 1 || batch_no % ck_nsh == ck_sh;
-        batch_no++;
         const bool build = !defer_ck && mine;
+        if (build && hist_cap && nt.size()) {  // refuse before anything is applied
+            uint32_t pend = 0;
+            for (uint64_t w : pend_mask.w) pend += (uint32_t)__builtin_popcountll(w);
+            if (hist_n + pend + 1 > hist_cap)
+                throw Error(RP_ESTATE, "checksum history full (history_cap of rp_members_checksum_shard): read and "
+                                       "drain it with rp_members_checksum_history_drain");
+        }
+        batch_no++;
         const uint32_t nb = (cap + kBk - 1) / kBk;
         if (use_bucket_fold(k, nb)) {
             const uint32_t ntiles = (k + kBkTile - 1) / kBkTile;
@@ -1328,12 +1335,11 @@ struct Members {
         RP_HIP(hipGetLastError());
         uint32_t nb = 0;
         for (uint64_t w : pend_mask.w) nb += (uint32_t)__builtin_popcountll(w);
+        // update_dev refuses a batch the history cannot take before it launches anything, so the
+        // nb entries always fit here and this path never throws with the group half-flushed
         if (nb) {
-            if (hist_n + nb > hist_cap)
-                throw Error(RP_ESTATE, "checksum history full (rp_members_checksum_shard history_cap)");
             hipLaunchKernelGGL(k_ck_hist, dim3(1), dim3(1), 0, ck_st, ck_meta.p + 4 * first, npending, pend_mask,
                                ck_hist.p + 2ull * hist_n);
-            RP_HIP(hipGetLastError());
             hist_n += nb;
         }
         pend_mask = {};
@@ -1341,6 +1347,7 @@ struct Members {
         group_busy[cur_group] = true;
         cur_group = (cur_group + 1) % ngroups;
         npending = 0;
+        RP_HIP(hipGetLastError());
     }
     // flush and wait, before a host read of the checksum
     void settle_checksums() {
@@ -1537,13 +1544,19 @@ int rp_members_checksum(rp_members* h, uint32_t* out, int* is_set) {
 }
 
 int rp_members_defer_checksum(rp_members* h, int defer) {
-    return guard([&] { MB(h).defer_ck = defer != 0; });
+    return guard([&] {
+        rp::Members& m = MB(h);
+        // a deferred batch records no history entry, which would misalign the per-batch record
+        RP_REQUIRE(!(defer && m.hist_cap), "defer_checksum: not with a checksum history (checksum_shard)");
+        m.defer_ck = defer != 0;
+    });
 }
 
 int rp_members_checksum_shard(rp_members* h, uint32_t nshards, uint32_t shard, uint32_t history_cap) {
     return guard([&] {
         rp::Members& m = MB(h);
         RP_REQUIRE(nshards >= 1 && shard < nshards, "checksum_shard: shard must be < nshards");
+        RP_REQUIRE(!(history_cap && m.defer_ck), "checksum_shard: a history needs per-batch checksums (defer is on)");
         m.settle_checksums();  // pending strings keep the old numbering
         m.ck_nsh = nshards;
         m.ck_sh = shard;
@@ -1568,6 +1581,20 @@ int rp_members_checksum_history(rp_members* h, uint32_t* hash, uint8_t* applied,
             }
         }
         if (n) *n = m.hist_n;
+    });
+}
+
+int rp_members_checksum_history_drain(rp_members* h, uint32_t count) {
+    return guard([&] {
+        rp::Members& m = MB(h);
+        m.settle_checksums();
+        RP_REQUIRE(count <= m.hist_n, "checksum_history_drain: count exceeds the recorded entries");
+        if (count && count < m.hist_n) {  // keep the entries after the drained ones, in order
+            std::vector<uint32_t> v(2ull * (m.hist_n - count));  // (the ranges may overlap)
+            RP_HIP(hipMemcpy(v.data(), m.ck_hist.p + 2ull * count, 4ull * v.size(), hipMemcpyDeviceToHost));
+            RP_HIP(hipMemcpy(m.ck_hist.p, v.data(), 4ull * v.size(), hipMemcpyHostToDevice));
+        }
+        m.hist_n -= count;
     });
 }
 

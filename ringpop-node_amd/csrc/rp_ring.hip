@@ -714,6 +714,19 @@ __device__ __forceinline__ void lookupn_redo(const uint8_t* __restrict__ keys, c
     if (counts) counts[k] = (uint8_t)cnt;
 }
 
+// Phase cycle counters of the lean kernel (diagnostics only: built with -DRP_LK_PROF by
+// tools/build_prof.sh; the product build has none of this). A wave stamps s_memtime at each
+// phase boundary, the stamp depending on the phase's last result; the per-phase sums over all
+// waves land in g_lk_prof (printed by launch_lookupn under RP_LK_PROF_PRINT).
+#ifdef RP_LK_PROF
+__device__ unsigned long long g_lk_prof[10];
+#define LK_T(var, dep) \
+    uint64_t var;      \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var) : "v"(dep))
+#else
+#define LK_T(var, dep)
+#endif
+
 // The C2 hot kernel, lean form (round 2): the same layout, loads and results as
 // k_lookupn_compact, with fewer vector instructions per key (the SQ counters put that kernel at
 // ~2.9x the VALU issue of the hash-only ablation).
@@ -815,9 +828,13 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
         for (int q = 0; q < NEED; q++) row[kk * NEED + q] = res[q];
         if (cnt) cnt[kk] = (uint8_t)rc;
     };
+#ifdef RP_LK_PROF
+    uint64_t pa[6] = {0, 0, 0, 0, 0, 0}, ntl = 0;
+#endif
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint64_t base = t * TK;
         uint32_t h[KPL];
+        LK_T(t0, tid);
         {
             const u32x4* s4 = reinterpret_cast<const u32x4*>(keys + base * LEN);
             u32x4 pre[PER];
@@ -836,6 +853,12 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
                     if (k >= hs * VS && k < (hs + 1) * VS) reinterpret_cast<u32x4*>(sk)[k - hs * VS] = pre[q];
                 }
                 __syncthreads();
+#ifdef RP_LK_PROF
+                if (hs == 0) {
+                    LK_T(tk, sk[tid]);
+                    pa[0] += tk - t0;
+                }
+#endif
 #pragma unroll
                 for (int k = hs * (KPL / HS); k < (hs + 1) * (KPL / HS); k++) {
                     uint32_t w[W4];
@@ -845,6 +868,7 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
                 }
             }
         }
+        LK_T(t2, h[KPL - 1]);
         __syncthreads();  // sk is reused as so below
         u32x2 rec[KPL];
 #pragma unroll
@@ -861,6 +885,7 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
             bc[k] = (rec[k].y >> s4) & 15u;
             win[k] = load16(lo[k] + wstart(h[k], bc[k]));
         }
+        LK_T(t3, lo[KPL - 1]);
         uint32_t nag = 0;  // wave-uniform length of this wave's list
 #pragma unroll
         for (int k = 0; k < KPL; k++) {
@@ -919,19 +944,38 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
                 if (sp < kSlowPerTile) slow_list[t * kSlowPerTile + sp] = kk;
             }
         }
+        LK_T(t4, nag);
         // second windows, one listed key per lane (the list is this wave's own LDS rows)
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         for (uint32_t j = lane; j < (nag < AG ? nag : AG); j += 64)
             finish2(load16(ag[wv][0][j]), ag[wv][1][j], ag[wv][2][j], so, counts ? counts + base : nullptr,
                     &nslow_tile, slow_list + t * kSlowPerTile);
+        LK_T(t5a, nag);
         __syncthreads();
+        LK_T(t5, tid);
         if (tid == 0) slow_cnt[t] = nslow_tile;
         u32x4* d4 = reinterpret_cast<u32x4*>(out + base * NEED);
         const u32x4* s4 = reinterpret_cast<const u32x4*>(so);
 #pragma unroll
         for (int k = tid; k < TK * NEED / 4; k += kLkThreads) __builtin_nontemporal_store(s4[k], d4 + k);
         __syncthreads();
+#ifdef RP_LK_PROF
+        LK_T(t6, tid);
+        pa[1] += t2 - t0;
+        pa[2] += t3 - t2;
+        pa[3] += t4 - t3;
+        pa[4] += t5a - t4;
+        pa[5] += t6 - t5;
+        ntl += 1;
+        (void)t5;
+#endif
     }
+#ifdef RP_LK_PROF
+    if (lane == 0) {
+        for (int i = 0; i < 6; i++) atomicAdd(&g_lk_prof[i], (unsigned long long)pa[i]);
+        atomicAdd(&g_lk_prof[6], (unsigned long long)ntl);
+    }
+#endif
     if constexpr (FUSE) {
         // this workgroup's tiles t = blockIdx.x + i * gridDim.x; their rows are stored (the barrier
         // above orders the overwrites after them)
@@ -1643,6 +1687,20 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
                                dim3(256), 0, st, keys, fv, np, W, out, counts, r.slow.p, r.nslow.p, ntiles,
                                (uint32_t)TK);
         RP_HIP(hipGetLastError());
+#ifdef RP_LK_PROF
+        if (getenv_flag("RP_LK_PROF_PRINT")) {
+            unsigned long long v[10];
+            RP_HIP(hipStreamSynchronize(st));
+            RP_HIP(hipMemcpyFromSymbol(v, HIP_SYMBOL(g_lk_prof), sizeof v));
+            const double nw = (double)(v[6] ? v[6] : 1);
+            fprintf(stderr,
+                    "[rp] lean phase cycles per wave-tile (%llu): keys-arrive %.0f hash-all %.0f idx %.0f win1+loop %.0f "
+                    "finish2 %.0f barrier+store %.0f\n",
+                    v[6], v[0] / nw, v[1] / nw, v[2] / nw, v[3] / nw, v[4] / nw, v[5] / nw);
+            memset(v, 0, sizeof v);
+            RP_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_lk_prof), v, sizeof v));
+        }
+#endif
         if (getenv_flag("RP_LOOKUP_DEBUG")) {
             std::vector<uint32_t> c(ntiles);
             RP_HIP(hipMemcpyAsync(c.data(), r.nslow.p, 4 * ntiles, hipMemcpyDeviceToHost, st));

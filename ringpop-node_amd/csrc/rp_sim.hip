@@ -3324,6 +3324,7 @@ struct Sim {
     // chains; stage 3 waits for it before phase D2 changes views again (RP_SIM_EARLY=1: on)
     hipStream_t st2 = nullptr;
     hipEvent_t ev_c = nullptr, ev_early = nullptr;
+    hipEvent_t ev_ext = nullptr;  // rp_sim_wait_stream: the next stage waits for a caller's stream
     bool early_pending = false;
     bool early_on = [] {
         const char* e = getenv("RP_SIM_EARLY");
@@ -4191,6 +4192,7 @@ int rp_sim_destroy(rp_sim* s) {
             (void)hipStreamDestroy(s->impl.st2);
             (void)hipEventDestroy(s->impl.ev_c);
             (void)hipEventDestroy(s->impl.ev_early);
+            if (s->impl.ev_ext) (void)hipEventDestroy(s->impl.ev_ext);
         }
         delete s;
     });
@@ -4253,6 +4255,15 @@ int rp_sim_inbox(rp_sim* s, const uint64_t* nmsg, const uint64_t* nrec, void** b
         S.prepare_in(nmsg, nrec);
         RP_HIP(hipStreamSynchronize(S.st));
         if (buf) *buf = S.in.buf.p;
+    });
+}
+
+int rp_sim_wait_stream(rp_sim* s, void* stream) {
+    return guard([&] {
+        rp::Sim& S = SM(s);
+        if (!S.ev_ext) RP_HIP(hipEventCreateWithFlags(&S.ev_ext, hipEventDisableTiming));
+        RP_HIP(hipEventRecord(S.ev_ext, (hipStream_t)stream));
+        RP_HIP(hipStreamWaitEvent(S.st, S.ev_ext, 0));
     });
 }
 

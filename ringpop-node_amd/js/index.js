@@ -72,27 +72,41 @@ HashRing.prototype._refreshChecksum = function _refreshChecksum() {
     this.emit('checksumComputed');
 };
 
-// The servers map after a batch (index.js:60-94: adds in order, then removes in order), and
-// whether it changed; the device must agree.
-HashRing.prototype._applyServers = function _applyServers(add, remove, deviceChanged) {
-    var changed = false;
+// The reference's decisions for a batch (index.js:60-94: adds in order, then removes in order,
+// each tested with `!!this.servers[name]`), made before the device is touched: only the names
+// that change go to the device, and the servers map is committed after the device succeeded, so
+// the two never diverge (a name the map already answers for, e.g. 'constructor', is skipped on
+// both sides, as in the reference).
+HashRing.prototype._planServers = function _planServers(add, remove) {
+    var servers = this.servers, over = Object.create(null);
+    function present(name) { return name in over ? over[name] : !!servers[name]; }
+    var plan = {add: [], remove: []};
     for (var i = 0; i < add.length; i++) {
-        if (!this.servers[add[i]]) { this.servers[add[i]] = true; changed = true; }
+        if (!present(add[i])) { over[add[i]] = true; plan.add.push(add[i]); }
     }
     for (var j = 0; j < remove.length; j++) {
-        if (this.servers[remove[j]]) { delete this.servers[remove[j]]; changed = true; }
+        if (present(remove[j])) { over[remove[j]] = false; plan.remove.push(remove[j]); }
     }
-    if (changed !== !!deviceChanged) {
-        throw new Error('ringpop_amd: device ring and servers map disagree (ringChanged ' +
-            deviceChanged + ' vs ' + changed + ')');
+    return plan;
+};
+
+HashRing.prototype._applyPlan = function _applyPlan(plan) {
+    var changed = plan.add.length + plan.remove.length > 0;
+    if (!changed) { return false; }
+    var deviceChanged = native.ringAddRemove(this._h, plan.add, plan.remove,
+        this._replicaTokens(plan.add), this._replicaTokens(plan.remove));
+    if (!deviceChanged) {
+        throw new Error('ringpop_amd: the device ring did not change for ' + JSON.stringify(plan));
     }
-    return changed;
+    for (var i = 0; i < plan.add.length; i++) { this.servers[plan.add[i]] = true; }
+    for (var j = 0; j < plan.remove.length; j++) { delete this.servers[plan.remove[j]]; }
+    return true;
 };
 
 // addServer(name) — index.js:39-48
 HashRing.prototype.addServer = function addServer(name) {
     if (this.hasServer(name)) { return; }
-    this._applyServers([name], [], native.ringAddRemove(this._h, [name], null, this._replicaTokens([name]), null));
+    this._applyPlan(this._planServers([name], []));
     this._refreshChecksum();
     this.emit('added', name);
 };
@@ -100,7 +114,7 @@ HashRing.prototype.addServer = function addServer(name) {
 // removeServer(name) — index.js:124-133
 HashRing.prototype.removeServer = function removeServer(name) {
     if (!this.hasServer(name)) { return; }
-    this._applyServers([], [name], native.ringAddRemove(this._h, null, [name], null, this._replicaTokens([name])));
+    this._applyPlan(this._planServers([], [name]));
     this._refreshChecksum();
     this.emit('removed', name);
 };
@@ -108,11 +122,7 @@ HashRing.prototype.removeServer = function removeServer(name) {
 // addRemoveServers(add, remove) -> ringChanged — index.js:60-94 (no added/removed events,
 // as in the reference).
 HashRing.prototype.addRemoveServers = function addRemoveServers(serversToAdd, serversToRemove) {
-    serversToAdd = serversToAdd || [];
-    serversToRemove = serversToRemove || [];
-    var changed = this._applyServers(serversToAdd, serversToRemove,
-        native.ringAddRemove(this._h, serversToAdd, serversToRemove,
-            this._replicaTokens(serversToAdd), this._replicaTokens(serversToRemove)));
+    var changed = this._applyPlan(this._planServers(serversToAdd || [], serversToRemove || []));
     if (changed) { this._refreshChecksum(); }
     return changed;
 };

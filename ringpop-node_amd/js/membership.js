@@ -121,6 +121,16 @@ Member.prototype._applyVerdict = function _applyVerdict(update, damp) {
     if (this.incarnationNumber !== update.incarnationNumber) { this.incarnationNumber = update.incarnationNumber; }
     if (cfg(this.ringpop, 'dampScoringEnabled', false) && update.address !== this.ringpop.whoami()) {
         if (damp) {
+            // _applyUpdatePenalty starts with decayDampScore, which emits 'dampScoreDecayed'
+            // (decayed, previous) before the penalty (member.js:45-66,136): the decayed value is
+            // the same expression over this member's last score and timestamp at the device's now
+            var old = this.dampScore;
+            if (old !== null && old !== undefined) {
+                var decay = Math.pow(Math.E, -1 * ((damp.now - this.lastUpdateTimestamp) / 1000) * Math.LN2 /
+                    cfg(this.ringpop, 'dampScoringHalfLife', 60));
+                this.emit('dampScoreDecayed', Math.max(Math.round(this.lastUpdateDampScore * decay),
+                    cfg(this.ringpop, 'dampScoringMin', 0)), old);
+            }
             this.dampScore = damp.score;
             if (damp.exceeded) { this.emit('suppressLimitExceeded'); }
         } else {

@@ -18,6 +18,14 @@ var util = require('util');
 var refRoot = process.argv[2];
 var input = JSON.parse(fs.readFileSync(process.argv[3], 'utf8'));
 var initMembership = require(path.join(refRoot, 'lib/membership/index.js'));
+// every Member's 'dampScoreDecayed' (member.js:65), in emission order: [address, new, old]
+var RefMember = require(path.join(refRoot, 'lib/membership/member.js'));
+var decayed = [];
+var origEmit = RefMember.prototype.emit;
+RefMember.prototype.emit = function (ev, a, b) {
+    if (ev === 'dampScoreDecayed') { decayed.push([this.address, a, b]); }
+    return origEmit.apply(this, arguments);
+};
 
 var clock = 0;
 Date.now = function () { return clock; };
@@ -59,6 +67,7 @@ input.cases.forEach(function (c) {
         clock = op.now;
         powLog = [];
         suppressed.length = 0;
+        decayed.length = 0;
         var o = {};
         if (op.type === 'ready') {
             rp.isReady = op.value;
@@ -74,6 +83,7 @@ input.cases.forEach(function (c) {
             o.applied = applied.map(function (u) { return u._i; });
         }
         o.suppressed = suppressed.slice();
+        o.decayed = decayed.slice();
         o.members = m.members.map(function (x) {
             return [x.address, x.dampScore, x.lastUpdateDampScore, x.lastUpdateTimestamp];
         });

@@ -20,6 +20,13 @@ fs.mkdirSync(path.join(root, 'lib', 'membership'), {recursive: true});
 fs.writeFileSync(path.join(root, 'lib', 'membership', 'index.js'), "throw new Error('not the drop-in');\n");
 drop.install(root);
 var initMembership = require(path.join(root, 'lib', 'membership', 'index.js'));
+// every Member's 'dampScoreDecayed' in emission order, as ref_damp.js records the reference's
+var decayed = [];
+var origEmit = drop.Member.prototype.emit;
+drop.Member.prototype.emit = function (ev, a, b) {
+    if (ev === 'dampScoreDecayed') { decayed.push([this.address, a, b]); }
+    return origEmit.apply(this, arguments);
+};
 
 var clock = 0;
 Date.now = function () { return clock; };
@@ -113,6 +120,7 @@ util.inherits(DampRingpop, FakeRingpop);
     c.ops.forEach(function (op, j) {
         clock = op.now;
         suppressed.length = 0;
+        decayed.length = 0;
         var tag = 'damp ' + c.name + ' op ' + j, o = c.out[j];
         if (op.type === 'ready') {
             rp.isReady = op.value;
@@ -128,6 +136,7 @@ util.inherits(DampRingpop, FakeRingpop);
             eq(tag + ' applied', applied.map(function (u) { return u._i; }), o.applied);
         }
         eq(tag + ' suppressed', suppressed, o.suppressed);
+        eq(tag + ' dampScoreDecayed', decayed, o.decayed);
         eq(tag + ' damp state', m.members.map(function (x) {
             return [x.address, x.dampScore, x.lastUpdateDampScore, x.lastUpdateTimestamp];
         }), o.members);

@@ -49,8 +49,10 @@ def _reference(gpu, n, k, nbatch):
     return cks, ex, st, inc
 
 
-@pytest.mark.parametrize("G", [2, 3])
-def test_dist_membership_matches_single_gpu(gpu, tmp_path, G):
+@pytest.mark.parametrize("G,mode", [(2, ""), (3, ""), (2, "each")])
+def test_dist_membership_matches_single_gpu(gpu, tmp_path, G, mode):
+    """mode "each": every rank reads .checksum after every batch (the value of a batch another
+    rank hashed) through a 2-entry device history that each read drains."""
     n, k, nbatch = 6000, 5000, 7
     out = str(tmp_path / "merge.npz")
     port = _free_port()
@@ -59,12 +61,48 @@ def test_dist_membership_matches_single_gpu(gpu, tmp_path, G):
     for r in range(G):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(G), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, worker, str(n), str(k), str(nbatch), out, "gloo"], env=env))
+        procs.append(subprocess.Popen([sys.executable, worker, str(n), str(k), str(nbatch), out, "gloo", mode],
+                                      env=env))
     assert [p.wait(timeout=100) for p in procs] == [0] * G
     d = np.load(out)
     cks, ex, st, inc = _reference(gpu, n, k, nbatch)
     assert [int(c) for c in d["checksums"]] == cks
+    if mode == "each":
+        assert [int(c) for c in d["reads"]] == cks
     assert np.array_equal(d["ex"], ex) and np.array_equal(d["st"], st) and np.array_equal(d["inc"], inc)
+
+
+def test_checksum_history_full_refuses_before_applying(gpu):
+    """A batch whose history entry would not fit history_cap fails with RP_ESTATE and applies
+    nothing (the table and the handle's pending state are as before); after a drain the stream
+    goes on and every recorded value equals a plain handle's."""
+    S = _load("rp_synth", os.path.join(REPO, "ringpop-node_amd", "synth.py"))
+    n = k = 2000
+    names, _, inc0 = S.c3_members(n)
+    a = gpu.Membership(whoami=names[0], capacity=n)
+    b = gpu.Membership(whoami=names[0], capacity=n)
+    a.intern(names)
+    b.intern(names)
+    a.checksum_shard(1, 0, 3)
+    with pytest.raises(gpu.RingpopAmdError):  # a deferred batch would record no entry
+        gpu.check(gpu.lib().rp_members_defer_checksum(a._h, 1))
+    want = []
+    for i in range(5):
+        ids, us, ui = S.c3_updates(n, k, seed=900 + i, base_inc=inc0 + 3 * (i // 2))
+        if i == 3:
+            before = a.dump()
+            with pytest.raises(gpu.RingpopAmdError, match="history full"):
+                a.update_ids(ids, us, ui, now_ms=1 + i)
+            after = a.dump()
+            assert all(np.array_equal(x, y) for x, y in zip(before, after))
+            h, _ = a.checksum_history()
+            assert len(h) == 3
+            gpu.check(gpu.lib().rp_members_checksum_history_drain(a._h, 2))
+        a.update_ids(ids, us, ui, now_ms=1 + i)
+        b.update_ids(ids, us, ui, now_ms=1 + i)
+        want.append(b.checksum)
+    h, app = a.checksum_history()  # batch 2 (kept by the drain of two), 3, 4
+    assert list(app) == [1, 1, 1] and [int(x) for x in h] == want[2:5]
 
 
 def test_checksum_history_single_handle(gpu):

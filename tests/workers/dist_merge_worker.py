@@ -3,7 +3,11 @@ processes on the same box): every rank folds the same C3-shaped batch stream on 
 of the member table; checksums are divided by batch (b % G == rank). Rank 0 writes the gathered
 per-batch checksums and its final table to OUT (npz).
 
-    RANK=r WORLD_SIZE=g MASTER_ADDR=127.0.0.1 MASTER_PORT=p python dist_merge_worker.py n k nbatch out backend
+    RANK=r WORLD_SIZE=g MASTER_ADDR=127.0.0.1 MASTER_PORT=p python dist_merge_worker.py n k nbatch out backend [each]
+
+With `each`, every rank reads `m.checksum` after every batch (a collective on a DistMembership)
+with a 2-entry device history, so the record is drained by every read; rank 0 also writes those
+per-batch reads.
 """
 import importlib.util
 import os
@@ -52,22 +56,25 @@ def main():
     else:
         dist.init_process_group("gloo")
     names, _, inc0 = S.c3_members(n)
-    m = rpa.DistMembership(whoami=names[0], capacity=n, device=local)
+    each = len(sys.argv) > 6 and sys.argv[6] == "each"
+    m = rpa.DistMembership(whoami=names[0], capacity=n, device=local, history_cap=2 if each else 1 << 16)
     assert m.intern(names) == list(range(n))
     stream = torch.cuda.current_stream()
-    keep = []
+    keep, reads = [], []
     for b, (ids, us, ui) in enumerate(batches(S, n, k, nbatch, inc0)):
         d = [torch.from_numpy(np.ascontiguousarray(ids).view(np.int32)).cuda(), torch.from_numpy(us).cuda(),
              torch.from_numpy(ui).cuda()]
         keep.append(d)
         m.update_dev(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), len(ids), 1434500000000 + b,
                      stream=stream.cuda_stream)
+        if each:
+            reads.append(m.checksum)
     torch.cuda.synchronize()
     cks = m.checksums()
     ex, st, inc = m.dump()
     if dist.get_rank() == 0:
         np.savez(out, checksums=np.array([-1 if c is None else c for c in cks], dtype=np.int64), ex=ex, st=st,
-                 inc=inc)
+                 inc=inc, reads=np.array([-1 if c is None else c for c in reads], dtype=np.int64))
     m.close()
     dist.barrier()
     dist.destroy_process_group()

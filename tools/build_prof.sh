@@ -1,10 +1,14 @@
 #!/bin/bash
-# Builds ringpop-node_amd/librpamd_prof.so: the library with the checksum kernel's cycle
-# counters compiled in (-DRP_CK_PROF; printf per epoch loop). Load it with RP_AMD_LIB=<path>.
+# Builds a diagnostics copy of the library with cycle counters compiled in. Load it with
+# RP_AMD_LIB=<path>.
+#   tools/build_prof.sh              -> librpamd_prof.so   (-DRP_CK_PROF: checksum chain epochs)
+#   DEFS=-DRP_LK_PROF OUT=librpamd_lkprof.so tools/build_prof.sh   (lean lookup phases)
 set -e
 cd "$(dirname "$0")/../ringpop-node_amd/csrc"
-B=${TMPDIR:-/tmp}/rp_profbuild
+DEFS=${DEFS:--DRP_CK_PROF}
+OUT=${OUT:-librpamd_prof.so}
+B=${TMPDIR:-/tmp}/rp_profbuild_${OUT%.so}
 mkdir -p $B
-for f in *.hip; do /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -DRP_CK_PROF ${EXTRA:-} -c $f -o $B/${f%.hip}.o & done
+for f in *.hip; do /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $DEFS ${EXTRA:-} -c $f -o $B/${f%.hip}.o & done
 wait
-/opt/rocm/bin/hipcc -O3 -fPIC --offload-arch=gfx950 -shared -o ../librpamd_prof.so $B/*.o
+/opt/rocm/bin/hipcc -O3 -fPIC --offload-arch=gfx950 -shared -o ../$OUT $B/*.o
