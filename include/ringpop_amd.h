@@ -101,6 +101,13 @@ int rp_ring_lookup(rp_ring *r, const char *keys, const uint64_t *off, uint32_t s
                    uint32_t *owners);
 int rp_ring_lookupn(rp_ring *r, const char *keys, const uint64_t *off, uint32_t stride, uint64_t n,
                     int32_t nrep, uint32_t *owners, uint8_t *counts);
+/* Low-latency single calls (RingPop.lookup / lookupN per request, index.js:434-471): with
+ * idle_ms > 0, a one-key rp_ring_lookup / rp_ring_lookupn (key <= 180 B, n <= 8) is answered by a
+ * resident service wave (one workgroup on one CU) that polls pinned, device-mapped host lines,
+ * instead of a kernel launch and a stream sync per call. The wave exits after idle_ms without a
+ * request (and after 30 s in all) and is relaunched by the next call; a ring mutation stops it.
+ * idle_ms = 0 (the default) turns it off. */
+int rp_ring_service(rp_ring *r, uint32_t idle_ms);
 /* Same with precomputed key hashes (hashFunc(key) done by the caller). */
 int rp_ring_lookup_hashes(rp_ring *r, const uint32_t *hashes, uint64_t n, uint32_t *owners);
 int rp_ring_lookupn_hashes(rp_ring *r, const uint32_t *hashes, uint64_t n, int32_t nrep,

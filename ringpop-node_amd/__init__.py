@@ -122,6 +122,7 @@ SIGNATURES = {
     "rp_members_checksum_shard": (_INT, [_P, _U32, _U32, _U32]),
     "rp_members_checksum_history": (_INT, [_P, _P, _P, _U32, _P]),
     "rp_members_checksum_history_drain": (_INT, [_P, _U32]),
+    "rp_ring_service": (_INT, [_P, _U32]),
     "rp_members_damp_configure": (_INT, [_P, _P]),
     "rp_members_damp_last": (_INT, [_P, _P, _P, _U32]),
     "rp_members_damp_decay": (_INT, [_P, ctypes.c_int64]),
@@ -245,6 +246,11 @@ class HashRing:
         R = self.replicaPoints
         return np.array([self.hashFunc(s + str(i)) & 0xFFFFFFFF for s in names for i in range(R)],
                         dtype=np.uint32)
+
+    def service(self, idle_ms):
+        """rp_ring_service: idle_ms > 0 answers one-key lookup / lookupN calls through the resident
+        lookup service (no launch per call); 0 turns it off."""
+        check(lib().rp_ring_service(self._h, int(idle_ms)))
 
     def addRemoveServers(self, serversToAdd=None, serversToRemove=None):
         """lib/ring/index.js:60-94; returns ringChanged. The reference's per-name decisions (adds in

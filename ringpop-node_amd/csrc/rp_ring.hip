@@ -13,6 +13,7 @@
 // registers (fh::hash32_words), searched bucket-first, walked for distinct owners, and the
 // owner rows are staged back through LDS for coalesced stores.
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -746,7 +747,11 @@ __device__ unsigned long long g_lk_prof[10];
 // profiles/r03/ab_lookup_occ.json: the 119-121 VGPRs and 4 waves per SIMD stay.)
 // FUSE: the workgroup finishes its own tiles' deferred keys after its last tile (one thread per
 // list slot, 8 tiles at a time) instead of k_lookupn_fix_tiles (A/B: RP_LOOKUP_FUSEFIX).
-template <int KPL, int NEED, int HS = 1, bool FUSE = false>
+// STG: how the key tile reaches LDS. 0: every lane loads all its 16-B pieces of the tile into
+// registers first (PER x u32x4 held), then the slices go through LDS one after another. 1: the
+// slices are DMA'd global -> LDS (global_load_lds_dwordx4, no VGPR destination) into a ring of
+// two slice buffers, slice s + 2 issued as soon as slice s is hashed (A/B: RP_LOOKUP_STG=1).
+template <int KPL, int NEED, int HS = 1, bool FUSE = false, int STG = 0>
 __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __restrict__ keys, uint64_t ntiles,
                                                              CompactView cv, uint32_t* __restrict__ out,
                                                              uint8_t* __restrict__ counts,
@@ -763,7 +768,9 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
     static_assert(KPL % HS == 0 && V4 % HS == 0, "slices of whole keys");
     constexpr int SK = TK * W4 / HS, SO = TK * NEED;
     constexpr int VS = V4 / HS;  // 16-B vectors per slice
-    __shared__ __attribute__((aligned(16))) uint32_t lds[SK > SO ? SK : SO];
+    constexpr int SKR = STG == 1 ? 2 * SK : SK;  // STG 1: two slice buffers
+    static_assert(STG == 0 || (SK * 4) % 1024 == 0, "DMA slices of whole 1-KB wave pieces");
+    __shared__ __attribute__((aligned(16))) uint32_t lds[SKR > SO ? SKR : SO];
     constexpr uint32_t AG = 64;  // list slots per wave (8 % of 64 * KPL keys: ~41 at KPL 8)
     __shared__ uint32_t ag[NW][3][AG];  // per-wave second-window list: start, K, kk | bc << 12 | search << 16
     __shared__ uint32_t nslow_tile;
@@ -835,7 +842,60 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
         const uint64_t base = t * TK;
         uint32_t h[KPL];
         LK_T(t0, tid);
-        {
+        if constexpr (STG == 1) {
+            // DMA ring: slice s in buffer s & 1; a slice is SLI 1-KB wave pieces dealt over the
+            // waves (wave w takes pieces w, w + NW, ...), so wave w waits for its own pieces of
+            // slice s with a counted vmcnt (its pieces of slice s + 1 may stay in flight), then
+            // the workgroup barrier makes every wave's pieces visible
+            constexpr int SLB = SK * 4, SLI = SLB / 1024, PW = SLI / NW, PX = SLI % NW;
+            const uint8_t* src = keys + base * LEN;
+            uint8_t* ring = reinterpret_cast<uint8_t*>(lds);
+            auto dma = [&](int sl) {
+#pragma unroll
+                for (int i = 0; i < PW + 1; i++)
+                    if (i < PW || wv < PX)
+                        __builtin_amdgcn_global_load_lds(
+                            reinterpret_cast<const void*>(src + sl * SLB + (i * NW + wv) * 1024 + lane * 16),
+                            ring + (sl & 1) * SLB + (i * NW + wv) * 1024, 16, 0, 0);
+            };
+            if (tid == 0) nslow_tile = 0;
+            dma(0);
+            if (HS > 1) dma(1);
+#pragma unroll
+            for (int hs = 0; hs < HS; hs++) {
+                if (hs + 1 < HS) {
+                    if (wv < PX)
+                        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW + 1) : "memory");
+                    else
+                        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+#ifdef RP_LK_PROF
+                if (hs == 0) {
+                    LK_T(tk, lds[tid]);
+                    pa[0] += tk - t0;
+                }
+#endif
+                const uint32_t* sb = lds + (hs & 1) * SK;
+#pragma unroll
+                for (int k = hs * (KPL / HS); k < (hs + 1) * (KPL / HS); k++) {
+                    uint32_t w[W4];
+#pragma unroll
+                    for (int j = 0; j < W4; j++) w[j] = sb[(tid + (k - hs * (KPL / HS)) * kLkThreads) * W4 + j];
+                    h[k] = fh::hash32_words<LEN>(w);
+                }
+                if (hs + 2 < HS) {  // this buffer is free once every wave has hashed from it
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    __builtin_amdgcn_s_barrier();
+                    asm volatile("" ::: "memory");
+                    dma(hs + 2);
+                }
+            }
+        } else {
             const u32x4* s4 = reinterpret_cast<const u32x4*>(keys + base * LEN);
             u32x4 pre[PER];
 #pragma unroll
@@ -1125,6 +1185,84 @@ __global__ __launch_bounds__(64) void k_lookupn_small(const SmallKeys sk, View r
     if (counts) counts[k] = (uint8_t)(c > 255 ? 255 : c);
 }
 
+// The lookup service (rp_ring_service): one resident wave answers single-key lookup / lookupN
+// calls (RingPop.lookup per request, index.js:434-451) through pinned, device-mapped host lines,
+// so a call costs the PCIe round trips instead of a launch and a stream sync. Request: a header
+// line {seq, len, np, W, stop} and up to kSvcChunks key lines of 60 B + their copy of seq in the
+// last dword (the host writes a line's bytes before its seq, so a line read with the expected
+// seq holds the new bytes). Response: owners + count, then seq in its own line, released at
+// system scope. The wave exits on the stop flag, after idle_ticks of no request, or after
+// max_ticks in all (s_memrealtime, 100 MHz), so it always drains; the host relaunches it when a
+// request finds it gone.
+constexpr uint32_t kSvcChunks = 3, kSvcKeyMax = kSvcChunks * 60;
+struct SvcLines {
+    uint32_t req[16 * (1 + kSvcChunks)];  // header line + key lines
+    uint32_t resp[16];                    // owners[0..W), count at [15]
+    uint32_t resp_seq[16];                // [0] = the answered seq
+};
+template <class View>
+__global__ __launch_bounds__(64) void k_lookup_service(SvcLines* io, View rv, uint32_t last, uint64_t idle_ticks,
+                                                       uint64_t max_ticks) {
+    __shared__ uint32_t kw[kSvcChunks * 15];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    uint64_t t_idle = t_start;
+    while (true) {
+        const uint32_t v = lane < 16 * (1 + kSvcChunks)
+                               ? __hip_atomic_load(&io->req[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                               : 0u;
+        const uint32_t seq = __builtin_amdgcn_readfirstlane(__shfl(v, 0, 64));
+        const uint32_t stop = __builtin_amdgcn_readfirstlane(__shfl(v, 4, 64));
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (stop || now - t_start > max_ticks) break;
+        if (seq == last) {
+            if (now - t_idle > idle_ticks) break;
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        const uint32_t len = __builtin_amdgcn_readfirstlane(__shfl(v, 1, 64));
+        const int np = (int)__builtin_amdgcn_readfirstlane(__shfl(v, 2, 64));
+        const uint32_t W = __builtin_amdgcn_readfirstlane(__shfl(v, 3, 64));
+        const uint32_t nch = (len + 59) / 60;
+        // every key line the request uses must carry this seq (else re-read)
+        const bool line_ok = lane < 16 || (lane >> 4) > nch || (lane & 15) != 15 || v == seq;
+        if (__ballot(!line_ok) != 0 || len > kSvcKeyMax || W > 16) {
+            if (len > kSvcKeyMax || W > 16) {  // malformed: answer empty
+                if (lane < 16) __hip_atomic_store(&io->resp[lane], lane == 15 ? 0u : NIL, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_SYSTEM);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                if (lane == 0) __hip_atomic_store(&io->resp_seq[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                last = seq;
+                t_idle = now;
+            }
+            continue;
+        }
+        if (lane >= 16 && (lane & 15) < 15) kw[((lane >> 4) - 1) * 15 + (lane & 15)] = v;
+        __syncthreads();
+        uint32_t res[8] = {NIL, NIL, NIL, NIL, NIL, NIL, NIL, NIL};
+        int c = 0;
+        if (lane == 0) {
+            const uint32_t i = rv.find(fh::hash32(fh::PtrSrc{reinterpret_cast<const uint8_t*>(kw)}, len));
+            c = ring_walk<8>(rv, i, np > 8 ? 8 : np, res);
+        }
+        // lane 0's row to lanes 0..W-1, then the seq after it (system-scope release)
+        uint32_t mine = NIL;
+#pragma unroll
+        for (uint32_t q = 0; q < 8; q++) {
+            const uint32_t x = __shfl(res[q], 0, 64);
+            mine = lane == q ? x : mine;
+        }
+        const uint32_t cnt = (uint32_t)__shfl(c, 0, 64);
+        if (lane < 16) __hip_atomic_store(&io->resp[lane], lane == 15 ? cnt : (lane < W ? mine : NIL), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        if (lane == 0) __hip_atomic_store(&io->resp_seq[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __syncthreads();
+        last = seq;
+        t_idle = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
 // ---- build kernels ----
 
 // tokens[a*R + i] = farmhash32(name(ids[a]) + String(i)); owners likewise = ids[a].
@@ -1372,6 +1510,12 @@ struct Ring {
     uint32_t* pin_out_dev = nullptr;
     uint8_t* pin_cnt_dev = nullptr;
     DevBuf<uint64_t> io_off;
+    // the lookup service (rp_ring_service): its pinned lines, stream, last answered seq
+    SvcLines* svc = nullptr;
+    SvcLines* svc_dev = nullptr;
+    hipStream_t svc_st = nullptr;
+    uint32_t svc_idle_ms = 0, svc_seq = 0;
+    bool svc_running = false;
     // group keys by owner (handleOrProxyAll)
     DevBuf<uint32_t> grp_own, grp_key, grp_first, grp_dk, grp_dv, grp_rank;
     Scratch ws;
@@ -1641,9 +1785,13 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
         const CompactFixView fv{r.tok.p, r.own.p, r.cidx.p, r.view(), r.M, r.ccb};
         // deferred keys finished by the lean kernel's own workgroups (A/B): only <8, 3, 4>
         const bool fuse = getenv_flag("RP_LOOKUP_FUSEFIX") && lean && half == 4 && kpl == 8 && need == 3 && cv.ablate != 3;
+        const bool stg1 = getenv_flag("RP_LOOKUP_STG") && lean && half == 4 && kpl == 8 && need == 3 && !fuse;
 #define RP_COMPACT(KPL, NEED)                                                                                  \
     do {                                                                                                        \
-        if (lean && half == 4 && KPL % 4 == 0 && fuse)                                                          \
+        if (KPL == 8 && NEED == 3 && stg1)                                                                      \
+            hipLaunchKernelGGL((k_lookupn_lean<8, 3, 4, false, 1>), dim3(g), dim3(kLkThreads), 0, st, keys,     \
+                               ntiles, cv, out, counts, r.slow.p, r.nslow.p, fv, np);                           \
+        else if (lean && half == 4 && KPL % 4 == 0 && fuse)                                                     \
             hipLaunchKernelGGL((k_lookupn_lean<KPL, NEED, (KPL % 4 == 0 ? 4 : 1), true>), dim3(g), dim3(kLkThreads), \
                                0, st, keys, ntiles, cv, out, counts, r.slow.p, r.nslow.p, fv, np);               \
         else if (lean && half == 4 && KPL % 4 == 0)                                                             \
@@ -1904,6 +2052,24 @@ int rp_ring_create(uint32_t replica_points, int device, rp_ring** out) {
     });
 }
 
+// ---- the lookup service (rp_ring_service; k_lookup_service)
+static void svc_stop(rp::Ring& r) {
+    if (!r.svc || !r.svc_running) return;
+    __atomic_store_n(&r.svc->req[4], 1u, __ATOMIC_RELEASE);
+    RP_HIP(hipStreamSynchronize(r.svc_st));
+    r.svc_running = false;
+    __atomic_store_n(&r.svc->req[4], 0u, __ATOMIC_RELEASE);
+}
+
+static void svc_launch(rp::Ring& r, uint32_t last) {
+    using namespace rp;
+    const uint64_t idle = (uint64_t)r.svc_idle_ms * 100000ull, maxt = 30ull * 100000000ull;  // 100 MHz ticks
+    hipLaunchKernelGGL((k_lookup_service<RingView>), dim3(1), dim3(64), 0, r.svc_st, r.svc_dev, r.view(), last, idle,
+                       maxt);
+    RP_HIP(hipGetLastError());
+    r.svc_running = true;
+}
+
 int rp_ring_destroy(rp_ring* r) {
     return guard([&] {
         if (!r) return;
@@ -1911,6 +2077,14 @@ int rp_ring_destroy(rp_ring* r) {
         if (r->impl.st) {
             (void)hipStreamSynchronize(r->impl.st);
             (void)hipStreamDestroy(r->impl.st);
+        }
+        if (r->impl.svc) {
+            try {
+                svc_stop(r->impl);
+            } catch (...) {
+            }
+            (void)hipStreamDestroy(r->impl.svc_st);
+            (void)hipHostFree(r->impl.svc);
         }
         if (r->impl.pin_out) (void)hipHostFree(r->impl.pin_out);
         if (r->impl.pin_cnt) (void)hipHostFree(r->impl.pin_cnt);
@@ -1924,6 +2098,7 @@ int rp_ring_add_remove(rp_ring* h, const char* add_bytes, const uint32_t* add_of
     return guard([&] {
         rp::Ring& r = R(h);
         RP_REQUIRE(n_add == 0 || (add_bytes && add_off), "add names missing");
+        svc_stop(r);  // the service reads the table this rebuilds
         RP_REQUIRE(n_rem == 0 || (rem_bytes && rem_off), "remove names missing");
         // lib/ring/index.js:69-76 — adds in order, skipping servers already present
         std::vector<uint32_t> add_ids, rem_ids;
@@ -2124,9 +2299,60 @@ static bool host_lookup_small(rp::Ring& r, const char* keys, const uint64_t* off
     return true;
 }
 
+// one key through the service: false when it does not apply (off, long key, wide row)
+static bool svc_lookup(rp::Ring& r, const char* key, uint32_t len, int np, uint32_t W, uint32_t* owners,
+                       uint8_t* counts) {
+    using namespace rp;
+    const int need = np <= 0 ? 1 : np;
+    if (!r.svc_idle_ms || len > kSvcKeyMax || W > 8 || need > 8 || r.M == 0) return false;
+    if (!r.svc) {
+        RP_HIP(hipHostMalloc(reinterpret_cast<void**>(&r.svc), sizeof(SvcLines), hipHostMallocMapped | hipHostMallocCoherent));
+        memset(r.svc, 0, sizeof(SvcLines));
+        RP_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&r.svc_dev), r.svc, 0));
+        RP_HIP(hipStreamCreateWithFlags(&r.svc_st, hipStreamNonBlocking));
+        r.svc_seq = 0;
+    }
+    SvcLines* io = r.svc;
+    const uint32_t s = r.svc_seq + 1;
+    for (uint32_t c = 0; c * 60 < len; c++) {  // each key line's bytes, then its seq
+        memcpy(&io->req[16 * (c + 1)], key + 60 * c, std::min<uint32_t>(60, len - 60 * c));
+        __atomic_store_n(&io->req[16 * (c + 1) + 15], s, __ATOMIC_RELEASE);
+    }
+    io->req[1] = len;
+    io->req[2] = (uint32_t)np;
+    io->req[3] = W;
+    __atomic_store_n(&io->req[0], s, __ATOMIC_RELEASE);
+    if (!r.svc_running || hipStreamQuery(r.svc_st) == hipSuccess) {
+        if (r.svc_running) RP_HIP(hipStreamSynchronize(r.svc_st));
+        svc_launch(r, s - 1);
+    }
+    uint64_t spins = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (__atomic_load_n(&io->resp_seq[0], __ATOMIC_ACQUIRE) != s) {
+        __builtin_ia32_pause();
+        if ((++spins & 4095) == 0) {
+            if (hipStreamQuery(r.svc_st) == hipSuccess && __atomic_load_n(&io->resp_seq[0], __ATOMIC_ACQUIRE) != s) {
+                svc_launch(r, s - 1);  // it exited (idle or lifetime) before taking this request
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+                svc_stop(r);
+                throw Error(RP_EDEVICE, "lookup service: no answer within 5 s");
+            }
+        }
+    }
+    r.svc_seq = s;
+    for (uint32_t q = 0; q < W; q++) owners[q] = io->resp[q];
+    if (counts) counts[0] = (uint8_t)io->resp[15];
+    return true;
+}
+
 static void host_lookup(rp::Ring& r, const char* keys, const uint64_t* off, uint32_t stride, const uint32_t* hashes,
                         uint64_t n, int np, uint32_t W, uint32_t* owners, uint8_t* counts) {
     if (n == 0) return;
+    if (!hashes && n == 1 &&
+        svc_lookup(r, keys + (stride ? 0 : off[0]), (uint32_t)(stride ? stride : off[1] - off[0]), np, W, owners,
+                   counts))
+        return;
     if (!hashes && host_lookup_small(r, keys, off, stride, n, np, W, owners, counts)) return;
     const uint8_t* dk = nullptr;
     const uint64_t* doff = nullptr;
@@ -2152,6 +2378,14 @@ static void host_lookup(rp::Ring& r, const char* keys, const uint64_t* off, uint
     RP_HIP(hipMemcpyAsync(owners, r.io_b.p, n * W * 4, hipMemcpyDeviceToHost, r.st));
     if (counts) RP_HIP(hipMemcpyAsync(counts, r.io_cnt.p, n, hipMemcpyDeviceToHost, r.st));
     RP_HIP(hipStreamSynchronize(r.st));
+}
+
+int rp_ring_service(rp_ring* h, uint32_t idle_ms) {
+    return guard([&] {
+        rp::Ring& r = R(h);
+        svc_stop(r);
+        r.svc_idle_ms = idle_ms;
+    });
 }
 
 int rp_ring_lookup(rp_ring* h, const char* keys, const uint64_t* off, uint32_t stride, uint64_t n, uint32_t* owners) {

@@ -44,6 +44,9 @@ function HashRing(options) {
     this.device = this.options.device || 0;
     requireDevice(this.device);
     this._h = native.ringCreate(this.replicaPoints, this.device);
+    // options.serviceIdleMs > 0: single-key lookup / lookupN calls go through the resident lookup
+    // service (rp_ring_service: pinned host lines polled by one device wave, no launch per call)
+    if (this.options.serviceIdleMs) { native.ringService(this._h, this.options.serviceIdleMs >>> 0); }
     // servers (index.js:32): name -> true in insertion order, as the reference keeps it (its
     // Object.keys order is getStats().servers). Host bookkeeping of the same add / remove
     // decisions the device makes; every change is checked against the device's answer.

@@ -336,6 +336,16 @@ static napi_value js_ring_server_count(napi_env env, napi_callback_info info) {
     return make_u32(env, n);
 }
 
+static napi_value js_ring_service(napi_env env, napi_callback_info info) {
+    ARGS(2);
+    handle_t *h = get_handle(env, argv[0], 1);
+    if (!h) return NULL;
+    uint32_t idle = 0;
+    NAPI_OK(napi_get_value_uint32(env, argv[1], &idle));
+    RP_OK(rp_ring_service((rp_ring *)h->p, idle));
+    return make_u32(env, idle);
+}
+
 static napi_value js_ring_token_count(napi_env env, napi_callback_info info) {
     ARGS(1);
     handle_t *h = get_handle(env, argv[0], 1);
@@ -1153,6 +1163,7 @@ static napi_value init(napi_env env, napi_value exports) {
         {"ringChecksum", js_ring_checksum},
         {"ringChecksumString", js_ring_checksum_string},
         {"ringServerCount", js_ring_server_count},
+        {"ringService", js_ring_service},
         {"ringTokenCount", js_ring_token_count},
         {"ringHasServer", js_ring_has_server},
         {"ringServers", js_ring_servers},

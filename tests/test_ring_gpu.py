@@ -126,6 +126,9 @@ LAYOUTS = {
     # deferred keys finished by the lean kernel's own workgroups (no k_lookupn_fix_tiles)
     "fusefix": {"RP_LOOKUP_FUSEFIX": "1"},
     "fusefix-grid3": {"RP_LOOKUP_FUSEFIX": "1", "RP_LOOKUP_GRID": "3"},
+    # key slices DMA'd global -> LDS (global_load_lds_dwordx4) through a two-buffer ring
+    "stg1": {"RP_LOOKUP_STG": "1"},
+    "stg1-grid3": {"RP_LOOKUP_STG": "1", "RP_LOOKUP_GRID": "3"},
     # window 1 at the bucket start (the round-2 placement) instead of the predicted start
     "wpred0": {"RP_LOOKUP_WPRED": "0"},
     "lean-kpl4": {"RP_LOOKUP_HALF": "0", "RP_LOOKUP_KPL": "4"},
@@ -199,6 +202,37 @@ def test_small_host_batches_vs_oracle(gpu, orc, nkeys, monkeypatch):
     monkeypatch.delenv("RP_RING_SMALL")
     g1, c1 = ring.lookupn_ids(keys, 3)
     assert np.array_equal(g0, g1) and np.array_equal(c0, c1)
+
+
+def test_lookup_service_vs_oracle(gpu, orc):
+    """The resident lookup service (rp_ring_service): one-key lookup / lookupN calls through
+    pinned host lines, against the oracle, for key lengths 0..180 (1-3 key lines; longer keys
+    and n > 8 take the small path), across a ring mutation (which stops the service and rebuilds
+    the table it reads), an idle exit (the next call relaunches it) and turning it off."""
+    import time
+    ring, oracle = _random_history(orc, gpu, 8, 50, 100, 3)
+    rng = random.Random(77)
+    keys = ["".join(rng.choice("abcdef0123456789:-./") for _ in range(L)) for L in
+            list(range(0, 70)) + [119, 120, 121, 179, 180, 181, 300]]
+    hs = [orc.hash32(k) for k in keys]
+    ring.service(50)
+
+    def check_all(r, o):
+        for k, h in zip(keys, hs):
+            assert [r.name(x) for x in r.lookup_ids([k])] == [o.name(o.lookup_hash(h))], k
+            for n in (0, 1, 3, 8, 9):
+                g, gc = r.lookupn_ids([k], n)
+                assert [r.name(x) for x in g[0][:gc[0]]] == [o.name(x) for x in o.lookupn_hash(h, n)], (n, k)
+
+    check_all(ring, oracle)
+    extra = ["svc-%d:3000" % i for i in range(5)]
+    ring.addRemoveServers(extra, [])
+    oracle.add_remove(extra, [])
+    check_all(ring, oracle)
+    time.sleep(0.2)  # past the 50 ms idle exit
+    check_all(ring, oracle)
+    ring.service(0)
+    check_all(ring, oracle)
 
 
 def test_device_farmhash_and_keygen(gpu, orc):

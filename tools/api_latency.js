@@ -49,12 +49,35 @@ var keys = [];
 for (var k = 0; k < 8192; k++) { keys.push(uuid()); }
 out.lookup = timeit(function (i) { ring.lookup(keys[i % keys.length]); }, 2000, 200);
 out.lookupN3 = timeit(function (i) { ring.lookupN(keys[i % keys.length], 3); }, 2000, 200);
+// the same single calls through the resident lookup service (rp_ring_service)
+native_service: {
+    amd.native.ringService(ring._h, 2000);
+    out.lookup_service = timeit(function (i) { ring.lookup(keys[i % keys.length]); }, 2000, 200);
+    out.lookupN3_service = timeit(function (i) { ring.lookupN(keys[i % keys.length], 3); }, 2000, 200);
+    amd.native.ringService(ring._h, 0);
+}
 out.lookupNBatch3 = {};
 [1, 64, 4096].forEach(function (b) {
     var r = timeit(function (i) { ring.lookupNBatch(keys.slice((i * b) % 4096, (i * b) % 4096 + b), 3); }, b > 64 ? 200 : 1000, 50);
     r.us_per_key = r.median_us / b;
     out.lookupNBatch3[b] = r;
 });
+// per-call ring mutation on the C2 ring, the call pattern of lib/on_membership_event.js:106-134
+// (one applied alive / faulty / leave update -> ring.addRemoveServers with a handful of names):
+// addServer of a new name, removeServer of it again, and addRemoveServers([new], [old]) that
+// swaps one server (then swaps it back), each a device sort + merge + checksum
+var extra = [];
+for (var x = 0; x < 64; x++) { extra.push(addr(nServers + 1000 + x)); }
+out.addServer = timeit(function (i) { ring.addServer(extra[i % 64]); ring.removeServer(extra[i % 64]); }, 100, 5);
+out.addServer.note = 'one addServer + one removeServer per call';
+out.addServer.median_us_per_mutation = out.addServer.median_us / 2;
+out.addRemoveServers = timeit(function (i) {
+    var a = extra[i % 64], b = servers[(i * 7919) % nServers];
+    ring.addRemoveServers([a], [b]);
+    ring.addRemoveServers([b], [a]);
+}, 100, 5);
+out.addRemoveServers.note = 'two addRemoveServers([a], [b]) calls per timed call';
+out.addRemoveServers.median_us_per_mutation = out.addRemoveServers.median_us / 2;
 ring.destroy();
 
 // the drop-in Membership (js/membership.js) with a stand-in ringpop, n members, then ping-sized

@@ -51,6 +51,23 @@ function ringCase(name, c) {
     for (i = 0; i < nn; i++) { sink += ring.lookupN(keys[i], 3).length; }
     dt = now() - t0;
     r.lookupN3 = {keys: nn, per_s: nn / dt, seconds: dt};
+    // per-call mutation (the call pattern of lib/on_membership_event.js:106-134): addServer +
+    // removeServer of a new name, and addRemoveServers([new], [old]) swapping one server and back
+    var extra = c.extra || [];
+    if (extra.length) {
+        var reps = extra.length;
+        t0 = now();
+        for (i = 0; i < reps; i++) { ring.addServer(extra[i]); ring.removeServer(extra[i]); }
+        r.add_remove_server_ms_per_mutation = (now() - t0) * 1e3 / (2 * reps);
+        t0 = now();
+        for (i = 0; i < reps; i++) {
+            var b = c.servers[(i * 7919) % c.servers.length];
+            ring.addRemoveServers([extra[i]], [b]);
+            ring.addRemoveServers([b], [extra[i]]);
+        }
+        r.addRemoveServers_swap_ms_per_call = (now() - t0) * 1e3 / (2 * reps);
+        r.mutation_calls = 2 * reps;
+    }
     r.sink = sink;
     out.results[name] = r;
 }

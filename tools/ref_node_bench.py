@@ -27,7 +27,8 @@ def main():
     keys = [k.tobytes().decode() for k in pyoracle.uuid_keys(42, 0, 1_000_000)]
     rings = [
         {"name": "C1", "servers": large[:1000], "keys": keys, "lookupNKeys": 100_000},
-        {"name": "C2", "servers": [S.c2_addr(i) for i in range(10_000)], "keys": keys, "lookupNKeys": 10_000},
+        {"name": "C2", "servers": [S.c2_addr(i) for i in range(10_000)], "keys": keys, "lookupNKeys": 10_000,
+         "extra": [S.c2_addr(11_000 + i) for i in range(20)]},
     ]
     n = k = 100_000
     names, _, inc0 = S.c3_members(n)
