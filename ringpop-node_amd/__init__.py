@@ -270,9 +270,10 @@ class HashRing:
             return False
         ab, ao = _pack(add)
         rb, ro = _pack(rem)
+        at, rt = self._tokens(add), self._tokens(rem)  # kept alive across the call
         changed = ctypes.c_int()
-        check(lib().rp_ring_add_remove(self._h, ab, ao.ctypes.data, len(add), _ptr(self._tokens(add)),
-                                       rb, ro.ctypes.data, len(rem), _ptr(self._tokens(rem)), ctypes.byref(changed)))
+        check(lib().rp_ring_add_remove(self._h, ab, ao.ctypes.data, len(add), _ptr(at),
+                                       rb, ro.ctypes.data, len(rem), _ptr(rt), ctypes.byref(changed)))
         if not changed.value:
             raise RingpopAmdError("the device ring did not change for add %r remove %r" % (add, rem))
         for a in add:

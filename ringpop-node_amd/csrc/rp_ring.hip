@@ -751,7 +751,7 @@ __device__ unsigned long long g_lk_prof[10];
 // registers first (PER x u32x4 held), then the slices go through LDS one after another. 1: the
 // slices are DMA'd global -> LDS (global_load_lds_dwordx4, no VGPR destination) into a ring of
 // two slice buffers, slice s + 2 issued as soon as slice s is hashed (A/B: RP_LOOKUP_STG=1).
-template <int KPL, int NEED, int HS = 1, bool FUSE = false, int STG = 0>
+template <int KPL, int NEED, int HS = 1, bool FUSE = false, int STG = 0, int LH = 1>
 __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __restrict__ keys, uint64_t ntiles,
                                                              CompactView cv, uint32_t* __restrict__ out,
                                                              uint8_t* __restrict__ counts,
@@ -768,7 +768,7 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
     static_assert(KPL % HS == 0 && V4 % HS == 0, "slices of whole keys");
     constexpr int SK = TK * W4 / HS, SO = TK * NEED;
     constexpr int VS = V4 / HS;  // 16-B vectors per slice
-    constexpr int SKR = STG == 1 ? 2 * SK : SK;  // STG 1: two slice buffers
+    constexpr int SKR = STG ? 2 * SK : SK;  // STG 1 / 2: two slice buffers
     static_assert(STG == 0 || (SK * 4) % 1024 == 0, "DMA slices of whole 1-KB wave pieces");
     __shared__ __attribute__((aligned(16))) uint32_t lds[SKR > SO ? SKR : SO];
     constexpr uint32_t AG = 64;  // list slots per wave (8 % of 64 * KPL keys: ~41 at KPL 8)
@@ -842,7 +842,7 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
         const uint64_t base = t * TK;
         uint32_t h[KPL];
         LK_T(t0, tid);
-        if constexpr (STG == 1) {
+        if constexpr (STG == 1 || STG == 2) {
             // DMA ring: slice s in buffer s & 1; a slice is SLI 1-KB wave pieces dealt over the
             // waves (wave w takes pieces w, w + NW, ...), so wave w waits for its own pieces of
             // slice s with a counted vmcnt (its pieces of slice s + 1 may stay in flight), then
@@ -853,10 +853,26 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
             auto dma = [&](int sl) {
 #pragma unroll
                 for (int i = 0; i < PW + 1; i++)
-                    if (i < PW || wv < PX)
-                        __builtin_amdgcn_global_load_lds(
-                            reinterpret_cast<const void*>(src + sl * SLB + (i * NW + wv) * 1024 + lane * 16),
-                            ring + (sl & 1) * SLB + (i * NW + wv) * 1024, 16, 0, 0);
+                    if (i < PW || wv < PX) {
+                        const void* g = reinterpret_cast<const void*>(src + sl * SLB + (i * NW + wv) * 1024 + lane * 16);
+                        uint8_t* l = ring + (sl & 1) * SLB + (i * NW + wv) * 1024;
+                        if constexpr (STG == 1) {
+                            __builtin_amdgcn_global_load_lds(g, l, 16, 0, 0);
+                        } else {
+                            // the same DMA in asm: the compiler does not see an LDS write in flight,
+                            // so it does not drain vmcnt(0) before the next slice's ds_reads (the
+                            // counted waits below order them)
+                            const uint32_t lo = __builtin_amdgcn_readfirstlane(
+                                (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)l);
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is set here; the kernel has no other m0 use
+                            asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                                         :
+                                         : "v"(g), "s"(lo)
+                                         : "memory", "m0");
+#pragma clang diagnostic pop
+                        }
+                    }
             };
             if (tid == 0) nslow_tile = 0;
             dma(0);
@@ -930,34 +946,53 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
         }
         LK_T(t2, h[KPL - 1]);
         __syncthreads();  // sk is reused as so below
-        u32x2 rec[KPL];
-#pragma unroll
-        for (int k = 0; k < KPL; k++)
-            rec[k] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(idx_r, (int)((h[k] >> (bsh + 3u)) * 8u), 0, 0));
-        uint32_t lo[KPL], bc[KPL];
-        u32x4 win[KPL];
-#pragma unroll
-        for (int k = 0; k < KPL; k++) {
-            const uint32_t s4 = ((h[k] >> bsh) & 7u) * 4u;
-            const uint32_t below = rec[k].y & ((1u << s4) - 1u);
-            lo[k] = rec[k].x + __builtin_amdgcn_sad_u8(below & 0x0F0F0F0Fu, 0u,
-                                                       __builtin_amdgcn_sad_u8((below >> 4) & 0x0F0F0F0Fu, 0u, 0u));
-            bc[k] = (rec[k].y >> s4) & 15u;
-            win[k] = load16(lo[k] + wstart(h[k], bc[k]));
-        }
-        LK_T(t3, lo[KPL - 1]);
         uint32_t nag = 0;  // wave-uniform length of this wave's list
+        // LH > 1: the index and window trips run for KPL / LH keys at a time (fewer live
+        // registers in this phase; A/B: RP_LOOKUP_LH)
+        constexpr int KH = KPL / LH;
+        static_assert(KPL % LH == 0, "whole halves");
+#ifdef RP_LK_PROF
+        uint64_t t3 = 0;
+#endif
 #pragma unroll
-        for (int k = 0; k < KPL; k++) {
+        for (int hh = 0; hh < LH; hh++) {
+        if (hh) __builtin_amdgcn_sched_barrier(0);
+        u32x2 rec[KH];
+#pragma unroll
+        for (int kq = 0; kq < KH; kq++) {
+            const int k = hh * KH + kq;
+            rec[kq] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(idx_r, (int)((h[k] >> (bsh + 3u)) * 8u), 0, 0));
+        }
+        uint32_t lo[KH], bc[KH];
+        u32x4 win[KH];
+#pragma unroll
+        for (int kq = 0; kq < KH; kq++) {
+            const int k = hh * KH + kq;
+            const uint32_t s4 = ((h[k] >> bsh) & 7u) * 4u;
+            const uint32_t below = rec[kq].y & ((1u << s4) - 1u);
+            lo[kq] = rec[kq].x + __builtin_amdgcn_sad_u8(below & 0x0F0F0F0Fu, 0u,
+                                                         __builtin_amdgcn_sad_u8((below >> 4) & 0x0F0F0F0Fu, 0u, 0u));
+            bc[kq] = (rec[kq].y >> s4) & 15u;
+            win[kq] = load16(lo[kq] + wstart(h[k], bc[kq]));
+        }
+#ifdef RP_LK_PROF
+        if (hh == 0) {
+            LK_T(t3h, lo[KH - 1]);
+            t3 = t3h;
+        }
+#endif
+#pragma unroll
+        for (int kq = 0; kq < KH; kq++) {
+            const int k = hh * KH + kq;
             uint32_t e[5];
-            ent5v(win[k], e);
+            ent5v(win[kq], e);
             const uint32_t K = ((h[k] & rmask) >> cv.fsh) << cv.ob;
-            const uint32_t w = wstart(h[k], bc[k]);
+            const uint32_t w = wstart(h[k], bc[kq]);
             uint32_t lt = 0;  // in-bucket window entries below the key: the position is lo + w + lt
             bool tie = false;
 #pragma unroll
             for (int j = 0; j < 5; j++) {
-                const bool inb = (uint32_t)j + w < bc[k];
+                const bool inb = (uint32_t)j + w < bc[kq];
                 lt += (inb && e[j] < K);
                 tie |= (inb && e[j] - K < obit);
             }
@@ -975,7 +1010,7 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
 #pragma unroll
                 for (int b = a + 1; b < NEED; b++) dup |= r[a] == r[b];
             const uint32_t kk = tid + k * kLkThreads;
-            bool slow = (tie && !cv.exact) | (lo[k] + 20u > cv.M);
+            bool slow = (tie && !cv.exact) | (lo[kq] + 20u > cv.M);
             const bool under = w > 0u && lt == 0u;  // the key lies before window 1's first entry
             const bool again = !slow && (lt > SPAN || dup || under);
             const uint64_t m = __ballot(again);
@@ -986,10 +1021,10 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
                     // under: search from w - 2 (the position is at most w), guarded when > 0; past
                     // window 1 inside the bucket: search on from w + 5; else the position is known
                     const uint32_t b0 = under ? (w > 2u ? w - 2u : 0u) : w + 5u;
-                    const bool search = under || (lt == 5u && bc[k] > w + 5u);
-                    ag[wv][0][pos] = lo[k] + (search ? b0 : w + lt);
+                    const bool search = under || (lt == 5u && bc[kq] > w + 5u);
+                    ag[wv][0][pos] = lo[kq] + (search ? b0 : w + lt);
                     ag[wv][1][pos] = K;
-                    ag[wv][2][pos] = kk | (bc[k] << 12) | ((uint32_t)search << 16) | ((search ? b0 : 0u) << 17) |
+                    ag[wv][2][pos] = kk | (bc[kq] << 12) | ((uint32_t)search << 16) | ((search ? b0 : 0u) << 17) |
                                      ((uint32_t)(under && b0 > 0u) << 21);
                 } else {
                     slow = true;
@@ -1004,6 +1039,7 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
                 if (sp < kSlowPerTile) slow_list[t * kSlowPerTile + sp] = kk;
             }
         }
+        }  // halves
         LK_T(t4, nag);
         // second windows, one listed key per lane (the list is this wave's own LDS rows)
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1200,9 +1236,12 @@ struct SvcLines {
     uint32_t resp[16];                    // owners[0..W), count at [15]
     uint32_t resp_seq[16];                // [0] = the answered seq
 };
+// With the compact layout built, a key with 1..4 owners wanted takes compact_fix_walk (the
+// index record, the bucket's tokens, the next 8 owners: three dependent trips) instead of the
+// wide binary search and walk.
 template <class View>
-__global__ __launch_bounds__(64) void k_lookup_service(SvcLines* io, View rv, uint32_t last, uint64_t idle_ticks,
-                                                       uint64_t max_ticks) {
+__global__ __launch_bounds__(64) void k_lookup_service(SvcLines* io, View rv, CompactFixView fv, uint32_t use_compact,
+                                                       uint32_t last, uint64_t idle_ticks, uint64_t max_ticks) {
     __shared__ uint32_t kw[kSvcChunks * 15];
     const uint32_t lane = threadIdx.x;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
@@ -1242,8 +1281,15 @@ __global__ __launch_bounds__(64) void k_lookup_service(SvcLines* io, View rv, ui
         uint32_t res[8] = {NIL, NIL, NIL, NIL, NIL, NIL, NIL, NIL};
         int c = 0;
         if (lane == 0) {
-            const uint32_t i = rv.find(fh::hash32(fh::PtrSrc{reinterpret_cast<const uint8_t*>(kw)}, len));
-            c = ring_walk<8>(rv, i, np > 8 ? 8 : np, res);
+            const uint32_t hk = fh::hash32(fh::PtrSrc{reinterpret_cast<const uint8_t*>(kw)}, len);
+            if (use_compact && np >= 1 && np <= 4) {
+                uint32_t r4[4];
+                c = compact_fix_walk(fv, hk, np, r4);
+#pragma unroll
+                for (int q = 0; q < 4; q++) res[q] = r4[q];
+            } else {
+                c = ring_walk<8>(rv, rv.find(hk), np > 8 ? 8 : np, res);
+            }
         }
         // lane 0's row to lanes 0..W-1, then the seq after it (system-scope release)
         uint32_t mine = NIL;
@@ -1785,10 +1831,31 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
         const CompactFixView fv{r.tok.p, r.own.p, r.cidx.p, r.view(), r.M, r.ccb};
         // deferred keys finished by the lean kernel's own workgroups (A/B): only <8, 3, 4>
         const bool fuse = getenv_flag("RP_LOOKUP_FUSEFIX") && lean && half == 4 && kpl == 8 && need == 3 && cv.ablate != 3;
-        const bool stg1 = getenv_flag("RP_LOOKUP_STG") && lean && half == 4 && kpl == 8 && need == 3 && !fuse;
+        const bool stg1 = getenv("RP_LOOKUP_STG") && atoi(getenv("RP_LOOKUP_STG")) == 1 && lean && half == 4 && kpl == 8 &&
+                          need == 3 && !fuse;
+        // RP_LOOKUP_STG=2: asm DMA ring (RP_LOOKUP_STGHS = 4 | 8 key slices; RP_LOOKUP_LH = 1 | 2)
+        const bool stg2 = lean && kpl == 8 && need == 3 && !fuse && getenv("RP_LOOKUP_STG") && atoi(getenv("RP_LOOKUP_STG")) == 2;
+        const int lh = (lean && (half == 4 || stg2) && kpl == 8 && need == 3 && !fuse)
+                           ? (int)env_pos("RP_LOOKUP_LH", stg2 ? 2 : 1) : 1;
+        const int stghs = (int)env_pos("RP_LOOKUP_STGHS", 8);
 #define RP_COMPACT(KPL, NEED)                                                                                  \
     do {                                                                                                        \
-        if (KPL == 8 && NEED == 3 && stg1)                                                                      \
+        if (KPL == 8 && NEED == 3 && stg2 && stghs == 8 && lh == 1)                                             \
+            hipLaunchKernelGGL((k_lookupn_lean<8, 3, 8, false, 2, 1>), dim3(g), dim3(kLkThreads), 0, st, keys,  \
+                               ntiles, cv, out, counts, r.slow.p, r.nslow.p, fv, np);                           \
+        else if (KPL == 8 && NEED == 3 && stg2 && stghs == 8)                                                   \
+            hipLaunchKernelGGL((k_lookupn_lean<8, 3, 8, false, 2, 2>), dim3(g), dim3(kLkThreads), 0, st, keys,  \
+                               ntiles, cv, out, counts, r.slow.p, r.nslow.p, fv, np);                           \
+        else if (KPL == 8 && NEED == 3 && stg2)                                                                 \
+            hipLaunchKernelGGL((k_lookupn_lean<8, 3, 4, false, 2, 2>), dim3(g), dim3(kLkThreads), 0, st, keys,  \
+                               ntiles, cv, out, counts, r.slow.p, r.nslow.p, fv, np);                           \
+        else if (KPL == 8 && NEED == 3 && stg1 && lh == 2)                                                      \
+            hipLaunchKernelGGL((k_lookupn_lean<8, 3, 4, false, 1, 2>), dim3(g), dim3(kLkThreads), 0, st, keys,  \
+                               ntiles, cv, out, counts, r.slow.p, r.nslow.p, fv, np);                           \
+        else if (KPL == 8 && NEED == 3 && lh == 2)                                                              \
+            hipLaunchKernelGGL((k_lookupn_lean<8, 3, 4, false, 0, 2>), dim3(g), dim3(kLkThreads), 0, st, keys,  \
+                               ntiles, cv, out, counts, r.slow.p, r.nslow.p, fv, np);                           \
+        else if (KPL == 8 && NEED == 3 && stg1)                                                                 \
             hipLaunchKernelGGL((k_lookupn_lean<8, 3, 4, false, 1>), dim3(g), dim3(kLkThreads), 0, st, keys,     \
                                ntiles, cv, out, counts, r.slow.p, r.nslow.p, fv, np);                           \
         else if (lean && half == 4 && KPL % 4 == 0 && fuse)                                                     \
@@ -2064,8 +2131,9 @@ static void svc_stop(rp::Ring& r) {
 static void svc_launch(rp::Ring& r, uint32_t last) {
     using namespace rp;
     const uint64_t idle = (uint64_t)r.svc_idle_ms * 100000ull, maxt = 30ull * 100000000ull;  // 100 MHz ticks
-    hipLaunchKernelGGL((k_lookup_service<RingView>), dim3(1), dim3(64), 0, r.svc_st, r.svc_dev, r.view(), last, idle,
-                       maxt);
+    const CompactFixView fv{r.tok.p, r.own.p, r.cidx.p, r.view(), r.M, r.ccb};
+    hipLaunchKernelGGL((k_lookup_service<RingView>), dim3(1), dim3(64), 0, r.svc_st, r.svc_dev, r.view(), fv,
+                       r.compact ? 1u : 0u, last, idle, maxt);
     RP_HIP(hipGetLastError());
     r.svc_running = true;
 }

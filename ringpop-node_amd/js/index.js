@@ -155,14 +155,16 @@ HashRing.prototype.deviceServerCount = function deviceServerCount() {
     return native.ringServerCount(this._h);
 };
 
-// lookup(key) — index.js:145-154 (a batch of one; use lookupBatch for throughput).
+// lookup(key) — index.js:145-154 (one key; use lookupBatch for throughput).
 HashRing.prototype.lookup = function lookup(str) {
-    return this.lookupBatch([str])[0];
+    if (this._customHash) { return this.lookupBatch([str])[0]; }
+    return native.ringLookup1(this._h, str);
 };
 
 // lookupN(key, n) — index.js:157-189.
 HashRing.prototype.lookupN = function lookupN(str, n) {
-    return this.lookupNBatch([str], n)[0];
+    if (this._customHash) { return this.lookupNBatch([str], n)[0]; }
+    return native.ringLookupN1(this._h, str, n | 0);
 };
 
 HashRing.prototype._hashes = function _hashes(keys) {

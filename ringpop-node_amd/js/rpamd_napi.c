@@ -426,6 +426,66 @@ static napi_value js_ring_lookup(napi_env env, napi_callback_info info) {
     return arr;
 }
 
+/* lookup1(h, key) -> name | null and lookupN1(h, key, n) -> [names]: one key, no arrays in
+ * between (RingPop.lookup / lookupN per request, index.js:434-471; the ring service, when on,
+ * answers them without a launch). */
+static int key_utf8(napi_env env, napi_value v, char *stack, size_t cap, char **out, size_t *len) {
+    napi_value str;
+    if (napi_coerce_to_string(env, v, &str) != napi_ok) {
+        napi_throw_type_error(env, NULL, "key is not coercible to string");
+        return -1;
+    }
+    napi_get_value_string_utf8(env, str, NULL, 0, len);
+    *out = *len < cap ? stack : (char *)malloc(*len + 1);
+    size_t got = 0;
+    napi_get_value_string_utf8(env, str, *out, *len + 1, &got);
+    *len = got;
+    return 0;
+}
+
+static napi_value js_ring_lookup1(napi_env env, napi_callback_info info) {
+    ARGS(2);
+    handle_t *h = get_handle(env, argv[0], 1);
+    if (!h) return NULL;
+    rp_ring *r = (rp_ring *)h->p;
+    char stack[256], *k = NULL;
+    size_t len = 0;
+    if (key_utf8(env, argv[1], stack, sizeof stack, &k, &len)) return NULL;
+    uint64_t off[2] = {0, len};
+    uint32_t own = RP_NULL_ID;
+    int rc = rp_ring_lookup(r, k, off, 0, 1, &own);
+    if (k != stack) free(k);
+    RP_OK(rc);
+    return ring_name(env, r, own);
+}
+
+static napi_value js_ring_lookupn1(napi_env env, napi_callback_info info) {
+    ARGS(3);
+    handle_t *h = get_handle(env, argv[0], 1);
+    if (!h) return NULL;
+    rp_ring *r = (rp_ring *)h->p;
+    int32_t nrep = 0;
+    NAPI_OK(napi_get_value_int32(env, argv[2], &nrep));
+    char stack[256], *k = NULL;
+    size_t len = 0;
+    if (key_utf8(env, argv[1], stack, sizeof stack, &k, &len)) return NULL;
+    const uint32_t W = nrep > 1 ? (uint32_t)nrep : 1u;
+    uint32_t own_s[16], *own = W <= 16 ? own_s : (uint32_t *)malloc(4ull * W);
+    uint8_t cnt = 0;
+    uint64_t off[2] = {0, len};
+    int rc = rp_ring_lookupn(r, k, off, 0, 1, nrep, own, &cnt);
+    if (k != stack) free(k);
+    if (rc) {
+        if (own != own_s) free(own);
+        RP_OK(rc);
+    }
+    napi_value arr;
+    napi_create_array_with_length(env, cnt, &arr);
+    for (uint32_t j = 0; j < cnt; j++) napi_set_element(env, arr, j, ring_name(env, r, own[j]));
+    if (own != own_s) free(own);
+    return arr;
+}
+
 /* groupKeys(h, keys[] | Uint32Array hashes) -> {dests: [name|null], groupOff: Uint32Array,
  * perm: Uint32Array}: handleOrProxyAll's _.groupBy(keys, lookup) (index.js:609-667, :616) and
  * lookupKeys (lib/request-proxy/send.js:171-179) on the device. A null dest = the empty ring's
@@ -1164,6 +1224,8 @@ static napi_value init(napi_env env, napi_value exports) {
         {"ringChecksumString", js_ring_checksum_string},
         {"ringServerCount", js_ring_server_count},
         {"ringService", js_ring_service},
+        {"ringLookup1", js_ring_lookup1},
+        {"ringLookupN1", js_ring_lookupn1},
         {"ringTokenCount", js_ring_token_count},
         {"ringHasServer", js_ring_has_server},
         {"ringServers", js_ring_servers},

@@ -16,7 +16,7 @@ pytestmark = pytest.mark.skipif(NODE is None or not os.path.isdir("/usr/include/
                                 reason="node / N-API headers not in this image")
 
 EXPORTS = ["version", "deviceCount", "hash32", "destroy", "ringCreate", "ringAddRemove", "ringChecksum",
-           "ringChecksumString", "ringServerCount", "ringService", "ringTokenCount", "ringHasServer", "ringServers",
+           "ringChecksumString", "ringServerCount", "ringService", "ringLookup1", "ringLookupN1", "ringTokenCount", "ringHasServer", "ringServers",
            "ringOwnerName", "ringLookup", "ringLookupN", "ringLookupNHashes", "ringGroupKeys", "membersCreate", "membersIntern",
            "membersSetLocal", "membersUpdate", "membersSet", "membersChecksum", "membersComputeChecksum",
            "membersChecksumString", "membersDump", "membersDampConfigure", "membersDampLast", "membersDampDecay",

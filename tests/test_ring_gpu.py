@@ -129,6 +129,14 @@ LAYOUTS = {
     # key slices DMA'd global -> LDS (global_load_lds_dwordx4) through a two-buffer ring
     "stg1": {"RP_LOOKUP_STG": "1"},
     "stg1-grid3": {"RP_LOOKUP_STG": "1", "RP_LOOKUP_GRID": "3"},
+    "stg1-lh2": {"RP_LOOKUP_STG": "1", "RP_LOOKUP_LH": "2"},
+    "lh2": {"RP_LOOKUP_LH": "2"},
+    # the same DMA issued from asm (no compiler drain before the slice reads): 8 or 4 key slices,
+    # lookups in two halves or all at once
+    "stg2": {"RP_LOOKUP_STG": "2"},
+    "stg2-grid3": {"RP_LOOKUP_STG": "2", "RP_LOOKUP_GRID": "3"},
+    "stg2-lh1": {"RP_LOOKUP_STG": "2", "RP_LOOKUP_LH": "1"},
+    "stg2-hs4": {"RP_LOOKUP_STG": "2", "RP_LOOKUP_STGHS": "4"},
     # window 1 at the bucket start (the round-2 placement) instead of the predicted start
     "wpred0": {"RP_LOOKUP_WPRED": "0"},
     "lean-kpl4": {"RP_LOOKUP_HALF": "0", "RP_LOOKUP_KPL": "4"},
@@ -142,7 +150,8 @@ LAYOUTS = {
 
 def set_layout(monkeypatch, layout):
     for k in ("RP_RING_WIDE", "RP_RING_NOWINDOW", "RP_RING_LAYOUT", "RP_LOOKUP_KPL", "RP_LOOKUP_LEAN", "RP_LOOKUP_HALF",
-              "RP_LOOKUP_GRID", "RP_LOOKUP_FUSEFIX", "RP_LOOKUP_WPRED"):
+              "RP_LOOKUP_GRID", "RP_LOOKUP_FUSEFIX", "RP_LOOKUP_WPRED", "RP_LOOKUP_STG", "RP_LOOKUP_LH",
+              "RP_LOOKUP_STGHS"):
         monkeypatch.delenv(k, raising=False)
     for k, v in LAYOUTS[layout].items():
         monkeypatch.setenv(k, v)
@@ -284,7 +293,7 @@ def test_device_resident_lookupn_c1_vs_oracle(gpu, orc, layout, monkeypatch):
     assert np.array_equal(d_l.cpu().numpy().view(np.uint32), w[:, 0])
 
 
-@pytest.mark.parametrize("layout", ["compact", "round1", "lean-kpl4", "half-kpl8", "fusefix", "wpred0"])
+@pytest.mark.parametrize("layout", ["compact", "round1", "lean-kpl4", "half-kpl8", "fusefix", "wpred0", "stg2", "stg1"])
 def test_c2_full_size_properties(gpu, orc, layout, monkeypatch):
     set_layout(monkeypatch, layout)
     # C2: 10k servers x 100 points (~1M tokens); 2^24 keys on device; size-independent
@@ -335,7 +344,7 @@ def test_edge_cases(gpu):
 
 @pytest.mark.parametrize("layout", ["compact", "compact-kpl1", "compact-kpl3", "compact-kpl8", "round1",
                                     "round1-kpl1", "half", "half-kpl2", "half-kpl8", "quarter-kpl8", "lean-kpl4", "window",
-                                    "fusefix", "wpred0"])
+                                    "fusefix", "wpred0", "stg2", "stg2-hs4"])
 @pytest.mark.parametrize("nserv,R", [(1, 100), (2, 2000), (3, 700), (5, 5), (40, 1), (64, 3)])
 def test_window_kernel_slow_paths_vs_oracle(gpu, orc, nserv, R, layout, monkeypatch):
     """Rings that force the window kernels' exact fallbacks: long buckets, runs of one owner,

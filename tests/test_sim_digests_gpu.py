@@ -4,7 +4,7 @@ maxPiggybackCount, the cumulative stats and the convergence round must equal the
 (tests/golden/sim_digests.json, made by tests/golden/make_sim_digests.py; the oracle itself is
 pinned to the reference by tests/golden/sim_golden.json).
 
-C5 runs once on one GPU (~170 GB of view rows) and once as 8 shard handles in one process
+C5 runs once on one GPU (210 GB of view rows: 21 B per member per view) and once as 8 shard handles in one process
 exchanging messages (the per-GPU layout of an 8-GPU run)."""
 import hashlib
 

@@ -41,6 +41,11 @@ def main():
         "compact-kpl1/lookupN3": ({"RP_LOOKUP_LEAN": "0", "RP_LOOKUP_KPL": "1"}, 3),
         "lean-kpl4/lookupN3": ({"RP_LOOKUP_HALF": "0", "RP_LOOKUP_KPL": "4"}, 3),
         "default/lookupN3": ({}, 3),
+        "stg1/lookupN3": ({"RP_LOOKUP_STG": "1"}, 3),
+        "lh2/lookupN3": ({"RP_LOOKUP_LH": "2"}, 3),
+        "stg2/lookupN3": ({"RP_LOOKUP_STG": "2"}, 3),
+        "stg2-lh1/lookupN3": ({"RP_LOOKUP_STG": "2", "RP_LOOKUP_LH": "1"}, 3),
+        "stg2-hs4/lookupN3": ({"RP_LOOKUP_STG": "2", "RP_LOOKUP_STGHS": "4"}, 3),
         "lean-kpl2/lookupN3": ({"RP_LOOKUP_LEAN": "1", "RP_LOOKUP_KPL": "2"}, 3),
         "half-kpl4/lookupN3": ({"RP_LOOKUP_HALF": "2", "RP_LOOKUP_KPL": "4"}, 3),
         "half-kpl8/lookupN3": ({"RP_LOOKUP_HALF": "2", "RP_LOOKUP_KPL": "8"}, 3),
@@ -67,7 +72,7 @@ def main():
     }
     if a.only:
         variants = {k: v for k, v in variants.items() if k in a.only.split(",")}
-    knobs = ("RP_LOOKUP_HALF", "RP_LOOKUP_LEAN", "RP_LOOKUP_KPL", "RP_RING_LAYOUT", "RP_LOOKUP_ABLATE", "RP_RING_WIDE", "RP_LOOKUP_GRID", "RP_LOOKUP_OCC")
+    knobs = ("RP_LOOKUP_HALF", "RP_LOOKUP_LEAN", "RP_LOOKUP_KPL", "RP_RING_LAYOUT", "RP_LOOKUP_ABLATE", "RP_RING_WIDE", "RP_LOOKUP_GRID", "RP_LOOKUP_OCC", "RP_LOOKUP_STG", "RP_LOOKUP_LH", "RP_LOOKUP_STGHS")
     times = {k: [] for k in variants}
     digests = {}
     for r in range(a.rounds + 1):
