@@ -379,8 +379,8 @@ __global__ __launch_bounds__(1024) void k_fold_ovf(const uint32_t* __restrict__ 
 // their batch index), then one workgroup folds one bucket with the bucket's 128 KB of rows
 // resident in its XCD's L2, so the row accesses and the rank counters stop being random HBM /
 // memory-side atomics (k_link's one atomic per change was half of a 2^22 batch). Three launches:
-//   k_bk_scatter a 4,096-change tile sorts its 16-B records {id, batch index | status << 30,
-//                incarnation} by bucket in LDS and stores them as one contiguous run at
+//   k_bk_scatter a 4,096-change tile sorts its 12-B records {bucket-local id, tile-relative
+//                index, status; incarnation} by bucket in LDS and stores them as one contiguous run at
 //                recs + tile * kBkTile (whole lines); seg[bucket][tile] = the bucket's segment
 //                of that run (start << 16 | length). No global count pass or scan: the fold
 //                walks a bucket's segments of every tile.
@@ -391,9 +391,9 @@ __global__ __launch_bounds__(1024) void k_fold_ovf(const uint32_t* __restrict__ 
 //                batch index in LDS and folded by one lane; an address with more than kSlots + 1
 //                changes (or a bucket whose repeated changes overflow the LDS list) is marked
 //                for the overflow fold (k_fold_ovf / k_ovf_len, as on the grouped path). The
-//                1-B result goes to resid[id] (coalesced), or to resj[batch index] for an
-//                address with repeated changes (resid holds kResRep)
-//   k_bk_gather  applied per change in batch order, from resid[ids[j]] (4 MB, L2-resident),
+//                result goes to a 2-bit per-id map res2 (coalesced), or to resj[batch index] for
+//                an address with repeated changes (res2 holds kRes2Rep)
+//   k_bk_gather  applied per change in batch order, from res2[ids[j]] (1 MB, L2-resident),
 //                four changes per lane (the new status / incarnation outputs are copied from the
 //                input by k_bk_scatter; the fold rewrites the local overrides)
 #ifndef RP_BK_BITS
@@ -411,7 +411,11 @@ static_assert(kBkDup <= 1024, "k_bk_fold: one repeated change per thread, 10-bit
 static_assert(kBk % kBkFT == 0 && kBkFT % 64 == 0, "k_bk_fold: whole ids per lane");
 constexpr uint32_t kBkMaxBuckets = 2048;               // (LDS of the scatter tiles): 8M ids
 constexpr uint8_t kResLocal = 4;                       // result: the local override rewrote (status, inc)
-constexpr uint8_t kResRep = 8;                         // resid: repeated changes, results in resj
+constexpr uint8_t kResRep = 8;                         // repeated changes, results in resj
+static_assert(RP_BK_BITS + 12 <= 30, "bucket-local id + tile-relative index + status in 32 bits");
+// the per-id result the gather reads, 2 bits (16 ids per word): 0 / 1 / 2 = applied, 3 = repeated
+// changes (the results are in resj)
+constexpr uint32_t kRes2Rep = 3;
 
 // seg layout: groups of 16 buckets, then tile, then bucket (one 64-B line per (group, tile)), so
 // a scatter tile writes whole lines and the 16 buckets that share a line fold on one XCD
@@ -419,20 +423,28 @@ __host__ __device__ __forceinline__ uint64_t seg_at(uint32_t b, uint32_t t, uint
     return ((uint64_t)(b >> 4) * ntiles + t) * 16 + (b & 15u);
 }
 
-struct alignas(16) BRec {
-    uint32_t id;
-    uint32_t js;  // batch index | status << 30
-    int64_t inc;
+// A staged change, 12 B: {bucket-local id | tile-relative batch index << kBkBits | status << 30,
+// incarnation lo, hi}. The tile is the run it sits in (the fold knows it from the segment), so
+// the batch index is tile * kBkTile + the relative index: no 16-B record with a full id and index.
+struct BRec {
+    uint32_t x;
+    uint32_t lo, hi;
 };
+static_assert(sizeof(BRec) == 12, "12-byte records");
+constexpr uint32_t kBkRelBits = 12;
+static_assert((1u << kBkRelBits) >= kBkTile, "tile-relative batch index");
+__device__ __forceinline__ uint32_t brec_x(uint32_t il, uint32_t rel, uint32_t st) {
+    return il | (rel << kBkBits) | (st << 30);
+}
 
 __global__ __launch_bounds__(kBkST) void k_bk_scatter(const uint32_t* __restrict__ ids, const uint8_t* __restrict__ chs,
                                                     const int64_t* __restrict__ chi, uint32_t k, uint32_t nb,
                                                     uint32_t ntiles, BRec* __restrict__ recs,
                                                     uint32_t* __restrict__ seg, uint8_t* __restrict__ nst,
                                                     int64_t* __restrict__ ninc) {
-    __shared__ uint4 stage[kBkTile];
+    __shared__ __attribute__((aligned(16))) uint32_t stage[kBkTile * 3];
     __shared__ uint32_t h[kBkMaxBuckets], s_w[kBkST / 64];
-    __shared__ uint16_t ls[kBkMaxBuckets];  // <= 4,096 (76 KB in all: two tiles per CU)
+    __shared__ uint16_t ls[kBkMaxBuckets];  // <= 4,096 (60 KB in all: two tiles per CU)
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t t = blockIdx.x, base = t * kBkTile;
     const uint32_t n = k - base < kBkTile ? k - base : kBkTile;
@@ -484,14 +496,19 @@ __global__ __launch_bounds__(kBkST) void k_bk_scatter(const uint32_t* __restrict
     for (uint32_t q = 0; q < PER; q++) {
         const uint32_t i = tid + q * kBkST;
         if (i < n) {
-            const uint32_t j = base + i, b = idv[q] >> kBkBits;
+            const uint32_t b = idv[q] >> kBkBits, e = 3u * (ls[b] + rk[q]);
             const int64_t inc8 = incv[q];
-            stage[ls[b] + rk[q]] = uint4{idv[q], j | ((uint32_t)(stv[q] & 3u) << 30), (uint32_t)(uint64_t)inc8,
-                                         (uint32_t)((uint64_t)inc8 >> 32)};
+            stage[e] = brec_x(idv[q] & (kBk - 1u), i, stv[q] & 3u);
+            stage[e + 1] = (uint32_t)(uint64_t)inc8;
+            stage[e + 2] = (uint32_t)((uint64_t)inc8 >> 32);
         }
     }
     __syncthreads();
-    for (uint32_t q = tid; q < n; q += kBkST) *reinterpret_cast<uint4*>(recs + base + q) = stage[q];
+    // the tile's run: n records of 12 B at recs + tile * kBkTile (16-B stores; the tile's run
+    // starts 16-B aligned, and its padded tail is never read)
+    uint4* d4 = reinterpret_cast<uint4*>(recs + (uint64_t)t * kBkTile);
+    const uint4* s4 = reinterpret_cast<const uint4*>(stage);
+    for (uint32_t q = tid; q < (3u * n + 3u) / 4u; q += kBkST) d4[q] = s4[q];
 }
 
 // One change on a member row (the step of fold_address without damp scoring): returns applied
@@ -529,9 +546,10 @@ __device__ __forceinline__ void bk_local(const FoldArgs& A, uint32_t j) {
 // list that would overflow) to the overflow fold.
 __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs, const uint32_t* __restrict__ seg,
                                                   uint32_t ntiles, uint32_t nb, FoldArgs A,
-                                                  uint8_t* __restrict__ resid, uint8_t* __restrict__ resj,
+                                                  uint32_t* __restrict__ res2, uint8_t* __restrict__ resj,
                                                   uint32_t* __restrict__ ovf, uint32_t* __restrict__ part) {
     __shared__ uint32_t cnt[kBk], fjs[kBk];
+    __shared__ uint8_t rcode[kBk];  // the bucket's 2-bit result codes, packed 16 to a word at the end
     __shared__ int64_t finc[kBk];
     // repeated changes: key (address << 40 | batch index << 10 | entry), the entry's status and
     // incarnation beside it, so the per-address fold reads only LDS
@@ -558,23 +576,24 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
     for (uint32_t t = tid; t < ntiles; t += kBkFT) {
         const uint32_t e = seg[seg_at(b, t, ntiles)], n = e & 0xFFFFu;
         const BRec* r = recs + (uint64_t)t * kBkTile + (e >> 16);
+        const uint32_t jt = t * kBkTile;  // the tile's first batch index
         for (uint32_t i0 = 0; i0 < n; i0 += 8) {
-            uint4 v[8];
+            BRec v[8];
 #pragma unroll
-            for (uint32_t q = 0; q < 8; q++)
-                v[q] = i0 + q < n ? *reinterpret_cast<const uint4*>(r + i0 + q) : uint4{0, 0, 0, 0};
+            for (uint32_t q = 0; q < 8; q++) v[q] = i0 + q < n ? r[i0 + q] : BRec{0, 0, 0};
 #pragma unroll
             for (uint32_t q = 0; q < 8; q++)
                 if (i0 + q < n) {
-                    const uint32_t il = v[q].x - id0;
-                    const int64_t in = (int64_t)(((uint64_t)v[q].w << 32) | v[q].z);
+                    const uint32_t il = v[q].x & (kBk - 1u);
+                    const uint32_t js = (jt + ((v[q].x >> kBkBits) & (kBkTile - 1u))) | (v[q].x & 0xC0000000u);
+                    const int64_t in = (int64_t)(((uint64_t)v[q].hi << 32) | v[q].lo);
                     const uint32_t old = atomicAdd(&cnt[il], 1u);
                     if (old == 0) {
-                        fjs[il] = v[q].y;
+                        fjs[il] = js;
                         finc[il] = in;
                     } else {
                         const uint32_t d = atomicAdd(&s_nd, 1u);
-                        if (d < kBkDup) dput(d, il, v[q].y, in);
+                        if (d < kBkDup) dput(d, il, js, in);
                     }
                 }
         }
@@ -617,9 +636,19 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
                 *ovf = 1u;
             }
         }
-        resid[id] = r;
+        rcode[q] = r == kResRep ? (uint8_t)kRes2Rep : (uint8_t)(r & 3u);
     }
     __syncthreads();
+    if (tid < kBk / 16) {  // 16 codes to a word: the gather's map is 1 MB at 2^22 ids, not 4 MB
+        const uint4 c4 = reinterpret_cast<const uint4*>(rcode)[tid];
+        const uint32_t c[4] = {c4.x, c4.y, c4.z, c4.w};
+        uint32_t w = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int bb = 0; bb < 4; bb++) w |= ((c[i] >> (8 * bb)) & 3u) << (2 * (4 * i + bb));
+        res2[(id0 >> 4) + tid] = w;
+    }
     if (listed && nd) {  // repeated addresses: sort by (address, batch index), fold per address
         // rank sort (nd <= kBkDup <= kBkFT: one key per thread; the wave reads each key as a broadcast)
         const uint64_t my = tid < nd ? dk[tid] : 0;
@@ -661,17 +690,18 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
     }
 }
 
-// applied per change in batch order from resid[ids[j]] (4 MB, L2-resident) or resj[j]. V = 4:
-// four consecutive changes per lane (16-B id loads, 4-B stores; the host checks the alignment).
+// applied per change in batch order from the 2-bit map res2 (1 MB at 2^22 ids, L2-resident) or
+// resj[j]. V = 4: four consecutive changes per lane (16-B id loads, 4-B stores; the host checks
+// the alignment).
 template <uint32_t V>
-__global__ __launch_bounds__(256) void k_bk_gather(const uint32_t* __restrict__ ids, const uint8_t* __restrict__ resid,
+__global__ __launch_bounds__(256) void k_bk_gather(const uint32_t* __restrict__ ids, const uint32_t* __restrict__ res2,
                                                    const uint8_t* __restrict__ resj, uint32_t k,
                                                    uint8_t* __restrict__ applied) {
     const uint32_t j0 = (blockIdx.x * blockDim.x + threadIdx.x) * V;
     if (j0 >= k) return;
     auto one = [&](uint32_t j, uint32_t id) -> uint32_t {
-        const uint8_t r = resid[id];
-        return (r == kResRep ? resj[j] : r) & 3u;
+        const uint32_t r = (res2[id >> 4] >> (2u * (id & 15u))) & 3u;
+        return r == kRes2Rep ? resj[j] & 3u : r;
     };
     if (V == 4 && j0 + 4 <= k) {
         const uint4 iv = *reinterpret_cast<const uint4*>(ids + j0);
@@ -1061,7 +1091,8 @@ struct Members {
     // = 0 | 1 overrides the size rule)
     DevBuf<uint32_t> bk_seg;
     DevBuf<BRec> bk_recs;
-    DevBuf<uint8_t> bk_resid, bk_resj;
+    DevBuf<uint32_t> bk_res2;  // the bucket fold's 2-bit per-id results (k_bk_gather)
+    DevBuf<uint8_t> bk_resj;
     static constexpr uint32_t kBkMin = 1u << 19;
     bool use_bucket_fold(uint32_t k, uint32_t nb) const {
         if (damp_on || nb > kBkMaxBuckets || k >= (1u << 30) || !grouped_fold) return false;
@@ -1177,21 +1208,21 @@ struct Members {
             const uint32_t ntiles = (k + kBkTile - 1) / kBkTile;
             bk_seg.reserve((uint64_t)((nb + 15) / 16) * 16 * ntiles);
             bk_recs.reserve((uint64_t)ntiles * kBkTile);
-            bk_resid.reserve((uint64_t)nb * kBk);
+            bk_res2.reserve((uint64_t)nb * kBk / 16);
             bk_resj.reserve(k);
             g_part.reserve(nb + 1);
             hipLaunchKernelGGL(k_bk_scatter, dim3(ntiles), dim3(kBkST), 0, s, ids, chs, chi, k, nb, ntiles, bk_recs.p,
                                bk_seg.p, nst, ninc);
             hipLaunchKernelGGL(k_bk_fold, dim3((nb + 7) / 8 * 8), dim3(kBkFT), 0, s, bk_recs.p, bk_seg.p, ntiles, nb, A,
-                               bk_resid.p, bk_resj.p, ovf, g_part.p);
+                               bk_res2.p, bk_resj.p, ovf, g_part.p);
             if (applied) {
                 const bool v4 = ((uintptr_t)ids & 15) == 0 && ((uintptr_t)applied & 3) == 0;
                 if (v4)
                     hipLaunchKernelGGL(k_bk_gather<4>, dim3(grid_for((k + 3) / 4, 256, 1u << 30)), dim3(256), 0, s,
-                                       ids, bk_resid.p, bk_resj.p, k, applied);
+                                       ids, bk_res2.p, bk_resj.p, k, applied);
                 else
                     hipLaunchKernelGGL(k_bk_gather<1>, dim3(grid_for(k, 256, 1u << 30)), dim3(256), 0, s, ids,
-                                       bk_resid.p, bk_resj.p, k, applied);
+                                       bk_res2.p, bk_resj.p, k, applied);
             }
             RP_HIP(hipGetLastError());
             if (build && nt.size()) {
