@@ -252,14 +252,15 @@ def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=512, warmup=3, 
         ck = m.checksums()[-1]  # the last batch's checksum (gathered once, after the timed region)
     out = {"workload": "C3: %d-member table, %d updates/batch (1%% repeated addresses), fold + 1 checksum "
                        "per batch%s" % (n, k, ", %d replicas, batch-strided checksums" % world if world > 1 else ""),
-           "n_gpus": world, "scaling": "strong",
+           "n_gpus": world, "scaling": "strong", "batches": batches,
            "updates_per_s": k * batches / dt, "ms_per_batch": dt * 1e3 / batches,
            "gpu_ms_per_batch": e0.elapsed_time(e1) / batches, "checksum": ck,
            "note": "every batch applies most of its updates and its checksum string is built after it; the "
                    "strings' serial farmhash chains run in groups of 128 side by side (one workgroup each) on a "
-                   "side stream, overlapping the next batches' folds (256 slots within a 1 GiB pool, "
+                   "side stream, overlapping the next batches' folds (4 groups of 128 slots within a 2 GiB pool, "
                    "RP_MEMBERS_CK_BYTES); the last batch's checksum is read inside the timed region, so "
-                   "the final group's chains are in the time"}
+                   "the final group's chains (one serial chain's latency, ~4.4 ms) are in the time: over "
+                   "%d batches that drain adds ~%.1f us per batch" % (batches, 4400.0 / batches)}
     if world > 1 or not extras:  # the fold-only and large-batch legs are per-replica: rank 0's one-GPU run
         m.close()
         return out
@@ -560,6 +561,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-merge", action="store_true")
+    ap.add_argument("--merge-batches", type=int, default=2048,
+                    help="C3 update batches in the timed stream (the final group's chains, one 4.4 ms chain latency, "
+                         "are inside it: 2.1 us per batch at 2048, 8.6 at 512)")
     ap.add_argument("--no-wire", action="store_true")
     ap.add_argument("--no-api", action="store_true", help="skip the node per-call latency leg")
     ap.add_argument("--sim-n", type=int, default=10000, help="C4 members, one GPU (0: skip)")
@@ -646,7 +650,8 @@ def main():
     torch.cuda.empty_cache()
     merge = None
     if not args.no_merge:
-        merge = merge_bench(rpa, torch, local, world=world, dist=dist, reduce_max=reduce_max)
+        merge = merge_bench(rpa, torch, local, batches=args.merge_batches, world=world, dist=dist,
+                            reduce_max=reduce_max)
     sim5 = sim_bench(rpa, torch, dist, local, n=args.sim5_n, world=world, reduce_max=reduce_max) \
         if args.sim5_n else None
     if rank == 0:

@@ -1056,7 +1056,8 @@ struct Members {
     // RP_MEMBERS_CK_BYTES (default 1 GiB of HBM), at most kMaxSlots. Groups of 128: a launch of
     // 128 chains (one workgroup each) takes about as long as one of 64, and the folds and string
     // builds of the next 128 batches take about as long (C3: 1.00-1.07 G updates/s against 0.86
-    // with groups of 64, 0.44 with 32; RP_MEMBERS_GROUP_SLOTS overrides).
+    // with groups of 64, 0.44 with 32; RP_MEMBERS_GROUP_SLOTS overrides). The pool is 2 GiB by
+    // default (RP_MEMBERS_CK_BYTES): 4 groups at C3.
     static constexpr uint32_t kMaxSlots = 1024, kGroupSlots = 128, kMaxGroups = 4;
     uint32_t nslots = 1, group_slots = 1, ngroups = 1;
     DevBuf<uint8_t> ck_buf;   // nslots strings of slot_bytes
@@ -1314,7 +1315,10 @@ struct Members {
             for (auto& b : group_busy) b = false;
             cur_group = 0;
             ck_buf.release();
-            const uint64_t budget = env_pos("RP_MEMBERS_CK_BYTES", 1ull << 30);
+            // 2 GiB of HBM: at C3's 3.6 MB strings, 4 groups of 128 slots, so the folds never wait
+            // for a group's previous chains (1 GiB / 2 groups: 51.4 against 45.2 us per batch over
+            // a 512-batch stream, profiles/r04/r04e/)
+            const uint64_t budget = env_pos("RP_MEMBERS_CK_BYTES", 2ull << 30);
             nslots = (uint32_t)std::min<uint64_t>(kMaxSlots, std::max<uint64_t>(1, budget / need));
             const uint32_t gmax = (uint32_t)env_pos("RP_MEMBERS_GROUP_SLOTS", kGroupSlots);  // A/B: chains per launch
             group_slots = std::max<uint32_t>(1, std::min<uint32_t>(gmax, nslots / 2));

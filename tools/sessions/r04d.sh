@@ -11,3 +11,6 @@ python3 -c "
 import json
 for l in open('$O/fold_ab.jsonl'):
     d=json.loads(l); print(d['label'].split('/')[-1], round(d['big']['ms_mean'],4), round(d['big']['ms_p50'],4), d['big']['applied_last'])"
+timeout -k 10 300 rocprofv3 --kernel-trace -d $O/c3 -o run -- python3 -u tools/c3_timeline.py run 300 > $O/c3_run.log 2>&1 || { echo c3 run failed; tail -20 $O/c3_run.log; exit 1; }
+tail -2 $O/c3_run.log
+python3 tools/c3_timeline.py show $O/c3/run_results.db > $O/c3_show.txt 2>&1; tail -45 $O/c3_show.txt
