@@ -1162,6 +1162,12 @@ __global__ __launch_bounds__(256) void k_pass1(SimDev S, const uint32_t* __restr
 // over a shared LDS ring of the base string. A view with more deviated pieces than its list holds,
 // or a wave whose lanes drift further apart than the ring allows, uses the L2 path
 // (lane_checksum).
+// Fixup statistics of k_ck_lanes (diagnostics only, -DRP_CKL_STAT; printed per launch under
+// RP_CKL_STAT_PRINT): [0] wave-groups, [1] wave-groups that ran a fixup, [2] lane-groups with a
+// fixup, [3] active lane-groups, [4] waves
+#ifdef RP_CKL_STAT
+__device__ unsigned long long g_ckl_stat[8];
+#endif
 __global__ __launch_bounds__(256) void k_ck_lanes(SimDev S, const uint32_t* __restrict__ sel,
                                                   const uint32_t* __restrict__ nsel) {
     __shared__ __attribute__((aligned(16))) uint32_t rings[4][kRingW + 24];
@@ -1387,6 +1393,17 @@ __global__ __launch_bounds__(256) void k_ck_lanes(SimDev S, const uint32_t* __re
                 if ((uint32_t)j < ng) chunk(j);
             pin();
         }
+#ifdef RP_CKL_STAT
+        {
+            const uint64_t fx = __ballot(ng1 && q1 + 20 * ng1 > C.pos), av = __ballot(act && ng1);
+            if (lane == 0 && av) {
+                atomicAdd(&g_ckl_stat[0], 1ull);
+                atomicAdd(&g_ckl_stat[1], fx ? 1ull : 0ull);
+                atomicAdd(&g_ckl_stat[2], (unsigned long long)__popcll(fx));
+                atomicAdd(&g_ckl_stat[3], (unsigned long long)__popcll(av));
+            }
+        }
+#endif
         if (__builtin_expect(ng1 && q1 + 20 * ng1 > C.pos, 0) && S.ck_ablate == 0) fixup(q1, ng1, nw, n5, n6, n7);
 #pragma unroll
         for (int j = 0; j < 4; j++) {
@@ -3472,6 +3489,18 @@ struct Sim {
             hipLaunchKernelGGL(k_ck_pc<3>, dim3(groups), dim3(256), 0, st, d, sel, nsel);
         else
             hipLaunchKernelGGL(k_ck_lanes, dim3(grid_for(NL, 256, 1u << 20)), dim3(256), 0, st, d, sel, nsel);
+#ifdef RP_CKL_STAT
+        if (getenv("RP_CKL_STAT_PRINT")) {
+            unsigned long long v[8];
+            RP_HIP(hipStreamSynchronize(st));
+            RP_HIP(hipMemcpyFromSymbol(v, HIP_SYMBOL(g_ckl_stat), sizeof v));
+            if (v[0])
+                fprintf(stderr, "[rp] k_ck_lanes: %llu wave-groups, %.1f %% with a fixup; lane-groups %.2f %% with one\n",
+                        v[0], 100.0 * v[1] / v[0], v[3] ? 100.0 * v[2] / v[3] : 0.0);
+            memset(v, 0, sizeof v);
+            RP_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_ckl_stat), v, sizeof v));
+        }
+#endif
         d.p1_pre = 0;
         if (twins) hipLaunchKernelGGL(k_twin_copy, dim3(grid_for(NL, 256)), dim3(256), 0, st, d, twin_of.p);
         RP_HIP(hipGetLastError());
