@@ -655,6 +655,10 @@ constexpr uint32_t kWBuf = 8192;  // message bytes staged per wave (longer: the 
 constexpr uint32_t kWTok = 2048;  // quotes + structural characters per message
 constexpr uint32_t kWLvl = 1024;  // array-level tokens (records + separators)
 constexpr int kDecWaves = 4;
+#ifndef RP_WIRE_MEMBERS
+#define RP_WIRE_MEMBERS 0
+#endif
+constexpr bool kWaveMembers = RP_WIRE_MEMBERS != 0;  // records parsed a lane per member (-DRP_WIRE_MEMBERS=1; A/B)
 
 struct WaveLds {
     uint32_t buf[kWBuf / 4 + 2];
@@ -898,6 +902,169 @@ __device__ bool wave_record(const WaveMsg& M, const Names& nm, uint64_t base, ui
     return f.alen != 0 && f.st != 0xFF && has_inc;
 }
 
+// The records of the changes array [arr, arr_end] (nrec <= 64, record depth d + 1) parsed member
+// by member, a lane per member (round 4): a message's ~6 members x 32 records run on all 64 lanes
+// in about three passes instead of one lane walking each record's members one after another, and
+// the address / source name lookups then run one per lane. true: all nrec records parsed into
+// out[]. false: the caller runs wave_record per record instead (which accepts or hands the message
+// to the thread parser) — on anything it would take a different route for: a nested member value,
+// a repeated known key (last one wins), more boundary tokens than fit, any record it would reject.
+// LDS: the caller's level-list scan leaves the nb boundary tokens (record opens, member
+// separators, record closes) at the top of W.lvl, below nothing of the level list (W.lvl[0,
+// 2 nrec - 1), which wave_record needs); the per-record fields go over the W.dep bytes, the array
+// being known to hold no nested value (wave_record reads W.dep only for those).
+__device__ bool wave_records_mp(const WaveMsg& M, WaveLds& W, const Names& nm, uint64_t base, uint32_t nb,
+                                uint32_t nrec, RecF* __restrict__ out, uint32_t lane) {
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const uint16_t* BT = W.lvl + kWLvl - 1;  // boundary i at BT[-i]
+    if (nb > kWLvl || nb < 2) return false;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // per-record fields over the W.dep bytes (1,984 of its 2,048)
+    uint8_t* R = reinterpret_cast<uint8_t*>(W.dep);
+    int64_t* r_inc = reinterpret_cast<int64_t*>(R);
+    int64_t* r_sinc = reinterpret_cast<int64_t*>(R + 512);
+    uint32_t* r_aref = reinterpret_cast<uint32_t*>(R + 1024);  // address offset | length << 16
+    uint32_t* r_sref = reinterpret_cast<uint32_t*>(R + 1280);  // source offset | length << 16, then its id
+    uint16_t* r_id = reinterpret_cast<uint16_t*>(R + 1536);
+    uint8_t* r_st = R + 1664;
+    uint32_t* r_fl = reinterpret_cast<uint32_t*>(R + 1728);  // bit k: known key k seen
+    if (lane < nrec) {
+        r_fl[lane] = 0;
+        r_st[lane] = 0xFF;
+        r_aref[lane] = 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // members: boundary i that is a '{' or ',' starts one; its value ends at boundary i + 1
+    const uint16_t* P = W.pos;
+    const uint8_t* TC = W.tc;
+    uint32_t recbase = 0;
+    bool bad = false;
+    for (uint32_t i0 = 0; i0 < nb; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        const bool in = i < nb;
+        const uint32_t bt = in ? BT[-(int32_t)i] : 0u;
+        const uint8_t bc = in ? TC[bt] : (uint8_t)'}';
+        const uint64_t mo = __ballot(in && bc == '{');
+        const int32_t rec = (int32_t)(recbase + (uint32_t)__popcll(mo & lt)) + ((in && bc == '{') ? 0 : -1);
+        recbase += (uint32_t)__popcll(mo);
+        if (!in || bc == '}') continue;
+        if (i + 1 >= nb || rec < 0 || (uint32_t)rec >= nrec) {
+            bad = true;
+            continue;
+        }
+        const uint32_t t = bt + 1, sep = BT[-(int32_t)i - 1];
+        if (t + 2 >= sep) {  // {} , {,} ...: no key
+            bad = true;
+            continue;
+        }
+        const uint32_t pm = P[t - 1], p0 = P[t], p1 = P[t + 1], p2 = P[t + 2], p3 = P[t + 3], p4 = P[t + 4];
+        const uint8_t c0 = TC[t], c1 = TC[t + 1], c2 = TC[t + 2], c3 = TC[t + 3];
+        if (!((c0 == '"') & (c1 == '"') & (c2 == ':')) || !M.clean(pm, p0) || !M.clean(p1, p2)) {
+            bad = true;
+            continue;
+        }
+        const uint8_t* kp = M.b + p0 + 1;
+        const uint32_t kl = p1 - p0 - 1;
+        const int kind = kl == 7 ? (key_eq(kp, "address") ? 1 : 0)
+                       : kl == 6 ? (key_eq(kp, "source") ? 2 : key_eq(kp, "status") ? 3 : 0)
+                       : kl == 2 ? (key_eq(kp, "id") ? 4 : 0)
+                       : kl == 17 ? (key_eq(kp, "incarnationNumber") ? 5 : 0)
+                       : kl == 23 ? (key_eq(kp, "sourceIncarnationNumber") ? 6 : 0) : 0;
+        uint32_t nx;
+        uint32_t vs = 0, vl = 0;  // a string value's offset and length
+        int64_t x = 0;
+        if (kind >= 1 && kind <= 4) {
+            if (c3 != '"' || !M.clean(p2, p3)) {
+                bad = true;
+                continue;
+            }
+            vs = p3 + 1;
+            vl = p4 - vs;
+            nx = t + 5;
+        } else if (kind >= 5) {
+            if (!M.int_tok(t + 2, x)) {
+                bad = true;
+                continue;
+            }
+            nx = t + 3;
+        } else {
+            nx = M.skip(t + 3);  // a string or a scalar (nested values were refused above)
+        }
+        if (nx != sep || (TC[nx - 1] != ':' && !M.clean(P[nx - 1], P[nx]))) {
+            bad = true;
+            continue;
+        }
+        if (kind) {
+            const uint32_t old = atomicOr(&r_fl[rec], 1u << kind);
+            if (old & (1u << kind)) {  // a repeated key: the thread parser keeps the last one
+                bad = true;
+                continue;
+            }
+        }
+        if (kind == 1) {
+            r_aref[rec] = vs | (vl << 16);
+        } else if (kind == 2) {
+            r_sref[rec] = vs | (vl << 16);
+        } else if (kind == 3) {
+            const uint8_t st = status_code(M.b + vs, vl);
+            if (st == 0xFF) {
+                bad = true;
+                continue;
+            }
+            r_st[rec] = st;
+        } else if (kind == 4) {
+            r_id[rec] = (uint16_t)vs;
+        } else if (kind == 5) {
+            r_inc[rec] = x;
+        } else if (kind == 6) {
+            r_sinc[rec] = x;
+        }
+    }
+    if (__ballot(bad) != 0 || recbase != nrec) return false;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // the source names on lanes nrec .. 2 nrec - 1 when they fit, beside the addresses
+    const bool split = 2 * nrec <= 64;
+    if (split && lane >= nrec && lane < 2 * nrec) {
+        const uint32_t r = lane - nrec;
+        if (r_fl[r] & (1u << 2)) {
+            const uint32_t sr = r_sref[r];
+            r_sref[r] = name_find(nm, M.b + (sr & 0xFFFFu), sr >> 16);
+        }
+    }
+    uint32_t addr = NULL_ID;
+    uint32_t fl = 0, ar = 0;
+    if (lane < nrec) {
+        fl = r_fl[lane];
+        ar = r_aref[lane];
+        if (ar >> 16) addr = name_find(nm, M.b + (ar & 0xFFFFu), ar >> 16);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    bool rok = true;
+    if (lane < nrec) {
+        RecF f;
+        f.addr = addr;
+        f.alen = ar >> 16;
+        f.aoff = base + (ar & 0xFFFFu);
+        f.st = r_st[lane];
+        f.inc = (fl & (1u << 5)) ? r_inc[lane] : 0;
+        f.sinc = (fl & (1u << 6)) ? r_sinc[lane] : LLONG_MIN;
+        f.idoff = (fl & (1u << 4)) ? base + r_id[lane] : ~0ull;
+        f.src = NULL_ID;
+        if (fl & (1u << 2)) {
+            const uint32_t sr = r_sref[lane];
+            f.src = split ? sr : name_find(nm, M.b + (sr & 0xFFFFu), sr >> 16);
+        }
+        if (!(fl & (1u << 1))) f.aoff = 0;  // as wave_record leaves it with no address member
+        rok = f.alen != 0 && f.st != 0xFF && (fl & (1u << 5));
+        out[lane] = f;
+    }
+    return __ballot(!rok) == 0;
+}
+
 // Stash slots of message m: [stash_slot(m), stash_slot(m + 1)). An accepted record is at least
 // kMinRec bytes ({"address":"x","status":"alive","incarnationNumber":0} is 55), so a message of
 // L bytes holds at most L / kMinRec records and floor(off / kMinRec) + m leaves room for them.
@@ -947,6 +1114,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
     WaveLds& W = lds[wv];
     const uint64_t lt = (1ull << lane) - 1ull;
     uint32_t nwave = 0;  // messages this wave parsed itself (RP_WIRE_DEBUG)
+    uint32_t nmp = 0;    // of them, records parsed a lane per member
     const uint32_t nwaves = gridDim.x * kDecWaves;
     for (uint32_t m = blockIdx.x * kDecWaves + wv; m < n_msgs; m += nwaves) {
 #ifdef RP_WIRE_PROF
@@ -1192,17 +1360,33 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
         WPROF(3);
         // the changes array: its level tokens are { , { , ... {
         uint32_t nrec = 0;
+        uint32_t nb = 0;  // member boundaries (~0: a nested member value)
         if (ok) {
             const int32_t d = W.dep[arr];
             uint32_t nl = 0;
+            bool deep = false;
             for (uint32_t t0 = arr + 1; t0 < arr_end; t0 += 64) {
                 const uint32_t t = t0 + lane;
-                const bool lv = t < arr_end && W.dep[t] == d + 1;
+                const bool in = t < arr_end;
+                const int32_t dt = in ? (int32_t)W.dep[t] : 0;
+                const bool lv = in && dt == d + 1;
                 const uint64_t L = __ballot(lv);
                 const uint32_t idx = nl + (uint32_t)__popcll(L & lt);
                 if (lv && idx < kWLvl) W.lvl[idx] = (uint16_t)t;
                 nl += (uint32_t)__popcll(L);
+                if (kWaveMembers) {
+                    // the member boundaries too: record opens (level d + 1), member separators and
+                    // record closes (d + 2), from the top of W.lvl down (never over a level token)
+                    const uint8_t c = in ? W.tc[t] : (uint8_t)' ';
+                    const bool b = (lv && c == '{') || (in && dt == d + 2 && (c == ',' || c == '}'));
+                    deep |= in && dt > d + 2;
+                    const uint64_t mb = __ballot(b);
+                    const uint32_t ib = nb + (uint32_t)__popcll(mb & lt);
+                    if (b && ib + nl < kWLvl) W.lvl[kWLvl - 1 - ib] = (uint16_t)t;
+                    nb += (uint32_t)__popcll(mb);
+                }
             }
+            nb = (__ballot(deep) != 0 || nl + nb > kWLvl) ? ~0u : nb;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             // n records give 2n - 1 level tokens; an empty array none
             if (nl == 0)
@@ -1231,12 +1415,18 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
         const uint64_t s0 = stash_slot(I, m), s1 = stash_slot(I, m + 1);
         ok = ok && nrec <= s1 - s0;
         bool rok = true;
-        for (uint32_t r = lane; ok && r < nrec; r += 64) {
-            const uint32_t t0 = W.lvl[2 * r];
-            const uint32_t t1 = (2 * r + 1 < (nrec * 2 - 1) ? W.lvl[2 * r + 1] : arr_end) - 1;
-            RecF f;
-            rok &= wave_record(M, nm, b0, t0, t1, f);
-            stash[s0 + r] = f;
+        bool mp = false;
+        if (ok && nrec > 0 && nrec <= 64 && kWaveMembers)  // a lane per member (wave-uniform)
+            mp = wave_records_mp(M, W, nm, b0, nb, nrec, stash + s0, lane);
+        nmp += mp ? 1u : 0u;
+        if (!mp) {
+            for (uint32_t r = lane; ok && r < nrec; r += 64) {
+                const uint32_t t0 = W.lvl[2 * r];
+                const uint32_t t1 = (2 * r + 1 < (nrec * 2 - 1) ? W.lvl[2 * r + 1] : arr_end) - 1;
+                RecF f;
+                rok &= wave_record(M, nm, b0, t0, t1, f);
+                stash[s0 + r] = f;
+            }
         }
         ok = ok && __ballot(!rok) == 0;
         WPROF(5);
@@ -1258,6 +1448,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
         __builtin_amdgcn_wave_barrier();
     }
     if (n_by_waves && lane == 0 && nwave) atomicAdd(n_by_waves, nwave);
+    if (n_by_waves && lane == 0 && nmp) atomicAdd(n_by_waves + 1, nmp);
 }
 
 // After the scan of the counts: the wave-parsed messages' records from their stash slots to
@@ -1411,8 +1602,8 @@ int rp_wire_decode_dev(rp_members* m, const uint8_t* d_buf, const uint64_t* d_ms
             const bool dbg = getenv("RP_WIRE_DEBUG") != nullptr;
             rp::DevBuf<uint32_t> nbw;
             if (dbg) {
-                nbw.reserve(1);
-                RP_HIP(hipMemsetAsync(nbw.p, 0, 4, st));
+                nbw.reserve(2);
+                RP_HIP(hipMemsetAsync(nbw.p, 0, 8, st));
             }
             hipLaunchKernelGGL(rp::k_decode_wave, dim3(g), dim3(64 * rp::kDecWaves), 0, st, I, nm, O, n_msgs, vb, ve,
                                stash.p, slow.p, dbg ? nbw.p : nullptr);
@@ -1426,9 +1617,10 @@ int rp_wire_decode_dev(rp_members* m, const uint8_t* d_buf, const uint64_t* d_ms
             RP_HIP(hipStreamSynchronize(st));  // stash and slow are local
             rp::scratch_check(*ws, st);
             if (dbg) {
-                uint32_t h = 0;
-                RP_HIP(hipMemcpy(&h, nbw.p, 4, hipMemcpyDeviceToHost));
-                fprintf(stderr, "[rp] wire decode: %u of %u messages by waves\n", h, n_msgs);
+                uint32_t h[2] = {0, 0};
+                RP_HIP(hipMemcpy(h, nbw.p, 8, hipMemcpyDeviceToHost));
+                fprintf(stderr, "[rp] wire decode: %u of %u messages by waves (records a lane per member: %u)\n", h[0],
+                        n_msgs, h[1]);
             }
 #ifdef RP_WIRE_PROF
             {
