@@ -658,6 +658,10 @@ constexpr int kDecWaves = 4;
 #ifndef RP_WIRE_MEMBERS
 #define RP_WIRE_MEMBERS 0
 #endif
+#ifndef RP_WIRE_NAME_SPLIT
+#define RP_WIRE_NAME_SPLIT 0
+#endif
+constexpr bool kWaveNameSplit = RP_WIRE_NAME_SPLIT != 0;  // records' names looked up together (A/B)
 constexpr bool kWaveMembers = RP_WIRE_MEMBERS != 0;  // records parsed a lane per member (-DRP_WIRE_MEMBERS=1; A/B)
 
 struct WaveLds {
@@ -683,6 +687,78 @@ __device__ __forceinline__ uint32_t swar_bits(uint32_t m) {
 __device__ __forceinline__ bool wave_isws(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
 __device__ __forceinline__ bool wave_isopen(uint8_t c) { return c == '{' || c == '['; }
 __device__ __forceinline__ bool wave_isclose(uint8_t c) { return c == '}' || c == ']'; }
+
+// k's bytes as little-endian dwords against w (bytes past k's length ignored): the wave
+// decoder reads keys and values as aligned LDS dwords funnel-shifted into place, not bytewise
+template <int N>
+__device__ __forceinline__ bool words_eq(const uint32_t* w, const char (&k)[N]) {
+    uint32_t d = 0;
+#pragma unroll
+    for (int i = 0; i < (N + 2) / 4; i++) {
+        uint32_t kw = 0, m = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            if (4 * i + j < N - 1) {
+                kw |= (uint32_t)(uint8_t)k[4 * i + j] << (8 * j);
+                m |= 0xFFu << (8 * j);
+            }
+        d |= (w[i] ^ kw) & m;
+    }
+    return d == 0;
+}
+
+// farmhash's byte source over the staged message: byte ib + o of the LDS dwords d
+struct LdsSrc {
+    const uint32_t* d;
+    uint32_t ib;
+    __device__ uint32_t w(uint32_t o) const {
+        const uint32_t x = ib + o;
+        return __builtin_amdgcn_alignbyte(d[(x >> 2) + 1], d[x >> 2], x & 3u);
+    }
+    __device__ int8_t b(uint32_t o) const {
+        const uint32_t x = ib + o;
+        return (int8_t)(d[x >> 2] >> (8u * (x & 3u)));
+    }
+};
+
+// name_eq with the candidate's bytes read as global dwords (only those holding the name) and
+// the string's as LDS dwords, 16 bytes a step
+__device__ bool name_eq_lds(const Names& nm, const uint32_t* d, uint32_t ib, uint32_t len, uint32_t id) {
+    const uint64_t a = nm.off[id];
+    if (nm.off[id + 1] - a != len) return false;
+    const uintptr_t ga = reinterpret_cast<uintptr_t>(nm.bytes + a);
+    const uint32_t* g = reinterpret_cast<const uint32_t*>(ga & ~(uintptr_t)3);
+    const uint32_t gs = (uint32_t)(ga & 3u), ls = ib & 3u;
+    const uint32_t ng = (gs + len + 3) / 4;
+    const uint32_t* l = d + (ib >> 2);
+    for (uint32_t i = 0; i < len; i += 16) {
+        const uint32_t k = i / 4;
+        uint32_t G[5], L[5];
+#pragma unroll
+        for (uint32_t j = 0; j < 5; j++) {
+            G[j] = k + j < ng ? g[k + j] : 0u;
+            L[j] = l[k + j];
+        }
+        uint32_t dd = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) {
+            const uint32_t o = i + 4 * j;
+            const uint32_t m = o >= len ? 0u : len - o >= 4 ? ~0u : (1u << (8 * (len - o))) - 1u;
+            dd |= (__builtin_amdgcn_alignbyte(G[j + 1], G[j], gs) ^ __builtin_amdgcn_alignbyte(L[j + 1], L[j], ls)) & m;
+        }
+        if (dd) return false;
+    }
+    return true;
+}
+
+__device__ uint32_t name_find_lds(const Names& nm, const uint32_t* d, uint32_t ib, uint32_t len) {
+    uint32_t slot = fh::hash32(LdsSrc{d, ib}, len) & nm.hmask;
+    while (true) {
+        const uint32_t id = nm.htab[slot];
+        if (id == NULL_ID || name_eq_lds(nm, d, ib, len, id)) return id;
+        slot = (slot + 1) & nm.hmask;
+    }
+}
 
 struct WaveMsg {
     const WaveLds* W;
@@ -743,9 +819,11 @@ struct WaveMsg {
             uint32_t s, e;
             return scalar(t, s, e) && integer(s, e, v);
         }
-        uint8_t c[19];  // up to 19 bytes past the buffer's end stay inside this wave's WaveLds
+        uint32_t w[5];  // up to 23 bytes past the buffer's end stay inside this wave's WaveLds
+        words<5>(lo, w);
+        uint8_t c[19];
 #pragma unroll
-        for (int i = 0; i < 19; i++) c[i] = at(lo + i);
+        for (int i = 0; i < 19; i++) c[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
         const uint32_t n = hi - lo;
         const bool neg = c[0] == '-';
         if (n - (neg ? 1u : 0u) == 0 || n - (neg ? 1u : 0u) > 18) return false;
@@ -760,6 +838,56 @@ struct WaveMsg {
         }
         v = neg ? -(int64_t)x : (int64_t)x;
         return ok;
+    }
+    // the 4N message bytes from byte o as dwords (aligned LDS reads, funnel-shifted)
+    template <int N>
+    __device__ __forceinline__ void words(uint32_t o, uint32_t (&w)[N]) const {
+        const uint32_t x = sh + o;
+        const uint32_t* d = W->buf + (x >> 2);
+        uint32_t L[N + 1];
+#pragma unroll
+        for (int i = 0; i <= N; i++) L[i] = d[i];
+#pragma unroll
+        for (int i = 0; i < N; i++) w[i] = __builtin_amdgcn_alignbyte(L[i + 1], L[i], x & 3u);
+    }
+    // a record member's key at byte o, kl bytes: 1 address, 2 source, 3 status, 4 id,
+    // 5 incarnationNumber, 6 sourceIncarnationNumber, 0 any other
+    __device__ int rec_kind(uint32_t o, uint32_t kl) const {
+        uint32_t w[6];
+        words<6>(o, w);
+        return kl == 7 ? (words_eq(w, "address") ? 1 : 0)
+             : kl == 6 ? (words_eq(w, "source") ? 2 : words_eq(w, "status") ? 3 : 0)
+             : kl == 2 ? (words_eq(w, "id") ? 4 : 0)
+             : kl == 17 ? (words_eq(w, "incarnationNumber") ? 5 : 0)
+             : kl == 23 ? (words_eq(w, "sourceIncarnationNumber") ? 6 : 0) : 0;
+    }
+    // a body member's key (top_kind's codes)
+    __device__ int top_kind_w(uint32_t o, uint32_t kl) const {
+        uint32_t w[6];
+        words<6>(o, w);
+        switch (kl) {
+            case 7: return words_eq(w, "changes") ? 1 : 0;
+            case 10: return words_eq(w, "membership") ? 1 : words_eq(w, "pingStatus") ? 4 : 0;
+            case 8: return words_eq(w, "checksum") ? 2 : 0;
+            case 18: return words_eq(w, "membershipChecksum") ? 2 : 0;
+            case 23: return words_eq(w, "sourceIncarnationNumber") ? 3 : 0;
+            case 6: return words_eq(w, "source") ? 5 : words_eq(w, "target") ? 6 : 0;
+            case 11: return words_eq(w, "coordinator") ? 5 : 0;
+            default: return 0;
+        }
+    }
+    // status_code of the string at byte o
+    __device__ uint8_t status(uint32_t o, uint32_t len) const {
+        uint32_t w[2];
+        words<2>(o, w);
+        if (len == 5) return words_eq(w, "alive") ? ST_ALIVE : words_eq(w, "leave") ? ST_LEAVE : 0xFF;
+        if (len == 7) return words_eq(w, "suspect") ? ST_SUSPECT : 0xFF;
+        if (len == 6) return words_eq(w, "faulty") ? ST_FAULTY : 0xFF;
+        return 0xFF;
+    }
+    // name_find of the string at byte o
+    __device__ uint32_t find(const Names& nm, uint32_t o, uint32_t len) const {
+        return name_find_lds(nm, W->buf, sh + o, len);
     }
     // the token closing the nested value opened at token t (same depth after it)
     __device__ uint32_t match(uint32_t t) const {
@@ -811,7 +939,11 @@ struct RecF {
 // false: leave the message to the thread parser. Each member's tokens (key, ':', value and
 // the separator after it) are read from LDS together, so a member costs about three dependent
 // LDS trips: its tokens, then its key's and value's bytes, then the name lookups.
-__device__ bool wave_record(const WaveMsg& M, const Names& nm, uint64_t base, uint32_t t0, uint32_t t1, RecF& f) {
+// DEFER: the address is not looked up (the caller looks up every record's address and source
+// at once, a name per lane) and the source's byte offset | length << 16 is left in sref.
+template <bool DEFER>
+__device__ bool wave_record(const WaveMsg& M, const Names& nm, uint64_t base, uint32_t t0, uint32_t t1, RecF& f,
+                            uint32_t& sref) {
     f.addr = NULL_ID;
     f.src = NULL_ID;
     f.alen = 0;
@@ -833,15 +965,8 @@ __device__ bool wave_record(const WaveMsg& M, const Names& nm, uint64_t base, ui
                        p5 = P[t + 5];
         const uint8_t c0 = TC[t], c1 = TC[t + 1], c2 = TC[t + 2], c3 = TC[t + 3], c4 = TC[t + 4], c5 = TC[t + 5];
         if (!((c0 == '"') & (c1 == '"') & (c2 == ':')) || !M.clean(pm, p0) || !M.clean(p1, p2)) return false;
-        const uint8_t* kp = M.b + p0 + 1;
-        const uint32_t kl = p1 - p0 - 1;
         // 1 address, 2 source, 3 status, 4 id, 5 incarnationNumber, 6 sourceIncarnationNumber
-        // (dispatched on the length: one compare)
-        const int kind = kl == 7 ? (key_eq(kp, "address") ? 1 : 0)
-                       : kl == 6 ? (key_eq(kp, "source") ? 2 : key_eq(kp, "status") ? 3 : 0)
-                       : kl == 2 ? (key_eq(kp, "id") ? 4 : 0)
-                       : kl == 17 ? (key_eq(kp, "incarnationNumber") ? 5 : 0)
-                       : kl == 23 ? (key_eq(kp, "sourceIncarnationNumber") ? 6 : 0) : 0;
+        const int kind = M.rec_kind(p0 + 1, p1 - p0 - 1);
         uint32_t nx;
         uint8_t cn, cb;  // the separator token's character and the one before it
         uint32_t pb, pn;  // their positions
@@ -852,11 +977,14 @@ __device__ bool wave_record(const WaveMsg& M, const Names& nm, uint64_t base, ui
             if (kind == 1) {
                 f.aoff = base + so;
                 f.alen = sl;
-                f.addr = name_find(nm, M.b + so, sl);
+                if (!DEFER) f.addr = M.find(nm, so, sl);
             } else if (kind == 2) {
-                f.src = name_find(nm, M.b + so, sl);
+                if (DEFER)
+                    sref = so | (sl << 16);
+                else
+                    f.src = M.find(nm, so, sl);
             } else if (kind == 3) {
-                f.st = status_code(M.b + so, sl);
+                f.st = M.status(so, sl);
                 if (f.st == 0xFF) return false;
             } else {
                 f.idoff = base + so;
@@ -965,13 +1093,7 @@ __device__ bool wave_records_mp(const WaveMsg& M, WaveLds& W, const Names& nm, u
             bad = true;
             continue;
         }
-        const uint8_t* kp = M.b + p0 + 1;
-        const uint32_t kl = p1 - p0 - 1;
-        const int kind = kl == 7 ? (key_eq(kp, "address") ? 1 : 0)
-                       : kl == 6 ? (key_eq(kp, "source") ? 2 : key_eq(kp, "status") ? 3 : 0)
-                       : kl == 2 ? (key_eq(kp, "id") ? 4 : 0)
-                       : kl == 17 ? (key_eq(kp, "incarnationNumber") ? 5 : 0)
-                       : kl == 23 ? (key_eq(kp, "sourceIncarnationNumber") ? 6 : 0) : 0;
+        const int kind = M.rec_kind(p0 + 1, p1 - p0 - 1);
         uint32_t nx;
         uint32_t vs = 0, vl = 0;  // a string value's offset and length
         int64_t x = 0;
@@ -1008,7 +1130,7 @@ __device__ bool wave_records_mp(const WaveMsg& M, WaveLds& W, const Names& nm, u
         } else if (kind == 2) {
             r_sref[rec] = vs | (vl << 16);
         } else if (kind == 3) {
-            const uint8_t st = status_code(M.b + vs, vl);
+            const uint8_t st = M.status(vs, vl);
             if (st == 0xFF) {
                 bad = true;
                 continue;
@@ -1031,7 +1153,7 @@ __device__ bool wave_records_mp(const WaveMsg& M, WaveLds& W, const Names& nm, u
         const uint32_t r = lane - nrec;
         if (r_fl[r] & (1u << 2)) {
             const uint32_t sr = r_sref[r];
-            r_sref[r] = name_find(nm, M.b + (sr & 0xFFFFu), sr >> 16);
+            r_sref[r] = M.find(nm, sr & 0xFFFFu, sr >> 16);
         }
     }
     uint32_t addr = NULL_ID;
@@ -1039,7 +1161,7 @@ __device__ bool wave_records_mp(const WaveMsg& M, WaveLds& W, const Names& nm, u
     if (lane < nrec) {
         fl = r_fl[lane];
         ar = r_aref[lane];
-        if (ar >> 16) addr = name_find(nm, M.b + (ar & 0xFFFFu), ar >> 16);
+        if (ar >> 16) addr = M.find(nm, ar & 0xFFFFu, ar >> 16);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1056,7 +1178,7 @@ __device__ bool wave_records_mp(const WaveMsg& M, WaveLds& W, const Names& nm, u
         f.src = NULL_ID;
         if (fl & (1u << 2)) {
             const uint32_t sr = r_sref[lane];
-            f.src = split ? sr : name_find(nm, M.b + (sr & 0xFFFFu), sr >> 16);
+            f.src = split ? sr : M.find(nm, sr & 0xFFFFu, sr >> 16);
         }
         if (!(fl & (1u << 1))) f.aoff = 0;  // as wave_record leaves it with no address member
         rok = f.alen != 0 && f.st != 0xFF && (fl & (1u << 5));
@@ -1285,7 +1407,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
                     }
                     const uint32_t v = t + 3;
                     uint32_t nx = ntok;
-                    const int kind = top_kind(B + W.pos[t] + 1, (uint32_t)(W.pos[t + 1] - W.pos[t] - 1));
+                    const int kind = M.top_kind_w(W.pos[t] + 1, (uint32_t)(W.pos[t + 1] - W.pos[t] - 1));
                     if (kind == 1) {
                         if (seen || v >= last || M.tch(v) != '[' || !M.clean(W.pos[v - 1], W.pos[v])) {
                             ok = false;
@@ -1320,7 +1442,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
                         ok = v + 1 < last && M.tch(v) == '"' && M.clean(W.pos[v - 1], W.pos[v]);
                         if (ok) {
                             const uint32_t so = W.pos[v] + 1, sl = W.pos[v + 1] - so;
-                            const uint32_t id = lane == 0 ? name_find(nm, B + so, sl) : 0u;
+                            const uint32_t id = lane == 0 ? M.find(nm, so, sl) : 0u;
                             const uint32_t idb = __shfl(id, 0, 64);
                             if (kind == 6)
                                 mtgt = idb;
@@ -1419,12 +1541,33 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
         if (ok && nrec > 0 && nrec <= 64 && kWaveMembers)  // a lane per member (wave-uniform)
             mp = wave_records_mp(M, W, nm, b0, nb, nrec, stash + s0, lane);
         nmp += mp ? 1u : 0u;
-        if (!mp) {
+        if (!mp && kWaveNameSplit && nrec <= 32) {
+            // a lane per record, then its address and source names looked up together: lanes
+            // [0, nrec) the addresses, [nrec, 2 nrec) the sources
+            RecF f;
+            uint32_t sref = ~0u;
+            if (ok && lane < nrec) {
+                const uint32_t t0 = W.lvl[2 * lane];
+                const uint32_t t1 = (2 * lane + 1 < (nrec * 2 - 1) ? W.lvl[2 * lane + 1] : arr_end) - 1;
+                rok = wave_record<true>(M, nm, b0, t0, t1, f, sref);
+            }
+            const uint32_t sx = __shfl(sref, (int)((lane - nrec) & 63u), 64);
+            const uint32_t aref = lane < nrec && f.alen ? (uint32_t)(f.aoff - b0) | (f.alen << 16) : ~0u;
+            const uint32_t ref = lane < nrec ? aref : lane < 2 * nrec ? sx : ~0u;
+            const uint32_t id = ok && ref != ~0u ? M.find(nm, ref & 0xFFFFu, ref >> 16) : NULL_ID;
+            const uint32_t sid = __shfl(id, (int)((lane + nrec) & 63u), 64);
+            if (ok && lane < nrec) {
+                f.addr = id;
+                f.src = sref != ~0u ? sid : NULL_ID;
+                stash[s0 + lane] = f;
+            }
+        } else if (!mp) {
             for (uint32_t r = lane; ok && r < nrec; r += 64) {
                 const uint32_t t0 = W.lvl[2 * r];
                 const uint32_t t1 = (2 * r + 1 < (nrec * 2 - 1) ? W.lvl[2 * r + 1] : arr_end) - 1;
                 RecF f;
-                rok &= wave_record(M, nm, b0, t0, t1, f);
+                uint32_t sref;
+                rok &= wave_record<false>(M, nm, b0, t0, t1, f, sref);
                 stash[s0 + r] = f;
             }
         }
