@@ -21,6 +21,9 @@ struct Scratch {
     // device error word: kErrSpin (a look-back wait gave up) | kErrTicket (a ticket past the
     // launch's units); read and cleared by scratch_check at the host's next sync point
     DevBuf<uint32_t> err;
+    // the wire decoder's record stash and slow-path flags (grow-only: a 640 MB decode keeps
+    // ~750 MB here rather than allocating and freeing it per call)
+    DevBuf<uint8_t> wire_stash, wire_slow;
     uint32_t epoch = 0;
     // the stream that last used this scratch: a launch on another stream first waits for it
     // (use_on), so two streams never interleave tickets or look-back words
