@@ -33,9 +33,12 @@ struct NameTable {
     DevBuf<uint8_t> sbytes;
     DevBuf<uint32_t> soff;
     uint32_t sbytes_n = 0;
-    // open-addressing index over the device names: 2^hbits slots holding ids (0xFFFFFFFF empty),
-    // keyed by farmhash32 of the name, linear probing (the wire decoder's interning)
-    DevBuf<uint32_t> htab;
+    // open-addressing index over the device names (the wire decoder's interning): 2^hbits slots
+    // of 32 B, keyed by farmhash32 of the name, linear probing. A slot holds the id (0xFFFFFFFF
+    // empty), the name's length, its byte offset and its first kNameInline bytes (zero padded),
+    // so a probe of a name that short is one 32-byte read, not id -> offsets -> bytes.
+    static constexpr uint32_t kSlotWords = 8, kNameInline = 20;
+    DevBuf<uint32_t> hslot;
     uint32_t htab_n = 0, hbits = 0;
 
     uint32_t size() const { return (uint32_t)names.size(); }

@@ -27,12 +27,27 @@ __global__ void k_name_chunk(const uint8_t* __restrict__ names, const uint64_t* 
 }
 
 __global__ void k_name_hash_insert(const uint8_t* __restrict__ names, const uint64_t* __restrict__ noff, uint32_t n,
-                                   uint32_t* __restrict__ htab, uint32_t mask) {
+                                   uint32_t* __restrict__ hs, uint32_t mask) {
     const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gstride) {
         const uint64_t b = noff[i];
-        uint32_t slot = fh::hash32(fh::PtrSrc{names + b}, (uint32_t)(noff[i + 1] - b)) & mask;
-        while (atomicCAS(&htab[slot], 0xFFFFFFFFu, (uint32_t)i) != 0xFFFFFFFFu) slot = (slot + 1) & mask;
+        const uint32_t L = (uint32_t)(noff[i + 1] - b);
+        uint32_t slot = fh::hash32(fh::PtrSrc{names + b}, L) & mask;
+        while (atomicCAS(&hs[NameTable::kSlotWords * slot], 0xFFFFFFFFu, (uint32_t)i) != 0xFFFFFFFFu)
+            slot = (slot + 1) & mask;
+        uint32_t* w = hs + NameTable::kSlotWords * slot;
+        w[1] = L;
+        w[2] = (uint32_t)b;
+#pragma unroll
+        for (uint32_t q = 0; q < NameTable::kNameInline / 4; q++) {
+            uint32_t x = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++) {
+                const uint32_t o = 4 * q + j;
+                x |= (o < L ? (uint32_t)names[b + o] : 0u) << (8 * j);
+            }
+            w[3 + q] = x;
+        }
     }
 }
 
@@ -79,15 +94,16 @@ void NameTable::sort_bytes(hipStream_t st, Scratch& ws) {
 
 void NameTable::hash_index(hipStream_t st) {
     const uint32_t n = (uint32_t)names.size();
-    if (htab_n == n && htab.p) return;
+    if (htab_n == n && hslot.p) return;
     sync(st);
     uint32_t b = 4;
     while ((1ull << b) < 2ull * n) b++;  // load factor <= 1/2
-    htab.reserve(1ull << b);
-    RP_HIP(hipMemsetAsync(htab.p, 0xFF, 4ull << b, st));
+    if (h_bytes.size() > 0xFFFFFF00ull) throw Error(RP_EINVAL, "names past 4 GB of bytes (32-bit offsets in the index)");
+    hslot.reserve((uint64_t)kSlotWords << b);
+    RP_HIP(hipMemsetAsync(hslot.p, 0xFF, (4ull * kSlotWords) << b, st));
     if (n)
         hipLaunchKernelGGL(k_name_hash_insert, dim3(grid_for(n, 256)), dim3(256), 0, st, d_bytes.p, d_noff.p, n,
-                           htab.p, (1u << b) - 1u);
+                           hslot.p, (1u << b) - 1u);
     RP_HIP(hipGetLastError());
     hbits = b;
     htab_n = n;

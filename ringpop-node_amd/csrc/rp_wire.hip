@@ -44,7 +44,7 @@ struct Names {
     const uint64_t* off;
     const uint32_t* sorted;
     uint32_t n;
-    const uint32_t* htab;  // NameTable::htab (hash index of the names)
+    const uint32_t* hslot;  // NameTable::hslot (hash index of the names, 8 words a slot)
     uint32_t hmask;
 };
 
@@ -362,8 +362,9 @@ __device__ bool name_eq(const Names& nm, const uint8_t* s, uint32_t len, uint32_
 __device__ uint32_t name_find(const Names& nm, const uint8_t* s, uint32_t len) {
     uint32_t slot = fh::hash32(fh::PtrSrc{s}, len) & nm.hmask;
     while (true) {
-        const uint32_t id = nm.htab[slot];
-        if (id == NULL_ID || name_eq(nm, s, len, id)) return id;
+        const uint32_t* w = nm.hslot + (uint64_t)NameTable::kSlotWords * slot;
+        const uint32_t id = w[0];
+        if (id == NULL_ID || (w[1] == len && name_eq(nm, s, len, id))) return id;
         slot = (slot + 1) & nm.hmask;
     }
 }
@@ -662,15 +663,19 @@ constexpr int kDecWaves = 4;
 #define RP_WIRE_NAME_SPLIT 1
 #endif
 constexpr bool kWaveNameSplit = RP_WIRE_NAME_SPLIT != 0;  // records' names looked up together (3.36 vs 3.58 ms; 0: A/B)
-constexpr bool kWaveMembers = RP_WIRE_MEMBERS != 0;  // records parsed a lane per member (-DRP_WIRE_MEMBERS=1; A/B)
+constexpr bool kWaveMembers = RP_WIRE_MEMBERS != 0;
+#ifndef RP_WIRE_CLS16
+#define RP_WIRE_CLS16 1
+#endif
+constexpr bool kWaveCls16 = RP_WIRE_CLS16 != 0;  // classifier: 16 bytes per lane a step (0: 4 bytes; A/B)  // records parsed a lane per member (-DRP_WIRE_MEMBERS=1; A/B)
 
-struct WaveLds {
-    uint32_t buf[kWBuf / 4 + 2];
+struct alignas(16) WaveLds {
+    alignas(16) uint32_t buf[kWBuf / 4 + 2];
     uint16_t pos[kWTok];   // token byte offset in the message
     int8_t dep[kWTok];     // depth before the token ({ [ open, } ] close)
     uint8_t tc[kWTok];     // the token's character
     alignas(16) uint16_t lvl[kWLvl];  // the changes array's level tokens (the classifier's scratch before)
-    uint64_t scal[kWBuf / 64 + 4];  // buffer bytes outside strings that are neither tokens nor
+    uint64_t scal[kWBuf / 64 + 16];  // buffer bytes outside strings that are neither tokens nor
                                     // whitespace (bit sh + i: message byte i)
     uint16_t op1[32], cl2[32];      // openers at depth 1 / closers at depth 2, in order: the k-th pair
 };
@@ -721,12 +726,10 @@ struct LdsSrc {
     }
 };
 
-// name_eq with the candidate's bytes read as global dwords (only those holding the name) and
-// the string's as LDS dwords, 16 bytes a step
-__device__ bool name_eq_lds(const Names& nm, const uint32_t* d, uint32_t ib, uint32_t len, uint32_t id) {
-    const uint64_t a = nm.off[id];
-    if (nm.off[id + 1] - a != len) return false;
-    const uintptr_t ga = reinterpret_cast<uintptr_t>(nm.bytes + a);
+// len bytes of a name at g (global, read as the dwords holding them) against the staged bytes
+// from ib (LDS dwords), 16 bytes a step
+__device__ bool bytes_eq_lds(const uint8_t* gp, const uint32_t* d, uint32_t ib, uint32_t len) {
+    const uintptr_t ga = reinterpret_cast<uintptr_t>(gp);
     const uint32_t* g = reinterpret_cast<const uint32_t*>(ga & ~(uintptr_t)3);
     const uint32_t gs = (uint32_t)(ga & 3u), ls = ib & 3u;
     const uint32_t ng = (gs + len + 3) / 4;
@@ -751,11 +754,31 @@ __device__ bool name_eq_lds(const Names& nm, const uint32_t* d, uint32_t ib, uin
     return true;
 }
 
+// name_find over the staged bytes: the string's first kNameInline bytes are compared with the
+// slot's copy (one 32-byte read a probe); only a longer name reads the rest of its bytes
 __device__ uint32_t name_find_lds(const Names& nm, const uint32_t* d, uint32_t ib, uint32_t len) {
+    constexpr uint32_t kIn = NameTable::kNameInline;
     uint32_t slot = fh::hash32(LdsSrc{d, ib}, len) & nm.hmask;
+    uint32_t sw[kIn / 4];
+    {
+        const uint32_t* l = d + (ib >> 2);
+        uint32_t L[kIn / 4 + 1];
+#pragma unroll
+        for (uint32_t j = 0; j <= kIn / 4; j++) L[j] = l[j];
+#pragma unroll
+        for (uint32_t j = 0; j < kIn / 4; j++) {
+            const uint32_t o = 4 * j;
+            const uint32_t m = o >= len ? 0u : len - o >= 4 ? ~0u : (1u << (8 * (len - o))) - 1u;
+            sw[j] = __builtin_amdgcn_alignbyte(L[j + 1], L[j], ib & 3u) & m;
+        }
+    }
     while (true) {
-        const uint32_t id = nm.htab[slot];
-        if (id == NULL_ID || name_eq_lds(nm, d, ib, len, id)) return id;
+        const uint4* w = reinterpret_cast<const uint4*>(nm.hslot + (uint64_t)NameTable::kSlotWords * slot);
+        const uint4 a = w[0], b = w[1];
+        if (a.x == NULL_ID) return NULL_ID;
+        const uint32_t dd = (a.w ^ sw[0]) | (b.x ^ sw[1]) | (b.y ^ sw[2]) | (b.z ^ sw[3]) | (b.w ^ sw[4]);
+        if (a.y == len && dd == 0 && (len <= kIn || bytes_eq_lds(nm.bytes + a.z + kIn, d, ib + kIn, len - kIn)))
+            return a.x;
         slot = (slot + 1) & nm.hmask;
     }
 }
@@ -1291,66 +1314,137 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
         uint32_t ntok = 0, quotes = 0;
         bool bad = false;
         const uint32_t nbd = (sh + len + 3) / 4;
-        uint8_t* nib = reinterpret_cast<uint8_t*>(W.lvl);
-        for (uint32_t d0 = 0; ok && d0 < nbd; d0 += 64) {
-            const uint32_t dw = d0 + lane;
-            uint32_t x = dw < nbd ? W.buf[dw] : 0x20202020u;
-            // the message's bytes of this dword (a neighbour's bytes at either end read as blanks)
-            const int lo = min(max((int)sh - (int)(4 * dw), 0), 4);
-            const int hi = min(max((int)(sh + len) - (int)(4 * dw), 0), 4);
-            const uint32_t m_in = (uint32_t)((0x80808080ull << (8 * lo)) & (0x80808080ull >> (8 * (4 - hi))));
-            const uint32_t bm = (m_in >> 7) * 0xFFu;
-            x = (x & bm) | (0x20202020u & ~bm);
-            // bytes as bit 7 of each byte lane (SWAR)
-            const uint32_t Q = swar_eq(x, '"');
-            uint32_t p = Q ^ (Q << 8);
-            p ^= p << 16;  // bit 7 of byte j: odd number of the lane's quotes up to byte j
-            const uint64_t Po = __ballot((p >> 31) & 1u);
-            const uint32_t pre = (quotes + (uint32_t)__popcll(Po & lt)) & 1u;
-            const uint32_t instr = p ^ (pre ? 0x80808080u : 0u);  // opening quote + body
-            const uint32_t xd = x & 0xDFDFDFDFu;                  // { [ → 0x5B, } ] → 0x5D
-            const uint32_t structural = (swar_eq(xd, 0x5B) | swar_eq(xd, 0x5D) | swar_eq(x, ':') | swar_eq(x, ',')) &
-                                        ~instr & ~Q;
-            const uint32_t tokb = Q | structural;
-            const uint32_t ws = swar_eq(x, ' ') | swar_eq(x, '\t') | swar_eq(x, '\n') | swar_eq(x, '\r');
-            const uint32_t lt20 = ~(((x & 0x7F7F7F7Fu) + 0x60606060u) | x) & 0x80808080u;
-            const uint32_t str_body = instr & ~Q;
-            const uint32_t ctrlb = (lt20 & ~(ws & ~str_body)) | swar_eq(x, '\\');
-            const uint32_t sb = ~instr & ~tokb & ~ws & 0x80808080u;
-            const uint32_t tm = swar_bits(tokb), sm = swar_bits(sb);
-            const bool ctrl = ctrlb != 0;
-            bad |= __ballot(ctrl) != 0;
-            const uint32_t k = (uint32_t)__builtin_popcount(tm);
-            const uint64_t K0 = __ballot(k & 1u), K1 = __ballot(k & 2u), K2 = __ballot(k & 4u);
-            uint32_t idx = ntok + (uint32_t)__popcll(K0 & lt) + 2u * (uint32_t)__popcll(K1 & lt) +
-                           4u * (uint32_t)__popcll(K2 & lt);
+        if (kWaveCls16) {
+            // 1 KB per step, 16 staged bytes (four dwords) per lane: one prefix of the lanes'
+            // quote parities and one of their token counts (five ballots) per step, and the
+            // lane's 16 scalar bits stored straight into the bitmap as a u16
+            for (uint32_t d0 = 0; ok && d0 < nbd; d0 += 256) {
+                const uint32_t dw0 = d0 + 4u * lane;
+                uint4 v = make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
+                if (dw0 < nbd) v = *reinterpret_cast<const uint4*>(&W.buf[dw0]);  // past nbd: masked below
+                uint32_t x[4] = {v.x, v.y, v.z, v.w};
+                uint32_t p[4], Qd[4];
+                uint32_t par = 0;
 #pragma unroll
-            for (int j = 0; j < 4; j++)
-                if ((tm >> j) & 1u) {
-                    if (idx < kWTok) {
-                        W.pos[idx] = (uint16_t)(4 * dw + j - sh);
-                        W.tc[idx] = (uint8_t)(x >> (8 * j));
-                    }
-                    idx++;
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t dw = dw0 + k;
+                    const int lo = min(max((int)sh - (int)(4 * dw), 0), 4);
+                    const int hi = min(max((int)(sh + len) - (int)(4 * dw), 0), 4);
+                    const uint32_t m_in = (uint32_t)((0x80808080ull << (8 * lo)) & (0x80808080ull >> (8 * (4 - hi))));
+                    const uint32_t bm = (m_in >> 7) * 0xFFu;
+                    x[k] = (x[k] & bm) | (0x20202020u & ~bm);
+                    const uint32_t Q = swar_eq(x[k], '"');
+                    uint32_t pp = Q ^ (Q << 8);
+                    pp ^= pp << 16;
+                    p[k] = pp ^ (par ? 0x80808080u : 0u);  // parity of the lane's quotes up to each byte
+                    par ^= (pp >> 31) & 1u;
+                    Qd[k] = Q;
                 }
-            nib[lane] = (uint8_t)sm;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            if (lane < 4) {  // 16 lanes' nibbles → the bitmap word of 64 buffer bytes
-                const uint4 v = *reinterpret_cast<const uint4*>(nib + 16 * lane);
-                uint64_t a = (uint64_t)v.x | ((uint64_t)v.y << 32), c = (uint64_t)v.z | ((uint64_t)v.w << 32);
-                a = (a | (a >> 4)) & 0x00FF00FF00FF00FFull;
-                a = (a | (a >> 8)) & 0x0000FFFF0000FFFFull;
-                a = (a | (a >> 16)) & 0xFFFFFFFFull;
-                c = (c | (c >> 4)) & 0x00FF00FF00FF00FFull;
-                c = (c | (c >> 8)) & 0x0000FFFF0000FFFFull;
-                c = (c | (c >> 16)) & 0xFFFFFFFFull;
-                W.scal[d0 / 16 + lane] = a | (c << 32);
+                const uint64_t Po = __ballot(par);
+                const uint32_t pre = (quotes + (uint32_t)__popcll(Po & lt)) & 1u;
+                uint32_t tm = 0, sm = 0;
+                bool ctrl = false;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t Q = Qd[k], xk = x[k];
+                    const uint32_t instr = p[k] ^ (pre ? 0x80808080u : 0u);
+                    const uint32_t xd = xk & 0xDFDFDFDFu;
+                    const uint32_t structural =
+                        (swar_eq(xd, 0x5B) | swar_eq(xd, 0x5D) | swar_eq(xk, ':') | swar_eq(xk, ',')) & ~instr & ~Q;
+                    const uint32_t tokb = Q | structural;
+                    const uint32_t ws = swar_eq(xk, ' ') | swar_eq(xk, '\t') | swar_eq(xk, '\n') | swar_eq(xk, '\r');
+                    const uint32_t lt20 = ~(((xk & 0x7F7F7F7Fu) + 0x60606060u) | xk) & 0x80808080u;
+                    const uint32_t str_body = instr & ~Q;
+                    ctrl |= ((lt20 & ~(ws & ~str_body)) | swar_eq(xk, '\\')) != 0;
+                    const uint32_t sb = ~instr & ~tokb & ~ws & 0x80808080u;
+                    tm |= swar_bits(tokb) << (4 * k);
+                    sm |= swar_bits(sb) << (4 * k);
+                }
+                bad |= __ballot(ctrl) != 0;
+                const uint32_t kc = (uint32_t)__builtin_popcount(tm);
+                const uint64_t K0 = __ballot(kc & 1u), K1 = __ballot(kc & 2u), K2 = __ballot(kc & 4u),
+                               K3 = __ballot(kc & 8u), K4 = __ballot(kc & 16u);
+                uint32_t idx = ntok + (uint32_t)__popcll(K0 & lt) + 2u * (uint32_t)__popcll(K1 & lt) +
+                               4u * (uint32_t)__popcll(K2 & lt) + 8u * (uint32_t)__popcll(K3 & lt) +
+                               16u * (uint32_t)__popcll(K4 & lt);
+#pragma unroll
+                for (int j = 0; j < 16; j++)
+                    if ((tm >> j) & 1u) {
+                        if (idx < kWTok) {
+                            W.pos[idx] = (uint16_t)(4 * dw0 + j - sh);
+                            W.tc[idx] = (uint8_t)(x[j >> 2] >> (8 * (j & 3)));
+                        }
+                        idx++;
+                    }
+                reinterpret_cast<uint16_t*>(W.scal)[(d0 >> 2) + lane] = (uint16_t)sm;
+                ntok += (uint32_t)__popcll(K0) + 2u * (uint32_t)__popcll(K1) + 4u * (uint32_t)__popcll(K2) +
+                        8u * (uint32_t)__popcll(K3) + 16u * (uint32_t)__popcll(K4);
+                quotes += (uint32_t)__popcll(Po);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            ntok += (uint32_t)__popcll(K0) + 2u * (uint32_t)__popcll(K1) + 4u * (uint32_t)__popcll(K2);
-            quotes += (uint32_t)__popcll(Po);
+        } else {
+            uint8_t* nib = reinterpret_cast<uint8_t*>(W.lvl);
+            for (uint32_t d0 = 0; ok && d0 < nbd; d0 += 64) {
+                const uint32_t dw = d0 + lane;
+                uint32_t x = dw < nbd ? W.buf[dw] : 0x20202020u;
+                // the message's bytes of this dword (a neighbour's bytes at either end read as blanks)
+                const int lo = min(max((int)sh - (int)(4 * dw), 0), 4);
+                const int hi = min(max((int)(sh + len) - (int)(4 * dw), 0), 4);
+                const uint32_t m_in = (uint32_t)((0x80808080ull << (8 * lo)) & (0x80808080ull >> (8 * (4 - hi))));
+                const uint32_t bm = (m_in >> 7) * 0xFFu;
+                x = (x & bm) | (0x20202020u & ~bm);
+                // bytes as bit 7 of each byte lane (SWAR)
+                const uint32_t Q = swar_eq(x, '"');
+                uint32_t p = Q ^ (Q << 8);
+                p ^= p << 16;  // bit 7 of byte j: odd number of the lane's quotes up to byte j
+                const uint64_t Po = __ballot((p >> 31) & 1u);
+                const uint32_t pre = (quotes + (uint32_t)__popcll(Po & lt)) & 1u;
+                const uint32_t instr = p ^ (pre ? 0x80808080u : 0u);  // opening quote + body
+                const uint32_t xd = x & 0xDFDFDFDFu;                  // { [ → 0x5B, } ] → 0x5D
+                const uint32_t structural = (swar_eq(xd, 0x5B) | swar_eq(xd, 0x5D) | swar_eq(x, ':') | swar_eq(x, ',')) &
+                                            ~instr & ~Q;
+                const uint32_t tokb = Q | structural;
+                const uint32_t ws = swar_eq(x, ' ') | swar_eq(x, '\t') | swar_eq(x, '\n') | swar_eq(x, '\r');
+                const uint32_t lt20 = ~(((x & 0x7F7F7F7Fu) + 0x60606060u) | x) & 0x80808080u;
+                const uint32_t str_body = instr & ~Q;
+                const uint32_t ctrlb = (lt20 & ~(ws & ~str_body)) | swar_eq(x, '\\');
+                const uint32_t sb = ~instr & ~tokb & ~ws & 0x80808080u;
+                const uint32_t tm = swar_bits(tokb), sm = swar_bits(sb);
+                const bool ctrl = ctrlb != 0;
+                bad |= __ballot(ctrl) != 0;
+                const uint32_t k = (uint32_t)__builtin_popcount(tm);
+                const uint64_t K0 = __ballot(k & 1u), K1 = __ballot(k & 2u), K2 = __ballot(k & 4u);
+                uint32_t idx = ntok + (uint32_t)__popcll(K0 & lt) + 2u * (uint32_t)__popcll(K1 & lt) +
+                               4u * (uint32_t)__popcll(K2 & lt);
+    #pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if ((tm >> j) & 1u) {
+                        if (idx < kWTok) {
+                            W.pos[idx] = (uint16_t)(4 * dw + j - sh);
+                            W.tc[idx] = (uint8_t)(x >> (8 * j));
+                        }
+                        idx++;
+                    }
+                nib[lane] = (uint8_t)sm;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                if (lane < 4) {  // 16 lanes' nibbles → the bitmap word of 64 buffer bytes
+                    const uint4 v = *reinterpret_cast<const uint4*>(nib + 16 * lane);
+                    uint64_t a = (uint64_t)v.x | ((uint64_t)v.y << 32), c = (uint64_t)v.z | ((uint64_t)v.w << 32);
+                    a = (a | (a >> 4)) & 0x00FF00FF00FF00FFull;
+                    a = (a | (a >> 8)) & 0x0000FFFF0000FFFFull;
+                    a = (a | (a >> 16)) & 0xFFFFFFFFull;
+                    c = (c | (c >> 4)) & 0x00FF00FF00FF00FFull;
+                    c = (c | (c >> 8)) & 0x0000FFFF0000FFFFull;
+                    c = (c | (c >> 16)) & 0xFFFFFFFFull;
+                    W.scal[d0 / 16 + lane] = a | (c << 32);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                ntok += (uint32_t)__popcll(K0) + 2u * (uint32_t)__popcll(K1) + 4u * (uint32_t)__popcll(K2);
+                quotes += (uint32_t)__popcll(Po);
+            }
         }
         ok = ok && !bad && ntok <= kWTok && (quotes & 1u) == 0 && ntok > 0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1615,7 +1709,7 @@ __global__ void k_zero_tail(uint32_t* p, uint32_t n) {
 Names names_of(NameTable& nt, hipStream_t st, Scratch& ws) {
     nt.sort(st, ws);
     nt.hash_index(st);
-    return Names{nt.d_bytes.p, nt.d_noff.p, nt.sorted.p, nt.size(), nt.htab.p, (1u << nt.hbits) - 1u};
+    return Names{nt.d_bytes.p, nt.d_noff.p, nt.sorted.p, nt.size(), nt.hslot.p, (1u << nt.hbits) - 1u};
 }
 
 }  // namespace

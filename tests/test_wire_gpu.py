@@ -392,3 +392,45 @@ def test_wave_decoder_equals_thread_decoder(gpu, monkeypatch, capfd, grid):
     by_waves = int(line.split()[3])
     big = sum(1 for t in texts if len(t.encode()) > 8192)
     assert by_waves >= n_ok - big, line
+
+
+@pytest.mark.parametrize("thread", [False, True], ids=["waves", "thread-parser"])
+def test_decode_name_lengths_around_the_inline_prefix(gpu, monkeypatch, thread):
+    """The decoder's name index keeps a name's first 20 bytes in its hash slot and reads only
+    the rest from the name bytes: interned names of 0..70 bytes, names sharing their first 20
+    bytes (and more) with one another, and strings that are a prefix or an extension of an
+    interned name by one byte (not interned: NULL id). Records' address / source and the body's
+    source and target go through the same lookup."""
+    rng = random.Random(3)
+    base = "".join(rng.choice("0123456789abcdef.:") for _ in range(70))
+    names = sorted({base[:n] for n in range(1, 71)} | {base[:20] + "x" + base[21:n] for n in range(21, 40)} |
+                   {"10.0.%d.%d:%d" % (i, i * 7 % 256, 3000 + i) for i in range(40)} |
+                   {"".join(rng.choice("abc") for _ in range(rng.randrange(1, 64))) for _ in range(200)})
+    m = gpu.Membership()
+    ids = dict(zip(names, m.intern(names)))
+    probes = names + [n + "q" for n in names[:60]] + [n[:-1] for n in names[:60] if len(n) > 1]
+    rng.shuffle(probes)
+    texts = []
+    want_addr, want_src, want_hsrc, want_tgt = [], [], [], []
+    for i in range(0, len(probes), 5):
+        chunk = probes[i:i + 5]
+        recs = []
+        for j, a in enumerate(chunk):
+            s = chunk[(j + 1) % len(chunk)]
+            recs.append({"address": a, "status": "alive", "incarnationNumber": 7, "source": s})
+            want_addr.append(ids.get(a, NULL))
+            want_src.append(ids.get(s, NULL))
+        hs, tg = chunk[0], chunk[-1]
+        want_hsrc.append(ids.get(hs, NULL))
+        want_tgt.append(ids.get(tg, NULL))
+        texts.append(json.dumps({"checksum": 1, "changes": recs, "source": hs, "sourceIncarnationNumber": 2,
+                                 "target": tg}, separators=(",", ":")))
+    if thread:
+        monkeypatch.setenv("RP_WIRE_THREAD", "1")
+    d = gpu.wire_decode(m, texts)
+    assert (d["err"] == 0).all()
+    assert d["addr"].tolist() == want_addr
+    assert d["src"].tolist() == want_src
+    assert d["source"].tolist() == want_hsrc
+    assert d["target"].tolist() == want_tgt
+    m.close()
