@@ -653,9 +653,18 @@ __global__ void k_decode(In I, Names nm, Out O, uint32_t n_msgs, const uint8_t* 
 // exactly as the thread parser would (k_decode: its grammar and its error offsets) is left to
 // the thread parser: the wave kernel marks it in `slow` and k_decode picks only those up.
 constexpr uint32_t kWBuf = 8192;  // message bytes staged per wave (longer: the thread parser)
-constexpr uint32_t kWTok = 2048;  // quotes + structural characters per message
-constexpr uint32_t kWLvl = 1024;  // array-level tokens (records + separators)
-constexpr int kDecWaves = 4;
+#ifndef RP_WIRE_TOK
+#define RP_WIRE_TOK 2048
+#endif
+#ifndef RP_WIRE_LVL
+#define RP_WIRE_LVL 1024
+#endif
+#ifndef RP_WIRE_WAVES
+#define RP_WIRE_WAVES 4
+#endif
+constexpr uint32_t kWTok = RP_WIRE_TOK;  // quotes + structural characters per message
+constexpr uint32_t kWLvl = RP_WIRE_LVL;  // array-level tokens (records + separators)
+constexpr int kDecWaves = RP_WIRE_WAVES;
 #ifndef RP_WIRE_MEMBERS
 #define RP_WIRE_MEMBERS 0
 #endif
@@ -664,6 +673,7 @@ constexpr int kDecWaves = 4;
 #endif
 constexpr bool kWaveNameSplit = RP_WIRE_NAME_SPLIT != 0;  // records' names looked up together (3.36 vs 3.58 ms; 0: A/B)
 constexpr bool kWaveMembers = RP_WIRE_MEMBERS != 0;
+static_assert(!kWaveMembers || kWTok >= 2048, "the member-parallel walk keeps 1,984 B of record fields over W.dep");
 #ifndef RP_WIRE_CLS16
 #define RP_WIRE_CLS16 1
 #endif
