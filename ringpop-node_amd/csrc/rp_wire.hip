@@ -653,18 +653,14 @@ __global__ void k_decode(In I, Names nm, Out O, uint32_t n_msgs, const uint8_t* 
 // exactly as the thread parser would (k_decode: its grammar and its error offsets) is left to
 // the thread parser: the wave kernel marks it in `slow` and k_decode picks only those up.
 constexpr uint32_t kWBuf = 8192;  // message bytes staged per wave (longer: the thread parser)
-#ifndef RP_WIRE_TOK
-#define RP_WIRE_TOK 2048
-#endif
-#ifndef RP_WIRE_LVL
-#define RP_WIRE_LVL 1024
-#endif
-#ifndef RP_WIRE_WAVES
-#define RP_WIRE_WAVES 4
-#endif
-constexpr uint32_t kWTok = RP_WIRE_TOK;  // quotes + structural characters per message
-constexpr uint32_t kWLvl = RP_WIRE_LVL;  // array-level tokens (records + separators)
-constexpr int kDecWaves = RP_WIRE_WAVES;
+// Two LDS layouts. The first pass holds up to 1,280 tokens and 512 level tokens in 15.6 KB a
+// wave, so ten waves fit a CU (2.30 ms per 640 MB against 2.63 with the full layout's eight:
+// profiles/r04/r04m); a message past either bound is left (slow = 2) for a second pass with the
+// full layout (2,048 tokens, 1,024 level tokens, 19.7 KB a wave), which hands anything else it
+// cannot take to the thread parser as the first pass does.
+constexpr uint32_t kWTok = 2048, kWLvl = 1024;   // the full layout
+constexpr uint32_t kWTokS = 1280, kWLvlS = 512;  // the first pass
+constexpr int kDecWaves = 4, kDecWavesS = 2;     // waves a workgroup
 #ifndef RP_WIRE_MEMBERS
 #define RP_WIRE_MEMBERS 0
 #endif
@@ -672,23 +668,26 @@ constexpr int kDecWaves = RP_WIRE_WAVES;
 #define RP_WIRE_NAME_SPLIT 1
 #endif
 constexpr bool kWaveNameSplit = RP_WIRE_NAME_SPLIT != 0;  // records' names looked up together (3.36 vs 3.58 ms; 0: A/B)
-constexpr bool kWaveMembers = RP_WIRE_MEMBERS != 0;
-static_assert(!kWaveMembers || kWTok >= 2048, "the member-parallel walk keeps 1,984 B of record fields over W.dep");
+constexpr bool kWaveMembers = RP_WIRE_MEMBERS != 0;  // records parsed a lane per member (-DRP_WIRE_MEMBERS=1; A/B)
 #ifndef RP_WIRE_CLS16
 #define RP_WIRE_CLS16 1
 #endif
-constexpr bool kWaveCls16 = RP_WIRE_CLS16 != 0;  // classifier: 16 bytes per lane a step (0: 4 bytes; A/B)  // records parsed a lane per member (-DRP_WIRE_MEMBERS=1; A/B)
+constexpr bool kWaveCls16 = RP_WIRE_CLS16 != 0;  // classifier: 16 bytes per lane a step (0: 4 bytes; A/B)
 
-struct alignas(16) WaveLds {
+template <uint32_t TOK, uint32_t LVL>
+struct alignas(16) WaveLdsT {
+    static constexpr uint32_t kTok = TOK, kLvl = LVL;
     alignas(16) uint32_t buf[kWBuf / 4 + 2];
-    uint16_t pos[kWTok];   // token byte offset in the message
-    int8_t dep[kWTok];     // depth before the token ({ [ open, } ] close)
-    uint8_t tc[kWTok];     // the token's character
-    alignas(16) uint16_t lvl[kWLvl];  // the changes array's level tokens (the classifier's scratch before)
+    uint16_t pos[TOK];   // token byte offset in the message
+    int8_t dep[TOK];     // depth before the token ({ [ open, } ] close)
+    uint8_t tc[TOK];     // the token's character
+    alignas(16) uint16_t lvl[LVL];  // the changes array's level tokens (the classifier's scratch before)
     uint64_t scal[kWBuf / 64 + 16];  // buffer bytes outside strings that are neither tokens nor
                                     // whitespace (bit sh + i: message byte i)
     uint16_t op1[32], cl2[32];      // openers at depth 1 / closers at depth 2, in order: the k-th pair
 };
+using WaveLds = WaveLdsT<kWTok, kWLvl>;
+using WaveLdsS = WaveLdsT<kWTokS, kWLvlS>;
 
 // SWAR over the four bytes of a dword: bit 7 of byte j set where byte j == c
 __device__ __forceinline__ uint32_t swar_eq(uint32_t x, uint8_t c) {
@@ -793,8 +792,9 @@ __device__ uint32_t name_find_lds(const Names& nm, const uint32_t* d, uint32_t i
     }
 }
 
+template <class WL>
 struct WaveMsg {
-    const WaveLds* W;
+    const WL* W;
     const uint8_t* b;  // message byte 0 in LDS
     uint32_t len, ntok;
     uint32_t sh;       // byte 0's offset in the staged dwords
@@ -974,8 +974,8 @@ struct RecF {
 // LDS trips: its tokens, then its key's and value's bytes, then the name lookups.
 // DEFER: the address is not looked up (the caller looks up every record's address and source
 // at once, a name per lane) and the source's byte offset | length << 16 is left in sref.
-template <bool DEFER>
-__device__ bool wave_record(const WaveMsg& M, const Names& nm, uint64_t base, uint32_t t0, uint32_t t1, RecF& f,
+template <bool DEFER, class WL>
+__device__ bool wave_record(const WaveMsg<WL>& M, const Names& nm, uint64_t base, uint32_t t0, uint32_t t1, RecF& f,
                             uint32_t& sref) {
     f.addr = NULL_ID;
     f.src = NULL_ID;
@@ -1074,11 +1074,13 @@ __device__ bool wave_record(const WaveMsg& M, const Names& nm, uint64_t base, ui
 // separators, record closes) at the top of W.lvl, below nothing of the level list (W.lvl[0,
 // 2 nrec - 1), which wave_record needs); the per-record fields go over the W.dep bytes, the array
 // being known to hold no nested value (wave_record reads W.dep only for those).
-__device__ bool wave_records_mp(const WaveMsg& M, WaveLds& W, const Names& nm, uint64_t base, uint32_t nb,
+template <class WL>
+__device__ bool wave_records_mp(const WaveMsg<WL>& M, WL& W, const Names& nm, uint64_t base, uint32_t nb,
                                 uint32_t nrec, RecF* __restrict__ out, uint32_t lane) {
     const uint64_t lt = (1ull << lane) - 1ull;
-    const uint16_t* BT = W.lvl + kWLvl - 1;  // boundary i at BT[-i]
-    if (nb > kWLvl || nb < 2) return false;
+    static_assert(WL::kTok >= 2048, "the record fields take 1,984 B over W.dep");
+    const uint16_t* BT = W.lvl + WL::kLvl - 1;  // boundary i at BT[-i]
+    if (nb > WL::kLvl || nb < 2) return false;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     // per-record fields over the W.dep bytes (1,984 of its 2,048)
@@ -1260,18 +1262,23 @@ __device__ unsigned long long g_wprof[8];
 // count is needed first) and its count; a scan of the counts gives the record offsets and
 // k_decode_place moves the records to them. A message the wave parser does not accept is
 // counted by the wave's lane 0 with the thread parser and marked slow; k_decode fills those.
-__global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, Out O, uint32_t n_msgs,
-                                                                 uint64_t vb, uint64_t ve, RecF* __restrict__ stash,
-                                                                 uint8_t* __restrict__ slow,
-                                                                 uint32_t* __restrict__ n_by_waves) {
-    __shared__ WaveLds lds[kDecWaves];
+// PASS 0: the only pass; 1: the first of two (a message past the layout's token or level bound
+// is marked slow = 2, nothing else done for it); 2: the second (only the messages marked 2)
+template <class WL, int WAVES, int PASS>
+__global__ __launch_bounds__(64 * WAVES) void k_decode_wave(In I, Names nm, Out O, uint32_t n_msgs, uint64_t vb,
+                                                            uint64_t ve, RecF* __restrict__ stash,
+                                                            uint8_t* __restrict__ slow,
+                                                            uint32_t* __restrict__ n_by_waves) {
+    __shared__ WL lds[WAVES];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    WaveLds& W = lds[wv];
+    WL& W = lds[wv];
     const uint64_t lt = (1ull << lane) - 1ull;
     uint32_t nwave = 0;  // messages this wave parsed itself (RP_WIRE_DEBUG)
     uint32_t nmp = 0;    // of them, records parsed a lane per member
-    const uint32_t nwaves = gridDim.x * kDecWaves;
-    for (uint32_t m = blockIdx.x * kDecWaves + wv; m < n_msgs; m += nwaves) {
+    const uint32_t nwaves = gridDim.x * WAVES;
+    for (uint32_t m = blockIdx.x * WAVES + wv; m < n_msgs; m += nwaves) {
+        if (PASS == 2 && slow[m] != 2) continue;  // wave-uniform
+        bool retry = false;  // PASS 1: past this layout's bounds
 #ifdef RP_WIRE_PROF
         uint64_t tprof = clock64();
 #endif
@@ -1380,7 +1387,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
 #pragma unroll
                 for (int j = 0; j < 16; j++)
                     if ((tm >> j) & 1u) {
-                        if (idx < kWTok) {
+                        if (idx < WL::kTok) {
                             W.pos[idx] = (uint16_t)(4 * dw0 + j - sh);
                             W.tc[idx] = (uint8_t)(x[j >> 2] >> (8 * (j & 3)));
                         }
@@ -1430,7 +1437,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
     #pragma unroll
                 for (int j = 0; j < 4; j++)
                     if ((tm >> j) & 1u) {
-                        if (idx < kWTok) {
+                        if (idx < WL::kTok) {
                             W.pos[idx] = (uint16_t)(4 * dw + j - sh);
                             W.tc[idx] = (uint8_t)(x >> (8 * j));
                         }
@@ -1456,7 +1463,8 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
                 quotes += (uint32_t)__popcll(Po);
             }
         }
-        ok = ok && !bad && ntok <= kWTok && (quotes & 1u) == 0 && ntok > 0;
+        retry = ok && !bad && ntok > WL::kTok;
+        ok = ok && !bad && ntok <= WL::kTok && (quotes & 1u) == 0 && ntok > 0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         WPROF(1);
         // depth before every token
@@ -1483,7 +1491,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
         ok = ok && !neg && depth == 0 && nop1 <= 32 && nop1 == ncl2;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         WPROF(2);
-        WaveMsg M{&W, B, len, ntok, sh};
+        WaveMsg<WL> M{&W, B, len, ntok, sh};
         // the top level, wave-uniformly: [records] or {key: value, ...}
         uint32_t arr = ntok, arr_end = ntok;  // the changes array's '[' and ']'
         uint32_t ck = 0, msrc = NULL_ID, mtgt = NULL_ID;
@@ -1598,7 +1606,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
                 const bool lv = in && dt == d + 1;
                 const uint64_t L = __ballot(lv);
                 const uint32_t idx = nl + (uint32_t)__popcll(L & lt);
-                if (lv && idx < kWLvl) W.lvl[idx] = (uint16_t)t;
+                if (lv && idx < WL::kLvl) W.lvl[idx] = (uint16_t)t;
                 nl += (uint32_t)__popcll(L);
                 if (kWaveMembers) {
                     // the member boundaries too: record opens (level d + 1), member separators and
@@ -1608,17 +1616,18 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
                     deep |= in && dt > d + 2;
                     const uint64_t mb = __ballot(b);
                     const uint32_t ib = nb + (uint32_t)__popcll(mb & lt);
-                    if (b && ib + nl < kWLvl) W.lvl[kWLvl - 1 - ib] = (uint16_t)t;
+                    if (b && ib + nl < WL::kLvl) W.lvl[WL::kLvl - 1 - ib] = (uint16_t)t;
                     nb += (uint32_t)__popcll(mb);
                 }
             }
-            nb = (__ballot(deep) != 0 || nl + nb > kWLvl) ? ~0u : nb;
+            nb = (__ballot(deep) != 0 || nl + nb > WL::kLvl) ? ~0u : nb;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             // n records give 2n - 1 level tokens; an empty array none
             if (nl == 0)
                 ok = arr_end == arr + 1 && M.clean(W.pos[arr], W.pos[arr_end]);
             else
-                ok = nl < kWLvl && (nl & 1u) == 1u;
+                ok = nl < WL::kLvl && (nl & 1u) == 1u;
+            retry = nl >= WL::kLvl;
             bool pat = true;
             for (uint32_t j = lane; ok && j < nl; j += 64) {
                 const uint32_t t = W.lvl[j];
@@ -1642,8 +1651,10 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
         ok = ok && nrec <= s1 - s0;
         bool rok = true;
         bool mp = false;
-        if (ok && nrec > 0 && nrec <= 64 && kWaveMembers)  // a lane per member (wave-uniform)
-            mp = wave_records_mp(M, W, nm, b0, nb, nrec, stash + s0, lane);
+        if constexpr (kWaveMembers && WL::kTok >= 2048) {
+            if (ok && nrec > 0 && nrec <= 64)  // a lane per member (wave-uniform)
+                mp = wave_records_mp(M, W, nm, b0, nb, nrec, stash + s0, lane);
+        }
         nmp += mp ? 1u : 0u;
         if (!mp && kWaveNameSplit && nrec <= 32) {
             // a lane per record, then its address and source names looked up together: lanes
@@ -1678,10 +1689,11 @@ __global__ __launch_bounds__(64 * kDecWaves) void k_decode_wave(In I, Names nm, 
         ok = ok && __ballot(!rok) == 0;
         WPROF(5);
         nwave += ok ? 1u : 0u;
+        retry = PASS == 1 && !ok && retry;
         if (lane == 0) {
-            slow[m] = ok ? 0 : 1;
+            slow[m] = ok ? 0 : retry ? 2 : 1;
             // the record count (the thread parser's, 0 when the message does not parse)
-            O.cnt[m] = ok ? nrec : thread_parse<false>(I, nm, O, m, 0, 0);
+            O.cnt[m] = ok ? nrec : retry ? 0u : thread_parse<false>(I, nm, O, m, 0, 0);
             if (ok) {
                 O.err[m] = 0;
                 if (O.m_checksum) O.m_checksum[m] = ck;
@@ -1838,9 +1850,11 @@ int rp_wire_decode_dev(rp_members* m, const uint8_t* d_buf, const uint64_t* d_ms
             vb += reinterpret_cast<uint64_t>(d_buf);
             ve += reinterpret_cast<uint64_t>(d_buf);
             // a wave per message (3.73 ms at 100 k messages against 3.75-3.86 with 512-8192
-            // workgroups striding; tools/wire_grid.sh); RP_WIRE_GRID caps it (A/B)
-            const unsigned g = rp::grid_for(n_msgs, rp::kDecWaves,
-                                            (unsigned)rp::env_pos("RP_WIRE_GRID", 1u << 20));
+            // workgroups striding; tools/wire_grid.sh); RP_WIRE_GRID caps it (A/B).
+            // RP_WIRE_ONEPASS=1: the full layout alone (A/B)
+            const bool onepass = getenv("RP_WIRE_ONEPASS") != nullptr;
+            const unsigned gcap = (unsigned)rp::env_pos("RP_WIRE_GRID", 1u << 20);
+            const unsigned g = rp::grid_for(n_msgs, onepass ? rp::kDecWaves : rp::kDecWavesS, gcap);
             const uint64_t nslots = (ve - vb) / rp::kMinRec + n_msgs + 1;
             ws->wire_stash.reserve(nslots * sizeof(rp::RecF));
             ws->wire_slow.reserve(n_msgs);
@@ -1852,8 +1866,20 @@ int rp_wire_decode_dev(rp_members* m, const uint8_t* d_buf, const uint64_t* d_ms
                 nbw.reserve(2);
                 RP_HIP(hipMemsetAsync(nbw.p, 0, 8, st));
             }
-            hipLaunchKernelGGL(rp::k_decode_wave, dim3(g), dim3(64 * rp::kDecWaves), 0, st, I, nm, O, n_msgs, vb, ve,
-                               stash, slow, dbg ? nbw.p : nullptr);
+            if (onepass) {
+                hipLaunchKernelGGL((rp::k_decode_wave<rp::WaveLds, rp::kDecWaves, 0>), dim3(g),
+                                   dim3(64 * rp::kDecWaves), 0, st, I, nm, O, n_msgs, vb, ve, stash, slow,
+                                   dbg ? nbw.p : nullptr);
+            } else {
+                hipLaunchKernelGGL((rp::k_decode_wave<rp::WaveLdsS, rp::kDecWavesS, 1>), dim3(g),
+                                   dim3(64 * rp::kDecWavesS), 0, st, I, nm, O, n_msgs, vb, ve, stash, slow,
+                                   dbg ? nbw.p : nullptr);
+                // the messages past the first layout's bounds: 1,024 workgroups striding the flags
+                hipLaunchKernelGGL((rp::k_decode_wave<rp::WaveLds, rp::kDecWaves, 2>),
+                                   dim3(rp::grid_for(n_msgs, rp::kDecWaves, std::min(gcap, 1024u))),
+                                   dim3(64 * rp::kDecWaves), 0, st, I, nm, O, n_msgs, vb, ve, stash, slow,
+                                   dbg ? nbw.p : nullptr);
+            }
             RP_HIP(hipGetLastError());
             rp::scan_exclusive_u32(d_msg_rec_off, d_msg_rec_off, n_msgs, st, *ws);
             hipLaunchKernelGGL(rp::k_decode_place, dim3(rp::grid_for((uint64_t)n_msgs * 64, 256, 8192)), dim3(256), 0,

@@ -434,3 +434,59 @@ def test_decode_name_lengths_around_the_inline_prefix(gpu, monkeypatch, thread):
     assert d["source"].tolist() == want_hsrc
     assert d["target"].tolist() == want_tgt
     m.close()
+
+
+def _count_tokens(t):
+    """Quotes and the structural characters outside strings (the wave decoder's tokens)."""
+    n, ins, esc = 0, False, False
+    for ch in t:
+        if ins:
+            if esc:
+                esc = False
+            elif ch == "\\":
+                esc = True
+            elif ch == '"':
+                ins = False
+                n += 1
+        elif ch == '"':
+            ins = True
+            n += 1
+        elif ch in "{}[]:,":
+            n += 1
+    return n
+
+
+def test_two_pass_layouts_match_thread_parser(gpu, monkeypatch, capfd):
+    """The wave decoder's first pass holds 1,280 tokens a message; longer token lists are left to
+    the second pass (2,048 tokens), past that to the thread parser. Changes arrays of 40..120 short
+    records (about 740 to 2,180 tokens in under 8 KB) decode identically through both passes, the
+    full layout alone (RP_WIRE_ONEPASS=1) and the thread parser, and the waves take every message
+    of at most 2,048 tokens."""
+    rng = random.Random(9)
+    names = ["n%d" % i for i in range(200)]
+    m = gpu.Membership()
+    m.intern(names)
+    texts = []
+    for k in range(40, 124, 4):
+        recs = [{"address": rng.choice(names + ["zz%d" % k]), "status": rng.choice(list(ST)),
+                 "incarnationNumber": rng.randrange(10 ** 6)} for _ in range(k)]
+        texts.append(json.dumps({"checksum": k, "changes": recs, "source": names[k], "sourceIncarnationNumber": 1},
+                                separators=(",", ":")))
+    toks = [_count_tokens(t) for t in texts]
+    assert min(toks) < 1280 < max(toks) and max(toks) > 2048 and any(1280 < x <= 2048 for x in toks)
+    assert all(len(t) <= 8192 for t in texts)
+    monkeypatch.setenv("RP_WIRE_DEBUG", "1")
+    capfd.readouterr()
+    d2 = gpu.wire_decode(m, texts)
+    line = [x for x in capfd.readouterr().err.splitlines() if "by waves" in x][-1]
+    assert int(line.split()[3]) == sum(1 for x in toks if x <= 2048), line
+    monkeypatch.setenv("RP_WIRE_ONEPASS", "1")
+    d1 = gpu.wire_decode(m, texts)
+    monkeypatch.delenv("RP_WIRE_ONEPASS")
+    monkeypatch.setenv("RP_WIRE_THREAD", "1")
+    dt = gpu.wire_decode(m, texts)
+    for k in dt:
+        assert np.array_equal(d2[k], dt[k]), k
+        assert np.array_equal(d1[k], dt[k]), k
+    assert (dt["err"] == 0).all()
+    m.close()
