@@ -24,6 +24,7 @@ struct Scratch {
     // the wire decoder's record stash and slow-path flags (grow-only: a 640 MB decode keeps
     // ~750 MB here rather than allocating and freeing it per call)
     DevBuf<uint8_t> wire_stash, wire_slow;
+    DevBuf<uint32_t> wire_retry;  // messages the decoder's first pass left to its second
     uint32_t epoch = 0;
     // the stream that last used this scratch: a launch on another stream first waits for it
     // (use_on), so two streams never interleave tickets or look-back words

@@ -673,6 +673,10 @@ constexpr bool kWaveMembers = RP_WIRE_MEMBERS != 0;  // records parsed a lane pe
 #define RP_WIRE_CLS16 1
 #endif
 constexpr bool kWaveCls16 = RP_WIRE_CLS16 != 0;  // classifier: 16 bytes per lane a step (0: 4 bytes; A/B)
+#ifndef RP_WIRE_BODY_LANES
+#define RP_WIRE_BODY_LANES 1
+#endif
+constexpr bool kWaveBodyLanes = RP_WIRE_BODY_LANES != 0;  // body members a lane each (0: the serial walk; A/B)
 
 template <uint32_t TOK, uint32_t LVL>
 struct alignas(16) WaveLdsT {
@@ -685,6 +689,7 @@ struct alignas(16) WaveLdsT {
     uint64_t scal[kWBuf / 64 + 16];  // buffer bytes outside strings that are neither tokens nor
                                     // whitespace (bit sh + i: message byte i)
     uint16_t op1[32], cl2[32];      // openers at depth 1 / closers at depth 2, in order: the k-th pair
+    uint16_t sep1[64];              // the body's member separators (',' at depth 1), in order
 };
 using WaveLds = WaveLdsT<kWTok, kWLvl>;
 using WaveLdsS = WaveLdsT<kWTokS, kWLvlS>;
@@ -1268,13 +1273,16 @@ template <class WL, int WAVES, int PASS>
 __global__ __launch_bounds__(64 * WAVES) void k_decode_wave(In I, Names nm, Out O, uint32_t n_msgs, uint64_t vb,
                                                             uint64_t ve, RecF* __restrict__ stash,
                                                             uint8_t* __restrict__ slow,
-                                                            uint32_t* __restrict__ n_by_waves) {
+                                                            uint32_t* __restrict__ n_by_waves,
+                                                            uint32_t* __restrict__ n_retry) {
+    if (PASS == 2 && __builtin_nontemporal_load(n_retry) == 0) return;  // nothing left by the first pass
     __shared__ WL lds[WAVES];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     WL& W = lds[wv];
     const uint64_t lt = (1ull << lane) - 1ull;
     uint32_t nwave = 0;  // messages this wave parsed itself (RP_WIRE_DEBUG)
     uint32_t nmp = 0;    // of them, records parsed a lane per member
+    uint32_t nretry = 0;  // PASS 1: messages left to the second pass
     const uint32_t nwaves = gridDim.x * WAVES;
     for (uint32_t m = blockIdx.x * WAVES + wv; m < n_msgs; m += nwaves) {
         if (PASS == 2 && slow[m] != 2) continue;  // wave-uniform
@@ -1470,7 +1478,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_decode_wave(In I, Names nm, Out 
         // depth before every token
         int32_t depth = 0;
         bool neg = false;
-        uint32_t nop1 = 0, ncl2 = 0;
+        uint32_t nop1 = 0, ncl2 = 0, nsep1 = 0;
         for (uint32_t t0 = 0; ok && t0 < ntok; t0 += 64) {
             const uint32_t t = t0 + lane;
             const uint8_t ch = t < ntok ? W.tc[t] : (uint8_t)' ';
@@ -1484,6 +1492,10 @@ __global__ __launch_bounds__(64 * WAVES) void k_decode_wave(In I, Names nm, Out 
             const uint32_t io = nop1 + (uint32_t)__popcll(O1 & lt), ic = ncl2 + (uint32_t)__popcll(C2 & lt);
             if (((O1 >> lane) & 1ull) && io < 32) W.op1[io] = (uint16_t)t;
             if (((C2 >> lane) & 1ull) && ic < 32) W.cl2[ic] = (uint16_t)t;
+            const uint64_t S1 = __ballot(t < ntok && ch == ',' && d == 1);
+            const uint32_t is = nsep1 + (uint32_t)__popcll(S1 & lt);
+            if (((S1 >> lane) & 1ull) && is < 64) W.sep1[is] = (uint16_t)t;
+            nsep1 += (uint32_t)__popcll(S1);
             nop1 += (uint32_t)__popcll(O1);
             ncl2 += (uint32_t)__popcll(C2);
             depth += __popcll(Op) - __popcll(Cl);
@@ -1506,6 +1518,89 @@ __global__ __launch_bounds__(64 * WAVES) void k_decode_wave(In I, Names nm, Out 
                 ok = M.tch(last) == ']';
                 arr = 0;
                 arr_end = last;
+            } else if (ok && c == '{' && kWaveBodyLanes && nsep1 < 64) {
+                // a lane per body member (member j: after separator j - 1 up to separator j, the
+                // last one up to the closing '}'), with the serial walk's checks and its results:
+                // the last of a repeated key wins, a repeated or missing changes array fails
+                ok = M.tch(last) == '}';
+                const uint32_t ns = nsep1;
+                const bool act = ok && lane <= ns;
+                bool okl = act, isopen = false;
+                int kind = -1;
+                uint32_t t = 1, e = last, nx = ntok, sref = ~0u, a0 = ntok, a1 = ntok;
+                int64_t x = 0;
+                uint8_t ps = 0xFF;
+                if (act) {
+                    t = lane == 0 ? 1u : (uint32_t)W.sep1[lane - 1] + 1u;
+                    e = lane < ns ? (uint32_t)W.sep1[lane] : last;
+                    const uint8_t c0 = M.tch(t), c1 = M.tch(t + 1), c2 = M.tch(t + 2);
+                    okl = t + 2 < e && (c0 == '"') & (c1 == '"') & (c2 == ':') && M.clean(W.pos[t - 1], W.pos[t]) &&
+                          M.clean(W.pos[t + 1], W.pos[t + 2]);
+                    if (okl) {
+                        kind = M.top_kind_w(W.pos[t] + 1, (uint32_t)(W.pos[t + 1] - W.pos[t] - 1));
+                        isopen = t + 3 < last && wave_isopen(M.tch(t + 3));
+                    }
+                }
+                // the k-th nested value of a changes / unknown member is the k-th depth-1 opener
+                const uint64_t Mo = __ballot(okl && isopen && (kind == 1 || kind == 0));
+                if (okl) {
+                    const uint32_t v = t + 3;
+                    const uint32_t k = (uint32_t)__popcll(Mo & lt);
+                    if (kind == 1) {
+                        okl = isopen && M.tch(v) == '[' && M.clean(W.pos[v - 1], W.pos[v]) && k < nop1 && W.op1[k] == v;
+                        a0 = v;
+                        a1 = okl ? (uint32_t)W.cl2[k] : ntok;
+                        okl = okl && a1 < last && M.tch(a1) == ']';
+                        nx = a1 + 1;
+                    } else if (kind == 2 || kind == 3) {
+                        okl = M.int_tok(t + 2, x);
+                        nx = v;
+                    } else if (kind == 4) {
+                        uint32_t s0, e0;
+                        okl = M.scalar(t + 2, s0, e0);
+                        if (okl && e0 - s0 == 4 && B[s0] == 't' && B[s0 + 1] == 'r' && B[s0 + 2] == 'u' && B[s0 + 3] == 'e')
+                            ps = 1;
+                        else if (okl && e0 - s0 == 5 && B[s0] == 'f' && B[s0 + 1] == 'a' && B[s0 + 2] == 'l' &&
+                                 B[s0 + 3] == 's' && B[s0 + 4] == 'e')
+                            ps = 0;
+                        else
+                            okl = false;
+                        nx = v;
+                    } else if (kind == 5 || kind == 6) {
+                        okl = v + 1 < last && M.tch(v) == '"' && M.clean(W.pos[v - 1], W.pos[v]);
+                        if (okl) sref = (uint32_t)(W.pos[v] + 1) | ((uint32_t)(W.pos[v + 1] - W.pos[v] - 1) << 16);
+                        nx = v + 2;
+                    } else if (isopen) {
+                        okl = k < nop1 && W.op1[k] == v && M.clean(W.pos[v - 1], W.pos[v]);
+                        nx = okl ? (uint32_t)W.cl2[k] + 1u : ntok;
+                    } else {
+                        nx = M.skip(v);
+                    }
+                    okl = okl && nx == e && (M.clean(W.pos[nx - 1], W.pos[nx]) || M.tch(nx - 1) == ':');
+                }
+                const uint64_t K1 = __ballot(okl && kind == 1);
+                ok = ok && __ballot(act && !okl) == 0 && __popcll(K1) == 1;
+                if (ok) {
+                    const int l1 = __builtin_ctzll(K1);
+                    arr = __shfl(a0, l1, 64);
+                    arr_end = __shfl(a1, l1, 64);
+                    const uint64_t K2 = __ballot(kind == 2), K3 = __ballot(kind == 3), K4 = __ballot(kind == 4),
+                                   K5 = __ballot(kind == 5), K6 = __ballot(kind == 6);
+                    const int w2 = 63 - __builtin_clzll(K2 | 1ull), w3 = 63 - __builtin_clzll(K3 | 1ull),
+                              w4 = 63 - __builtin_clzll(K4 | 1ull), w5 = 63 - __builtin_clzll(K5 | 1ull),
+                              w6 = 63 - __builtin_clzll(K6 | 1ull);
+                    const int64_t x2 = __shfl(x, w2, 64), x3 = __shfl(x, w3, 64);
+                    const uint32_t p4 = __shfl((uint32_t)ps, w4, 64);
+                    if (K2) ck = (uint32_t)x2;
+                    if (K3) msinc = x3;
+                    if (K4) pst = (uint8_t)p4;
+                    // the source and target names, looked up side by side
+                    const bool wn = (K5 && (int)lane == w5) || (K6 && (int)lane == w6);
+                    const uint32_t id = wn ? M.find(nm, sref & 0xFFFFu, sref >> 16) : NULL_ID;
+                    const uint32_t i5 = __shfl(id, w5, 64), i6 = __shfl(id, w6, 64);
+                    if (K5) msrc = i5;
+                    if (K6) mtgt = i6;
+                }
             } else if (ok && c == '{') {
                 ok = M.tch(last) == '}';
                 uint32_t t = 1, kop = 0;  // kop: the next depth-1 opener, in walk order
@@ -1690,6 +1785,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_decode_wave(In I, Names nm, Out 
         WPROF(5);
         nwave += ok ? 1u : 0u;
         retry = PASS == 1 && !ok && retry;
+        nretry += retry ? 1u : 0u;
         if (lane == 0) {
             slow[m] = ok ? 0 : retry ? 2 : 1;
             // the record count (the thread parser's, 0 when the message does not parse)
@@ -1706,6 +1802,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_decode_wave(In I, Names nm, Out 
         WPROF(6);
         __builtin_amdgcn_wave_barrier();
     }
+    if (PASS == 1 && lane == 0 && nretry) atomicAdd(n_retry, nretry);
     if (n_by_waves && lane == 0 && nwave) atomicAdd(n_by_waves, nwave);
     if (n_by_waves && lane == 0 && nmp) atomicAdd(n_by_waves + 1, nmp);
 }
@@ -1860,6 +1957,8 @@ int rp_wire_decode_dev(rp_members* m, const uint8_t* d_buf, const uint64_t* d_ms
             ws->wire_slow.reserve(n_msgs);
             rp::RecF* stash = reinterpret_cast<rp::RecF*>(ws->wire_stash.p);
             uint8_t* slow = ws->wire_slow.p;
+            ws->wire_retry.reserve(1);
+            RP_HIP(hipMemsetAsync(ws->wire_retry.p, 0, 4, st));
             const bool dbg = getenv("RP_WIRE_DEBUG") != nullptr;
             rp::DevBuf<uint32_t> nbw;
             if (dbg) {
@@ -1869,16 +1968,16 @@ int rp_wire_decode_dev(rp_members* m, const uint8_t* d_buf, const uint64_t* d_ms
             if (onepass) {
                 hipLaunchKernelGGL((rp::k_decode_wave<rp::WaveLds, rp::kDecWaves, 0>), dim3(g),
                                    dim3(64 * rp::kDecWaves), 0, st, I, nm, O, n_msgs, vb, ve, stash, slow,
-                                   dbg ? nbw.p : nullptr);
+                                   dbg ? nbw.p : nullptr, ws->wire_retry.p);
             } else {
                 hipLaunchKernelGGL((rp::k_decode_wave<rp::WaveLdsS, rp::kDecWavesS, 1>), dim3(g),
                                    dim3(64 * rp::kDecWavesS), 0, st, I, nm, O, n_msgs, vb, ve, stash, slow,
-                                   dbg ? nbw.p : nullptr);
+                                   dbg ? nbw.p : nullptr, ws->wire_retry.p);
                 // the messages past the first layout's bounds: 1,024 workgroups striding the flags
                 hipLaunchKernelGGL((rp::k_decode_wave<rp::WaveLds, rp::kDecWaves, 2>),
                                    dim3(rp::grid_for(n_msgs, rp::kDecWaves, std::min(gcap, 1024u))),
                                    dim3(64 * rp::kDecWaves), 0, st, I, nm, O, n_msgs, vb, ve, stash, slow,
-                                   dbg ? nbw.p : nullptr);
+                                   dbg ? nbw.p : nullptr, ws->wire_retry.p);
             }
             RP_HIP(hipGetLastError());
             rp::scan_exclusive_u32(d_msg_rec_off, d_msg_rec_off, n_msgs, st, *ws);

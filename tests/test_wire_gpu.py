@@ -348,7 +348,7 @@ def _fuzz_texts(cases, seed):
         if not t:
             continue
         i = rng.randrange(len(t))
-        kind = rng.randrange(6)
+        kind = rng.randrange(9)
         if kind == 0:
             mutants.append(t[:i] + t[i + 1:])  # delete
         elif kind == 1:
@@ -359,8 +359,14 @@ def _fuzz_texts(cases, seed):
             mutants.append(t.replace("}", ",}", 1))  # trailing comma
         elif kind == 4:
             mutants.append(t.replace('"status"', '"status":"alive","status"', 1))  # duplicate key
-        else:
+        elif kind == 5:
             mutants.append(t + rng.choice([" ", "x", "]", ",", "{}"]))  # trailing bytes
+        elif kind == 6:  # a repeated body key: the last one wins
+            mutants.append(t.replace('"source"', '"source":"%s","source"' % rng.choice(["x", "127.0.0.1:3001"]), 1))
+        elif kind == 7:
+            mutants.append(t.replace('"checksum"', '"checksum":5,"checksum"', 1))
+        else:  # a repeated changes array
+            mutants.append(t.replace('"changes"', '"changes":[],"changes"', 1))
     return out + mutants
 
 
