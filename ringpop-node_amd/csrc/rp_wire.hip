@@ -673,6 +673,9 @@ constexpr bool kWaveMembers = RP_WIRE_MEMBERS != 0;  // records parsed a lane pe
 #define RP_WIRE_CLS16 1
 #endif
 constexpr bool kWaveCls16 = RP_WIRE_CLS16 != 0;  // classifier: 16 bytes per lane a step (0: 4 bytes; A/B)
+#ifndef RP_WIRE_ABL
+#define RP_WIRE_ABL 0  // timing ablations (results wrong): 1 no body name lookups, 2 no record name lookups
+#endif
 #ifndef RP_WIRE_BODY_LANES
 #define RP_WIRE_BODY_LANES 1
 #endif
@@ -690,6 +693,7 @@ struct alignas(16) WaveLdsT {
                                     // whitespace (bit sh + i: message byte i)
     uint16_t op1[32], cl2[32];      // openers at depth 1 / closers at depth 2, in order: the k-th pair
     uint16_t sep1[64];              // the body's member separators (',' at depth 1), in order
+    alignas(16) uint32_t hprobe[16];  // the body's source / target first probe slots (LDS DMA)
 };
 using WaveLds = WaveLdsT<kWTok, kWLvl>;
 using WaveLdsS = WaveLdsT<kWTokS, kWLvlS>;
@@ -769,32 +773,54 @@ __device__ bool bytes_eq_lds(const uint8_t* gp, const uint32_t* d, uint32_t ib, 
 }
 
 // name_find over the staged bytes: the string's first kNameInline bytes are compared with the
-// slot's copy (one 32-byte read a probe); only a longer name reads the rest of its bytes
-__device__ uint32_t name_find_lds(const Names& nm, const uint32_t* d, uint32_t ib, uint32_t len) {
+// slot's copy (one 32-byte read a probe); only a longer name reads the rest of its bytes.
+// name_probe: the probe sequence from a slot whose 32 bytes (a, b) are already loaded; the
+// first slot is compared inline, a collision's further probes (rare at load factor <= 1/2) out
+// of line.
+__device__ __forceinline__ bool name_slot_eq(const Names& nm, const uint32_t* d, uint32_t ib, uint32_t len, uint4 a,
+                                             uint4 b) {
     constexpr uint32_t kIn = NameTable::kNameInline;
-    uint32_t slot = fh::hash32(LdsSrc{d, ib}, len) & nm.hmask;
-    uint32_t sw[kIn / 4];
-    {
-        const uint32_t* l = d + (ib >> 2);
-        uint32_t L[kIn / 4 + 1];
+    const uint32_t* l = d + (ib >> 2);
+    uint32_t L[kIn / 4 + 1];
 #pragma unroll
-        for (uint32_t j = 0; j <= kIn / 4; j++) L[j] = l[j];
+    for (uint32_t j = 0; j <= kIn / 4; j++) L[j] = l[j];
+    const uint32_t bw[kIn / 4] = {a.w, b.x, b.y, b.z, b.w};
+    uint32_t dd = 0;
 #pragma unroll
-        for (uint32_t j = 0; j < kIn / 4; j++) {
-            const uint32_t o = 4 * j;
-            const uint32_t m = o >= len ? 0u : len - o >= 4 ? ~0u : (1u << (8 * (len - o))) - 1u;
-            sw[j] = __builtin_amdgcn_alignbyte(L[j + 1], L[j], ib & 3u) & m;
-        }
+    for (uint32_t j = 0; j < kIn / 4; j++) {
+        const uint32_t o = 4 * j;
+        const uint32_t m = o >= len ? 0u : len - o >= 4 ? ~0u : (1u << (8 * (len - o))) - 1u;
+        dd |= (__builtin_amdgcn_alignbyte(L[j + 1], L[j], ib & 3u) & m) ^ bw[j];
     }
+    return a.y == len && dd == 0 && (len <= kIn || bytes_eq_lds(nm.bytes + a.z + kIn, d, ib + kIn, len - kIn));
+}
+
+__device__ uint32_t name_probe_more(const Names& nm, const uint32_t* d, uint32_t ib, uint32_t len,
+                                                 uint32_t slot) {
     while (true) {
+        slot = (slot + 1) & nm.hmask;
         const uint4* w = reinterpret_cast<const uint4*>(nm.hslot + (uint64_t)NameTable::kSlotWords * slot);
         const uint4 a = w[0], b = w[1];
         if (a.x == NULL_ID) return NULL_ID;
-        const uint32_t dd = (a.w ^ sw[0]) | (b.x ^ sw[1]) | (b.y ^ sw[2]) | (b.z ^ sw[3]) | (b.w ^ sw[4]);
-        if (a.y == len && dd == 0 && (len <= kIn || bytes_eq_lds(nm.bytes + a.z + kIn, d, ib + kIn, len - kIn)))
-            return a.x;
-        slot = (slot + 1) & nm.hmask;
+        if (name_slot_eq(nm, d, ib, len, a, b)) return a.x;
     }
+}
+
+__device__ __forceinline__ uint32_t name_probe(const Names& nm, const uint32_t* d, uint32_t ib, uint32_t len,
+                                               uint32_t slot, uint4 a, uint4 b) {
+    if (a.x == NULL_ID) return NULL_ID;
+    if (name_slot_eq(nm, d, ib, len, a, b)) return a.x;
+    return name_probe_more(nm, d, ib, len, slot);
+}
+
+__device__ __forceinline__ uint32_t name_slot(const Names& nm, const uint32_t* d, uint32_t ib, uint32_t len) {
+    return fh::hash32(LdsSrc{d, ib}, len) & nm.hmask;
+}
+
+__device__ uint32_t name_find_lds(const Names& nm, const uint32_t* d, uint32_t ib, uint32_t len) {
+    const uint32_t slot = name_slot(nm, d, ib, len);
+    const uint4* w = reinterpret_cast<const uint4*>(nm.hslot + (uint64_t)NameTable::kSlotWords * slot);
+    return name_probe(nm, d, ib, len, slot, w[0], w[1]);
 }
 
 template <class WL>
@@ -1507,6 +1533,22 @@ __global__ __launch_bounds__(64 * WAVES) void k_decode_wave(In I, Names nm, Out 
         // the top level, wave-uniformly: [records] or {key: value, ...}
         uint32_t arr = ntok, arr_end = ntok;  // the changes array's '[' and ']'
         uint32_t ck = 0, msrc = NULL_ID, mtgt = NULL_ID;
+        uint32_t href5 = ~0u, href6 = ~0u;  // the body's source / target (offset | length << 16), to look up
+        uint32_t hslot = 0;                 // lanes 0 / 1: their name's first slot (DMA'd to W.hprobe)
+        auto body_names = [&]() {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the probes' DMA
+            uint32_t id = NULL_ID;
+            const uint32_t r = lane == 0 ? href5 : lane == 1 ? href6 : ~0u;
+            if (r != ~0u) {
+                const uint4 a = *reinterpret_cast<const uint4*>(&W.hprobe[4 * lane]);
+                const uint4 b = *reinterpret_cast<const uint4*>(&W.hprobe[8 + 4 * lane]);
+                id = name_probe(nm, W.buf, sh + (r & 0xFFFFu), r >> 16, hslot, a, b);
+            }
+            const uint32_t h5 = __shfl(id, 0, 64), h6 = __shfl(id, 1, 64);
+            if (href5 != ~0u) msrc = h5;
+            if (href6 != ~0u) mtgt = h6;
+            href5 = href6 = ~0u;
+        };
         int64_t msinc = LLONG_MIN;
         uint8_t pst = 0xFF;
         if (ok) {
@@ -1594,12 +1636,35 @@ __global__ __launch_bounds__(64 * WAVES) void k_decode_wave(In I, Names nm, Out 
                     if (K2) ck = (uint32_t)x2;
                     if (K3) msinc = x3;
                     if (K4) pst = (uint8_t)p4;
-                    // the source and target names, looked up side by side
-                    const bool wn = (K5 && (int)lane == w5) || (K6 && (int)lane == w6);
-                    const uint32_t id = wn ? M.find(nm, sref & 0xFFFFu, sref >> 16) : NULL_ID;
-                    const uint32_t i5 = __shfl(id, w5, 64), i6 = __shfl(id, w6, 64);
-                    if (K5) msrc = i5;
-                    if (K6) mtgt = i6;
+                    // the source and target names: looked up with the records' names
+                    const uint32_t r5 = __shfl(sref, w5, 64), r6 = __shfl(sref, w6, 64);
+                    href5 = K5 && !(RP_WIRE_ABL & 1) ? r5 : ~0u;
+                    href6 = K6 && !(RP_WIRE_ABL & 1) ? r6 : ~0u;
+                    if (href5 != ~0u || href6 != ~0u) {
+                        // lanes 0 / 1 hash the source / target and start their first probes' 32-B
+                        // slot reads as LDS DMA (no VGPR destination, nothing waits on them until
+                        // body_names(), after the records' walk): [a0 a1 b0 b1] in W.hprobe.
+                        // Both lanes issue (a dummy slot for a missing name), so the DMA's lane
+                        // layout does not depend on the exec mask.
+                        const uint32_t la = __builtin_amdgcn_readfirstlane(
+                            (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)W.hprobe);
+                        if (lane < 2) {
+                            const uint32_t r = lane == 0 ? href5 : href6;
+                            hslot = r != ~0u ? name_slot(nm, W.buf, sh + (r & 0xFFFFu), r >> 16) : 0u;
+                            const uint32_t* g = nm.hslot + (uint64_t)NameTable::kSlotWords * hslot;
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+                            asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                                         :
+                                         : "v"(g), "s"(la)
+                                         : "memory", "m0");
+                            asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                                         :
+                                         : "v"(g + 4), "s"(la + 32u)
+                                         : "memory", "m0");
+#pragma clang diagnostic pop
+                        }
+                    }
                 }
             } else if (ok && c == '{') {
                 ok = M.tch(last) == '}';
@@ -1761,10 +1826,11 @@ __global__ __launch_bounds__(64 * WAVES) void k_decode_wave(In I, Names nm, Out 
                 const uint32_t t1 = (2 * lane + 1 < (nrec * 2 - 1) ? W.lvl[2 * lane + 1] : arr_end) - 1;
                 rok = wave_record<true>(M, nm, b0, t0, t1, f, sref);
             }
+            if (href5 != ~0u || href6 != ~0u) body_names();  // their probes landed during the walk
             const uint32_t sx = __shfl(sref, (int)((lane - nrec) & 63u), 64);
             const uint32_t aref = lane < nrec && f.alen ? (uint32_t)(f.aoff - b0) | (f.alen << 16) : ~0u;
             const uint32_t ref = lane < nrec ? aref : lane < 2 * nrec ? sx : ~0u;
-            const uint32_t id = ok && ref != ~0u ? M.find(nm, ref & 0xFFFFu, ref >> 16) : NULL_ID;
+            const uint32_t id = ok && ref != ~0u && !(RP_WIRE_ABL & 2) ? M.find(nm, ref & 0xFFFFu, ref >> 16) : NULL_ID;
             const uint32_t sid = __shfl(id, (int)((lane + nrec) & 63u), 64);
             if (ok && lane < nrec) {
                 f.addr = id;
@@ -1782,6 +1848,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_decode_wave(In I, Names nm, Out 
             }
         }
         ok = ok && __ballot(!rok) == 0;
+        if (href5 != ~0u || href6 != ~0u) body_names();  // not taken inside the records' pass
         WPROF(5);
         nwave += ok ? 1u : 0u;
         retry = PASS == 1 && !ok && retry;
