@@ -229,12 +229,12 @@ __global__ __launch_bounds__(256) void k_fold(const uint32_t* __restrict__ sk, c
 // counter is cleared by k_link, so the batch needs no memset.
 constexpr uint32_t kSlots = 15;  // changes per address on the grouped path: kSlots + 1
 constexpr uint32_t kOvfMark = 0xFFFFFFFFu;  // row counter of an address left to k_fold_ovf
-constexpr uint32_t kDoneWords = 4;  // [0] spare, [1] k_fold, [2] k_ovf_len's ticket, [3] spare
+constexpr uint32_t kDoneWords = 4;  // [0] k_link_fold barrier count, [1] k_fold, [2] k_ovf_len's ticket, [3] barrier generation
 
-__global__ void k_link(const uint32_t* __restrict__ ids, uint32_t k, MRow* __restrict__ rows,
-                       uint32_t* __restrict__ slots, uint8_t* __restrict__ rk, uint32_t* __restrict__ ovf,
-                       uint32_t* __restrict__ napplied) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void link_one(uint32_t i, const uint32_t* __restrict__ ids, uint32_t k,
+                                         MRow* __restrict__ rows, uint32_t* __restrict__ slots,
+                                         uint8_t* __restrict__ rk, uint32_t* __restrict__ ovf,
+                                         uint32_t* __restrict__ napplied) {
     if (i == 0) *napplied = 0;
     if (i >= k) return;
     const uint32_t id = ids[i];
@@ -244,10 +244,16 @@ __global__ void k_link(const uint32_t* __restrict__ ids, uint32_t k, MRow* __res
     if (r == kSlots + 1u) *ovf = 1u;
 }
 
+__global__ void k_link(const uint32_t* __restrict__ ids, uint32_t k, MRow* __restrict__ rows,
+                       uint32_t* __restrict__ slots, uint8_t* __restrict__ rk, uint32_t* __restrict__ ovf,
+                       uint32_t* __restrict__ napplied) {
+    link_one(blockIdx.x * blockDim.x + threadIdx.x, ids, k, rows, slots, rk, ovf, napplied);
+}
+
 // The workgroup's applied count goes to part[blockIdx.x] (summed by k_ovf_len or k_fold_ovf).
-__global__ __launch_bounds__(256) void k_fold_fast(const uint32_t* __restrict__ ids, uint32_t k,
-                                                   const uint8_t* __restrict__ rk, const uint32_t* __restrict__ slots,
-                                                   FoldArgs A, uint32_t* __restrict__ part) {
+__device__ __forceinline__ void fold_fast_block(const uint32_t* __restrict__ ids, uint32_t k,
+                                                const uint8_t* __restrict__ rk, const uint32_t* __restrict__ slots,
+                                                const FoldArgs& A, uint32_t* __restrict__ part) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t napp = 0;
     if (i < k && rk[i] == 0) {
@@ -277,6 +283,51 @@ __global__ __launch_bounds__(256) void k_fold_fast(const uint32_t* __restrict__ 
     napp = block_sum256(napp);
     if (threadIdx.x == 0) part[blockIdx.x] = napp;
     if (threadIdx.x == 0 && blockIdx.x == 0) part[gridDim.x] = 0;  // the overflow fold's count (k_ovf_len)
+}
+
+__global__ __launch_bounds__(256) void k_fold_fast(const uint32_t* __restrict__ ids, uint32_t k,
+                                                   const uint8_t* __restrict__ rk, const uint32_t* __restrict__ slots,
+                                                   FoldArgs A, uint32_t* __restrict__ part) {
+    fold_fast_block(ids, k, rk, slots, A, part);
+}
+
+// Every workgroup of the launch waits here until all have arrived (count / generation words,
+// zero between launches; the last to arrive resets the count and bumps the generation). Only
+// for grids that are resident at once (the caller checks the occupancy); a wait that outlasts
+// kLbSpinCap polls gives up and reports kErrSpin, so no launch can hang.
+__device__ __forceinline__ void grid_sync(uint32_t* cnt, uint32_t* gen, uint32_t* err) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this thread's writes, before the arrival
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t g = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t arrived = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+        if (arrived == gridDim.x) {
+            __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            uint32_t spin = 0;
+            while (__hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g) {
+                if (++spin == kLbSpinCap) {
+                    atomicOr(err, kErrSpin);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+// k_link and k_fold_fast in one launch, a grid barrier between them (round 4): one launch fewer
+// per batch on the grouped path (C3).
+__global__ __launch_bounds__(256) void k_link_fold(const uint32_t* __restrict__ ids, uint32_t k,
+                                                   uint32_t* __restrict__ slots, uint8_t* __restrict__ rk,
+                                                   uint32_t* __restrict__ ovf, uint32_t* __restrict__ napplied,
+                                                   FoldArgs A, uint32_t* __restrict__ part, uint32_t* __restrict__ err) {
+    link_one(blockIdx.x * blockDim.x + threadIdx.x, ids, k, A.rows, slots, rk, ovf, napplied);
+    grid_sync(napplied + 2, napplied + 5, err);
+    fold_fast_block(ids, k, rk, slots, A, part);
 }
 
 // The grouped path's overflow fold: the addresses k_fold_fast marked (more than kSlots + 1
@@ -1095,6 +1146,30 @@ struct Members {
     DevBuf<uint32_t> bk_res2;  // the bucket fold's 2-bit per-id results (k_bk_gather)
     DevBuf<uint8_t> bk_resj;
     static constexpr uint32_t kBkMin = 1u << 19;
+    // RP_MEMBERS_FUSE=1 (A/B, off by default): k_link_fold for a grid that is resident at once
+    // with half the machine to spare (its grid barrier needs every workgroup running). Measured
+    // slower: the C3 fold 0.098-0.102 ms against 0.021 for the two launches, the batch 115-119
+    // against 39 us (profiles/r04/r04s): the barrier's agent-scope release / acquire (an L2
+    // write-back and invalidate per wave, since the XCDs' L2s are not coherent) costs far more
+    // than the launch it saves.
+    int fuse_cap = -1;
+    bool fuse_fold(uint32_t g1, hipStream_t s) {
+        const char* e = getenv("RP_MEMBERS_FUSE");
+        if (!e || *e != '1') return false;
+        if (fuse_cap < 0) {
+            int dev = 0, cus = 0, nbl = 0;
+            RP_HIP(hipGetDevice(&dev));
+            RP_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+            RP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nbl, reinterpret_cast<const void*>(k_link_fold), 256, 0));
+            fuse_cap = cus * nbl / 2;
+        }
+        if ((int)g1 > fuse_cap) return false;
+        if (!ws.err.p) {
+            ws.err.reserve(1);
+            RP_HIP(hipMemsetAsync(ws.err.p, 0, sizeof(uint32_t), s));
+        }
+        return true;
+    }
     bool use_bucket_fold(uint32_t k, uint32_t nb) const {
         if (damp_on || nb > kBkMaxBuckets || k >= (1u << 30) || !grouped_fold) return false;
         const char* e = getenv("RP_MEMBERS_BUCKET_FOLD");
@@ -1237,8 +1312,14 @@ struct Members {
             g_rk.reserve(k);
             const unsigned g1 = (unsigned)((k + 255) / 256);
             g_part.reserve(g1 + 1);
-            hipLaunchKernelGGL(k_link, dim3(g1), dim3(256), 0, s, ids, k, rows.p, g_slots.p, g_rk.p, ovf, napplied.p);
-            hipLaunchKernelGGL(k_fold_fast, dim3(g1), dim3(256), 0, s, ids, k, g_rk.p, g_slots.p, A, g_part.p);
+            if (fuse_fold(g1, s)) {
+                hipLaunchKernelGGL(k_link_fold, dim3(g1), dim3(256), 0, s, ids, k, g_slots.p, g_rk.p, ovf, napplied.p, A,
+                                   g_part.p, ws.err.p);
+            } else {
+                hipLaunchKernelGGL(k_link, dim3(g1), dim3(256), 0, s, ids, k, rows.p, g_slots.p, g_rk.p, ovf,
+                                   napplied.p);
+                hipLaunchKernelGGL(k_fold_fast, dim3(g1), dim3(256), 0, s, ids, k, g_rk.p, g_slots.p, A, g_part.p);
+            }
             RP_HIP(hipGetLastError());
             if (build && nt.size()) {  // the overflow fold rides on the string build's length launch
                 const OvfArgs ov{ids, k, ovf, A, g_part.p, g1, n_applied_out};
