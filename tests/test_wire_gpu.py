@@ -496,3 +496,33 @@ def test_two_pass_layouts_match_thread_parser(gpu, monkeypatch, capfd):
         assert np.array_equal(d1[k], dt[k]), k
     assert (dt["err"] == 0).all()
     m.close()
+
+
+def test_bodies_past_64_members_take_the_serial_walk(gpu, monkeypatch, capfd):
+    """The body's members are parsed a lane each up to 64 members; a body with more (unknown
+    members around the known ones, a repeated source) takes the wave-uniform serial walk. Both
+    give the thread parser's columns and headers, and the waves take every such message."""
+    rng = random.Random(5)
+    names = ["10.0.0.%d:3000" % i for i in range(40)]
+    m = gpu.Membership()
+    m.intern(names)
+    texts = []
+    for nextra in (0, 30, 62, 63, 64, 65, 90):
+        body = [("checksum", 7), ("source", names[1]), ("sourceIncarnationNumber", 3)]
+        # scalars, and a few nested values (the wave parser tracks up to 32 depth-1 openers)
+        body += [("x%d" % j, [1, {"a": 1}] if j % 9 == 4 else rng.choice([1, "s", None, True])) for j in range(nextra)]
+        body.insert(rng.randrange(len(body) + 1), ("changes", [{"address": rng.choice(names), "status": "alive",
+                                                                 "incarnationNumber": j} for j in range(5)]))
+        body.append(("source", names[2]))  # the last repeated key wins
+        texts.append("{" + ",".join(json.dumps(k) + ":" + json.dumps(v) for k, v in body) + "}")
+    monkeypatch.setenv("RP_WIRE_DEBUG", "1")
+    capfd.readouterr()
+    dw = gpu.wire_decode(m, texts)
+    line = [x for x in capfd.readouterr().err.splitlines() if "by waves" in x][-1]
+    assert int(line.split()[3]) == len(texts), line
+    monkeypatch.setenv("RP_WIRE_THREAD", "1")
+    dt = gpu.wire_decode(m, texts)
+    for k in dt:
+        assert np.array_equal(dw[k], dt[k]), k
+    assert (dt["err"] == 0).all() and (dt["source"] == m.intern([names[2]])[0]).all()
+    m.close()
