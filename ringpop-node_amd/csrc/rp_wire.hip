@@ -1376,14 +1376,20 @@ __global__ __launch_bounds__(64 * WAVES) void k_decode_wave(In I, Names nm, Out 
                 uint32_t x[4] = {v.x, v.y, v.z, v.w};
                 uint32_t p[4], Qd[4];
                 uint32_t par = 0;
+                if (4 * dw0 < sh || 4 * dw0 + 16 > sh + len) {  // the message's first / last bytes only
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const uint32_t dw = dw0 + k;
+                        const int lo = min(max((int)sh - (int)(4 * dw), 0), 4);
+                        const int hi = min(max((int)(sh + len) - (int)(4 * dw), 0), 4);
+                        const uint32_t m_in =
+                            (uint32_t)((0x80808080ull << (8 * lo)) & (0x80808080ull >> (8 * (4 - hi))));
+                        const uint32_t bm = (m_in >> 7) * 0xFFu;
+                        x[k] = (x[k] & bm) | (0x20202020u & ~bm);
+                    }
+                }
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
-                    const uint32_t dw = dw0 + k;
-                    const int lo = min(max((int)sh - (int)(4 * dw), 0), 4);
-                    const int hi = min(max((int)(sh + len) - (int)(4 * dw), 0), 4);
-                    const uint32_t m_in = (uint32_t)((0x80808080ull << (8 * lo)) & (0x80808080ull >> (8 * (4 - hi))));
-                    const uint32_t bm = (m_in >> 7) * 0xFFu;
-                    x[k] = (x[k] & bm) | (0x20202020u & ~bm);
                     const uint32_t Q = swar_eq(x[k], '"');
                     uint32_t pp = Q ^ (Q << 8);
                     pp ^= pp << 16;
