@@ -673,6 +673,10 @@ constexpr bool kWaveMembers = RP_WIRE_MEMBERS != 0;  // records parsed a lane pe
 #define RP_WIRE_CLS16 1
 #endif
 constexpr bool kWaveCls16 = RP_WIRE_CLS16 != 0;  // classifier: 16 bytes per lane a step (0: 4 bytes; A/B)
+#ifndef RP_WIRE_NIBBLE
+#define RP_WIRE_NIBBLE 1
+#endif
+constexpr bool kWaveNibbleCls = RP_WIRE_NIBBLE != 0;  // byte classes by nibble tables (0: SWAR compares; A/B)
 #ifndef RP_WIRE_ABL
 #define RP_WIRE_ABL 0  // timing ablations (results wrong): 1 no body name lookups, 2 no record name lookups
 #endif
@@ -702,6 +706,21 @@ using WaveLdsS = WaveLdsT<kWTokS, kWLvlS>;
 __device__ __forceinline__ uint32_t swar_eq(uint32_t x, uint8_t c) {
     const uint32_t t = x ^ (0x01010101u * c);
     return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+}
+// The classifier's byte classes from two nibble-table lookups (v_perm_b32 per 8 entries), for
+// the four bytes of x at once: class = LO[x & 15] & HI[x >> 4] with bits 0 '"', 1 ',', 2 ':',
+// 3 { } [ ], 4 backslash, 5 space, 6 tab / LF / CR, 7 any byte below 0x20. A byte of no class
+// (including every byte >= 0x80) is 0.
+__device__ __forceinline__ uint32_t byte_class(uint32_t x) {
+    const uint32_t lo = x & 0x0F0F0F0Fu, hi = (x >> 4) & 0x0F0F0F0Fu;
+    // LO: 0 A0, 1 80, 2 81, 3-8 80, 9 C0, A C4, B 88, C 92, D C8, E-F 80
+    const uint32_t l0 = __builtin_amdgcn_perm(0x80808080u, 0x808180A0u, lo & 0x07070707u);
+    const uint32_t l1 = __builtin_amdgcn_perm(0x8080C892u, 0x88C4C080u, lo & 0x07070707u);
+    const uint32_t ml = ((lo >> 3) & 0x01010101u) * 0xFFu;
+    // HI: 0 C0, 1 80, 2 23, 3 04, 4 00, 5 18, 6 00, 7 08, 8-F 00
+    const uint32_t h0 = __builtin_amdgcn_perm(0x08001800u, 0x042380C0u, hi & 0x07070707u);
+    const uint32_t mh = ((hi >> 3) & 0x01010101u) * 0xFFu;
+    return ((l1 & ml) | (l0 & ~ml)) & (h0 & ~mh);
 }
 // bit 7 of bytes 0..3 → bits 0..3
 __device__ __forceinline__ uint32_t swar_bits(uint32_t m) {
@@ -1388,9 +1407,11 @@ __global__ __launch_bounds__(64 * WAVES) void k_decode_wave(In I, Names nm, Out 
                         x[k] = (x[k] & bm) | (0x20202020u & ~bm);
                     }
                 }
+                uint32_t cls[4];
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
-                    const uint32_t Q = swar_eq(x[k], '"');
+                    cls[k] = kWaveNibbleCls ? byte_class(x[k]) : 0u;
+                    const uint32_t Q = kWaveNibbleCls ? (cls[k] << 7) & 0x80808080u : swar_eq(x[k], '"');
                     uint32_t pp = Q ^ (Q << 8);
                     pp ^= pp << 16;
                     p[k] = pp ^ (par ? 0x80808080u : 0u);  // parity of the lane's quotes up to each byte
@@ -1403,16 +1424,25 @@ __global__ __launch_bounds__(64 * WAVES) void k_decode_wave(In I, Names nm, Out 
                 bool ctrl = false;
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
-                    const uint32_t Q = Qd[k], xk = x[k];
+                    const uint32_t Q = Qd[k], xk = x[k], c = cls[k];
                     const uint32_t instr = p[k] ^ (pre ? 0x80808080u : 0u);
-                    const uint32_t xd = xk & 0xDFDFDFDFu;
-                    const uint32_t structural =
-                        (swar_eq(xd, 0x5B) | swar_eq(xd, 0x5D) | swar_eq(xk, ':') | swar_eq(xk, ',')) & ~instr & ~Q;
+                    uint32_t st_any, ws, lt20, bsl;
+                    if (kWaveNibbleCls) {  // the class bits (byte_class) as bit 7 of each byte
+                        st_any = ((c & 0x0E0E0E0Eu) + 0x7F7F7F7Fu) & 0x80808080u;
+                        ws = ((c & 0x60606060u) + 0x7F7F7F7Fu) & 0x80808080u;
+                        lt20 = c & 0x80808080u;
+                        bsl = (c << 3) & 0x80808080u;
+                    } else {
+                        const uint32_t xd = xk & 0xDFDFDFDFu;
+                        st_any = swar_eq(xd, 0x5B) | swar_eq(xd, 0x5D) | swar_eq(xk, ':') | swar_eq(xk, ',');
+                        ws = swar_eq(xk, ' ') | swar_eq(xk, '\t') | swar_eq(xk, '\n') | swar_eq(xk, '\r');
+                        lt20 = ~(((xk & 0x7F7F7F7Fu) + 0x60606060u) | xk) & 0x80808080u;
+                        bsl = swar_eq(xk, '\\');
+                    }
+                    const uint32_t structural = st_any & ~instr & ~Q;
                     const uint32_t tokb = Q | structural;
-                    const uint32_t ws = swar_eq(xk, ' ') | swar_eq(xk, '\t') | swar_eq(xk, '\n') | swar_eq(xk, '\r');
-                    const uint32_t lt20 = ~(((xk & 0x7F7F7F7Fu) + 0x60606060u) | xk) & 0x80808080u;
                     const uint32_t str_body = instr & ~Q;
-                    ctrl |= ((lt20 & ~(ws & ~str_body)) | swar_eq(xk, '\\')) != 0;
+                    ctrl |= ((lt20 & ~(ws & ~str_body)) | bsl) != 0;
                     const uint32_t sb = ~instr & ~tokb & ~ws & 0x80808080u;
                     tm |= swar_bits(tokb) << (4 * k);
                     sm |= swar_bits(sb) << (4 * k);
