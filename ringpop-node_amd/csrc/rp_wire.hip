@@ -677,6 +677,10 @@ constexpr bool kWaveCls16 = RP_WIRE_CLS16 != 0;  // classifier: 16 bytes per lan
 #define RP_WIRE_NIBBLE 1
 #endif
 constexpr bool kWaveNibbleCls = RP_WIRE_NIBBLE != 0;  // byte classes by nibble tables (0: SWAR compares; A/B)
+#ifndef RP_WIRE_TOKLOOP
+#define RP_WIRE_TOKLOOP 1
+#endif
+constexpr bool kWaveTokLoop = RP_WIRE_TOKLOOP != 0;  // token writes: a loop over set bits (0: 16 predicated; A/B)
 #ifndef RP_WIRE_ABL
 #define RP_WIRE_ABL 0  // timing ablations (results wrong): 1 no body name lookups, 2 no record name lookups
 #endif
@@ -1454,15 +1458,28 @@ __global__ __launch_bounds__(64 * WAVES) void k_decode_wave(In I, Names nm, Out 
                 uint32_t idx = ntok + (uint32_t)__popcll(K0 & lt) + 2u * (uint32_t)__popcll(K1 & lt) +
                                4u * (uint32_t)__popcll(K2 & lt) + 8u * (uint32_t)__popcll(K3 & lt) +
                                16u * (uint32_t)__popcll(K4 & lt);
-#pragma unroll
-                for (int j = 0; j < 16; j++)
-                    if ((tm >> j) & 1u) {
+                if (kWaveTokLoop) {
+                    // a lane's tokens one per iteration (as many iterations as the densest lane has)
+                    for (uint32_t mm = tm; mm; mm &= mm - 1u) {
+                        const uint32_t j = (uint32_t)__builtin_ctz(mm);
+                        const uint32_t w = j < 8 ? (j < 4 ? x[0] : x[1]) : (j < 12 ? x[2] : x[3]);
                         if (idx < WL::kTok) {
                             W.pos[idx] = (uint16_t)(4 * dw0 + j - sh);
-                            W.tc[idx] = (uint8_t)(x[j >> 2] >> (8 * (j & 3)));
+                            W.tc[idx] = (uint8_t)(w >> (8 * (j & 3u)));
                         }
                         idx++;
                     }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 16; j++)
+                        if ((tm >> j) & 1u) {
+                            if (idx < WL::kTok) {
+                                W.pos[idx] = (uint16_t)(4 * dw0 + j - sh);
+                                W.tc[idx] = (uint8_t)(x[j >> 2] >> (8 * (j & 3)));
+                            }
+                            idx++;
+                        }
+                }
                 reinterpret_cast<uint16_t*>(W.scal)[(d0 >> 2) + lane] = (uint16_t)sm;
                 ntok += (uint32_t)__popcll(K0) + 2u * (uint32_t)__popcll(K1) + 4u * (uint32_t)__popcll(K2) +
                         8u * (uint32_t)__popcll(K3) + 16u * (uint32_t)__popcll(K4);
