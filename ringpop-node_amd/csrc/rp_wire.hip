@@ -680,6 +680,10 @@ constexpr bool kWaveNibbleCls = RP_WIRE_NIBBLE != 0;  // byte classes by nibble 
 #ifndef RP_WIRE_TOKLOOP
 #define RP_WIRE_TOKLOOP 1
 #endif
+#ifndef RP_WIRE_FUSED_LVL
+#define RP_WIRE_FUSED_LVL 1
+#endif
+constexpr bool kWaveFusedLvl = RP_WIRE_FUSED_LVL != 0;  // level list from the depth pass (0: its own scan; A/B)
 constexpr bool kWaveTokLoop = RP_WIRE_TOKLOOP != 0;  // token writes: a loop over set bits (0: 16 predicated; A/B)
 #ifndef RP_WIRE_ABL
 #define RP_WIRE_ABL 0  // timing ablations (results wrong): 1 no body name lookups, 2 no record name lookups
@@ -1319,7 +1323,7 @@ __device__ unsigned long long g_wprof[8];
 // PASS 0: the only pass; 1: the first of two (a message past the layout's token or level bound
 // is marked slow = 2, nothing else done for it); 2: the second (only the messages marked 2)
 template <class WL, int WAVES, int PASS>
-__global__ __launch_bounds__(64 * WAVES) void k_decode_wave(In I, Names nm, Out O, uint32_t n_msgs, uint64_t vb,
+__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WL::kTok < 2048 ? 3 : 1))) void k_decode_wave(In I, Names nm, Out O, uint32_t n_msgs, uint64_t vb,
                                                             uint64_t ve, RecF* __restrict__ stash,
                                                             uint8_t* __restrict__ slow,
                                                             uint32_t* __restrict__ n_by_waves,
@@ -1557,7 +1561,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_decode_wave(In I, Names nm, Out 
         // depth before every token
         int32_t depth = 0;
         bool neg = false;
-        uint32_t nop1 = 0, ncl2 = 0, nsep1 = 0;
+        uint32_t nop1 = 0, ncl2 = 0, nsep1 = 0, nlv2 = 0;
         for (uint32_t t0 = 0; ok && t0 < ntok; t0 += 64) {
             const uint32_t t = t0 + lane;
             const uint8_t ch = t < ntok ? W.tc[t] : (uint8_t)' ';
@@ -1571,6 +1575,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_decode_wave(In I, Names nm, Out 
             const uint32_t io = nop1 + (uint32_t)__popcll(O1 & lt), ic = ncl2 + (uint32_t)__popcll(C2 & lt);
             if (((O1 >> lane) & 1ull) && io < 32) W.op1[io] = (uint16_t)t;
             if (((C2 >> lane) & 1ull) && ic < 32) W.cl2[ic] = (uint16_t)t;
+            if (kWaveFusedLvl) {  // the level tokens of a body's depth-1 array, in case it is the changes
+                const uint64_t L2 = __ballot(t < ntok && d == 2 && (ch == '{' || ch == ','));
+                const uint32_t il = nlv2 + (uint32_t)__popcll(L2 & lt);
+                if (((L2 >> lane) & 1ull) && il < WL::kLvl) W.lvl[il] = (uint16_t)t;
+                nlv2 += (uint32_t)__popcll(L2);
+            }
             const uint64_t S1 = __ballot(t < ntok && ch == ',' && d == 1);
             const uint32_t is = nsep1 + (uint32_t)__popcll(S1 & lt);
             if (((S1 >> lane) & 1ull) && is < 64) W.sep1[is] = (uint16_t)t;
@@ -1808,11 +1818,26 @@ __global__ __launch_bounds__(64 * WAVES) void k_decode_wave(In I, Names nm, Out 
         // the changes array: its level tokens are { , { , ... {
         uint32_t nrec = 0;
         uint32_t nb = 0;  // member boundaries (~0: a nested member value)
+        uint32_t lv0 = 0;  // the level list is W.lvl[lv0, lv0 + nl)
         if (ok) {
             const int32_t d = W.dep[arr];
             uint32_t nl = 0;
             bool deep = false;
-            for (uint32_t t0 = arr + 1; t0 < arr_end; t0 += 64) {
+            const bool fused = kWaveFusedLvl && !kWaveMembers && d == 1 && nlv2 <= WL::kLvl;
+            if (fused) {
+                // the depth pass listed every depth-2 '{' / ',': the changes array's are the run
+                // of them between its brackets (counted by two ballot passes over the list)
+                uint32_t a0 = 0, a1 = 0;
+                for (uint32_t j0 = 0; j0 < nlv2; j0 += 64) {
+                    const uint32_t j = j0 + lane;
+                    const uint32_t t = j < nlv2 ? (uint32_t)W.lvl[j] : 0xFFFFFFFFu;
+                    a0 += (uint32_t)__popcll(__ballot(t <= arr));
+                    a1 += (uint32_t)__popcll(__ballot(t < arr_end));
+                }
+                lv0 = __builtin_amdgcn_readfirstlane(a0);
+                nl = __builtin_amdgcn_readfirstlane(a1 - a0);
+            }
+            for (uint32_t t0 = arr + 1; !fused && t0 < arr_end; t0 += 64) {
                 const uint32_t t = t0 + lane;
                 const bool in = t < arr_end;
                 const int32_t dt = in ? (int32_t)W.dep[t] : 0;
@@ -1843,15 +1868,17 @@ __global__ __launch_bounds__(64 * WAVES) void k_decode_wave(In I, Names nm, Out 
             retry = nl >= WL::kLvl;
             bool pat = true;
             for (uint32_t j = lane; ok && j < nl; j += 64) {
-                const uint32_t t = W.lvl[j];
+                const uint32_t t = W.lvl[lv0 + j];
                 const uint8_t c = M.tch(t);
                 pat &= (j & 1u) ? c == ',' : c == '{';
                 // a record's last token is its '}', right before the next level token
                 if (!(j & 1u)) {
-                    const uint32_t nxt = j + 1 < nl ? W.lvl[j + 1] : arr_end;
+                    const uint32_t nxt = j + 1 < nl ? W.lvl[lv0 + j + 1] : arr_end;
                     pat &= M.tch(nxt - 1) == '}' && W.dep[nxt - 1] == d + 2 && M.clean(W.pos[nxt - 1], W.pos[nxt]);
-                    const uint32_t prv = j == 0 ? arr : W.lvl[j - 1];
-                    pat &= M.clean(W.pos[prv], W.pos[t]);
+                    const uint32_t prv = j == 0 ? arr : W.lvl[lv0 + j - 1];
+                    // the fused list holds only '{' and ',': no other token may sit between a
+                    // record's opener and the '[' or ',' before it
+                    pat &= M.clean(W.pos[prv], W.pos[t]) && (!fused || t == prv + 1);
                 }
             }
             ok = ok && __ballot(!pat) == 0;
@@ -1875,8 +1902,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_decode_wave(In I, Names nm, Out 
             RecF f;
             uint32_t sref = ~0u;
             if (ok && lane < nrec) {
-                const uint32_t t0 = W.lvl[2 * lane];
-                const uint32_t t1 = (2 * lane + 1 < (nrec * 2 - 1) ? W.lvl[2 * lane + 1] : arr_end) - 1;
+                const uint32_t t0 = W.lvl[lv0 + 2 * lane];
+                const uint32_t t1 = (2 * lane + 1 < (nrec * 2 - 1) ? W.lvl[lv0 + 2 * lane + 1] : arr_end) - 1;
                 rok = wave_record<true>(M, nm, b0, t0, t1, f, sref);
             }
             if (href5 != ~0u || href6 != ~0u) body_names();  // their probes landed during the walk
@@ -1892,8 +1919,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_decode_wave(In I, Names nm, Out 
             }
         } else if (!mp) {
             for (uint32_t r = lane; ok && r < nrec; r += 64) {
-                const uint32_t t0 = W.lvl[2 * r];
-                const uint32_t t1 = (2 * r + 1 < (nrec * 2 - 1) ? W.lvl[2 * r + 1] : arr_end) - 1;
+                const uint32_t t0 = W.lvl[lv0 + 2 * r];
+                const uint32_t t1 = (2 * r + 1 < (nrec * 2 - 1) ? W.lvl[lv0 + 2 * r + 1] : arr_end) - 1;
                 RecF f;
                 uint32_t sref;
                 rok &= wave_record<false>(M, nm, b0, t0, t1, f, sref);
