@@ -684,6 +684,10 @@ constexpr bool kWaveNibbleCls = RP_WIRE_NIBBLE != 0;  // byte classes by nibble 
 #define RP_WIRE_FUSED_LVL 1
 #endif
 constexpr bool kWaveFusedLvl = RP_WIRE_FUSED_LVL != 0;  // level list from the depth pass (0: its own scan; A/B)
+#ifndef RP_WIRE_DEPTH4
+#define RP_WIRE_DEPTH4 1
+#endif
+constexpr bool kWaveDepth4 = RP_WIRE_DEPTH4 != 0;  // depth pass: four tokens per lane a step (0: one; A/B)
 constexpr bool kWaveTokLoop = RP_WIRE_TOKLOOP != 0;  // token writes: a loop over set bits (0: 16 predicated; A/B)
 #ifndef RP_WIRE_ABL
 #define RP_WIRE_ABL 0  // timing ablations (results wrong): 1 no body name lookups, 2 no record name lookups
@@ -1562,7 +1566,73 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WL::
         int32_t depth = 0;
         bool neg = false;
         uint32_t nop1 = 0, ncl2 = 0, nsep1 = 0, nlv2 = 0;
-        for (uint32_t t0 = 0; ok && t0 < ntok; t0 += 64) {
+        // 256 tokens a step, four per lane (their characters in one LDS read, their depths in one
+        // write): the lanes' depth changes (-4..4) prefixed by four ballots; the level / opener /
+        // closer / separator lists compacted from per-lane counts (three ballots each, the rare
+        // three only in steps that hold one)
+        for (uint32_t t0 = 0; kWaveDepth4 && ok && t0 < ntok; t0 += 256) {
+            const uint32_t tb = t0 + 4u * lane;
+            const uint32_t cw = tb < ntok ? *reinterpret_cast<const uint32_t*>(&W.tc[tb]) : 0x20202020u;
+            uint32_t op = 0, cl = 0;  // bit k: token tb + k opens / closes
+            int32_t pk[4];
+            int32_t run = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint8_t c = tb + k < ntok ? (uint8_t)(cw >> (8 * k)) : (uint8_t)' ';
+                const bool o = wave_isopen(c), x = wave_isclose(c);
+                op |= (o ? 1u : 0u) << k;
+                cl |= (x ? 1u : 0u) << k;
+                pk[k] = run;
+                run += (o ? 1 : 0) - (x ? 1 : 0);
+            }
+            const uint32_t u = (uint32_t)(run + 4);
+            const uint64_t B0 = __ballot(u & 1u), B1 = __ballot(u & 2u), B2 = __ballot(u & 4u), B3 = __ballot(u & 8u);
+            const int32_t excl = (int32_t)((uint32_t)__popcll(B0 & lt) + 2u * (uint32_t)__popcll(B1 & lt) +
+                                           4u * (uint32_t)__popcll(B2 & lt) + 8u * (uint32_t)__popcll(B3 & lt)) -
+                                 4 * (int32_t)lane;
+            const int32_t tot = (int32_t)((uint32_t)__popcll(B0) + 2u * (uint32_t)__popcll(B1) +
+                                          4u * (uint32_t)__popcll(B2) + 8u * (uint32_t)__popcll(B3)) -
+                                4 * 64;
+            uint32_t dw = 0, l2 = 0, o1 = 0, c2 = 0, s1 = 0;
+            bool bad_d = false;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int32_t d = depth + excl + pk[k];
+                const bool v = tb + k < ntok;
+                const uint8_t c = (uint8_t)(cw >> (8 * k));
+                dw |= (uint32_t)(uint8_t)(int8_t)d << (8 * k);
+                const bool x = (cl >> k) & 1u, o = (op >> k) & 1u;
+                bad_d |= v && (d < 0 || d > 120 || (x && d < 1));
+                l2 |= (v && d == 2 && (c == '{' || c == ',') ? 1u : 0u) << k;
+                o1 |= (v && o && d == 1 ? 1u : 0u) << k;
+                c2 |= (v && x && d == 2 ? 1u : 0u) << k;
+                s1 |= (v && c == ',' && d == 1 ? 1u : 0u) << k;
+            }
+            if (tb < ntok) *reinterpret_cast<uint32_t*>(&W.dep[tb]) = dw;
+            neg |= __ballot(bad_d) != 0;
+            // a list's entries of this step: lane counts 0..4 prefixed by three ballots
+            auto compact = [&](uint32_t bits, uint32_t& n, uint16_t* list, uint32_t cap) {
+                const uint32_t cnt = (uint32_t)__builtin_popcount(bits);
+                const uint64_t C0 = __ballot(cnt & 1u), C1 = __ballot(cnt & 2u), C2b = __ballot(cnt & 4u);
+                uint32_t i = n + (uint32_t)__popcll(C0 & lt) + 2u * (uint32_t)__popcll(C1 & lt) +
+                             4u * (uint32_t)__popcll(C2b & lt);
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    if ((bits >> k) & 1u) {
+                        if (i < cap) list[i] = (uint16_t)(tb + k);
+                        i++;
+                    }
+                n += (uint32_t)__popcll(C0) + 2u * (uint32_t)__popcll(C1) + 4u * (uint32_t)__popcll(C2b);
+            };
+            if (kWaveFusedLvl) compact(l2, nlv2, W.lvl, WL::kLvl);
+            if (__ballot((o1 | c2 | s1) != 0) != 0) {
+                compact(o1, nop1, W.op1, 32);
+                compact(c2, ncl2, W.cl2, 32);
+                compact(s1, nsep1, W.sep1, 64);
+            }
+            depth += tot;
+        }
+        for (uint32_t t0 = 0; !kWaveDepth4 && ok && t0 < ntok; t0 += 64) {
             const uint32_t t = t0 + lane;
             const uint8_t ch = t < ntok ? W.tc[t] : (uint8_t)' ';
             const uint64_t Op = __ballot(t < ntok && wave_isopen(ch));
