@@ -25,6 +25,7 @@
 // by binary search over its byte-ordered ids. Strings with escapes are rejected (addresses and
 // uuids never hold one), numbers must be integral. Count pass -> scan -> fill pass.
 #include <climits>
+#include <type_traits>
 
 #include "rp_names.h"
 #include "rp_swim.h"
@@ -697,22 +698,31 @@ constexpr bool kWaveTokLoop = RP_WIRE_TOKLOOP != 0;  // token writes: a loop ove
 #endif
 constexpr bool kWaveBodyLanes = RP_WIRE_BODY_LANES != 0;  // body members a lane each (0: the serial walk; A/B)
 
-template <uint32_t TOK, uint32_t LVL>
+// BUF: message bytes staged (a longer message goes to the next pass); HASTC: the tokens'
+// characters kept (else read back through pos from the staged bytes)
+template <uint32_t TOK, uint32_t LVL, uint32_t BUF = kWBuf, bool HASTC = true>
 struct alignas(16) WaveLdsT {
-    static constexpr uint32_t kTok = TOK, kLvl = LVL;
-    alignas(16) uint32_t buf[kWBuf / 4 + 2];
+    static constexpr uint32_t kTok = TOK, kLvl = LVL, kBuf = BUF;
+    static constexpr bool kHasTc = HASTC;
+    alignas(16) uint32_t buf[BUF / 4 + 2];
     uint16_t pos[TOK];   // token byte offset in the message
     int8_t dep[TOK];     // depth before the token ({ [ open, } ] close)
-    uint8_t tc[TOK];     // the token's character
+    uint8_t tc[HASTC ? TOK : 4];  // the token's character
     alignas(16) uint16_t lvl[LVL];  // the changes array's level tokens (the classifier's scratch before)
-    uint64_t scal[kWBuf / 64 + 16];  // buffer bytes outside strings that are neither tokens nor
+    uint64_t scal[BUF / 64 + 16];  // buffer bytes outside strings that are neither tokens nor
                                     // whitespace (bit sh + i: message byte i)
     uint16_t op1[32], cl2[32];      // openers at depth 1 / closers at depth 2, in order: the k-th pair
     uint16_t sep1[64];              // the body's member separators (',' at depth 1), in order
     alignas(16) uint32_t hprobe[16];  // the body's source / target first probe slots (LDS DMA)
 };
 using WaveLds = WaveLdsT<kWTok, kWLvl>;
-using WaveLdsS = WaveLdsT<kWTokS, kWLvlS>;
+#ifndef RP_WIRE_SMALL2
+#define RP_WIRE_SMALL2 1
+#endif
+// RP_WIRE_SMALL2 (round 4): the first pass with 7 KB of message bytes, 256 level tokens and no
+// token characters (12.9 KB a wave: 12 waves a CU) instead of 8 KB / 512 / characters kept
+// (15.8 KB: 10 waves a CU)
+using WaveLdsS = std::conditional_t<RP_WIRE_SMALL2 != 0, WaveLdsT<kWTokS, 256, 7168, false>, WaveLdsT<kWTokS, kWLvlS>>;
 
 // SWAR over the four bytes of a dword: bit 7 of byte j set where byte j == c
 __device__ __forceinline__ uint32_t swar_eq(uint32_t x, uint8_t c) {
@@ -861,7 +871,12 @@ struct WaveMsg {
     uint32_t len, ntok;
     uint32_t sh;       // byte 0's offset in the staged dwords
     __device__ uint8_t at(uint32_t i) const { return b[i]; }
-    __device__ uint8_t tch(uint32_t t) const { return W->tc[t]; }
+    __device__ uint8_t tch(uint32_t t) const {
+        if constexpr (WL::kHasTc)
+            return W->tc[t];
+        else
+            return b[W->pos[t]];
+    }
     // no scalar byte strictly between byte offsets lo and hi
     __device__ bool clean(uint32_t lo, uint32_t hi) const {
         for (uint32_t i = lo + 1; i < hi;) {
@@ -1049,7 +1064,6 @@ __device__ bool wave_record(const WaveMsg<WL>& M, const Names& nm, uint64_t base
     f.sinc = LLONG_MIN;
     bool has_inc = false;
     const uint16_t* P = M.W->pos;
-    const uint8_t* TC = M.W->tc;
     uint32_t t = t0 + 1;
     if (t >= t1) return false;  // {} : no address
     while (true) {
@@ -1058,7 +1072,8 @@ __device__ bool wave_record(const WaveMsg<WL>& M, const Names& nm, uint64_t base
         if (t + 2 >= t1) return false;
         const uint32_t pm = P[t - 1], p0 = P[t], p1 = P[t + 1], p2 = P[t + 2], p3 = P[t + 3], p4 = P[t + 4],
                        p5 = P[t + 5];
-        const uint8_t c0 = TC[t], c1 = TC[t + 1], c2 = TC[t + 2], c3 = TC[t + 3], c4 = TC[t + 4], c5 = TC[t + 5];
+        const uint8_t c0 = M.tch(t), c1 = M.tch(t + 1), c2 = M.tch(t + 2), c3 = M.tch(t + 3), c4 = M.tch(t + 4),
+                      c5 = M.tch(t + 5);
         if (!((c0 == '"') & (c1 == '"') & (c2 == ':')) || !M.clean(pm, p0) || !M.clean(p1, p2)) return false;
         // 1 address, 2 source, 3 status, 4 id, 5 incarnationNumber, 6 sourceIncarnationNumber
         const int kind = M.rec_kind(p0 + 1, p1 - p0 - 1);
@@ -1163,14 +1178,13 @@ __device__ bool wave_records_mp(const WaveMsg<WL>& M, WL& W, const Names& nm, ui
     __builtin_amdgcn_wave_barrier();
     // members: boundary i that is a '{' or ',' starts one; its value ends at boundary i + 1
     const uint16_t* P = W.pos;
-    const uint8_t* TC = W.tc;
     uint32_t recbase = 0;
     bool bad = false;
     for (uint32_t i0 = 0; i0 < nb; i0 += 64) {
         const uint32_t i = i0 + lane;
         const bool in = i < nb;
         const uint32_t bt = in ? BT[-(int32_t)i] : 0u;
-        const uint8_t bc = in ? TC[bt] : (uint8_t)'}';
+        const uint8_t bc = in ? M.tch(bt) : (uint8_t)'}';
         const uint64_t mo = __ballot(in && bc == '{');
         const int32_t rec = (int32_t)(recbase + (uint32_t)__popcll(mo & lt)) + ((in && bc == '{') ? 0 : -1);
         recbase += (uint32_t)__popcll(mo);
@@ -1185,7 +1199,7 @@ __device__ bool wave_records_mp(const WaveMsg<WL>& M, WL& W, const Names& nm, ui
             continue;
         }
         const uint32_t pm = P[t - 1], p0 = P[t], p1 = P[t + 1], p2 = P[t + 2], p3 = P[t + 3], p4 = P[t + 4];
-        const uint8_t c0 = TC[t], c1 = TC[t + 1], c2 = TC[t + 2], c3 = TC[t + 3];
+        const uint8_t c0 = M.tch(t), c1 = M.tch(t + 1), c2 = M.tch(t + 2), c3 = M.tch(t + 3);
         if (!((c0 == '"') & (c1 == '"') & (c2 == ':')) || !M.clean(pm, p0) || !M.clean(p1, p2)) {
             bad = true;
             continue;
@@ -1211,7 +1225,7 @@ __device__ bool wave_records_mp(const WaveMsg<WL>& M, WL& W, const Names& nm, ui
         } else {
             nx = M.skip(t + 3);  // a string or a scalar (nested values were refused above)
         }
-        if (nx != sep || (TC[nx - 1] != ':' && !M.clean(P[nx - 1], P[nx]))) {
+        if (nx != sep || (M.tch(nx - 1) != ':' && !M.clean(P[nx - 1], P[nx]))) {
             bad = true;
             continue;
         }
@@ -1349,7 +1363,8 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WL::
 #endif
         const uint64_t b0 = I.msg_off[m], b1 = I.msg_off[m + 1];
         const uint64_t len64 = b1 - b0;
-        bool ok = len64 > 0 && len64 <= kWBuf;
+        bool ok = len64 > 0 && len64 <= WL::kBuf;
+        retry = PASS == 1 && len64 > WL::kBuf && len64 <= kWBuf;  // the next pass stages up to kWBuf
         const uintptr_t p0 = reinterpret_cast<uintptr_t>(I.buf) + b0;
         const uint32_t sh = (uint32_t)(p0 & 3u);
         const uint32_t len = ok ? (uint32_t)len64 : 0u;
@@ -1473,7 +1488,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WL::
                         const uint32_t w = j < 8 ? (j < 4 ? x[0] : x[1]) : (j < 12 ? x[2] : x[3]);
                         if (idx < WL::kTok) {
                             W.pos[idx] = (uint16_t)(4 * dw0 + j - sh);
-                            W.tc[idx] = (uint8_t)(w >> (8 * (j & 3u)));
+                            if constexpr (WL::kHasTc) W.tc[idx] = (uint8_t)(w >> (8 * (j & 3u)));
                         }
                         idx++;
                     }
@@ -1483,7 +1498,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WL::
                         if ((tm >> j) & 1u) {
                             if (idx < WL::kTok) {
                                 W.pos[idx] = (uint16_t)(4 * dw0 + j - sh);
-                                W.tc[idx] = (uint8_t)(x[j >> 2] >> (8 * (j & 3)));
+                                if constexpr (WL::kHasTc) W.tc[idx] = (uint8_t)(x[j >> 2] >> (8 * (j & 3)));
                             }
                             idx++;
                         }
@@ -1534,7 +1549,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WL::
                     if ((tm >> j) & 1u) {
                         if (idx < WL::kTok) {
                             W.pos[idx] = (uint16_t)(4 * dw + j - sh);
-                            W.tc[idx] = (uint8_t)(x >> (8 * j));
+                            if constexpr (WL::kHasTc) W.tc[idx] = (uint8_t)(x >> (8 * j));
                         }
                         idx++;
                     }
@@ -1558,10 +1573,11 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WL::
                 quotes += (uint32_t)__popcll(Po);
             }
         }
-        retry = ok && !bad && ntok > WL::kTok;
+        retry = retry || (ok && !bad && ntok > WL::kTok);
         ok = ok && !bad && ntok <= WL::kTok && (quotes & 1u) == 0 && ntok > 0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         WPROF(1);
+        WaveMsg<WL> M{&W, B, len, ntok, sh};
         // depth before every token
         int32_t depth = 0;
         bool neg = false;
@@ -1572,7 +1588,14 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WL::
         // three only in steps that hold one)
         for (uint32_t t0 = 0; kWaveDepth4 && ok && t0 < ntok; t0 += 256) {
             const uint32_t tb = t0 + 4u * lane;
-            const uint32_t cw = tb < ntok ? *reinterpret_cast<const uint32_t*>(&W.tc[tb]) : 0x20202020u;
+            uint32_t cw = 0x20202020u;
+            if constexpr (WL::kHasTc) {
+                if (tb < ntok) cw = *reinterpret_cast<const uint32_t*>(&W.tc[tb]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    if (tb + k < ntok) cw = (cw & ~(0xFFu << (8 * k))) | ((uint32_t)M.tch(tb + k) << (8 * k));
+            }
             uint32_t op = 0, cl = 0;  // bit k: token tb + k opens / closes
             int32_t pk[4];
             int32_t run = 0;
@@ -1634,7 +1657,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WL::
         }
         for (uint32_t t0 = 0; !kWaveDepth4 && ok && t0 < ntok; t0 += 64) {
             const uint32_t t = t0 + lane;
-            const uint8_t ch = t < ntok ? W.tc[t] : (uint8_t)' ';
+            const uint8_t ch = t < ntok ? M.tch(t) : (uint8_t)' ';
             const uint64_t Op = __ballot(t < ntok && wave_isopen(ch));
             const uint64_t Cl = __ballot(t < ntok && wave_isclose(ch));
             const int32_t d = depth + __popcll(Op & lt) - __popcll(Cl & lt);
@@ -1662,7 +1685,6 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WL::
         ok = ok && !neg && depth == 0 && nop1 <= 32 && nop1 == ncl2;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         WPROF(2);
-        WaveMsg<WL> M{&W, B, len, ntok, sh};
         // the top level, wave-uniformly: [records] or {key: value, ...}
         uint32_t arr = ntok, arr_end = ntok;  // the changes array's '[' and ']'
         uint32_t ck = 0, msrc = NULL_ID, mtgt = NULL_ID;
@@ -1919,7 +1941,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WL::
                 if (kWaveMembers) {
                     // the member boundaries too: record opens (level d + 1), member separators and
                     // record closes (d + 2), from the top of W.lvl down (never over a level token)
-                    const uint8_t c = in ? W.tc[t] : (uint8_t)' ';
+                    const uint8_t c = in ? M.tch(t) : (uint8_t)' ';
                     const bool b = (lv && c == '{') || (in && dt == d + 2 && (c == ',' || c == '}'));
                     deep |= in && dt > d + 2;
                     const uint64_t mb = __ballot(b);
@@ -1935,7 +1957,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WL::
                 ok = arr_end == arr + 1 && M.clean(W.pos[arr], W.pos[arr_end]);
             else
                 ok = nl < WL::kLvl && (nl & 1u) == 1u;
-            retry = nl >= WL::kLvl;
+            retry = retry || nl >= WL::kLvl;
             bool pat = true;
             for (uint32_t j = lane; ok && j < nl; j += 64) {
                 const uint32_t t = W.lvl[lv0 + j];
