@@ -661,7 +661,10 @@ constexpr uint32_t kWBuf = 8192;  // message bytes staged per wave (longer: the 
 // cannot take to the thread parser as the first pass does.
 constexpr uint32_t kWTok = 2048, kWLvl = 1024;   // the full layout
 constexpr uint32_t kWTokS = 1280, kWLvlS = 512;  // the first pass
-constexpr int kDecWaves = 4, kDecWavesS = 2;     // waves a workgroup
+#ifndef RP_WIRE_WAVES_S
+#define RP_WIRE_WAVES_S 2
+#endif
+constexpr int kDecWaves = 4, kDecWavesS = RP_WIRE_WAVES_S;     // waves a workgroup
 #ifndef RP_WIRE_MEMBERS
 #define RP_WIRE_MEMBERS 0
 #endif
