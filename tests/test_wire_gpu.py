@@ -22,6 +22,7 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
 import pywire  # noqa: E402
+import wire_texts as wt  # noqa: E402
 
 ST = {"alive": 0, "suspect": 1, "faulty": 2, "leave": 3}
 NULL = 0xFFFFFFFF
@@ -316,80 +317,28 @@ def test_host_buffer_full_api(gpu):
     assert L.rp_wire_decode(m._h, None, P(moff), 1, P(ro2), cap, ctypes.byref(rout), None, P(err)) != 0
 
 
-def _fuzz_texts(cases, seed):
-    """The reference's bodies re-serialised with random layouts and unknown members, then a set of
-    single-character mutations (most of them invalid JSON)."""
-    rng = random.Random(seed)
-    kinds = ["ping", "issueAs", "pingResponse", "fullSync", "pingReq", "pingReqResponse", "joinResponse"]
-    base = [c["out"][k] for c in cases for k in kinds]
-    ws = [" ", "\n", "\t", "\r\n ", ""]
-
-    def shuffle(o):
-        if isinstance(o, dict):
-            items = [(k, shuffle(v)) for k, v in o.items()]
-            rng.shuffle(items)
-            if rng.random() < 0.3:
-                items.insert(rng.randrange(len(items) + 1), ("x%d" % rng.randrange(9), rng.choice(
-                    [None, True, False, -12, "s:t[r]{,}", [1, {"b": "]"}, []], {"a": {"c": [None]}}, 3.5e2])))
-            return dict(items)
-        if isinstance(o, list):
-            return [shuffle(v) for v in o]
-        return o
-
-    out = []
-    for t in base:
-        out.append(t)
-        o = json.loads(t)
-        for _ in range(2):
-            sep = (rng.choice(ws) + "," + rng.choice(ws), rng.choice(ws) + ":" + rng.choice(ws))
-            out.append(rng.choice(ws) + json.dumps(shuffle(o), separators=sep) + rng.choice(ws))
-    mutants = []
-    for t in rng.sample(out, min(len(out), 400)):
-        if not t:
-            continue
-        i = rng.randrange(len(t))
-        kind = rng.randrange(9)
-        if kind == 0:
-            mutants.append(t[:i] + t[i + 1:])  # delete
-        elif kind == 1:
-            mutants.append(t[:i] + rng.choice('{}[]:,"\\ \t0a-.e\x01') + t[i:])  # insert
-        elif kind == 2:
-            mutants.append(t[:i])  # truncate
-        elif kind == 3:
-            mutants.append(t.replace("}", ",}", 1))  # trailing comma
-        elif kind == 4:
-            mutants.append(t.replace('"status"', '"status":"alive","status"', 1))  # duplicate key
-        elif kind == 5:
-            mutants.append(t + rng.choice([" ", "x", "]", ",", "{}"]))  # trailing bytes
-        elif kind == 6:  # a repeated body key: the last one wins
-            mutants.append(t.replace('"source"', '"source":"%s","source"' % rng.choice(["x", "127.0.0.1:3001"]), 1))
-        elif kind == 7:
-            mutants.append(t.replace('"checksum"', '"checksum":5,"checksum"', 1))
-        else:  # a repeated changes array
-            mutants.append(t.replace('"changes"', '"changes":[],"changes"', 1))
-    return out + mutants
-
-
 @pytest.mark.parametrize("grid", [None, "3"], ids=["wave-per-message", "waves-stride-messages"])
 def test_wave_decoder_equals_thread_decoder(gpu, monkeypatch, capfd, grid):
     """The wave-per-message decoder (k_decode_wave) and the thread parser (RP_WIRE_THREAD=1)
-    return identical columns, offsets, headers and error offsets on the reference's bodies,
-    re-laid-out variants with unknown members, and single-character mutants; the waves take
-    every well-formed message. grid "3": three workgroups, so every wave parses many messages
-    one after another in the same LDS (RP_WIRE_GRID)."""
-    cases = golden()
+    return the contract's columns (oracle/pywire.decode_columns: errors and their offsets,
+    records, headers) on the reference's bodies, re-laid-out variants with unknown members, and
+    single-character mutants, and identical columns to one another; the waves take every
+    well-formed message. grid "3": three workgroups, so every wave parses many messages one after
+    another in the same LDS (RP_WIRE_GRID)."""
+    cases = wt.golden()
     m = gpu.Membership()
-    for c in cases:
-        m.intern([mm[0] for mm in c["members"]] + [c["target"]])
-    texts = _fuzz_texts(cases, 11)
+    ids = wt.name_ids(m, wt.golden_names(cases))
+    texts = wt.fuzz_texts(cases, 11)
     if grid:
         monkeypatch.setenv("RP_WIRE_GRID", grid)
     monkeypatch.setenv("RP_WIRE_DEBUG", "1")
     capfd.readouterr()
     dw = gpu.wire_decode(m, texts)
     err = capfd.readouterr().err
+    wt.check_against_contract(dw, texts, ids, "waves")
     monkeypatch.setenv("RP_WIRE_THREAD", "1")
     dt = gpu.wire_decode(m, texts)
+    wt.check_against_contract(dt, texts, ids, "thread")
     for k in dt:
         assert np.array_equal(dw[k], dt[k]), k
     n_ok = int((dt["err"] == 0).sum())
@@ -439,46 +388,20 @@ def test_decode_name_lengths_around_the_inline_prefix(gpu, monkeypatch, thread):
     assert d["src"].tolist() == want_src
     assert d["source"].tolist() == want_hsrc
     assert d["target"].tolist() == want_tgt
+    wt.check_against_contract(d, texts, {n.encode(): int(i) for n, i in ids.items()}, "names")
     m.close()
-
-
-def _count_tokens(t):
-    """Quotes and the structural characters outside strings (the wave decoder's tokens)."""
-    n, ins, esc = 0, False, False
-    for ch in t:
-        if ins:
-            if esc:
-                esc = False
-            elif ch == "\\":
-                esc = True
-            elif ch == '"':
-                ins = False
-                n += 1
-        elif ch == '"':
-            ins = True
-            n += 1
-        elif ch in "{}[]:,":
-            n += 1
-    return n
 
 
 def test_two_pass_layouts_match_thread_parser(gpu, monkeypatch, capfd):
     """The wave decoder's first pass holds 1,280 tokens a message; longer token lists are left to
     the second pass (2,048 tokens), past that to the thread parser. Changes arrays of 40..120 short
-    records (about 740 to 2,180 tokens in under 8 KB) decode identically through both passes, the
-    full layout alone (RP_WIRE_ONEPASS=1) and the thread parser, and the waves take every message
-    of at most 2,048 tokens."""
-    rng = random.Random(9)
-    names = ["n%d" % i for i in range(200)]
+    records (about 740 to 2,180 tokens in under 8 KB) decode to the contract's columns through both
+    passes, the full layout alone (RP_WIRE_ONEPASS=1) and the thread parser, and the waves take
+    every message of at most 2,048 tokens."""
+    names, texts = wt.long_array_texts()
     m = gpu.Membership()
-    m.intern(names)
-    texts = []
-    for k in range(40, 124, 4):
-        recs = [{"address": rng.choice(names + ["zz%d" % k]), "status": rng.choice(list(ST)),
-                 "incarnationNumber": rng.randrange(10 ** 6)} for _ in range(k)]
-        texts.append(json.dumps({"checksum": k, "changes": recs, "source": names[k], "sourceIncarnationNumber": 1},
-                                separators=(",", ":")))
-    toks = [_count_tokens(t) for t in texts]
+    ids = wt.name_ids(m, names)
+    toks = [wt.count_tokens(t) for t in texts]
     assert min(toks) < 1280 < max(toks) and max(toks) > 2048 and any(1280 < x <= 2048 for x in toks)
     assert all(len(t) <= 8192 for t in texts)
     monkeypatch.setenv("RP_WIRE_DEBUG", "1")
@@ -491,6 +414,8 @@ def test_two_pass_layouts_match_thread_parser(gpu, monkeypatch, capfd):
     monkeypatch.delenv("RP_WIRE_ONEPASS")
     monkeypatch.setenv("RP_WIRE_THREAD", "1")
     dt = gpu.wire_decode(m, texts)
+    for what, d in (("two-pass", d2), ("one-pass", d1), ("thread", dt)):
+        wt.check_against_contract(d, texts, ids, what)
     for k in dt:
         assert np.array_equal(d2[k], dt[k]), k
         assert np.array_equal(d1[k], dt[k]), k
@@ -498,30 +423,49 @@ def test_two_pass_layouts_match_thread_parser(gpu, monkeypatch, capfd):
     m.close()
 
 
+def test_messages_past_the_first_pass_bytes(gpu, monkeypatch, capfd):
+    """Messages of 7.2-8 KB with fewer than 1,280 tokens (long addresses, sources, ids and an
+    unknown padding string; some addresses not interned) leave the first pass for its 7 KB byte
+    buffer, not its token count: the default two-pass layout, the full layout alone
+    (RP_WIRE_ONEPASS=1) and the thread parser all give the contract's columns, and the waves take
+    every message."""
+    names, texts = wt.big_byte_texts()
+    m = gpu.Membership()
+    ids = wt.name_ids(m, names)
+    assert all(7168 < len(t) <= 8192 for t in texts) and all(wt.count_tokens(t) < 1280 for t in texts)
+    monkeypatch.setenv("RP_WIRE_DEBUG", "1")
+    capfd.readouterr()
+    d2 = gpu.wire_decode(m, texts)
+    line = [x for x in capfd.readouterr().err.splitlines() if "by waves" in x][-1]
+    assert int(line.split()[3]) == len(texts), line
+    monkeypatch.setenv("RP_WIRE_ONEPASS", "1")
+    d1 = gpu.wire_decode(m, texts)
+    monkeypatch.delenv("RP_WIRE_ONEPASS")
+    monkeypatch.setenv("RP_WIRE_THREAD", "1")
+    dt = gpu.wire_decode(m, texts)
+    for what, d in (("two-pass", d2), ("one-pass", d1), ("thread", dt)):
+        wt.check_against_contract(d, texts, ids, what)
+    assert (dt["err"] == 0).all() and int(dt["rec_off"][-1]) > 10 * len(texts)
+    m.close()
+
+
 def test_bodies_past_64_members_take_the_serial_walk(gpu, monkeypatch, capfd):
     """The body's members are parsed a lane each up to 64 members; a body with more (unknown
     members around the known ones, a repeated source) takes the wave-uniform serial walk. Both
-    give the thread parser's columns and headers, and the waves take every such message."""
-    rng = random.Random(5)
-    names = ["10.0.0.%d:3000" % i for i in range(40)]
+    give the contract's columns and headers (and the thread parser's), and the waves take every
+    such message."""
+    names, texts = wt.many_member_texts()
     m = gpu.Membership()
-    m.intern(names)
-    texts = []
-    for nextra in (0, 30, 62, 63, 64, 65, 90):
-        body = [("checksum", 7), ("source", names[1]), ("sourceIncarnationNumber", 3)]
-        # scalars, and a few nested values (the wave parser tracks up to 32 depth-1 openers)
-        body += [("x%d" % j, [1, {"a": 1}] if j % 9 == 4 else rng.choice([1, "s", None, True])) for j in range(nextra)]
-        body.insert(rng.randrange(len(body) + 1), ("changes", [{"address": rng.choice(names), "status": "alive",
-                                                                 "incarnationNumber": j} for j in range(5)]))
-        body.append(("source", names[2]))  # the last repeated key wins
-        texts.append("{" + ",".join(json.dumps(k) + ":" + json.dumps(v) for k, v in body) + "}")
+    ids = wt.name_ids(m, names)
     monkeypatch.setenv("RP_WIRE_DEBUG", "1")
     capfd.readouterr()
     dw = gpu.wire_decode(m, texts)
     line = [x for x in capfd.readouterr().err.splitlines() if "by waves" in x][-1]
     assert int(line.split()[3]) == len(texts), line
+    wt.check_against_contract(dw, texts, ids, "waves")
     monkeypatch.setenv("RP_WIRE_THREAD", "1")
     dt = gpu.wire_decode(m, texts)
+    wt.check_against_contract(dt, texts, ids, "thread")
     for k in dt:
         assert np.array_equal(dw[k], dt[k]), k
     assert (dt["err"] == 0).all() and (dt["source"] == m.intern([names[2]])[0]).all()
