@@ -231,7 +231,7 @@ def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=512, warmup=3, 
 
     for b in range(warmup):
         one(b)
-    m.checksum
+    m.local_checksum() if world > 1 else m.checksum
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
@@ -241,7 +241,8 @@ def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=512, warmup=3, 
     e0.record(stream)
     for b in range(batches):
         one(warmup + b)
-    ck = m.checksum  # reads this replica's last checksum: every pending chain runs inside the timed region
+    # this replica's last checksum: every pending chain runs inside the timed region
+    ck = m.local_checksum() if world > 1 else m.checksum
     e1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -249,7 +250,7 @@ def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=512, warmup=3, 
     dt = time.perf_counter() - t0
     if world > 1:
         dt = reduce_max([dt])[0]
-        ck = m.checksums()[-1]  # the last batch's checksum (gathered once, after the timed region)
+        ck = m.latest_checksum()  # the last batch's checksum (gathered once, after the timed region)
     out = {"workload": "C3: %d-member table, %d updates/batch (1%% repeated addresses), fold + 1 checksum "
                        "per batch%s" % (n, k, ", %d replicas, batch-strided checksums" % world if world > 1 else ""),
            "n_gpus": world, "scaling": "strong", "batches": batches,
@@ -503,13 +504,20 @@ def api_latency_bench(timeout=300):
     return out
 
 
-def pmc_traffic():
+def pmc_traffic(keys, servers, nrep):
+    """roofline.traffic for this line: the PMC-measured HBM bytes per key of the C2 lookupN(3)
+    kernel (profiles/pmc_traffic.json, separate rocprofv3 --pmc passes) times this run's keys per
+    step, labelled with the kernel and run they were measured on. None off the C2 shape (another
+    server count or n), where no measurement exists."""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if not os.path.exists(p):
+    if not os.path.exists(p) or servers != 10000 or nrep != 3:
         return None, None
     with open(p) as f:
         d = json.load(f)
-    return d.get("lookupn_hbm_bytes_per_launch"), d.get("measured_on")
+    per_key = d["lookupn_hbm_bytes_per_launch"] / d["keys_per_launch"]
+    src = "%s; %.2f B/key measured over %d keys per launch (%s), scaled to %d keys" % (
+        d.get("measured_on"), per_key, d["keys_per_launch"], d.get("kernel"), keys)
+    return per_key * keys, src
 
 
 # ------------------------------------------------------------------ launcher
@@ -656,7 +664,7 @@ def main():
         if args.sim5_n else None
     if rank == 0:
         achieved = BYTES_PER_LOOKUPN3 * B / (kern_ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic()
+        traffic, traffic_src = pmc_traffic(B, args.servers, args.nrep)
         out = {
             "metric": METRIC,
             "value": total / elapsed,

@@ -105,8 +105,11 @@ int rp_ring_lookupn(rp_ring *r, const char *keys, const uint64_t *off, uint32_t 
  * idle_ms > 0, a one-key rp_ring_lookup / rp_ring_lookupn (key <= 180 B, n <= 8) is answered by a
  * resident service wave (one workgroup on one CU) that polls pinned, device-mapped host lines,
  * instead of a kernel launch and a stream sync per call. The wave exits after idle_ms without a
- * request (and after 30 s in all) and is relaunched by the next call; a ring mutation stops it.
- * idle_ms = 0 (the default) turns it off. */
+ * request (and after 30 s in all) and is relaunched by the next call; a ring mutation and every
+ * other device call on this ring (batch lookups, grouping, dump) stop it first. While it is
+ * resident, a device-buffer release anywhere else in the process (another handle's buffer
+ * growing: hipFree synchronizes the device) waits for it to idle out: keep idle_ms short where
+ * other handles allocate. idle_ms = 0 (the default) turns it off. */
 int rp_ring_service(rp_ring *r, uint32_t idle_ms);
 /* Same with precomputed key hashes (hashFunc(key) done by the caller). */
 int rp_ring_lookup_hashes(rp_ring *r, const uint32_t *hashes, uint64_t n, uint32_t *owners);

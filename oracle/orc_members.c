@@ -10,6 +10,7 @@
  *   Membership.getJoinPosition (Math.random injected: Philox)    lib/membership/index.js:129-131
  * Members are identified by interned address ids 0..n_names-1 (names given up front).
  */
+#include <stdint.h>
 #include <stdio.h>
 #include <pthread.h>
 #include <stdlib.h>
@@ -199,14 +200,68 @@ static void *copy_worker(void *p) {
     return NULL;
 }
 
+/* A persistent pool for the *_mt paths: T - 1 workers parked on a barrier, the caller is
+ * thread 0. Creating threads per phase (three phases per batch) cost more than the phases
+ * (bench C3 baseline, round 4: 16 threads slower than 1). */
+typedef void *(*pool_fn)(void *);
+static struct {
+    int T;
+    pthread_t th[256];
+    pthread_barrier_t start, done;
+    pool_fn fn;
+    void *arg[256];
+    int quit;
+} g_pool;
+
+static void *pool_main(void *p) {
+    const int t = (int)(intptr_t)p;
+    for (;;) {
+        pthread_barrier_wait(&g_pool.start);
+        if (g_pool.quit) return NULL;
+        g_pool.fn(g_pool.arg[t]);
+        pthread_barrier_wait(&g_pool.done);
+    }
+}
+
+static void pool_stop(void) {
+    if (g_pool.T <= 1) return;
+    g_pool.quit = 1;
+    pthread_barrier_wait(&g_pool.start);
+    for (int t = 1; t < g_pool.T; t++) pthread_join(g_pool.th[t], NULL);
+    pthread_barrier_destroy(&g_pool.start);
+    pthread_barrier_destroy(&g_pool.done);
+    g_pool.T = 0;
+    g_pool.quit = 0;
+}
+
+/* fn(args[t]) for t < T on the pool, the caller running t = 0; returns when all are done. */
+static void pool_run(int T, pool_fn fn, void *const *args) {
+    if (T <= 1) {
+        fn(args[0]);
+        return;
+    }
+    if (g_pool.T != T) {
+        pool_stop();
+        pthread_barrier_init(&g_pool.start, NULL, (unsigned)T);
+        pthread_barrier_init(&g_pool.done, NULL, (unsigned)T);
+        g_pool.T = T;
+        for (int t = 1; t < T; t++) pthread_create(&g_pool.th[t], NULL, pool_main, (void *)(intptr_t)t);
+    }
+    g_pool.fn = fn;
+    for (int t = 0; t < T; t++) g_pool.arg[t] = args[t];
+    pthread_barrier_wait(&g_pool.start);
+    fn(args[0]);
+    pthread_barrier_wait(&g_pool.done);
+}
+
 static void compute_checksum_mt(orc_members *m, int T) {
     if (T <= 1 || m->n_names < 4096) {
         compute_checksum(m);
         return;
     }
     ensure_buf(m);
-    pthread_t th[256];
     fmt_job jobs[256];
+    void *args[256] = {0};
     const uint32_t per = (m->n_names + T - 1) / T;
     for (int t = 0; t < T; t++) {
         uint32_t k0 = (uint32_t)t * per, k1 = k0 + per;
@@ -220,16 +275,15 @@ static void compute_checksum_mt(orc_members *m, int T) {
             m->tbuf[t] = (char *)malloc(m->tcap[t]);
         }
         jobs[t] = (fmt_job){m, k0, k1, m->tbuf[t], 0, 0, m->buf};
-        pthread_create(&th[t], NULL, fmt_worker, &jobs[t]);
+        args[t] = &jobs[t];
     }
+    pool_run(T, fmt_worker, args);
     uint64_t o = 0;
     for (int t = 0; t < T; t++) {
-        pthread_join(th[t], NULL);
         jobs[t].off = o;
         o += jobs[t].len;
     }
-    for (int t = 0; t < T; t++) pthread_create(&th[t], NULL, copy_worker, &jobs[t]);
-    for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
+    pool_run(T, copy_worker, args);
     if (o) o--;
     m->checksum = orc_hash32((const uint8_t *)m->buf, o);
     m->has_checksum = 1;
@@ -299,7 +353,7 @@ typedef struct {
     const uint32_t *ids;
     const uint8_t *status;
     const int64_t *inc;
-    uint32_t k, t, T;
+    uint32_t k, lo, hi; /* this thread's ids: [lo, hi) */
     int64_t now_ms;
     uint8_t *applied;
     uint32_t napplied;
@@ -310,7 +364,7 @@ static void *fold_worker(void *p) {
     orc_members *m = j->m;
     for (uint32_t i = 0; i < j->k; i++) {
         uint32_t id = j->ids[i];
-        if ((uint32_t)(((uint64_t)id * j->T) / m->n_names) != j->t) continue; /* contiguous id ranges: no false sharing */
+        if (id < j->lo || id >= j->hi) continue; /* contiguous id ranges: no false sharing */
         uint8_t st = j->status[i];
         int64_t in = j->inc[i];
         int applied = 0;
@@ -337,17 +391,18 @@ uint32_t orc_members_update_mt(orc_members *m, const uint32_t *ids, const uint8_
         if (!m->exists[ids[i]] || !m->is_ready) return 0xFFFFFFFFu; /* only the no-create, ready case */
     if (threads < 1) threads = 1;
     if (threads > 256) threads = 256;
-    pthread_t th[256];
     fold_job jobs[256];
+    void *args[256] = {0};
+    const uint32_t per = (m->n_names + threads - 1) / threads;
     for (int t = 0; t < threads; t++) {
-        jobs[t] = (fold_job){m, ids, status, inc, k, (uint32_t)t, (uint32_t)threads, now_ms, applied_out, 0};
-        pthread_create(&th[t], NULL, fold_worker, &jobs[t]);
+        const uint32_t lo = (uint32_t)t * per, hi = lo + per;
+        jobs[t] = (fold_job){m, ids, status, inc, k, lo < m->n_names ? lo : m->n_names,
+                             hi < m->n_names ? hi : m->n_names, now_ms, applied_out, 0};
+        args[t] = &jobs[t];
     }
+    pool_run(threads, fold_worker, args);
     uint32_t napplied = 0;
-    for (int t = 0; t < threads; t++) {
-        pthread_join(th[t], NULL);
-        napplied += jobs[t].napplied;
-    }
+    for (int t = 0; t < threads; t++) napplied += jobs[t].napplied;
     if (napplied) compute_checksum_mt(m, threads);
     return napplied;
 }

@@ -712,37 +712,45 @@ class DistMembership(Membership):
         self._group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self._hist_h = np.zeros(0, dtype=np.uint32)  # this rank's drained record
-        self._hist_a = np.zeros(0, dtype=np.uint8)
+        # the gathered record (round 5): values interleaved so far and the carried
+        # value; each gather moves only the entries recorded since the previous one
+        self._out = []
+        self._cur = None
         self.checksum_shard(self.world, self.rank, history_cap)
 
     @property
     def checksum(self):
-        """Membership.checksum after the last batch. Rank g hashes only batches b % G == g, so the
-        latest value lives on one rank: with G > 1 this is a collective (every rank must read it,
-        as with checksums()); with G = 1 it is the device's own value."""
+        """Membership.checksum after the last batch. With G = 1 the device's own value. With
+        G > 1 the latest value lives on one rank, so reading it is a collective: use
+        latest_checksum() on every rank (local_checksum() for this rank's own latest value)."""
         if self.world == 1:
             return Membership.checksum.fget(self)
-        cs = self.checksums()
-        return cs[-1] if cs else Membership.checksum.fget(self)
+        raise RingpopAmdError("DistMembership.checksum over %d ranks is a collective: call "
+                              "latest_checksum() on every rank" % self.world)
+
+    def local_checksum(self):
+        """The checksum of the latest batch this rank hashed (b % G == rank), after its pending
+        chains finish; no collective."""
+        return Membership.checksum.fget(self)
+
+    def latest_checksum(self):
+        """Membership.checksum after the last batch (a collective: every rank calls it)."""
+        self._gather()
+        return self._cur
 
     def compute_checksum(self):
         """computeChecksum() of this rank's replica, which is the whole table: local, no collective."""
         check(lib().rp_members_compute_checksum(self._h))
         return Membership.checksum.fget(self)
 
-    def checksums(self):
-        """The checksum after every update batch since construction (None before the first
-        applied one), in batch order: every rank's recorded values gathered and interleaved, a
-        batch that applied nothing carrying the previous value forward (index.js:306-309).
-        A collective: every rank calls it."""
+    def _gather(self):
+        """Drain this rank's device record, gather every rank's entries recorded since the last
+        gather (one all-gather of the counts, one of the entries) and interleave them in batch
+        order onto the host record."""
         import torch
         h, a = self.checksum_history()
         if len(h):
             check(lib().rp_members_checksum_history_drain(self._h, len(h)))
-            self._hist_h = np.concatenate([self._hist_h, h])
-            self._hist_a = np.concatenate([self._hist_a, a])
-        h, a = self._hist_h, self._hist_a
         if self.world > 1:
             # nccl (RCCL) gathers device tensors; gloo host tensors
             dev = "cuda" if self._dist.get_backend(self._group) == "nccl" else "cpu"
@@ -751,24 +759,34 @@ class DistMembership(Membership):
             self._dist.all_gather(ns, n, group=self._group)
             ns = [int(x.item()) for x in ns]
             cap = max(ns)
+            if cap == 0:
+                return
             mine = torch.zeros(cap, 2, dtype=torch.int64)
             mine[:len(h), 0] = torch.from_numpy(h.astype(np.int64))
             mine[:len(h), 1] = torch.from_numpy(a.astype(np.int64))
             parts = [torch.zeros(cap, 2, dtype=torch.int64, device=dev) for _ in range(self.world)]
             self._dist.all_gather(parts, mine.to(dev), group=self._group)
-            parts = [x.cpu() for x in parts]
+            parts = [x.cpu().numpy() for x in parts]
         else:
             ns = [len(h)]
-            parts = [torch.from_numpy(np.stack([h.astype(np.int64), a.astype(np.int64)], axis=1))]
-        total = sum(ns)
-        out, cur = [], None
-        for b in range(total):
-            g, j = b % self.world, b // self.world
-            hv, av = int(parts[g][j, 0]), int(parts[g][j, 1])
+            parts = [np.stack([h.astype(np.int64), a.astype(np.int64)], axis=1)]
+        ptr = [0] * self.world
+        b0 = len(self._out)
+        for b in range(b0, b0 + sum(ns)):
+            g = b % self.world
+            hv, av = parts[g][ptr[g]]
+            ptr[g] += 1
             if av:
-                cur = hv
-            out.append(cur)
-        return out
+                self._cur = int(hv)
+            self._out.append(self._cur)
+
+    def checksums(self):
+        """The checksum after every update batch since construction (None before the first
+        applied one), in batch order: every rank's recorded values gathered and interleaved, a
+        batch that applied nothing carrying the previous value forward (index.js:306-309).
+        A collective: every rank calls it."""
+        self._gather()
+        return list(self._out)
 
 
 SIM_EVENT = {"kill": 0, "revive": 1, "leave": 2, "join": 3}
@@ -1088,8 +1106,16 @@ class MessageExchange:
         self.device = torch.device("cuda", device) if self.on_device and isinstance(device, int) else \
             (device if self.on_device else "cpu")
         self._copy = copy
-        self._cnt = torch.zeros(2 * self.G, dtype=torch.int64, device=self.device)
-        self._rcnt = torch.zeros(2 * self.G, dtype=torch.int64, device=self.device)
+        # the per-peer counts are host integers already (the outbox read), and all_to_all_single
+        # takes its split sizes as host integers: with nccl they cross ranks over a gloo group of
+        # the same ranks (no device collective, no device -> host read, round 5)
+        if self.on_device:
+            ranks = list(range(self.G)) if group is None else dist.get_process_group_ranks(group)
+            self._cgroup = dist.new_group(ranks=ranks, backend="gloo")
+        else:
+            self._cgroup = group
+        self._cnt = torch.zeros(2 * self.G, dtype=torch.int64)
+        self._rcnt = torch.zeros(2 * self.G, dtype=torch.int64)
         self._host = {}  # gloo staging buffers, kept across rounds
         self._events = []  # (start, end) of every byte collective queued on the device
 
@@ -1123,12 +1149,13 @@ class MessageExchange:
         for this rank in source order. after(stream): with the nccl backend, called with torch's
         stream once the byte collective is queued on it, so the consumer orders its next work
         after it on the device (rp_sim_wait_stream); without it the host waits for the stream.
-        The per-peer counts do cross to the host once per exchange: torch's all_to_all_single
-        takes its split sizes as host integers, and the inbox is sized from them."""
+        The per-peer counts are host integers (torch's all_to_all_single takes its split sizes
+        as host integers, and the inbox is sized from them); they cross ranks on the host (a gloo
+        group beside the nccl one), so the exchange itself never waits for the device."""
         torch, dist, G = self.torch, self.dist, self.G
         self._cnt.copy_(torch.from_numpy(np.stack([out_nmsg, out_nrec], axis=1).astype(np.int64).reshape(-1)))
-        dist.all_to_all_single(self._rcnt, self._cnt, group=self.group)
-        rc = self._rcnt.cpu().numpy().reshape(G, 2)
+        dist.all_to_all_single(self._rcnt, self._cnt, group=self._cgroup)
+        rc = self._rcnt.numpy().reshape(G, 2)
         in_nmsg, in_nrec = rc[:, 0].astype(np.uint64), rc[:, 1].astype(np.uint64)
         seg_out = [int(out_nmsg[g]) * MSG_BYTES + int(out_nrec[g]) * REC_BYTES for g in range(G)]
         seg_in = [int(in_nmsg[g]) * MSG_BYTES + int(in_nrec[g]) * REC_BYTES for g in range(G)]
@@ -1158,13 +1185,17 @@ class MessageExchange:
             self.copy(in_buf, recv.data_ptr(), tot_in)
         return in_nmsg, in_nrec
 
-    def sum_bytes(self, buf, nbytes):
-        """Byte-wise sum of every rank's device buffer into each rank's (the join exchange)."""
+    def sum_bytes(self, buf, nbytes, after=None):
+        """Byte-wise sum of every rank's device buffer into each rank's (the join exchange).
+        after(stream): as in exchange (nccl: the consumer waits on the device, not the host)."""
         torch, dist = self.torch, self.dist
         if self.on_device:
             t = torch.as_tensor(_DeviceBytes(buf, nbytes), device=self.device)
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
-            torch.cuda.current_stream().synchronize()
+            if after is not None:
+                after(torch.cuda.current_stream().cuda_stream)
+            else:
+                torch.cuda.current_stream().synchronize()
         else:
             h = self._staging("join", nbytes)
             self.copy(h.data_ptr(), buf, nbytes)
@@ -1204,7 +1235,7 @@ class DistGossipSim:
                 if not has:
                     break
                 t = time.perf_counter()
-                self.xchg.sum_bytes(buf, nb)
+                self.xchg.sum_bytes(buf, nb, after=wait)
                 self.exchange_s += time.perf_counter() - t
                 sh.join_import()
             for k in range(SIM_STAGES):

@@ -105,6 +105,11 @@ struct CompactView {
     uint32_t idx_bytes;
     uint32_t wpred;  // lean kernel: window 1 starts where the key's hash falls in its bucket (A/B:
                      // RP_LOOKUP_WPRED=0 starts it at the bucket start)
+    // round 5: the hinted index (lookupN(3) in the lean kernel): per group of 8 buckets
+    // {14-bit signed base - pred(g) | 8 x 2-bit window-start hints, nibble counts}, pred(g) =
+    // g * M >> (cb - 3); hint h moves window 1's start by h - 1 entries (chosen at build time per
+    // bucket so that the most of its hash range resolves in window 1). idxh null: no hints.
+    const uint32_t* idxh;
 };
 
 // Exact view for the compact kernel's deferred keys: the bucket start comes from the compact
@@ -751,8 +756,13 @@ __device__ unsigned long long g_lk_prof[10];
 // registers first (PER x u32x4 held), then the slices go through LDS one after another. 1: the
 // slices are DMA'd global -> LDS (global_load_lds_dwordx4, no VGPR destination) into a ring of
 // two slice buffers, slice s + 2 issued as soon as slice s is hashed (A/B: RP_LOOKUP_STG=1).
-template <int KPL, int NEED, int HS = 1, bool FUSE = false, int STG = 0, int LH = 1>
-__global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __restrict__ keys, uint64_t ntiles,
+// PF (round 5; STG 0 only): the next tile's key loads are issued at the tail of this tile, after
+// the listed keys' second-window loads and before their results are used, so the key stream's HBM
+// latency runs under the second windows, the barrier and the row stores instead of after them
+// (vmcnt retires in issue order: the second windows are waited for with the key loads still
+// outstanding). A/B: RP_LOOKUP_PF.
+template <int KPL, int NEED, int HS = 1, bool FUSE = false, int STG = 0, int LH = 1, bool PF = false>
+__global__ __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_lookupn_lean(const uint8_t* __restrict__ keys, uint64_t ntiles,
                                                              CompactView cv, uint32_t* __restrict__ out,
                                                              uint8_t* __restrict__ counts,
                                                              uint32_t* __restrict__ slow_list,
@@ -782,8 +792,10 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
     const uint32_t rmask = (1u << bsh) - 1u;
     const __amdgpu_buffer_rsrc_t ent_r =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(cv.ent), 0, (int)cv.ent_bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t idx_r =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(cv.idx), 0, (int)cv.idx_bytes, 0x00020000);
+    // lookupN(3) reads the hinted index when the ring has one (round 5; RP_LOOKUP_HINT=0: A/B)
+    const bool hinted = NEED == 3 && cv.idxh != nullptr && !(cv.ablate & 4u);
+    const __amdgpu_buffer_rsrc_t idx_r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint32_t*>(hinted ? cv.idxh : cv.idx), 0, (int)cv.idx_bytes, 0x00020000);
     auto load16 = [&](uint32_t pos) {
         return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ent_r, (int)(3u * pos), 0, 0));
     };
@@ -801,9 +813,10 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
     // (Poisson buckets of 1.9 tokens; lookupN(2): 3.3 % -> 1.6 %). Long buckets (> 10) keep w = 0,
     // and so does lookup (NEED 1), whose window at 0 already resolves positions 0..4 (0.9 % of keys
     // past it against 1.5 % with the predicted start).
-    auto wstart = [&](uint32_t hk, uint32_t bck) -> uint32_t {
-        const uint32_t fl = (((hk << cv.cb) >> 24) * bck) >> 8;
-        return (NEED >= 2 && cv.wpred && bck <= 10u && fl > 1u) ? fl - 1u : 0u;
+    // hint (the hinted index): the start moves by hint - 1 entries (1 = the plain prediction)
+    auto wstart = [&](uint32_t hk, uint32_t bck, uint32_t hint) -> uint32_t {
+        const int fl = (int)((((hk << cv.cb) >> 24) * bck) >> 8) - 2 + (int)hint;
+        return (NEED >= 2 && cv.wpred && bck <= 10u && fl > 0) ? (uint32_t)fl : 0u;
     };
     // a listed key's second window (held by one lane): finish it, write its row into `row`
     auto finish2 = [&](const u32x4 win, uint32_t K, uint32_t w2, uint32_t* row, uint8_t* cnt, uint32_t* nsl,
@@ -838,6 +851,16 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
 #ifdef RP_LK_PROF
     uint64_t pa[6] = {0, 0, 0, 0, 0, 0}, ntl = 0;
 #endif
+    static_assert(!PF || (STG == 0 && V4 % kLkThreads == 0), "PF: register staging of whole tiles");
+    u32x4 pre[PF ? PER : 1];
+    auto load_tile = [&](uint64_t tt) {
+        const u32x4* s4 = reinterpret_cast<const u32x4*>(keys + tt * TK * LEN);
+#pragma unroll
+        for (int q = 0; q < PER; q++) pre[q] = __builtin_nontemporal_load(s4 + tid + q * kLkThreads);
+    };
+    if constexpr (PF) {
+        if (blockIdx.x < ntiles) load_tile(blockIdx.x);
+    }
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint64_t base = t * TK;
         uint32_t h[KPL];
@@ -911,6 +934,25 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
                     dma(hs + 2);
                 }
             }
+        } else if constexpr (PF) {
+            if (tid == 0) nslow_tile = 0;
+#pragma unroll
+            for (int hs = 0; hs < HS; hs++) {
+                if (hs) __syncthreads();  // the previous slice is hashed
+#pragma unroll
+                for (int q = 0; q < PER; q++) {
+                    const int k = tid + q * kLkThreads;
+                    if (k >= hs * VS && k < (hs + 1) * VS) reinterpret_cast<u32x4*>(sk)[k - hs * VS] = pre[q];
+                }
+                __syncthreads();
+#pragma unroll
+                for (int k = hs * (KPL / HS); k < (hs + 1) * (KPL / HS); k++) {
+                    uint32_t w[W4];
+#pragma unroll
+                    for (int j = 0; j < W4; j++) w[j] = sk[(tid + (k - hs * (KPL / HS)) * kLkThreads) * W4 + j];
+                    h[k] = fh::hash32_words<LEN>(w);
+                }
+            }
         } else {
             const u32x4* s4 = reinterpret_cast<const u32x4*>(keys + base * LEN);
             u32x4 pre[PER];
@@ -961,19 +1003,37 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
 #pragma unroll
         for (int kq = 0; kq < KH; kq++) {
             const int k = hh * KH + kq;
-            rec[kq] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(idx_r, (int)((h[k] >> (bsh + 3u)) * 8u), 0, 0));
+            if (cv.ablate & 4u)  // diagnostics: no index trip (a record made from the hash)
+                rec[kq] = u32x2{(uint32_t)(((uint64_t)h[k] * (cv.M - 32u)) >> 32), h[k] & 0x11111111u};
+            else
+                rec[kq] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(idx_r, (int)((h[k] >> (bsh + 3u)) * 8u), 0, 0));
         }
-        uint32_t lo[KH], bc[KH];
+        uint32_t lo[KH], bc[KH], ws[KH];
         u32x4 win[KH];
 #pragma unroll
         for (int kq = 0; kq < KH; kq++) {
             const int k = hh * KH + kq;
             const uint32_t s4 = ((h[k] >> bsh) & 7u) * 4u;
             const uint32_t below = rec[kq].y & ((1u << s4) - 1u);
-            lo[kq] = rec[kq].x + __builtin_amdgcn_sad_u8(below & 0x0F0F0F0Fu, 0u,
-                                                         __builtin_amdgcn_sad_u8((below >> 4) & 0x0F0F0F0Fu, 0u, 0u));
+            uint32_t base = rec[kq].x, hint = 1u;
+            if (hinted) {  // base = pred(g) + the 14-bit delta; the bucket's 2-bit hint
+                const uint32_t g = h[k] >> (bsh + 3u);
+                base = (uint32_t)(((uint64_t)g * cv.M) >> (cv.cb - 3u)) + (uint32_t)((int32_t)(rec[kq].x << 18) >> 18);
+                hint = (rec[kq].x >> (14u + (s4 >> 1))) & 3u;
+            }
+            lo[kq] = base + __builtin_amdgcn_sad_u8(below & 0x0F0F0F0Fu, 0u,
+                                                    __builtin_amdgcn_sad_u8((below >> 4) & 0x0F0F0F0Fu, 0u, 0u));
             bc[kq] = (rec[kq].y >> s4) & 15u;
-            win[kq] = load16(lo[kq] + wstart(h[k], bc[kq]));
+            ws[kq] = wstart(h[k], bc[kq], hint);
+            if (cv.ablate & 10u) {  // diagnostics: 2 = windows rounded down to 16 B (no line crossing);
+                                    // 8 = no window trip (entries made from the record)
+                const uint32_t pos = lo[kq] + ws[kq];
+                win[kq] = (cv.ablate & 8u) ? u32x4{rec[kq].x, rec[kq].y, h[k], pos}
+                                           : __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                          ent_r, (int)((3u * pos) & ~15u), 0, 0));
+            } else {
+                win[kq] = load16(lo[kq] + ws[kq]);
+            }
         }
 #ifdef RP_LK_PROF
         if (hh == 0) {
@@ -987,7 +1047,7 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
             uint32_t e[5];
             ent5v(win[kq], e);
             const uint32_t K = ((h[k] & rmask) >> cv.fsh) << cv.ob;
-            const uint32_t w = wstart(h[k], bc[kq]);
+            const uint32_t w = ws[kq];
             uint32_t lt = 0;  // in-bucket window entries below the key: the position is lo + w + lt
             bool tie = false;
 #pragma unroll
@@ -1012,7 +1072,7 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
             const uint32_t kk = tid + k * kLkThreads;
             bool slow = (tie && !cv.exact) | (lo[kq] + 20u > cv.M);
             const bool under = w > 0u && lt == 0u;  // the key lies before window 1's first entry
-            const bool again = !slow && (lt > SPAN || dup || under);
+            const bool again = !slow && (lt > SPAN || dup || under) && !(cv.ablate & 1u);  // 1: diagnostics
             const uint64_t m = __ballot(again);
             const uint32_t pos = nag + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             nag += (uint32_t)__popcll(m);
@@ -1043,9 +1103,24 @@ __global__ __launch_bounds__(kLkThreads) void k_lookupn_lean(const uint8_t* __re
         LK_T(t4, nag);
         // second windows, one listed key per lane (the list is this wave's own LDS rows)
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        for (uint32_t j = lane; j < (nag < AG ? nag : AG); j += 64)
-            finish2(load16(ag[wv][0][j]), ag[wv][1][j], ag[wv][2][j], so, counts ? counts + base : nullptr,
-                    &nslow_tile, slow_list + t * kSlowPerTile);
+        if constexpr (PF) {
+            // AG == 64: one listed key per lane at most. Lanes without one load past the buffer's
+            // range (no memory request, zeros returned), so the load is not under a branch and the
+            // wait for it counts the key loads issued after it.
+            static_assert(AG == 64, "one listed key per lane");
+            const bool has2 = (uint32_t)lane < nag;
+            const u32x4 w2 = __builtin_bit_cast(
+                u32x4, __builtin_amdgcn_raw_buffer_load_b128(ent_r, has2 ? (int)(3u * ag[wv][0][lane]) : 0x7FFFFFF0, 0, 0));
+            const uint64_t tn = t + gridDim.x;
+            load_tile(tn < ntiles ? tn : t);  // the last tile re-loads its own keys (in bounds, unused)
+            if (has2)
+                finish2(w2, ag[wv][1][lane], ag[wv][2][lane], so, counts ? counts + base : nullptr, &nslow_tile,
+                        slow_list + t * kSlowPerTile);
+        } else {
+            for (uint32_t j = lane; j < (nag < AG ? nag : AG); j += 64)
+                finish2(load16(ag[wv][0][j]), ag[wv][1][j], ag[wv][2][j], so, counts ? counts + base : nullptr,
+                        &nslow_tile, slow_list + t * kSlowPerTile);
+        }
         LK_T(t5a, nag);
         __syncthreads();
         LK_T(t5, tid);
@@ -1463,6 +1538,67 @@ __global__ void k_cindex(const uint32_t* __restrict__ bst, uint32_t ngroups, uin
     }
 }
 
+// The hinted index of the lean kernel's lookupN(3) (round 5): per group g of 8 buckets,
+// x = (base - pred(g)) & 0x3FFF | hints << 14 and y = the nibble counts (as k_cindex), pred(g) =
+// g * M >> (cb - 3). Bucket s's 2-bit hint h moves window 1's start to max(0, fl - 1 + h - 1)
+// (fl = the key's 8 top residual bits x count >> 8, the lean kernel's prediction): of the three,
+// the start whose window resolves the largest share of the bucket's hash range (a key whose
+// position in the bucket is rel resolves at w = 0 when rel <= 2, at w > 0 when rel is w + 1 or
+// w + 2). Buckets of more than 10 tokens keep w = 0 (hint 1). over |= 1 when a base delta does
+// not fit 14 bits (the lean kernel then runs without hints).
+__global__ void k_cindex_hint(const uint32_t* __restrict__ tok, const uint32_t* __restrict__ bst, uint32_t M,
+                              uint32_t cb, uint32_t ngroups, uint32_t* __restrict__ idx, uint32_t* __restrict__ over) {
+    const uint32_t bsh = 32u - cb;
+    const uint32_t qsh = bsh - 8u;  // residual >> qsh = the 8 bits the kernel's prediction reads
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ngroups; g += gstride) {
+        const uint32_t base = bst[g * 8];
+        const int64_t delta = (int64_t)base - (int64_t)(((uint64_t)g * M) >> (cb - 3));
+        if (delta < -8192 || delta > 8191) atomicOr(over, 1u);
+        uint32_t nib = 0, hints = 0;
+        for (int s = 0; s < 8; s++) {
+            const uint32_t lo = bst[g * 8 + s], bc = bst[g * 8 + s + 1] - lo;
+            nib |= (bc > 15u ? 15u : bc) << (4 * s);
+            uint32_t best = 1;
+            if (bc <= 10u) {
+                // resolved length of the hash range for each hint, walking the 256 prediction
+                // slices and the bucket's token residuals in order
+                uint64_t g0 = 0, g1 = 0, g2 = 0;  // resolved lengths for hints 0, 1, 2
+                uint32_t j = 0;  // tokens below the slice start
+                const uint64_t S = 1ull << qsh;
+                for (uint32_t q = 0; q < 256; q++) {
+                    const uint32_t fl = (q * bc) >> 8;
+                    uint64_t a = (uint64_t)q * S;
+                    const uint64_t e = a + S;
+                    uint32_t rel = j;
+                    while (true) {
+                        // [a, nxt) has position rel
+                        const uint64_t tn = rel < bc ? (uint64_t)(tok[lo + rel] & ((1u << bsh) - 1u)) + 1ull : e;
+                        const uint64_t nxt = tn < e ? tn : e;
+                        if (nxt > a) {
+                            auto ok = [&](int w0) {
+                                const uint32_t w = w0 > 0 ? (uint32_t)w0 : 0u;
+                                return w == 0 ? rel <= 2u : (rel == w + 1 || rel == w + 2);
+                            };
+                            g0 += ok((int)fl - 2) ? nxt - a : 0;
+                            g1 += ok((int)fl - 1) ? nxt - a : 0;
+                            g2 += ok((int)fl) ? nxt - a : 0;
+                            a = nxt;
+                        }
+                        if (a >= e) break;
+                        rel++;
+                    }
+                    while (j < bc && (uint64_t)(tok[lo + j] & ((1u << bsh) - 1u)) < e) j++;
+                }
+                best = (g1 >= g0 && g1 >= g2) ? 1u : (g0 >= g2 ? 0u : 2u);
+            }
+            hints |= best << (2 * s);
+        }
+        idx[2 * g] = ((uint32_t)delta & 0x3FFFu) | (hints << 14);
+        idx[2 * g + 1] = nib;
+    }
+}
+
 // checksum string pieces: len of (name + ';') for in-ring servers in name order.
 __global__ void k_ck_len(const uint32_t* __restrict__ sorted_ids, uint32_t n,
                          const uint8_t* __restrict__ in_ring, const uint64_t* __restrict__ noff,
@@ -1538,6 +1674,8 @@ struct Ring {
     // compact lookup layout (the C2 hot path; valid while every interned id < 2^16)
     DevBuf<uint8_t> cent;
     DevBuf<uint32_t> cidx;
+    DevBuf<uint32_t> cidxh;  // the hinted index (k_cindex_hint); valid when chint
+    bool chint = false;
     bool compact = false;
     uint32_t ccb = 0, cob = 0, cfsh = 0;
     // checksum string + value
@@ -1574,7 +1712,9 @@ struct Ring {
         const char* a = getenv("RP_LOOKUP_ABLATE");
         return CompactView{cent.p, cidx.p, M, ccb, cob, cfsh, cfsh == 0, a ? (uint32_t)atoi(a) : 0u,
                            (uint32_t)(3ull * ((uint64_t)M + kEnt3Pad + 6) + 16), (uint32_t)(8ull << (ccb - 3)),
-                           getenv("RP_LOOKUP_WPRED") && !strcmp(getenv("RP_LOOKUP_WPRED"), "0") ? 0u : 1u};
+                           getenv("RP_LOOKUP_WPRED") && !strcmp(getenv("RP_LOOKUP_WPRED"), "0") ? 0u : 1u,
+                           chint && !(getenv("RP_LOOKUP_HINT") && !strcmp(getenv("RP_LOOKUP_HINT"), "0")) ? cidxh.p
+                                                                                                       : nullptr};
     }
 };
 
@@ -1625,6 +1765,16 @@ static void ring_build_compact(Ring& r) {
                        r.own.p, r.M, cb, ob, fsh, r.cent.p);
     RP_HIP(hipGetLastError());
     if (read_u32(r.scalar.p, r.st) != 0) return;
+    // the hinted index of the lean lookupN(3) (needs bucket bits >= 11: 8 prediction bits below)
+    r.chint = false;
+    if (32 - cb >= 8 && r.M < (1u << 30)) {
+        r.cidxh.reserve(2 * ngroups);
+        RP_HIP(hipMemsetAsync(r.scalar.p, 0, sizeof(uint32_t), r.st));
+        hipLaunchKernelGGL(k_cindex_hint, dim3(grid_for(ngroups, 256)), dim3(256), 0, r.st, r.tok.p, r.tmpk.p, r.M,
+                           cb, (uint32_t)ngroups, r.cidxh.p, r.scalar.p);
+        RP_HIP(hipGetLastError());
+        r.chint = read_u32(r.scalar.p, r.st) == 0;
+    }
     r.compact = true;
     r.ccb = cb;
     r.cob = ob;
@@ -1838,8 +1988,15 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
         const int lh = (lean && (half == 4 || stg2) && kpl == 8 && need == 3 && !fuse)
                            ? (int)env_pos("RP_LOOKUP_LH", stg2 ? 2 : 1) : 1;
         const int stghs = (int)env_pos("RP_LOOKUP_STGHS", 8);
+        // RP_LOOKUP_PF=1: the next tile's keys prefetched at the tail of each tile (A/B)
+        const bool pf = lean && half == 4 && kpl == 8 && need == 3 && !fuse && !stg1 && !stg2 && lh == 1 &&
+                        getenv_flag("RP_LOOKUP_PF");
 #define RP_COMPACT(KPL, NEED)                                                                                  \
     do {                                                                                                        \
+        if (KPL == 8 && NEED == 3 && pf)                                                                        \
+            hipLaunchKernelGGL((k_lookupn_lean<8, 3, 4, false, 0, 1, true>), dim3(g), dim3(kLkThreads), 0, st,  \
+                               keys, ntiles, cv, out, counts, r.slow.p, r.nslow.p, fv, np);                     \
+        else                                                                                                    \
         if (KPL == 8 && NEED == 3 && stg2 && stghs == 8 && lh == 1)                                             \
             hipLaunchKernelGGL((k_lookupn_lean<8, 3, 8, false, 2, 1>), dim3(g), dim3(kLkThreads), 0, st, keys,  \
                                ntiles, cv, out, counts, r.slow.p, r.nslow.p, fv, np);                           \
@@ -2120,6 +2277,10 @@ int rp_ring_create(uint32_t replica_points, int device, rp_ring** out) {
 }
 
 // ---- the lookup service (rp_ring_service; k_lookup_service)
+// While the service wave is resident (up to idle_ms after a request), any hipFree in the process
+// (a device buffer growing or released) synchronizes the device and so waits for the wave to
+// idle out. Every other device path of this ring stops the service first; buffers of
+// other handles in the same process can still wait up to idle_ms (include/ringpop_amd.h).
 static void svc_stop(rp::Ring& r) {
     if (!r.svc || !r.svc_running) return;
     __atomic_store_n(&r.svc->req[4], 1u, __ATOMIC_RELEASE);
@@ -2219,6 +2380,7 @@ int rp_ring_checksum_string(rp_ring* h, char* buf, uint64_t cap, uint64_t* len) 
         rp::Ring& r = R(h);
         uint64_t L = 0;
         const uint32_t nn = r.nt.size();
+        svc_stop(r);
         if (r.has_checksum && nn) {
             uint32_t total = 0;
             RP_HIP(hipMemcpyAsync(&total, r.pos.p + nn, 4, hipMemcpyDeviceToHost, r.st));
@@ -2282,6 +2444,7 @@ int rp_ring_dump(rp_ring* h, uint32_t* tokens, uint32_t* owners, uint32_t cap) {
     return guard([&] {
         rp::Ring& r = R(h);
         const uint32_t n = std::min(cap, r.M);
+        svc_stop(r);
         if (n) {
             if (tokens) RP_HIP(hipMemcpyAsync(tokens, r.tok.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, r.st));
             if (owners) RP_HIP(hipMemcpyAsync(owners, r.own.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, r.st));
@@ -2303,6 +2466,7 @@ int rp_ring_lookupn_dev(rp_ring* h, const uint8_t* d_keys, const uint64_t* d_off
     return guard([&] {
         rp::Ring& r = R(h);
         RP_REQUIRE(n == 0 || (d_keys && d_owners && (stride || d_off)), "lookupn_dev: null buffer");
+        svc_stop(r);
         const uint32_t W = nrep > 1 ? (uint32_t)nrep : 1u;
         rp::launch_lookupn(r, d_keys, d_off, stride, nullptr, n, np_for(r, nrep), W, d_owners, d_counts,
                            rp::as_stream(stream));
@@ -2314,6 +2478,7 @@ int rp_ring_lookup_dev(rp_ring* h, const uint8_t* d_keys, const uint64_t* d_off,
     return guard([&] {
         rp::Ring& r = R(h);
         RP_REQUIRE(n == 0 || (d_keys && d_owners && (stride || d_off)), "lookup_dev: null buffer");
+        svc_stop(r);
         // lookup (:145-154) == a one-step walk, independent of getServerCount
         rp::launch_lookupn(r, d_keys, d_off, stride, nullptr, n, 1, 1, d_owners, nullptr, rp::as_stream(stream));
     });
@@ -2324,6 +2489,7 @@ int rp_ring_lookupn_hashes_dev(rp_ring* h, const uint32_t* d_hashes, uint64_t n,
     return guard([&] {
         rp::Ring& r = R(h);
         RP_REQUIRE(n == 0 || (d_hashes && d_owners), "lookupn_hashes_dev: null buffer");
+        svc_stop(r);
         const uint32_t W = nrep > 1 ? (uint32_t)nrep : 1u;
         rp::launch_lookupn(r, nullptr, nullptr, 0, d_hashes, n, np_for(r, nrep), W, d_owners, d_counts,
                            rp::as_stream(stream));
@@ -2421,6 +2587,7 @@ static void host_lookup(rp::Ring& r, const char* keys, const uint64_t* off, uint
         svc_lookup(r, keys + (stride ? 0 : off[0]), (uint32_t)(stride ? stride : off[1] - off[0]), np, W, owners,
                    counts))
         return;
+    svc_stop(r);
     if (!hashes && host_lookup_small(r, keys, off, stride, n, np, W, owners, counts)) return;
     const uint8_t* dk = nullptr;
     const uint64_t* doff = nullptr;
@@ -2501,6 +2668,7 @@ int rp_ring_group_keys_dev(rp_ring* h, const uint8_t* d_keys, const uint64_t* d_
         rp::Ring& r = R(h);
         RP_REQUIRE(d_dests && d_group_off && d_perm && d_ndest, "group_keys_dev: null output buffer");
         RP_REQUIRE(n == 0 || (d_keys && (stride || d_off)), "group_keys_dev: null key buffer");
+        svc_stop(r);
         rp::group_keys(r, d_keys, d_off, stride, nullptr, n, self_id, d_dests, d_group_off, d_perm, d_ndest,
                        rp::as_stream(stream));
     });
@@ -2510,6 +2678,7 @@ int rp_ring_group_keys_dev(rp_ring* h, const uint8_t* d_keys, const uint64_t* d_
 static void host_group(rp::Ring& r, const char* keys, const uint64_t* off, uint32_t stride, const uint32_t* hashes,
                        uint64_t n, uint32_t self_id, uint32_t* dests, uint32_t* goff, uint32_t* perm, uint32_t* ndest) {
     RP_REQUIRE(dests && goff && perm && ndest, "group_keys: null output buffer");
+    svc_stop(r);
     const uint8_t* dk = nullptr;
     const uint64_t* doff = nullptr;
     const uint32_t* dh = nullptr;

@@ -51,8 +51,10 @@ def _reference(gpu, n, k, nbatch):
 
 @pytest.mark.parametrize("G,mode", [(2, ""), (3, ""), (2, "each")])
 def test_dist_membership_matches_single_gpu(gpu, tmp_path, G, mode):
-    """mode "each": every rank reads .checksum after every batch (the value of a batch another
-    rank hashed) through a 2-entry device history that each read drains."""
+    """mode "each": every rank reads latest_checksum() after every batch (the value of a batch
+    another rank hashed) through a 2-entry device history that each read drains; only the entries
+    since the previous read are gathered. The .checksum property refuses on G > 1 ranks (a read on
+    one rank alone would hang a collective)."""
     n, k, nbatch = 6000, 5000, 7
     out = str(tmp_path / "merge.npz")
     port = _free_port()

@@ -139,6 +139,11 @@ LAYOUTS = {
     "stg2-hs4": {"RP_LOOKUP_STG": "2", "RP_LOOKUP_STGHS": "4"},
     # window 1 at the bucket start (the round-2 placement) instead of the predicted start
     "wpred0": {"RP_LOOKUP_WPRED": "0"},
+    # the next tile's keys loaded at the tail of each tile (round 5, measured slower; A/B only)
+    "pf": {"RP_LOOKUP_PF": "1"},
+    "pf-grid3": {"RP_LOOKUP_PF": "1", "RP_LOOKUP_GRID": "3"},
+    # lookupN(3) without the hinted index (the round-4 index and window start)
+    "hint0": {"RP_LOOKUP_HINT": "0"},
     "lean-kpl4": {"RP_LOOKUP_HALF": "0", "RP_LOOKUP_KPL": "4"},
     "round1": {"RP_LOOKUP_LEAN": "0"},
     "round1-kpl1": {"RP_LOOKUP_LEAN": "0", "RP_LOOKUP_KPL": "1"},
@@ -151,7 +156,7 @@ LAYOUTS = {
 def set_layout(monkeypatch, layout):
     for k in ("RP_RING_WIDE", "RP_RING_NOWINDOW", "RP_RING_LAYOUT", "RP_LOOKUP_KPL", "RP_LOOKUP_LEAN", "RP_LOOKUP_HALF",
               "RP_LOOKUP_GRID", "RP_LOOKUP_FUSEFIX", "RP_LOOKUP_WPRED", "RP_LOOKUP_STG", "RP_LOOKUP_LH",
-              "RP_LOOKUP_STGHS"):
+              "RP_LOOKUP_STGHS", "RP_LOOKUP_PF", "RP_LOOKUP_HINT"):
         monkeypatch.delenv(k, raising=False)
     for k, v in LAYOUTS[layout].items():
         monkeypatch.setenv(k, v)
@@ -244,6 +249,32 @@ def test_lookup_service_vs_oracle(gpu, orc):
     check_all(ring, oracle)
 
 
+def test_lookup_service_then_growing_batch(gpu, orc):
+    """A batch lookup after service lookups does not wait for the service wave to idle out
+    (ADVICE r4): with idle_ms = 3000, single-key lookups leave the wave resident; a batch larger
+    than any before (its staging buffers grow: hipFree synchronizes the device) must return well
+    under idle_ms, because every non-service ring path stops the service first. Results against
+    the oracle."""
+    import time
+    ring, oracle = _random_history(orc, gpu, 8, 50, 100, 3)
+    ring.service(3000)
+    rng = random.Random(5)
+    keys = ["k%d-%s" % (i, rng.random()) for i in range(40)]
+    for k in keys[:8]:
+        assert [ring.name(x) for x in ring.lookup_ids([k])] == [oracle.name(oracle.lookup_hash(orc.hash32(k)))]
+    big = ["b%d" % i for i in range(200000)]
+    t0 = time.perf_counter()
+    g, gc = ring.lookupn_ids(big, 3)
+    dt = time.perf_counter() - t0
+    assert dt < 1.5, dt
+    hs = [orc.hash32(k) for k in big[:2000]]
+    for row, c, h in zip(g[:2000], gc[:2000], hs):
+        assert [ring.name(x) for x in row[:c]] == [oracle.name(x) for x in oracle.lookupn_hash(h, 3)]
+    # the service comes back for the next single call
+    assert [ring.name(x) for x in ring.lookup_ids([keys[9]])] == [oracle.name(oracle.lookup_hash(orc.hash32(keys[9])))]
+    ring.service(0)
+
+
 def test_device_farmhash_and_keygen(gpu, orc):
     rng = random.Random(2)
     strs = [bytes(rng.randrange(256) for _ in range(n)) for n in list(range(0, 80)) * 3 + [500, 4096]]
@@ -305,7 +336,7 @@ def _c2_oracle_owners(orc, oracle, n):
     return _C2_OWNERS[n]
 
 
-@pytest.mark.parametrize("layout", ["compact", "round1", "lean-kpl4", "half-kpl8", "fusefix", "wpred0", "stg2", "stg1"])
+@pytest.mark.parametrize("layout", ["compact", "round1", "lean-kpl4", "half-kpl8", "fusefix", "wpred0", "stg2", "stg1", "pf", "hint0"])
 def test_c2_full_size_properties(gpu, orc, layout, monkeypatch):
     set_layout(monkeypatch, layout)
     # C2: 10k servers x 100 points (~1M tokens); 2^24 keys on device; size-independent

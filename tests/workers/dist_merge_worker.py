@@ -5,7 +5,7 @@ per-batch checksums and its final table to OUT (npz).
 
     RANK=r WORLD_SIZE=g MASTER_ADDR=127.0.0.1 MASTER_PORT=p python dist_merge_worker.py n k nbatch out backend [each]
 
-With `each`, every rank reads `m.checksum` after every batch (a collective on a DistMembership)
+With `each`, every rank reads `m.latest_checksum()` after every batch (a collective)
 with a 2-entry device history, so the record is drained by every read; rank 0 also writes those
 per-batch reads.
 """
@@ -68,8 +68,14 @@ def main():
         m.update_dev(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), len(ids), 1434500000000 + b,
                      stream=stream.cuda_stream)
         if each:
-            reads.append(m.checksum)
+            reads.append(m.latest_checksum())
     torch.cuda.synchronize()
+    try:
+        m.checksum
+        raise AssertionError("DistMembership.checksum must refuse on G > 1 ranks")
+    except rpa.RingpopAmdError:
+        pass
+    assert m.local_checksum() is not None
     cks = m.checksums()
     ex, st, inc = m.dump()
     if dist.get_rank() == 0:
