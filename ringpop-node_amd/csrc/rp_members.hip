@@ -10,6 +10,7 @@
 // and hashed by the long-chain farmhash kernel; every step is gated on "anything applied" read
 // from device memory, so a batch never syncs with the host.
 #include <algorithm>
+#include <cstring>
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -595,6 +596,10 @@ __device__ __forceinline__ void bk_local(const FoldArgs& A, uint32_t j) {
 // so the rows move as whole lines: a single change folds at once, repeated changes go to the
 // sorted LDS list (one lane per address, in batch order), more than kSlots + 1 changes (or a
 // list that would overflow) to the overflow fold.
+// DIRECT (round 5): each change's applied flag is stored straight to applied[batch index] (a
+// scattered byte; the batch index is in the record, fjs / the repeated list) and k_bk_gather with
+// its 2-bit map does not run. A/B: RP_BK_DIRECT=0 keeps the map and the gather.
+template <bool DIRECT>
 __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs, const uint32_t* __restrict__ seg,
                                                   uint32_t ntiles, uint32_t nb, FoldArgs A,
                                                   uint32_t* __restrict__ res2, uint8_t* __restrict__ resj,
@@ -678,6 +683,7 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
             int64_t in = (int64_t)(((uint64_t)wv4[u].y << 32) | wv4[u].x);
             r = bk_step(A, id, ex, st, in, (uint8_t)(fjs[q] >> 30), finc[q]);
             row_store(A.rows + id, in, st, 1);
+            if (DIRECT && A.applied) A.applied[fjs[q] & 0x3FFFFFFFu] = r & 3u;
             if (r & kResLocal) bk_local(A, fjs[q] & 0x3FFFFFFFu);
             napp += (r & 3u) ? 1u : 0u;
         } else if (c > 1) {
@@ -690,7 +696,7 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
         rcode[q] = r == kResRep ? (uint8_t)kRes2Rep : (uint8_t)(r & 3u);
     }
     __syncthreads();
-    if (tid < kBk / 16) {  // 16 codes to a word: the gather's map is 1 MB at 2^22 ids, not 4 MB
+    if (!DIRECT && tid < kBk / 16) {  // 16 codes to a word: the gather's map is 1 MB at 2^22 ids, not 4 MB
         const uint4 c4 = reinterpret_cast<const uint4*>(rcode)[tid];
         const uint32_t c[4] = {c4.x, c4.y, c4.z, c4.w};
         uint32_t w = 0;
@@ -722,7 +728,8 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
                 const uint64_t key = dk[e];
                 const uint32_t j = (uint32_t)(key >> 10) & 0x3FFFFFFFu, x = (uint32_t)key & (kBkDup - 1);
                 const uint8_t r = bk_step(A, id, ex, st, in, dst[x] & 3u, dinc[x]);
-                resj[j] = r;
+                if (!DIRECT) resj[j] = r;
+                else if (A.applied) A.applied[j] = r & 3u;
                 if (r & kResLocal) bk_local(A, j);
                 napp += (r & 3u) ? 1u : 0u;
             }
@@ -1289,9 +1296,14 @@ struct Members {
             g_part.reserve(nb + 1);
             hipLaunchKernelGGL(k_bk_scatter, dim3(ntiles), dim3(kBkST), 0, s, ids, chs, chi, k, nb, ntiles, bk_recs.p,
                                bk_seg.p, nst, ninc);
-            hipLaunchKernelGGL(k_bk_fold, dim3((nb + 7) / 8 * 8), dim3(kBkFT), 0, s, bk_recs.p, bk_seg.p, ntiles, nb, A,
-                               bk_res2.p, bk_resj.p, ovf, g_part.p);
-            if (applied) {
+            const bool direct = !(getenv("RP_BK_DIRECT") && !strcmp(getenv("RP_BK_DIRECT"), "0"));
+            if (direct)
+                hipLaunchKernelGGL(k_bk_fold<true>, dim3((nb + 7) / 8 * 8), dim3(kBkFT), 0, s, bk_recs.p, bk_seg.p,
+                                   ntiles, nb, A, bk_res2.p, bk_resj.p, ovf, g_part.p);
+            else
+                hipLaunchKernelGGL(k_bk_fold<false>, dim3((nb + 7) / 8 * 8), dim3(kBkFT), 0, s, bk_recs.p, bk_seg.p,
+                                   ntiles, nb, A, bk_res2.p, bk_resj.p, ovf, g_part.p);
+            if (applied && !direct) {
                 const bool v4 = ((uintptr_t)ids & 15) == 0 && ((uintptr_t)applied & 3) == 0;
                 if (v4)
                     hipLaunchKernelGGL(k_bk_gather<4>, dim3(grid_for((k + 3) / 4, 256, 1u << 30)), dim3(256), 0, s,

@@ -1310,6 +1310,8 @@ struct SvcLines {
     uint32_t req[16 * (1 + kSvcChunks)];  // header line + key lines
     uint32_t resp[16];                    // owners[0..W), count at [15]
     uint32_t resp_seq[16];                // [0] = the answered seq
+    uint64_t resp2[8];                    // k_lookup_service3: owner q | seq << 32 (one 64-B line)
+    uint32_t diag[16];                    // k_lookup_service3 with prof: seq, then phase ticks (100 MHz)
 };
 // With the compact layout built, a key with 1..4 owners wanted takes compact_fix_walk (the
 // index record, the bucket's tokens, the next 8 owners: three dependent trips) instead of the
@@ -1382,6 +1384,147 @@ __global__ __launch_bounds__(64) void k_lookup_service(SvcLines* io, View rv, Co
         last = seq;
         t_idle = __builtin_amdgcn_s_memrealtime();
     }
+}
+
+// One key on the compact layout in two dependent trips (the index record, one 5-entry window at
+// the predicted start, as k_lookupn_lean): true with the first `need` distinct owners when window 1
+// holds them; false when the key needs more (a fingerprint tie, a long bucket, the ring end, a
+// position or repeated owners past the window), and the caller takes the exact walk.
+__device__ __forceinline__ bool svc_compact_window(const CompactView& cv, uint32_t h, int need, uint32_t (&res)[4],
+                                                   int& cnt) {
+    const uint32_t bsh = 32u - cv.cb;
+    const uint32_t g = h >> (bsh + 3u), s4 = ((h >> bsh) & 7u) * 4u;
+    const u32x2 rec = *reinterpret_cast<const u32x2*>(cv.idx + 2ull * g);
+    const uint32_t below = rec.y & ((1u << s4) - 1u);
+    const uint32_t x = (below & 0x0F0F0F0Fu) + ((below >> 4) & 0x0F0F0F0Fu);
+    const uint32_t lo = rec.x + ((x * 0x01010101u) >> 24);
+    const uint32_t bc = (rec.y >> s4) & 15u;
+    if (bc > 10u || lo + 20u > cv.M) return false;
+    const uint32_t fl = (((h << cv.cb) >> 24) * bc) >> 8;
+    const uint32_t w = (need >= 2 && fl > 1u) ? fl - 1u : 0u;
+    const u32x4_a1 v = *reinterpret_cast<const u32x4_a1*>(cv.ent + 3ull * (lo + w));
+    const uint32_t e[5] = {v.x & 0xFFFFFFu, (v.x >> 24) | ((v.y & 0xFFFFu) << 8), (v.y >> 16) | ((v.z & 0xFFu) << 16),
+                           v.z >> 8, v.w & 0xFFFFFFu};
+    const uint32_t omask = (1u << cv.ob) - 1u, obit = 1u << cv.ob;
+    const uint32_t K = ((h & ((1u << bsh) - 1u)) >> cv.fsh) << cv.ob;
+    uint32_t lt = 0;
+    bool tie = false;
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        const bool inb = (uint32_t)j + w < bc;
+        lt += (inb && e[j] < K);
+        tie |= (inb && e[j] - K < obit);
+    }
+    if ((tie && !cv.exact) || (w > 0u && lt == 0u)) return false;
+    const uint32_t rc = dedupe5(e, lt, omask, (uint32_t)need, res);
+    if (rc < (uint32_t)need) return false;
+    cnt = (int)rc;
+    return true;
+}
+
+// The lookup service, round 5 form (RP_RING_SVC=2, the default). Round 5 measured the round-4
+// kernel's call (5.0 us in node) with device stamps (RP_SVC_PROF): the poll's PCIe round trip
+// ~1.1 us, the key's farmhash on one lane from LDS ~0.5 us, three dependent table trips, the
+// answer's line and its seq line. A three-wave form (a poller with 8 reads in flight, a worker,
+// an L2-warming wave) was slower (6.0 us): the poller's PCIe reads in flight delayed the worker's
+// table loads on the same CU (lookup 1.4 us at 1 read in flight, 2.8 at 8) and the LDS hand-off
+// cost 0.4 us. So this form is one wave again, and:
+//   - the host hashes the key (farmhash32, as the reference's lookup does on the CPU) and sends
+//     {seq, hash, np, W, stop, ..., seq} in one 64-B header line: no key lines, no device hash,
+//     and no key-length limit;
+//   - one poll in flight, and nothing else outstanding when a request is seen;
+//   - the compact layout answers in two trips (svc_compact_window: the index record and one
+//     window), the exact walk otherwise;
+//   - the answer is one 64-B line of 8 words {owner | seq << 32} (no fence, no second line: the
+//     host takes the line when every word carries its seq);
+//   - while idle, after each poll is issued, the wave touches 32 KB of the compact tables (8
+//     loads of one 64-B line a lane, done within the poll's round trip; the whole 3.5 MB about
+//     every 0.15 ms), so its XCD's L2 keeps them warm.
+// RP_SVC_PROF=1 writes per-call device phase ticks into diag (poll round trip, lookup).
+template <class View>
+__global__ __launch_bounds__(64) void k_lookup_service3(SvcLines* io, View rv, CompactFixView fv, CompactView cv,
+                                                       uint32_t use_compact, uint32_t last, uint64_t idle_ticks,
+                                                       uint64_t max_ticks, uint32_t warm, uint32_t prof) {
+    const uint32_t lane = threadIdx.x;
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    uint64_t t_idle = t_start;
+    const uint64_t nidx = cv.idx_bytes, nwarm = nidx + cv.ent_bytes;
+    uint64_t woff = 0;
+    uint32_t acc = 0;
+    while (true) {
+        const uint64_t tp = __builtin_amdgcn_s_memrealtime();
+        const uint32_t v = lane < 16 ? __hip_atomic_load(&io->req[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
+        if (warm && use_compact) {  // issued after the poll, done within its round trip
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint64_t o = woff + 64ull * lane;
+                const uint32_t x = o < nidx ? cv.idx[o >> 2]
+                                   : o + 4 <= nwarm ? *reinterpret_cast<const uint32_t*>(cv.ent + ((o - nidx) & ~3ull))
+                                                    : 0u;
+                acc ^= x;
+                woff = woff + 4096 >= nwarm ? 0 : woff + 4096;
+            }
+        }
+        const uint32_t seq = __builtin_amdgcn_readfirstlane(__shfl(v, 0, 64));
+        const uint32_t stop = __builtin_amdgcn_readfirstlane(__shfl(v, 4, 64));
+        const uint32_t tail = __builtin_amdgcn_readfirstlane(__shfl(v, 15, 64));
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (stop || now - t_start > max_ticks) break;
+        if (seq == last || tail != seq) {
+            if (seq == last && now - t_idle > idle_ticks) break;
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the warm load, before the lookup's own
+        asm volatile("" ::"v"(acc));
+        const uint32_t hk = __builtin_amdgcn_readfirstlane(__shfl(v, 1, 64));
+        const int np = (int)__builtin_amdgcn_readfirstlane(__shfl(v, 2, 64));
+        const uint32_t W = __builtin_amdgcn_readfirstlane(__shfl(v, 3, 64));
+        uint32_t res[8] = {NIL, NIL, NIL, NIL, NIL, NIL, NIL, NIL};
+        uint32_t path = 0;
+        if (lane == 0) {
+            bool ok = false;
+            if (use_compact && np >= 1 && np <= 4) {
+                uint32_t r4[4] = {NIL, NIL, NIL, NIL};
+                int c = 0;
+                ok = svc_compact_window(cv, hk, np, r4, c);
+                path = ok ? 1u : 2u;
+                if (!ok) {
+                    c = compact_fix_walk(fv, hk, np, r4);
+                    ok = true;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++) res[q] = r4[q];
+            }
+            if (!ok) {
+                ring_walk<8>(rv, rv.find(hk), np > 8 ? 8 : np, res);
+                path = 3;
+            }
+        }
+        uint32_t o = NIL;
+#pragma unroll
+        for (uint32_t q = 0; q < 8; q++) {
+            const uint32_t x = __shfl(res[q], 0, 64);
+            o = lane == q ? x : o;
+        }
+        if (prof) {  // diag: seq, poll round trip, lookup (ticks), path
+            asm volatile("" ::"v"(o));
+            const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+            const uint32_t pth = (uint32_t)__shfl(path, 0, 64);
+            const uint32_t d[4] = {seq, (uint32_t)(now - tp), (uint32_t)(t1 - now), pth};
+            uint32_t dv = 0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) dv = lane == (uint32_t)q ? d[q] : dv;
+            if (lane < 4) __hip_atomic_store(&io->diag[lane], dv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        if (lane < 8)
+            __hip_atomic_store(&io->resp2[lane], (uint64_t)(lane < W ? o : NIL) | ((uint64_t)seq << 32), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        last = seq;
+        t_idle = __builtin_amdgcn_s_memrealtime();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("" ::"v"(acc));
 }
 
 // ---- build kernels ----
@@ -1700,6 +1843,8 @@ struct Ring {
     hipStream_t svc_st = nullptr;
     uint32_t svc_idle_ms = 0, svc_seq = 0;
     bool svc_running = false;
+    bool svc_v2 = true;  // k_lookup_service3 (RP_RING_SVC=1: the round-4 kernel; read at rp_ring_service)
+    uint64_t svc_prof[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // RP_SVC_PROF: tick sums, path counts, calls
     // group keys by owner (handleOrProxyAll)
     DevBuf<uint32_t> grp_own, grp_key, grp_first, grp_dk, grp_dv, grp_rank;
     Scratch ws;
@@ -2282,6 +2427,16 @@ int rp_ring_create(uint32_t replica_points, int device, rp_ring** out) {
 // idle out. Every other device path of this ring stops the service first; buffers of
 // other handles in the same process can still wait up to idle_ms (include/ringpop_amd.h).
 static void svc_stop(rp::Ring& r) {
+    if (r.svc_prof[8] && getenv("RP_SVC_PROF")) {
+        const double n = (double)r.svc_prof[8];
+        fprintf(stderr,
+                "[rp] service: %llu calls; device us per call: poll round trip %.3f, lookup %.3f; "
+                "window %llu, exact walk %llu, wide walk %llu\n",
+                (unsigned long long)r.svc_prof[8], r.svc_prof[0] / n / 100.0, r.svc_prof[1] / n / 100.0,
+                (unsigned long long)r.svc_prof[5],
+                (unsigned long long)r.svc_prof[6], (unsigned long long)r.svc_prof[7]);
+        for (auto& x : r.svc_prof) x = 0;
+    }
     if (!r.svc || !r.svc_running) return;
     __atomic_store_n(&r.svc->req[4], 1u, __ATOMIC_RELEASE);
     RP_HIP(hipStreamSynchronize(r.svc_st));
@@ -2293,8 +2448,13 @@ static void svc_launch(rp::Ring& r, uint32_t last) {
     using namespace rp;
     const uint64_t idle = (uint64_t)r.svc_idle_ms * 100000ull, maxt = 30ull * 100000000ull;  // 100 MHz ticks
     const CompactFixView fv{r.tok.p, r.own.p, r.cidx.p, r.view(), r.M, r.ccb};
-    hipLaunchKernelGGL((k_lookup_service<RingView>), dim3(1), dim3(64), 0, r.svc_st, r.svc_dev, r.view(), fv,
-                       r.compact ? 1u : 0u, last, idle, maxt);
+    if (r.svc_v2) {
+        const uint32_t warm = (uint32_t)env_pos("RP_SVC_WARM", 1) == 1u, prof = getenv("RP_SVC_PROF") ? 1u : 0u;
+        hipLaunchKernelGGL((k_lookup_service3<RingView>), dim3(1), dim3(64), 0, r.svc_st, r.svc_dev, r.view(), fv,
+                           r.cview(), r.compact ? 1u : 0u, last, idle, maxt, warm, prof);
+    } else
+        hipLaunchKernelGGL((k_lookup_service<RingView>), dim3(1), dim3(64), 0, r.svc_st, r.svc_dev, r.view(), fv,
+                           r.compact ? 1u : 0u, last, idle, maxt);
     RP_HIP(hipGetLastError());
     r.svc_running = true;
 }
@@ -2534,11 +2694,14 @@ static bool host_lookup_small(rp::Ring& r, const char* keys, const uint64_t* off
 }
 
 // one key through the service: false when it does not apply (off, long key, wide row)
-static bool svc_lookup(rp::Ring& r, const char* key, uint32_t len, int np, uint32_t W, uint32_t* owners,
-                       uint8_t* counts) {
+// one key (or, with hash non-null, one caller hash) through the service: false when it does not
+// apply (off, a wide row; the round-4 kernel: a long key or a caller hash)
+static bool svc_lookup(rp::Ring& r, const char* key, uint32_t len, const uint32_t* hash, int np, uint32_t W,
+                       uint32_t* owners, uint8_t* counts) {
     using namespace rp;
     const int need = np <= 0 ? 1 : np;
-    if (!r.svc_idle_ms || len > kSvcKeyMax || W > 8 || need > 8 || r.M == 0) return false;
+    if (!r.svc_idle_ms || W > 8 || need > 8 || r.M == 0) return false;
+    if (!r.svc_v2 && (hash || len > kSvcKeyMax)) return false;
     if (!r.svc) {
         RP_HIP(hipHostMalloc(reinterpret_cast<void**>(&r.svc), sizeof(SvcLines), hipHostMallocMapped | hipHostMallocCoherent));
         memset(r.svc, 0, sizeof(SvcLines));
@@ -2548,13 +2711,19 @@ static bool svc_lookup(rp::Ring& r, const char* key, uint32_t len, int np, uint3
     }
     SvcLines* io = r.svc;
     const uint32_t s = r.svc_seq + 1;
-    for (uint32_t c = 0; c * 60 < len; c++) {  // each key line's bytes, then its seq
-        memcpy(&io->req[16 * (c + 1)], key + 60 * c, std::min<uint32_t>(60, len - 60 * c));
-        __atomic_store_n(&io->req[16 * (c + 1) + 15], s, __ATOMIC_RELEASE);
+    if (r.svc_v2) {
+        // the key's hash, on the host as the reference computes it (lib/ring/index.js:145-154)
+        io->req[1] = hash ? *hash : fh::hash32(fh::PtrSrc{reinterpret_cast<const uint8_t*>(key)}, len);
+    } else {
+        for (uint32_t c = 0; c * 60 < len; c++) {  // each key line's bytes, then its seq
+            memcpy(&io->req[16 * (c + 1)], key + 60 * c, std::min<uint32_t>(60, len - 60 * c));
+            __atomic_store_n(&io->req[16 * (c + 1) + 15], s, __ATOMIC_RELEASE);
+        }
+        io->req[1] = len;
     }
-    io->req[1] = len;
     io->req[2] = (uint32_t)np;
     io->req[3] = W;
+    __atomic_store_n(&io->req[15], s, __ATOMIC_RELEASE);  // the header's trailing copy of seq
     __atomic_store_n(&io->req[0], s, __ATOMIC_RELEASE);
     if (!r.svc_running || hipStreamQuery(r.svc_st) == hipSuccess) {
         if (r.svc_running) RP_HIP(hipStreamSynchronize(r.svc_st));
@@ -2562,10 +2731,18 @@ static bool svc_lookup(rp::Ring& r, const char* key, uint32_t len, int np, uint3
     }
     uint64_t spins = 0;
     const auto t0 = std::chrono::steady_clock::now();
-    while (__atomic_load_n(&io->resp_seq[0], __ATOMIC_ACQUIRE) != s) {
+    // v2: the answer line is taken when all 8 of its words carry seq s (no torn line)
+    auto answered = [&]() -> bool {
+        if (!r.svc_v2) return __atomic_load_n(&io->resp_seq[0], __ATOMIC_ACQUIRE) == s;
+        if ((uint32_t)(__atomic_load_n(&io->resp2[7], __ATOMIC_ACQUIRE) >> 32) != s) return false;
+        for (int q = 0; q < 7; q++)
+            if ((uint32_t)(__atomic_load_n(&io->resp2[q], __ATOMIC_ACQUIRE) >> 32) != s) return false;
+        return true;
+    };
+    while (!answered()) {
         __builtin_ia32_pause();
         if ((++spins & 4095) == 0) {
-            if (hipStreamQuery(r.svc_st) == hipSuccess && __atomic_load_n(&io->resp_seq[0], __ATOMIC_ACQUIRE) != s) {
+            if (hipStreamQuery(r.svc_st) == hipSuccess && !answered()) {
                 svc_launch(r, s - 1);  // it exited (idle or lifetime) before taking this request
             }
             if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
@@ -2575,6 +2752,21 @@ static bool svc_lookup(rp::Ring& r, const char* key, uint32_t len, int np, uint3
         }
     }
     r.svc_seq = s;
+    if (r.svc_v2 && getenv("RP_SVC_PROF") && __atomic_load_n(&io->diag[0], __ATOMIC_ACQUIRE) == s) {
+        r.svc_prof[0] += io->diag[1];
+        r.svc_prof[1] += io->diag[2];
+        r.svc_prof[4 + (io->diag[3] & 3)]++;
+        r.svc_prof[8]++;
+    }
+    if (r.svc_v2) {
+        uint32_t c = 0;
+        for (uint32_t q = 0; q < W; q++) {
+            owners[q] = (uint32_t)io->resp2[q];
+            c += (c == q && owners[q] != NIL) ? 1u : 0u;
+        }
+        if (counts) counts[0] = (uint8_t)c;
+        return true;
+    }
     for (uint32_t q = 0; q < W; q++) owners[q] = io->resp[q];
     if (counts) counts[0] = (uint8_t)io->resp[15];
     return true;
@@ -2583,9 +2775,9 @@ static bool svc_lookup(rp::Ring& r, const char* key, uint32_t len, int np, uint3
 static void host_lookup(rp::Ring& r, const char* keys, const uint64_t* off, uint32_t stride, const uint32_t* hashes,
                         uint64_t n, int np, uint32_t W, uint32_t* owners, uint8_t* counts) {
     if (n == 0) return;
-    if (!hashes && n == 1 &&
-        svc_lookup(r, keys + (stride ? 0 : off[0]), (uint32_t)(stride ? stride : off[1] - off[0]), np, W, owners,
-                   counts))
+    if (n == 1 && (hashes ? svc_lookup(r, nullptr, 0, hashes, np, W, owners, counts)
+                          : svc_lookup(r, keys + (stride ? 0 : off[0]), (uint32_t)(stride ? stride : off[1] - off[0]),
+                                       nullptr, np, W, owners, counts)))
         return;
     svc_stop(r);
     if (!hashes && host_lookup_small(r, keys, off, stride, n, np, W, owners, counts)) return;
@@ -2620,6 +2812,7 @@ int rp_ring_service(rp_ring* h, uint32_t idle_ms) {
         rp::Ring& r = R(h);
         svc_stop(r);
         r.svc_idle_ms = idle_ms;
+        r.svc_v2 = !(getenv("RP_RING_SVC") && !strcmp(getenv("RP_RING_SVC"), "1"));
     });
 }
 

@@ -298,14 +298,18 @@ def test_hot_addresses_take_the_overflow_fold(gpu, orc, sorted_fold, monkeypatch
     assert m.generate_checksum_string() == o.checksum_string()
 
 
-def test_bucket_fold_repeats_overflow_and_large_batch(gpu, orc, monkeypatch):
+@pytest.mark.parametrize("applied_by", ["fold", "gather"])
+def test_bucket_fold_repeats_overflow_and_large_batch(gpu, orc, monkeypatch, applied_by):
     """The bucket fold (batches of 2^19+ changes by default) against the oracle: a 2^20-change
     batch over 2^20 members (256 buckets of 4,096 ids; its applied flags, the status and
     incarnation of every change as rewritten by the local override, and the checksum), and a
     batch whose first four buckets hold 6,000 addresses with two changes each (12,000 repeated
     changes: more than a bucket's LDS list of 512, so the buckets' repeated addresses take the
     overflow fold); the local member's repeated suspect / faulty changes take the local
-    override."""
+    override. applied_by "gather": the round-4 2-bit map and k_bk_gather (RP_BK_DIRECT=0) instead of
+    the fold's direct stores."""
+    if applied_by == "gather":
+        monkeypatch.setenv("RP_BK_DIRECT", "0")
     S = synth()
     n = 1 << 20
     names, st0, inc0 = S.c3_members(n)

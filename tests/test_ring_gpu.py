@@ -218,7 +218,8 @@ def test_small_host_batches_vs_oracle(gpu, orc, nkeys, monkeypatch):
     assert np.array_equal(g0, g1) and np.array_equal(c0, c1)
 
 
-def test_lookup_service_vs_oracle(gpu, orc):
+@pytest.mark.parametrize("svc", ["2", "1"], ids=["three-wave", "round4"])
+def test_lookup_service_vs_oracle(gpu, orc, svc, monkeypatch):
     """The resident lookup service (rp_ring_service): one-key lookup / lookupN calls through
     pinned host lines, against the oracle, for key lengths 0..180 (1-3 key lines; longer keys
     and n > 8 take the small path), across a ring mutation (which stops the service and rebuilds
@@ -229,6 +230,7 @@ def test_lookup_service_vs_oracle(gpu, orc):
     keys = ["".join(rng.choice("abcdef0123456789:-./") for _ in range(L)) for L in
             list(range(0, 70)) + [119, 120, 121, 179, 180, 181, 300]]
     hs = [orc.hash32(k) for k in keys]
+    monkeypatch.setenv("RP_RING_SVC", svc)  # read by ring.service()
     ring.service(50)
 
     def check_all(r, o):
@@ -247,6 +249,36 @@ def test_lookup_service_vs_oracle(gpu, orc):
     check_all(ring, oracle)
     ring.service(0)
     check_all(ring, oracle)
+
+
+def test_lookup_service_c2_vs_oracle(gpu, orc):
+    """The three-wave service on the C2 ring (10k servers x 100 points, the compact layout): 3,000
+    single-key lookup and lookupN(1..4) calls with 36-byte UUID keys against the oracle; most
+    take the two-trip window (svc_compact_window), the rest the exact walk."""
+    servers = c2_servers(orc, 10000)
+    ring = gpu.HashRing()
+    ring.addRemoveServers(servers)
+    oracle = orc.Ring(100)
+    oracle.add_remove(servers)
+    keys = [k.tobytes().decode() for k in orc.uuid_keys(7, 0, 3000)]
+    ring.service(200)
+    for i, k in enumerate(keys):
+        h = orc.hash32(k)
+        n = 1 + i % 4
+        g, gc = ring.lookupn_ids([k], n)
+        assert [ring.name(x) for x in g[0][:gc[0]]] == [oracle.name(x) for x in oracle.lookupn_hash(h, n)], (i, k)
+        if i % 10 == 0:
+            assert [ring.name(x) for x in ring.lookup_ids([k])] == [oracle.name(oracle.lookup_hash(h))]
+        if i % 10 == 5:  # a caller hash (hashFunc) through the service
+            g, gc = ring.lookupn_hashes([h ^ 0x5bd1e995], n)
+            assert [ring.name(x) for x in g[0][:gc[0]]] == \
+                [oracle.name(x) for x in oracle.lookupn_hash(h ^ 0x5bd1e995, n)], (i, k)
+    # keys past the round-4 kernel's 180 bytes go through the service too
+    for L in (181, 500, 4000):
+        k = "x" * L
+        h = orc.hash32(k)
+        assert [ring.name(x) for x in ring.lookup_ids([k])] == [oracle.name(oracle.lookup_hash(h))]
+    ring.service(0)
 
 
 def test_lookup_service_then_growing_batch(gpu, orc):
