@@ -756,12 +756,7 @@ __device__ unsigned long long g_lk_prof[10];
 // registers first (PER x u32x4 held), then the slices go through LDS one after another. 1: the
 // slices are DMA'd global -> LDS (global_load_lds_dwordx4, no VGPR destination) into a ring of
 // two slice buffers, slice s + 2 issued as soon as slice s is hashed (A/B: RP_LOOKUP_STG=1).
-// PF (round 5; STG 0 only): the next tile's key loads are issued at the tail of this tile, after
-// the listed keys' second-window loads and before their results are used, so the key stream's HBM
-// latency runs under the second windows, the barrier and the row stores instead of after them
-// (vmcnt retires in issue order: the second windows are waited for with the key loads still
-// outstanding). A/B: RP_LOOKUP_PF.
-template <int KPL, int NEED, int HS = 1, bool FUSE = false, int STG = 0, int LH = 1, bool PF = false>
+template <int KPL, int NEED, int HS = 1, bool FUSE = false, int STG = 0, int LH = 1>
 __global__ __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_lookupn_lean(const uint8_t* __restrict__ keys, uint64_t ntiles,
                                                              CompactView cv, uint32_t* __restrict__ out,
                                                              uint8_t* __restrict__ counts,
@@ -851,16 +846,6 @@ __global__ __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(4)))
 #ifdef RP_LK_PROF
     uint64_t pa[6] = {0, 0, 0, 0, 0, 0}, ntl = 0;
 #endif
-    static_assert(!PF || (STG == 0 && V4 % kLkThreads == 0), "PF: register staging of whole tiles");
-    u32x4 pre[PF ? PER : 1];
-    auto load_tile = [&](uint64_t tt) {
-        const u32x4* s4 = reinterpret_cast<const u32x4*>(keys + tt * TK * LEN);
-#pragma unroll
-        for (int q = 0; q < PER; q++) pre[q] = __builtin_nontemporal_load(s4 + tid + q * kLkThreads);
-    };
-    if constexpr (PF) {
-        if (blockIdx.x < ntiles) load_tile(blockIdx.x);
-    }
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint64_t base = t * TK;
         uint32_t h[KPL];
@@ -932,25 +917,6 @@ __global__ __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(4)))
                     __builtin_amdgcn_s_barrier();
                     asm volatile("" ::: "memory");
                     dma(hs + 2);
-                }
-            }
-        } else if constexpr (PF) {
-            if (tid == 0) nslow_tile = 0;
-#pragma unroll
-            for (int hs = 0; hs < HS; hs++) {
-                if (hs) __syncthreads();  // the previous slice is hashed
-#pragma unroll
-                for (int q = 0; q < PER; q++) {
-                    const int k = tid + q * kLkThreads;
-                    if (k >= hs * VS && k < (hs + 1) * VS) reinterpret_cast<u32x4*>(sk)[k - hs * VS] = pre[q];
-                }
-                __syncthreads();
-#pragma unroll
-                for (int k = hs * (KPL / HS); k < (hs + 1) * (KPL / HS); k++) {
-                    uint32_t w[W4];
-#pragma unroll
-                    for (int j = 0; j < W4; j++) w[j] = sk[(tid + (k - hs * (KPL / HS)) * kLkThreads) * W4 + j];
-                    h[k] = fh::hash32_words<LEN>(w);
                 }
             }
         } else {
@@ -1103,24 +1069,9 @@ __global__ __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(4)))
         LK_T(t4, nag);
         // second windows, one listed key per lane (the list is this wave's own LDS rows)
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if constexpr (PF) {
-            // AG == 64: one listed key per lane at most. Lanes without one load past the buffer's
-            // range (no memory request, zeros returned), so the load is not under a branch and the
-            // wait for it counts the key loads issued after it.
-            static_assert(AG == 64, "one listed key per lane");
-            const bool has2 = (uint32_t)lane < nag;
-            const u32x4 w2 = __builtin_bit_cast(
-                u32x4, __builtin_amdgcn_raw_buffer_load_b128(ent_r, has2 ? (int)(3u * ag[wv][0][lane]) : 0x7FFFFFF0, 0, 0));
-            const uint64_t tn = t + gridDim.x;
-            load_tile(tn < ntiles ? tn : t);  // the last tile re-loads its own keys (in bounds, unused)
-            if (has2)
-                finish2(w2, ag[wv][1][lane], ag[wv][2][lane], so, counts ? counts + base : nullptr, &nslow_tile,
-                        slow_list + t * kSlowPerTile);
-        } else {
-            for (uint32_t j = lane; j < (nag < AG ? nag : AG); j += 64)
-                finish2(load16(ag[wv][0][j]), ag[wv][1][j], ag[wv][2][j], so, counts ? counts + base : nullptr,
-                        &nslow_tile, slow_list + t * kSlowPerTile);
-        }
+        for (uint32_t j = lane; j < (nag < AG ? nag : AG); j += 64)
+            finish2(load16(ag[wv][0][j]), ag[wv][1][j], ag[wv][2][j], so, counts ? counts + base : nullptr,
+                    &nslow_tile, slow_list + t * kSlowPerTile);
         LK_T(t5a, nag);
         __syncthreads();
         LK_T(t5, tid);
@@ -1437,9 +1388,9 @@ __device__ __forceinline__ bool svc_compact_window(const CompactView& cv, uint32
 //     window), the exact walk otherwise;
 //   - the answer is one 64-B line of 8 words {owner | seq << 32} (no fence, no second line: the
 //     host takes the line when every word carries its seq);
-//   - while idle, after each poll is issued, the wave touches 32 KB of the compact tables (8
-//     loads of one 64-B line a lane, done within the poll's round trip; the whole 3.5 MB about
-//     every 0.15 ms), so its XCD's L2 keeps them warm.
+//   - RP_SVC_WARM=1: while idle, after each poll is issued, the wave touches 32 KB of the compact
+//     tables (the whole 3.5 MB about every 0.15 ms) to keep them in its XCD's L2. Measured without
+//     effect on the lookup's two trips (1.08 us either way, r05g) and 0.1 us slower polls: off.
 // RP_SVC_PROF=1 writes per-call device phase ticks into diag (poll round trip, lookup).
 template <class View>
 __global__ __launch_bounds__(64) void k_lookup_service3(SvcLines* io, View rv, CompactFixView fv, CompactView cv,
@@ -2133,15 +2084,8 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
         const int lh = (lean && (half == 4 || stg2) && kpl == 8 && need == 3 && !fuse)
                            ? (int)env_pos("RP_LOOKUP_LH", stg2 ? 2 : 1) : 1;
         const int stghs = (int)env_pos("RP_LOOKUP_STGHS", 8);
-        // RP_LOOKUP_PF=1: the next tile's keys prefetched at the tail of each tile (A/B)
-        const bool pf = lean && half == 4 && kpl == 8 && need == 3 && !fuse && !stg1 && !stg2 && lh == 1 &&
-                        getenv_flag("RP_LOOKUP_PF");
 #define RP_COMPACT(KPL, NEED)                                                                                  \
     do {                                                                                                        \
-        if (KPL == 8 && NEED == 3 && pf)                                                                        \
-            hipLaunchKernelGGL((k_lookupn_lean<8, 3, 4, false, 0, 1, true>), dim3(g), dim3(kLkThreads), 0, st,  \
-                               keys, ntiles, cv, out, counts, r.slow.p, r.nslow.p, fv, np);                     \
-        else                                                                                                    \
         if (KPL == 8 && NEED == 3 && stg2 && stghs == 8 && lh == 1)                                             \
             hipLaunchKernelGGL((k_lookupn_lean<8, 3, 8, false, 2, 1>), dim3(g), dim3(kLkThreads), 0, st, keys,  \
                                ntiles, cv, out, counts, r.slow.p, r.nslow.p, fv, np);                           \
@@ -2449,7 +2393,7 @@ static void svc_launch(rp::Ring& r, uint32_t last) {
     const uint64_t idle = (uint64_t)r.svc_idle_ms * 100000ull, maxt = 30ull * 100000000ull;  // 100 MHz ticks
     const CompactFixView fv{r.tok.p, r.own.p, r.cidx.p, r.view(), r.M, r.ccb};
     if (r.svc_v2) {
-        const uint32_t warm = (uint32_t)env_pos("RP_SVC_WARM", 1) == 1u, prof = getenv("RP_SVC_PROF") ? 1u : 0u;
+        const uint32_t warm = (uint32_t)env_pos("RP_SVC_WARM", 0) == 1u, prof = getenv("RP_SVC_PROF") ? 1u : 0u;
         hipLaunchKernelGGL((k_lookup_service3<RingView>), dim3(1), dim3(64), 0, r.svc_st, r.svc_dev, r.view(), fv,
                            r.cview(), r.compact ? 1u : 0u, last, idle, maxt, warm, prof);
     } else

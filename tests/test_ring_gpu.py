@@ -139,9 +139,6 @@ LAYOUTS = {
     "stg2-hs4": {"RP_LOOKUP_STG": "2", "RP_LOOKUP_STGHS": "4"},
     # window 1 at the bucket start (the round-2 placement) instead of the predicted start
     "wpred0": {"RP_LOOKUP_WPRED": "0"},
-    # the next tile's keys loaded at the tail of each tile (round 5, measured slower; A/B only)
-    "pf": {"RP_LOOKUP_PF": "1"},
-    "pf-grid3": {"RP_LOOKUP_PF": "1", "RP_LOOKUP_GRID": "3"},
     # lookupN(3) without the hinted index (the round-4 index and window start)
     "hint0": {"RP_LOOKUP_HINT": "0"},
     "lean-kpl4": {"RP_LOOKUP_HALF": "0", "RP_LOOKUP_KPL": "4"},
@@ -156,7 +153,7 @@ LAYOUTS = {
 def set_layout(monkeypatch, layout):
     for k in ("RP_RING_WIDE", "RP_RING_NOWINDOW", "RP_RING_LAYOUT", "RP_LOOKUP_KPL", "RP_LOOKUP_LEAN", "RP_LOOKUP_HALF",
               "RP_LOOKUP_GRID", "RP_LOOKUP_FUSEFIX", "RP_LOOKUP_WPRED", "RP_LOOKUP_STG", "RP_LOOKUP_LH",
-              "RP_LOOKUP_STGHS", "RP_LOOKUP_PF", "RP_LOOKUP_HINT"):
+              "RP_LOOKUP_STGHS", "RP_LOOKUP_HINT"):
         monkeypatch.delenv(k, raising=False)
     for k, v in LAYOUTS[layout].items():
         monkeypatch.setenv(k, v)
@@ -368,7 +365,7 @@ def _c2_oracle_owners(orc, oracle, n):
     return _C2_OWNERS[n]
 
 
-@pytest.mark.parametrize("layout", ["compact", "round1", "lean-kpl4", "half-kpl8", "fusefix", "wpred0", "stg2", "stg1", "pf", "hint0"])
+@pytest.mark.parametrize("layout", ["compact", "round1", "lean-kpl4", "half-kpl8", "fusefix", "wpred0", "stg2", "stg1", "hint0"])
 def test_c2_full_size_properties(gpu, orc, layout, monkeypatch):
     set_layout(monkeypatch, layout)
     # C2: 10k servers x 100 points (~1M tokens); 2^24 keys on device; size-independent

@@ -20,7 +20,7 @@ import bench  # noqa: E402
 
 KNOBS = ("RP_LOOKUP_HALF", "RP_LOOKUP_LEAN", "RP_LOOKUP_KPL", "RP_RING_LAYOUT", "RP_LOOKUP_ABLATE", "RP_RING_WIDE",
          "RP_LOOKUP_GRID", "RP_LOOKUP_STG", "RP_LOOKUP_LH", "RP_LOOKUP_STGHS", "RP_LOOKUP_PF", "RP_LOOKUP_WPRED",
-         "RP_LOOKUP_FUSEFIX", "RP_LOOKUP_HINT")
+         "RP_LOOKUP_FUSEFIX", "RP_LOOKUP_HINT", "RP_LOOKUP_L18")
 
 
 def main():
