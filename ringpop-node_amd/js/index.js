@@ -78,8 +78,8 @@ HashRing.prototype._refreshChecksum = function _refreshChecksum() {
 // The reference's decisions for a batch (index.js:60-94: adds in order, then removes in order,
 // each tested with `!!this.servers[name]`), made before the device is touched: only the names
 // that change go to the device, and the servers map is committed after the device succeeded, so
-// the two never diverge (a name the map already answers for, e.g. 'constructor', is skipped on
-// both sides, as in the reference).
+// the two never diverge (an add of a name the map already answers for, e.g. 'constructor', is
+// skipped, as in the reference; see _applyPlan for removals of such names).
 HashRing.prototype._planServers = function _planServers(add, remove) {
     var servers = this.servers, over = Object.create(null);
     function present(name) { return name in over ? over[name] : !!servers[name]; }
@@ -93,16 +93,24 @@ HashRing.prototype._planServers = function _planServers(add, remove) {
     return plan;
 };
 
+// A removal the reference accepts for a name the servers map only inherits ('constructor',
+// 'toString', ...: `!!this.servers[name]` is true) deletes nothing and removes no token, yet
+// still counts as a change (checksum recomputed, 'removed' emitted, ringChanged true). Such names
+// never reach the device, which holds own names only (tests/golden/ring_ops_golden.json).
 HashRing.prototype._applyPlan = function _applyPlan(plan) {
     var changed = plan.add.length + plan.remove.length > 0;
     if (!changed) { return false; }
-    var deviceChanged = native.ringAddRemove(this._h, plan.add, plan.remove,
-        this._replicaTokens(plan.add), this._replicaTokens(plan.remove));
-    if (!deviceChanged) {
-        throw new Error('ringpop_amd: the device ring did not change for ' + JSON.stringify(plan));
+    var own = Object.prototype.hasOwnProperty, servers = this.servers;
+    var remove = plan.remove.filter(function (n) { return own.call(servers, n); });
+    if (plan.add.length + remove.length > 0) {
+        var deviceChanged = native.ringAddRemove(this._h, plan.add, remove,
+            this._replicaTokens(plan.add), this._replicaTokens(remove));
+        if (!deviceChanged) {
+            throw new Error('ringpop_amd: the device ring did not change for ' + JSON.stringify(plan));
+        }
     }
-    for (var i = 0; i < plan.add.length; i++) { this.servers[plan.add[i]] = true; }
-    for (var j = 0; j < plan.remove.length; j++) { delete this.servers[plan.remove[j]]; }
+    for (var i = 0; i < plan.add.length; i++) { servers[plan.add[i]] = true; }
+    for (var j = 0; j < remove.length; j++) { delete servers[remove[j]]; }
     return true;
 };
 

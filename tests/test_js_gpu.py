@@ -37,6 +37,16 @@ def test_js_hashring_matches_reference_goldens(gpu, tmp_path):
     assert res["checks"] > 400
 
 
+def test_js_hashring_inherited_names_match_reference(gpu, tmp_path):
+    """Single add / remove / addRemoveServers / hasServer calls with names the servers map
+    inherits from Object.prototype ('constructor', 'toString', ...) and ordinary names, against
+    the reference's own results (tests/golden/make_ring_ops.py): a removal of an inherited name
+    reports a change, recomputes the checksum and emits 'removed' without touching the device."""
+    res = run_node("ring_ops_parity.js", {"cases": gu.load("ring_ops_golden.json")["cases"]}, tmp_path)
+    assert res["nfail"] == 0, res["fails"]
+    assert res["checks"] >= 70
+
+
 def test_js_gossipsim_matches_reference_goldens(gpu, tmp_path):
     import importlib.util
     spec = importlib.util.spec_from_file_location("rp_synth", os.path.join(REPO, "ringpop-node_amd", "synth.py"))

@@ -70,3 +70,19 @@ def test_oracle_matches_reference_ring(orc, case_name):
         for n, lists in b["lookupN"].items():
             got = [[names.index(ring.name(x)) for x in ring.lookupn_hash(h, int(n))] for h in hs]
             assert got == lists, "lookupN n=%s" % n
+
+
+def test_ring_ops_golden_inherited_names(orc):
+    """tests/golden/ring_ops_golden.json (reference single calls with names the servers map
+    inherits, e.g. 'constructor'): after every call the ring equals the oracle ring of the listed
+    own servers (checksum, token count); inherited names never own a token."""
+    for case in gu.load("ring_ops_golden.json")["cases"]:
+        R = case["replicaPoints"]
+        for op, r in zip(case["ops"], case["results"]):
+            ring = orc.Ring(R)
+            ring.add_remove(r["servers"], [])
+            assert ring.checksum == r["checksum"], op
+            assert ring.token_count() == r["size"] == R * r["serverCount"], op
+        rets = [r["ret"] for r in case["results"]]
+        assert rets[3] is None and "removed:constructor" in case["results"][3]["events"]
+        assert rets[4] is False and rets[5] is True
