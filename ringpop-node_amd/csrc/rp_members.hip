@@ -455,7 +455,10 @@ __global__ __launch_bounds__(1024) void k_fold_ovf(const uint32_t* __restrict__ 
 #define RP_BK_FT 512
 #endif
 constexpr uint32_t kBkBits = RP_BK_BITS, kBk = 1u << kBkBits;  // ids per bucket (4,096: 64 KB of rows)
-constexpr uint32_t kBkTile = 4096;                             // changes per scatter tile
+#ifndef RP_BK_TILE
+#define RP_BK_TILE 4096
+#endif
+constexpr uint32_t kBkTile = RP_BK_TILE;                       // changes per scatter tile
 constexpr uint32_t kBkST = 1024;                               // threads per scatter tile
 constexpr uint32_t kBkFT = RP_BK_FT;                           // threads per fold workgroup
 constexpr uint32_t kBkDup = kBkFT;                             // repeated-address changes a bucket sorts in LDS
@@ -464,7 +467,8 @@ static_assert(kBk % kBkFT == 0 && kBkFT % 64 == 0, "k_bk_fold: whole ids per lan
 constexpr uint32_t kBkMaxBuckets = 2048;               // (LDS of the scatter tiles): 8M ids
 constexpr uint8_t kResLocal = 4;                       // result: the local override rewrote (status, inc)
 constexpr uint8_t kResRep = 8;                         // repeated changes, results in resj
-static_assert(RP_BK_BITS + 12 <= 30, "bucket-local id + tile-relative index + status in 32 bits");
+static_assert(RP_BK_BITS + (RP_BK_TILE > 4096 ? 13 : 12) <= 30, "bucket-local id + tile-relative index + status in 32 bits");
+static_assert(RP_BK_TILE == 4096 || RP_BK_TILE == 8192, "scatter tiles of 4,096 or 8,192 changes");
 // the per-id result the gather reads, 2 bits (16 ids per word): 0 / 1 / 2 = applied, 3 = repeated
 // changes (the results are in resj)
 constexpr uint32_t kRes2Rep = 3;
@@ -483,19 +487,33 @@ struct BRec {
     uint32_t lo, hi;
 };
 static_assert(sizeof(BRec) == 12, "12-byte records");
-constexpr uint32_t kBkRelBits = 12;
+constexpr uint32_t kBkRelBits = kBkTile > 4096 ? 13 : 12;
 static_assert((1u << kBkRelBits) >= kBkTile, "tile-relative batch index");
 __device__ __forceinline__ uint32_t brec_x(uint32_t il, uint32_t rel, uint32_t st) {
     return il | (rel << kBkBits) | (st << 30);
 }
 
+// Compact records (round 5): a tile whose incarnations span less than 2^32 (ms timestamps of one
+// batch always do) stores 8-B records {x, incarnation - tile base} and its base in tb[tile];
+// otherwise 12-B records and tb[tile] = kBkWide. The fold reads a tile's base beside its segment.
+constexpr int64_t kBkWide = INT64_MIN;
+__device__ __forceinline__ void bk_minmax(int64_t& mn, int64_t& mx) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const int64_t a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
+        mn = a < mn ? a : mn;
+        mx = b > mx ? b : mx;
+    }
+}
+
 __global__ __launch_bounds__(kBkST) void k_bk_scatter(const uint32_t* __restrict__ ids, const uint8_t* __restrict__ chs,
                                                     const int64_t* __restrict__ chi, uint32_t k, uint32_t nb,
                                                     uint32_t ntiles, BRec* __restrict__ recs,
-                                                    uint32_t* __restrict__ seg, uint8_t* __restrict__ nst,
-                                                    int64_t* __restrict__ ninc) {
+                                                    uint32_t* __restrict__ seg, int64_t* __restrict__ tb,
+                                                    uint8_t* __restrict__ nst, int64_t* __restrict__ ninc) {
     __shared__ __attribute__((aligned(16))) uint32_t stage[kBkTile * 3];
     __shared__ uint32_t h[kBkMaxBuckets], s_w[kBkST / 64];
+    __shared__ int64_t s_mn[kBkST / 64], s_mx[kBkST / 64];
     __shared__ uint16_t ls[kBkMaxBuckets];  // <= 4,096 (60 KB in all: two tiles per CU)
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t t = blockIdx.x, base = t * kBkTile;
@@ -513,17 +531,38 @@ __global__ __launch_bounds__(kBkST) void k_bk_scatter(const uint32_t* __restrict
         stv[q] = i < n ? chs[base + i] : (uint8_t)0;
         incv[q] = i < n ? chi[base + i] : 0;
     }
+    // the outputs start as copies; the fold rewrites local overrides. Outputs that alias the
+    // inputs (the reference rewrites its update objects in place) need no copy.
+    const bool cst = nst && nst != chs, cinc = ninc && ninc != chi;
 #pragma unroll
-    for (uint32_t q = 0; q < PER; q++) {  // the outputs start as copies; the fold rewrites local overrides
+    for (uint32_t q = 0; q < PER; q++) {
         const uint32_t i = tid + q * kBkST;
         if (i < n) {
-            if (nst) nst[base + i] = stv[q];
-            if (ninc) ninc[base + i] = incv[q];
+            if (cst) nst[base + i] = stv[q];
+            if (cinc) ninc[base + i] = incv[q];
         }
+    }
+    int64_t mn = INT64_MAX, mx = INT64_MIN;
+#pragma unroll
+    for (uint32_t q = 0; q < PER; q++)
+        if (tid + q * kBkST < n) {
+            mn = incv[q] < mn ? incv[q] : mn;
+            mx = incv[q] > mx ? incv[q] : mx;
+        }
+    bk_minmax(mn, mx);
+    if (lane == 0) {
+        s_mn[wv] = mn;
+        s_mx[wv] = mx;
     }
 #pragma unroll
     for (uint32_t q = 0; q < PER; q++) rk[q] = tid + q * kBkST < n ? atomicAdd(&h[idv[q] >> kBkBits], 1u) : 0u;
     __syncthreads();
+    for (uint32_t w = 0; w < kBkST / 64; w++) {
+        mn = s_mn[w] < mn ? s_mn[w] : mn;
+        mx = s_mx[w] > mx ? s_mx[w] : mx;
+    }
+    const bool c8 = tb != nullptr && mn != kBkWide && (uint64_t)(mx - mn) <= 0xFFFFFFFFull;  // block-uniform
+    if (tid == 0 && tb) tb[t] = c8 ? mn : kBkWide;
     // exclusive scan of h over the buckets (contiguous runs per thread, then across threads)
     const uint32_t per = (nb + kBkST - 1) / kBkST, b0 = min(nb, tid * per), b1 = min(nb, b0 + per);
     uint32_t run = 0;
@@ -544,23 +583,28 @@ __global__ __launch_bounds__(kBkST) void k_bk_scatter(const uint32_t* __restrict
         ex += h[b];
     }
     __syncthreads();
+    const uint32_t rw = c8 ? 2u : 3u;  // record words
 #pragma unroll
     for (uint32_t q = 0; q < PER; q++) {
         const uint32_t i = tid + q * kBkST;
         if (i < n) {
-            const uint32_t b = idv[q] >> kBkBits, e = 3u * (ls[b] + rk[q]);
+            const uint32_t b = idv[q] >> kBkBits, e = rw * (ls[b] + rk[q]);
             const int64_t inc8 = incv[q];
             stage[e] = brec_x(idv[q] & (kBk - 1u), i, stv[q] & 3u);
-            stage[e + 1] = (uint32_t)(uint64_t)inc8;
-            stage[e + 2] = (uint32_t)((uint64_t)inc8 >> 32);
+            if (c8) {
+                stage[e + 1] = (uint32_t)(uint64_t)(inc8 - mn);
+            } else {
+                stage[e + 1] = (uint32_t)(uint64_t)inc8;
+                stage[e + 2] = (uint32_t)((uint64_t)inc8 >> 32);
+            }
         }
     }
     __syncthreads();
-    // the tile's run: n records of 12 B at recs + tile * kBkTile (16-B stores; the tile's run
-    // starts 16-B aligned, and its padded tail is never read)
+    // the tile's run: n records of 8 or 12 B at recs + tile * kBkTile (16-B stores; the tile's
+    // run starts 16-B aligned, and its padded tail is never read)
     uint4* d4 = reinterpret_cast<uint4*>(recs + (uint64_t)t * kBkTile);
     const uint4* s4 = reinterpret_cast<const uint4*>(stage);
-    for (uint32_t q = tid; q < (3u * n + 3u) / 4u; q += kBkST) d4[q] = s4[q];
+    for (uint32_t q = tid; q < (rw * n + 3u) / 4u; q += kBkST) d4[q] = s4[q];
 }
 
 // One change on a member row (the step of fold_address without damp scoring): returns applied
@@ -599,9 +643,21 @@ __device__ __forceinline__ void bk_local(const FoldArgs& A, uint32_t j) {
 // DIRECT (round 5): each change's applied flag is stored straight to applied[batch index] (a
 // scattered byte; the batch index is in the record, fjs / the repeated list) and k_bk_gather with
 // its 2-bit map does not run. A/B: RP_BK_DIRECT=0 keeps the map and the gather.
+// Phase cycle counters of k_bk_fold (diagnostics only: -DRP_BK_PROF; the product build has none):
+// thread 0 of every workgroup stamps s_memtime after each phase's barrier; the sums over the
+// workgroups land in g_bk_prof (printed by the launcher under RP_BK_PROF_PRINT).
+#ifdef RP_BK_PROF
+__device__ unsigned long long g_bk_prof[8];
+#define BK_T(var)   \
+    uint64_t var;   \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var))
+#else
+#define BK_T(var)
+#endif
 template <bool DIRECT>
 __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs, const uint32_t* __restrict__ seg,
-                                                  uint32_t ntiles, uint32_t nb, FoldArgs A,
+                                                  const int64_t* __restrict__ tb, uint32_t ntiles, uint32_t nb,
+                                                  FoldArgs A,
                                                   uint32_t* __restrict__ res2, uint8_t* __restrict__ resj,
                                                   uint32_t* __restrict__ ovf, uint32_t* __restrict__ part) {
     __shared__ uint32_t cnt[kBk], fjs[kBk];
@@ -627,34 +683,49 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
     for (uint32_t q = tid; q < kBk; q += kBkFT) cnt[q] = 0;
     if (tid == 0) s_nd = 0;
     __syncthreads();
+    BK_T(t0);
     // a lane per tile segment, up to 8 records in flight; a change that finds its address
     // already counted goes straight to the repeated list (the first change is added below)
+    auto take = [&](uint32_t x, uint32_t jt, int64_t in) {
+        const uint32_t il = x & (kBk - 1u);
+        const uint32_t js = (jt + ((x >> kBkBits) & (kBkTile - 1u))) | (x & 0xC0000000u);
+        const uint32_t old = atomicAdd(&cnt[il], 1u);
+        if (old == 0) {
+            fjs[il] = js;
+            finc[il] = in;
+        } else {
+            const uint32_t d = atomicAdd(&s_nd, 1u);
+            if (d < kBkDup) dput(d, il, js, in);
+        }
+    };
     for (uint32_t t = tid; t < ntiles; t += kBkFT) {
         const uint32_t e = seg[seg_at(b, t, ntiles)], n = e & 0xFFFFu;
-        const BRec* r = recs + (uint64_t)t * kBkTile + (e >> 16);
+        const int64_t base = tb ? tb[t] : kBkWide;
         const uint32_t jt = t * kBkTile;  // the tile's first batch index
-        for (uint32_t i0 = 0; i0 < n; i0 += 8) {
-            BRec v[8];
+        if (base != kBkWide) {  // 8-B records
+            const uint2* r = reinterpret_cast<const uint2*>(recs + (uint64_t)t * kBkTile) + (e >> 16);
+            for (uint32_t i0 = 0; i0 < n; i0 += 8) {
+                uint2 v[8];
 #pragma unroll
-            for (uint32_t q = 0; q < 8; q++) v[q] = i0 + q < n ? r[i0 + q] : BRec{0, 0, 0};
+                for (uint32_t q = 0; q < 8; q++) v[q] = i0 + q < n ? r[i0 + q] : uint2{0, 0};
 #pragma unroll
-            for (uint32_t q = 0; q < 8; q++)
-                if (i0 + q < n) {
-                    const uint32_t il = v[q].x & (kBk - 1u);
-                    const uint32_t js = (jt + ((v[q].x >> kBkBits) & (kBkTile - 1u))) | (v[q].x & 0xC0000000u);
-                    const int64_t in = (int64_t)(((uint64_t)v[q].hi << 32) | v[q].lo);
-                    const uint32_t old = atomicAdd(&cnt[il], 1u);
-                    if (old == 0) {
-                        fjs[il] = js;
-                        finc[il] = in;
-                    } else {
-                        const uint32_t d = atomicAdd(&s_nd, 1u);
-                        if (d < kBkDup) dput(d, il, js, in);
-                    }
-                }
+                for (uint32_t q = 0; q < 8; q++)
+                    if (i0 + q < n) take(v[q].x, jt, base + (int64_t)v[q].y);
+            }
+        } else {
+            const BRec* r = recs + (uint64_t)t * kBkTile + (e >> 16);
+            for (uint32_t i0 = 0; i0 < n; i0 += 8) {
+                BRec v[8];
+#pragma unroll
+                for (uint32_t q = 0; q < 8; q++) v[q] = i0 + q < n ? r[i0 + q] : BRec{0, 0, 0};
+#pragma unroll
+                for (uint32_t q = 0; q < 8; q++)
+                    if (i0 + q < n) take(v[q].x, jt, (int64_t)(((uint64_t)v[q].hi << 32) | v[q].lo));
+            }
         }
     }
     __syncthreads();
+    BK_T(t1);
     // + the first change of every repeated address
     for (uint32_t q = tid; q < kBk; q += kBkFT)
         if (cnt[q] > 1) {
@@ -662,6 +733,7 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
             if (d < kBkDup) dput(d, q, fjs[q], finc[q]);
         }
     __syncthreads();
+    BK_T(t2);
     const uint32_t nd = s_nd;
     const bool listed = nd <= kBkDup;  // block-uniform
     uint32_t napp = 0;
@@ -696,6 +768,7 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
         rcode[q] = r == kResRep ? (uint8_t)kRes2Rep : (uint8_t)(r & 3u);
     }
     __syncthreads();
+    BK_T(t3);
     if (!DIRECT && tid < kBk / 16) {  // 16 codes to a word: the gather's map is 1 MB at 2^22 ids, not 4 MB
         const uint4 c4 = reinterpret_cast<const uint4*>(rcode)[tid];
         const uint32_t c[4] = {c4.x, c4.y, c4.z, c4.w};
@@ -740,6 +813,16 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
     for (int o = 32; o >= 1; o >>= 1) napp += __shfl_xor(napp, o, 64);
     if ((tid & 63) == 0) s_w[tid >> 6] = napp;
     __syncthreads();
+    BK_T(t4);
+#ifdef RP_BK_PROF
+    if (tid == 0) {
+        atomicAdd(&g_bk_prof[0], (unsigned long long)(t1 - t0));
+        atomicAdd(&g_bk_prof[1], (unsigned long long)(t2 - t1));
+        atomicAdd(&g_bk_prof[2], (unsigned long long)(t3 - t2));
+        atomicAdd(&g_bk_prof[3], (unsigned long long)(t4 - t3));
+        atomicAdd(&g_bk_prof[4], 1ull);
+    }
+#endif
     if (tid == 0) {
         uint32_t t = 0;
         for (int w = 0; w < (int)(kBkFT / 64); w++) t += s_w[w];
@@ -1150,6 +1233,7 @@ struct Members {
     // = 0 | 1 overrides the size rule)
     DevBuf<uint32_t> bk_seg;
     DevBuf<BRec> bk_recs;
+    DevBuf<int64_t> bk_tb;  // per scatter tile: the compact records' incarnation base, or kBkWide
     DevBuf<uint32_t> bk_res2;  // the bucket fold's 2-bit per-id results (k_bk_gather)
     DevBuf<uint8_t> bk_resj;
     static constexpr uint32_t kBkMin = 1u << 19;
@@ -1294,15 +1378,29 @@ struct Members {
             bk_res2.reserve((uint64_t)nb * kBk / 16);
             bk_resj.reserve(k);
             g_part.reserve(nb + 1);
+            bk_tb.reserve(ntiles);
+            const bool rec8 = !(getenv("RP_BK_REC8") && !strcmp(getenv("RP_BK_REC8"), "0"));  // A/B: 0 = 12-B always
             hipLaunchKernelGGL(k_bk_scatter, dim3(ntiles), dim3(kBkST), 0, s, ids, chs, chi, k, nb, ntiles, bk_recs.p,
-                               bk_seg.p, nst, ninc);
+                               bk_seg.p, rec8 ? bk_tb.p : nullptr, nst, ninc);
             const bool direct = !(getenv("RP_BK_DIRECT") && !strcmp(getenv("RP_BK_DIRECT"), "0"));
             if (direct)
                 hipLaunchKernelGGL(k_bk_fold<true>, dim3((nb + 7) / 8 * 8), dim3(kBkFT), 0, s, bk_recs.p, bk_seg.p,
-                                   ntiles, nb, A, bk_res2.p, bk_resj.p, ovf, g_part.p);
+                                   rec8 ? bk_tb.p : nullptr, ntiles, nb, A, bk_res2.p, bk_resj.p, ovf, g_part.p);
             else
                 hipLaunchKernelGGL(k_bk_fold<false>, dim3((nb + 7) / 8 * 8), dim3(kBkFT), 0, s, bk_recs.p, bk_seg.p,
-                                   ntiles, nb, A, bk_res2.p, bk_resj.p, ovf, g_part.p);
+                                   rec8 ? bk_tb.p : nullptr, ntiles, nb, A, bk_res2.p, bk_resj.p, ovf, g_part.p);
+#ifdef RP_BK_PROF
+            if (getenv("RP_BK_PROF_PRINT")) {
+                unsigned long long v[8];
+                RP_HIP(hipStreamSynchronize(s));
+                RP_HIP(hipMemcpyFromSymbol(v, HIP_SYMBOL(g_bk_prof), sizeof v));
+                const double nw = (double)(v[4] ? v[4] : 1);
+                fprintf(stderr, "[rp] k_bk_fold cycles per workgroup (%llu): records %.0f dup-heads %.0f rows+map %.0f dups+count %.0f\n",
+                        v[4], v[0] / nw, v[1] / nw, v[2] / nw, v[3] / nw);
+                memset(v, 0, sizeof v);
+                RP_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_bk_prof), v, sizeof v));
+            }
+#endif
             if (applied && !direct) {
                 const bool v4 = ((uintptr_t)ids & 15) == 0 && ((uintptr_t)applied & 3) == 0;
                 if (v4)

@@ -991,12 +991,13 @@ __global__ __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(4)))
                                                     __builtin_amdgcn_sad_u8((below >> 4) & 0x0F0F0F0Fu, 0u, 0u));
             bc[kq] = (rec[kq].y >> s4) & 15u;
             ws[kq] = wstart(h[k], bc[kq], hint);
-            if (cv.ablate & 10u) {  // diagnostics: 2 = windows rounded down to 16 B (no line crossing);
-                                    // 8 = no window trip (entries made from the record)
+            if (cv.ablate & 26u) {  // diagnostics: 2 = windows rounded down to 16 B (no line crossing);
+                                    // 8 = no window trip (entries made from the record); 16 = windows
+                                    // rounded down to 4 B (dword-aligned, still crossing lines)
                 const uint32_t pos = lo[kq] + ws[kq];
                 win[kq] = (cv.ablate & 8u) ? u32x4{rec[kq].x, rec[kq].y, h[k], pos}
                                            : __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                                          ent_r, (int)((3u * pos) & ~15u), 0, 0));
+                                                                          ent_r, (int)((3u * pos) & ((cv.ablate & 2u) ? ~15u : ~3u)), 0, 0));
             } else {
                 win[kq] = load16(lo[kq] + ws[kq]);
             }

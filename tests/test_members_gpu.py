@@ -338,3 +338,50 @@ def test_bucket_fold_repeats_overflow_and_large_batch(gpu, orc, monkeypatch, app
     assert np.array_equal(ga > 0, oa > 0)
     assert np.array_equal(gs, os_) and np.array_equal(gi, oi)
     assert m.checksum == o.checksum
+
+
+@pytest.mark.parametrize("records", ["auto", "wide"])
+def test_bucket_fold_wide_tiles_and_in_place_outputs(gpu, orc, monkeypatch, records):
+    """The bucket fold's record formats (round 5) and outputs that alias the inputs, against the
+    oracle. A 2^19-change batch over 2^19 members (128 scatter tiles): tiles 1 and 5 hold
+    incarnations spanning more than 2^32 (12-B records there, 8-B records with a tile base
+    elsewhere; records "wide": RP_BK_REC8=0, 12-B records everywhere), and the local member has
+    suspect / faulty changes that the local override rewrites. The status and incarnation
+    outputs are the input arrays themselves, as the reference rewrites its update objects in
+    place (member.js evaluateUpdate): after the call they must hold the oracle's outputs."""
+    import torch
+
+    if records == "wide":
+        monkeypatch.setenv("RP_BK_REC8", "0")
+    S = synth()
+    n = 1 << 19
+    names, st0, inc0 = S.c3_members(n)
+    m = gpu.Membership(whoami=names[0], capacity=n)
+    o = orc.Members(names, local=names[0], join_seed=0)
+    ids0 = np.asarray(m.intern(names), dtype=np.uint32)
+    m.update_ids(ids0, st0, inc0, now_ms=1)
+    o.update_ids(ids0, st0, inc0, False, 1)
+    ids, us, ui = S.c3_updates(n, n, seed=43, base_inc=inc0)
+    rng = np.random.default_rng(5)
+    for t in (1, 5):  # a few far-future and far-past incarnations in two tiles
+        at = t * 4096 + rng.permutation(4096)[:40]
+        ui[at[:20]] += 1 << 33
+        ui[at[20:]] = -(1 << 40) + rng.integers(0, 1000, 20)
+    ids[[77, 4096 * 3 + 5, 4096 * 100 + 9]] = 0  # the local member
+    us[[77, 4096 * 3 + 5, 4096 * 100 + 9]] = [1, 2, 1]
+    ui[[77, 4096 * 3 + 5, 4096 * 100 + 9]] = inc0[0] + np.array([1, 2, 3])
+    now = 1434500000011
+    oa, os_, oi, ona = o.update_ids(ids, us, ui, False, now)
+    d_ids = torch.from_numpy(ids.view(np.int32)).cuda()
+    d_st = torch.from_numpy(us.copy()).cuda()
+    d_inc = torch.from_numpy(ui.copy()).cuda()
+    d_app = torch.empty(n, dtype=torch.uint8, device="cuda")
+    d_na = torch.zeros(1, dtype=torch.int32, device="cuda")
+    m.update_dev(d_ids.data_ptr(), d_st.data_ptr(), d_inc.data_ptr(), n, now, d_app.data_ptr(), d_st.data_ptr(),
+                 d_inc.data_ptr(), d_na.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert int(d_na.item()) == ona
+    assert np.array_equal(d_app.cpu().numpy() > 0, oa > 0)
+    assert np.array_equal(d_st.cpu().numpy(), os_) and np.array_equal(d_inc.cpu().numpy(), oi)
+    assert (oi[[77, 4096 * 3 + 5, 4096 * 100 + 9]] == now).all()  # the override ran
+    assert m.checksum == o.checksum

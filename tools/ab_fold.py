@@ -2,7 +2,10 @@
 members, fresh 2^22-update batches (checksum deferred, as bench.py's fold_large), the variants'
 environment knobs switched batch by batch in rotation, HIP events per batch.
 
-    python tools/ab_fold.py --variants '{"new": {}, "old": {"RP_BK_PRE": "0", "RP_BK_GV": "4"}}' [--rounds 6]
+    python tools/ab_fold.py --variants '{"new": {}, "old": {"RP_BK_REC8": "0"}, "inplace": {"INPLACE": "1"}}' [--rounds 6]
+
+(INPLACE=1: the status / incarnation outputs alias the inputs, as the reference rewrites its
+update objects in place; otherwise separate output arrays.)
 
 Prints per variant the median / min ms per batch and the fraction of 8 TB/s at 49 B per update.
 """
@@ -15,7 +18,7 @@ import sys
 import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KNOBS = ("RP_BK_DIRECT",)
+KNOBS = ("RP_BK_DIRECT", "RP_BK_REC8")
 
 
 def _load(name, path):
@@ -58,15 +61,16 @@ def main():
     na = torch.zeros(1, dtype=torch.int32, device="cuda")
     nb = [0]
 
-    def one():
+    def one(inplace):
         b = nb[0]
         nb[0] += 1
         d = sets[b % nsets]
         inc = d[2] + 3 * nsets * (b // nsets)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
+        os_, oi = (d[1], inc) if inplace else (nst, ninc)  # in place: the outputs are the inputs
         m.update_dev(d[0].data_ptr(), d[1].data_ptr(), inc.data_ptr(), k, 1434500000000 + b, app.data_ptr(),
-                     nst.data_ptr(), ninc.data_ptr(), na.data_ptr(), sp)
+                     os_.data_ptr(), oi.data_ptr(), na.data_ptr(), sp)
         e1.record(stream)
         torch.cuda.synchronize()
         return e0.elapsed_time(e1), int(na.item())
@@ -76,8 +80,8 @@ def main():
         for name, env in variants.items():
             for kn in KNOBS:
                 os.environ.pop(kn, None)
-            os.environ.update(env)
-            ms, napp = one()
+            os.environ.update({x: v for x, v in env.items() if x != "INPLACE"})
+            ms, napp = one(env.get("INPLACE") == "1")
             if r:
                 times[name].append(ms)
         print("round %d done (applied %d)" % (r, napp), flush=True)

@@ -1,6 +1,6 @@
 """A/B timing of C2 lookupN(3) variants in ONE process, interleaved rounds (round 5).
 
-    python tools/ab_lk.py --variants '{"base": {}, "pf": {"RP_LOOKUP_PF": "1"}}' [--rounds 7] [--log2 26]
+    python tools/ab_lk.py --variants '{"base": {}, "al": {"RP_LOOKUP_AL": "1"}}' [--rounds 7] [--log2 26]
 
 Each variant is a set of environment knobs read by the launcher at call time. The C2 ring
 (10k servers x 100 points) and 2^26 device keys are built once. Every variant's output digest is
@@ -19,8 +19,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 
 KNOBS = ("RP_LOOKUP_HALF", "RP_LOOKUP_LEAN", "RP_LOOKUP_KPL", "RP_RING_LAYOUT", "RP_LOOKUP_ABLATE", "RP_RING_WIDE",
-         "RP_LOOKUP_GRID", "RP_LOOKUP_STG", "RP_LOOKUP_LH", "RP_LOOKUP_STGHS", "RP_LOOKUP_PF", "RP_LOOKUP_WPRED",
-         "RP_LOOKUP_FUSEFIX", "RP_LOOKUP_HINT", "RP_LOOKUP_L18")
+         "RP_LOOKUP_GRID", "RP_LOOKUP_STG", "RP_LOOKUP_LH", "RP_LOOKUP_STGHS", "RP_LOOKUP_WPRED",
+         "RP_LOOKUP_FUSEFIX", "RP_LOOKUP_HINT", "RP_LOOKUP_AL")
 
 
 def main():

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="c3,c3ck,big")
     ap.add_argument("--big-log2", type=int, default=22)
+    ap.add_argument("--inplace", action="store_true", help="status / incarnation outputs alias the inputs")
     args = ap.parse_args()
     only = set(args.only.split(","))
     import torch
@@ -67,8 +68,9 @@ def main():
 
         def one(b):
             d = sets[b % nsets]
+            os_, oi = (d[1], incs[b]) if args.inplace else (nst, ninc)
             m.update_dev(d[0].data_ptr(), d[1].data_ptr(), incs[b].data_ptr(), k, 1434500000000 + b, app.data_ptr(),
-                         nst.data_ptr(), ninc.data_ptr(), na.data_ptr(), sp)
+                         os_.data_ptr(), oi.data_ptr(), na.data_ptr(), sp)
             return None
 
         keep = [one(b) for b in range(2)]

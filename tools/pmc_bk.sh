@@ -10,7 +10,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" \
     "TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum"; do
   tag=$(echo $grp | tr ' ' '_' | cut -c1-40)
   timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$OUT/$tag" -o run -- \
-      python3 tools/merge_fold_ab.py --only big --reps 3 > "$OUT/$tag.log" 2>&1
+      python3 tools/merge_fold_ab.py --only big --reps 3 ${PMC_BK_ARGS:-} > "$OUT/$tag.log" 2>&1
   rc=$?
   echo "pmc $grp rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 "$OUT/$tag.log"; exit $rc; fi
