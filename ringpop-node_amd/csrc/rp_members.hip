@@ -461,8 +461,11 @@ constexpr uint32_t kBkBits = RP_BK_BITS, kBk = 1u << kBkBits;  // ids per bucket
 constexpr uint32_t kBkTile = RP_BK_TILE;                       // changes per scatter tile
 constexpr uint32_t kBkST = 1024;                               // threads per scatter tile
 constexpr uint32_t kBkFT = RP_BK_FT;                           // threads per fold workgroup
-constexpr uint32_t kBkDup = kBkFT;                             // repeated-address changes a bucket sorts in LDS
-static_assert(kBkDup <= 1024, "k_bk_fold: one repeated change per thread, 10-bit entry in the key");
+#ifndef RP_BK_DUP
+#define RP_BK_DUP 256
+#endif
+constexpr uint32_t kBkDup = RP_BK_DUP;  // repeated-address changes a bucket sorts in LDS (1 % repeats: ~80)
+static_assert(kBkDup <= kBkFT && kBkDup <= 1024, "k_bk_fold: one repeated change per thread, 10-bit entry in the key");
 static_assert(kBk % kBkFT == 0 && kBkFT % 64 == 0, "k_bk_fold: whole ids per lane");
 constexpr uint32_t kBkMaxBuckets = 2048;               // (LDS of the scatter tiles): 8M ids
 constexpr uint8_t kResLocal = 4;                       // result: the local override rewrote (status, inc)
@@ -497,6 +500,7 @@ __device__ __forceinline__ uint32_t brec_x(uint32_t il, uint32_t rel, uint32_t s
 // batch always do) stores 8-B records {x, incarnation - tile base} and its base in tb[tile];
 // otherwise 12-B records and tb[tile] = kBkWide. The fold reads a tile's base beside its segment.
 constexpr int64_t kBkWide = INT64_MIN;
+constexpr uint32_t kBkNone = 0xFFFFFFFFu, kBkRep = 1u << 29;  // k_bk_fold's fjs: no change / repeated
 __device__ __forceinline__ void bk_minmax(int64_t& mn, int64_t& mx) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
@@ -635,11 +639,11 @@ __device__ __forceinline__ void bk_local(const FoldArgs& A, uint32_t j) {
     if (A.new_inc) A.new_inc[j] = A.now_ms;
 }
 
-// A workgroup per bucket (72.5 KB of LDS: two per CU): per id the change count and the first
-// change, read from the bucket's segments in record order; then the bucket's ids in id order,
-// so the rows move as whole lines: a single change folds at once, repeated changes go to the
-// sorted LDS list (one lane per address, in batch order), more than kSlots + 1 changes (or a
-// list that would overflow) to the overflow fold.
+// A workgroup per bucket (52 KB of LDS since round 5: three per CU): per id the first change
+// (an LDS CAS; a later change flags the id as repeated), read from the bucket's segments in
+// record order; then the bucket's ids in id order, so the rows move as whole lines: a single
+// change folds at once, repeated changes go to the sorted LDS list (one lane per address, in
+// batch order), a bucket whose repeated changes overflow the list to the overflow fold.
 // DIRECT (round 5): each change's applied flag is stored straight to applied[batch index] (a
 // scattered byte; the batch index is in the record, fjs / the repeated list) and k_bk_gather with
 // its 2-bit map does not run. A/B: RP_BK_DIRECT=0 keeps the map and the gather.
@@ -660,8 +664,10 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
                                                   FoldArgs A,
                                                   uint32_t* __restrict__ res2, uint8_t* __restrict__ resj,
                                                   uint32_t* __restrict__ ovf, uint32_t* __restrict__ part) {
-    __shared__ uint32_t cnt[kBk], fjs[kBk];
-    __shared__ uint8_t rcode[kBk];  // the bucket's 2-bit result codes, packed 16 to a word at the end
+    // fjs: per id the first change's {batch index | status << 30} (kBkNone: none; kBkRep set when
+    // the address has repeated changes; a batch index is below 2^29), first by an LDS CAS
+    __shared__ uint32_t fjs[kBk];
+    __shared__ uint8_t rcode[DIRECT ? 16 : kBk];  // (map path) 2-bit result codes, packed 16 to a word
     __shared__ int64_t finc[kBk];
     // repeated changes: key (address << 40 | batch index << 10 | entry), the entry's status and
     // incarnation beside it, so the per-address fold reads only LDS
@@ -680,7 +686,7 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
         dst[d] = (uint8_t)(js >> 30);
         dinc[d] = in;
     };
-    for (uint32_t q = tid; q < kBk; q += kBkFT) cnt[q] = 0;
+    for (uint32_t q = tid; q < kBk; q += kBkFT) fjs[q] = kBkNone;
     if (tid == 0) s_nd = 0;
     __syncthreads();
     BK_T(t0);
@@ -689,11 +695,11 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
     auto take = [&](uint32_t x, uint32_t jt, int64_t in) {
         const uint32_t il = x & (kBk - 1u);
         const uint32_t js = (jt + ((x >> kBkBits) & (kBkTile - 1u))) | (x & 0xC0000000u);
-        const uint32_t old = atomicAdd(&cnt[il], 1u);
-        if (old == 0) {
-            fjs[il] = js;
+        const uint32_t old = atomicCAS(&fjs[il], kBkNone, js);
+        if (old == kBkNone) {
             finc[il] = in;
         } else {
+            if (!(old & kBkRep)) atomicOr(&fjs[il], kBkRep);
             const uint32_t d = atomicAdd(&s_nd, 1u);
             if (d < kBkDup) dput(d, il, js, in);
         }
@@ -727,11 +733,13 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
     __syncthreads();
     BK_T(t1);
     // + the first change of every repeated address
-    for (uint32_t q = tid; q < kBk; q += kBkFT)
-        if (cnt[q] > 1) {
+    for (uint32_t q = tid; q < kBk; q += kBkFT) {
+        const uint32_t v = fjs[q];
+        if (v != kBkNone && (v & kBkRep)) {
             const uint32_t d = atomicAdd(&s_nd, 1u);
-            if (d < kBkDup) dput(d, q, fjs[q], finc[q]);
+            if (d < kBkDup) dput(d, q, v & ~kBkRep, finc[q]);
         }
+    }
     __syncthreads();
     BK_T(t2);
     const uint32_t nd = s_nd;
@@ -741,31 +749,31 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
     uint4 wv4[PI];
 #pragma unroll
     for (uint32_t u = 0; u < PI; u++) {  // each lane's rows in flight together
-        const uint32_t q = tid + u * kBkFT;
-        if (cnt[q] == 1) wv4[u] = *reinterpret_cast<const uint4*>(A.rows + id0 + q);
+        const uint32_t q = tid + u * kBkFT, v = fjs[q];
+        if (v != kBkNone && !(v & kBkRep)) wv4[u] = *reinterpret_cast<const uint4*>(A.rows + id0 + q);
     }
 #pragma unroll
     for (uint32_t u = 0; u < PI; u++) {  // ids in order: coalesced rows and results
         const uint32_t q = tid + u * kBkFT;
-        const uint32_t c = cnt[q], id = id0 + q;
+        const uint32_t v = fjs[q], id = id0 + q;
         uint8_t r = 0;
-        if (c == 1) {
+        if (v != kBkNone && !(v & kBkRep)) {
             bool ex = ((wv4[u].z >> 8) & 0xFFu) != 0;
             uint8_t st = (uint8_t)(wv4[u].z & 0xFFu);
             int64_t in = (int64_t)(((uint64_t)wv4[u].y << 32) | wv4[u].x);
-            r = bk_step(A, id, ex, st, in, (uint8_t)(fjs[q] >> 30), finc[q]);
+            r = bk_step(A, id, ex, st, in, (uint8_t)(v >> 30), finc[q]);
             row_store(A.rows + id, in, st, 1);
-            if (DIRECT && A.applied) A.applied[fjs[q] & 0x3FFFFFFFu] = r & 3u;
-            if (r & kResLocal) bk_local(A, fjs[q] & 0x3FFFFFFFu);
+            if (DIRECT && A.applied) A.applied[v & 0x1FFFFFFFu] = r & 3u;
+            if (r & kResLocal) bk_local(A, v & 0x1FFFFFFFu);
             napp += (r & 3u) ? 1u : 0u;
-        } else if (c > 1) {
+        } else if (v != kBkNone) {
             r = kResRep;
-            if (c > kSlots + 1 || !listed) {  // the overflow fold takes the address
+            if (!listed) {  // the overflow fold takes the address
                 A.rows[id].cnt = kOvfMark;
                 *ovf = 1u;
             }
         }
-        rcode[q] = r == kResRep ? (uint8_t)kRes2Rep : (uint8_t)(r & 3u);
+        if (!DIRECT) rcode[q] = r == kResRep ? (uint8_t)kRes2Rep : (uint8_t)(r & 3u);
     }
     __syncthreads();
     BK_T(t3);
@@ -791,7 +799,6 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
         for (uint32_t q = tid; q < nd; q += kBkFT) {
             const uint32_t il = (uint32_t)(dk[q] >> 40);
             if (q > 0 && (uint32_t)(dk[q - 1] >> 40) == il) continue;  // not a segment head
-            if (cnt[il] > kSlots + 1) continue;                         // the overflow fold's
             const uint32_t id = id0 + il;
             const MRow row = row_load(A.rows + id);
             bool ex = row.exists != 0;
@@ -799,7 +806,7 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
             int64_t in = row.inc;
             for (uint32_t e = q; e < nd && (uint32_t)(dk[e] >> 40) == il; e++) {
                 const uint64_t key = dk[e];
-                const uint32_t j = (uint32_t)(key >> 10) & 0x3FFFFFFFu, x = (uint32_t)key & (kBkDup - 1);
+                const uint32_t j = (uint32_t)(key >> 10) & 0x3FFFFFFFu, x = (uint32_t)key & 1023u;
                 const uint8_t r = bk_step(A, id, ex, st, in, dst[x] & 3u, dinc[x]);
                 if (!DIRECT) resj[j] = r;
                 else if (A.applied) A.applied[j] = r & 3u;
@@ -1262,7 +1269,7 @@ struct Members {
         return true;
     }
     bool use_bucket_fold(uint32_t k, uint32_t nb) const {
-        if (damp_on || nb > kBkMaxBuckets || k >= (1u << 30) || !grouped_fold) return false;
+        if (damp_on || nb > kBkMaxBuckets || k >= (1u << 29) || !grouped_fold) return false;
         const char* e = getenv("RP_MEMBERS_BUCKET_FOLD");
         if (e && *e) return *e != '0';
         return k >= kBkMin;
