@@ -100,8 +100,10 @@ HashRing.prototype._planServers = function _planServers(add, remove) {
 HashRing.prototype._applyPlan = function _applyPlan(plan) {
     var changed = plan.add.length + plan.remove.length > 0;
     if (!changed) { return false; }
-    var own = Object.prototype.hasOwnProperty, servers = this.servers;
-    var remove = plan.remove.filter(function (n) { return own.call(servers, n); });
+    var own = Object.prototype.hasOwnProperty, servers = this.servers, adding = Object.create(null);
+    for (var a = 0; a < plan.add.length; a++) { adding[plan.add[a]] = true; }
+    // a name added earlier in this batch is on the device by the time its removal runs
+    var remove = plan.remove.filter(function (n) { return own.call(servers, n) || n in adding; });
     if (plan.add.length + remove.length > 0) {
         var deviceChanged = native.ringAddRemove(this._h, plan.add, remove,
             this._replicaTokens(plan.add), this._replicaTokens(remove));

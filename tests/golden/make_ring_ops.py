@@ -27,6 +27,8 @@ CASES = [
         ["removeServer", A[5]],
         ["addRemoveServers", ["constructor", A[5]], ["isPrototypeOf"]],
         ["hasServer", "toString"],
+        ["addRemoveServers", ["10.0.0.9:3000"], ["10.0.0.9:3000", "constructor"]],
+        ["addRemoveServers", ["10.0.0.8:3000", "10.0.0.8:3000"], ["toString", "10.0.0.8:3000", A[1]]],
     ]},
 ]
 

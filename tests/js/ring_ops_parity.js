@@ -14,7 +14,7 @@ var checks = 0;
 function eq(what, got, want) {
     checks++;
     if (JSON.stringify(got) !== JSON.stringify(want)) {
-        fails.push({what: what, got: JSON.stringify(got).slice(0, 200), want: JSON.stringify(want).slice(0, 200)});
+        fails.push({what: what, got: String(JSON.stringify(got)).slice(0, 200), want: String(JSON.stringify(want)).slice(0, 200)});
     }
 }
 

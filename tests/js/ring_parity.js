@@ -25,7 +25,7 @@ function makeHash(kind, mod) {  // tests/golden/ref_ring.js makeHash, with the e
 function eq(what, got, want) {
     checks++;
     if (JSON.stringify(got) !== JSON.stringify(want)) {
-        fails.push({what: what, got: JSON.stringify(got).slice(0, 200), want: JSON.stringify(want).slice(0, 200)});
+        fails.push({what: what, got: String(JSON.stringify(got)).slice(0, 200), want: String(JSON.stringify(want)).slice(0, 200)});
     }
 }
 
@@ -36,7 +36,7 @@ input.cases.forEach(function (c) {
     var ring = new amd.HashRing(opts);
     var idx = {};
     c.names.forEach(function (n, i) { idx[n] = i; });
-    function toIdx(x) { return x === null || x === undefined ? -1 : idx[x]; }
+    function toIdx(x) { return x === null || x === undefined ? -1 : (x in idx ? idx[x] : 'unknown:' + x); }
     var events = {checksumComputed: 0};
     ring.on('checksumComputed', function () { events.checksumComputed++; });
     eq(c.name + ' initial checksum', ring.checksum, null);
