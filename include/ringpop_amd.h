@@ -102,9 +102,10 @@ int rp_ring_lookup(rp_ring *r, const char *keys, const uint64_t *off, uint32_t s
 int rp_ring_lookupn(rp_ring *r, const char *keys, const uint64_t *off, uint32_t stride, uint64_t n,
                     int32_t nrep, uint32_t *owners, uint8_t *counts);
 /* Low-latency single calls (RingPop.lookup / lookupN per request, index.js:434-471): with
- * idle_ms > 0, a one-key rp_ring_lookup / rp_ring_lookupn (key <= 180 B, n <= 8) is answered by a
- * resident service wave (one workgroup on one CU) that polls pinned, device-mapped host lines,
- * instead of a kernel launch and a stream sync per call. The wave exits after idle_ms without a
+ * idle_ms > 0, a one-key rp_ring_lookup / rp_ring_lookupn / rp_ring_lookupn_hashes (n <= 8; the
+ * host hashes the key) is answered by a resident service wave (one workgroup on one CU) that
+ * polls a pinned, device-mapped request line and reads one record of its direct table (built at
+ * its first launch after a ring change), instead of a kernel launch and a stream sync per call. The wave exits after idle_ms without a
  * request (and after 30 s in all) and is relaunched by the next call; a ring mutation and every
  * other device call on this ring (batch lookups, grouping, dump) stop it first. While it is
  * resident, a device-buffer release anywhere else in the process (another handle's buffer

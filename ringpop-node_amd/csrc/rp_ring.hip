@@ -1374,6 +1374,100 @@ __device__ __forceinline__ bool svc_compact_window(const CompactView& cv, uint32
     return true;
 }
 
+// The service's direct table (round 5): one 64-B record per bucket of the top B hash bits (2^B >= M,
+// B >= 16, so the bucket fixes all but <= 16 token bits and a record answers exactly, no
+// fingerprints), read as one aligned line: the lookup is one dependent trip instead of the compact
+// layout's two. Record words:
+//   [0]     token count c (<= 7; 15: more, the caller takes the other paths) | successors s << 8 |
+//           complete << 16 (s < 16 only because the ring has fewer distinct owners)
+//   [1..7]  the bucket's tokens in ring order: low 32 - B bits | owner << 16
+//   [8..15] the first 16 distinct owners from the first token after the bucket onwards (cyclic),
+//           two 16-bit ids a word
+// lookupN(h, n <= 8) = the first n distinct of (owners of the bucket's tokens >= h, then the
+// successors): the successors are the distinct owners of the rest of the walk in first-seen order,
+// so deduplicating the concatenation gives the walk's answer (lib/ring/index.js:157-189). Only
+// for rings whose interned ids fit 16 bits. tools/svc_latency.js prices it (r05w).
+constexpr uint32_t kDtEnt = 7, kDtSucc = 16, kDtWalk = 4096;
+__global__ __launch_bounds__(256) void k_dt_build(const uint32_t* __restrict__ tok, const uint32_t* __restrict__ own,
+                                                  uint32_t M, uint32_t B, uint4* __restrict__ dt) {
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >> B) return;
+    const uint32_t sh = 32u - B;
+    auto lower = [&](uint64_t key) {  // first i with tok[i] >= key
+        uint32_t lo = 0, hi = M;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if ((uint64_t)tok[mid] < key) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo;
+    };
+    const uint32_t lo = lower(b << sh), hi = lower((b + 1) << sh);
+    const uint32_t c = hi - lo;
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) w[i] = 0xFFFFFFFFu;
+    if (c > kDtEnt) {
+        w[0] = 15u;
+    } else {
+        for (uint32_t i = 0; i < c; i++) w[1 + i] = (tok[lo + i] & ((1u << sh) - 1u)) | (own[lo + i] << 16);
+        uint32_t su[kDtSucc], ns = 0, k = 0;
+        const uint32_t lim = M < kDtWalk ? M : kDtWalk;
+        for (; k < lim && ns < kDtSucc; k++) {
+            const uint32_t j = hi + k >= M ? hi + k - M : hi + k;
+            const uint32_t o = own[j];
+            bool seen = false;
+            for (uint32_t q = 0; q < ns; q++) seen |= su[q] == o;
+            if (!seen) su[ns++] = o;
+        }
+        const uint32_t complete = (ns < kDtSucc && k == M) ? 1u : 0u;
+        w[0] = c | (ns << 8) | (complete << 16);
+        for (uint32_t q = 0; q < kDtSucc; q += 2)
+            w[8 + q / 2] = (q < ns ? su[q] : 0xFFFFu) | ((q + 1 < ns ? su[q + 1] : 0xFFFFu) << 16);
+    }
+    uint4* d = dt + 4 * b;
+#pragma unroll
+    for (int q = 0; q < 4; q++) d[q] = uint4{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
+}
+
+// The answer from a record, across the wave: lane i < 16 holds record word i (x). Lane i takes
+// item i of (owners of the bucket's tokens >= h, then the successors), flags it when no earlier
+// item has its owner, and the flagged items' ranks are their slots. Returns false (wave-uniform)
+// when the record cannot say (an overflowing bucket, too few successors); else cnt and, in lane
+// q < 8, the q-th owner (NIL past cnt).
+__device__ __forceinline__ bool dt_answer(uint32_t x, uint32_t lane, uint32_t h, uint32_t B, uint32_t need,
+                                          uint32_t* slot, uint32_t& mine, int& cnt) {
+    const uint32_t w0 = __builtin_amdgcn_readfirstlane(x);
+    const uint32_t c = w0 & 15u, ns = (w0 >> 8) & 31u, complete = (w0 >> 16) & 1u;
+    if (c > kDtEnt) return false;
+    const uint32_t rmask = (1u << (32u - B)) - 1u, hr = h & rmask;
+    const uint32_t e = __shfl(x, 1 + (lane < kDtEnt ? lane : 0), 64);
+    const uint32_t f = (uint32_t)__popcll(__ballot(lane < c && (e & 0xFFFFu & rmask) < hr));  // tokens below h
+    const uint32_t na = c - f;
+    const uint32_t ea = __shfl(x, 1 + f + (lane < na ? lane : 0), 64);
+    const uint32_t k = lane - na;
+    const uint32_t sw = __shfl(x, 8 + ((lane >= na && k < kDtSucc ? k : 0) >> 1), 64);
+    const bool valid = lane < na || (lane >= na && k < ns);
+    const uint32_t t = lane < na ? (ea >> 16) : ((sw >> (16 * (k & 1))) & 0xFFFFu);
+    bool dup = false;
+#pragma unroll
+    for (uint32_t j = 0; j < kDtEnt + kDtSucc; j++) {
+        const uint32_t tj = __builtin_amdgcn_readlane(t, j);
+        dup |= j < lane && tj == t;
+    }
+    const uint64_t fb = __ballot(valid && !dup);
+    const uint32_t total = (uint32_t)__popcll(fb);
+    if (total < need && !complete) return false;
+    const uint32_t rank = (uint32_t)__popcll(fb & ((1ull << lane) - 1ull));
+    if (valid && !dup && rank < 8) slot[rank] = t;
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the slots are written (one wave: no barrier)
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t got = total < need ? total : need;
+    mine = lane < got ? slot[lane] : NIL;
+    cnt = (int)got;
+    return true;
+}
+
 // The lookup service, round 5 form (RP_RING_SVC=2, the default). Round 5 measured the round-4
 // kernel's call (5.0 us in node) with device stamps (RP_SVC_PROF): the poll's PCIe round trip
 // ~1.1 us, the key's farmhash on one lane from LDS ~0.5 us, three dependent table trips, the
@@ -1396,7 +1490,9 @@ __device__ __forceinline__ bool svc_compact_window(const CompactView& cv, uint32
 template <class View>
 __global__ __launch_bounds__(64) void k_lookup_service3(SvcLines* io, View rv, CompactFixView fv, CompactView cv,
                                                        uint32_t use_compact, uint32_t last, uint64_t idle_ticks,
-                                                       uint64_t max_ticks, uint32_t warm, uint32_t prof) {
+                                                       uint64_t max_ticks, uint32_t warm, uint32_t prof,
+                                                       const uint32_t* __restrict__ dt, uint32_t dtb) {
+    __shared__ uint32_t dslot[8];
     const uint32_t lane = threadIdx.x;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     uint64_t t_idle = t_start;
@@ -1434,7 +1530,15 @@ __global__ __launch_bounds__(64) void k_lookup_service3(SvcLines* io, View rv, C
         const uint32_t W = __builtin_amdgcn_readfirstlane(__shfl(v, 3, 64));
         uint32_t res[8] = {NIL, NIL, NIL, NIL, NIL, NIL, NIL, NIL};
         uint32_t path = 0;
-        if (lane == 0) {
+        bool dok = false;
+        uint32_t dmine = NIL;
+        if (dt && np >= 1 && np <= 8) {  // the direct table: one 64-B line, lanes 0..15
+            const uint32_t x = lane < 16 ? dt[16ull * (hk >> (32u - dtb)) + lane] : 0u;
+            int c = 0;
+            dok = dt_answer(x, lane, hk, dtb, (uint32_t)np, dslot, dmine, c);
+            path = dok ? 4u : 0u;
+        }
+        if (lane == 0 && !dok) {
             bool ok = false;
             if (use_compact && np >= 1 && np <= 4) {
                 uint32_t r4[4] = {NIL, NIL, NIL, NIL};
@@ -1459,6 +1563,7 @@ __global__ __launch_bounds__(64) void k_lookup_service3(SvcLines* io, View rv, C
             const uint32_t x = __shfl(res[q], 0, 64);
             o = lane == q ? x : o;
         }
+        if (dok) o = dmine;
         if (prof) {  // diag: seq, poll round trip, lookup (ticks), path
             asm volatile("" ::"v"(o));
             const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
@@ -1771,6 +1876,7 @@ struct Ring {
     DevBuf<uint32_t> cidx;
     DevBuf<uint32_t> cidxh;  // the hinted index (k_cindex_hint); valid when chint
     bool chint = false;
+    bool chint_pending = false;  // the compact layout changed and the hinted index is not built yet
     bool compact = false;
     uint32_t ccb = 0, cob = 0, cfsh = 0;
     // checksum string + value
@@ -1796,6 +1902,9 @@ struct Ring {
     uint32_t svc_idle_ms = 0, svc_seq = 0;
     bool svc_running = false;
     bool svc_v2 = true;  // k_lookup_service3 (RP_RING_SVC=1: the round-4 kernel; read at rp_ring_service)
+    DevBuf<uint4> svc_dt;       // the service's direct table (k_dt_build), built at its first launch after a change
+    uint32_t svc_dtb = 0;       // its bucket bits; 0: none (ids past 16 bits, M > 2^22, RP_SVC_DT=0)
+    bool svc_dt_valid = false;  // false after every ring change
     uint64_t svc_prof[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // RP_SVC_PROF: tick sums, path counts, calls
     // group keys by owner (handleOrProxyAll)
     DevBuf<uint32_t> grp_own, grp_key, grp_first, grp_dk, grp_dv, grp_rank;
@@ -1863,22 +1972,33 @@ static void ring_build_compact(Ring& r) {
     RP_HIP(hipGetLastError());
     if (read_u32(r.scalar.p, r.st) != 0) return;
     // the hinted index of the lean lookupN(3) (needs bucket bits >= 11: 8 prediction bits below)
+    // is built by the first batch lookup that reads it (ring_build_hint): ~1 ms at C2, which a
+    // per-call mutation (addServer / removeServer) should not pay
     r.chint = false;
-    if (32 - cb >= 8 && r.M < (1u << 30)) {
-        r.cidxh.reserve(2 * ngroups);
-        RP_HIP(hipMemsetAsync(r.scalar.p, 0, sizeof(uint32_t), r.st));
-        hipLaunchKernelGGL(k_cindex_hint, dim3(grid_for(ngroups, 256)), dim3(256), 0, r.st, r.tok.p, r.tmpk.p, r.M,
-                           cb, (uint32_t)ngroups, r.cidxh.p, r.scalar.p);
-        RP_HIP(hipGetLastError());
-        r.chint = read_u32(r.scalar.p, r.st) == 0;
-    }
+    r.chint_pending = 32 - cb >= 8 && r.M < (1u << 30);
     r.compact = true;
     r.ccb = cb;
     r.cob = ob;
     r.cfsh = fsh;
 }
 
+static void ring_build_hint(Ring& r) {
+    r.chint_pending = false;
+    r.chint = false;
+    const uint32_t cb = r.ccb;
+    const uint64_t nbk = 1ull << cb, ngroups = nbk >> 3;
+    r.tmpk.reserve(nbk + 1);
+    hipLaunchKernelGGL(k_bucket_index, dim3(grid_for(nbk + 1, 256)), dim3(256), 0, r.st, r.tok.p, r.M, cb, r.tmpk.p);
+    r.cidxh.reserve(2 * ngroups);
+    RP_HIP(hipMemsetAsync(r.scalar.p, 0, sizeof(uint32_t), r.st));
+    hipLaunchKernelGGL(k_cindex_hint, dim3(grid_for(ngroups, 256)), dim3(256), 0, r.st, r.tok.p, r.tmpk.p, r.M, cb,
+                       (uint32_t)ngroups, r.cidxh.p, r.scalar.p);
+    RP_HIP(hipGetLastError());
+    r.chint = read_u32(r.scalar.p, r.st) == 0;
+}
+
 static void ring_rebuild_index(Ring& r) {
+    r.svc_dt_valid = false;
     r.bbits = choose_bbits(r.M);
     const uint64_t nbk = (1ull << r.bbits) + 1;
     r.bstart.reserve(nbk);
@@ -2057,6 +2177,7 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(keys) & 15) == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
     if (use_compact && fixed36 && aligned16 && (uint32_t)need == W && W <= 4 && n >= (uint64_t)kLkThreads * 4) {
         RP_REQUIRE(n < (1ull << 32), "lookupn: at most 2^32-1 keys per call");
+        if (r.chint_pending && need == 3) ring_build_hint(r);
         const CompactView cv = r.cview();
         // lookupN(3) (the C2 bench): 8 keys per lane, staged through LDS in four slices (0.925-0.926
         // against 0.962-0.970 ms for 4 keys per lane; two slices 0.926-0.932; 6 keys per lane
@@ -2376,9 +2497,9 @@ static void svc_stop(rp::Ring& r) {
         const double n = (double)r.svc_prof[8];
         fprintf(stderr,
                 "[rp] service: %llu calls; device us per call: poll round trip %.3f, lookup %.3f; "
-                "window %llu, exact walk %llu, wide walk %llu\n",
+                "direct table %llu, window %llu, exact walk %llu, wide walk %llu\n",
                 (unsigned long long)r.svc_prof[8], r.svc_prof[0] / n / 100.0, r.svc_prof[1] / n / 100.0,
-                (unsigned long long)r.svc_prof[5],
+                (unsigned long long)r.svc_prof[4], (unsigned long long)r.svc_prof[5],
                 (unsigned long long)r.svc_prof[6], (unsigned long long)r.svc_prof[7]);
         for (auto& x : r.svc_prof) x = 0;
     }
@@ -2395,8 +2516,23 @@ static void svc_launch(rp::Ring& r, uint32_t last) {
     const CompactFixView fv{r.tok.p, r.own.p, r.cidx.p, r.view(), r.M, r.ccb};
     if (r.svc_v2) {
         const uint32_t warm = (uint32_t)env_pos("RP_SVC_WARM", 0) == 1u, prof = getenv("RP_SVC_PROF") ? 1u : 0u;
+        if (!r.svc_dt_valid) {  // the direct table for this ring (A/B: RP_SVC_DT=0)
+            r.svc_dtb = 0;
+            uint32_t B = 16;
+            while (B < 22 && (1ull << B) < r.M) B++;
+            const bool dt_on = !(getenv("RP_SVC_DT") && !strcmp(getenv("RP_SVC_DT"), "0"));
+            if (dt_on && r.M > 0 && (1ull << B) >= r.M && r.nt.size() < 0xFFFFu) {
+                r.svc_dt.reserve(4ull << B);
+                hipLaunchKernelGGL(k_dt_build, dim3(grid_for(1ull << B, 256, 1u << 20)), dim3(256), 0, r.svc_st, r.tok.p,
+                                   r.own.p, r.M, B, r.svc_dt.p);
+                RP_HIP(hipGetLastError());
+                r.svc_dtb = B;
+            }
+            r.svc_dt_valid = true;
+        }
+        const uint32_t* dt = r.svc_dtb ? reinterpret_cast<const uint32_t*>(r.svc_dt.p) : nullptr;
         hipLaunchKernelGGL((k_lookup_service3<RingView>), dim3(1), dim3(64), 0, r.svc_st, r.svc_dev, r.view(), fv,
-                           r.cview(), r.compact ? 1u : 0u, last, idle, maxt, warm, prof);
+                           r.cview(), r.compact ? 1u : 0u, last, idle, maxt, warm, prof, dt, r.svc_dtb);
     } else
         hipLaunchKernelGGL((k_lookup_service<RingView>), dim3(1), dim3(64), 0, r.svc_st, r.svc_dev, r.view(), fv,
                            r.compact ? 1u : 0u, last, idle, maxt);

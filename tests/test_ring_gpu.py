@@ -215,12 +215,17 @@ def test_small_host_batches_vs_oracle(gpu, orc, nkeys, monkeypatch):
     assert np.array_equal(g0, g1) and np.array_equal(c0, c1)
 
 
-@pytest.mark.parametrize("svc", ["2", "1"], ids=["three-wave", "round4"])
+@pytest.mark.parametrize("svc", ["2", "2-nodt", "1"], ids=["v3", "v3-window", "round4"])
 def test_lookup_service_vs_oracle(gpu, orc, svc, monkeypatch):
     """The resident lookup service (rp_ring_service): one-key lookup / lookupN calls through
     pinned host lines, against the oracle, for key lengths 0..180 (1-3 key lines; longer keys
     and n > 8 take the small path), across a ring mutation (which stops the service and rebuilds
-    the table it reads), an idle exit (the next call relaunches it) and turning it off."""
+    the table it reads), an idle exit (the next call relaunches it) and turning it off. "v3":
+    the host-hashed service with its direct table (few servers: the successor lists are
+    complete); "v3-window": RP_SVC_DT=0, the compact window and walks."""
+    if svc.endswith("-nodt"):
+        monkeypatch.setenv("RP_SVC_DT", "0")
+        svc = svc[:-5]
     import time
     ring, oracle = _random_history(orc, gpu, 8, 50, 100, 3)
     rng = random.Random(77)
@@ -248,10 +253,13 @@ def test_lookup_service_vs_oracle(gpu, orc, svc, monkeypatch):
     check_all(ring, oracle)
 
 
-def test_lookup_service_c2_vs_oracle(gpu, orc):
-    """The three-wave service on the C2 ring (10k servers x 100 points, the compact layout): 3,000
-    single-key lookup and lookupN(1..4) calls with 36-byte UUID keys against the oracle; most
-    take the two-trip window (svc_compact_window), the rest the exact walk."""
+@pytest.mark.parametrize("dt", ["1", "0"], ids=["direct", "window"])
+def test_lookup_service_c2_vs_oracle(gpu, orc, monkeypatch, dt):
+    """The service on the C2 ring (10k servers x 100 points): 3,000 single-key lookup and
+    lookupN(1..8) calls with 36-byte UUID keys against the oracle. "direct": one 64-B record of
+    the direct table per key (k_dt_build; 2^20 buckets); "window": RP_SVC_DT=0, the compact
+    layout's two-trip window (svc_compact_window, n <= 4) and the exact walks."""
+    monkeypatch.setenv("RP_SVC_DT", dt)
     servers = c2_servers(orc, 10000)
     ring = gpu.HashRing()
     ring.addRemoveServers(servers)
@@ -261,7 +269,7 @@ def test_lookup_service_c2_vs_oracle(gpu, orc):
     ring.service(200)
     for i, k in enumerate(keys):
         h = orc.hash32(k)
-        n = 1 + i % 4
+        n = 1 + i % 8
         g, gc = ring.lookupn_ids([k], n)
         assert [ring.name(x) for x in g[0][:gc[0]]] == [oracle.name(x) for x in oracle.lookupn_hash(h, n)], (i, k)
         if i % 10 == 0:
@@ -275,6 +283,32 @@ def test_lookup_service_c2_vs_oracle(gpu, orc):
         k = "x" * L
         h = orc.hash32(k)
         assert [ring.name(x) for x in ring.lookup_ids([k])] == [oracle.name(oracle.lookup_hash(h))]
+    ring.service(0)
+
+
+def test_lookup_service_direct_table_collisions(gpu, orc):
+    """The direct table where it cannot answer alone: a caller hashFunc with few distinct values
+    (hash32 % 257: about half the buckets hold more than 7 equal tokens and overflow their record,
+    the others answer from it; equal tokens keep the ring's order), 40 servers x 50 points; lookupN(1..8) and lookup of 600 keys
+    through the service against the oracle with the same tokens (the record, or the fallback
+    paths when it overflows)."""
+    servers = ["dt-%d:3000" % i for i in range(40)]
+    R = 50
+
+    def hf(s):
+        return orc.hash32(s) % 257 * 16711433 & 0xFFFFFFFF
+
+    ring = gpu.HashRing({"replicaPoints": R, "hashFunc": hf})
+    ring.addRemoveServers(servers)
+    oracle = orc.Ring(R)
+    oracle.add_remove(servers, [], [hf(s + str(i)) for s in servers for i in range(R)], None)
+    ring.service(200)
+    rng = random.Random(11)
+    for i in range(600):
+        h = rng.getrandbits(32) if i % 3 else hf("key-%d" % i)
+        n = 1 + i % 8
+        g, gc = ring.lookupn_hashes([h], n)
+        assert [ring.name(x) for x in g[0][:gc[0]]] == [oracle.name(x) for x in oracle.lookupn_hash(h, n)], (i, h, n)
     ring.service(0)
 
 
