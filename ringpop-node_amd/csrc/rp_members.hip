@@ -520,95 +520,106 @@ __global__ __launch_bounds__(kBkST) void k_bk_scatter(const uint32_t* __restrict
     __shared__ int64_t s_mn[kBkST / 64], s_mx[kBkST / 64];
     __shared__ uint16_t ls[kBkMaxBuckets];  // <= 4,096 (60 KB in all: two tiles per CU)
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const uint32_t t = blockIdx.x, base = t * kBkTile;
-    const uint32_t n = k - base < kBkTile ? k - base : kBkTile;
-    for (uint32_t b = tid; b < nb; b += kBkST) h[b] = 0;
-    __syncthreads();
     constexpr uint32_t PER = kBkTile / kBkST;
     uint32_t rk[PER], idv[PER];
     uint8_t stv[PER];
     int64_t incv[PER];
+    auto load = [&](uint32_t tt) {  // every load of a tile in flight at once
+        const uint32_t bs = tt * kBkTile, nn = k - bs < kBkTile ? k - bs : kBkTile;
 #pragma unroll
-    for (uint32_t q = 0; q < PER; q++) {  // every load in flight before the first atomic
-        const uint32_t i = tid + q * kBkST;
-        idv[q] = i < n ? ids[base + i] : 0u;
-        stv[q] = i < n ? chs[base + i] : (uint8_t)0;
-        incv[q] = i < n ? chi[base + i] : 0;
-    }
+        for (uint32_t q = 0; q < PER; q++) {
+            const uint32_t i = tid + q * kBkST;
+            idv[q] = i < nn ? ids[bs + i] : 0u;
+            stv[q] = i < nn ? chs[bs + i] : (uint8_t)0;
+            incv[q] = i < nn ? chi[bs + i] : 0;
+        }
+    };
     // the outputs start as copies; the fold rewrites local overrides. Outputs that alias the
     // inputs (the reference rewrites its update objects in place) need no copy.
     const bool cst = nst && nst != chs, cinc = ninc && ninc != chi;
+    // a workgroup takes tiles blockIdx.x, + gridDim.x, ...: the next tile's inputs are loaded
+    // while this tile's records are stored (round 5; one tile per workgroup when the grid covers
+    // every tile)
+    uint32_t t = blockIdx.x;
+    if (t < ntiles) load(t);
+    for (; t < ntiles; t += gridDim.x) {
+        const uint32_t base = t * kBkTile;
+        const uint32_t n = k - base < kBkTile ? k - base : kBkTile;
+        for (uint32_t b = tid; b < nb; b += kBkST) h[b] = 0;
+        __syncthreads();
 #pragma unroll
-    for (uint32_t q = 0; q < PER; q++) {
-        const uint32_t i = tid + q * kBkST;
-        if (i < n) {
-            if (cst) nst[base + i] = stv[q];
-            if (cinc) ninc[base + i] = incv[q];
-        }
-    }
-    int64_t mn = INT64_MAX, mx = INT64_MIN;
-#pragma unroll
-    for (uint32_t q = 0; q < PER; q++)
-        if (tid + q * kBkST < n) {
-            mn = incv[q] < mn ? incv[q] : mn;
-            mx = incv[q] > mx ? incv[q] : mx;
-        }
-    bk_minmax(mn, mx);
-    if (lane == 0) {
-        s_mn[wv] = mn;
-        s_mx[wv] = mx;
-    }
-#pragma unroll
-    for (uint32_t q = 0; q < PER; q++) rk[q] = tid + q * kBkST < n ? atomicAdd(&h[idv[q] >> kBkBits], 1u) : 0u;
-    __syncthreads();
-    for (uint32_t w = 0; w < kBkST / 64; w++) {
-        mn = s_mn[w] < mn ? s_mn[w] : mn;
-        mx = s_mx[w] > mx ? s_mx[w] : mx;
-    }
-    const bool c8 = tb != nullptr && mn != kBkWide && (uint64_t)(mx - mn) <= 0xFFFFFFFFull;  // block-uniform
-    if (tid == 0 && tb) tb[t] = c8 ? mn : kBkWide;
-    // exclusive scan of h over the buckets (contiguous runs per thread, then across threads)
-    const uint32_t per = (nb + kBkST - 1) / kBkST, b0 = min(nb, tid * per), b1 = min(nb, b0 + per);
-    uint32_t run = 0;
-    for (uint32_t b = b0; b < b1; b++) run += h[b];
-    uint32_t inc = run;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t x = __shfl_up(inc, o, 64);
-        if (lane >= (uint32_t)o) inc += x;
-    }
-    if (lane == 63) s_w[wv] = inc;
-    __syncthreads();
-    uint32_t ex = inc - run;
-    for (uint32_t w = 0; w < wv; w++) ex += s_w[w];
-    for (uint32_t b = b0; b < b1; b++) {
-        ls[b] = ex;
-        seg[seg_at(b, t, ntiles)] = (ex << 16) | h[b];  // start <= 4,096, length <= 4,096
-        ex += h[b];
-    }
-    __syncthreads();
-    const uint32_t rw = c8 ? 2u : 3u;  // record words
-#pragma unroll
-    for (uint32_t q = 0; q < PER; q++) {
-        const uint32_t i = tid + q * kBkST;
-        if (i < n) {
-            const uint32_t b = idv[q] >> kBkBits, e = rw * (ls[b] + rk[q]);
-            const int64_t inc8 = incv[q];
-            stage[e] = brec_x(idv[q] & (kBk - 1u), i, stv[q] & 3u);
-            if (c8) {
-                stage[e + 1] = (uint32_t)(uint64_t)(inc8 - mn);
-            } else {
-                stage[e + 1] = (uint32_t)(uint64_t)inc8;
-                stage[e + 2] = (uint32_t)((uint64_t)inc8 >> 32);
+        for (uint32_t q = 0; q < PER; q++) {
+            const uint32_t i = tid + q * kBkST;
+            if (i < n) {
+                if (cst) nst[base + i] = stv[q];
+                if (cinc) ninc[base + i] = incv[q];
             }
         }
+        int64_t mn = INT64_MAX, mx = INT64_MIN;
+#pragma unroll
+        for (uint32_t q = 0; q < PER; q++)
+            if (tid + q * kBkST < n) {
+                mn = incv[q] < mn ? incv[q] : mn;
+                mx = incv[q] > mx ? incv[q] : mx;
+            }
+        bk_minmax(mn, mx);
+        if (lane == 0) {
+            s_mn[wv] = mn;
+            s_mx[wv] = mx;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < PER; q++) rk[q] = tid + q * kBkST < n ? atomicAdd(&h[idv[q] >> kBkBits], 1u) : 0u;
+        __syncthreads();
+        for (uint32_t w = 0; w < kBkST / 64; w++) {
+            mn = s_mn[w] < mn ? s_mn[w] : mn;
+            mx = s_mx[w] > mx ? s_mx[w] : mx;
+        }
+        const bool c8 = tb != nullptr && mn != kBkWide && (uint64_t)(mx - mn) <= 0xFFFFFFFFull;  // block-uniform
+        if (tid == 0 && tb) tb[t] = c8 ? mn : kBkWide;
+        // exclusive scan of h over the buckets (contiguous runs per thread, then across threads)
+        const uint32_t per = (nb + kBkST - 1) / kBkST, b0 = min(nb, tid * per), b1 = min(nb, b0 + per);
+        uint32_t run = 0;
+        for (uint32_t b = b0; b < b1; b++) run += h[b];
+        uint32_t inc = run;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t x = __shfl_up(inc, o, 64);
+            if (lane >= (uint32_t)o) inc += x;
+        }
+        if (lane == 63) s_w[wv] = inc;
+        __syncthreads();
+        uint32_t ex = inc - run;
+        for (uint32_t w = 0; w < wv; w++) ex += s_w[w];
+        for (uint32_t b = b0; b < b1; b++) {
+            ls[b] = ex;
+            seg[seg_at(b, t, ntiles)] = (ex << 16) | h[b];  // start <= 4,096, length <= 4,096
+            ex += h[b];
+        }
+        __syncthreads();
+        const uint32_t rw = c8 ? 2u : 3u;  // record words
+#pragma unroll
+        for (uint32_t q = 0; q < PER; q++) {
+            const uint32_t i = tid + q * kBkST;
+            if (i < n) {
+                const uint32_t b = idv[q] >> kBkBits, e = rw * (ls[b] + rk[q]);
+                const int64_t inc8 = incv[q];
+                stage[e] = brec_x(idv[q] & (kBk - 1u), i, stv[q] & 3u);
+                if (c8) {
+                    stage[e + 1] = (uint32_t)(uint64_t)(inc8 - mn);
+                } else {
+                    stage[e + 1] = (uint32_t)(uint64_t)inc8;
+                    stage[e + 2] = (uint32_t)((uint64_t)inc8 >> 32);
+                }
+            }
+        }
+        if (t + gridDim.x < ntiles) load(t + gridDim.x);  // in flight under the stores below
+        __syncthreads();
+        // the tile's run: n records of 8 or 12 B at recs + tile * kBkTile (16-B stores; the tile's
+        // run starts 16-B aligned, and its padded tail is never read)
+        uint4* d4 = reinterpret_cast<uint4*>(recs + (uint64_t)t * kBkTile);
+        const uint4* s4 = reinterpret_cast<const uint4*>(stage);
+        for (uint32_t q = tid; q < (rw * n + 3u) / 4u; q += kBkST) d4[q] = s4[q];
     }
-    __syncthreads();
-    // the tile's run: n records of 8 or 12 B at recs + tile * kBkTile (16-B stores; the tile's
-    // run starts 16-B aligned, and its padded tail is never read)
-    uint4* d4 = reinterpret_cast<uint4*>(recs + (uint64_t)t * kBkTile);
-    const uint4* s4 = reinterpret_cast<const uint4*>(stage);
-    for (uint32_t q = tid; q < (rw * n + 3u) / 4u; q += kBkST) d4[q] = s4[q];
 }
 
 // One change on a member row (the step of fold_address without damp scoring): returns applied
@@ -1387,8 +1398,10 @@ struct Members {
             g_part.reserve(nb + 1);
             bk_tb.reserve(ntiles);
             const bool rec8 = !(getenv("RP_BK_REC8") && !strcmp(getenv("RP_BK_REC8"), "0"));  // A/B: 0 = 12-B always
-            hipLaunchKernelGGL(k_bk_scatter, dim3(ntiles), dim3(kBkST), 0, s, ids, chs, chi, k, nb, ntiles, bk_recs.p,
-                               bk_seg.p, rec8 ? bk_tb.p : nullptr, nst, ninc);
+            // workgroups of the scatter (A/B: RP_BK_SGRID; 0 or >= ntiles: one tile each)
+            const uint32_t sg = (uint32_t)env_pos("RP_BK_SGRID", 0);
+            hipLaunchKernelGGL(k_bk_scatter, dim3(sg && sg < ntiles ? sg : ntiles), dim3(kBkST), 0, s, ids, chs, chi, k,
+                               nb, ntiles, bk_recs.p, bk_seg.p, rec8 ? bk_tb.p : nullptr, nst, ninc);
             const bool direct = !(getenv("RP_BK_DIRECT") && !strcmp(getenv("RP_BK_DIRECT"), "0"));
             if (direct)
                 hipLaunchKernelGGL(k_bk_fold<true>, dim3((nb + 7) / 8 * 8), dim3(kBkFT), 0, s, bk_recs.p, bk_seg.p,

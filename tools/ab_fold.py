@@ -18,7 +18,7 @@ import sys
 import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KNOBS = ("RP_BK_DIRECT", "RP_BK_REC8")
+KNOBS = ("RP_BK_DIRECT", "RP_BK_REC8", "RP_BK_SGRID")
 
 
 def _load(name, path):
