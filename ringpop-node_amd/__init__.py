@@ -1111,11 +1111,20 @@ class MessageExchange:
         # the same ranks (no device collective, no device -> host read, round 5)
         if self.on_device:
             ranks = list(range(self.G)) if group is None else dist.get_process_group_ranks(group)
-            self._cgroup = dist.new_group(ranks=ranks, backend="gloo")
+            # one node (bench.py, tests): gloo over loopback, whatever the hostname resolves to
+            os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+            try:
+                self._cgroup = dist.new_group(ranks=ranks, backend="gloo")
+            except Exception:  # no gloo here: the counts go over the nccl group (a device read)
+                self._cgroup = None
         else:
             self._cgroup = group
-        self._cnt = torch.zeros(2 * self.G, dtype=torch.int64)
-        self._rcnt = torch.zeros(2 * self.G, dtype=torch.int64)
+        self._cdev = self.on_device and self._cgroup is None
+        cdev = self.device if self._cdev else "cpu"
+        if self._cdev:
+            self._cgroup = group
+        self._cnt = torch.zeros(2 * self.G, dtype=torch.int64, device=cdev)
+        self._rcnt = torch.zeros(2 * self.G, dtype=torch.int64, device=cdev)
         self._host = {}  # gloo staging buffers, kept across rounds
         self._events = []  # (start, end) of every byte collective queued on the device
 
@@ -1155,7 +1164,7 @@ class MessageExchange:
         torch, dist, G = self.torch, self.dist, self.G
         self._cnt.copy_(torch.from_numpy(np.stack([out_nmsg, out_nrec], axis=1).astype(np.int64).reshape(-1)))
         dist.all_to_all_single(self._rcnt, self._cnt, group=self._cgroup)
-        rc = self._rcnt.numpy().reshape(G, 2)
+        rc = (self._rcnt.cpu() if self._cdev else self._rcnt).numpy().reshape(G, 2)
         in_nmsg, in_nrec = rc[:, 0].astype(np.uint64), rc[:, 1].astype(np.uint64)
         seg_out = [int(out_nmsg[g]) * MSG_BYTES + int(out_nrec[g]) * REC_BYTES for g in range(G)]
         seg_in = [int(in_nmsg[g]) * MSG_BYTES + int(in_nrec[g]) * REC_BYTES for g in range(G)]
