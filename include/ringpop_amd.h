@@ -161,11 +161,16 @@ int rp_members_set_local(rp_members *m, uint32_t local_id);
 /* Membership.update(changes) for k changes (ids, status, incarnation) evaluated in array order
  * with Date.now() = now_ms. applied[i]: 0 not applied, 1 applied, 2 created a new member;
  * new_status/new_inc: the update as applied (local override rewrites it). If anything applied
- * the checksum is recomputed once. Host buffers (all outputs nullable). */
+ * the checksum is recomputed once. Host buffers (all outputs nullable). Incarnations must lie in
+ * [-2^60, 2^60) (a JS Number is exact to 2^53; the member table stores 61 bits) and statuses in
+ * 0..3, else RP_EINVAL with nothing applied. */
 int rp_members_update(rp_members *m, const uint32_t *ids, const uint8_t *status, const int64_t *inc, uint32_t k,
                       int64_t now_ms, uint8_t *applied, uint8_t *new_status, int64_t *new_inc,
                       uint32_t *n_applied);
-/* Same, device buffers, stream-ordered, no host synchronization (d_n_applied nullable). */
+/* Same, device buffers, stream-ordered, no host synchronization (d_n_applied nullable). An
+ * incarnation outside [-2^60, 2^60) is reported as RP_EDEVICE by the handle's next host-
+ * synchronizing call. The status / incarnation outputs may be the input arrays themselves (the
+ * reference rewrites its update objects in place): the copy is then skipped. */
 int rp_members_update_dev(rp_members *m, const uint32_t *d_ids, const uint8_t *d_status, const int64_t *d_inc,
                           uint32_t k, int64_t now_ms, uint8_t *d_applied, uint8_t *d_new_status,
                           int64_t *d_new_inc, uint32_t *d_n_applied, void *stream);

@@ -37,35 +37,34 @@ struct DampArgs {
     uint8_t* exc;   // per change: 'suppressLimitExceeded' emitted (member.js:141-152)
 };
 
-// One member row in HBM (16 B, one aligned load / store per member): incarnation, status,
-// exists, and the grouped fold's per-batch change counter (0 between batches).
-struct alignas(16) MRow {
+// One member row in HBM, 8 B since round 5 (16 B before, with the grouped fold's change counter,
+// which now has its own array): incarnation << 3 | exists << 2 | status, the incarnation a
+// signed 61-bit integer (a JS Number is exact to 2^53, a wire number has at most 18 digits;
+// kMemberIncMax bounds what a row can hold and the fold reports anything past it). One dwordx2
+// load / store per row; the 2^22 bucket fold moves half the row bytes it did.
+struct alignas(8) MRow {
+    uint64_t v;
+};
+static_assert(sizeof(MRow) == 8, "MRow is one 8-byte load");
+constexpr int64_t kMemberIncMax = (1ll << 60) - 1, kMemberIncMin = -(1ll << 60);
+struct MRowV {  // a row as loaded
     int64_t inc;
     uint8_t status;
     uint8_t exists;
-    uint16_t pad;
-    uint32_t cnt;
 };
-static_assert(sizeof(MRow) == 16, "MRow is one 16-byte load");
-
-// One dwordx4 load / store per row (a struct copy would be split into per-field accesses).
-__device__ __forceinline__ MRow row_load(const MRow* p) {
-    const uint4 v = *reinterpret_cast<const uint4*>(p);
-    MRow r;
-    r.inc = (int64_t)(((uint64_t)v.y << 32) | v.x);
-    r.status = (uint8_t)(v.z & 0xFFu);
-    r.exists = (uint8_t)((v.z >> 8) & 0xFFu);
-    r.pad = 0;
-    r.cnt = v.w;
-    return r;
+__host__ __device__ __forceinline__ MRowV row_unpack(uint64_t v) {
+    return MRowV{(int64_t)v >> 3, (uint8_t)(v & 3u), (uint8_t)((v >> 2) & 1u)};
 }
-__device__ __forceinline__ void row_store(MRow* p, int64_t inc, uint8_t status, uint8_t exists, uint32_t cnt = 0) {
-    uint4 v;
-    v.x = (uint32_t)(uint64_t)inc;
-    v.y = (uint32_t)((uint64_t)inc >> 32);
-    v.z = (uint32_t)status | ((uint32_t)exists << 8);
-    v.w = cnt;  // the grouped fold's change counter, normally cleared
-    *reinterpret_cast<uint4*>(p) = v;
+__host__ __device__ __forceinline__ uint64_t row_pack(int64_t inc, uint8_t status, uint8_t exists) {
+    return ((uint64_t)inc << 3) | ((uint64_t)(exists ? 1u : 0u) << 2) | (uint64_t)(status & 3u);
+}
+__device__ __forceinline__ MRowV row_load(const MRow* p) { return row_unpack(*reinterpret_cast<const uint64_t*>(p)); }
+// err (nullable): kErrRange when the incarnation does not fit the row (the row then holds garbage;
+// the call reports RP_EDEVICE at the handle's next sync)
+__device__ __forceinline__ void row_store(MRow* p, int64_t inc, uint8_t status, uint8_t exists,
+                                          uint32_t* err = nullptr) {
+    if (err && (inc > kMemberIncMax || inc < kMemberIncMin)) atomicOr(err, kErrRange);
+    *reinterpret_cast<uint64_t*>(p) = row_pack(inc, status, exists);
 }
 
 // The batch and table operands of one Membership.update fold.
@@ -73,6 +72,8 @@ struct FoldArgs {
     const uint8_t* ch_status;
     const int64_t* ch_inc;
     MRow* rows;
+    uint32_t* cnt;  // per member: the grouped fold's change counter (0 between batches) / kOvfMark
+    uint32_t* err;  // the handle's device error word (kErrRange)
     uint32_t local_id;
     int64_t now_ms;
     uint8_t* applied;
@@ -92,7 +93,7 @@ struct FoldArgs {
 // Returns the number of changes applied (the caller sums them per wave: one atomic per wave,
 // not per address, on the batch's applied counter).
 template <class Change>
-__device__ __forceinline__ uint32_t fold_address(const FoldArgs& A, uint32_t id, MRow row, uint32_t c, Change change,
+__device__ __forceinline__ uint32_t fold_address(const FoldArgs& A, uint32_t id, MRowV row, uint32_t c, Change change,
                                                  uint32_t cnt_after = 0) {
     const DampArgs& da = A.da;
     bool ex = row.exists != 0;
@@ -140,7 +141,8 @@ __device__ __forceinline__ uint32_t fold_address(const FoldArgs& A, uint32_t id,
             da.exc[j] = exc ? 1 : 0;
         }
     }
-    row_store(A.rows + id, in, st, ex ? 1 : 0, cnt_after);
+    row_store(A.rows + id, in, st, ex ? 1 : 0, A.err);
+    A.cnt[id] = cnt_after;
     if (da.score) {
         da.score[id] = sc;
         da.last[id] = ls;
@@ -233,22 +235,22 @@ constexpr uint32_t kOvfMark = 0xFFFFFFFFu;  // row counter of an address left to
 constexpr uint32_t kDoneWords = 4;  // [0] k_link_fold barrier count, [1] k_fold, [2] k_ovf_len's ticket, [3] barrier generation
 
 __device__ __forceinline__ void link_one(uint32_t i, const uint32_t* __restrict__ ids, uint32_t k,
-                                         MRow* __restrict__ rows, uint32_t* __restrict__ slots,
+                                         uint32_t* __restrict__ cnt, uint32_t* __restrict__ slots,
                                          uint8_t* __restrict__ rk, uint32_t* __restrict__ ovf,
                                          uint32_t* __restrict__ napplied) {
     if (i == 0) *napplied = 0;
     if (i >= k) return;
     const uint32_t id = ids[i];
-    const uint32_t r = atomicAdd(&rows[id].cnt, 1u);
+    const uint32_t r = atomicAdd(&cnt[id], 1u);
     rk[i] = r < 255u ? (uint8_t)r : (uint8_t)255;
     if (r >= 1u && r <= kSlots) slots[(uint64_t)id * kSlots + (r - 1u)] = i;
     if (r == kSlots + 1u) *ovf = 1u;
 }
 
-__global__ void k_link(const uint32_t* __restrict__ ids, uint32_t k, MRow* __restrict__ rows,
+__global__ void k_link(const uint32_t* __restrict__ ids, uint32_t k, uint32_t* __restrict__ cnt,
                        uint32_t* __restrict__ slots, uint8_t* __restrict__ rk, uint32_t* __restrict__ ovf,
                        uint32_t* __restrict__ napplied) {
-    link_one(blockIdx.x * blockDim.x + threadIdx.x, ids, k, rows, slots, rk, ovf, napplied);
+    link_one(blockIdx.x * blockDim.x + threadIdx.x, ids, k, cnt, slots, rk, ovf, napplied);
 }
 
 // The workgroup's applied count goes to part[blockIdx.x] (summed by k_ovf_len or k_fold_ovf).
@@ -259,10 +261,10 @@ __device__ __forceinline__ void fold_fast_block(const uint32_t* __restrict__ ids
     uint32_t napp = 0;
     if (i < k && rk[i] == 0) {
         const uint32_t id = ids[i];
-        const MRow row = row_load(A.rows + id);
-        const uint32_t c = row.cnt;
+        const MRowV row = row_load(A.rows + id);
+        const uint32_t c = A.cnt[id];
         if (c > kSlots + 1) {  // more changes than slots: marked for k_fold_ovf
-            A.rows[id].cnt = kOvfMark;
+            A.cnt[id] = kOvfMark;
         } else if (c <= 1) {
             napp = fold_address(A, id, row, 1, [&](uint32_t) { return i; });
         } else {
@@ -326,7 +328,7 @@ __global__ __launch_bounds__(256) void k_link_fold(const uint32_t* __restrict__ 
                                                    uint32_t* __restrict__ slots, uint8_t* __restrict__ rk,
                                                    uint32_t* __restrict__ ovf, uint32_t* __restrict__ napplied,
                                                    FoldArgs A, uint32_t* __restrict__ part, uint32_t* __restrict__ err) {
-    link_one(blockIdx.x * blockDim.x + threadIdx.x, ids, k, A.rows, slots, rk, ovf, napplied);
+    link_one(blockIdx.x * blockDim.x + threadIdx.x, ids, k, A.cnt, slots, rk, ovf, napplied);
     grid_sync(napplied + 2, napplied + 5, err);
     fold_fast_block(ids, k, rk, slots, A, part);
 }
@@ -349,7 +351,7 @@ __device__ uint32_t ovf_fold(const uint32_t* __restrict__ ids, uint32_t k, const
         bool f = false;
         if (i < k) {
             id = ids[i];
-            f = __hip_atomic_load(&A.rows[id].cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == kOvfMark;
+            f = __hip_atomic_load(&A.cnt[id], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == kOvfMark;
         }
         const uint64_t bal = __ballot(f);
         if (lane == 0) s_cnt[wv] = (uint32_t)__popcll(bal);
@@ -394,7 +396,7 @@ __device__ uint32_t ovf_fold(const uint32_t* __restrict__ ids, uint32_t k, const
     }
     for (uint32_t i = tid; i < k; i += NT) {
         const uint32_t id = ids[i];
-        if (A.rows[id].cnt == kOvfMark) A.rows[id].cnt = 0;
+        if (A.cnt[id] == kOvfMark) A.cnt[id] = 0;
     }
     return napp;
 }
@@ -757,11 +759,11 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
     const bool listed = nd <= kBkDup;  // block-uniform
     uint32_t napp = 0;
     constexpr uint32_t PI = kBk / kBkFT;  // ids per lane
-    uint4 wv4[PI];
+    uint64_t wv4[PI];
 #pragma unroll
     for (uint32_t u = 0; u < PI; u++) {  // each lane's rows in flight together
         const uint32_t q = tid + u * kBkFT, v = fjs[q];
-        if (v != kBkNone && !(v & kBkRep)) wv4[u] = *reinterpret_cast<const uint4*>(A.rows + id0 + q);
+        if (v != kBkNone && !(v & kBkRep)) wv4[u] = *reinterpret_cast<const uint64_t*>(A.rows + id0 + q);
     }
 #pragma unroll
     for (uint32_t u = 0; u < PI; u++) {  // ids in order: coalesced rows and results
@@ -769,18 +771,19 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
         const uint32_t v = fjs[q], id = id0 + q;
         uint8_t r = 0;
         if (v != kBkNone && !(v & kBkRep)) {
-            bool ex = ((wv4[u].z >> 8) & 0xFFu) != 0;
-            uint8_t st = (uint8_t)(wv4[u].z & 0xFFu);
-            int64_t in = (int64_t)(((uint64_t)wv4[u].y << 32) | wv4[u].x);
+            const MRowV rw = row_unpack(wv4[u]);
+            bool ex = rw.exists != 0;
+            uint8_t st = rw.status;
+            int64_t in = rw.inc;
             r = bk_step(A, id, ex, st, in, (uint8_t)(v >> 30), finc[q]);
-            row_store(A.rows + id, in, st, 1);
+            row_store(A.rows + id, in, st, 1, A.err);
             if (DIRECT && A.applied) A.applied[v & 0x1FFFFFFFu] = r & 3u;
             if (r & kResLocal) bk_local(A, v & 0x1FFFFFFFu);
             napp += (r & 3u) ? 1u : 0u;
         } else if (v != kBkNone) {
             r = kResRep;
             if (!listed) {  // the overflow fold takes the address
-                A.rows[id].cnt = kOvfMark;
+                A.cnt[id] = kOvfMark;
                 *ovf = 1u;
             }
         }
@@ -811,7 +814,7 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
             const uint32_t il = (uint32_t)(dk[q] >> 40);
             if (q > 0 && (uint32_t)(dk[q - 1] >> 40) == il) continue;  // not a segment head
             const uint32_t id = id0 + il;
-            const MRow row = row_load(A.rows + id);
+            const MRowV row = row_load(A.rows + id);
             bool ex = row.exists != 0;
             uint8_t st = row.status;
             int64_t in = row.inc;
@@ -824,7 +827,7 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
                 if (r & kResLocal) bk_local(A, j);
                 napp += (r & 3u) ? 1u : 0u;
             }
-            row_store(A.rows + id, in, st, ex ? 1 : 0);
+            row_store(A.rows + id, in, st, ex ? 1 : 0, A.err);
         }
     }
 #pragma unroll
@@ -878,7 +881,7 @@ __global__ void k_damp_decay(const MRow* __restrict__ rows, uint32_t n, double* 
                              int64_t now_ms) {
     const uint32_t gstride = gridDim.x * blockDim.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gstride)
-        if (rows[i].exists) score[i] = damp::decayed(c, last[i], ts[i], now_ms);
+        if (row_load(rows + i).exists) score[i] = damp::decayed(c, last[i], ts[i], now_ms);
 }
 
 template <class T>
@@ -962,7 +965,7 @@ constexpr uint32_t kMckStage = 24576;  // LDS bytes a tile's pieces are assemble
 // so a tile's names are one contiguous run; only the row is a random access.
 struct MckItem {
     uint32_t id, len, nlen, sh;
-    MRow row;
+    MRowV row;
     uint64_t noff;
     uint32_t w[8];
 };
@@ -1185,7 +1188,7 @@ __global__ void k_rows_split(const MRow* __restrict__ rows, uint32_t n, uint8_t*
                              uint8_t* __restrict__ st, int64_t* __restrict__ inc) {
     const uint32_t gstride = gridDim.x * blockDim.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gstride) {
-        const MRow r = row_load(rows + i);
+        const MRowV r = row_load(rows + i);
         ex[i] = r.exists;
         st[i] = r.status;
         inc[i] = r.inc;
@@ -1201,7 +1204,8 @@ struct Members {
     uint32_t local_id = 0xFFFFFFFFu;
     uint32_t cap = 0;
     bool defer_ck = false;  // rp_members_defer_checksum
-    DevBuf<MRow> rows;          // the member table, one 16-B row per id
+    DevBuf<MRow> rows;          // the member table, one 8-B row per id
+    DevBuf<uint32_t> rcnt;      // per id: the grouped fold's change counter / overflow mark
     DevBuf<uint32_t> ck;        // [0] checksum, [1] is_set
     // [0] per-batch applied count (the checksum gate), [1] the grouped path overflowed (cleared
     // by the sorted fold that then runs), [2..) the launches' last-workgroup counters
@@ -1329,7 +1333,8 @@ struct Members {
     void grow(uint32_t need) {
         if (need <= cap) return;
         uint32_t nc = std::max<uint32_t>(need, cap ? cap * 2 : 1024);
-        grow_one<MRow>(rows, cap, nc, MRow{0, 0, 0, 0, 0});
+        grow_one<MRow>(rows, cap, nc, MRow{0});
+        grow_one<uint32_t>(rcnt, cap, nc, 0u);
         if (damp_on) {
             grow_one<double>(d_score, cap, nc, dcfg.initial);
             grow_one<double>(d_last, cap, nc, dcfg.initial);
@@ -1370,7 +1375,12 @@ struct Members {
             d_exc.reserve(k);
             d_out_k = k;
         }
-        const FoldArgs A{chs, chi, rows.p, local_id, now_ms, applied, nst, ninc, napplied.p, damp_args(true)};
+        if (!ws.err.p) {
+            ws.err.reserve(1);
+            RP_HIP(hipMemsetAsync(ws.err.p, 0, sizeof(uint32_t), s));
+        }
+        const FoldArgs A{chs, chi, rows.p, rcnt.p, ws.err.p, local_id, now_ms, applied, nst, ninc, napplied.p,
+                         damp_args(true)};
         int bits = 8;
         while (bits < 32 && (1ull << bits) < nt.size()) bits += 8;
         sk.reserve(k);
@@ -1446,7 +1456,7 @@ struct Members {
                 hipLaunchKernelGGL(k_link_fold, dim3(g1), dim3(256), 0, s, ids, k, g_slots.p, g_rk.p, ovf, napplied.p, A,
                                    g_part.p, ws.err.p);
             } else {
-                hipLaunchKernelGGL(k_link, dim3(g1), dim3(256), 0, s, ids, k, rows.p, g_slots.p, g_rk.p, ovf,
+                hipLaunchKernelGGL(k_link, dim3(g1), dim3(256), 0, s, ids, k, rcnt.p, g_slots.p, g_rk.p, ovf,
                                    napplied.p);
                 hipLaunchKernelGGL(k_fold_fast, dim3(g1), dim3(256), 0, s, ids, k, g_rk.p, g_slots.p, A, g_part.p);
             }
@@ -1714,7 +1724,12 @@ int rp_members_update(rp_members* h, const uint32_t* ids, const uint8_t* status,
     return guard([&] {
         rp::Members& m = MB(h);
         RP_REQUIRE(k == 0 || (ids && status && inc), "update: null change buffers");
-        for (uint32_t i = 0; i < k; i++) RP_REQUIRE(ids[i] < m.nt.size(), "update: id was never interned");
+        for (uint32_t i = 0; i < k; i++) {
+            RP_REQUIRE(ids[i] < m.nt.size(), "update: id was never interned");
+            // a member row holds a 61-bit incarnation and a 2-bit status (MRow)
+            RP_REQUIRE(inc[i] >= rp::kMemberIncMin && inc[i] <= rp::kMemberIncMax && status[i] < 4,
+                       "update: incarnation outside [-2^60, 2^60) or status past leave");
+        }
         const uint32_t kk = k ? k : 1;
         m.io_ids.reserve(kk);
         m.io_st.reserve(kk);
@@ -1755,7 +1770,11 @@ int rp_members_set(rp_members* h, const uint32_t* ids, const uint8_t* status, co
     return guard([&] {
         rp::Members& m = MB(h);
         RP_REQUIRE(k == 0 || (ids && status && inc), "set: null change buffers");
-        for (uint32_t i = 0; i < k; i++) RP_REQUIRE(ids[i] < m.nt.size(), "set: id was never interned");
+        for (uint32_t i = 0; i < k; i++) {
+            RP_REQUIRE(ids[i] < m.nt.size(), "set: id was never interned");
+            RP_REQUIRE(inc[i] >= rp::kMemberIncMin && inc[i] <= rp::kMemberIncMax && status[i] < 4,
+                       "set: incarnation outside [-2^60, 2^60) or status past leave");
+        }
         const uint32_t kk = k ? k : 1;
         m.io_ids.reserve(kk + 1);
         m.io_st.reserve(kk);

@@ -385,3 +385,37 @@ def test_bucket_fold_wide_tiles_and_in_place_outputs(gpu, orc, monkeypatch, reco
     assert np.array_equal(d_st.cpu().numpy(), os_) and np.array_equal(d_inc.cpu().numpy(), oi)
     assert (oi[[77, 4096 * 3 + 5, 4096 * 100 + 9]] == now).all()  # the override ran
     assert m.checksum == o.checksum
+
+
+def test_member_rows_incarnation_range(gpu, orc):
+    """Member rows hold a 61-bit incarnation (8-B rows since round 5): the extremes of the range
+    fold like any value against the oracle; one past it is refused by the host call (RP_EINVAL,
+    nothing applied) and reported by the device call at the next sync (RP_EDEVICE)."""
+    import torch
+
+    names = ["10.9.0.%d:1" % i for i in range(8)]
+    m = gpu.Membership(whoami=names[0], capacity=16)
+    o = orc.Members(names, local=names[0], join_seed=0)
+    ids = np.asarray(m.intern(names), dtype=np.uint32)
+    lo, hi = -(1 << 60), (1 << 60) - 1
+    for inc in ([lo] * 8, [hi - 1] * 8, [hi] * 8, [-5, 0, 1 << 53, lo + 1, hi, 7, -(1 << 59), 1 << 40]):
+        st = np.array([0, 1, 2, 3, 0, 1, 2, 3], np.uint8)
+        inc = np.asarray(inc, np.int64)
+        ga, gs, gi, gna = m.update_ids(ids, st, inc, now_ms=1434500000000)
+        oa, os_, oi, ona = o.update_ids(ids, st, inc, False, 1434500000000)
+        assert gna == ona and np.array_equal(ga > 0, oa > 0)
+        assert np.array_equal(gs, os_) and np.array_equal(gi, oi)
+        assert m.checksum == o.checksum
+    with pytest.raises(gpu.RingpopAmdError):
+        m.update_ids(ids[:1], np.zeros(1, np.uint8), np.array([1 << 60], np.int64), now_ms=1)
+    with pytest.raises(gpu.RingpopAmdError):
+        m.update_ids(ids[:1], np.array([4], np.uint8), np.array([5], np.int64), now_ms=1)
+    assert m.checksum == o.checksum  # nothing applied
+    d_ids = torch.from_numpy(ids[1:2].view(np.int32)).cuda()
+    d_st = torch.zeros(1, dtype=torch.uint8, device="cuda")
+    d_inc = torch.full((1,), 1 << 61, dtype=torch.int64, device="cuda")
+    m.update_dev(d_ids.data_ptr(), d_st.data_ptr(), d_inc.data_ptr(), 1, 2, None, None, None, None,
+                 torch.cuda.current_stream().cuda_stream)
+    with pytest.raises(gpu.RingpopAmdError):
+        m.checksum
+    m.close()
