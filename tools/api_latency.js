@@ -41,7 +41,7 @@ function timeit(fn, n, w) {
 }
 
 var out = {servers: nServers};
-var ring = new amd.HashRing();
+var ring = new amd.HashRing({serviceIdleMs: 0});  // the launch-per-call legs first; the service below
 var servers = [];
 for (var s = 0; s < nServers; s++) { servers.push(addr(s)); }
 ring.addRemoveServers(servers);
