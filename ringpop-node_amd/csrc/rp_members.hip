@@ -228,8 +228,8 @@ __global__ __launch_bounds__(256) void k_fold(const uint32_t* __restrict__ sk, c
 //   repeated address, its slots (contiguous, no dependent list walk), puts the indices in
 //   arrival order in registers and folds them. An address with more changes is marked
 //   (counter = kOvfMark) and left to k_fold_ovf, one gated launch after it.
-// Each address costs one atomic, one 16-B row load and one 16-B row store; the batch's applied
-// counter is cleared by k_link, so the batch needs no memset.
+// Each address costs one atomic on its counter, one 8-B row load and one 8-B row store (and its
+// counter reset); the batch's applied counter is cleared by k_link, so the batch needs no memset.
 constexpr uint32_t kSlots = 15;  // changes per address on the grouped path: kSlots + 1
 constexpr uint32_t kOvfMark = 0xFFFFFFFFu;  // row counter of an address left to k_fold_ovf
 constexpr uint32_t kDoneWords = 4;  // [0] k_link_fold barrier count, [1] k_fold, [2] k_ovf_len's ticket, [3] barrier generation
@@ -430,26 +430,27 @@ __global__ __launch_bounds__(1024) void k_fold_ovf(const uint32_t* __restrict__ 
 
 // Bucket path (large batches, round 3): the batch is partitioned by id into buckets of kBk ids
 // (a stable-per-id order is not needed: an address's changes are put back in arrival order by
-// their batch index), then one workgroup folds one bucket with the bucket's 128 KB of rows
+// their batch index), then one workgroup folds one bucket with the bucket's 32 KB of rows
 // resident in its XCD's L2, so the row accesses and the rank counters stop being random HBM /
-// memory-side atomics (k_link's one atomic per change was half of a 2^22 batch). Three launches:
-//   k_bk_scatter a 4,096-change tile sorts its 12-B records {bucket-local id, tile-relative
-//                index, status; incarnation} by bucket in LDS and stores them as one contiguous run at
-//                recs + tile * kBkTile (whole lines); seg[bucket][tile] = the bucket's segment
-//                of that run (start << 16 | length). No global count pass or scan: the fold
-//                walks a bucket's segments of every tile.
+// memory-side atomics (k_link's one atomic per change was half of a 2^22 batch). Two launches
+// and the gated overflow fold:
+//   k_bk_scatter a 4,096-change tile sorts its records (8 B with a tile incarnation base, else
+//                12 B: {bucket-local id, tile-relative index, status; incarnation}) by bucket in
+//                LDS and stores them as one contiguous run at recs + tile * kBkTile (whole
+//                lines); seg[bucket][tile] = the bucket's segment of that run (start << 16 |
+//                length). No global count pass or scan: the fold walks a bucket's segments of
+//                every tile.
 //   k_bk_fold    a workgroup per bucket: reads the bucket's segments once, in order, keeping
-//                per id the change count and the first change (batch index, status,
-//                incarnation) in LDS; then the bucket's ids in id order (rows as whole lines):
-//                a single change folds from LDS, an address's repeated changes are sorted by
-//                batch index in LDS and folded by one lane; an address with more than kSlots + 1
-//                changes (or a bucket whose repeated changes overflow the LDS list) is marked
-//                for the overflow fold (k_fold_ovf / k_ovf_len, as on the grouped path). The
-//                result goes to a 2-bit per-id map res2 (coalesced), or to resj[batch index] for
-//                an address with repeated changes (res2 holds kRes2Rep)
-//   k_bk_gather  applied per change in batch order, from res2[ids[j]] (1 MB, L2-resident),
-//                four changes per lane (the new status / incarnation outputs are copied from the
-//                input by k_bk_scatter; the fold rewrites the local overrides)
+//                per id the first change (batch index, status, incarnation) in LDS and flagging
+//                repeated ids; then the bucket's ids in id order (rows as whole lines): a single
+//                change folds from LDS, an address's repeated changes are sorted by batch index
+//                in LDS and folded by one lane; a bucket whose repeated changes overflow the LDS
+//                list marks them for the overflow fold (k_fold_ovf / k_ovf_len, as on the grouped
+//                path). Applied flags go straight to applied[batch index] (DIRECT), or (A/B) to a
+//                2-bit per-id map res2 / resj[batch index] that
+//   k_bk_gather  turns back into batch order, from res2[ids[j]] (1 MB, L2-resident), four
+//                changes per lane. The new status / incarnation outputs are copied from the
+//                input by k_bk_scatter (unless they alias it); the fold rewrites local overrides.
 #ifndef RP_BK_BITS
 #define RP_BK_BITS 12
 #endif
@@ -484,8 +485,8 @@ __host__ __device__ __forceinline__ uint64_t seg_at(uint32_t b, uint32_t t, uint
     return ((uint64_t)(b >> 4) * ntiles + t) * 16 + (b & 15u);
 }
 
-// A staged change, 12 B: {bucket-local id | tile-relative batch index << kBkBits | status << 30,
-// incarnation lo, hi}. The tile is the run it sits in (the fold knows it from the segment), so
+// A staged change in the wide form, 12 B: {bucket-local id | tile-relative batch index << kBkBits |
+// status << 30, incarnation lo, hi} (the compact form keeps x and the incarnation - tile base). The tile is the run it sits in (the fold knows it from the segment), so
 // the batch index is tile * kBkTile + the relative index: no 16-B record with a full id and index.
 struct BRec {
     uint32_t x;
