@@ -488,3 +488,31 @@ def test_device_long_hash_vs_oracle(gpu, orc, length):
     gpu.check(gpu.lib().rp_hash32_long_dev(d.data_ptr(), length, out.data_ptr(), None))
     torch.cuda.synchronize()
     assert int(out.cpu().numpy().view(np.uint32)[0]) == orc.hash32(bytes(b[:length]))
+
+
+@pytest.mark.parametrize("servers,R,mod", [(1, 1, 0), (2, 3, 0), (3, 50, 0), (5, 7, 97), (17, 20, 0), (40, 100, 65521)])
+def test_lookup_service_direct_table_small_rings(gpu, orc, servers, R, mod):
+    """The service's direct table on small rings (fewer distinct owners than its 16 successor
+    slots: the records carry the complete flag), with and without colliding caller tokens:
+    lookupN(1..8) of 400 hashes each (random, at token values, one past them, 0 and 2^32 - 1)
+    against the oracle."""
+    names = ["s%d:%d" % (i, 3000 + i) for i in range(servers)]
+
+    def hf(s):
+        h = orc.hash32(s)
+        return (h % mod) * 65537 & 0xFFFFFFFF if mod else h
+
+    ring = gpu.HashRing({"replicaPoints": R, "hashFunc": hf})
+    ring.addRemoveServers(names)
+    oracle = orc.Ring(R)
+    toks = [hf(s + str(i)) for s in names for i in range(R)]
+    oracle.add_remove(names, [], toks, None)
+    ring.service(200)
+    rng = random.Random(servers * 1000 + R)
+    hs = [0, 0xFFFFFFFF] + [t for t in toks[:60]] + [(t + 1) & 0xFFFFFFFF for t in toks[:60]]
+    hs += [rng.getrandbits(32) for _ in range(400 - len(hs))]
+    for i, h in enumerate(hs):
+        n = 1 + i % 8
+        g, gc = ring.lookupn_hashes([h], n)
+        assert [ring.name(x) for x in g[0][:gc[0]]] == [oracle.name(x) for x in oracle.lookupn_hash(h, n)], (i, h, n)
+    ring.service(0)
