@@ -764,7 +764,7 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
 #pragma unroll
     for (uint32_t u = 0; u < PI; u++) {  // each lane's rows in flight together
         const uint32_t q = tid + u * kBkFT, v = fjs[q];
-        if (v != kBkNone && !(v & kBkRep)) wv4[u] = *reinterpret_cast<const uint64_t*>(A.rows + id0 + q);
+        if (v != kBkNone) wv4[u] = *reinterpret_cast<const uint64_t*>(A.rows + id0 + q);
     }
 #pragma unroll
     for (uint32_t u = 0; u < PI; u++) {  // ids in order: coalesced rows and results
@@ -786,6 +786,8 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
             if (!listed) {  // the overflow fold takes the address
                 A.cnt[id] = kOvfMark;
                 *ovf = 1u;
+            } else {  // its row, for the repeated fold below (finc of a repeated id is free by now)
+                finc[q] = (int64_t)wv4[u];
             }
         }
         if (!DIRECT) rcode[q] = r == kResRep ? (uint8_t)kRes2Rep : (uint8_t)(r & 3u);
@@ -815,7 +817,7 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
             const uint32_t il = (uint32_t)(dk[q] >> 40);
             if (q > 0 && (uint32_t)(dk[q - 1] >> 40) == il) continue;  // not a segment head
             const uint32_t id = id0 + il;
-            const MRowV row = row_load(A.rows + id);
+            const MRowV row = row_unpack((uint64_t)finc[il]);  // loaded with the bucket's rows
             bool ex = row.exists != 0;
             uint8_t st = row.status;
             int64_t in = row.inc;
