@@ -513,6 +513,7 @@ __device__ __forceinline__ void bk_minmax(int64_t& mn, int64_t& mx) {
     }
 }
 
+template <bool LOOP>
 __global__ __launch_bounds__(kBkST) void k_bk_scatter(const uint32_t* __restrict__ ids, const uint8_t* __restrict__ chs,
                                                     const int64_t* __restrict__ chi, uint32_t k, uint32_t nb,
                                                     uint32_t ntiles, BRec* __restrict__ recs,
@@ -540,12 +541,13 @@ __global__ __launch_bounds__(kBkST) void k_bk_scatter(const uint32_t* __restrict
     // the outputs start as copies; the fold rewrites local overrides. Outputs that alias the
     // inputs (the reference rewrites its update objects in place) need no copy.
     const bool cst = nst && nst != chs, cinc = ninc && ninc != chi;
-    // a workgroup takes tiles blockIdx.x, + gridDim.x, ...: the next tile's inputs are loaded
-    // while this tile's records are stored (round 5; one tile per workgroup when the grid covers
-    // every tile)
+    // LOOP (A/B, RP_BK_SGRID): a workgroup takes tiles blockIdx.x, + gridDim.x, ...: the next
+    // tile's inputs are loaded while this tile's records are stored. The default grid covers every
+    // tile once and is compiled without that loop: the prefetched inputs cost 36 VGPRs (94 against
+    // 58), which left one 1,024-thread tile a CU instead of two (2^22 fold 0.089 -> 0.077 ms, r05an)
     uint32_t t = blockIdx.x;
     if (t < ntiles) load(t);
-    for (; t < ntiles; t += gridDim.x) {
+    for (; t < ntiles; t = LOOP ? t + gridDim.x : ntiles) {
         const uint32_t base = t * kBkTile;
         const uint32_t n = k - base < kBkTile ? k - base : kBkTile;
         for (uint32_t b = tid; b < nb; b += kBkST) h[b] = 0;
@@ -615,7 +617,7 @@ __global__ __launch_bounds__(kBkST) void k_bk_scatter(const uint32_t* __restrict
                 }
             }
         }
-        if (t + gridDim.x < ntiles) load(t + gridDim.x);  // in flight under the stores below
+        if (LOOP && t + gridDim.x < ntiles) load(t + gridDim.x);  // in flight under the stores below
         __syncthreads();
         // the tile's run: n records of 8 or 12 B at recs + tile * kBkTile (16-B stores; the tile's
         // run starts 16-B aligned, and its padded tail is never read)
@@ -1413,8 +1415,12 @@ struct Members {
             const bool rec8 = !(getenv("RP_BK_REC8") && !strcmp(getenv("RP_BK_REC8"), "0"));  // A/B: 0 = 12-B always
             // workgroups of the scatter (A/B: RP_BK_SGRID; 0 or >= ntiles: one tile each)
             const uint32_t sg = (uint32_t)env_pos("RP_BK_SGRID", 0);
-            hipLaunchKernelGGL(k_bk_scatter, dim3(sg && sg < ntiles ? sg : ntiles), dim3(kBkST), 0, s, ids, chs, chi, k,
-                               nb, ntiles, bk_recs.p, bk_seg.p, rec8 ? bk_tb.p : nullptr, nst, ninc);
+            if (sg && sg < ntiles)
+                hipLaunchKernelGGL(k_bk_scatter<true>, dim3(sg), dim3(kBkST), 0, s, ids, chs, chi, k, nb, ntiles,
+                                   bk_recs.p, bk_seg.p, rec8 ? bk_tb.p : nullptr, nst, ninc);
+            else
+                hipLaunchKernelGGL(k_bk_scatter<false>, dim3(ntiles), dim3(kBkST), 0, s, ids, chs, chi, k, nb, ntiles,
+                                   bk_recs.p, bk_seg.p, rec8 ? bk_tb.p : nullptr, nst, ninc);
             const bool direct = !(getenv("RP_BK_DIRECT") && !strcmp(getenv("RP_BK_DIRECT"), "0"));
             if (direct)
                 hipLaunchKernelGGL(k_bk_fold<true>, dim3((nb + 7) / 8 * 8), dim3(kBkFT), 0, s, bk_recs.p, bk_seg.p,
