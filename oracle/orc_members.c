@@ -32,9 +32,13 @@ struct orc_members {
     /* per id */
     uint8_t *exists, *status;
     int64_t *inc;
-    /* members array order (ids) */
+    /* members array order (ids): order[0 .. ord_n) is materialised; the inserts since then are
+       logged (id, position at insert time) and placed by materialise_order, so a bulk fill of
+       millions of members is O(n log n) instead of one memmove per insert */
     uint32_t *order;
-    uint32_t count;
+    uint32_t count, ord_n;
+    uint32_t *pend_id, *pend_pos;
+    uint32_t pend_n;
     /* stash (ring of change batches, flattened) */
     uint32_t *st_id; uint8_t *st_status; int64_t *st_inc; uint32_t *st_batch_end;
     uint32_t st_n, st_cap, st_batches, st_bcap;
@@ -77,6 +81,8 @@ orc_members *orc_members_new(const char *names, const uint32_t *off, uint32_t n,
     m->status = (uint8_t *)calloc(n, 1);
     m->inc = (int64_t *)calloc(n, sizeof(int64_t));
     m->order = (uint32_t *)malloc(sizeof(uint32_t) * (n + 1));
+    m->pend_id = (uint32_t *)malloc(sizeof(uint32_t) * (n + 1));
+    m->pend_pos = (uint32_t *)malloc(sizeof(uint32_t) * (n + 1));
     m->sorted = (uint32_t *)malloc(sizeof(uint32_t) * (n + 1));
     for (uint32_t i = 0; i < n; i++) m->sorted[i] = i;
     g_m = m;
@@ -86,7 +92,7 @@ orc_members *orc_members_new(const char *names, const uint32_t *off, uint32_t n,
 
 void orc_members_free(orc_members *m) {
     if (!m) return;
-    free(m->nb); free(m->noff); free(m->exists); free(m->status); free(m->inc); free(m->order);
+    free(m->nb); free(m->noff); free(m->exists); free(m->status); free(m->inc); free(m->order); free(m->pend_id); free(m->pend_pos);
     free(m->st_id); free(m->st_status); free(m->st_inc); free(m->st_batch_end);
     free(m->sorted); free(m->buf);
     for (int t = 0; t < 256; t++) free(m->tbuf[t]);
@@ -105,13 +111,53 @@ static uint32_t join_position(orc_members *m) {
     return (uint32_t)(((uint64_t)r[0] * m->count) >> 32);
 }
 
+/* members.splice(pos, 0, member) (index.js:286-291), logged; each id is inserted at most once */
 static void insert_member(orc_members *m, uint32_t id, uint8_t st, int64_t inc, uint32_t pos) {
     m->exists[id] = 1;
     m->status[id] = st;
     m->inc[id] = inc;
-    memmove(m->order + pos + 1, m->order + pos, sizeof(uint32_t) * (m->count - pos));
-    m->order[pos] = id;
+    m->pend_id[m->pend_n] = id;
+    m->pend_pos[m->pend_n] = pos;
+    m->pend_n++;
     m->count++;
+}
+
+/* The array the logged splices produce: taken in reverse, a splice at position p owns the p-th
+ * (0-based) slot not owned by a later splice (a Fenwick tree over the final slots finds it); the
+ * materialised members fill the slots left, in their order. */
+static void materialise_order(orc_members *m) {
+    const uint32_t P = m->pend_n, N = m->count;
+    if (P == 0) return;
+    uint32_t *fw = (uint32_t *)calloc(N + 1, sizeof(uint32_t));
+    uint32_t *out = (uint32_t *)malloc(sizeof(uint32_t) * (N + 1));
+    uint8_t *taken = (uint8_t *)calloc(N, 1);
+    for (uint32_t i = 1; i <= N; i++) { /* all slots free: fw = prefix counts of ones */
+        fw[i] += 1;
+        const uint32_t j = i + (i & (0u - i));
+        if (j <= N) fw[j] += fw[i];
+    }
+    uint32_t top = 1;
+    while ((top << 1) <= N) top <<= 1;
+    for (uint32_t q = P; q-- > 0;) {
+        uint32_t want = m->pend_pos[q] + 1, at = 0; /* the want-th free slot (1-based) */
+        for (uint32_t b = top; b; b >>= 1)
+            if (at + b <= N && fw[at + b] < want) {
+                at += b;
+                want -= fw[at];
+            }
+        out[at] = m->pend_id[q]; /* slot at (0-based) */
+        taken[at] = 1;
+        for (uint32_t i = at + 1; i <= N; i += i & (0u - i)) fw[i] -= 1;
+    }
+    uint32_t r = 0;
+    for (uint32_t i = 0; i < N; i++)
+        if (!taken[i]) out[i] = m->order[r++];
+    memcpy(m->order, out, sizeof(uint32_t) * N);
+    m->ord_n = N;
+    m->pend_n = 0;
+    free(fw);
+    free(out);
+    free(taken);
 }
 
 /* Member._isOtherOverride (member.js:171-202) */
@@ -442,7 +488,8 @@ int orc_members_checksum(const orc_members *m, uint32_t *out) {
 
 uint32_t orc_members_count(const orc_members *m) { return m->count; }
 
-void orc_members_order(const orc_members *m, uint32_t *ids_out) {
+void orc_members_order(orc_members *m, uint32_t *ids_out) {
+    materialise_order(m);
     memcpy(ids_out, m->order, sizeof(uint32_t) * m->count);
 }
 

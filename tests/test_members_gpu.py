@@ -340,6 +340,38 @@ def test_bucket_fold_repeats_overflow_and_large_batch(gpu, orc, monkeypatch, app
     assert m.checksum == o.checksum
 
 
+def test_bucket_fold_bench_size(gpu, orc):
+    """The bench's fold_large shape against the oracle: 2^22 members and a batch of 2^22 + 2^16
+    changes (1,040 scatter tiles, so a fold lane walks three tile segments, not two; the 2^16
+    ids past the table's size repeat an address, plus C3's 1 % repeats), in place, as bench.py
+    runs it: applied flags, rewritten status / incarnation and the checksum."""
+    import torch
+
+    S = synth()
+    n, k = 1 << 22, (1 << 22) + (1 << 16)
+    names, st0, inc0 = S.c3_members(n)
+    m = gpu.Membership(whoami=names[0], capacity=n)
+    o = orc.Members(names, local=names[0], join_seed=0)
+    ids0 = np.asarray(m.intern(names), dtype=np.uint32)
+    m.update_ids(ids0, st0, inc0, now_ms=1)
+    o.update_ids(ids0, st0, inc0, False, 1)
+    ids, us, ui = S.c3_updates(n, k, seed=47, base_inc=inc0)
+    now = 1434500000013
+    oa, os_, oi, ona = o.update_ids(ids, us, ui, False, now)
+    d_ids = torch.from_numpy(ids.view(np.int32)).cuda()
+    d_st = torch.from_numpy(us.copy()).cuda()
+    d_inc = torch.from_numpy(ui.copy()).cuda()
+    d_app = torch.empty(k, dtype=torch.uint8, device="cuda")
+    d_na = torch.zeros(1, dtype=torch.int32, device="cuda")
+    m.update_dev(d_ids.data_ptr(), d_st.data_ptr(), d_inc.data_ptr(), k, now, d_app.data_ptr(), d_st.data_ptr(),
+                 d_inc.data_ptr(), d_na.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert int(d_na.item()) == ona
+    assert np.array_equal(d_app.cpu().numpy() > 0, oa > 0)
+    assert np.array_equal(d_st.cpu().numpy(), os_) and np.array_equal(d_inc.cpu().numpy(), oi)
+    assert m.checksum == o.checksum
+
+
 @pytest.mark.parametrize("records", ["auto", "wide"])
 def test_bucket_fold_wide_tiles_and_in_place_outputs(gpu, orc, monkeypatch, records):
     """The bucket fold's record formats (round 5) and outputs that alias the inputs, against the
