@@ -411,10 +411,11 @@ __global__ __launch_bounds__(1024) void k_fold_ovf(const uint32_t* __restrict__ 
                                                    uint32_t* __restrict__ out) {
     __shared__ uint32_t s_on, s_w[16];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    uint32_t v = 0;  // the counts are loaded beside the gate word (the overflow fold leaves part alone)
+    for (uint32_t b = tid; b < nparts; b += 1024) v += part[b];
     if (tid == 0) s_on = *ovf;
     __syncthreads();
-    uint32_t v = s_on ? ovf_fold<1024>(ids, k, A) : 0u;
-    for (uint32_t b = tid; b < nparts; b += 1024) v += part[b];
+    if (s_on) v += ovf_fold<1024>(ids, k, A);
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
     if (lane == 0) s_w[wv] = v;
