@@ -26,6 +26,8 @@ EXPECT = {
     "k_bk_foldILb1E": 3,
     # the C2 lookupN(3) kernel: 4 workgroups (16 waves) a CU
     "k_lookupn_leanILi8ELi3ELi4ELb0ELi0ELi1E": 4,
+    # the C5 refresh: two 4-wave workgroups a CU, two chain waves a SIMD
+    "10k_ck_lanesE": 2,
 }
 # (every kernel named here carries __launch_bounds__ equal to its launch size, so the metadata's
 # .max_flat_workgroup_size is the workgroup the launcher uses)
