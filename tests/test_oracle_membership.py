@@ -50,3 +50,33 @@ def test_membership_oracle_matches_reference(orc, case_name):
                 assert [[a, m.member(a)["status"], m.member(a)["incarnationNumber"]] for a in m.order()] == want
             if isinstance(op.get("checksumString"), str):
                 assert m.checksum_string() == op["checksumString"]
+
+
+def test_member_order_independent_of_read_schedule(orc):
+    """The oracle places joined members lazily (a log of splice positions resolved by a Fenwick
+    tree when the order is read, round 5): the members array must come out the same whether it
+    is read after every batch or once at the end, over batches that mix new members (random join
+    positions) and existing ones."""
+    import numpy as np
+
+    rng = np.random.default_rng(3)
+    n = 5000
+    names = ["10.1.%d.%d:3000" % (i >> 8, i & 255) for i in range(n)]
+    a = orc.Members(names, local=names[0], join_seed=11)
+    b = orc.Members(names, local=names[0], join_seed=11)
+    orders = []
+    for step in range(40):
+        k = int(rng.integers(1, 400))
+        ids = rng.integers(0, n if step > 5 else n // 4, k).astype(np.uint32)
+        st = rng.integers(0, 4, k).astype(np.uint8)
+        inc = rng.integers(1, 50, k).astype(np.int64)
+        ra = a.update_ids(ids, st, inc, False, 1000 + step)
+        rb = b.update_ids(ids, st, inc, False, 1000 + step)
+        assert ra[3] == rb[3]
+        orders.append(a.order())
+    assert b.order() == orders[-1]
+    assert len(set(orders[-1])) == len(orders[-1]) == a.count()
+    # every read is a prefix-consistent snapshot: members keep their relative order as others join
+    for o1, o2 in zip(orders, orders[1:]):
+        pos = {x: i for i, x in enumerate(o2)}
+        assert all(pos[x] < pos[y] for x, y in zip(o1, o1[1:]))
