@@ -756,6 +756,16 @@ __device__ unsigned long long g_lk_prof[10];
 // registers first (PER x u32x4 held), then the slices go through LDS one after another. 1: the
 // slices are DMA'd global -> LDS (global_load_lds_dwordx4, no VGPR destination) into a ring of
 // two slice buffers, slice s + 2 issued as soon as slice s is hashed (A/B: RP_LOOKUP_STG=1).
+// The lean kernel's timing ablations (RP_LOOKUP_ABLATE, round 5) exist only in a diagnostics
+// build (-DRP_LK_ABLATE, tools/build_prof.sh). Read at run time (as from r05a to r05au), their
+// uniform branches around the index and window loads split the loads' clusters: 3,394
+// instructions and 181 branches against 3,191 and 139, 0.926 against 0.886 ms per 2^26-key step
+// on one box, below round 4's kernel (0.903; profiles/r05/r05aw/).
+#ifdef RP_LK_ABLATE
+#define RP_LKA(cv) ((cv).ablate)
+#else
+#define RP_LKA(cv) 0u
+#endif
 template <int KPL, int NEED, int HS = 1, bool FUSE = false, int STG = 0, int LH = 1>
 __global__ __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_lookupn_lean(const uint8_t* __restrict__ keys, uint64_t ntiles,
                                                              CompactView cv, uint32_t* __restrict__ out,
@@ -788,7 +798,7 @@ __global__ __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(4)))
     const __amdgpu_buffer_rsrc_t ent_r =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(cv.ent), 0, (int)cv.ent_bytes, 0x00020000);
     // lookupN(3) reads the hinted index when the ring has one (round 5; RP_LOOKUP_HINT=0: A/B)
-    const bool hinted = NEED == 3 && cv.idxh != nullptr && !(cv.ablate & 4u);
+    const bool hinted = NEED == 3 && cv.idxh != nullptr && !(RP_LKA(cv) & 4u);
     const __amdgpu_buffer_rsrc_t idx_r = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint32_t*>(hinted ? cv.idxh : cv.idx), 0, (int)cv.idx_bytes, 0x00020000);
     auto load16 = [&](uint32_t pos) {
@@ -969,7 +979,7 @@ __global__ __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(4)))
 #pragma unroll
         for (int kq = 0; kq < KH; kq++) {
             const int k = hh * KH + kq;
-            if (cv.ablate & 4u)  // diagnostics: no index trip (a record made from the hash)
+            if (RP_LKA(cv) & 4u)  // diagnostics: no index trip (a record made from the hash)
                 rec[kq] = u32x2{(uint32_t)(((uint64_t)h[k] * (cv.M - 32u)) >> 32), h[k] & 0x11111111u};
             else
                 rec[kq] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(idx_r, (int)((h[k] >> (bsh + 3u)) * 8u), 0, 0));
@@ -991,13 +1001,13 @@ __global__ __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(4)))
                                                     __builtin_amdgcn_sad_u8((below >> 4) & 0x0F0F0F0Fu, 0u, 0u));
             bc[kq] = (rec[kq].y >> s4) & 15u;
             ws[kq] = wstart(h[k], bc[kq], hint);
-            if (cv.ablate & 26u) {  // diagnostics: 2 = windows rounded down to 16 B (no line crossing);
+            if (RP_LKA(cv) & 26u) {  // diagnostics: 2 = windows rounded down to 16 B (no line crossing);
                                     // 8 = no window trip (entries made from the record); 16 = windows
                                     // rounded down to 4 B (dword-aligned, still crossing lines)
                 const uint32_t pos = lo[kq] + ws[kq];
-                win[kq] = (cv.ablate & 8u) ? u32x4{rec[kq].x, rec[kq].y, h[k], pos}
+                win[kq] = (RP_LKA(cv) & 8u) ? u32x4{rec[kq].x, rec[kq].y, h[k], pos}
                                            : __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                                          ent_r, (int)((3u * pos) & ((cv.ablate & 2u) ? ~15u : ~3u)), 0, 0));
+                                                                          ent_r, (int)((3u * pos) & ((RP_LKA(cv) & 2u) ? ~15u : ~3u)), 0, 0));
             } else {
                 win[kq] = load16(lo[kq] + ws[kq]);
             }
@@ -1039,7 +1049,7 @@ __global__ __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(4)))
             const uint32_t kk = tid + k * kLkThreads;
             bool slow = (tie && !cv.exact) | (lo[kq] + 20u > cv.M);
             const bool under = w > 0u && lt == 0u;  // the key lies before window 1's first entry
-            const bool again = !slow && (lt > SPAN || dup || under) && !(cv.ablate & 1u);  // 1: diagnostics
+            const bool again = !slow && (lt > SPAN || dup || under) && !(RP_LKA(cv) & 1u);  // 1: diagnostics
             const uint64_t m = __ballot(again);
             const uint32_t pos = nag + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             nag += (uint32_t)__popcll(m);

@@ -3,6 +3,7 @@
 # RP_AMD_LIB=<path>.
 #   tools/build_prof.sh              -> librpamd_prof.so   (-DRP_CK_PROF: checksum chain epochs)
 #   DEFS=-DRP_LK_PROF OUT=librpamd_lkprof.so tools/build_prof.sh   (lean lookup phases)
+#   DEFS=-DRP_LK_ABLATE OUT=librpamd_lkabl.so tools/build_prof.sh (RP_LOOKUP_ABLATE timing ablations)
 set -e
 cd "$(dirname "$0")/../ringpop-node_amd/csrc"
 DEFS=${DEFS:--DRP_CK_PROF}
