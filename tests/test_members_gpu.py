@@ -372,12 +372,13 @@ def test_bucket_fold_bench_size(gpu, orc):
     assert m.checksum == o.checksum
 
 
-@pytest.mark.parametrize("records", ["auto", "wide"])
+@pytest.mark.parametrize("records", ["auto", "wide", "looped"])
 def test_bucket_fold_wide_tiles_and_in_place_outputs(gpu, orc, monkeypatch, records):
     """The bucket fold's record formats (round 5) and outputs that alias the inputs, against the
     oracle. A 2^19-change batch over 2^19 members (128 scatter tiles): tiles 1 and 5 hold
     incarnations spanning more than 2^32 (12-B records there, 8-B records with a tile base
-    elsewhere; records "wide": RP_BK_REC8=0, 12-B records everywhere), and the local member has
+    elsewhere; records "wide": RP_BK_REC8=0, 12-B records everywhere; "looped": the scatter's
+    A/B instance whose workgroups loop over tiles), and the local member has
     suspect / faulty changes that the local override rewrites. The status and incarnation
     outputs are the input arrays themselves, as the reference rewrites its update objects in
     place (member.js evaluateUpdate): after the call they must hold the oracle's outputs."""
@@ -385,6 +386,8 @@ def test_bucket_fold_wide_tiles_and_in_place_outputs(gpu, orc, monkeypatch, reco
 
     if records == "wide":
         monkeypatch.setenv("RP_BK_REC8", "0")
+    if records == "looped":  # the scatter's tile-loop instance (RP_BK_SGRID: 48 workgroups over 128 tiles)
+        monkeypatch.setenv("RP_BK_SGRID", "48")
     S = synth()
     n = 1 << 19
     names, st0, inc0 = S.c3_members(n)
