@@ -390,7 +390,11 @@ int rp_sim_stats(rp_sim *s, uint64_t *out4);
  * its 24-byte records); before stage k + 1 the caller fills the inbox (rp_sim_inbox sizes it for
  * the per-source counts and returns its device buffer) with every source's segment for this
  * shard, in source-shard order — one all-to-all-v moves the bytes as they lie. The buffers are
- * owned by the handle and valid until its next stage. rp_sim_exchange_local does the
+ * owned by the handle and valid until its next stage. Neither call waits for the device (round
+ * 6): the counts are on the host when rp_sim_stage returns, but the outbox bytes are written, and
+ * the inbox is still read by the previous stage, on the handle's stream. Before reading the
+ * outbox or writing the inbox the caller orders itself after that stream with
+ * rp_sim_order_stream (a device stream waits on the device; NULL: the host waits). rp_sim_exchange_local does the
  * exchange for handles of one process; across processes the host moves the bytes (RCCL
  * all-to-all-v; ringpop-node_amd DistGossipSim). Checksums / views / stats are per shard
  * (checksums: the shard's nodes in id order); convergence reduces rp_sim_converged_local
@@ -406,6 +410,9 @@ int rp_sim_inbox(rp_sim *s, const uint64_t *nmsg, const uint64_t *nrec, void **b
  * `stream`: a caller that moved the inbox bytes with a collective on its own stream (RCCL on
  * torch's stream) orders the import after it this way. */
 int rp_sim_wait_stream(rp_sim *s, void *stream);
+/* The converse: `stream` waits (on the device) for the work queued so far on the handle's stream;
+ * stream NULL: the host waits for it. */
+int rp_sim_order_stream(rp_sim *s, void *stream);
 int rp_sim_exchange_local(rp_sim *const *shards, uint32_t nshards);
 int rp_sim_converged_local(rp_sim *s, uint32_t *out4);
 /* JOIN events on a sharded simulator (a joiner reads its responders' views, which other shards

@@ -106,6 +106,7 @@ SIGNATURES = {
     "rp_sim_inbox": (_INT, [_P, _P, _P, _P]),
     "rp_sim_exchange_local": (_INT, [_P, _U32]),
     "rp_sim_wait_stream": (_INT, [_P, _P]),
+    "rp_sim_order_stream": (_INT, [_P, _P]),
     "rp_sim_join_export": (_INT, [_P, _P, _P, _P]),
     "rp_sim_join_import": (_INT, [_P]),
     "rp_sim_join_exchange_local": (_INT, [_P, _U32]),
@@ -1095,7 +1096,7 @@ class MessageExchange:
     the inbox in HBM directly, over xGMI, with no staging copies. With gloo the bytes go through
     one host buffer each way (`copy(dst, src, nbytes)` moves them; tests)."""
 
-    def __init__(self, group=None, device=None, copy=None):
+    def __init__(self, group=None, device=None, copy=None, side_counts=None):
         import torch
         import torch.distributed as dist
         self.torch, self.dist, self.group = torch, dist, group
@@ -1108,25 +1109,50 @@ class MessageExchange:
         self._copy = copy
         # the per-peer counts are host integers already (the outbox read), and all_to_all_single
         # takes its split sizes as host integers: with nccl they cross ranks over a gloo group of
-        # the same ranks (no device collective, no device -> host read, round 5)
-        if self.on_device:
-            ranks = list(range(self.G)) if group is None else dist.get_process_group_ranks(group)
-            # one node (bench.py, tests): gloo over loopback, whatever the hostname resolves to
-            os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
-            try:
-                self._cgroup = dist.new_group(ranks=ranks, backend="gloo")
-            except Exception:  # no gloo here: the counts go over the nccl group (a device read)
-                self._cgroup = None
-        else:
-            self._cgroup = group
+        # the same ranks (no device collective, no device -> host read, round 5). side_counts
+        # forces that side group on (gloo tests) or off. Every rank of `group` must construct the
+        # exchange (the side group is built with local synchronization: ranks outside `group`
+        # take no part).
+        self._cgroup = None
+        if self.on_device if side_counts is None else side_counts:
+            self._cgroup = self._side_count_group()
         self._cdev = self.on_device and self._cgroup is None
         cdev = self.device if self._cdev else "cpu"
-        if self._cdev:
+        if self._cgroup is None:
             self._cgroup = group
         self._cnt = torch.zeros(2 * self.G, dtype=torch.int64, device=cdev)
         self._rcnt = torch.zeros(2 * self.G, dtype=torch.int64, device=cdev)
         self._host = {}  # gloo staging buffers, kept across rounds
         self._events = []  # (start, end) of every byte collective queued on the device
+
+    def _side_count_group(self):
+        """A gloo group of this exchange's ranks for the per-peer counts, or None when any rank
+        could not build one (every rank then counts over the main group: the choice is agreed
+        by an all-reduce, so no two ranks ever use different count groups). Loopback is used
+        only when every rank runs on this host (an all-gather of the host names' hashes), and
+        only for the side group's creation: the process environment is restored."""
+        import socket
+        import zlib
+        torch, dist, group = self.torch, self.dist, self.group
+        ranks = list(range(self.G)) if group is None else dist.get_process_group_ranks(group)
+        dev = self.device if self.on_device else "cpu"
+        h = torch.tensor([zlib.crc32(socket.gethostname().encode())], dtype=torch.int64, device=dev)
+        hs = [torch.empty_like(h) for _ in range(self.G)]
+        dist.all_gather(hs, h, group=group)
+        loopback = len({int(x.item()) for x in hs}) == 1 and "GLOO_SOCKET_IFNAME" not in os.environ
+        cg = None
+        try:
+            if loopback:
+                os.environ["GLOO_SOCKET_IFNAME"] = "lo"
+            cg = dist.new_group(ranks=ranks, backend="gloo", use_local_synchronization=True)
+        except Exception:  # no gloo here
+            cg = None
+        finally:
+            if loopback:
+                os.environ.pop("GLOO_SOCKET_IFNAME", None)
+        ok = torch.tensor([0 if cg is None else 1], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+        return cg if int(ok.item()) == 1 else None
 
     def device_ms(self):
         """Device time of the byte collectives queued since the last call (nccl; 0 with gloo)."""
@@ -1152,12 +1178,15 @@ class MessageExchange:
             self._host[key] = t
         return t
 
-    def exchange(self, out_nmsg, out_nrec, out_buf, alloc_in, after=None):
+    def exchange(self, out_nmsg, out_nrec, out_buf, alloc_in, after=None, before=None):
         """out_*: this rank's outbox (counts per destination, its packed buffer's address).
         alloc_in(in_nmsg, in_nrec) -> the inbox's address, which receives every source's segment
         for this rank in source order. after(stream): with the nccl backend, called with torch's
         stream once the byte collective is queued on it, so the consumer orders its next work
         after it on the device (rp_sim_wait_stream); without it the host waits for the stream.
+        before(stream): called once the inbox is sized, before the bytes move, with torch's stream
+        (nccl) or None (gloo: the host is about to read the outbox), so that the reader waits for
+        the producer's outbox fill and its last reads of the inbox (rp_sim_order_stream).
         The per-peer counts are host integers (torch's all_to_all_single takes its split sizes
         as host integers, and the inbox is sized from them); they cross ranks on the host (a gloo
         group beside the nccl one), so the exchange itself never waits for the device."""
@@ -1170,6 +1199,8 @@ class MessageExchange:
         seg_in = [int(in_nmsg[g]) * MSG_BYTES + int(in_nrec[g]) * REC_BYTES for g in range(G)]
         tot_out, tot_in = sum(seg_out), sum(seg_in)
         in_buf = alloc_in(in_nmsg, in_nrec)
+        if before is not None:
+            before(torch.cuda.current_stream().cuda_stream if self.on_device else None)
         if self.on_device:
             send = torch.as_tensor(_DeviceBytes(out_buf, tot_out), device=self.device) if tot_out else \
                 torch.empty(0, dtype=torch.uint8, device=self.device)
@@ -1238,6 +1269,7 @@ class DistGossipSim:
         import time
         sh = self.shard
         wait = lambda stream: check(lib().rp_sim_wait_stream(sh._h, stream))  # noqa: E731
+        order = lambda stream: check(lib().rp_sim_order_stream(sh._h, stream))  # noqa: E731
         for _ in range(rounds):
             while True:  # the round's joins: every rank exports, the buffers are summed, then import
                 has, buf, nb = sh.join_export()
@@ -1253,7 +1285,7 @@ class DistGossipSim:
                     nm, nr, buf = sh.outbox()
                     self.exchange_bytes += int(nm.sum()) * MSG_BYTES + int(nr.sum()) * REC_BYTES
                     t = time.perf_counter()
-                    self.xchg.exchange(nm, nr, buf, sh.inbox, after=wait)
+                    self.xchg.exchange(nm, nr, buf, sh.inbox, after=wait, before=order)
                     self.exchange_s += time.perf_counter() - t
 
     @property

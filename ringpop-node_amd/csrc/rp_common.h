@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <atomic>
 #include <stdexcept>
 #include <string>
 
@@ -40,9 +41,33 @@ enum : int {
         if (!(cond)) throw ::rp::Error(::rp::RP_EINVAL, (msg));                               \
     } while (0)
 
-// Run a C-ABI body; convert exceptions into an int status + rp_last_error().
+// Resident lookup services (rp_ring_service, rp_ring.hip) against every other device call.
+// While a service wave is resident, hipFree (a buffer growing or released) synchronizes the
+// device and waits for it, and the service's stream may share a hardware queue with any other
+// stream of the process (GPU_MAX_HW_QUEUES). So every C-ABI call that may touch the device holds
+// a QuietScope: it stops every resident service before its body runs, and a service lookup that
+// arrives meanwhile (another thread) takes the launch path instead of starting a wave, until the
+// scope ends. The pair of counters is a Dekker handshake: a scope raises g_quiet, then reads
+// g_svc_live; a service raises g_svc_live, then reads g_quiet (both sequentially consistent), so
+// at least one of them sees the other.
+extern std::atomic<int> g_quiet;     // QuietScopes open in the process
+extern std::atomic<int> g_svc_live;  // services launched and not yet stopped
+void svc_quiesce(const void* keep);  // stop every resident service but `keep`'s ring's
+
+struct QuietScope {
+    QuietScope() {
+        g_quiet.fetch_add(1);
+        if (g_svc_live.load() > 0) svc_quiesce(nullptr);
+    }
+    ~QuietScope() { g_quiet.fetch_sub(1); }
+    QuietScope(const QuietScope&) = delete;
+    QuietScope& operator=(const QuietScope&) = delete;
+};
+
+// Run a C-ABI body; convert exceptions into an int status + rp_last_error(). guard_host is for
+// entry points that touch no device state (or, the ring's lookups, manage the service themselves).
 template <class F>
-int guard(F&& f) {
+int guard_host(F&& f) {
     try {
         f();
         return RP_OK;
@@ -56,6 +81,14 @@ int guard(F&& f) {
         set_error(e.what());
         return RP_EINVAL;
     }
+}
+
+template <class F>
+int guard(F&& f) {
+    return guard_host([&] {
+        QuietScope quiet;
+        f();
+    });
 }
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }

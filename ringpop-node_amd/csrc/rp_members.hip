@@ -59,11 +59,11 @@ __host__ __device__ __forceinline__ uint64_t row_pack(int64_t inc, uint8_t statu
     return ((uint64_t)inc << 3) | ((uint64_t)(exists ? 1u : 0u) << 2) | (uint64_t)(status & 3u);
 }
 __device__ __forceinline__ MRowV row_load(const MRow* p) { return row_unpack(*reinterpret_cast<const uint64_t*>(p)); }
-// err (nullable): kErrRange when the incarnation does not fit the row (the row then holds garbage;
-// the call reports RP_EDEVICE at the handle's next sync)
+// err (nullable): kErrRange when the incarnation or the status does not fit the row (the row then
+// holds garbage; the call reports RP_EDEVICE at the handle's next sync)
 __device__ __forceinline__ void row_store(MRow* p, int64_t inc, uint8_t status, uint8_t exists,
                                           uint32_t* err = nullptr) {
-    if (err && (inc > kMemberIncMax || inc < kMemberIncMin)) atomicOr(err, kErrRange);
+    if (err && (inc > kMemberIncMax || inc < kMemberIncMin || status > 3u)) atomicOr(err, kErrRange);
     *reinterpret_cast<uint64_t*>(p) = row_pack(inc, status, exists);
 }
 
@@ -111,6 +111,7 @@ __device__ __forceinline__ uint32_t fold_address(const FoldArgs& A, uint32_t id,
         const uint32_t j = change(q);
         uint8_t us = A.ch_status[j];
         int64_t ui = A.ch_inc[j];
+        if (us > 3u && A.err) atomicOr(A.err, kErrRange);  // a status past leave (no rule takes it)
         uint8_t a;
         bool exc = false;
         if (!ex) {  // _createMember verbatim (index.js:277-291): a fresh Member (member.js:28-41)
@@ -519,7 +520,8 @@ __global__ __launch_bounds__(kBkST) void k_bk_scatter(const uint32_t* __restrict
                                                     const int64_t* __restrict__ chi, uint32_t k, uint32_t nb,
                                                     uint32_t ntiles, BRec* __restrict__ recs,
                                                     uint32_t* __restrict__ seg, int64_t* __restrict__ tb,
-                                                    uint8_t* __restrict__ nst, int64_t* __restrict__ ninc) {
+                                                    uint8_t* __restrict__ nst, int64_t* __restrict__ ninc,
+                                                    uint32_t* __restrict__ err) {
     __shared__ __attribute__((aligned(16))) uint32_t stage[kBkTile * 3];
     __shared__ uint32_t h[kBkMaxBuckets], s_w[kBkST / 64];
     __shared__ int64_t s_mn[kBkST / 64], s_mx[kBkST / 64];
@@ -553,14 +555,17 @@ __global__ __launch_bounds__(kBkST) void k_bk_scatter(const uint32_t* __restrict
         const uint32_t n = k - base < kBkTile ? k - base : kBkTile;
         for (uint32_t b = tid; b < nb; b += kBkST) h[b] = 0;
         __syncthreads();
+        bool bad = false;  // a status past leave: the record keeps 2 bits (row_store's kErrRange)
 #pragma unroll
         for (uint32_t q = 0; q < PER; q++) {
             const uint32_t i = tid + q * kBkST;
             if (i < n) {
                 if (cst) nst[base + i] = stv[q];
                 if (cinc) ninc[base + i] = incv[q];
+                bad |= stv[q] > 3u;
             }
         }
+        if (bad) atomicOr(err, kErrRange);
         int64_t mn = INT64_MAX, mx = INT64_MIN;
 #pragma unroll
         for (uint32_t q = 0; q < PER; q++)
@@ -931,14 +936,14 @@ __global__ void k_flag_nonzero(const uint32_t* __restrict__ mark, uint32_t k, ui
 __global__ void k_set_apply(const uint32_t* __restrict__ mark, const uint32_t* __restrict__ pos, uint32_t k,
                             const uint32_t* __restrict__ ids, const uint8_t* __restrict__ chs,
                             const int64_t* __restrict__ chi, MRow* __restrict__ rows, uint32_t* __restrict__ pick,
-                            uint32_t* __restrict__ npick, DampArgs da) {
+                            uint32_t* __restrict__ npick, DampArgs da, uint32_t* __restrict__ err) {
     const uint32_t gstride = gridDim.x * blockDim.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < k; i += gstride) {
         if (i == 0 && npick) *npick = pos[k];
         const uint32_t m = mark[i];
         if (!m) continue;
         const uint32_t j = m - 1u, id = ids[j];
-        row_store(rows + id, chi[j], chs[j], 1);
+        row_store(rows + id, chi[j], chs[j], 1, err);
         if (da.score) {
             da.score[id] = da.last[id] = da.c.initial;
             da.ts[id] = 0;
@@ -1418,10 +1423,10 @@ struct Members {
             const uint32_t sg = (uint32_t)env_pos("RP_BK_SGRID", 0);
             if (sg && sg < ntiles)
                 hipLaunchKernelGGL(k_bk_scatter<true>, dim3(sg), dim3(kBkST), 0, s, ids, chs, chi, k, nb, ntiles,
-                                   bk_recs.p, bk_seg.p, rec8 ? bk_tb.p : nullptr, nst, ninc);
+                                   bk_recs.p, bk_seg.p, rec8 ? bk_tb.p : nullptr, nst, ninc, ws.err.p);
             else
                 hipLaunchKernelGGL(k_bk_scatter<false>, dim3(ntiles), dim3(kBkST), 0, s, ids, chs, chi, k, nb, ntiles,
-                                   bk_recs.p, bk_seg.p, rec8 ? bk_tb.p : nullptr, nst, ninc);
+                                   bk_recs.p, bk_seg.p, rec8 ? bk_tb.p : nullptr, nst, ninc, ws.err.p);
             const bool direct = !(getenv("RP_BK_DIRECT") && !strcmp(getenv("RP_BK_DIRECT"), "0"));
             if (direct)
                 hipLaunchKernelGGL(k_bk_fold<true>, dim3((nb + 7) / 8 * 8), dim3(kBkFT), 0, s, bk_recs.p, bk_seg.p,
@@ -1495,6 +1500,10 @@ struct Members {
             if (npick) RP_HIP(hipMemsetAsync(npick, 0, sizeof(uint32_t), s));
             return;
         }
+        if (!ws.err.p) {
+            ws.err.reserve(1);
+            RP_HIP(hipMemsetAsync(ws.err.p, 0, sizeof(uint32_t), s));
+        }
         sk.reserve(k);
         sv.reserve(k);
         mk.reserve(k);
@@ -1507,7 +1516,7 @@ struct Members {
         hipLaunchKernelGGL(k_flag_nonzero, dim3(grid_for(k, 256)), dim3(256), 0, s, mk.p, k, mpos.p);
         scan_exclusive_u32(mpos.p, mpos.p, k, s, ws);
         hipLaunchKernelGGL(k_set_apply, dim3(grid_for(k, 256)), dim3(256), 0, s, mk.p, mpos.p, k, ids, chs, chi,
-                           rows.p, pick, npick, damp_args(false));
+                           rows.p, pick, npick, damp_args(false), ws.err.p);
         RP_HIP(hipGetLastError());
         checksum_dev(s, nullptr);
     }

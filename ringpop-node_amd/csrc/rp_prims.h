@@ -50,7 +50,7 @@ struct Scratch {
     }
 };
 
-constexpr uint32_t kErrSpin = 1u, kErrTicket = 2u, kErrRange = 4u;  // kErrRange: a member incarnation past +-2^60
+constexpr uint32_t kErrSpin = 1u, kErrTicket = 2u, kErrRange = 4u;  // kErrRange: a member incarnation past +-2^60 or status > 3
 
 // Throws (RP_EDEVICE) if a single-pass launch on this scratch reported a broken ordering since
 // the last check; synchronizes `st`.

@@ -478,7 +478,8 @@ void scratch_check(Scratch& ws, hipStream_t st) {
         RP_HIP(hipMemsetAsync(ws.err.p, 0, sizeof(uint32_t), st));
         RP_HIP(hipStreamSynchronize(st));
         if (e & kErrRange)
-            throw Error(RP_EDEVICE, "a member incarnation outside [-2^60, 2^60) reached the member table: results "
+            throw Error(RP_EDEVICE, "a member incarnation outside [-2^60, 2^60) or a status past leave (3) reached the "
+                                    "member table: results "
                                     "of the last calls on this handle are not valid");
         throw Error(RP_EDEVICE, std::string("device primitive reported a broken ordering (") +
                                     (e & kErrSpin ? "look-back wait gave up" : "") +

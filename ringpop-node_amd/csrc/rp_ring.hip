@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -1130,6 +1131,154 @@ __global__ __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(4)))
     }
 }
 
+// ---- The LDS-index kernel (round 6). The lean kernel above takes two dependent L2 trips per key
+// (the index record, then the window); its ablations price the index trip at 0.21 of 0.93 ms, and
+// the access-pattern microbenchmark (profiles/r01c/ub_access_patterns.txt) puts one random 16-B
+// load per key from a 3 MB table at 0.62 ms against 0.80 for two dependent ones. Here the index
+// lives in LDS: one 768-thread workgroup per CU loads the NG group records (<= 128 KB, k_lidx_build)
+// once, and each wave then streams its own tiles of 64 x KPL keys: 16-B non-temporal key loads,
+// transposed through the wave's 2.3-KB LDS slice (one key per lane per slice) and hashed; the
+// group record from LDS gives the bucket's first position and token count; the window is 10
+// entries (32 B, two 16-B loads) from max(0, floor(u c) - 3) into the bucket (u: the key's place in
+// the bucket's hash range), which holds the key's position and its NEED owners for all but ~0.6 %
+// of C2 keys (a fingerprint tie: 0.43 %; a window that misses; a long bucket; the ring end). Those
+// are deferred to k_lookupn_fix_tiles (the exact tokens) through the per-tile lists, as in the
+// compact kernels.
+struct LdsView {
+    const uint8_t* ent;  // 3 B per token (k_lpack3), M + kEnt3Pad + 6 entries (+16 B)
+    const uint4* idx;    // ng group records (k_lidx_build)
+    uint32_t M, ng, lg, fb, ob;
+    uint32_t ent_bytes;
+};
+constexpr bool kLdsDefault = false;      // RP_LOOKUP_LDS=1 selects it (A/B)
+constexpr int kLdsThreads = 768;          // 12 waves: one workgroup a CU (the index takes up to 128 KB)
+constexpr uint32_t kLdsMaxGroups = 8192;  // 128 KB of group records
+
+template <int KPL, int NEED>
+__global__ __launch_bounds__(kLdsThreads) __attribute__((amdgpu_waves_per_eu(3))) void k_lookupn_lds(
+    const uint8_t* __restrict__ keys, uint64_t nwt, LdsView lv, uint32_t* __restrict__ out,
+    uint8_t* __restrict__ counts, uint32_t* __restrict__ slow_list, uint32_t* __restrict__ slow_cnt) {
+    constexpr int LEN = 36, W4 = LEN / 4, NWV = kLdsThreads / 64;
+    constexpr int TK = 64 * KPL;       // keys per wave-tile
+    constexpr int V4 = TK * W4 / 4;    // 16-B key vectors per wave-tile
+    constexpr int PER = V4 / 64;       // per lane
+    constexpr int SV = 64 * W4 / 4;    // vectors per slice of 64 keys
+    static_assert(V4 % 64 == 0 && NEED >= 1 && NEED <= 4, "tile shape");
+    __shared__ uint4 s_idx[kLdsMaxGroups];
+    __shared__ __attribute__((aligned(16))) uint32_t s_key[NWV][64 * W4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (uint32_t i = tid; i < lv.ng; i += kLdsThreads) s_idx[i] = lv.idx[i];
+    __syncthreads();
+    const uint32_t omask = (1u << lv.ob) - 1u, obit = 1u << lv.ob, lg = lv.lg, gsh = 32u - lv.lg;
+    const uint32_t fsh = 32u - lv.fb;
+    const __amdgpu_buffer_rsrc_t ent_r =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(lv.ent), 0, (int)lv.ent_bytes, 0x00020000);
+    uint32_t* const sk = s_key[wv];
+    const uint64_t nwaves = (uint64_t)gridDim.x * NWV;
+    auto nsum = [](uint32_t w, uint32_t acc) {  // the sum of w's eight nibbles, plus acc
+        return __builtin_amdgcn_sad_u8(w & 0x0F0F0F0Fu, 0u, __builtin_amdgcn_sad_u8((w >> 4) & 0x0F0F0F0Fu, 0u, acc));
+    };
+    for (uint64_t wt = (uint64_t)blockIdx.x * NWV + wv; wt < nwt; wt += nwaves) {
+        const uint64_t base = wt * TK;
+        const u32x4* s4 = reinterpret_cast<const u32x4*>(keys + base * LEN);
+        u32x4 pre[PER];
+#pragma unroll
+        for (int q = 0; q < PER; q++) pre[q] = __builtin_nontemporal_load(s4 + lane + 64 * q);
+        uint32_t h[KPL];
+#pragma unroll
+        for (int k = 0; k < KPL; k++) {  // slice k: keys k * 64 + lane, one per lane
+#pragma unroll
+            for (int q = 0; q < PER; q++) {
+                const int v = (int)lane + 64 * q;
+                if (v >= SV * k && v < SV * (k + 1)) reinterpret_cast<u32x4*>(sk)[v - SV * k] = pre[q];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            uint32_t w[W4];
+#pragma unroll
+            for (int j = 0; j < W4; j++) w[j] = sk[lane * W4 + j];
+            h[k] = fh::hash32_words<LEN>(w);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        }
+        // the group records (LDS), every key's window start, both window loads in flight
+        uint32_t w0[KPL], bc[KPL], sw[KPL], K[KPL];
+        u32x4 wa[KPL], wb[KPL];
+#pragma unroll
+        for (int k = 0; k < KPL; k++) {
+            const uint32_t x = h[k] << lg;
+            const uint64_t t = (uint64_t)x * 28u;
+            const uint32_t j = (uint32_t)(t >> 32), fr = (uint32_t)t, g = h[k] >> gsh;
+            const uint4 rec = s_idx[g];
+            const uint32_t jb = 4u * j;  // the bucket's bit offset among the 112 count bits
+            const uint32_t m0 = jb >= 32u ? ~0u : (1u << jb) - 1u;
+            const uint32_t m1 = jb >= 64u ? ~0u : jb <= 32u ? 0u : (1u << (jb - 32u)) - 1u;
+            const uint32_t m2 = jb >= 96u ? ~0u : jb <= 64u ? 0u : (1u << (jb - 64u)) - 1u;
+            const uint32_t m3 = jb <= 96u ? 0u : (1u << (jb - 96u)) - 1u;
+            const uint32_t below = nsum(rec.x & m0, nsum(rec.y & m1, nsum(rec.z & m2, nsum(rec.w & m3, 0u))));
+            const uint32_t cw = jb < 32u ? rec.x : jb < 64u ? rec.y : jb < 96u ? rec.z : rec.w;
+            const uint32_t c = (cw >> (jb & 31u)) & 15u;
+            const uint32_t st = (uint32_t)(((uint64_t)g * lv.M) >> lg) + (uint32_t)((int32_t)rec.w >> 16) + below;
+            const uint32_t fl = ((fr >> 24) * c) >> 8;  // about the key's position in the bucket
+            const uint32_t s = fl > 3u ? fl - 3u : 0u;
+            w0[k] = st + s;
+            sw[k] = s;
+            bc[k] = c;
+            K[k] = (fr >> fsh) << lv.ob;
+            wa[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ent_r, (int)(3u * w0[k]), 0, 0));
+            wb[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ent_r, (int)(3u * w0[k] + 16u), 0, 0));
+        }
+        uint32_t nsl = 0;  // wave-uniform: this wave-tile's deferred keys
+#pragma unroll
+        for (int k = 0; k < KPL; k++) {
+            const u32x4 a = wa[k], b = wb[k];
+            const uint32_t e[10] = {a.x & 0xFFFFFFu,
+                                    (a.x >> 24) | ((a.y & 0xFFFFu) << 8),
+                                    (a.y >> 16) | ((a.z & 0xFFu) << 16),
+                                    a.z >> 8,
+                                    a.w & 0xFFFFFFu,
+                                    (a.w >> 24) | ((b.x & 0xFFFFu) << 8),
+                                    (b.x >> 16) | ((b.y & 0xFFu) << 16),
+                                    b.y >> 8,
+                                    b.z & 0xFFFFFFu,
+                                    (b.z >> 24) | ((b.w & 0xFFFFu) << 8)};
+            uint32_t lt = 0;  // in-bucket window entries below the key
+            bool tie = false;
+#pragma unroll
+            for (int j = 0; j < 10; j++) {
+                const bool inb = sw[k] + (uint32_t)j < bc[k];
+                lt += (inb && e[j] < K[k]);
+                tie |= (inb && e[j] - K[k] < obit);
+            }
+            uint32_t res[4] = {NIL, NIL, NIL, NIL}, rc = 0;
+#pragma unroll
+            for (int j = 0; j < 10; j++) {  // the first NEED distinct owners from the key's position
+                const uint32_t o = e[j] & omask;
+                const bool dup = (rc > 0 && o == res[0]) | (rc > 1 && o == res[1]) | (rc > 2 && o == res[2]);
+                if ((uint32_t)j >= lt && !dup && rc < (uint32_t)NEED) {
+                    res[0] = rc == 0 ? o : res[0];
+                    res[1] = rc == 1 ? o : res[1];
+                    res[2] = rc == 2 ? o : res[2];
+                    res[3] = rc == 3 ? o : res[3];
+                    rc++;
+                }
+            }
+            // deferred: a tie, a bucket of 15+ tokens, the key before the window (its guard entry
+            // is not below it) or past it, owners not distinct inside it, the ring end
+            const bool slow = tie | (bc[k] == 15u) | (sw[k] > 0u && lt == 0u) | (lt == 10u) | (rc < (uint32_t)NEED) |
+                              (w0[k] + 12u > lv.M);
+            const uint32_t kk = (uint32_t)k * 64u + lane;
+            uint32_t* row = out + (base + kk) * NEED;
+#pragma unroll
+            for (int q = 0; q < NEED; q++) __builtin_nontemporal_store(res[q], row + q);
+            if (counts) counts[base + kk] = (uint8_t)NEED;
+            const uint64_t m = __ballot(slow);
+            const uint32_t pos = nsl + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (slow && pos < kSlowPerTile) slow_list[wt * kSlowPerTile + pos] = kk;
+            nsl += (uint32_t)__popcll(m);
+        }
+        if (lane == 0) slow_cnt[wt] = nsl;
+    }
+}
+
 // Exact completion of the keys the compact kernels deferred: one thread per list slot
 // (kSlowPerTile per tile) redoes its key; the slots of a tile whose list overflowed share the
 // whole tile. (One thread per tile, redoing its list serially, took 0.043 ms per C2 launch.)
@@ -1809,6 +1958,57 @@ __global__ void k_cindex_hint(const uint32_t* __restrict__ tok, const uint32_t* 
     }
 }
 
+// The LDS-index layout (round 6; k_lookupn_lds). The bucket search structure moves out of L2 into
+// every CU's LDS, so a key takes one L2 trip (its window) instead of two (index record, then
+// window). NG groups (a power of two, <= 8,192: 128 KB) of 28 buckets, NB = 28 NG buckets over the
+// hash space: a hash h is in group g = h >> (32 - lg) and bucket j = floor(28 x / 2^32) of it, with
+// x = h << lg, and its fingerprint is the top fb bits of the remainder (28 x) mod 2^32 (monotone in
+// h within a bucket). A group record is 16 B: 28 4-bit token counts, then the group's first
+// position as an int16 delta from pred(g) = g M / NG. Entries are 3 B, (fp << ob) | owner.
+__device__ __forceinline__ uint32_t lds_first_pos(const uint32_t* __restrict__ tok, uint32_t M, uint32_t lg,
+                                                  uint32_t g, uint32_t j) {
+    // the least h in bucket (g, j): x >= ceil(j 2^32 / 28)
+    const uint64_t xm = ((uint64_t)j << 32) / 28u + (((uint64_t)j << 32) % 28u ? 1u : 0u);
+    const uint64_t hm = ((uint64_t)g << (32 - lg)) + (xm >> lg) + ((xm & ((1ull << lg) - 1u)) ? 1u : 0u);
+    return hm >= (1ull << 32) ? M : lower_bound_dev(tok, M, (uint32_t)hm);
+}
+__global__ void k_lidx_build(const uint32_t* __restrict__ tok, uint32_t M, uint32_t lg, uint32_t ng,
+                             uint4* __restrict__ idx, uint32_t* __restrict__ over) {
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ng; g += gstride) {
+        uint32_t w[4] = {0, 0, 0, 0};
+        uint32_t p = lds_first_pos(tok, M, lg, (uint32_t)g, 0);
+        const uint32_t base = p;
+        for (uint32_t j = 0; j < 28; j++) {
+            const uint32_t q = j == 27 ? (g + 1 == ng ? M : lds_first_pos(tok, M, lg, (uint32_t)g + 1, 0))
+                                       : lds_first_pos(tok, M, lg, (uint32_t)g, j + 1);
+            const uint32_t c = q - p;
+            w[j >> 3] |= (c > 15u ? 15u : c) << (4 * (j & 7));  // 15: the bucket's keys take the exact path
+            p = q;
+        }
+        const int64_t delta = (int64_t)base - (int64_t)(((uint64_t)g * M) >> lg);
+        if (delta < -32768 || delta > 32767) atomicOr(over, 1u);
+        w[3] |= ((uint32_t)delta & 0xFFFFu) << 16;
+        idx[g] = uint4{w[0], w[1], w[2], w[3]};
+    }
+}
+// LDS-index entries: 3 bytes per token, (fp << ob) | owner; padding entries are all ones
+__global__ void k_lpack3(const uint32_t* __restrict__ tok, const uint32_t* __restrict__ own, uint32_t M, uint32_t lg,
+                         uint32_t fb, uint32_t ob, uint8_t* __restrict__ ent) {
+    const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < (uint64_t)M + kEnt3Pad + 6; j += gstride) {
+        uint32_t v = 0xFFFFFFu;
+        if (j < M) {
+            const uint32_t x = tok[j] << lg;
+            const uint32_t fp = (uint32_t)((uint64_t)x * 28u) >> (32u - fb);
+            v = (fp << ob) | own[j];
+        }
+        ent[3 * j + 0] = (uint8_t)v;
+        ent[3 * j + 1] = (uint8_t)(v >> 8);
+        ent[3 * j + 2] = (uint8_t)(v >> 16);
+    }
+}
+
 // checksum string pieces: len of (name + ';') for in-ring servers in name order.
 __global__ void k_ck_len(const uint32_t* __restrict__ sorted_ids, uint32_t n,
                          const uint8_t* __restrict__ in_ring, const uint64_t* __restrict__ noff,
@@ -1889,6 +2089,11 @@ struct Ring {
     bool chint_pending = false;  // the compact layout changed and the hinted index is not built yet
     bool compact = false;
     uint32_t ccb = 0, cob = 0, cfsh = 0;
+    // the LDS-index layout (k_lookupn_lds, round 6), built by the first batch lookup after a change
+    DevBuf<uint8_t> lent;
+    DevBuf<uint4> lidx;
+    bool lds = false, lds_pending = false;
+    uint32_t lng = 0, llg = 0, lfb = 0;
     // checksum string + value
     DevBuf<uint8_t> d_inring;
     DevBuf<uint8_t> ck_buf;
@@ -1910,7 +2115,8 @@ struct Ring {
     SvcLines* svc_dev = nullptr;
     hipStream_t svc_st = nullptr;
     uint32_t svc_idle_ms = 0, svc_seq = 0;
-    bool svc_running = false;
+    std::atomic<bool> svc_live{false};  // a wave launched and not yet stopped (counted in g_svc_live)
+    std::recursive_mutex svc_mu;         // the service's lines and state (svc_lookup, svc_stop)
     bool svc_v2 = true;  // k_lookup_service3 (RP_RING_SVC=1: the round-4 kernel; read at rp_ring_service)
     DevBuf<uint4> svc_dt;       // the service's direct table (k_dt_build), built at its first launch after a change
     uint32_t svc_dtb = 0;       // its bucket bits; 0: none (ids past 16 bits, M > 2^22, RP_SVC_DT=0)
@@ -1986,6 +2192,8 @@ static void ring_build_compact(Ring& r) {
     // per-call mutation (addServer / removeServer) should not pay
     r.chint = false;
     r.chint_pending = 32 - cb >= 8 && r.M < (1u << 30);
+    r.lds = false;
+    r.lds_pending = ob <= 14;
     r.compact = true;
     r.ccb = cb;
     r.cob = ob;
@@ -2005,6 +2213,32 @@ static void ring_build_hint(Ring& r) {
                        (uint32_t)ngroups, r.cidxh.p, r.scalar.p);
     RP_HIP(hipGetLastError());
     r.chint = read_u32(r.scalar.p, r.st) == 0;
+}
+
+// The LDS-index layout (LdsView): ng = the power of two nearest M / 126 (about 4.5 tokens a bucket),
+// 64..8,192 groups; not built past 5.5 tokens a bucket at 8,192 groups (M > 1.26 M), for owner ids
+// past 14 bits (fingerprints under 10 bits), or when a group's base does not fit its int16 delta.
+static void ring_build_lds(Ring& r) {
+    r.lds_pending = false;
+    r.lds = false;
+    uint32_t lg = 6;
+    while (lg < 13 && (1ull << lg) * 126ull < r.M) lg++;
+    const uint64_t ng = 1ull << lg;
+    if ((double)r.M / (28.0 * (double)ng) > 5.5 || r.cob > 14) return;
+    const uint32_t fb = 24u - r.cob;
+    r.lidx.reserve(ng);
+    RP_HIP(hipMemsetAsync(r.scalar.p, 0, sizeof(uint32_t), r.st));
+    hipLaunchKernelGGL(k_lidx_build, dim3(grid_for(ng, 256)), dim3(256), 0, r.st, r.tok.p, r.M, lg, (uint32_t)ng,
+                       r.lidx.p, r.scalar.p);
+    r.lent.reserve(3ull * ((uint64_t)r.M + kEnt3Pad + 6) + 16);
+    hipLaunchKernelGGL(k_lpack3, dim3(grid_for((uint64_t)r.M + kEnt3Pad + 6, 256)), dim3(256), 0, r.st, r.tok.p,
+                       r.own.p, r.M, lg, fb, r.cob, r.lent.p);
+    RP_HIP(hipGetLastError());
+    if (read_u32(r.scalar.p, r.st) != 0) return;
+    r.lng = (uint32_t)ng;
+    r.llg = lg;
+    r.lfb = fb;
+    r.lds = true;
 }
 
 static void ring_rebuild_index(Ring& r) {
@@ -2185,6 +2419,58 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
     const char* lay = getenv("RP_RING_LAYOUT");  // A/B: "packed" forces the packed probe kernel
     const bool use_compact = r.compact && !(lay && !strcmp(lay, "packed")) && !getenv_flag("RP_RING_WIDE");
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(keys) & 15) == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
+    // the LDS-index kernel (round 6; RP_LOOKUP_LDS=0 keeps the lean kernel, 1 forces this one)
+    const char* lds_env = getenv("RP_LOOKUP_LDS");
+    const bool lds_on = lds_env ? !strcmp(lds_env, "1") : kLdsDefault;
+    if (use_compact && lds_on && fixed36 && aligned16 && (uint32_t)need == W && W <= 4 && n >= 64ull * 8 &&
+        !getenv("RP_LOOKUP_ABLATE")) {
+        if (r.lds_pending) ring_build_lds(r);
+        if (r.lds) {
+            RP_REQUIRE(n < (1ull << 32), "lookupn: at most 2^32-1 keys per call");
+            constexpr int KPL = 8;
+            const uint64_t TK = 64ull * KPL, nwt = n / TK, done = nwt * TK;
+            r.slow.reserve(nwt * kSlowPerTile + 1);
+            r.nslow.reserve(nwt + 1);
+            static const int cus = [] {
+                int dev = 0, c = 0;
+                (void)hipGetDevice(&dev);
+                (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+                return c > 0 ? c : 256;
+            }();
+            const unsigned g = (unsigned)std::min<uint64_t>((uint64_t)env_pos("RP_LOOKUP_LDS_GRID", (uint64_t)cus),
+                                                            (nwt + kLdsThreads / 64 - 1) / (kLdsThreads / 64));
+            const LdsView lv{r.lent.p, r.lidx.p, r.M, r.lng, r.llg, r.lfb, r.cob,
+                             (uint32_t)(3ull * ((uint64_t)r.M + kEnt3Pad + 6) + 16)};
+            switch (need) {
+                case 1: hipLaunchKernelGGL((k_lookupn_lds<KPL, 1>), dim3(g), dim3(kLdsThreads), 0, st, keys, nwt, lv, out, counts, r.slow.p, r.nslow.p); break;
+                case 2: hipLaunchKernelGGL((k_lookupn_lds<KPL, 2>), dim3(g), dim3(kLdsThreads), 0, st, keys, nwt, lv, out, counts, r.slow.p, r.nslow.p); break;
+                case 3: hipLaunchKernelGGL((k_lookupn_lds<KPL, 3>), dim3(g), dim3(kLdsThreads), 0, st, keys, nwt, lv, out, counts, r.slow.p, r.nslow.p); break;
+                default: hipLaunchKernelGGL((k_lookupn_lds<KPL, 4>), dim3(g), dim3(kLdsThreads), 0, st, keys, nwt, lv, out, counts, r.slow.p, r.nslow.p); break;
+            }
+            RP_HIP(hipGetLastError());
+            const CompactFixView fv{r.tok.p, r.own.p, r.cidx.p, r.view(), r.M, r.ccb};
+            const uint64_t fthreads = nwt * kSlowPerTile;
+            hipLaunchKernelGGL((k_lookupn_fix_tiles<CompactFixView>), dim3((unsigned)((fthreads + 255) / 256)), dim3(256),
+                               0, st, keys, fv, np, W, out, counts, r.slow.p, r.nslow.p, nwt, (uint32_t)TK);
+            RP_HIP(hipGetLastError());
+            if (getenv_flag("RP_LOOKUP_DEBUG")) {
+                std::vector<uint32_t> c(nwt);
+                RP_HIP(hipMemcpyAsync(c.data(), r.nslow.p, 4 * nwt, hipMemcpyDeviceToHost, st));
+                RP_HIP(hipStreamSynchronize(st));
+                uint64_t tot = 0, over = 0;
+                for (uint32_t x : c) {
+                    tot += x;
+                    over += x > kSlowPerTile;
+                }
+                fprintf(stderr, "[rp] lds lookupN: %llu keys, %llu deferred, %llu overflowed tiles (ng %u fb %u ob %u)\n",
+                        (unsigned long long)done, (unsigned long long)tot, (unsigned long long)over, r.lng, r.lfb, r.cob);
+            }
+            if (done < n)
+                launch_lookupn_view(r.view(), keys + done * 36, nullptr, 36, nullptr, n - done, np, W, out + done * W,
+                                    counts ? counts + done : nullptr, st);
+            return;
+        }
+    }
     if (use_compact && fixed36 && aligned16 && (uint32_t)need == W && W <= 4 && n >= (uint64_t)kLkThreads * 4) {
         RP_REQUIRE(n < (1ull << 32), "lookupn: at most 2^32-1 keys per call");
         if (r.chint_pending && need == 3) ring_build_hint(r);
@@ -2466,6 +2752,7 @@ struct rp_ring {
 };
 
 using rp::guard;
+using rp::guard_host;
 
 static rp::Ring& R(rp_ring* r) {
     if (!r) throw rp::Error(rp::RP_EINVAL, "null ring handle");
@@ -2499,10 +2786,20 @@ int rp_ring_create(uint32_t replica_points, int device, rp_ring** out) {
 
 // ---- the lookup service (rp_ring_service; k_lookup_service)
 // While the service wave is resident (up to idle_ms after a request), any hipFree in the process
-// (a device buffer growing or released) synchronizes the device and so waits for the wave to
-// idle out. Every other device path of this ring stops the service first; buffers of
-// other handles in the same process can still wait up to idle_ms (include/ringpop_amd.h).
+// (a device buffer growing or released) synchronizes the device and so waits for the wave to idle
+// out, and the wave's stream may share a hardware queue with another handle's. Every device call of
+// the library therefore stops every resident service first and keeps new ones from starting while
+// it runs (QuietScope, rp_common.h): rings with a service configured are listed
+// in a process-wide registry that svc_quiesce walks.
+}  // extern "C" (the registry and its counters have C++ linkage)
+namespace rp {
+std::atomic<int> g_quiet{0}, g_svc_live{0};
+}  // namespace rp
+static std::mutex g_svc_reg_mu;            // guards g_svc_reg; taken before any ring's svc_mu
+static std::vector<rp::Ring*> g_svc_reg;   // rings with a service configured (rp_ring_service)
+
 static void svc_stop(rp::Ring& r) {
+    std::lock_guard<std::recursive_mutex> lk(r.svc_mu);
     if (r.svc_prof[8] && getenv("RP_SVC_PROF")) {
         const double n = (double)r.svc_prof[8];
         fprintf(stderr,
@@ -2513,12 +2810,28 @@ static void svc_stop(rp::Ring& r) {
                 (unsigned long long)r.svc_prof[6], (unsigned long long)r.svc_prof[7]);
         for (auto& x : r.svc_prof) x = 0;
     }
-    if (!r.svc || !r.svc_running) return;
+    if (!r.svc || !r.svc_live.load()) return;
     __atomic_store_n(&r.svc->req[4], 1u, __ATOMIC_RELEASE);
-    RP_HIP(hipStreamSynchronize(r.svc_st));
-    r.svc_running = false;
+    const hipError_t e = hipStreamSynchronize(r.svc_st);
+    r.svc_live.store(false);
+    rp::g_svc_live.fetch_sub(1);
     __atomic_store_n(&r.svc->req[4], 0u, __ATOMIC_RELEASE);
+    RP_HIP(e);
 }
+
+void rp::svc_quiesce(const void* keep) {
+    std::lock_guard<std::mutex> g(g_svc_reg_mu);
+    for (rp::Ring* r : g_svc_reg)
+        if (r != keep && r->svc_live.load()) svc_stop(*r);
+}
+
+static void svc_register(rp::Ring& r, bool on) {
+    std::lock_guard<std::mutex> g(g_svc_reg_mu);
+    auto it = std::find(g_svc_reg.begin(), g_svc_reg.end(), &r);
+    if (on && it == g_svc_reg.end()) g_svc_reg.push_back(&r);
+    if (!on && it != g_svc_reg.end()) g_svc_reg.erase(it);
+}
+extern "C" {
 
 static void svc_launch(rp::Ring& r, uint32_t last) {
     using namespace rp;
@@ -2547,12 +2860,12 @@ static void svc_launch(rp::Ring& r, uint32_t last) {
         hipLaunchKernelGGL((k_lookup_service<RingView>), dim3(1), dim3(64), 0, r.svc_st, r.svc_dev, r.view(), fv,
                            r.compact ? 1u : 0u, last, idle, maxt);
     RP_HIP(hipGetLastError());
-    r.svc_running = true;
 }
 
 int rp_ring_destroy(rp_ring* r) {
     return guard([&] {
         if (!r) return;
+        svc_register(r->impl, false);  // no quiesce walks this ring from here on
         (void)hipSetDevice(r->impl.device);
         if (r->impl.st) {
             (void)hipStreamSynchronize(r->impl.st);
@@ -2619,7 +2932,7 @@ int rp_ring_add_remove(rp_ring* h, const char* add_bytes, const uint32_t* add_of
 }
 
 int rp_ring_checksum(rp_ring* h, uint32_t* out, int* is_set) {
-    return guard([&] {
+    return guard_host([&] {
         rp::Ring& r = R(h);
         if (out) *out = r.checksum;
         if (is_set) *is_set = r.has_checksum ? 1 : 0;
@@ -2648,15 +2961,15 @@ int rp_ring_checksum_string(rp_ring* h, char* buf, uint64_t cap, uint64_t* len) 
 }
 
 int rp_ring_server_count(rp_ring* h, uint32_t* out) {
-    return guard([&] { *out = R(h).server_count; });
+    return guard_host([&] { *out = R(h).server_count; });
 }
 
 int rp_ring_token_count(rp_ring* h, uint32_t* out) {
-    return guard([&] { *out = R(h).M; });
+    return guard_host([&] { *out = R(h).M; });
 }
 
 int rp_ring_has_server(rp_ring* h, const char* name, uint32_t len, int* out) {
-    return guard([&] {
+    return guard_host([&] {
         rp::Ring& r = R(h);
         const uint32_t id = r.nt.find(name, len);
         *out = (id != rp::NIL && r.in_ring[id]) ? 1 : 0;
@@ -2664,7 +2977,7 @@ int rp_ring_has_server(rp_ring* h, const char* name, uint32_t len, int* out) {
 }
 
 int rp_ring_server_id(rp_ring* h, const char* name, uint32_t len, uint32_t* id) {
-    return guard([&] {
+    return guard_host([&] {
         rp::Ring& r = R(h);
         *id = r.nt.find(name, len);
     });
@@ -2680,7 +2993,7 @@ const char* rp_ring_owner_name(rp_ring* h, uint32_t id, uint32_t* len) {
 }
 
 int rp_ring_servers(rp_ring* h, uint32_t* ids_out, uint32_t cap, uint32_t* n) {
-    return guard([&] {
+    return guard_host([&] {
         rp::Ring& r = R(h);
         std::vector<uint32_t> v;
         for (uint32_t id = 0; id < r.nt.size(); id++)
@@ -2784,7 +3097,6 @@ static bool host_lookup_small(rp::Ring& r, const char* keys, const uint64_t* off
     return true;
 }
 
-// one key through the service: false when it does not apply (off, long key, wide row)
 // one key (or, with hash non-null, one caller hash) through the service: false when it does not
 // apply (off, a wide row; the round-4 kernel: a long key or a caller hash)
 static bool svc_lookup(rp::Ring& r, const char* key, uint32_t len, const uint32_t* hash, int np, uint32_t W,
@@ -2793,6 +3105,9 @@ static bool svc_lookup(rp::Ring& r, const char* key, uint32_t len, const uint32_
     const int need = np <= 0 ? 1 : np;
     if (!r.svc_idle_ms || W > 8 || need > 8 || r.M == 0) return false;
     if (!r.svc_v2 && (hash || len > kSvcKeyMax)) return false;
+    if (g_quiet.load() > 0) return false;  // another thread's device call is running
+    if (g_svc_live.load() > (r.svc_live.load() ? 1 : 0)) rp::svc_quiesce(&r);  // another ring's wave
+    std::lock_guard<std::recursive_mutex> lk(r.svc_mu);
     if (!r.svc) {
         RP_HIP(hipHostMalloc(reinterpret_cast<void**>(&r.svc), sizeof(SvcLines), hipHostMallocMapped | hipHostMallocCoherent));
         memset(r.svc, 0, sizeof(SvcLines));
@@ -2801,6 +3116,22 @@ static bool svc_lookup(rp::Ring& r, const char* key, uint32_t len, const uint32_
         r.svc_seq = 0;
     }
     SvcLines* io = r.svc;
+    // a wave is needed: none launched, or the last one exited (idle or lifetime). Announce it in
+    // g_svc_live before reading g_quiet (the QuietScope handshake, rp_common.h); while another
+    // thread's device call runs, this lookup takes the launch path instead.
+    bool launch = false;
+    if (!r.svc_live.load()) {
+        r.svc_live.store(true);
+        g_svc_live.fetch_add(1);
+        if (g_quiet.load() > 0) {
+            r.svc_live.store(false);
+            g_svc_live.fetch_sub(1);
+            return false;
+        }
+        launch = true;
+    } else if (hipStreamQuery(r.svc_st) == hipSuccess) {
+        launch = true;
+    }
     const uint32_t s = r.svc_seq + 1;
     if (r.svc_v2) {
         // the key's hash, on the host as the reference computes it (lib/ring/index.js:145-154)
@@ -2816,10 +3147,7 @@ static bool svc_lookup(rp::Ring& r, const char* key, uint32_t len, const uint32_
     io->req[3] = W;
     __atomic_store_n(&io->req[15], s, __ATOMIC_RELEASE);  // the header's trailing copy of seq
     __atomic_store_n(&io->req[0], s, __ATOMIC_RELEASE);
-    if (!r.svc_running || hipStreamQuery(r.svc_st) == hipSuccess) {
-        if (r.svc_running) RP_HIP(hipStreamSynchronize(r.svc_st));
-        svc_launch(r, s - 1);
-    }
+    if (launch) svc_launch(r, s - 1);
     uint64_t spins = 0;
     const auto t0 = std::chrono::steady_clock::now();
     // v2: the answer line is taken when all 8 of its words carry seq s (no torn line)
@@ -2870,6 +3198,7 @@ static void host_lookup(rp::Ring& r, const char* keys, const uint64_t* off, uint
                           : svc_lookup(r, keys + (stride ? 0 : off[0]), (uint32_t)(stride ? stride : off[1] - off[0]),
                                        nullptr, np, W, owners, counts)))
         return;
+    rp::QuietScope quiet;  // the launch path: no resident service (this ring's or another's) meanwhile
     svc_stop(r);
     if (!hashes && host_lookup_small(r, keys, off, stride, n, np, W, owners, counts)) return;
     const uint8_t* dk = nullptr;
@@ -2902,13 +3231,14 @@ int rp_ring_service(rp_ring* h, uint32_t idle_ms) {
     return guard([&] {
         rp::Ring& r = R(h);
         svc_stop(r);
+        svc_register(r, idle_ms > 0);
         r.svc_idle_ms = idle_ms;
         r.svc_v2 = !(getenv("RP_RING_SVC") && !strcmp(getenv("RP_RING_SVC"), "1"));
     });
 }
 
 int rp_ring_lookup(rp_ring* h, const char* keys, const uint64_t* off, uint32_t stride, uint64_t n, uint32_t* owners) {
-    return guard([&] {
+    return guard_host([&] {
         rp::Ring& r = R(h);
         RP_REQUIRE(n == 0 || (keys && owners && (stride || off)), "lookup: null buffer");
         host_lookup(r, keys, off, stride, nullptr, n, 1, 1, owners, nullptr);
@@ -2917,7 +3247,7 @@ int rp_ring_lookup(rp_ring* h, const char* keys, const uint64_t* off, uint32_t s
 
 int rp_ring_lookupn(rp_ring* h, const char* keys, const uint64_t* off, uint32_t stride, uint64_t n, int32_t nrep,
                     uint32_t* owners, uint8_t* counts) {
-    return guard([&] {
+    return guard_host([&] {
         rp::Ring& r = R(h);
         RP_REQUIRE(n == 0 || (keys && owners && (stride || off)), "lookupn: null buffer");
         host_lookup(r, keys, off, stride, nullptr, n, np_for(r, nrep), nrep > 1 ? (uint32_t)nrep : 1u, owners,
@@ -2926,7 +3256,7 @@ int rp_ring_lookupn(rp_ring* h, const char* keys, const uint64_t* off, uint32_t 
 }
 
 int rp_ring_lookup_hashes(rp_ring* h, const uint32_t* hashes, uint64_t n, uint32_t* owners) {
-    return guard([&] {
+    return guard_host([&] {
         rp::Ring& r = R(h);
         RP_REQUIRE(n == 0 || (hashes && owners), "lookup_hashes: null buffer");
         host_lookup(r, nullptr, nullptr, 0, hashes, n, 1, 1, owners, nullptr);
@@ -2935,7 +3265,7 @@ int rp_ring_lookup_hashes(rp_ring* h, const uint32_t* hashes, uint64_t n, uint32
 
 int rp_ring_lookupn_hashes(rp_ring* h, const uint32_t* hashes, uint64_t n, int32_t nrep, uint32_t* owners,
                            uint8_t* counts) {
-    return guard([&] {
+    return guard_host([&] {
         rp::Ring& r = R(h);
         RP_REQUIRE(n == 0 || (hashes && owners), "lookupn_hashes: null buffer");
         host_lookup(r, nullptr, nullptr, 0, hashes, n, np_for(r, nrep), nrep > 1 ? (uint32_t)nrep : 1u, owners,

@@ -3209,6 +3209,17 @@ __global__ void k_csr(const uint32_t* __restrict__ keys, uint32_t n, uint32_t N,
     }
 }
 
+// The outbox's per-destination message offsets and the record offsets at them, in one array the
+// host reads with one copy (build_out's one host wait of a stage).
+__global__ void k_out_cnt_pack(const uint32_t* __restrict__ moff, const uint32_t* __restrict__ ooff, uint32_t G,
+                               uint32_t* __restrict__ out) {
+    for (uint32_t g = threadIdx.x; g <= G; g += blockDim.x) {
+        const uint32_t m = moff[g];
+        out[g] = m;
+        out[G + 1 + g] = ooff[m];
+    }
+}
+
 // ---- convergence over this shard's nodes that are up and have not left (scenario-runner.js's
 // hostToAliveWorker): {count, min checksum, max checksum, some wanted member not at its wanted
 // status in one of those views}. want[i] = member | status << 24: a member that left must be
@@ -3342,6 +3353,26 @@ struct Sim {
     hipStream_t st2 = nullptr;
     hipEvent_t ev_c = nullptr, ev_early = nullptr;
     hipEvent_t ev_ext = nullptr;  // rp_sim_wait_stream: the next stage waits for a caller's stream
+    hipEvent_t ev_ord = nullptr;  // rp_sim_order_stream: a caller's stream waits for this handle's
+    // Pinned host staging (round 6): a stage's outbox counts come back with one
+    // copy and one event wait, and the segment and inbox tables go up from a ring of pinned slots,
+    // so the host waits neither for the outbox fill nor for an import. A slot is rewritten
+    // kPinSlots uses later; every stage with an outbox waits for its counts, which follow every
+    // earlier copy on the stream, so no slot is rewritten before its copy ran.
+    static constexpr uint32_t kPinSlots = 8;
+    uint64_t* h_pin = nullptr;
+    uint32_t pin_next = 0;
+    hipEvent_t ev_cnt = nullptr;
+    DevBuf<uint32_t> ocnt_pack;
+    uint64_t* pin_slot() {  // 2G + 2 words
+        if (!h_pin) {
+            RP_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_pin), 8ull * kPinSlots * (2 * G + 2), hipHostMallocDefault));
+            RP_HIP(hipEventCreateWithFlags(&ev_cnt, hipEventDisableTiming));
+        }
+        uint64_t* p = h_pin + (uint64_t)(pin_next % kPinSlots) * (2 * G + 2);
+        pin_next++;
+        return p;
+    }
     bool early_pending = false;
     bool early_on = [] {
         const char* e = getenv("RP_SIM_EARLY");
@@ -3529,32 +3560,31 @@ struct Sim {
         hipLaunchKernelGGL(k_out_counts, dim3(grid_for(C, 256)), dim3(256), 0, st, d, kind, okey.p, oval.p, C, ocnt.p);
         scan_exclusive_u32(ocnt.p, ooff.p, C, st, ws);
         hipLaunchKernelGGL(k_csr, dim3(1), dim3(128), 0, st, okey.p, C, G, omoff.p);
+        ocnt_pack.reserve(2 * G + 2);
+        hipLaunchKernelGGL(k_out_cnt_pack, dim3(1), dim3(64), 0, st, omoff.p, ooff.p, G, ocnt_pack.p);
         RP_HIP(hipGetLastError());
-        std::vector<uint32_t> moff(G + 1);
-        RP_HIP(hipMemcpyAsync(moff.data(), omoff.p, 4ull * (G + 1), hipMemcpyDeviceToHost, st));
-        RP_HIP(hipStreamSynchronize(st));
-        std::vector<uint32_t> roff(G + 1);
-        for (uint32_t g = 0; g <= G; g++)
-            RP_HIP(hipMemcpyAsync(&roff[g], ooff.p + moff[g], 4, hipMemcpyDeviceToHost, st));
-        RP_HIP(hipStreamSynchronize(st));
+        const uint32_t* hc = reinterpret_cast<const uint32_t*>(pin_slot());
+        RP_HIP(hipMemcpyAsync(const_cast<uint32_t*>(hc), ocnt_pack.p, 4ull * (2 * G + 2), hipMemcpyDeviceToHost, st));
+        RP_HIP(hipEventRecord(ev_cnt, st));
+        RP_HIP(hipEventSynchronize(ev_cnt));  // the stage's one host wait: its counts
+        const uint32_t *moff = hc, *roff = hc + G + 1;
         out.tot_msg = moff[G];
         out.tot_rec = roff[G];
         sent_msgs += out.tot_msg;
         sent_recs += out.tot_rec;
-        std::vector<uint64_t> seg(G + 1);
         for (uint32_t g = 0; g < G; g++) {
             out.nmsg[g] = moff[g + 1] - moff[g];
             out.nrec[g] = roff[g + 1] - roff[g];
         }
+        uint64_t* seg = pin_slot();
         for (uint32_t g = 0; g <= G; g++) seg[g] = out.seg_off(g);
         out.size_for(out.bytes());
         oseg.reserve(G + 1);
-        RP_HIP(hipMemcpyAsync(oseg.p, seg.data(), 8ull * (G + 1), hipMemcpyHostToDevice, st));
+        RP_HIP(hipMemcpyAsync(oseg.p, seg, 8ull * (G + 1), hipMemcpyHostToDevice, st));
         if (out.tot_msg)
             hipLaunchKernelGGL(k_out_fill, dim3(grid_for(out.tot_msg, 1, 4096)), dim3(kT), 0, st, d, kind, okey.p,
                                oval.p, (uint32_t)out.tot_msg, ooff.p, omoff.p, oseg.p, out.buf.p);
-        RP_HIP(hipStreamSynchronize(st));  // seg (host) is reused
-        RP_HIP(hipGetLastError());
+        RP_HIP(hipGetLastError());  // no wait for the fill: rp_sim_order_stream orders its readers
     }
 
     // Size the inbox for per-source counts (the caller then fills in.buf, segments in source order).
@@ -3585,7 +3615,7 @@ struct Sim {
         d.in_buf = in.buf.p;
         d.nin = (uint32_t)in.tot_msg;
         if (in.tot_msg) {
-            std::vector<uint64_t> tab(2 * G + 1);
+            uint64_t* tab = pin_slot();
             uint64_t m = 0;
             for (uint32_t g = 0; g < G; g++) {
                 tab[g] = m;
@@ -3594,10 +3624,9 @@ struct Sim {
             }
             tab[G] = m;
             ibase.reserve(2 * G + 1);
-            RP_HIP(hipMemcpyAsync(ibase.p, tab.data(), 8ull * (2 * G + 1), hipMemcpyHostToDevice, st));
+            RP_HIP(hipMemcpyAsync(ibase.p, tab, 8ull * (2 * G + 1), hipMemcpyHostToDevice, st));
             hipLaunchKernelGGL(k_in_gather, dim3(grid_for(in.tot_msg, 256)), dim3(256), 0, st, imsg.p,
                                (uint32_t)in.tot_msg, in.buf.p, ibase.p, G);
-            RP_HIP(hipStreamSynchronize(st));  // tab (host) is reused
         }
         const uint32_t n = (uint32_t)in.tot_msg;
         if (kind == K_PING || kind == K_LEG) {
@@ -4221,7 +4250,12 @@ int rp_sim_destroy(rp_sim* s) {
             (void)hipStreamDestroy(s->impl.st2);
             (void)hipEventDestroy(s->impl.ev_c);
             (void)hipEventDestroy(s->impl.ev_early);
-            if (s->impl.ev_ext) (void)hipEventDestroy(s->impl.ev_ext);
+        }
+        if (s->impl.ev_ext) (void)hipEventDestroy(s->impl.ev_ext);
+        if (s->impl.ev_ord) (void)hipEventDestroy(s->impl.ev_ord);
+        if (s->impl.h_pin) {
+            (void)hipHostFree(s->impl.h_pin);
+            (void)hipEventDestroy(s->impl.ev_cnt);
         }
         delete s;
     });
@@ -4268,7 +4302,6 @@ int rp_sim_stage(rp_sim* s, int stage) {
 int rp_sim_outbox(rp_sim* s, uint64_t* nmsg, uint64_t* nrec, void** buf) {
     return guard([&] {
         rp::Sim& S = SM(s);
-        RP_HIP(hipStreamSynchronize(S.st));
         for (uint32_t g = 0; g < S.G; g++) {
             if (nmsg) nmsg[g] = S.out.nmsg.empty() ? 0 : S.out.nmsg[g];
             if (nrec) nrec[g] = S.out.nrec.empty() ? 0 : S.out.nrec[g];
@@ -4282,8 +4315,20 @@ int rp_sim_inbox(rp_sim* s, const uint64_t* nmsg, const uint64_t* nrec, void** b
         rp::Sim& S = SM(s);
         RP_REQUIRE(nmsg && nrec, "sim_inbox: counts required");
         S.prepare_in(nmsg, nrec);
-        RP_HIP(hipStreamSynchronize(S.st));
         if (buf) *buf = S.in.buf.p;
+    });
+}
+
+int rp_sim_order_stream(rp_sim* s, void* stream) {
+    return guard([&] {
+        rp::Sim& S = SM(s);
+        if (!stream) {
+            RP_HIP(hipStreamSynchronize(S.st));
+            return;
+        }
+        if (!S.ev_ord) RP_HIP(hipEventCreateWithFlags(&S.ev_ord, hipEventDisableTiming));
+        RP_HIP(hipEventRecord(S.ev_ord, S.st));
+        RP_HIP(hipStreamWaitEvent((hipStream_t)stream, S.ev_ord, 0));
     });
 }
 

@@ -37,15 +37,31 @@ def _outbox(rank, G, rnd):
     return nm, nr, segs
 
 
-def _worker(rank, G, port, q):
+def _worker(rank, W, port, q, sub=None):
+    """W world ranks; with `sub` (a list of world ranks) the exchange runs on that subgroup only,
+    with its per-peer counts on a side gloo group (the nccl path's count group, built with local
+    synchronization: the ranks outside `sub` never construct anything)."""
     import torch.distributed as dist
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from conftest import load_pkg
     rpa = load_pkg()
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=G)
-    x = rpa.MessageExchange(copy=lambda dst, src, nb: ctypes.memmove(dst, src, nb))
-    ok = True
+    env0 = os.environ.get("GLOO_SOCKET_IFNAME")
+    dist.init_process_group("gloo", rank=rank, world_size=W)
+    group = None
+    if sub is not None:
+        group = dist.new_group(ranks=sub, backend="gloo", use_local_synchronization=True) if rank in sub else None
+        if rank not in sub:
+            q.put((rank, True))
+            dist.destroy_process_group()
+            return
+    x = rpa.MessageExchange(group=group, copy=lambda dst, src, nb: ctypes.memmove(dst, src, nb),
+                            side_counts=sub is not None)
+    G = x.G
+    rank = x.rank
+    ok = os.environ.get("GLOO_SOCKET_IFNAME") == env0  # the environment is restored
+    if sub is not None:
+        ok &= x._cgroup is not None and x._cgroup is not group
     for rnd in range(3):
         nm, nr, segs = _outbox(rank, G, rnd)
         out = np.concatenate(segs + [np.zeros(1, np.uint8)])
@@ -66,7 +82,7 @@ def _worker(rank, G, port, q):
         ok &= in_nm.tolist() == want_nm and in_nr.tolist() == want_nr
         w = np.concatenate(want)
         ok &= np.array_equal(box["b"][:w.size], w)
-    q.put((rank, bool(ok)))
+    q.put((sub[rank] if sub is not None else rank, bool(ok)))
     dist.destroy_process_group()
 
 
@@ -81,3 +97,18 @@ def test_message_exchange_gloo_two_ranks():
     for p in ps:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+def test_message_exchange_on_a_subgroup_with_side_counts():
+    """the exchange built on a subgroup (world 3, ranks {0, 2}) with its counts on a
+    side gloo group; rank 1 takes no part in either group's creation."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker, args=(r, 3, port, q, [0, 2])) for r in range(3)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True, 2: True}

@@ -454,3 +454,37 @@ def test_member_rows_incarnation_range(gpu, orc):
     with pytest.raises(gpu.RingpopAmdError):
         m.checksum
     m.close()
+
+
+@pytest.mark.parametrize("path", ["grouped", "bucket", "set"])
+def test_device_status_past_leave_reported(gpu, path, monkeypatch):
+    """a status past leave (4) on a device call is not masked into alive..leave
+    silently: update_dev (the grouped fold and the bucket fold, whose 8-B records keep 2 status
+    bits) and set_dev report RP_EDEVICE at the handle's next sync, as an incarnation past 2^60
+    does; a valid batch after it works again."""
+    import torch
+
+    if path == "bucket":
+        monkeypatch.setenv("RP_MEMBERS_BUCKET_FOLD", "1")
+    names = ["10.9.1.%d:1" % i for i in range(64)]
+    m = gpu.Membership(whoami=names[0], capacity=64)
+    ids = np.asarray(m.intern(names), dtype=np.uint32)
+    m.update_ids(ids, np.zeros(64, np.uint8), np.full(64, 3, np.int64), now_ms=1)
+    d_ids = torch.from_numpy(ids[1:9].view(np.int32)).cuda()
+    st = np.array([0, 1, 2, 3, 4, 1, 0, 2], np.uint8)
+    d_st = torch.from_numpy(st).cuda()
+    d_inc = torch.full((8,), 9, dtype=torch.int64, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    if path == "set":
+        m.set_ready(False)
+        d_pick = torch.empty(9, dtype=torch.int32, device="cuda")
+        gpu.check(gpu.lib().rp_members_set_dev(m._h, d_ids.data_ptr(), d_st.data_ptr(), d_inc.data_ptr(), 8,
+                                               d_pick.data_ptr(), d_pick.data_ptr() + 32, s))
+    else:
+        m.update_dev(d_ids.data_ptr(), d_st.data_ptr(), d_inc.data_ptr(), 8, 2, None, None, None, None, s)
+    with pytest.raises(gpu.RingpopAmdError, match="status past leave"):
+        m.checksum
+    m.set_ready(True)
+    ga, _, _, gna = m.update_ids(ids[10:12], np.array([1, 2], np.uint8), np.array([7, 7], np.int64), now_ms=3)
+    assert gna == 2 and m.checksum is not None
+    m.close()

@@ -147,14 +147,21 @@ LAYOUTS = {
     "window": {"RP_RING_LAYOUT": "packed"},
     "packed": {"RP_RING_LAYOUT": "packed", "RP_RING_NOWINDOW": "1"},
     "wide": {"RP_RING_WIDE": "1"},
+    # the LDS-index kernel (round 6, k_lookupn_lds): the bucket index in every CU's LDS, one L2 trip
+    # a key; "lds-grid3": three workgroups striding every wave-tile
+    "lds": {"RP_LOOKUP_LDS": "1"},
+    "lds-grid3": {"RP_LOOKUP_LDS": "1", "RP_LOOKUP_LDS_GRID": "3"},
+    "lean": {"RP_LOOKUP_LDS": "0"},
 }
 
 
 def set_layout(monkeypatch, layout):
     for k in ("RP_RING_WIDE", "RP_RING_NOWINDOW", "RP_RING_LAYOUT", "RP_LOOKUP_KPL", "RP_LOOKUP_LEAN", "RP_LOOKUP_HALF",
               "RP_LOOKUP_GRID", "RP_LOOKUP_FUSEFIX", "RP_LOOKUP_WPRED", "RP_LOOKUP_STG", "RP_LOOKUP_LH",
-              "RP_LOOKUP_STGHS", "RP_LOOKUP_HINT"):
+              "RP_LOOKUP_STGHS", "RP_LOOKUP_HINT", "RP_LOOKUP_LDS", "RP_LOOKUP_LDS_GRID"):
         monkeypatch.delenv(k, raising=False)
+    if layout != "compact" and not layout.startswith("lds"):  # every other layout names a lean / older kernel
+        monkeypatch.setenv("RP_LOOKUP_LDS", "0")
     for k, v in LAYOUTS[layout].items():
         monkeypatch.setenv(k, v)
 
@@ -338,6 +345,85 @@ def test_lookup_service_then_growing_batch(gpu, orc):
     ring.service(0)
 
 
+def test_lookup_service_beside_growing_membership(gpu, orc):
+    """a resident service must not stall another handle. A ring with
+    service(3000) answers single-key lookups from a thread every ~2 ms (the per-request
+    RingPop.lookup of handleOrProxy, index.js:434-451) while a Membership in the same process
+    applies batches of new members whose buffers grow 10 -> 10k -> 100k (gossip's update,
+    lib/on_membership_event.js:106-134: both in one process). Before the QuietScope every
+    buffer growth (hipFree) waited for the wave, which the lookups kept resident for up to its
+    30 s lifetime. Each update and checksum read must return in < 50 ms; the updates equal the
+    oracle's, the lookups the ring oracle's."""
+    import threading
+    import time
+    servers = ["svc-m-%d:3000" % i for i in range(64)]
+    ring, roracle = gpu.HashRing(), orc.Ring(100)
+    ring.addRemoveServers(servers)
+    roracle.add_remove(servers)
+    keys = ["req-%d" % i for i in range(512)]
+    want = [roracle.name(roracle.lookup_hash(orc.hash32(k))) for k in keys]
+    ring.service(3000)
+    n = 110_000
+    names = ["10.%d.%d.%d:3000" % (i >> 16, (i >> 8) & 255, i & 255) for i in range(n)]
+    # warm the membership kernels (first-launch code object loads) before any timing
+    w = gpu.Membership(whoami=names[0])
+    w.update_ids(w.intern(names[:20]), [0] * 20, [5] * 20, now_ms=1)
+    _ = w.checksum
+    w.close()
+
+    stop = threading.Event()
+    log = {"n": 0, "bad": [], "lat": []}
+
+    def lookups():
+        i = 0
+        while not stop.is_set():
+            t0 = time.perf_counter()
+            got = ring.name(ring.lookup_ids([keys[i % len(keys)]])[0])
+            log["lat"].append(time.perf_counter() - t0)
+            if got != want[i % len(keys)]:
+                log["bad"].append(i)
+            log["n"] += 1
+            i += 1
+            time.sleep(0.002)
+
+    m = gpu.Membership(whoami=names[0], capacity=16)
+    o = orc.Members(names, local=names[0])
+    th = threading.Thread(target=lookups, daemon=True)
+    th.start()
+    try:
+        lo = 0
+        rng = np.random.default_rng(3)
+        for step, hi in enumerate((10, 10_000, 100_000, n)):
+            # new members (the table, names and checksum buffers grow) plus updates of known ones
+            ids_new = np.arange(lo, hi, dtype=np.uint32)
+            ids_old = rng.integers(0, max(lo, 1), size=(hi - lo) // 4, dtype=np.uint32)
+            ids = np.concatenate([ids_new, ids_old])
+            st = rng.integers(0, 4, size=len(ids), dtype=np.uint8)
+            inc = rng.integers(1, 4, size=len(ids), dtype=np.int64)
+            dev_ids = np.asarray(m.intern([names[i] for i in ids]), dtype=np.uint32)
+            ring.lookup_ids([keys[step]])  # the service wave is resident as the update starts
+            t0 = time.perf_counter()
+            ga, gs, gi, gna = m.update_ids(dev_ids, st, inc, now_ms=100 + step)
+            t_up = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            ck = m.checksum
+            t_ck = time.perf_counter() - t0
+            oa, os_, oi, ona = o.update_ids(ids, st, inc, False, 100 + step)
+            assert gna == ona and np.array_equal(ga > 0, oa > 0), step
+            assert np.array_equal(gs[oa > 0], os_[oa > 0]) and np.array_equal(gi[oa > 0], oi[oa > 0])
+            assert ck == o.checksum, step
+            assert t_up < 0.05 and t_ck < 0.05, (step, hi, t_up, t_ck)
+            lo = hi
+    finally:
+        stop.set()
+        th.join(10)
+    assert not log["bad"] and log["n"] >= 10, log["n"]
+    assert max(log["lat"]) < 0.5, max(log["lat"])
+    ring.service(0)
+    m.close()
+    ring.close()
+
+
 def test_device_farmhash_and_keygen(gpu, orc):
     rng = random.Random(2)
     strs = [bytes(rng.randrange(256) for _ in range(n)) for n in list(range(0, 80)) * 3 + [500, 4096]]
@@ -399,7 +485,8 @@ def _c2_oracle_owners(orc, oracle, n):
     return _C2_OWNERS[n]
 
 
-@pytest.mark.parametrize("layout", ["compact", "round1", "lean-kpl4", "half-kpl8", "fusefix", "wpred0", "stg2", "stg1", "hint0"])
+@pytest.mark.parametrize("layout", ["compact", "round1", "lean-kpl4", "half-kpl8", "fusefix", "wpred0", "stg2", "stg1", "hint0",
+                                    "lds", "lean"])
 def test_c2_full_size_properties(gpu, orc, layout, monkeypatch):
     set_layout(monkeypatch, layout)
     # C2: 10k servers x 100 points (~1M tokens); 2^24 keys on device; size-independent

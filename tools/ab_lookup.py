@@ -69,10 +69,17 @@ def main():
         "grid6144/lookupN3": ({"RP_LOOKUP_GRID": "6144"}, 3),
         "grid16384/lookupN3": ({"RP_LOOKUP_GRID": "16384"}, 3),
         "grid32768/lookupN3": ({"RP_LOOKUP_GRID": "32768"}, 3),
+        # round 6: the LDS-index kernel against the lean kernel
+        "lds/lookupN3": ({"RP_LOOKUP_LDS": "1"}, 3),
+        "lean/lookupN3": ({"RP_LOOKUP_LDS": "0"}, 3),
+        "lds/lookup": ({"RP_LOOKUP_LDS": "1"}, 1),
+        "lean/lookup": ({"RP_LOOKUP_LDS": "0"}, 1),
+        "lds-g512/lookupN3": ({"RP_LOOKUP_LDS": "1", "RP_LOOKUP_LDS_GRID": "512"}, 3),
+        "lds-g128/lookupN3": ({"RP_LOOKUP_LDS": "1", "RP_LOOKUP_LDS_GRID": "128"}, 3),
     }
     if a.only:
         variants = {k: v for k, v in variants.items() if k in a.only.split(",")}
-    knobs = ("RP_LOOKUP_HALF", "RP_LOOKUP_LEAN", "RP_LOOKUP_KPL", "RP_RING_LAYOUT", "RP_LOOKUP_ABLATE", "RP_RING_WIDE", "RP_LOOKUP_GRID", "RP_LOOKUP_OCC", "RP_LOOKUP_STG", "RP_LOOKUP_LH", "RP_LOOKUP_STGHS")
+    knobs = ("RP_LOOKUP_HALF", "RP_LOOKUP_LEAN", "RP_LOOKUP_KPL", "RP_RING_LAYOUT", "RP_LOOKUP_ABLATE", "RP_RING_WIDE", "RP_LOOKUP_GRID", "RP_LOOKUP_OCC", "RP_LOOKUP_STG", "RP_LOOKUP_LH", "RP_LOOKUP_STGHS", "RP_LOOKUP_LDS", "RP_LOOKUP_LDS_GRID")
     times = {k: [] for k in variants}
     digests = {}
     for r in range(a.rounds + 1):
