@@ -107,10 +107,12 @@ int rp_ring_lookupn(rp_ring *r, const char *keys, const uint64_t *off, uint32_t 
  * polls a pinned, device-mapped request line and reads one record of its direct table (built at
  * its first launch after a ring change), instead of a kernel launch and a stream sync per call. The wave exits after idle_ms without a
  * request (and after 30 s in all) and is relaunched by the next call; a ring mutation and every
- * other device call on this ring (batch lookups, grouping, dump) stop it first. While it is
- * resident, a device-buffer release anywhere else in the process (another handle's buffer
- * growing: hipFree synchronizes the device) waits for it to idle out: keep idle_ms short where
- * other handles allocate. idle_ms = 0 (the default) turns it off. */
+ * other device call on this ring (batch lookups, grouping, dump) stop it first. Every device
+ * call of this library on any other handle stops every resident service as well and keeps new
+ * ones from starting until it returns (a resident wave would make its hipFree wait, and its
+ * stream may share a hardware queue), so no call of the library waits for a wave to idle out;
+ * device work queued outside the library is not covered. idle_ms = 0 (the default) turns it
+ * off. */
 int rp_ring_service(rp_ring *r, uint32_t idle_ms);
 /* Same with precomputed key hashes (hashFunc(key) done by the caller). */
 int rp_ring_lookup_hashes(rp_ring *r, const uint32_t *hashes, uint64_t n, uint32_t *owners);

@@ -1139,9 +1139,10 @@ __global__ __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(4)))
 // once, and each wave then streams its own tiles of 64 x KPL keys: 16-B non-temporal key loads,
 // transposed through the wave's 2.3-KB LDS slice (one key per lane per slice) and hashed; the
 // group record from LDS gives the bucket's first position and token count; the window is 10
-// entries (32 B, two 16-B loads) from max(0, floor(u c) - 3) into the bucket (u: the key's place in
-// the bucket's hash range), which holds the key's position and its NEED owners for all but ~0.6 %
-// of C2 keys (a fingerprint tie: 0.43 %; a window that misses; a long bucket; the ring end). Those
+// entries (32 B, two 16-B loads) from max(0, floor(u c) - 4) into the bucket (u: the key's place in
+// the bucket's hash range), which holds the key's position and its NEED owners for all but ~0.45 %
+// of C2 keys (a fingerprint tie: 0.43 %; a window that misses; a group with a bucket of 16+
+// tokens; the ring end: the numpy emulation of the C2 ring in tools/emu_lds.py). Those
 // are deferred to k_lookupn_fix_tiles (the exact tokens) through the per-tile lists, as in the
 // compact kernels.
 struct LdsView {
@@ -1154,7 +1155,13 @@ constexpr bool kLdsDefault = false;      // RP_LOOKUP_LDS=1 selects it (A/B)
 constexpr int kLdsThreads = 768;          // 12 waves: one workgroup a CU (the index takes up to 128 KB)
 constexpr uint32_t kLdsMaxGroups = 8192;  // 128 KB of group records
 
-template <int KPL, int NEED>
+// STG 0: each lane loads its own keys (three loads per 36-B key: 16 + 16 + 4 B at a 36-B stride;
+// the lines a wave touches are the same as the coalesced form's), no LDS transposition; STG 1:
+// 16-B coalesced loads transposed through the wave's LDS slice (A/B: RP_LOOKUP_LDS_STG).
+// ABL (diagnostics, RP_LOOKUP_LDS_ABL; results wrong, times only): 1 = no window loads (entries
+// made from the group record), 2 = no LDS index read (a record made from the hash), 4 = rows not
+// stored (one store of their xor per lane-tile).
+template <int KPL, int NEED, int STG = 0, int ABL = 0>
 __global__ __launch_bounds__(kLdsThreads) __attribute__((amdgpu_waves_per_eu(3))) void k_lookupn_lds(
     const uint8_t* __restrict__ keys, uint64_t nwt, LdsView lv, uint32_t* __restrict__ out,
     uint8_t* __restrict__ counts, uint32_t* __restrict__ slow_list, uint32_t* __restrict__ slow_cnt) {
@@ -1165,7 +1172,7 @@ __global__ __launch_bounds__(kLdsThreads) __attribute__((amdgpu_waves_per_eu(3))
     constexpr int SV = 64 * W4 / 4;    // vectors per slice of 64 keys
     static_assert(V4 % 64 == 0 && NEED >= 1 && NEED <= 4, "tile shape");
     __shared__ uint4 s_idx[kLdsMaxGroups];
-    __shared__ __attribute__((aligned(16))) uint32_t s_key[NWV][64 * W4];
+    __shared__ __attribute__((aligned(16))) uint32_t s_key[STG ? NWV : 1][64 * W4];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     for (uint32_t i = tid; i < lv.ng; i += kLdsThreads) s_idx[i] = lv.idx[i];
     __syncthreads();
@@ -1173,18 +1180,32 @@ __global__ __launch_bounds__(kLdsThreads) __attribute__((amdgpu_waves_per_eu(3))
     const uint32_t fsh = 32u - lv.fb;
     const __amdgpu_buffer_rsrc_t ent_r =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(lv.ent), 0, (int)lv.ent_bytes, 0x00020000);
-    uint32_t* const sk = s_key[wv];
+    uint32_t* const sk = s_key[STG ? wv : 0];
     const uint64_t nwaves = (uint64_t)gridDim.x * NWV;
     auto nsum = [](uint32_t w, uint32_t acc) {  // the sum of w's eight nibbles, plus acc
         return __builtin_amdgcn_sad_u8(w & 0x0F0F0F0Fu, 0u, __builtin_amdgcn_sad_u8((w >> 4) & 0x0F0F0F0Fu, 0u, acc));
     };
     for (uint64_t wt = (uint64_t)blockIdx.x * NWV + wv; wt < nwt; wt += nwaves) {
         const uint64_t base = wt * TK;
+        uint32_t h[KPL];
+        if constexpr (STG == 0) {
+            uint32_t kw[KPL][W4];
+#pragma unroll
+            for (int k = 0; k < KPL; k++) {
+                const uint32_t* src = reinterpret_cast<const uint32_t*>(keys + (base + (uint64_t)k * 64 + lane) * LEN);
+                const u32x4_a4 a = *reinterpret_cast<const u32x4_a4*>(src);
+                const u32x4_a4 b = *reinterpret_cast<const u32x4_a4*>(src + 4);
+                kw[k][0] = a.x; kw[k][1] = a.y; kw[k][2] = a.z; kw[k][3] = a.w;
+                kw[k][4] = b.x; kw[k][5] = b.y; kw[k][6] = b.z; kw[k][7] = b.w;
+                kw[k][8] = src[8];
+            }
+#pragma unroll
+            for (int k = 0; k < KPL; k++) h[k] = fh::hash32_words<LEN>(kw[k]);
+        } else {
         const u32x4* s4 = reinterpret_cast<const u32x4*>(keys + base * LEN);
         u32x4 pre[PER];
 #pragma unroll
         for (int q = 0; q < PER; q++) pre[q] = __builtin_nontemporal_load(s4 + lane + 64 * q);
-        uint32_t h[KPL];
 #pragma unroll
         for (int k = 0; k < KPL; k++) {  // slice k: keys k * 64 + lane, one per lane
 #pragma unroll
@@ -1199,15 +1220,19 @@ __global__ __launch_bounds__(kLdsThreads) __attribute__((amdgpu_waves_per_eu(3))
             h[k] = fh::hash32_words<LEN>(w);
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         }
+        }  // STG
         // the group records (LDS), every key's window start, both window loads in flight
         uint32_t w0[KPL], bc[KPL], sw[KPL], K[KPL];
+        bool gfull[KPL];
         u32x4 wa[KPL], wb[KPL];
 #pragma unroll
         for (int k = 0; k < KPL; k++) {
             const uint32_t x = h[k] << lg;
             const uint64_t t = (uint64_t)x * 28u;
             const uint32_t j = (uint32_t)(t >> 32), fr = (uint32_t)t, g = h[k] >> gsh;
-            const uint4 rec = s_idx[g];
+            const uint4 rec = (ABL & 2) ? uint4{h[k] & 0x11111111u, h[k] & 0x22222222u, fr & 0x11111111u,
+                                                (h[k] & 0x00FF1111u)}
+                                        : s_idx[g];
             const uint32_t jb = 4u * j;  // the bucket's bit offset among the 112 count bits
             const uint32_t m0 = jb >= 32u ? ~0u : (1u << jb) - 1u;
             const uint32_t m1 = jb >= 64u ? ~0u : jb <= 32u ? 0u : (1u << (jb - 32u)) - 1u;
@@ -1218,15 +1243,22 @@ __global__ __launch_bounds__(kLdsThreads) __attribute__((amdgpu_waves_per_eu(3))
             const uint32_t c = (cw >> (jb & 31u)) & 15u;
             const uint32_t st = (uint32_t)(((uint64_t)g * lv.M) >> lg) + (uint32_t)((int32_t)rec.w >> 16) + below;
             const uint32_t fl = ((fr >> 24) * c) >> 8;  // about the key's position in the bucket
-            const uint32_t s = fl > 3u ? fl - 3u : 0u;
-            w0[k] = st + s;
+            const uint32_t s = fl > 4u ? fl - 4u : 0u;
+            gfull[k] = (rec.w >> 16) == 0x8000u;
+            w0[k] = gfull[k] ? 0u : st + s;
             sw[k] = s;
             bc[k] = c;
             K[k] = (fr >> fsh) << lv.ob;
-            wa[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ent_r, (int)(3u * w0[k]), 0, 0));
-            wb[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ent_r, (int)(3u * w0[k] + 16u), 0, 0));
+            if constexpr ((ABL & 1) != 0) {
+                wa[k] = u32x4{rec.x, rec.y, rec.z, w0[k]};
+                wb[k] = u32x4{rec.w, K[k], fr, st};
+            } else {
+                wa[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ent_r, (int)(3u * w0[k]), 0, 0));
+                wb[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ent_r, (int)(3u * w0[k] + 16u), 0, 0));
+            }
         }
         uint32_t nsl = 0;  // wave-uniform: this wave-tile's deferred keys
+        uint32_t sink = 0;
 #pragma unroll
         for (int k = 0; k < KPL; k++) {
             const u32x4 a = wa[k], b = wb[k];
@@ -1261,21 +1293,26 @@ __global__ __launch_bounds__(kLdsThreads) __attribute__((amdgpu_waves_per_eu(3))
                     rc++;
                 }
             }
-            // deferred: a tie, a bucket of 15+ tokens, the key before the window (its guard entry
+            // deferred: a tie, a group with a bucket of 16+ tokens, the key before the window (its guard entry
             // is not below it) or past it, owners not distinct inside it, the ring end
-            const bool slow = tie | (bc[k] == 15u) | (sw[k] > 0u && lt == 0u) | (lt == 10u) | (rc < (uint32_t)NEED) |
+            const bool slow = tie | gfull[k] | (sw[k] > 0u && lt == 0u) | (lt == 10u) | (rc < (uint32_t)NEED) |
                               (w0[k] + 12u > lv.M);
             const uint32_t kk = (uint32_t)k * 64u + lane;
             uint32_t* row = out + (base + kk) * NEED;
+            if constexpr ((ABL & 4) != 0) {
+                sink ^= res[0] ^ res[1] ^ res[2] ^ res[3];
+            } else {
 #pragma unroll
-            for (int q = 0; q < NEED; q++) __builtin_nontemporal_store(res[q], row + q);
-            if (counts) counts[base + kk] = (uint8_t)NEED;
+                for (int q = 0; q < NEED; q++) __builtin_nontemporal_store(res[q], row + q);
+                if (counts) counts[base + kk] = (uint8_t)NEED;
+            }
             const uint64_t m = __ballot(slow);
             const uint32_t pos = nsl + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             if (slow && pos < kSlowPerTile) slow_list[wt * kSlowPerTile + pos] = kk;
             nsl += (uint32_t)__popcll(m);
         }
         if (lane == 0) slow_cnt[wt] = nsl;
+        if constexpr ((ABL & 4) != 0) out[(base + lane) * NEED] = sink;
     }
 }
 
@@ -1979,16 +2016,20 @@ __global__ void k_lidx_build(const uint32_t* __restrict__ tok, uint32_t M, uint3
         uint32_t w[4] = {0, 0, 0, 0};
         uint32_t p = lds_first_pos(tok, M, lg, (uint32_t)g, 0);
         const uint32_t base = p;
+        bool full = false;
         for (uint32_t j = 0; j < 28; j++) {
             const uint32_t q = j == 27 ? (g + 1 == ng ? M : lds_first_pos(tok, M, lg, (uint32_t)g + 1, 0))
                                        : lds_first_pos(tok, M, lg, (uint32_t)g, j + 1);
             const uint32_t c = q - p;
-            w[j >> 3] |= (c > 15u ? 15u : c) << (4 * (j & 7));  // 15: the bucket's keys take the exact path
+            full |= c > 15u;
+            w[j >> 3] |= (c > 15u ? 15u : c) << (4 * (j & 7));
             p = q;
         }
         const int64_t delta = (int64_t)base - (int64_t)(((uint64_t)g * M) >> lg);
-        if (delta < -32768 || delta > 32767) atomicOr(over, 1u);
-        w[3] |= ((uint32_t)delta & 0xFFFFu) << 16;
+        if (delta < -32767 || delta > 32767) atomicOr(over, 1u);
+        // a bucket of 16+ tokens: the counts no longer sum to positions, so every key of the group
+        // takes the exact path (delta -32768 marks it)
+        w[3] |= (full ? 0x8000u : ((uint32_t)delta & 0xFFFFu)) << 16;
         idx[g] = uint4{w[0], w[1], w[2], w[3]};
     }
 }
@@ -2441,12 +2482,34 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
                                                             (nwt + kLdsThreads / 64 - 1) / (kLdsThreads / 64));
             const LdsView lv{r.lent.p, r.lidx.p, r.M, r.lng, r.llg, r.lfb, r.cob,
                              (uint32_t)(3ull * ((uint64_t)r.M + kEnt3Pad + 6) + 16)};
-            switch (need) {
-                case 1: hipLaunchKernelGGL((k_lookupn_lds<KPL, 1>), dim3(g), dim3(kLdsThreads), 0, st, keys, nwt, lv, out, counts, r.slow.p, r.nslow.p); break;
-                case 2: hipLaunchKernelGGL((k_lookupn_lds<KPL, 2>), dim3(g), dim3(kLdsThreads), 0, st, keys, nwt, lv, out, counts, r.slow.p, r.nslow.p); break;
-                case 3: hipLaunchKernelGGL((k_lookupn_lds<KPL, 3>), dim3(g), dim3(kLdsThreads), 0, st, keys, nwt, lv, out, counts, r.slow.p, r.nslow.p); break;
-                default: hipLaunchKernelGGL((k_lookupn_lds<KPL, 4>), dim3(g), dim3(kLdsThreads), 0, st, keys, nwt, lv, out, counts, r.slow.p, r.nslow.p); break;
+            const int stg = (int)env_pos("RP_LOOKUP_LDS_STG", 0) == 1 ? 1 : 0;
+            const int abl = getenv("RP_LOOKUP_LDS_ABL") ? atoi(getenv("RP_LOOKUP_LDS_ABL")) : 0;
+#define RP_LDSK(N, S, A) \
+    hipLaunchKernelGGL((k_lookupn_lds<KPL, N, S, A>), dim3(g), dim3(kLdsThreads), 0, st, keys, nwt, lv, out, counts, r.slow.p, r.nslow.p)
+            if (need == 3 && abl) {  // diagnostics: time ablations (results wrong)
+                switch (abl) {
+                    case 1: RP_LDSK(3, 0, 1); break;
+                    case 2: RP_LDSK(3, 0, 2); break;
+                    case 3: RP_LDSK(3, 0, 3); break;
+                    case 4: RP_LDSK(3, 0, 4); break;
+                    default: RP_LDSK(3, 0, 7); break;
+                }
+            } else if (stg) {
+                switch (need) {
+                    case 1: RP_LDSK(1, 1, 0); break;
+                    case 2: RP_LDSK(2, 1, 0); break;
+                    case 3: RP_LDSK(3, 1, 0); break;
+                    default: RP_LDSK(4, 1, 0); break;
+                }
+            } else {
+                switch (need) {
+                    case 1: RP_LDSK(1, 0, 0); break;
+                    case 2: RP_LDSK(2, 0, 0); break;
+                    case 3: RP_LDSK(3, 0, 0); break;
+                    default: RP_LDSK(4, 0, 0); break;
+                }
             }
+#undef RP_LDSK
             RP_HIP(hipGetLastError());
             const CompactFixView fv{r.tok.p, r.own.p, r.cidx.p, r.view(), r.M, r.ccb};
             const uint64_t fthreads = nwt * kSlowPerTile;

@@ -58,3 +58,6 @@ def test_bench_four_ranks_spawned_with_merge(gpu):
     assert out["sim_c5"]["n_gpus"] == 4 and out["sim_c5"]["converged"]
     assert out["merge"]["n_gpus"] == 4 and out["merge"]["updates_per_s"] > 0
     assert isinstance(out["merge"]["checksum"], int)
+    # the exchange's host and device time per round, shown with -rP
+    print("sim_c5 exchange:", json.dumps({k: v for k, v in out["sim_c5"].items()
+                                          if k.startswith("exchange") or k in ("rounds", "round_ms")}))

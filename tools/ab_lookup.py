@@ -76,10 +76,16 @@ def main():
         "lean/lookup": ({"RP_LOOKUP_LDS": "0"}, 1),
         "lds-g512/lookupN3": ({"RP_LOOKUP_LDS": "1", "RP_LOOKUP_LDS_GRID": "512"}, 3),
         "lds-g128/lookupN3": ({"RP_LOOKUP_LDS": "1", "RP_LOOKUP_LDS_GRID": "128"}, 3),
+        "lds-stg1/lookupN3": ({"RP_LOOKUP_LDS": "1", "RP_LOOKUP_LDS_STG": "1"}, 3),
+        "lds-abl1/lookupN3": ({"RP_LOOKUP_LDS": "1", "RP_LOOKUP_LDS_ABL": "1"}, 3),
+        "lds-abl2/lookupN3": ({"RP_LOOKUP_LDS": "1", "RP_LOOKUP_LDS_ABL": "2"}, 3),
+        "lds-abl3/lookupN3": ({"RP_LOOKUP_LDS": "1", "RP_LOOKUP_LDS_ABL": "3"}, 3),
+        "lds-abl4/lookupN3": ({"RP_LOOKUP_LDS": "1", "RP_LOOKUP_LDS_ABL": "4"}, 3),
+        "lds-abl7/lookupN3": ({"RP_LOOKUP_LDS": "1", "RP_LOOKUP_LDS_ABL": "7"}, 3),
     }
     if a.only:
         variants = {k: v for k, v in variants.items() if k in a.only.split(",")}
-    knobs = ("RP_LOOKUP_HALF", "RP_LOOKUP_LEAN", "RP_LOOKUP_KPL", "RP_RING_LAYOUT", "RP_LOOKUP_ABLATE", "RP_RING_WIDE", "RP_LOOKUP_GRID", "RP_LOOKUP_OCC", "RP_LOOKUP_STG", "RP_LOOKUP_LH", "RP_LOOKUP_STGHS", "RP_LOOKUP_LDS", "RP_LOOKUP_LDS_GRID")
+    knobs = ("RP_LOOKUP_HALF", "RP_LOOKUP_LEAN", "RP_LOOKUP_KPL", "RP_RING_LAYOUT", "RP_LOOKUP_ABLATE", "RP_RING_WIDE", "RP_LOOKUP_GRID", "RP_LOOKUP_OCC", "RP_LOOKUP_STG", "RP_LOOKUP_LH", "RP_LOOKUP_STGHS", "RP_LOOKUP_LDS", "RP_LOOKUP_LDS_GRID", "RP_LOOKUP_LDS_STG", "RP_LOOKUP_LDS_ABL")
     times = {k: [] for k in variants}
     digests = {}
     for r in range(a.rounds + 1):
