@@ -980,11 +980,13 @@ struct MckItem {
     uint64_t noff;
     uint32_t w[8];
 };
+// snap (nullable): the rows in rank order, as k_ovf_len copied them (the side-stream build reads
+// the copy, coalesced, while the next batch folds the table)
 __device__ __forceinline__ void mck_load(uint32_t i, const uint32_t* __restrict__ order, uint32_t n,
                                          const MRow* __restrict__ rows, const uint32_t* __restrict__ soff,
-                                         MckItem& t) {
-    t.id = i < n ? order[i] : 0u;
-    t.row = row_load(rows + t.id);
+                                         MckItem& t, const uint64_t* __restrict__ snap = nullptr) {
+    t.id = snap ? 0u : (i < n ? order[i] : 0u);
+    t.row = snap ? row_unpack(i < n ? snap[i] : 0ull) : row_load(rows + t.id);
     t.noff = i < n ? soff[i] : 0u;
     t.nlen = i < n ? soff[i + 1] - (uint32_t)t.noff : 0u;
     t.len = (i < n && t.row.exists) ? t.nlen + status_len(t.row.status) + dec_len(t.row.inc) + 1u : 0u;
@@ -1032,7 +1034,8 @@ __global__ __launch_bounds__(256) void k_ovf_len(const uint32_t* __restrict__ or
                                                  const uint32_t* __restrict__ soff, uint32_t* __restrict__ tile_tot,
                                                  const uint32_t* __restrict__ ids, uint32_t k, uint32_t* ovf, FoldArgs A,
                                                  uint32_t* part, uint32_t nparts, uint32_t* __restrict__ out,
-                                                 uint32_t* tick, uint32_t* err) {
+                                                 uint32_t* tick, uint32_t* err, uint64_t* __restrict__ snap,
+                                                 uint32_t* __restrict__ gate_copy) {
     __shared__ uint32_t s_on, s_t, s_w[4];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     if (tid == 0) s_on = __hip_atomic_load(ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1065,6 +1068,7 @@ __global__ __launch_bounds__(256) void k_ovf_len(const uint32_t* __restrict__ or
     }
     MckItem t;
     mck_load(blockIdx.x * 256u + tid, order, n, A.rows, soff, t);
+    if (snap && blockIdx.x * 256u + tid < n) snap[blockIdx.x * 256u + tid] = row_pack(t.row.inc, t.row.status, t.row.exists);
     const uint32_t total = block_sum256(t.len);
     if (tid == 0) tile_tot[blockIdx.x] = total;
     if (blockIdx.x == 0) {
@@ -1079,6 +1083,7 @@ __global__ __launch_bounds__(256) void k_ovf_len(const uint32_t* __restrict__ or
             const uint32_t a = s_w[0] + s_w[1] + s_w[2] + s_w[3];
             *A.n_applied = a;
             if (out) *out = a;
+            if (gate_copy) *gate_copy = a;
         }
     }
 }
@@ -1097,7 +1102,7 @@ __global__ __launch_bounds__(256) void k_mck_write(const uint32_t* __restrict__ 
                                                    const MRow* __restrict__ rows, const uint8_t* __restrict__ names,
                                                    const uint32_t* __restrict__ soff, const uint32_t* __restrict__ gate,
                                                    const uint32_t* __restrict__ tile_tot, uint8_t* __restrict__ buf,
-                                                   uint32_t* __restrict__ meta) {
+                                                   uint32_t* __restrict__ meta, const uint64_t* __restrict__ snap) {
     __shared__ uint32_t s_wsum[4], s_pre[4];
     __shared__ uint32_t s_stage[kMckStage / 4 + 4];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, tile = blockIdx.x;
@@ -1112,7 +1117,7 @@ __global__ __launch_bounds__(256) void k_mck_write(const uint32_t* __restrict__ 
     uint32_t pre = 0;  // this thread's share of the earlier tiles' totals
     for (uint32_t q = tid; q < tile; q += 256) pre += tile_tot[q];
     MckItem t;
-    mck_load(tile * 256u + tid, order, n, rows, soff, t);
+    mck_load(tile * 256u + tid, order, n, rows, soff, t, snap);
     mck_load_name(names, t);
     // inclusive scan of the lengths within each wave; wave totals and prefix shares
     uint32_t x = t.len;
@@ -1534,14 +1539,43 @@ struct Members {
         uint32_t nparts;
         uint32_t* out;
     };
+    // Side build (round 6; RP_MEMBERS_SIDE_BUILD=0 turns it off): for an update batch the length
+    // launch (k_ovf_len) also copies every member's row in rank order and the batch's applied count
+    // into one of two snapshot buffers, and the string writer (k_mck_write) runs on a build stream
+    // from that copy, so the main stream goes on to the next batch's fold instead of waiting for the
+    // writer. A snapshot buffer is rewritten only after the writer that read it (event); the group
+    // of slots is flushed from the build stream.
+    hipStream_t bs = nullptr;                     // the build stream
+    hipEvent_t ev_len = nullptr, ev_snap[2] = {};  // lengths + snapshot ready; snapshot p free again
+    bool snap_busy[2] = {false, false};
+    uint32_t snap_p = 0;
+    DevBuf<uint64_t> snap_rows[2];
+    DevBuf<uint32_t> snap_tiles[2], snap_gate;
+    hipStream_t pend_main = nullptr;  // the caller's stream of the pending group
+    // the writer reads the names' rank order and bytes (nt.sorted / soff / sbytes): a call that
+    // may rewrite them (interning, the wire codec's name index) waits for it first
+    void settle_build() {
+        if (bs) RP_HIP(hipStreamSynchronize(bs));
+    }
+    bool side_build() const {
+        const char* e = getenv("RP_MEMBERS_SIDE_BUILD");
+        return !(e && *e == '0');
+    }
     void checksum_dev(hipStream_t s, const uint32_t* gate, bool is_batch = false, const OvfArgs* ov = nullptr) {
         const uint32_t n = nt.size();
         if (!n) return;
         ck_len.reserve(n + 1);
         ck_pos.reserve(n + 1);
+        const bool side = ov != nullptr && side_build();
+        if (side && !bs) {
+            RP_HIP(hipStreamCreateWithFlags(&bs, hipStreamNonBlocking));
+            RP_HIP(hipEventCreateWithFlags(&ev_len, hipEventDisableTiming));
+            for (auto& e : ev_snap) RP_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
+        const hipStream_t bst = side ? bs : s;  // where this string is written
         // worst-case string: names + ';' + "suspect" + 20 digits per member
         const uint64_t need = (nt.h_bytes.size() + (uint64_t)n * 29 + 16 + 255) & ~255ull;
-        if (npending && (s != pend_st || need > slot_bytes)) {  // keep the group on one stream
+        if (npending && (s != pend_main || bst != pend_st || need > slot_bytes)) {  // keep the group on one stream
             flush_checksums();
             RP_HIP(hipStreamSynchronize(pend_st));
         }
@@ -1552,6 +1586,7 @@ struct Members {
         }
         if (need > slot_bytes) {
             RP_HIP(hipStreamSynchronize(ck_st));  // no chain still reads the old pool
+            if (bs) RP_HIP(hipStreamSynchronize(bs));  // no writer still writes it
             for (auto& b : group_busy) b = false;
             cur_group = 0;
             ck_buf.release();
@@ -1568,30 +1603,63 @@ struct Members {
         }
         if (npending == group_slots) flush_checksums();
         if (npending == 0 && group_busy[cur_group]) {  // this group's previous strings must be hashed
-            RP_HIP(hipStreamWaitEvent(s, ev_hashed[cur_group], 0));
+            RP_HIP(hipStreamWaitEvent(bst, ev_hashed[cur_group], 0));
             group_busy[cur_group] = false;
         }
-        pend_st = s;
+        pend_st = bst;
+        pend_main = s;
         ck_meta.reserve(4 * kMaxSlots);
         uint8_t* buf = ck_buf.p + slot_bytes * slot_index(npending);
         {
             const uint32_t ntl = (n + 255) / 256;
-            ck_tiles.reserve(ntl);
             uint32_t* meta = ck_meta.p + 4ull * slot_index(npending);
             if (ov) {
                 if (!ws.err.p) {
                     ws.err.reserve(1);
                     RP_HIP(hipMemsetAsync(ws.err.p, 0, sizeof(uint32_t), s));
                 }
-                hipLaunchKernelGGL(k_ovf_len, dim3(ntl), dim3(256), 0, s, nt.sorted.p, n, nt.soff.p, ck_tiles.p,
+                uint64_t* snap = nullptr;
+                uint32_t* tiles = nullptr;
+                uint32_t* gcopy = nullptr;
+                if (side) {
+                    const uint32_t p = snap_p;
+                    if (snap_busy[p]) RP_HIP(hipStreamWaitEvent(s, ev_snap[p], 0));  // its writer has read it
+                    if (snap_rows[p].cap < n) {
+                        RP_HIP(hipStreamSynchronize(bs));
+                        snap_rows[p].reserve(n);
+                    }
+                    snap_tiles[p].reserve(ntl);
+                    snap_gate.reserve(2);
+                    snap = snap_rows[p].p;
+                    tiles = snap_tiles[p].p;
+                    gcopy = snap_gate.p + p;
+                } else {
+                    ck_tiles.reserve(ntl);
+                    tiles = ck_tiles.p;
+                }
+                hipLaunchKernelGGL(k_ovf_len, dim3(ntl), dim3(256), 0, s, nt.sorted.p, n, nt.soff.p, tiles,
                                    ov->ids, ov->k, ov->ovf, ov->A, ov->part, ov->nparts, ov->out,
-                                   napplied.p + 2 + 2, ws.err.p);
+                                   napplied.p + 2 + 2, ws.err.p, snap, gcopy);
+                if (side) {
+                    const uint32_t p = snap_p;
+                    RP_HIP(hipEventRecord(ev_len, s));
+                    RP_HIP(hipStreamWaitEvent(bs, ev_len, 0));
+                    hipLaunchKernelGGL(k_mck_write, dim3(ntl), dim3(256), 0, bs, nt.sorted.p, n, rows.p, nt.sbytes.p,
+                                       nt.soff.p, gcopy, tiles, buf, meta, (const uint64_t*)snap);
+                    RP_HIP(hipEventRecord(ev_snap[p], bs));
+                    snap_busy[p] = true;
+                    snap_p ^= 1u;
+                } else {
+                    hipLaunchKernelGGL(k_mck_write, dim3(ntl), dim3(256), 0, s, nt.sorted.p, n, rows.p, nt.sbytes.p,
+                                       nt.soff.p, gate, tiles, buf, meta, (const uint64_t*)nullptr);
+                }
             } else {
+                ck_tiles.reserve(ntl);
                 hipLaunchKernelGGL(k_mck_len, dim3(ntl), dim3(256), 0, s, nt.sorted.p, n, rows.p, nt.soff.p,
                                    ck_tiles.p);
+                hipLaunchKernelGGL(k_mck_write, dim3(ntl), dim3(256), 0, s, nt.sorted.p, n, rows.p, nt.sbytes.p,
+                                   nt.soff.p, gate, ck_tiles.p, buf, meta, (const uint64_t*)nullptr);
             }
-            hipLaunchKernelGGL(k_mck_write, dim3(ntl), dim3(256), 0, s, nt.sorted.p, n, rows.p, nt.sbytes.p,
-                               nt.soff.p, gate, ck_tiles.p, buf, meta);
         }
         RP_HIP(hipGetLastError());
         if (is_batch && hist_cap) pend_mask.w[npending >> 6] |= 1ull << (npending & 63);
@@ -1631,6 +1699,13 @@ struct Members {
         for (auto& b : group_busy) b = false;
     }
     void release_streams() {
+        if (bs) {
+            (void)hipStreamSynchronize(bs);
+            (void)hipStreamDestroy(bs);
+            (void)hipEventDestroy(ev_len);
+            for (auto& e : ev_snap) (void)hipEventDestroy(e);
+            bs = nullptr;
+        }
         if (ck_st) {
             (void)hipStreamSynchronize(ck_st);
             (void)hipStreamDestroy(ck_st);
@@ -1657,6 +1732,7 @@ namespace rp {
 // The interned addresses the wire codec (rp_wire.hip) reads and resolves against.
 NameTable& members_names(rp_members* h, hipStream_t* st, Scratch** ws) {
     Members& m = MB(h);
+    m.settle_build();
     *st = m.st;
     *ws = &m.ws;
     return m.nt;
@@ -1713,6 +1789,7 @@ int rp_members_intern(rp_members* h, const char* bytes, const uint32_t* off, uin
     return guard([&] {
         rp::Members& m = MB(h);
         RP_REQUIRE(n == 0 || (bytes && off), "intern: null names");
+        m.settle_build();
         for (uint32_t i = 0; i < n; i++) {
             const uint32_t id = m.nt.intern(bytes + off[i], off[i + 1] - off[i]);
             if (ids_out) ids_out[i] = id;

@@ -59,12 +59,15 @@ def test_members_match_reference_goldens(gpu, case_name, fold, monkeypatch):
                 assert m.generate_checksum_string() == op["checksumString"]
 
 
-@pytest.mark.parametrize("fold", ["default", "bucket"])
+@pytest.mark.parametrize("fold", ["default", "bucket", "noside"])
 def test_c3_merge_vs_oracle(gpu, orc, fold, monkeypatch):
     """C3 at full size: 100k members, 100k updates with 1% duplicated addresses (25 buckets of
-    4,096 ids on the bucket path)."""
+    4,096 ids on the bucket path). "noside": the checksum string written on the caller's stream
+    (RP_MEMBERS_SIDE_BUILD=0) instead of the build stream from the row snapshot (round 6)."""
     if fold == "bucket":
         monkeypatch.setenv("RP_MEMBERS_BUCKET_FOLD", "1")
+    if fold == "noside":
+        monkeypatch.setenv("RP_MEMBERS_SIDE_BUILD", "0")
     S = synth()
     n = k = 100_000
     names, st0, inc0 = S.c3_members(n)
