@@ -49,6 +49,12 @@ int rp_hash32_batch_dev(const uint8_t *d_bytes, const uint64_t *d_off, uint64_t 
  * lib/ring/index.js:96-105 and lib/membership/index.js:48-75 are hashed this way): one serial
  * chain fed by producer lanes. d_out[0] = hash (d_out must hold 2 uint32). */
 int rp_hash32_long_dev(const uint8_t *d_bytes, uint64_t len, uint32_t *d_out, void *stream);
+/* farmhash32 of n long device strings side by side (the membership checksum groups): string b
+ * is d_bytes + b * stride; d_meta[4b] = its length + 1 (a builder's piece total), d_meta[4b + 1]
+ * = its gate (0: skipped, nothing written); the hash goes to d_meta[4b + 2] and d_meta[4b + 3] =
+ * 1. Each string must be readable 12 bytes past its end. 16-B aligned strings at a 16-B multiple
+ * stride run kHpStr strings a workgroup (RP_HL_PACK=0: one a workgroup). */
+int rp_hash32_long_multi_dev(const uint8_t *d_bytes, uint64_t stride, uint32_t n, uint32_t *d_meta, void *stream);
 
 /* Synthetic key stream: n UUID-v4-format 36-byte keys [k0, k0+n) of `seed`,
  * written at 36-byte stride. */

@@ -47,6 +47,7 @@ SIGNATURES = {
     "rp_hash32": (_U32, [ctypes.c_char_p, ctypes.c_size_t]),
     "rp_hash32_batch_dev": (_INT, [_P, _P, _U64, _P, _P]),
     "rp_hash32_long_dev": (_INT, [_P, _U64, _P, _P]),
+    "rp_hash32_long_multi_dev": (_INT, [_P, _U64, _U32, _P, _P]),
     "rp_gen_uuid_keys_dev": (_INT, [_U32, _U64, _U64, _P, _P]),
     "rp_ring_create": (_INT, [_U32, _INT, _P]),
     "rp_ring_destroy": (_INT, [_P]),

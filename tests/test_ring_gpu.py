@@ -444,6 +444,38 @@ def test_device_farmhash_and_keygen(gpu, orc):
     assert np.array_equal(d_k.cpu().numpy().reshape(n, 36), orc.uuid_keys(42, 12345, n))
 
 
+@pytest.mark.parametrize("pack", ["1", "0"], ids=["pack16", "one-per-workgroup"])
+def test_long_hash_multi_vs_oracle(gpu, orc, pack, monkeypatch):
+    """rp_hash32_long_multi_dev (the membership checksum groups' chains): 41 strings side by side,
+    lengths 0..1.3 MB (the <= 24-byte forms, every 20-byte chunk boundary near 25..65, long ones
+    of different lengths in one workgroup, so the packed kernel's lockstep part stops at the
+    shortest and the rest run masked), some gated off (left untouched), against the oracle's
+    farmhash32. "pack16": k_hash_long_pack, 16 strings a workgroup (round 6); the other: one
+    workgroup a string."""
+    monkeypatch.setenv("RP_HL_PACK", pack)
+    rng = np.random.default_rng(9)
+    lens = [0, 1, 4, 5, 12, 13, 24, 25, 26, 44, 45, 46, 64, 65, 66, 100, 1000, 4096, 20000, 100003,
+            1_300_000, 1_299_981, 1_299_999, 777_777, 65, 3, 2_000, 60_001, 45, 1_000_000, 999_990,
+            25, 250_000, 24, 400_019, 17, 1_234_567, 88, 9_999, 1_048_576, 31]
+    gate = [0 if i % 7 == 5 else 1 for i in range(len(lens))]
+    stride = ((max(lens) + 32 + 255) // 256) * 256
+    buf = rng.integers(32, 127, size=stride * len(lens), dtype=np.uint8)
+    meta = np.zeros(4 * len(lens), dtype=np.uint32)
+    meta[0::4] = np.asarray(lens, dtype=np.uint32) + 1
+    meta[1::4] = gate
+    meta[2::4] = 0xDEADBEEF
+    d_b = torch.from_numpy(buf).cuda()
+    d_m = torch.from_numpy(meta.view(np.int32)).cuda()
+    gpu.check(gpu.lib().rp_hash32_long_multi_dev(d_b.data_ptr(), stride, len(lens), d_m.data_ptr(), None))
+    torch.cuda.synchronize()
+    got = d_m.cpu().numpy().view(np.uint32).reshape(-1, 4)
+    for b, (L, g) in enumerate(zip(lens, gate)):
+        if g:
+            assert (got[b, 2], got[b, 3]) == (orc.hash32(buf[b * stride:b * stride + L].tobytes()), 1), (b, L)
+        else:
+            assert (got[b, 2], got[b, 3]) == (0xDEADBEEF, 0), (b, L)
+
+
 def c2_servers(orc, n):
     return [orc.c2_addr(i) for i in range(n)]
 

@@ -18,11 +18,18 @@ VARIANTS = {
     "g256": {"RP_MEMBERS_GROUP_SLOTS": "256", "RP_MEMBERS_CK_BYTES": str(4 << 30)},
     "g192": {"RP_MEMBERS_GROUP_SLOTS": "192", "RP_MEMBERS_CK_BYTES": str(3 << 30)},
     "side": {"RP_MEMBERS_SIDE_BUILD": "1"},
+    "fused": {"RP_MEMBERS_SIDE_BUILD": "2"},
+    "fused-g512": {"RP_MEMBERS_SIDE_BUILD": "2", "RP_MEMBERS_GROUP_SLOTS": "512", "RP_MEMBERS_CK_BYTES": str(6 << 30)},
+    "side-g512": {"RP_MEMBERS_SIDE_BUILD": "1", "RP_MEMBERS_GROUP_SLOTS": "512", "RP_MEMBERS_CK_BYTES": str(6 << 30)},
     "side-g256": {"RP_MEMBERS_SIDE_BUILD": "1", "RP_MEMBERS_GROUP_SLOTS": "256", "RP_MEMBERS_CK_BYTES": str(4 << 30)},
     "noside": {"RP_MEMBERS_SIDE_BUILD": "0"},
+    "pad-g256": {"RP_HL_LDS_PAD": "65536", "RP_MEMBERS_GROUP_SLOTS": "256", "RP_MEMBERS_CK_BYTES": str(4 << 30)},
+    "pad": {"RP_HL_LDS_PAD": "65536"},
+    "nopack": {"RP_HL_PACK": "0"},
+    "g512": {"RP_MEMBERS_GROUP_SLOTS": "512", "RP_MEMBERS_CK_BYTES": str(6 << 30)},
     "noside-g256": {"RP_MEMBERS_SIDE_BUILD": "0", "RP_MEMBERS_GROUP_SLOTS": "256", "RP_MEMBERS_CK_BYTES": str(4 << 30)},
 }
-KNOBS = ("RP_MEMBERS_GROUP_SLOTS", "RP_MEMBERS_CK_BYTES", "RP_MEMBERS_SIDE_BUILD")
+KNOBS = ("RP_MEMBERS_GROUP_SLOTS", "RP_MEMBERS_CK_BYTES", "RP_MEMBERS_SIDE_BUILD", "RP_HL_LDS_PAD", "RP_HL_PACK")
 
 
 def main():
