@@ -256,10 +256,11 @@ def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=512, warmup=3, 
            "n_gpus": world, "scaling": "strong", "batches": batches,
            "updates_per_s": k * batches / dt, "ms_per_batch": dt * 1e3 / batches,
            "gpu_ms_per_batch": e0.elapsed_time(e1) / batches, "checksum": ck,
-           "note": "every batch applies most of its updates and its checksum string is built after it; the "
-                   "strings' serial farmhash chains run in groups of 128 side by side (one workgroup each) on a "
-                   "side stream, overlapping the next batches' folds (4 groups of 128 slots within a 2 GiB pool, "
-                   "RP_MEMBERS_CK_BYTES); the last batch's checksum is read inside the timed region, so "
+           "note": "every batch applies most of its updates and its checksum string is built after it (written "
+                   "by the blocks appended to the next batch's fold launch); the strings' serial farmhash chains "
+                   "run in groups of 512 side by side (16 a workgroup) on a side stream, overlapping the next "
+                   "batches' folds (2 groups of 512 slots within a 6 GiB pool, RP_MEMBERS_CK_BYTES); the last "
+                   "batch's checksum is read inside the timed region, so "
                    "the final group's chains (one serial chain's latency, ~4.4 ms) are in the time: over "
                    "%d batches that drain adds ~%.1f us per batch" % (batches, 4400.0 / batches)}
     if world > 1 or not extras:  # the fold-only and large-batch legs are per-replica: rank 0's one-GPU run

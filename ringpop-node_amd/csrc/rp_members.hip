@@ -257,8 +257,9 @@ __global__ void k_link(const uint32_t* __restrict__ ids, uint32_t k, uint32_t* _
 // The workgroup's applied count goes to part[blockIdx.x] (summed by k_ovf_len or k_fold_ovf).
 __device__ __forceinline__ void fold_fast_block(const uint32_t* __restrict__ ids, uint32_t k,
                                                 const uint8_t* __restrict__ rk, const uint32_t* __restrict__ slots,
-                                                const FoldArgs& A, uint32_t* __restrict__ part) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+                                                const FoldArgs& A, uint32_t* __restrict__ part, uint32_t blk,
+                                                uint32_t nblk) {
+    const uint32_t i = blk * blockDim.x + threadIdx.x;
     uint32_t napp = 0;
     if (i < k && rk[i] == 0) {
         const uint32_t id = ids[i];
@@ -285,14 +286,14 @@ __device__ __forceinline__ void fold_fast_block(const uint32_t* __restrict__ ids
         }
     }
     napp = block_sum256(napp);
-    if (threadIdx.x == 0) part[blockIdx.x] = napp;
-    if (threadIdx.x == 0 && blockIdx.x == 0) part[gridDim.x] = 0;  // the overflow fold's count (k_ovf_len)
+    if (threadIdx.x == 0) part[blk] = napp;
+    if (threadIdx.x == 0 && blk == 0) part[nblk] = 0;  // the overflow fold's count (k_ovf_len)
 }
 
 __global__ __launch_bounds__(256) void k_fold_fast(const uint32_t* __restrict__ ids, uint32_t k,
                                                    const uint8_t* __restrict__ rk, const uint32_t* __restrict__ slots,
                                                    FoldArgs A, uint32_t* __restrict__ part) {
-    fold_fast_block(ids, k, rk, slots, A, part);
+    fold_fast_block(ids, k, rk, slots, A, part, blockIdx.x, gridDim.x);
 }
 
 // Every workgroup of the launch waits here until all have arrived (count / generation words,
@@ -331,7 +332,7 @@ __global__ __launch_bounds__(256) void k_link_fold(const uint32_t* __restrict__ 
                                                    FoldArgs A, uint32_t* __restrict__ part, uint32_t* __restrict__ err) {
     link_one(blockIdx.x * blockDim.x + threadIdx.x, ids, k, A.cnt, slots, rk, ovf, napplied);
     grid_sync(napplied + 2, napplied + 5, err);
-    fold_fast_block(ids, k, rk, slots, A, part);
+    fold_fast_block(ids, k, rk, slots, A, part, blockIdx.x, gridDim.x);
 }
 
 // The grouped path's overflow fold: the addresses k_fold_fast marked (more than kSlots + 1
@@ -1098,14 +1099,33 @@ __global__ __launch_bounds__(256) void k_mck_len(const uint32_t* __restrict__ or
     if (threadIdx.x == 0) tile_tot[blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(256) void k_mck_write(const uint32_t* __restrict__ order, uint32_t n,
-                                                   const MRow* __restrict__ rows, const uint8_t* __restrict__ names,
-                                                   const uint32_t* __restrict__ soff, const uint32_t* __restrict__ gate,
-                                                   const uint32_t* __restrict__ tile_tot, uint8_t* __restrict__ buf,
-                                                   uint32_t* __restrict__ meta, const uint64_t* __restrict__ snap) {
+// One tile of the checksum string (tile `tile` of `ntiles`); see k_mck_write.
+struct MckArgs {
+    const uint32_t* order;
+    uint32_t n;
+    const MRow* rows;
+    const uint8_t* names;
+    const uint32_t* soff;
+    const uint32_t* gate;
+    const uint32_t* tile_tot;
+    uint8_t* buf;
+    uint32_t* meta;
+    const uint64_t* snap;
+};
+__device__ __forceinline__ void mck_write_block(const MckArgs& a, uint32_t tile, uint32_t ntiles) {
+    const uint32_t* __restrict__ order = a.order;
+    const uint32_t n = a.n;
+    const MRow* __restrict__ rows = a.rows;
+    const uint8_t* __restrict__ names = a.names;
+    const uint32_t* __restrict__ soff = a.soff;
+    const uint32_t* __restrict__ gate = a.gate;
+    const uint32_t* __restrict__ tile_tot = a.tile_tot;
+    uint8_t* __restrict__ buf = a.buf;
+    uint32_t* __restrict__ meta = a.meta;
+    const uint64_t* __restrict__ snap = a.snap;
     __shared__ uint32_t s_wsum[4], s_pre[4];
     __shared__ uint32_t s_stage[kMckStage / 4 + 4];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, tile = blockIdx.x;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     if (gate && *gate == 0) {
         if (tile == 0 && tid == 0) {
             meta[0] = 0;
@@ -1138,7 +1158,7 @@ __global__ __launch_bounds__(256) void k_mck_write(const uint32_t* __restrict__ 
         total += s_wsum[w];
     }
     const uint32_t g0 = s_pre[0] + s_pre[1] + s_pre[2] + s_pre[3];
-    if (tid == 0 && tile == gridDim.x - 1) {
+    if (tid == 0 && tile == ntiles - 1) {
         meta[0] = g0 + total;
         meta[1] = 1;
         meta[3] = 0;
@@ -1173,6 +1193,23 @@ __global__ __launch_bounds__(256) void k_mck_write(const uint32_t* __restrict__ 
             for (uint32_t q = lo; q < hi; q++) buf[q] = st[q - g0];
         }
     }
+}
+
+
+__global__ __launch_bounds__(256) void k_mck_write(MckArgs a) { mck_write_block(a, blockIdx.x, gridDim.x); }
+
+// The grouped fold of batch b + 1 and the checksum string of batch b in one launch (round 6,
+// deferred string write): blocks [0, nfold) fold, the rest write the string from the row snapshot
+// k_ovf_len took of batch b, which the fold does not touch. Both are latency-bound, so their
+// blocks overlap; the string costs no launch, stream or event of its own.
+__global__ __launch_bounds__(256) void k_fold_fast_mck(const uint32_t* __restrict__ ids, uint32_t k,
+                                                       const uint8_t* __restrict__ rk,
+                                                       const uint32_t* __restrict__ slots, FoldArgs A,
+                                                       uint32_t* __restrict__ part, uint32_t nfold, MckArgs m) {
+    if (blockIdx.x < nfold)
+        fold_fast_block(ids, k, rk, slots, A, part, blockIdx.x, nfold);
+    else
+        mck_write_block(m, blockIdx.x - nfold, gridDim.x - nfold);
 }
 
 // the per-batch history (rp_members_checksum_shard): the group's update-batch slots (bit j of
@@ -1227,17 +1264,17 @@ struct Members {
     // by the sorted fold that then runs), [2..) the launches' last-workgroup counters
     DevBuf<uint32_t> napplied;
     // Checksum strings wait in slots until read or until a group of slots is pending, then one
-    // launch hashes the group side by side (one serial chain per workgroup): a batched caller
-    // pays one chain's latency per group instead of per batch. The slots form ngroups groups
-    // of group_slots; a full group is hashed on a side stream (ck_st) while the next batches
-    // fold and build their strings into the next group, so up to ngroups - 1 groups of chains
-    // overlap the folds. Reads flush and wait. The slot count is what fits
-    // RP_MEMBERS_CK_BYTES (default 1 GiB of HBM), at most kMaxSlots. Groups of 128: a launch of
-    // 128 chains (one workgroup each) takes about as long as one of 64, and the folds and string
-    // builds of the next 128 batches take about as long (C3: 1.00-1.07 G updates/s against 0.86
-    // with groups of 64, 0.44 with 32; RP_MEMBERS_GROUP_SLOTS overrides). The pool is 2 GiB by
-    // default (RP_MEMBERS_CK_BYTES): 4 groups at C3.
-    static constexpr uint32_t kMaxSlots = 1024, kGroupSlots = 128, kMaxGroups = 4;
+    // launch hashes the group side by side: a batched caller pays one chain's latency per group
+    // instead of per batch. The slots form ngroups groups of group_slots; a full group is hashed on
+    // a side stream (ck_st) while the next batches fold and build their strings into the next
+    // group, so up to ngroups - 1 groups of chains overlap the folds. Reads flush and wait. The
+    // slot count is what fits RP_MEMBERS_CK_BYTES (default 6 GiB of HBM), at most kMaxSlots.
+    // Groups of 512 (round 6; RP_MEMBERS_GROUP_SLOTS overrides): the packed chain kernel
+    // (k_hash_long_pack, 16 strings a workgroup) hashes 16 to 512 strings of 3.6 MB in the same
+    // ~4 ms, so the chains of a 512-batch group cost no more than a 128-batch one did (rounds 2-5:
+    // a workgroup a string, groups of 128, 2 GiB; 1.00-1.07 G updates/s against 0.86 with groups
+    // of 64 then).
+    static constexpr uint32_t kMaxSlots = 1024, kGroupSlots = 512, kMaxGroups = 4;
     uint32_t nslots = 1, group_slots = 1, ngroups = 1;
     DevBuf<uint8_t> ck_buf;   // nslots strings of slot_bytes
     uint64_t slot_bytes = 0;
@@ -1386,6 +1423,9 @@ struct Members {
             if (n_applied_out) RP_HIP(hipMemsetAsync(n_applied_out, 0, sizeof(uint32_t), s));
             return;
         }
+        if (pw.on && (pw.st != s || use_bucket_fold(k, (cap + kBk - 1) / kBk) || !grouped_fold ||
+                      getenv_on("RP_MEMBERS_FUSE")))
+            drain_write();  // only the grouped fold's launch carries a deferred string
         if (damp_on) {
             d_out.reserve(k);
             d_exc.reserve(k);
@@ -1478,7 +1518,13 @@ struct Members {
             } else {
                 hipLaunchKernelGGL(k_link, dim3(g1), dim3(256), 0, s, ids, k, rcnt.p, g_slots.p, g_rk.p, ovf,
                                    napplied.p);
-                hipLaunchKernelGGL(k_fold_fast, dim3(g1), dim3(256), 0, s, ids, k, g_rk.p, g_slots.p, A, g_part.p);
+                if (pw.on && pw.st == s) {  // the previous batch's string rides on this fold's launch
+                    pw.on = false;
+                    hipLaunchKernelGGL(k_fold_fast_mck, dim3(g1 + pw.ntl), dim3(256), 0, s, ids, k, g_rk.p, g_slots.p, A,
+                                       g_part.p, g1, pw.a);
+                } else {
+                    hipLaunchKernelGGL(k_fold_fast, dim3(g1), dim3(256), 0, s, ids, k, g_rk.p, g_slots.p, A, g_part.p);
+                }
             }
             RP_HIP(hipGetLastError());
             if (build && nt.size()) {  // the overflow fold rides on the string build's length launch
@@ -1539,40 +1585,63 @@ struct Members {
         uint32_t nparts;
         uint32_t* out;
     };
-    // Side build (round 6; RP_MEMBERS_SIDE_BUILD=0 turns it off): for an update batch the length
-    // launch (k_ovf_len) also copies every member's row in rank order and the batch's applied count
-    // into one of two snapshot buffers, and the string writer (k_mck_write) runs on a build stream
-    // from that copy, so the main stream goes on to the next batch's fold instead of waiting for the
-    // writer. A snapshot buffer is rewritten only after the writer that read it (event); the group
-    // of slots is flushed from the build stream.
-    hipStream_t bs = nullptr;                     // the build stream
+    // Where an update batch's checksum string is written (round 6; RP_MEMBERS_SIDE_BUILD selects,
+    // for A/B). For an update batch the length launch (k_ovf_len) also copies every member's row
+    // in rank order and the batch's applied count into a snapshot, so the writer no longer needs
+    // the table as it was after this batch:
+    //   2 (default) deferred: the string of batch b is written by the blocks that k_fold_fast_mck
+    //     appends to batch b + 1's fold launch (any other call first writes it with its own launch,
+    //     drain_write); one snapshot suffices, since batch b + 1's lengths follow that launch;
+    //   1 build stream: k_mck_write runs on a second stream from one of two snapshots, ordered by
+    //     events (0.0410 -> 0.0369 ms per C3 batch, r06e; the events cost the host ~9 us a batch);
+    //   0 inline: k_mck_write right after k_ovf_len on the caller's stream, from the table.
+    hipStream_t bs = nullptr;                     // the build stream (mode 1)
     hipEvent_t ev_len = nullptr, ev_snap[2] = {};  // lengths + snapshot ready; snapshot p free again
     bool snap_busy[2] = {false, false};
     uint32_t snap_p = 0;
     DevBuf<uint64_t> snap_rows[2];
     DevBuf<uint32_t> snap_tiles[2], snap_gate;
     hipStream_t pend_main = nullptr;  // the caller's stream of the pending group
-    // the writer reads the names' rank order and bytes (nt.sorted / soff / sbytes): a call that
-    // may rewrite them (interning, the wire codec's name index) waits for it first
-    void settle_build() {
-        if (bs) RP_HIP(hipStreamSynchronize(bs));
-    }
-    bool side_build() const {
+    struct PendingWrite {  // mode 2: the string k_fold_fast_mck (or drain_write) still has to write
+        bool on = false;
+        uint32_t ntl = 0;
+        hipStream_t st = nullptr;
+        MckArgs a{};
+    } pw;
+    int string_mode() const {
         const char* e = getenv("RP_MEMBERS_SIDE_BUILD");
-        return !(e && *e == '0');
+        return e && (*e == '0' || *e == '1') ? *e - '0' : 2;
+    }
+    // write a deferred string now (its own launch, on the stream it was deferred on)
+    void drain_write() {
+        if (!pw.on) return;
+        pw.on = false;
+        hipLaunchKernelGGL(k_mck_write, dim3(pw.ntl), dim3(256), 0, pw.st, pw.a);
+        RP_HIP(hipGetLastError());
+    }
+    // the writer reads the names' rank order and bytes (nt.sorted / soff / sbytes): a call that
+    // may rewrite them (interning, the wire codec's name index) has it written first
+    void settle_build() {
+        if (pw.on) {
+            const hipStream_t w = pw.st;
+            drain_write();
+            RP_HIP(hipStreamSynchronize(w));
+        }
+        if (bs) RP_HIP(hipStreamSynchronize(bs));
     }
     void checksum_dev(hipStream_t s, const uint32_t* gate, bool is_batch = false, const OvfArgs* ov = nullptr) {
         const uint32_t n = nt.size();
         if (!n) return;
+        drain_write();
         ck_len.reserve(n + 1);
         ck_pos.reserve(n + 1);
-        const bool side = ov != nullptr && side_build();
-        if (side && !bs) {
+        const int mode = ov ? string_mode() : 0;
+        if (mode == 1 && !bs) {
             RP_HIP(hipStreamCreateWithFlags(&bs, hipStreamNonBlocking));
             RP_HIP(hipEventCreateWithFlags(&ev_len, hipEventDisableTiming));
             for (auto& e : ev_snap) RP_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         }
-        const hipStream_t bst = side ? bs : s;  // where this string is written
+        const hipStream_t bst = mode == 1 ? bs : s;  // where this string is written
         // worst-case string: names + ';' + "suspect" + 20 digits per member
         const uint64_t need = (nt.h_bytes.size() + (uint64_t)n * 29 + 16 + 255) & ~255ull;
         if (npending && (s != pend_main || bst != pend_st || need > slot_bytes)) {  // keep the group on one stream
@@ -1590,10 +1659,11 @@ struct Members {
             for (auto& b : group_busy) b = false;
             cur_group = 0;
             ck_buf.release();
-            // 2 GiB of HBM: at C3's 3.6 MB strings, 4 groups of 128 slots, so the folds never wait
-            // for a group's previous chains (1 GiB / 2 groups: 51.4 against 45.2 us per batch over
-            // a 512-batch stream, profiles/r04/r04e/)
-            const uint64_t budget = env_pos("RP_MEMBERS_CK_BYTES", 2ull << 30);
+            // 6 GiB of HBM: at C3's 4.7 MB slots, 2 groups of 512 (round 6: the packed chain kernel
+            // hashes 16 to 512 strings in the same ~4 ms, so a group of 512 costs what one of 128
+            // did: 0.0384 -> 0.0311 ms per C3 batch, profiles/r06/r06j/); rounds 2-5 kept 2 GiB and
+            // groups of 128 (1 GiB / 2 groups: 51.4 against 45.2 us per batch, profiles/r04/r04e/)
+            const uint64_t budget = env_pos("RP_MEMBERS_CK_BYTES", 6ull << 30);
             nslots = (uint32_t)std::min<uint64_t>(kMaxSlots, std::max<uint64_t>(1, budget / need));
             const uint32_t gmax = (uint32_t)env_pos("RP_MEMBERS_GROUP_SLOTS", kGroupSlots);  // A/B: chains per launch
             group_slots = std::max<uint32_t>(1, std::min<uint32_t>(gmax, nslots / 2));
@@ -1621,11 +1691,11 @@ struct Members {
                 uint64_t* snap = nullptr;
                 uint32_t* tiles = nullptr;
                 uint32_t* gcopy = nullptr;
-                if (side) {
-                    const uint32_t p = snap_p;
-                    if (snap_busy[p]) RP_HIP(hipStreamWaitEvent(s, ev_snap[p], 0));  // its writer has read it
+                const uint32_t p = mode == 1 ? snap_p : 0u;
+                if (mode >= 1) {
+                    if (mode == 1 && snap_busy[p]) RP_HIP(hipStreamWaitEvent(s, ev_snap[p], 0));  // its writer has read it
                     if (snap_rows[p].cap < n) {
-                        RP_HIP(hipStreamSynchronize(bs));
+                        if (bs) RP_HIP(hipStreamSynchronize(bs));
                         snap_rows[p].reserve(n);
                     }
                     snap_tiles[p].reserve(ntl);
@@ -1640,25 +1710,29 @@ struct Members {
                 hipLaunchKernelGGL(k_ovf_len, dim3(ntl), dim3(256), 0, s, nt.sorted.p, n, nt.soff.p, tiles,
                                    ov->ids, ov->k, ov->ovf, ov->A, ov->part, ov->nparts, ov->out,
                                    napplied.p + 2 + 2, ws.err.p, snap, gcopy);
-                if (side) {
-                    const uint32_t p = snap_p;
+                const MckArgs ma{nt.sorted.p, n, rows.p, nt.sbytes.p, nt.soff.p, mode >= 1 ? gcopy : gate, tiles, buf,
+                                 meta, snap};
+                if (mode == 2) {
+                    pw.on = true;
+                    pw.ntl = ntl;
+                    pw.st = s;
+                    pw.a = ma;
+                } else if (mode == 1) {
                     RP_HIP(hipEventRecord(ev_len, s));
                     RP_HIP(hipStreamWaitEvent(bs, ev_len, 0));
-                    hipLaunchKernelGGL(k_mck_write, dim3(ntl), dim3(256), 0, bs, nt.sorted.p, n, rows.p, nt.sbytes.p,
-                                       nt.soff.p, gcopy, tiles, buf, meta, (const uint64_t*)snap);
+                    hipLaunchKernelGGL(k_mck_write, dim3(ntl), dim3(256), 0, bs, ma);
                     RP_HIP(hipEventRecord(ev_snap[p], bs));
                     snap_busy[p] = true;
                     snap_p ^= 1u;
                 } else {
-                    hipLaunchKernelGGL(k_mck_write, dim3(ntl), dim3(256), 0, s, nt.sorted.p, n, rows.p, nt.sbytes.p,
-                                       nt.soff.p, gate, tiles, buf, meta, (const uint64_t*)nullptr);
+                    hipLaunchKernelGGL(k_mck_write, dim3(ntl), dim3(256), 0, s, ma);
                 }
             } else {
                 ck_tiles.reserve(ntl);
                 hipLaunchKernelGGL(k_mck_len, dim3(ntl), dim3(256), 0, s, nt.sorted.p, n, rows.p, nt.soff.p,
                                    ck_tiles.p);
-                hipLaunchKernelGGL(k_mck_write, dim3(ntl), dim3(256), 0, s, nt.sorted.p, n, rows.p, nt.sbytes.p,
-                                   nt.soff.p, gate, ck_tiles.p, buf, meta, (const uint64_t*)nullptr);
+                const MckArgs ma{nt.sorted.p, n, rows.p, nt.sbytes.p, nt.soff.p, gate, ck_tiles.p, buf, meta, nullptr};
+                hipLaunchKernelGGL(k_mck_write, dim3(ntl), dim3(256), 0, s, ma);
             }
         }
         RP_HIP(hipGetLastError());
@@ -1670,6 +1744,7 @@ struct Members {
     // built, then commit the last gated one to ck (groups commit in batch order: one stream)
     void flush_checksums() {
         if (!npending) return;
+        drain_write();  // the group's last string, if its batch's successor has not written it
         RP_HIP(hipEventRecord(ev_built, pend_st));
         RP_HIP(hipStreamWaitEvent(ck_st, ev_built, 0));
         const uint64_t first = slot_index(0);

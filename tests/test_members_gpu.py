@@ -59,15 +59,18 @@ def test_members_match_reference_goldens(gpu, case_name, fold, monkeypatch):
                 assert m.generate_checksum_string() == op["checksumString"]
 
 
-@pytest.mark.parametrize("fold", ["default", "bucket", "noside"])
+@pytest.mark.parametrize("fold", ["default", "bucket", "inline", "stream"])
 def test_c3_merge_vs_oracle(gpu, orc, fold, monkeypatch):
     """C3 at full size: 100k members, 100k updates with 1% duplicated addresses (25 buckets of
-    4,096 ids on the bucket path). "noside": the checksum string written on the caller's stream
-    (RP_MEMBERS_SIDE_BUILD=0) instead of the build stream from the row snapshot (round 6)."""
+    4,096 ids on the bucket path). Where each batch's checksum string is written (round 6,
+    RP_MEMBERS_SIDE_BUILD): default, deferred into the next batch's fold launch from the row
+    snapshot; "stream", on a build stream from the snapshot; "inline", right after the lengths."""
     if fold == "bucket":
         monkeypatch.setenv("RP_MEMBERS_BUCKET_FOLD", "1")
-    if fold == "noside":
+    if fold == "inline":
         monkeypatch.setenv("RP_MEMBERS_SIDE_BUILD", "0")
+    if fold == "stream":
+        monkeypatch.setenv("RP_MEMBERS_SIDE_BUILD", "1")
     S = synth()
     n = k = 100_000
     names, st0, inc0 = S.c3_members(n)
@@ -223,6 +226,72 @@ def test_grouped_checksums_across_unread_batches(gpu, orc, nbatches, tail_noops)
     torch.cuda.synchronize()
     assert m.checksum == o.checksum
     assert m.generate_checksum_string() == o.checksum_string()
+
+
+def test_deferred_string_write_across_paths(gpu, orc, monkeypatch):
+    """The deferred checksum-string write (round 6: batch b's string rides on batch b + 1's fold
+    launch) across everything that must write it first instead: a batch on the bucket path, a
+    batch on the sorted path, new members interned between batches (the writer reads the names'
+    rank order), a Membership.set, an empty batch, and checksum reads; every batch's checksum
+    against the oracle (read back from the per-batch history, rp_members_checksum_shard with one
+    shard)."""
+    import torch
+
+    S = synth()
+    n0, k = 3000, 2000
+    names = [S.c2_addr(i) for i in range(n0 + 500)]
+    m = gpu.Membership(whoami=names[0], capacity=n0)
+    m.checksum_shard(1, 0, history_cap=64)
+    o = orc.Members(names, local=names[0], join_seed=0)
+    ids0 = np.asarray(m.intern(names[:n0]), dtype=np.uint32)
+    st0 = np.zeros(n0, np.uint8)
+    inc0 = np.full(n0, 100, np.int64)
+    m.update_ids(ids0, st0, inc0, now_ms=1)
+    o.update_ids(np.arange(n0), st0, inc0, False, 1)
+    want = [o.checksum]
+    stream = torch.cuda.current_stream().cuda_stream
+    app = torch.empty(k, dtype=torch.uint8, device="cuda")
+    na = torch.zeros(1, dtype=torch.int32, device="cuda")
+    rng = np.random.default_rng(4)
+    plan = ["g", "g", "bucket", "g", "sorted", "g", "intern", "g", "g", "read", "g", "empty", "g", "bucket",
+            "bucket", "g", "g"]
+    nn = n0
+    keep = []
+    for b, what in enumerate(plan):
+        for e in ("RP_MEMBERS_BUCKET_FOLD", "RP_MEMBERS_SORTED_FOLD"):
+            monkeypatch.delenv(e, raising=False)
+        if what == "intern":
+            new = names[nn:nn + 500]
+            ids_new = np.asarray(m.intern(new), dtype=np.uint32)
+            assert (ids_new == np.arange(nn, nn + 500)).all()
+            nn += 500
+            continue
+        if what == "read":
+            assert m.checksum == want[-1]
+            continue
+        if what == "bucket":
+            monkeypatch.setenv("RP_MEMBERS_BUCKET_FOLD", "1")
+        if what == "sorted":
+            monkeypatch.setenv("RP_MEMBERS_SORTED_FOLD", "1")
+        kk = 0 if what == "empty" else k
+        ids = rng.integers(0, nn, size=kk).astype(np.uint32)
+        us = rng.integers(0, 4, size=kk).astype(np.uint8)
+        ui = (100 + b + rng.integers(0, 3, size=kk)).astype(np.int64)
+        d = [torch.from_numpy(ids.view(np.int32)).cuda(), torch.from_numpy(us).cuda(), torch.from_numpy(ui).cuda()]
+        keep.append(d)
+        m.update_dev(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), kk, 1434500000000 + b, app.data_ptr(),
+                     None, None, na.data_ptr(), stream)
+        if kk:
+            o.update_ids(ids, us, ui, False, 1434500000000 + b)
+            want.append(o.checksum)
+    torch.cuda.synchronize()
+    for e in ("RP_MEMBERS_BUCKET_FOLD", "RP_MEMBERS_SORTED_FOLD"):
+        monkeypatch.delenv(e, raising=False)
+    assert m.checksum == want[-1]
+    h, a = m.checksum_history()
+    assert len(h) == len(want) and a.all()  # (every batch here applies something)
+    assert h.tolist() == want
+    m.close()
 
 
 @pytest.mark.parametrize("budget", [None, "3"], ids=["default-pool", "three-slots"])
