@@ -57,7 +57,12 @@ void svc_quiesce(const void* keep);  // stop every resident service but `keep`'s
 struct QuietScope {
     QuietScope() {
         g_quiet.fetch_add(1);
-        if (g_svc_live.load() > 0) svc_quiesce(nullptr);
+        try {
+            if (g_svc_live.load() > 0) svc_quiesce(nullptr);
+        } catch (...) {  // (the destructor does not run when the constructor throws)
+            g_quiet.fetch_sub(1);
+            throw;
+        }
     }
     ~QuietScope() { g_quiet.fetch_sub(1); }
     QuietScope(const QuietScope&) = delete;

@@ -675,6 +675,7 @@ __device__ __forceinline__ void bk_local(const FoldArgs& A, uint32_t j) {
 // workgroups land in g_bk_prof (printed by the launcher under RP_BK_PROF_PRINT).
 #ifdef RP_BK_PROF
 __device__ unsigned long long g_bk_prof[8];
+__device__ unsigned long long g_bk_wg[2 * kBkMaxBuckets];  // per bucket: start, end (s_memrealtime, 100 MHz)
 #define BK_T(var)   \
     uint64_t var;   \
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var))
@@ -704,6 +705,9 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
     const uint32_t per = (nb + 7) / 8, b = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
     if (b >= nb) return;
     const uint32_t tid = threadIdx.x, id0 = b << kBkBits;
+#ifdef RP_BK_PROF
+    if (tid == 0) g_bk_wg[2 * b] = __builtin_amdgcn_s_memrealtime();
+#endif
     auto dput = [&](uint32_t d, uint32_t il, uint32_t js, int64_t in) {
         dk[d] = ((uint64_t)il << 40) | ((uint64_t)(js & 0x3FFFFFFFu) << 10) | d;
         dst[d] = (uint8_t)(js >> 30);
@@ -854,6 +858,7 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
         atomicAdd(&g_bk_prof[2], (unsigned long long)(t3 - t2));
         atomicAdd(&g_bk_prof[3], (unsigned long long)(t4 - t3));
         atomicAdd(&g_bk_prof[4], 1ull);
+        g_bk_wg[2 * b + 1] = __builtin_amdgcn_s_memrealtime();
     }
 #endif
     if (tid == 0) {
@@ -1489,6 +1494,35 @@ struct Members {
                         v[4], v[0] / nw, v[1] / nw, v[2] / nw, v[3] / nw);
                 memset(v, 0, sizeof v);
                 RP_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_bk_prof), v, sizeof v));
+                // per-workgroup timeline (the grid's quantization): starts and ends in us
+                // from the first start; how many workgroups run at each tenth of the span
+                std::vector<unsigned long long> wg(2 * kBkMaxBuckets);
+                RP_HIP(hipMemcpyFromSymbol(wg.data(), HIP_SYMBOL(g_bk_wg), sizeof(unsigned long long) * 2 * nb));
+                unsigned long long t0 = ~0ull, t1 = 0;
+                std::vector<double> st(nb), du(nb);
+                for (uint32_t i = 0; i < nb; i++) {
+                    t0 = std::min(t0, wg[2 * i]);
+                    t1 = std::max(t1, wg[2 * i + 1]);
+                }
+                for (uint32_t i = 0; i < nb; i++) {
+                    st[i] = (wg[2 * i] - t0) / 100.0;
+                    du[i] = (wg[2 * i + 1] - wg[2 * i]) / 100.0;
+                }
+                std::vector<double> ss = st, dd = du;
+                std::sort(ss.begin(), ss.end());
+                std::sort(dd.begin(), dd.end());
+                const double span = (t1 - t0) / 100.0;
+                fprintf(stderr, "[rp] k_bk_fold workgroups %u: span %.1f us; starts p50 %.1f p75 %.1f p90 %.1f last %.1f; "
+                                "durations min %.1f p50 %.1f p90 %.1f max %.1f; running at tenths:",
+                        nb, span, ss[nb / 2], ss[nb * 3 / 4], ss[nb * 9 / 10], ss[nb - 1], dd[0], dd[nb / 2], dd[nb * 9 / 10],
+                        dd[nb - 1]);
+                for (int q = 0; q < 10; q++) {
+                    const double t = span * (q + 0.5) / 10.0;
+                    int c = 0;
+                    for (uint32_t i = 0; i < nb; i++) c += (st[i] <= t && st[i] + du[i] > t) ? 1 : 0;
+                    fprintf(stderr, " %d", c);
+                }
+                fprintf(stderr, "\n");
             }
 #endif
             if (applied && !direct) {
