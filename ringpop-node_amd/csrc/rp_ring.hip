@@ -3434,6 +3434,13 @@ int rp_hash32_long_dev(const uint8_t* d_bytes, uint64_t len, uint32_t* d_out, vo
     });
 }
 
+int rp_hash32_long_multi_dev(const uint8_t* d_bytes, uint64_t stride, uint32_t n, uint32_t* d_meta, void* stream) {
+    return guard([&] {
+        RP_REQUIRE(n == 0 || (d_bytes && d_meta), "hash32_long_multi_dev: null buffer");
+        rp::hash_long_multi(d_bytes, stride, n, d_meta, rp::as_stream(stream));
+    });
+}
+
 int rp_gen_uuid_keys_dev(uint32_t seed, uint64_t k0, uint64_t n, uint8_t* d_out, void* stream) {
     return guard([&] {
         if (!n) return;
