@@ -1454,11 +1454,13 @@ __global__ __launch_bounds__(64) void k_lookupn_small(const SmallKeys sk, View r
 // max_ticks in all (s_memrealtime, 100 MHz), so it always drains; the host relaunches it when a
 // request finds it gone.
 constexpr uint32_t kSvcChunks = 3, kSvcKeyMax = kSvcChunks * 60;
+constexpr uint32_t kSvcWaves = 8;     // k_lookup_service3's independent pollers (RP_SVC_WAVES)
+constexpr uint32_t kSvcPeriod = 120;  // their common poll period, 100 MHz ticks (RP_SVC_PERIOD)
 struct SvcLines {
     uint32_t req[16 * (1 + kSvcChunks)];  // header line + key lines
     uint32_t resp[16];                    // owners[0..W), count at [15]
     uint32_t resp_seq[16];                // [0] = the answered seq
-    uint64_t resp2[8];                    // k_lookup_service3: owner q | seq << 32 (one 64-B line)
+    uint64_t resp2[8][8];                 // k_lookup_service3: slot seq % 8, owner q | seq << 32 (64-B lines)
     uint32_t diag[16];                    // k_lookup_service3 with prof: seq, then phase ticks (100 MHz)
 };
 // With the compact layout built, a key with 1..4 owners wanted takes compact_fix_walk (the
@@ -1682,12 +1684,20 @@ __device__ __forceinline__ bool dt_answer(uint32_t x, uint32_t lane, uint32_t h,
 //   - RP_SVC_WARM=1: while idle, after each poll is issued, the wave touches 32 KB of the compact
 //     tables (the whole 3.5 MB about every 0.15 ms) to keep them in its XCD's L2. Measured without
 //     effect on the lookup's two trips (1.08 us either way, r05g) and 0.1 us slower polls: off.
+// Round 6: the wait for a request is the poll's phase, on average half a PCIe round trip before
+// the read that sees the line plus the return. So the service is kSvcWaves independent waves of
+// this same loop, one workgroup each (so on different CUs and XCDs, none delaying another's table
+// read), each with its one poll in flight at its own phase: the first to see a request answers
+// it, the later ones answer it again with the same line (a pure function of the request), and no
+// wave waits on another. The answer goes to line seq % 8, so a late duplicate can only land on
+// the line of a request eight calls old, never on the one the host is waiting for.
 // RP_SVC_PROF=1 writes per-call device phase ticks into diag (poll round trip, lookup).
 template <class View>
 __global__ __launch_bounds__(64) void k_lookup_service3(SvcLines* io, View rv, CompactFixView fv, CompactView cv,
                                                        uint32_t use_compact, uint32_t last, uint64_t idle_ticks,
                                                        uint64_t max_ticks, uint32_t warm, uint32_t prof,
-                                                       const uint32_t* __restrict__ dt, uint32_t dtb) {
+                                                       const uint32_t* __restrict__ dt, uint32_t dtb,
+                                                       uint32_t period) {
     __shared__ uint32_t dslot[8];
     const uint32_t lane = threadIdx.x;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
@@ -1695,7 +1705,17 @@ __global__ __launch_bounds__(64) void k_lookup_service3(SvcLines* io, View rv, C
     const uint64_t nidx = cv.idx_bytes, nwarm = nidx + cv.ent_bytes;
     uint64_t woff = 0;
     uint32_t acc = 0;
+    // period > 0 (several waves): wave i issues its polls on the device clock's slots
+    // n * period + i * period / waves, so the waves' reads reach the host line evenly spread
+    // instead of in step (launched together, they would otherwise poll at one phase)
+    uint64_t slot = period ? (t_start / period + 1) * period + (uint64_t)blockIdx.x * period / gridDim.x : 0;
     while (true) {
+        if (period) {
+            while (__builtin_amdgcn_s_memrealtime() < slot) __builtin_amdgcn_s_sleep(1);
+            const uint64_t t = __builtin_amdgcn_s_memrealtime();
+            do slot += period;
+            while (slot <= t);
+        }
         const uint64_t tp = __builtin_amdgcn_s_memrealtime();
         const uint32_t v = lane < 16 ? __hip_atomic_load(&io->req[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
         if (warm && use_compact) {  // issued after the poll, done within its round trip
@@ -1771,8 +1791,8 @@ __global__ __launch_bounds__(64) void k_lookup_service3(SvcLines* io, View rv, C
             if (lane < 4) __hip_atomic_store(&io->diag[lane], dv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         if (lane < 8)
-            __hip_atomic_store(&io->resp2[lane], (uint64_t)(lane < W ? o : NIL) | ((uint64_t)seq << 32), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&io->resp2[seq & 7u][lane], (uint64_t)(lane < W ? o : NIL) | ((uint64_t)seq << 32),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         last = seq;
         t_idle = __builtin_amdgcn_s_memrealtime();
     }
@@ -2917,8 +2937,11 @@ static void svc_launch(rp::Ring& r, uint32_t last) {
             r.svc_dt_valid = true;
         }
         const uint32_t* dt = r.svc_dtb ? reinterpret_cast<const uint32_t*>(r.svc_dt.p) : nullptr;
-        hipLaunchKernelGGL((k_lookup_service3<RingView>), dim3(1), dim3(64), 0, r.svc_st, r.svc_dev, r.view(), fv,
-                           r.cview(), r.compact ? 1u : 0u, last, idle, maxt, warm, prof, dt, r.svc_dtb);
+        // RP_SVC_WAVES pollers (one workgroup each, so one an XCD up to 8): see k_lookup_service3
+        const uint32_t waves = (uint32_t)std::min<uint64_t>(env_pos("RP_SVC_WAVES", kSvcWaves), 16);
+        hipLaunchKernelGGL((k_lookup_service3<RingView>), dim3(waves), dim3(64), 0, r.svc_st, r.svc_dev, r.view(), fv,
+                           r.cview(), r.compact ? 1u : 0u, last, idle, maxt, warm, prof, dt, r.svc_dtb,
+                           waves > 1 ? (uint32_t)env_pos("RP_SVC_PERIOD", kSvcPeriod) : 0u);
     } else
         hipLaunchKernelGGL((k_lookup_service<RingView>), dim3(1), dim3(64), 0, r.svc_st, r.svc_dev, r.view(), fv,
                            r.compact ? 1u : 0u, last, idle, maxt);
@@ -3216,9 +3239,10 @@ static bool svc_lookup(rp::Ring& r, const char* key, uint32_t len, const uint32_
     // v2: the answer line is taken when all 8 of its words carry seq s (no torn line)
     auto answered = [&]() -> bool {
         if (!r.svc_v2) return __atomic_load_n(&io->resp_seq[0], __ATOMIC_ACQUIRE) == s;
-        if ((uint32_t)(__atomic_load_n(&io->resp2[7], __ATOMIC_ACQUIRE) >> 32) != s) return false;
+        const uint64_t* a = io->resp2[s & 7u];
+        if ((uint32_t)(__atomic_load_n(&a[7], __ATOMIC_ACQUIRE) >> 32) != s) return false;
         for (int q = 0; q < 7; q++)
-            if ((uint32_t)(__atomic_load_n(&io->resp2[q], __ATOMIC_ACQUIRE) >> 32) != s) return false;
+            if ((uint32_t)(__atomic_load_n(&a[q], __ATOMIC_ACQUIRE) >> 32) != s) return false;
         return true;
     };
     while (!answered()) {
@@ -3243,7 +3267,7 @@ static bool svc_lookup(rp::Ring& r, const char* key, uint32_t len, const uint32_
     if (r.svc_v2) {
         uint32_t c = 0;
         for (uint32_t q = 0; q < W; q++) {
-            owners[q] = (uint32_t)io->resp2[q];
+            owners[q] = (uint32_t)io->resp2[s & 7u][q];
             c += (c == q && owners[q] != NIL) ? 1u : 0u;
         }
         if (counts) counts[0] = (uint8_t)c;
