@@ -1666,6 +1666,37 @@ __device__ __forceinline__ bool dt_answer(uint32_t x, uint32_t lane, uint32_t h,
     return true;
 }
 
+// dt_answer without LDS (round 6, the default; RP_SVC_ANS=0 keeps dt_answer): the items stay where
+// the record puts them, in item order by lane (the bucket's tokens >= h in lanes 1..c, the
+// successors spread to lanes 16..31 by one shuffle), and the first `need` distinct owners are
+// taken one at a time: the first remaining lane's owner, then every lane holding it dropped by a
+// ballot. A lookup (need 1) is one step; no 23-step duplicate scan, no LDS slots.
+__device__ __forceinline__ bool dt_answer_fast(uint32_t x, uint32_t lane, uint32_t h, uint32_t B, uint32_t need,
+                                               uint32_t& mine, int& cnt) {
+    const uint32_t w0 = __builtin_amdgcn_readlane(x, 0);
+    const uint32_t c = w0 & 15u, ns = (w0 >> 8) & 31u, complete = (w0 >> 16) & 1u;
+    if (c > kDtEnt) return false;
+    const uint32_t rmask = (1u << (32u - B)) - 1u, hr = h & rmask;
+    const uint32_t k = lane - 16u;
+    const bool sl = lane >= 16u && k < kDtSucc;
+    const uint32_t sw = __shfl(x, 8u + ((sl ? k : 0u) >> 1), 64);
+    const bool tk = lane >= 1u && lane <= c && (x & 0xFFFFu & rmask) >= hr;
+    const bool su = sl && k < ns;
+    const uint32_t t = tk ? (x >> 16) : ((sw >> (16u * (k & 1u))) & 0xFFFFu);
+    uint64_t rem = __ballot(tk || su);
+    uint32_t got = 0;
+    mine = NIL;
+    while (got < need && rem) {
+        const uint32_t v = __builtin_amdgcn_readlane(t, (uint32_t)__builtin_ctzll(rem));
+        mine = lane == got ? v : mine;
+        rem &= ~__ballot(t == v);
+        got++;
+    }
+    if (got < need && !complete) return false;
+    cnt = (int)got;
+    return true;
+}
+
 // The lookup service, round 5 form (RP_RING_SVC=2, the default). Round 5 measured the round-4
 // kernel's call (5.0 us in node) with device stamps (RP_SVC_PROF): the poll's PCIe round trip
 // ~1.1 us, the key's farmhash on one lane from LDS ~0.5 us, three dependent table trips, the
@@ -1697,7 +1728,7 @@ __global__ __launch_bounds__(64) void k_lookup_service3(SvcLines* io, View rv, C
                                                        uint32_t use_compact, uint32_t last, uint64_t idle_ticks,
                                                        uint64_t max_ticks, uint32_t warm, uint32_t prof,
                                                        const uint32_t* __restrict__ dt, uint32_t dtb,
-                                                       uint32_t period) {
+                                                       uint32_t period, uint32_t ans_old) {
     __shared__ uint32_t dslot[8];
     const uint32_t lane = threadIdx.x;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
@@ -1729,9 +1760,10 @@ __global__ __launch_bounds__(64) void k_lookup_service3(SvcLines* io, View rv, C
                 woff = woff + 4096 >= nwarm ? 0 : woff + 4096;
             }
         }
-        const uint32_t seq = __builtin_amdgcn_readfirstlane(__shfl(v, 0, 64));
-        const uint32_t stop = __builtin_amdgcn_readfirstlane(__shfl(v, 4, 64));
-        const uint32_t tail = __builtin_amdgcn_readfirstlane(__shfl(v, 15, 64));
+        const uint32_t seq = __builtin_amdgcn_readlane(v, 0);  // (register reads, no LDS trip)
+        const uint32_t stop = __builtin_amdgcn_readlane(v, 4);
+        const uint32_t tail = __builtin_amdgcn_readlane(v, 15);
+        asm volatile("s_waitcnt vmcnt(0)" ::"s"(seq) : "memory");  // the clock read after the poll's return
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
         if (stop || now - t_start > max_ticks) break;
         if (seq == last || tail != seq) {
@@ -1741,9 +1773,9 @@ __global__ __launch_bounds__(64) void k_lookup_service3(SvcLines* io, View rv, C
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the warm load, before the lookup's own
         asm volatile("" ::"v"(acc));
-        const uint32_t hk = __builtin_amdgcn_readfirstlane(__shfl(v, 1, 64));
-        const int np = (int)__builtin_amdgcn_readfirstlane(__shfl(v, 2, 64));
-        const uint32_t W = __builtin_amdgcn_readfirstlane(__shfl(v, 3, 64));
+        const uint32_t hk = __builtin_amdgcn_readlane(v, 1);
+        const int np = (int)__builtin_amdgcn_readlane(v, 2);
+        const uint32_t W = __builtin_amdgcn_readlane(v, 3);
         uint32_t res[8] = {NIL, NIL, NIL, NIL, NIL, NIL, NIL, NIL};
         uint32_t path = 0;
         bool dok = false;
@@ -1751,35 +1783,37 @@ __global__ __launch_bounds__(64) void k_lookup_service3(SvcLines* io, View rv, C
         if (dt && np >= 1 && np <= 8) {  // the direct table: one 64-B line, lanes 0..15
             const uint32_t x = lane < 16 ? dt[16ull * (hk >> (32u - dtb)) + lane] : 0u;
             int c = 0;
-            dok = dt_answer(x, lane, hk, dtb, (uint32_t)np, dslot, dmine, c);
+            dok = ans_old ? dt_answer(x, lane, hk, dtb, (uint32_t)np, dslot, dmine, c)
+                          : dt_answer_fast(x, lane, hk, dtb, (uint32_t)np, dmine, c);
             path = dok ? 4u : 0u;
         }
-        if (lane == 0 && !dok) {
-            bool ok = false;
-            if (use_compact && np >= 1 && np <= 4) {
-                uint32_t r4[4] = {NIL, NIL, NIL, NIL};
-                int c = 0;
-                ok = svc_compact_window(cv, hk, np, r4, c);
-                path = ok ? 1u : 2u;
-                if (!ok) {
-                    c = compact_fix_walk(fv, hk, np, r4);
-                    ok = true;
+        uint32_t o = dmine;
+        if (!dok) {  // (wave-uniform) the compact window or the walks, on lane 0
+            if (lane == 0) {
+                bool ok = false;
+                if (use_compact && np >= 1 && np <= 4) {
+                    uint32_t r4[4] = {NIL, NIL, NIL, NIL};
+                    int c = 0;
+                    ok = svc_compact_window(cv, hk, np, r4, c);
+                    path = ok ? 1u : 2u;
+                    if (!ok) {
+                        c = compact_fix_walk(fv, hk, np, r4);
+                        ok = true;
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; q++) res[q] = r4[q];
                 }
-#pragma unroll
-                for (int q = 0; q < 4; q++) res[q] = r4[q];
+                if (!ok) {
+                    ring_walk<8>(rv, rv.find(hk), np > 8 ? 8 : np, res);
+                    path = 3;
+                }
             }
-            if (!ok) {
-                ring_walk<8>(rv, rv.find(hk), np > 8 ? 8 : np, res);
-                path = 3;
+#pragma unroll
+            for (uint32_t q = 0; q < 8; q++) {
+                const uint32_t x = __shfl(res[q], 0, 64);
+                o = lane == q ? x : o;
             }
         }
-        uint32_t o = NIL;
-#pragma unroll
-        for (uint32_t q = 0; q < 8; q++) {
-            const uint32_t x = __shfl(res[q], 0, 64);
-            o = lane == q ? x : o;
-        }
-        if (dok) o = dmine;
         if (prof) {  // diag: seq, poll round trip, lookup (ticks), path
             asm volatile("" ::"v"(o));
             const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
@@ -2941,7 +2975,8 @@ static void svc_launch(rp::Ring& r, uint32_t last) {
         const uint32_t waves = (uint32_t)std::min<uint64_t>(env_pos("RP_SVC_WAVES", kSvcWaves), 16);
         hipLaunchKernelGGL((k_lookup_service3<RingView>), dim3(waves), dim3(64), 0, r.svc_st, r.svc_dev, r.view(), fv,
                            r.cview(), r.compact ? 1u : 0u, last, idle, maxt, warm, prof, dt, r.svc_dtb,
-                           waves > 1 ? (uint32_t)env_pos("RP_SVC_PERIOD", kSvcPeriod) : 0u);
+                           waves > 1 ? (uint32_t)env_pos("RP_SVC_PERIOD", kSvcPeriod) : 0u,
+                           (getenv("RP_SVC_ANS") && !strcmp(getenv("RP_SVC_ANS"), "0")) ? 1u : 0u);
     } else
         hipLaunchKernelGGL((k_lookup_service<RingView>), dim3(1), dim3(64), 0, r.svc_st, r.svc_dev, r.view(), fv,
                            r.compact ? 1u : 0u, last, idle, maxt);

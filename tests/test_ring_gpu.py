@@ -222,7 +222,8 @@ def test_small_host_batches_vs_oracle(gpu, orc, nkeys, monkeypatch):
     assert np.array_equal(g0, g1) and np.array_equal(c0, c1)
 
 
-@pytest.mark.parametrize("svc", ["2", "2-nodt", "2-w1", "1"], ids=["v3", "v3-window", "v3-one-wave", "round4"])
+@pytest.mark.parametrize("svc", ["2", "2-nodt", "2-w1", "2-ans0", "1"],
+                         ids=["v3", "v3-window", "v3-one-wave", "v3-lds-answer", "round4"])
 def test_lookup_service_vs_oracle(gpu, orc, svc, monkeypatch):
     """The resident lookup service (rp_ring_service): one-key lookup / lookupN calls through
     pinned host lines, against the oracle, for key lengths 0..180 (1-3 key lines; longer keys
@@ -230,13 +231,17 @@ def test_lookup_service_vs_oracle(gpu, orc, svc, monkeypatch):
     the table it reads), an idle exit (the next call relaunches it) and turning it off. "v3":
     the host-hashed service with its direct table (few servers: the successor lists are
     complete) and its kSvcWaves pollers answering each request, some more than once;
-    "v3-window": RP_SVC_DT=0, the compact window and walks; "v3-one-wave": RP_SVC_WAVES=1."""
+    "v3-window": RP_SVC_DT=0, the compact window and walks; "v3-one-wave": RP_SVC_WAVES=1;
+    "v3-lds-answer": RP_SVC_ANS=0, the round-5 record answer (LDS slots, duplicate scan)."""
     if svc.endswith("-nodt"):
         monkeypatch.setenv("RP_SVC_DT", "0")
         svc = svc[:-5]
     if svc.endswith("-w1"):
         monkeypatch.setenv("RP_SVC_WAVES", "1")
         svc = svc[:-3]
+    if svc.endswith("-ans0"):
+        monkeypatch.setenv("RP_SVC_ANS", "0")
+        svc = svc[:-5]
     import time
     ring, oracle = _random_history(orc, gpu, 8, 50, 100, 3)
     rng = random.Random(77)
