@@ -109,9 +109,10 @@ int rp_ring_lookupn(rp_ring *r, const char *keys, const uint64_t *off, uint32_t 
                     int32_t nrep, uint32_t *owners, uint8_t *counts);
 /* Low-latency single calls (RingPop.lookup / lookupN per request, index.js:434-471): with
  * idle_ms > 0, a one-key rp_ring_lookup / rp_ring_lookupn / rp_ring_lookupn_hashes (n <= 8; the
- * host hashes the key) is answered by a resident service wave (one workgroup on one CU) that
- * polls a pinned, device-mapped request line and reads one record of its direct table (built at
- * its first launch after a ring change), instead of a kernel launch and a stream sync per call. The wave exits after idle_ms without a
+ * host hashes the key) is answered by a resident service (eight one-wave workgroups, one an XCD,
+ * RP_SVC_WAVES) that polls a pinned, device-mapped request line on a staggered schedule and reads
+ * one record of its direct table (built at its first launch after a ring change), instead of a
+ * kernel launch and a stream sync per call. The waves exit after idle_ms without a
  * request (and after 30 s in all) and is relaunched by the next call; a ring mutation and every
  * other device call on this ring (batch lookups, grouping, dump) stop it first. Every device
  * call of this library on any other handle stops every resident service as well and keeps new

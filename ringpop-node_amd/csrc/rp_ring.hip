@@ -1747,9 +1747,16 @@ __global__ __launch_bounds__(64) void k_lookup_service3(SvcLines* io, View rv, C
             do slot += period;
             while (slot <= t);
         }
+        if (warm == 2 && dt) {  // this wave's slice of the direct table, a record a lane per poll, issued
+            // before the poll (loads return in order: one behind the poll would hold up the lookup's)
+            const uint64_t nrec = 1ull << dtb, r0 = nrec * blockIdx.x / gridDim.x, r1 = nrec * (blockIdx.x + 1) / gridDim.x;
+            const uint64_t r = r0 + woff + lane;
+            acc ^= r < r1 ? dt[16ull * r] : 0u;
+            woff = r0 + woff + 64 >= r1 ? 0 : woff + 64;
+        }
         const uint64_t tp = __builtin_amdgcn_s_memrealtime();
         const uint32_t v = lane < 16 ? __hip_atomic_load(&io->req[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
-        if (warm && use_compact) {  // issued after the poll, done within its round trip
+        if (warm == 1 && use_compact) {  // issued after the poll, done within its round trip
 #pragma unroll
             for (int k = 0; k < 8; k++) {
                 const uint64_t o = woff + 64ull * lane;
@@ -1763,7 +1770,7 @@ __global__ __launch_bounds__(64) void k_lookup_service3(SvcLines* io, View rv, C
         const uint32_t seq = __builtin_amdgcn_readlane(v, 0);  // (register reads, no LDS trip)
         const uint32_t stop = __builtin_amdgcn_readlane(v, 4);
         const uint32_t tail = __builtin_amdgcn_readlane(v, 15);
-        asm volatile("s_waitcnt vmcnt(0)" ::"s"(seq) : "memory");  // the clock read after the poll's return
+        if (prof) asm volatile("s_waitcnt vmcnt(0)" ::"s"(seq) : "memory");  // (stamps) the clock after the poll
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
         if (stop || now - t_start > max_ticks) break;
         if (seq == last || tail != seq) {
@@ -2955,7 +2962,7 @@ static void svc_launch(rp::Ring& r, uint32_t last) {
     const uint64_t idle = (uint64_t)r.svc_idle_ms * 100000ull, maxt = 30ull * 100000000ull;  // 100 MHz ticks
     const CompactFixView fv{r.tok.p, r.own.p, r.cidx.p, r.view(), r.M, r.ccb};
     if (r.svc_v2) {
-        const uint32_t warm = (uint32_t)env_pos("RP_SVC_WARM", 0) == 1u, prof = getenv("RP_SVC_PROF") ? 1u : 0u;
+        const uint32_t warm = (uint32_t)env_pos("RP_SVC_WARM", 0), prof = getenv("RP_SVC_PROF") ? 1u : 0u;
         if (!r.svc_dt_valid) {  // the direct table for this ring (A/B: RP_SVC_DT=0)
             r.svc_dtb = 0;
             uint32_t B = 16;
