@@ -188,7 +188,7 @@ def sim_cpu_baseline(n, kill_pct=1, seed=11, min_seconds=15.0, max_rounds=60, th
 # ------------------------------------------------------------------ device legs
 
 def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=512, warmup=3, world=1, dist=None,
-                reduce_max=None, extras=True):
+                reduce_max=None, extras=True, part_log2=22):
     """C3 (BASELINE.json configs[2]): 100k-member table, a stream of batches of 100k updates (1%
     repeated addresses), Membership.update fold + one checksum per batch, inputs resident in HBM.
     Also: the fold alone (checksum deferred) against the HBM roofline at 49 B/update, the
@@ -265,6 +265,9 @@ def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=512, warmup=3, 
                    "%d batches that drain adds ~%.1f us per batch" % (batches, 4400.0 / batches)}
     if world > 1 or not extras:  # the fold-only and large-batch legs are per-replica: rank 0's one-GPU run
         m.close()
+        if world > 1 and extras:
+            out["fold_large_partitioned"] = fold_large_part_bench(rpa, torch, S, local, world, dist, reduce_max,
+                                                                  nb=1 << part_log2)
         return out
     # the fold alone (k_link + k_fold_fast + the gated sorted path), HIP events per batch on the
     # launch stream
@@ -347,6 +350,50 @@ def merge_bench(rpa, torch, local, n=100_000, k=100_000, batches=512, warmup=3, 
     del big, big2, app, nst, ninc
     torch.cuda.empty_cache()
     return out
+
+
+def fold_large_part_bench(rpa, torch, S, local, world, dist, reduce_max, nb=1 << 22):
+    """The 2^22-update fold (fold_large) partitioned by member id over the ranks (PartMembership,
+    SURVEY §8e's row partition): every rank holds the whole batch in HBM and folds the changes of
+    its own 1/G of the ids (rp_members_update_range_dev: the scatter reads every change, writes
+    and folds only its buckets'), in place, no checksum; HIP events per batch on each rank, the
+    slowest rank's mean reported (strong scaling: the batch is fixed)."""
+    names_b = [c2_addr(i) for i in range(nb)]
+    mb = rpa.PartMembership(whoami=names_b[0], capacity=nb, device=local)
+    idb = np.asarray(mb.intern(names_b), dtype=np.uint32)
+    incb = S.c3_members(nb)[2]
+    mb.update_ids(idb, np.zeros(nb, np.uint8), incb, now_ms=1)
+    big = [tuple(torch.from_numpy(x).cuda() for x in (a.view(np.int32), s_, i_))
+           for a, s_, i_ in [S.c3_updates(nb, nb, seed=300 + b, base_inc=incb + 3 * b) for b in range(7)]]
+    app = torch.empty(nb, dtype=torch.uint8, device="cuda")
+    na = torch.zeros(1, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+
+    def one(b):
+        d = big[b % len(big)]
+        mb.update_dev(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), nb, 1434500000000 + b, app.data_ptr(),
+                      d[1].data_ptr(), d[2].data_ptr(), na.data_ptr(), sp)
+
+    one(0)
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(6)]
+    dist.barrier()
+    torch.cuda._sleep(4_000_000)  # (the host enqueues every batch before the GPU reaches them)
+    for b in range(6):
+        evs[b][0].record(stream)
+        one(b + 1)
+        evs[b][1].record(stream)
+    torch.cuda.synchronize()
+    ms = float(np.mean([a.elapsed_time(c) for a, c in evs]))
+    ms = reduce_max([ms])[0]
+    mb.close()
+    del big, app
+    torch.cuda.empty_cache()
+    return {"members": nb, "updates_per_batch": nb, "n_gpus": world, "scaling": "strong", "ms_per_batch": ms,
+            "updates_per_s": nb / (ms * 1e-3),
+            "note": "each rank folds the changes of its own 1/%d of the member ids out of the whole batch "
+                    "(outputs in place, no checksum); the slowest rank's mean over 6 batches" % world}
 
 
 def sim_bench(rpa, torch, dist, local, n=10_000, kill_pct=1, seed=11, max_rounds=300, max_seconds=240.0, world=1,
@@ -590,6 +637,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-merge", action="store_true")
+    ap.add_argument("--part-log2", type=int, default=22,
+                    help="members and updates per batch (log2) of the partitioned fold leg at --gpus > 1")
     ap.add_argument("--merge-batches", type=int, default=2048,
                     help="C3 update batches in the timed stream (the final group's chains, one 4.4 ms chain latency, "
                          "are inside it: 2.1 us per batch at 2048, 8.6 at 512)")
@@ -680,7 +729,7 @@ def main():
     merge = None
     if not args.no_merge:
         merge = merge_bench(rpa, torch, local, batches=args.merge_batches, world=world, dist=dist,
-                            reduce_max=reduce_max)
+                            reduce_max=reduce_max, part_log2=args.part_log2)
     sim5 = sim_bench(rpa, torch, dist, local, n=args.sim5_n, world=world, reduce_max=reduce_max) \
         if args.sim5_n else None
     if rank == 0:

@@ -183,6 +183,21 @@ int rp_members_update(rp_members *m, const uint32_t *ids, const uint8_t *status,
 int rp_members_update_dev(rp_members *m, const uint32_t *d_ids, const uint8_t *d_status, const int64_t *d_inc,
                           uint32_t k, int64_t now_ms, uint8_t *d_applied, uint8_t *d_new_status,
                           int64_t *d_new_inc, uint32_t *d_n_applied, void *stream);
+/* The merge partitioned by member id (lib/membership/index.js:249-324 split by id):
+ * the same update over device buffers, applied only to the changes whose id lies in [id_lo,
+ * id_hi) (whole buckets of 4,096 ids; id_hi may be the capacity). Those changes are evaluated in
+ * array order as update_dev would; the outputs (applied, new status / incarnation) of the other
+ * changes are left as they were, *d_n_applied counts this range's applied changes, and rows
+ * outside the range are not touched. No checksum is computed: a caller holding the table in
+ * ranges brings the rows together (rp_members_rows_copy) and calls rp_members_compute_checksum.
+ * Always the bucket path (no damp scoring, at most 8M ids). Stream-ordered, no host sync. */
+int rp_members_update_range_dev(rp_members *m, const uint32_t *d_ids, const uint8_t *d_status,
+                                const int64_t *d_inc, uint32_t k, int64_t now_ms, uint32_t id_lo, uint32_t id_hi,
+                                uint8_t *d_applied, uint8_t *d_new_status, int64_t *d_new_inc,
+                                uint32_t *d_n_applied, void *stream);
+/* The member rows of ids [id_lo, id_hi) (8 B each: incarnation << 3 | exists << 2 | status) to
+ * (into_table = 0) or from (1) a device buffer, on `stream`. */
+int rp_members_rows_copy(rp_members *m, void *d_buf, uint32_t id_lo, uint32_t id_hi, int into_table, void *stream);
 /* membership.checksum (null until the first applied update: *is_set = 0). */
 /* Membership.set (lib/membership/index.js:208-247) over the stash of k changes received while
  * not ready (arrival order; the caller keeps the stash, index.js:259-265):

@@ -77,6 +77,8 @@ SIGNATURES = {
     "rp_members_set_local": (_INT, [_P, _U32]),
     "rp_members_update": (_INT, [_P, _P, _P, _P, _U32, ctypes.c_int64, _P, _P, _P, _P]),
     "rp_members_update_dev": (_INT, [_P, _P, _P, _P, _U32, ctypes.c_int64, _P, _P, _P, _P, _P]),
+    "rp_members_update_range_dev": (_INT, [_P, _P, _P, _P, _U32, ctypes.c_int64, _U32, _U32, _P, _P, _P, _P, _P]),
+    "rp_members_rows_copy": (_INT, [_P, _P, _U32, _U32, ctypes.c_int, _P]),
     "rp_members_set": (_INT, [_P, _P, _P, _P, _U32, _P, _P]),
     "rp_members_set_dev": (_INT, [_P, _P, _P, _P, _U32, _P, _P, _P]),
     "rp_members_checksum": (_INT, [_P, _P, _P]),
@@ -644,6 +646,17 @@ class Membership:
         check(lib().rp_members_update_dev(self._h, d_ids, d_status, d_inc, k, int(now_ms), d_applied, d_new_status,
                                           d_new_inc, d_n_applied, stream))
 
+    def update_range_dev(self, d_ids, d_status, d_inc, k, now_ms, id_lo, id_hi, d_applied=None, d_new_status=None,
+                         d_new_inc=None, d_n_applied=None, stream=None):
+        """update_dev applied only to the changes whose id lies in [id_lo, id_hi) (whole buckets of
+        4,096 ids; rp_members_update_range_dev): no checksum, other changes' outputs untouched."""
+        check(lib().rp_members_update_range_dev(self._h, d_ids, d_status, d_inc, k, int(now_ms), id_lo, id_hi,
+                                                d_applied, d_new_status, d_new_inc, d_n_applied, stream))
+
+    def rows_copy(self, d_buf, id_lo, id_hi, into_table, stream=None):
+        """Member rows [id_lo, id_hi) (8 B each) to (into_table False) or from a device buffer."""
+        check(lib().rp_members_rows_copy(self._h, d_buf, id_lo, id_hi, 1 if into_table else 0, stream))
+
     def checksum_shard(self, nshards, shard, history_cap=0):
         """From now on checksum only update batches b % nshards == shard (rp_members_checksum_shard),
         recording each one's checksum when history_cap > 0."""
@@ -789,6 +802,90 @@ class DistMembership(Membership):
         A collective: every rank calls it."""
         self._gather()
         return list(self._out)
+
+
+class PartMembership(Membership):
+    """Membership.update over G GPUs partitioned by member id (SURVEY §8e's row partition of
+    lib/membership/index.js:249-324): rank g owns the ids [lo_g, hi_g) (equal runs of whole
+    4,096-id buckets of the capacity given here; the last rank's run is open-ended), folds only
+    the changes of its ids out of each batch (rp_members_update_range_dev) and keeps only its own
+    rows current. The batch is on every rank (as the reference's one process holds it), so no
+    change crosses ranks; every rank scans the batch and folds 1/G of it. The checksum hashes
+    every row in address order, so compute_checksum() / dump() first bring the ranges together
+    (one all-gather of 8 B per member: RCCL device tensors, or gloo host tensors) and are
+    collectives. Per-change outputs (applied, new status / incarnation) are written on the rank
+    that owns the change's id; update_dev returns nothing else. The replicated form
+    (DistMembership) is what C3's per-batch checksums want; this one is for large batches whose
+    fold is the cost."""
+
+    BUCKET = 4096
+
+    def __init__(self, whoami=None, capacity=1024, device=0, group=None):
+        import torch.distributed as dist
+        super().__init__(whoami=whoami, capacity=capacity, device=device)
+        self._dist = dist
+        self._group = group
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        nb = -(-max(int(capacity), 1) // self.BUCKET)
+        self.per_ids = -(-nb // self.world) * self.BUCKET
+        self.id_lo = min(self.rank * self.per_ids, nb * self.BUCKET)
+        self.id_hi = 0xFFFFF000 if self.rank == self.world - 1 else min((self.rank + 1) * self.per_ids,
+                                                                          nb * self.BUCKET)
+
+    def update_dev(self, d_ids, d_status, d_inc, k, now_ms, d_applied=None, d_new_status=None, d_new_inc=None,
+                   d_n_applied=None, stream=None):
+        """This rank's part of Membership.update over device buffers (stream-ordered, no sync)."""
+        self.update_range_dev(d_ids, d_status, d_inc, k, now_ms, self.id_lo, self.id_hi, d_applied, d_new_status,
+                              d_new_inc, d_n_applied, stream)
+
+    def gather_rows(self):
+        """Make this rank's table whole: every rank's own rows all-gathered (a collective)."""
+        import torch
+        n = ctypes.c_uint32()
+        check(lib().rp_members_count(self._h, ctypes.byref(n)))
+        nid = n.value
+        if self.world == 1 or nid == 0:
+            return
+        per = self.per_ids
+        if nid > self.world * per:
+            raise RingpopAmdError("PartMembership: %d members outgrew the partition of %d ids; construct it "
+                                  "with the capacity the table will reach" % (nid, self.world * per))
+        lo, hi = min(self.id_lo, nid), min(self.rank * per + per, nid)
+        sp = torch.cuda.current_stream().cuda_stream
+        mine = torch.zeros(per * 8, dtype=torch.uint8, device="cuda")
+        if hi > lo:
+            self.rows_copy(mine.data_ptr(), lo, hi, False, sp)
+        if self._dist.get_backend(self._group) == "nccl":
+            full = torch.empty(self.world * per * 8, dtype=torch.uint8, device="cuda")
+            self._dist.all_gather_into_tensor(full, mine, group=self._group)
+        else:  # gloo: host tensors
+            parts = [torch.empty(per * 8, dtype=torch.uint8) for _ in range(self.world)]
+            self._dist.all_gather(parts, mine.cpu(), group=self._group)
+            full = torch.cat(parts).cuda()
+        for g in range(self.world):
+            a, b = g * per, min(g * per + per, nid)
+            if g != self.rank and b > a:
+                self.rows_copy(full.data_ptr() + a * 8, a, b, True, sp)
+        torch.cuda.current_stream().synchronize()
+
+    @property
+    def checksum(self):
+        if self.world == 1:
+            return Membership.checksum.fget(self)
+        raise RingpopAmdError("PartMembership.checksum over %d ranks needs the rows together: call "
+                              "compute_checksum() on every rank" % self.world)
+
+    def compute_checksum(self):
+        """computeChecksum() over the whole table (a collective: gathers the rows first)."""
+        self.gather_rows()
+        check(lib().rp_members_compute_checksum(self._h))
+        return Membership.checksum.fget(self)
+
+    def dump(self):
+        """The whole table (a collective: gathers the rows first)."""
+        self.gather_rows()
+        return Membership.dump(self)
 
 
 SIM_EVENT = {"kill": 0, "revive": 1, "leave": 2, "join": 3}

@@ -522,7 +522,7 @@ __global__ __launch_bounds__(kBkST) void k_bk_scatter(const uint32_t* __restrict
                                                     uint32_t ntiles, BRec* __restrict__ recs,
                                                     uint32_t* __restrict__ seg, int64_t* __restrict__ tb,
                                                     uint8_t* __restrict__ nst, int64_t* __restrict__ ninc,
-                                                    uint32_t* __restrict__ err) {
+                                                    uint32_t* __restrict__ err, uint32_t b_lo, uint32_t b_hi) {
     __shared__ __attribute__((aligned(16))) uint32_t stage[kBkTile * 3];
     __shared__ uint32_t h[kBkMaxBuckets], s_w[kBkST / 64];
     __shared__ int64_t s_mn[kBkST / 64], s_mx[kBkST / 64];
@@ -561,8 +561,11 @@ __global__ __launch_bounds__(kBkST) void k_bk_scatter(const uint32_t* __restrict
         for (uint32_t q = 0; q < PER; q++) {
             const uint32_t i = tid + q * kBkST;
             if (i < n) {
-                if (cst) nst[base + i] = stv[q];
-                if (cinc) ninc[base + i] = incv[q];
+                const uint32_t bq = idv[q] >> kBkBits;
+                if (bq >= b_lo && bq < b_hi) {  // (a range update: only its own buckets' outputs)
+                    if (cst) nst[base + i] = stv[q];
+                    if (cinc) ninc[base + i] = incv[q];
+                }
                 bad |= stv[q] > 3u;
             }
         }
@@ -627,10 +630,12 @@ __global__ __launch_bounds__(kBkST) void k_bk_scatter(const uint32_t* __restrict
         if (LOOP && t + gridDim.x < ntiles) load(t + gridDim.x);  // in flight under the stores below
         __syncthreads();
         // the tile's run: n records of 8 or 12 B at recs + tile * kBkTile (16-B stores; the tile's
-        // run starts 16-B aligned, and its padded tail is never read)
+        // run starts 16-B aligned, and its padded tail is never read). A range update stores only
+        // the part of the run its buckets [b_lo, b_hi) hold (records sorted by bucket: one stretch)
         uint4* d4 = reinterpret_cast<uint4*>(recs + (uint64_t)t * kBkTile);
         const uint4* s4 = reinterpret_cast<const uint4*>(stage);
-        for (uint32_t q = tid; q < (rw * n + 3u) / 4u; q += kBkST) d4[q] = s4[q];
+        const uint32_t r0 = b_lo < nb ? ls[b_lo] : n, r1 = b_hi < nb ? ls[b_hi] : n;
+        for (uint32_t q = (rw * r0) / 4u + tid; q < (rw * r1 + 3u) / 4u; q += kBkST) d4[q] = s4[q];
     }
 }
 
@@ -685,7 +690,7 @@ __device__ unsigned long long g_bk_wg[2 * kBkMaxBuckets];  // per bucket: start,
 template <bool DIRECT>
 __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs, const uint32_t* __restrict__ seg,
                                                   const int64_t* __restrict__ tb, uint32_t ntiles, uint32_t nb,
-                                                  FoldArgs A,
+                                                  uint32_t b_lo, uint32_t b_hi, FoldArgs A,
                                                   uint32_t* __restrict__ res2, uint8_t* __restrict__ resj,
                                                   uint32_t* __restrict__ ovf, uint32_t* __restrict__ part) {
     // fjs: per id the first change's {batch index | status << 30} (kBkNone: none; kBkRep set when
@@ -702,8 +707,9 @@ __global__ __launch_bounds__(kBkFT) void k_bk_fold(const BRec* __restrict__ recs
     // XCD-aware: blocks are dealt round-robin over the 8 XCDs, so block i's XCD folds the
     // contiguous bucket range (i % 8) * per ...: neighbouring buckets, whose segments share record
     // lines in every tile run, fold at the same time in one L2
-    const uint32_t per = (nb + 7) / 8, b = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
-    if (b >= nb) return;
+    // (a range update folds buckets [b_lo, b_hi) only; the whole table: 0, nb)
+    const uint32_t per = (b_hi - b_lo + 7) / 8, b = b_lo + (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+    if (b >= b_hi) return;
     const uint32_t tid = threadIdx.x, id0 = b << kBkBits;
 #ifdef RP_BK_PROF
     if (tid == 0) g_bk_wg[2 * b] = __builtin_amdgcn_s_memrealtime();
@@ -1420,15 +1426,25 @@ struct Members {
     // Grouped path (every batch size): k_link + k_fold_fast + k_fold_ovf (gated on the overflow
     // word on the device: it folds only addresses with more than kSlots + 1 changes, and sums
     // the applied count into n_applied_out). RP_MEMBERS_SORTED_FOLD=1: radix sort + k_fold.
+    // ranged (rp_members_update_range_dev): only the changes whose id lies in [id_lo, id_hi), whole
+    // buckets of kBk ids, through the bucket path; no checksum (the rows outside are not this
+    // handle's to keep current).
     void update_dev(const uint32_t* ids, const uint8_t* chs, const int64_t* chi, uint32_t k, int64_t now_ms,
-                    uint8_t* applied, uint8_t* nst, int64_t* ninc, uint32_t* n_applied_out, hipStream_t s) {
+                    uint8_t* applied, uint8_t* nst, int64_t* ninc, uint32_t* n_applied_out, hipStream_t s,
+                    bool ranged = false, uint32_t id_lo = 0, uint32_t id_hi = 0) {
+        if (ranged) {
+            RP_REQUIRE(id_lo % kBk == 0 && (id_hi % kBk == 0 || id_hi >= cap) && id_lo <= id_hi,
+                       "update_range: the range must be whole buckets of 4,096 ids");
+            RP_REQUIRE(!damp_on && grouped_fold && (cap + kBk - 1) / kBk <= kBkMaxBuckets && k < (1u << 29),
+                       "update_range: needs the bucket fold (no damp scoring, at most 8M ids)");
+        }
         if (s != st) RP_HIP(hipStreamSynchronize(st));
         if (!k) {
             RP_HIP(hipMemsetAsync(napplied.p, 0, sizeof(uint32_t), s));
             if (n_applied_out) RP_HIP(hipMemsetAsync(n_applied_out, 0, sizeof(uint32_t), s));
             return;
         }
-        if (pw.on && (pw.st != s || use_bucket_fold(k, (cap + kBk - 1) / kBk) || !grouped_fold ||
+        if (pw.on && (ranged || pw.st != s || use_bucket_fold(k, (cap + kBk - 1) / kBk) || !grouped_fold ||
                       getenv_on("RP_MEMBERS_FUSE")))
             drain_write();  // only the grouped fold's launch carries a deferred string
         if (damp_on) {
@@ -1450,7 +1466,7 @@ struct Members {
         uint32_t* done = napplied.p + 2;
         const unsigned g = grid_for(k, 256);
         const bool mine = ck_nsh <= 1 || batch_no % ck_nsh == ck_sh;
-        const bool build = !defer_ck && mine;
+        const bool build = !defer_ck && mine && !ranged;
         if (build && hist_cap && nt.size()) {  // refuse before anything is applied
             uint32_t pend = 0;
             for (uint64_t w : pend_mask.w) pend += (uint32_t)__builtin_popcountll(w);
@@ -1460,7 +1476,9 @@ struct Members {
         }
         batch_no++;
         const uint32_t nb = (cap + kBk - 1) / kBk;
-        if (use_bucket_fold(k, nb)) {
+        const uint32_t b_lo = ranged ? std::min(nb, id_lo / kBk) : 0u;
+        const uint32_t b_hi = ranged ? (uint32_t)std::min<uint64_t>(nb, ((uint64_t)id_hi + kBk - 1) / kBk) : nb;
+        if (ranged || use_bucket_fold(k, nb)) {
             const uint32_t ntiles = (k + kBkTile - 1) / kBkTile;
             bk_seg.reserve((uint64_t)((nb + 15) / 16) * 16 * ntiles);
             bk_recs.reserve((uint64_t)ntiles * kBkTile);
@@ -1473,17 +1491,19 @@ struct Members {
             const uint32_t sg = (uint32_t)env_pos("RP_BK_SGRID", 0);
             if (sg && sg < ntiles)
                 hipLaunchKernelGGL(k_bk_scatter<true>, dim3(sg), dim3(kBkST), 0, s, ids, chs, chi, k, nb, ntiles,
-                                   bk_recs.p, bk_seg.p, rec8 ? bk_tb.p : nullptr, nst, ninc, ws.err.p);
+                                   bk_recs.p, bk_seg.p, rec8 ? bk_tb.p : nullptr, nst, ninc, ws.err.p, b_lo, b_hi);
             else
                 hipLaunchKernelGGL(k_bk_scatter<false>, dim3(ntiles), dim3(kBkST), 0, s, ids, chs, chi, k, nb, ntiles,
-                                   bk_recs.p, bk_seg.p, rec8 ? bk_tb.p : nullptr, nst, ninc, ws.err.p);
-            const bool direct = !(getenv("RP_BK_DIRECT") && !strcmp(getenv("RP_BK_DIRECT"), "0"));
+                                   bk_recs.p, bk_seg.p, rec8 ? bk_tb.p : nullptr, nst, ninc, ws.err.p, b_lo, b_hi);
+            const bool direct = ranged || !(getenv("RP_BK_DIRECT") && !strcmp(getenv("RP_BK_DIRECT"), "0"));
+            if (ranged) RP_HIP(hipMemsetAsync(g_part.p, 0, sizeof(uint32_t) * (nb + 1), s));  // other ranks' buckets
+            const dim3 fg((b_hi - b_lo + 7) / 8 * 8);
             if (direct)
-                hipLaunchKernelGGL(k_bk_fold<true>, dim3((nb + 7) / 8 * 8), dim3(kBkFT), 0, s, bk_recs.p, bk_seg.p,
-                                   rec8 ? bk_tb.p : nullptr, ntiles, nb, A, bk_res2.p, bk_resj.p, ovf, g_part.p);
+                hipLaunchKernelGGL(k_bk_fold<true>, fg, dim3(kBkFT), 0, s, bk_recs.p, bk_seg.p, rec8 ? bk_tb.p : nullptr,
+                                   ntiles, nb, b_lo, b_hi, A, bk_res2.p, bk_resj.p, ovf, g_part.p);
             else
-                hipLaunchKernelGGL(k_bk_fold<false>, dim3((nb + 7) / 8 * 8), dim3(kBkFT), 0, s, bk_recs.p, bk_seg.p,
-                                   rec8 ? bk_tb.p : nullptr, ntiles, nb, A, bk_res2.p, bk_resj.p, ovf, g_part.p);
+                hipLaunchKernelGGL(k_bk_fold<false>, fg, dim3(kBkFT), 0, s, bk_recs.p, bk_seg.p, rec8 ? bk_tb.p : nullptr,
+                                   ntiles, nb, b_lo, b_hi, A, bk_res2.p, bk_resj.p, ovf, g_part.p);
 #ifdef RP_BK_PROF
             if (getenv("RP_BK_PROF_PRINT")) {
                 unsigned long long v[8];
@@ -1921,6 +1941,35 @@ int rp_members_update_dev(rp_members* h, const uint32_t* d_ids, const uint8_t* d
         RP_REQUIRE(k == 0 || (d_ids && d_status && d_inc), "update_dev: null change buffers");
         m.update_dev(d_ids, d_status, d_inc, k, now_ms, d_applied, d_new_status, d_new_inc, d_n_applied,
                      rp::as_stream(stream));
+    });
+}
+
+int rp_members_update_range_dev(rp_members* h, const uint32_t* d_ids, const uint8_t* d_status, const int64_t* d_inc,
+                                uint32_t k, int64_t now_ms, uint32_t id_lo, uint32_t id_hi, uint8_t* d_applied,
+                                uint8_t* d_new_status, int64_t* d_new_inc, uint32_t* d_n_applied, void* stream) {
+    return guard([&] {
+        rp::Members& m = MB(h);
+        RP_REQUIRE(k == 0 || (d_ids && d_status && d_inc), "update_range_dev: null change buffers");
+        m.update_dev(d_ids, d_status, d_inc, k, now_ms, d_applied, d_new_status, d_new_inc, d_n_applied,
+                     rp::as_stream(stream), true, id_lo, id_hi);
+    });
+}
+
+int rp_members_rows_copy(rp_members* h, void* d_buf, uint32_t id_lo, uint32_t id_hi, int into_table, void* stream) {
+    return guard([&] {
+        rp::Members& m = MB(h);
+        RP_REQUIRE(id_lo <= id_hi && id_hi <= m.cap, "rows_copy: range outside the table's capacity");
+        RP_REQUIRE(id_lo == id_hi || d_buf, "rows_copy: null buffer");
+        if (id_lo == id_hi) return;
+        m.settle_build();  // a deferred string write still reads the rows' snapshot, not the rows
+        const hipStream_t s = rp::as_stream(stream);
+        if (s != m.st) RP_HIP(hipStreamSynchronize(m.st));
+        const uint64_t bytes = sizeof(rp::MRow) * (uint64_t)(id_hi - id_lo);
+        if (into_table)
+            RP_HIP(hipMemcpyAsync(m.rows.p + id_lo, d_buf, bytes, hipMemcpyDeviceToDevice, s));
+        else
+            RP_HIP(hipMemcpyAsync(d_buf, m.rows.p + id_lo, bytes, hipMemcpyDeviceToDevice, s));
+        if (s != m.st && into_table) RP_HIP(hipStreamSynchronize(s));  // the handle's own stream reads them next
     });
 }
 

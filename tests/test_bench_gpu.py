@@ -49,15 +49,19 @@ def test_bench_one_gpu_schema(gpu):
 
 def test_bench_four_ranks_spawned_with_merge(gpu):
     """`bench.py --gpus 4`: four ranks (gloo; they share the box's GPU), the C5-path simulator
-    sharded four ways and the C3 merge as four replicas with batch-strided checksums
-    (DistMembership); rank 0 reports n_gpus = 4 for both."""
-    small = [x for x in SMALL if x != "--no-merge"]
+    sharded four ways, the C3 merge as four replicas with batch-strided checksums
+    (DistMembership) and the fold partitioned by member id (PartMembership); rank 0 reports
+    n_gpus = 4 for each."""
+    small = [x for x in SMALL if x != "--no-merge"] + ["--part-log2", "16"]
     out = _bench(4, small, {"RP_BENCH_BACKEND": "gloo"})
     assert out["n_gpus"] == 4
     assert out["config"]["total_keys"] == 4 * 2 * (1 << 18)
     assert out["sim_c5"]["n_gpus"] == 4 and out["sim_c5"]["converged"]
     assert out["merge"]["n_gpus"] == 4 and out["merge"]["updates_per_s"] > 0
     assert isinstance(out["merge"]["checksum"], int)
+    # the id-partitioned fold (PartMembership) at 2^16 members / updates, four ways
+    fp = out["merge"]["fold_large_partitioned"]
+    assert fp["n_gpus"] == 4 and fp["members"] == 1 << 16 and fp["ms_per_batch"] > 0
     # the exchange's host and device time per round (VERDICT r5 item 4), shown with -rP
     print("sim_c5 exchange:", json.dumps({k: v for k, v in out["sim_c5"].items()
                                           if k.startswith("exchange") or k in ("rounds", "round_ms")}))
