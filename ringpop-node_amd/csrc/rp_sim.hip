@@ -144,6 +144,8 @@ struct SimDev {
     uint32_t* n_tim;
     uint32_t* t_head;  // first pending timer (the ones before it have fired or lapsed)
     uint64_t* vfp;     // [NL] twin fingerprint of each view, kept by block_apply (see twin_mix)
+    int64_t* vdt;      // [NL] each view's checksum-string length minus the base's, kept by block_apply
+                       // (the refresh's order, RP_SIM_CK_SORT; joined views are not updated)
     // per local node
     int64_t* it_idx;
     uint32_t *n_shuf, *ring_count, *max_piggy, *checksum;
@@ -293,6 +295,7 @@ struct Lds {
     uint32_t u[16];
     uint64_t u64;
     unsigned long long fpd;  // block_apply: the batch's twin-fingerprint delta
+    unsigned long long dtd;  // block_apply: the batch's string-length delta (vdt)
     uint32_t win[2][kHashWin][8] __attribute__((aligned(16)));
     uint32_t pad[8];  // the chain's one-chunk lookahead past win[1]
 };
@@ -1158,6 +1161,21 @@ __global__ __launch_bounds__(256) void k_pass1(SimDev S, const uint32_t* __restr
     }
 }
 
+// The compacted views to hash ordered by their string's total shift (refresh_checksums,
+// RP_SIM_CK_SORT), so that a wave's 64 lanes meet their deviated pieces in the same chunk groups
+// (the fixup path runs for the whole wave when any lane needs it). keys[i] from vdt (block_apply)
+// or from the view's pass-1 record.
+__global__ void k_ck_sort_keys(SimDev S, const uint32_t* __restrict__ sel, const uint32_t* __restrict__ nsel,
+                               uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, int from_vdt) {
+    const uint32_t n = *nsel;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t lv = sel[i];
+        const int64_t t = lv >= S.NL ? 0 : from_vdt ? S.vdt[lv] : S.p1[lv].dtot;
+        keys[i] = (uint32_t)(t + 0x80000000ll);
+        vals[i] = lv;
+    }
+}
+
 // Every live local node whose view changed: one node per lane, the wave's 64 chains in lockstep
 // over a shared LDS ring of the base string. A view with more deviated pieces than its list holds,
 // or a wave whose lanes drift further apart than the ring allows, uses the L2 path
@@ -1299,6 +1317,9 @@ __global__ __launch_bounds__(256) void k_ck_lanes(SimDev S, const uint32_t* __re
             const uint32_t qj = q + 20 * j;
             while (qj >= C.pend && C.cur.w < N) C.advance(S, V);
             uint32_t w[5];
+#ifdef RP_CKL_STAT
+            atomicAdd(&g_ckl_stat[(qj + 20 <= C.pos) ? 5 : (C.basedig && qj + 20 <= C.nstart) ? 6 : 7], 1ull);
+#endif
             if (qj + 20 <= C.pos) {
                 R.words((uint32_t)((int32_t)qj - C.delta), w);
             } else if (C.basedig && qj + 20 <= C.nstart) {
@@ -2040,7 +2061,7 @@ __device__ uint32_t block_apply(const SimDev& S, uint32_t lv, const Rec* recs, u
     uint32_t nc = S.n_chg[lv], nt = S.n_tim[lv];
     const bool stopped = S.stopped[lv] != 0;
     ApHash& HT = *reinterpret_cast<ApHash*>(&L.win[0][0][0]);
-    if (threadIdx.x == 0) L.fpd = 0;  // (visible after the loop's first block_scan)
+    if (threadIdx.x == 0) L.fpd = L.dtd = 0;  // (visible after the loop's first block_scan)
     const bool hashed = n >= kApHashMin && nc > 0 && nc <= kApHashMax && S.N < (1u << 30);
     if (hashed) {  // block-uniform
         for (uint32_t q = threadIdx.x; q < kApHash; q += kT) HT.key[q] = kApEmpty;
@@ -2059,6 +2080,7 @@ __device__ uint32_t block_apply(const SimDev& S, uint32_t lv, const Rec* recs, u
         bool applied = false, need_timer = false, need_new = false;
         uint32_t a = 0, slot = 0;
         uint64_t fpd = 0;
+        int64_t dtd = 0;
         uint8_t us = 0;
         int64_t ui = 0;
         Rec r{};
@@ -2096,6 +2118,12 @@ __device__ uint32_t block_apply(const SimDev& S, uint32_t lv, const Rec* recs, u
                 const uint32_t k = S.rank[a];
                 atomicOr(&S.dev[(uint64_t)lv * S.W + (k >> 5)], 1u << (k & 31));
                 fpd = twin_term(k, us, ui, S.inc0[a]) - twin_term(k, cur & ST_MASK, oi, S.inc0[a]);
+                {
+                    const int64_t i0 = S.inc0[a];
+                    dtd = (int64_t)status_len(us) - (int64_t)status_len(cur & ST_MASK);
+                    if (ui != i0) dtd += (int64_t)dec_len(ui) - (int64_t)dec_len(i0);
+                    if (oi != i0) dtd -= (int64_t)dec_len(oi) - (int64_t)dec_len(i0);
+                }
                 need_timer = us == ST_SUSPECT && a != v && !stopped;
                 // the local member becoming `leave` (LocalMemberLeaveEvent, member.js:87-95)
                 if (a == v && us == ST_LEAVE && (cur & ST_MASK) != ST_LEAVE) nleave++;
@@ -2113,6 +2141,7 @@ __device__ uint32_t block_apply(const SimDev& S, uint32_t lv, const Rec* recs, u
         }
         if (applied) {
             if (fpd) atomicAdd(&L.fpd, (unsigned long long)fpd);
+            if (dtd) atomicAdd(&L.dtd, (unsigned long long)dtd);
             if (!need_new) {
                 Change& c = chg[slot - 1];
                 c.cnt = 0;
@@ -2146,6 +2175,7 @@ __device__ uint32_t block_apply(const SimDev& S, uint32_t lv, const Rec* recs, u
         if (leaves) S.stopped[lv] = 1;
         if (tot) {
             S.vfp[lv] += L.fpd;
+            S.vdt[lv] += (int64_t)L.dtd;
             S.dirty[lv] = 1;
             atomicAdd(&S.stats[3], (unsigned long long)tot);
             if (adds || rems) {  // ringChanged -> adjustMaxPiggybackCount (dissemination.js:38-55)
@@ -3283,6 +3313,7 @@ __global__ void k_sim_init(SimDev S) {
         S.n_tim[lv] = 0;
         S.t_head[lv] = 0;
         S.vfp[lv] = 0;
+        S.vdt[lv] = 0;
         S.target[lv] = -1;
         S.nhelp[lv] = 0;
         S.stopped[lv] = 0;
@@ -3396,6 +3427,7 @@ struct Sim {
     DevBuf<uint32_t> ib_off, ib_idx, ikey;         // inbox build
     DevBuf<uint32_t> rsp_n, resp_idx, lresp_idx, d1list;
     DevBuf<uint64_t> boff, rsp_off, ibase, vfp;
+    DevBuf<int64_t> vdt;
     DevBuf<Change> chg;
     DevBuf<Timer> tim;
     DevBuf<Rec> pool;
@@ -3488,10 +3520,14 @@ struct Sim {
         // view is dirty and the machine is issue-bound, stay on k_ck_lanes (pc32 there: 111
         // against 96 ms). Choosing reads the dirty count back (one small copy per round).
         bool use32 = m && !strcmp(m, "pc32");
+        uint32_t nd_host = 0;
+        bool nd_known = false;
         if (!m && !pc && sel) {
             uint32_t nd = 0;
             RP_HIP(hipMemcpyAsync(&nd, nsel, 4, hipMemcpyDeviceToHost, st));
             RP_HIP(hipStreamSynchronize(st));
+            nd_host = nd;
+            nd_known = true;
             static const uint32_t per_cu = [] {  // A/B: RP_SIM_PC32_PER_CU
                 const char* e = getenv("RP_SIM_PC32_PER_CU");
                 return e && *e ? (uint32_t)atoi(e) : 3u;
@@ -3505,10 +3541,32 @@ struct Sim {
         // it saves (153 against 49 ms), so it stays in the kernel (RP_SIM_PASS1=0|1 overrides).
         const bool lanes_path = !use32 && !pc && !(m && !strcmp(m, "pair"));
         const char* p1e = getenv("RP_SIM_PASS1");
-        const bool pre1 = p1e && *p1e ? *p1e != '0' : !lanes_path;
+        // The lane path's order (round 6): the views to hash sorted by their string's length delta
+        // (vdt, kept by block_apply), so that a wave's 64 lanes reach their deviated pieces in the
+        // same chunk groups: the fixup path runs for a whole wave when any lane needs it, and in
+        // C5's peak refreshes list order put a fixup in 10-13 % of wave-groups against 3-4 %
+        // sorted (-DRP_CKL_STAT, profiles/r06/r06ab, r06ac); C5 p95 round 78 -> 68 ms (r06ae).
+        // RP_SIM_CK_SORT: 3 (default) that order, 1 = by this round's shifts from a pass-1
+        // launch (slower: the launch), 0 = list order.
+        const char* cks = getenv("RP_SIM_CK_SORT");
+        const int sort_mode = cks && *cks ? atoi(cks) : 3;
+        const bool sort_sel = lanes_path && sel && sort_mode > 0;
+        const bool pre1 = (sort_sel && sort_mode == 1) || (p1e && *p1e ? *p1e != '0' : !lanes_path);
         if (pre1 && !(m && !strcmp(m, "pair"))) {
             hipLaunchKernelGGL(k_pass1, dim3(grid_for((uint64_t)NL * 64, 256, 4096)), dim3(256), 0, st, d, sel, nsel);
             d.p1_pre = 1;
+        }
+        if (sort_sel) {
+            if (!nd_known) {
+                RP_HIP(hipMemcpyAsync(&nd_host, nsel, 4, hipMemcpyDeviceToHost, st));
+                RP_HIP(hipStreamSynchronize(st));
+            }
+            ck_sort_key.reserve(NL + 1);
+            ck_sort_sel.reserve(NL + 1);
+            hipLaunchKernelGGL(k_ck_sort_keys, dim3(grid_for(NL, 256, 1024)), dim3(256), 0, st, d, sel, nsel,
+                               ck_sort_key.p, ck_sort_sel.p, sort_mode == 3 ? 1 : 0);
+            if (nd_host > 1) radix_sort_pairs(ck_sort_key.p, ck_sort_sel.p, nd_host, 0, 32, st, ws);
+            sel = ck_sort_sel.p;  // (the count stays *nsel)
         }
         if (m && !strcmp(m, "pair"))  // A/B: the lane-pair chains, 32 views per workgroup
             hipLaunchKernelGGL((k_ck_pair<6, 2, 32>), dim3((NL + 31) / 32), dim3(512), 0, st, d, sel, nsel);
@@ -3526,8 +3584,9 @@ struct Sim {
             RP_HIP(hipStreamSynchronize(st));
             RP_HIP(hipMemcpyFromSymbol(v, HIP_SYMBOL(g_ckl_stat), sizeof v));
             if (v[0])
-                fprintf(stderr, "[rp] k_ck_lanes: %llu wave-groups, %.1f %% with a fixup; lane-groups %.2f %% with one\n",
-                        v[0], 100.0 * v[1] / v[0], v[3] ? 100.0 * v[2] / v[3] : 0.0);
+                fprintf(stderr, "[rp] k_ck_lanes: %llu wave-groups, %.1f %% with a fixup; lane-groups %.2f %% with one; "
+                                "redone lane-chunks: clean %llu, status overlay %llu, byte-wise %llu\n",
+                        v[0], 100.0 * v[1] / v[0], v[3] ? 100.0 * v[2] / v[3] : 0.0, v[5], v[6], v[7]);
             memset(v, 0, sizeof v);
             RP_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_ckl_stat), v, sizeof v));
         }
@@ -3540,6 +3599,7 @@ struct Sim {
     DevBuf<uint64_t> twin_fp;
     DevBuf<unsigned long long> twin_key;
     DevBuf<uint32_t> twin_rep, twin_of, twin_cnt, twin_list;
+    DevBuf<uint32_t> ck_sort_key, ck_sort_sel;  // RP_SIM_CK_SORT
     uint32_t twin_cap = 0;
 
     // Outbox of a message kind: sort candidates by destination shard (stable), scan the record
@@ -4092,7 +4152,7 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
         S.st_.reserve(NN + 1); S.inc.reserve(NN + 1); S.order.reserve(NN + 1); S.slot.reserve(NN + 1);
         S.dev.reserve(L1 * W);
         S.chg.reserve(L1 * cap); S.tim.reserve(L1 * cap);
-        S.n_chg.reserve(L1); S.n_tim.reserve(L1); S.t_head.reserve(L1); S.vfp.reserve(L1); S.p1buf.reserve(L1);
+        S.n_chg.reserve(L1); S.n_tim.reserve(L1); S.t_head.reserve(L1); S.vfp.reserve(L1); S.vdt.reserve(L1); S.p1buf.reserve(L1);
         S.it_idx.reserve(L1); S.n_shuf.reserve(L1); S.ring_count.reserve(L1); S.max_piggy.reserve(L1);
         S.checksum.reserve(L1); S.dirty.reserve(L1); S.dead.reserve(n); S.target.reserve(L1); S.ck_snap.reserve(L1);
         S.inc_snap.reserve(L1); S.ping_n.reserve(L1); S.leg_n.reserve(L1);
@@ -4147,7 +4207,7 @@ static void sim_create(uint32_t n, const char* names, const uint32_t* off, const
         d.st = S.st_.p; d.inc = S.inc.p; d.order = S.order.p; d.slot = S.slot.p; d.dev = S.dev.p;
         d.opos = use_opos ? S.opos.p : nullptr;
         d.xcap = (uint32_t)std::max<uint64_t>(2, std::min<uint64_t>(rp::kXCap, env_u64("RP_SIM_D1_XCAP", rp::kXCap)));
-        d.chg = S.chg.p; d.n_chg = S.n_chg.p; d.tim = S.tim.p; d.n_tim = S.n_tim.p; d.t_head = S.t_head.p; d.vfp = S.vfp.p; d.p1 = S.p1buf.p; d.p1_pre = 0;
+        d.chg = S.chg.p; d.n_chg = S.n_chg.p; d.tim = S.tim.p; d.n_tim = S.n_tim.p; d.t_head = S.t_head.p; d.vfp = S.vfp.p; d.vdt = S.vdt.p; d.p1 = S.p1buf.p; d.p1_pre = 0;
         d.it_idx = S.it_idx.p; d.n_shuf = S.n_shuf.p; d.ring_count = S.ring_count.p; d.max_piggy = S.max_piggy.p;
         d.checksum = S.checksum.p; d.dirty = S.dirty.p; d.dead = S.dead.p; d.stopped = S.stopped.p;
         d.sorted = S.nt.sorted.p; d.rank = S.rank.p; d.names = S.nt.d_bytes.p; d.noff = S.nt.d_noff.p;
