@@ -3550,7 +3550,23 @@ struct Sim {
         // launch (slower: the launch), 0 = list order.
         const char* cks = getenv("RP_SIM_CK_SORT");
         const int sort_mode = cks && *cks ? atoi(cks) : 3;
-        const bool sort_sel = lanes_path && sel && sort_mode > 0;
+        const bool is_pair = m && !strcmp(m, "pair");
+        // The same order on the producer/consumer paths when this handle is one shard of several
+        // (each rank of a sharded C5 refreshes on them): C5 in 8 shards on one GPU 147.7 -> 142.6
+        // ms per round; C4 on one GPU (not sharded) 2.41 -> 2.46, so not there (profiles/r06/
+        // r06ah, r06ai). RP_SIM_CK_SORT_PC=0|1 overrides.
+        const char* ckp = getenv("RP_SIM_CK_SORT_PC");
+        const bool pc_on = ckp && *ckp ? *ckp == '1' : G > 1;
+        const bool sort_pc = !lanes_path && !is_pair && sort_mode == 3 && pc_on;
+        if (sort_pc && !sel) {
+            twin_list.reserve(NL + 1);
+            RP_HIP(hipMemsetAsync(twin_list.p + NL, 0, 4, st));
+            hipLaunchKernelGGL(k_dirty_list, dim3(grid_for(NL, 256, 1024)), dim3(256), 0, st, d, twin_list.p,
+                               twin_list.p + NL);
+            sel = twin_list.p;
+            nsel = twin_list.p + NL;
+        }
+        const bool sort_sel = (lanes_path || sort_pc) && sel && sort_mode > 0;
         const bool pre1 = (sort_sel && sort_mode == 1) || (p1e && *p1e ? *p1e != '0' : !lanes_path);
         if (pre1 && !(m && !strcmp(m, "pair"))) {
             hipLaunchKernelGGL(k_pass1, dim3(grid_for((uint64_t)NL * 64, 256, 4096)), dim3(256), 0, st, d, sel, nsel);

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--n", type=int, default=100_000)
     ap.add_argument("--label", default="default")
     ap.add_argument("--max-rounds", type=int, default=120)
+    ap.add_argument("--shards", type=int, default=1, help="ShardedGossipSim in this process (one GPU)")
     args = ap.parse_args()
     import torch
     rpa = _load("ringpop_node_amd", os.path.join(REPO, "ringpop-node_amd", "__init__.py"))
@@ -41,7 +42,10 @@ def main():
     names = [S.c2_addr(i) for i in range(n)]
     inc0 = S.c3_members(n)[2]
     dead = S.kill_set(n, k, 11)
-    sim = rpa.GossipSim(names, inc0, dead, seed=11, suspicion_rounds=25)
+    if args.shards > 1:
+        sim = rpa.ShardedGossipSim(names, inc0, dead, args.shards, seed=11, suspicion_rounds=25)
+    else:
+        sim = rpa.GossipSim(names, inc0, dead, seed=11, suspicion_rounds=25)
     torch.cuda.synchronize()
     rows = []
     prev = sim.counters()["views_hashed"]
@@ -58,7 +62,7 @@ def main():
     cnt = sim.counters()
     sim.close()
     ms = np.array([x["ms"] for x in rows])
-    out = {"label": args.label, "n": n, "rounds": len(rows), "base_len": cnt["base_len"],
+    out = {"label": args.label, "n": n, "shards": args.shards, "rounds": len(rows), "base_len": cnt["base_len"],
            "chunks_per_chain": cnt["base_len"] // 20, "p50": float(np.percentile(ms, 50)),
            "p95": float(np.percentile(ms, 95)), "worst": int(ms.argmax()), "per_round": rows}
     print(json.dumps(out), flush=True)
