@@ -827,11 +827,17 @@ class PartMembership(Membership):
         self._group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        nb = -(-max(int(capacity), 1) // self.BUCKET)
-        self.per_ids = -(-nb // self.world) * self.BUCKET
-        self.id_lo = min(self.rank * self.per_ids, nb * self.BUCKET)
-        self.id_hi = 0xFFFFF000 if self.rank == self.world - 1 else min((self.rank + 1) * self.per_ids,
-                                                                          nb * self.BUCKET)
+        self.per_ids, self.id_lo, self.id_hi = self.partition(capacity, self.world, self.rank)
+
+    @classmethod
+    def partition(cls, capacity, world, rank):
+        """(ids per rank, id_lo, id_hi) of rank's run: equal runs of whole buckets of the capacity,
+        the last rank's run open-ended (0xFFFFF000, a bucket multiple past any table)."""
+        nb = -(-max(int(capacity), 1) // cls.BUCKET)
+        per = -(-nb // world) * cls.BUCKET
+        lo = min(rank * per, nb * cls.BUCKET)
+        hi = 0xFFFFF000 if rank == world - 1 else min((rank + 1) * per, nb * cls.BUCKET)
+        return per, lo, hi
 
     def update_dev(self, d_ids, d_status, d_inc, k, now_ms, d_applied=None, d_new_status=None, d_new_inc=None,
                    d_n_applied=None, stream=None):

@@ -112,3 +112,18 @@ def test_message_exchange_on_a_subgroup_with_side_counts():
     for p in ps:
         p.join(timeout=60)
     assert res == {0: True, 1: True, 2: True}
+
+
+@pytest.mark.parametrize("capacity,world", [(1, 1), (4096, 2), (4 * 4096 + 1234, 2), (4 * 4096 + 1234, 3),
+                                            (1 << 22, 8), (100_000, 8), (5, 4)])
+def test_part_membership_partition_covers_ids(rpa, capacity, world):
+    """PartMembership's id runs (host logic, no device): whole 4,096-id buckets, in rank order,
+    disjoint, covering every id of the table, the last one open-ended; what
+    rp_members_update_range_dev requires of a range."""
+    B = rpa.PartMembership.BUCKET
+    runs = [rpa.PartMembership.partition(capacity, world, r) for r in range(world)]
+    assert runs[0][1] == 0 and runs[-1][2] >= capacity
+    for (_, lo, hi), (_, lo2, _) in zip(runs, runs[1:]):
+        assert hi == lo2 and lo <= hi
+    for _, lo, hi in runs:
+        assert lo % B == 0 and hi % B == 0
