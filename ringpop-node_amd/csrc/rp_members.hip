@@ -1478,6 +1478,11 @@ struct Members {
         const uint32_t nb = (cap + kBk - 1) / kBk;
         const uint32_t b_lo = ranged ? std::min(nb, id_lo / kBk) : 0u;
         const uint32_t b_hi = ranged ? (uint32_t)std::min<uint64_t>(nb, ((uint64_t)id_hi + kBk - 1) / kBk) : nb;
+        if (ranged && b_lo >= b_hi) {  // a range past the table (a rank with no ids yet): nothing to fold
+            RP_HIP(hipMemsetAsync(napplied.p, 0, sizeof(uint32_t), s));
+            if (n_applied_out) RP_HIP(hipMemsetAsync(n_applied_out, 0, sizeof(uint32_t), s));
+            return;
+        }
         if (ranged || use_bucket_fold(k, nb)) {
             const uint32_t ntiles = (k + kBkTile - 1) / kBkTile;
             bk_seg.reserve((uint64_t)((nb + 15) / 16) * 16 * ntiles);

@@ -149,16 +149,17 @@ def _reference_part(gpu, n, k, nbatch):
     return cks, np.concatenate(apps), ex, st, inc
 
 
-@pytest.mark.parametrize("G", [2, 3])
-def test_part_membership_matches_single_gpu(gpu, tmp_path, G):
+@pytest.mark.parametrize("G,n", [(2, 4 * 4096 + 1234), (3, 4 * 4096 + 1234), (3, 6000)])
+def test_part_membership_matches_single_gpu(gpu, tmp_path, G, n):
     """The merge partitioned by member id (PartMembership): every rank folds the
     changes of its own ids (whole 4,096-id buckets) from the same batch stream, and the rows are
     all-gathered for the checksum after every batch. Per-batch checksums, every change's applied
     flag (from the rank owning its id; no rank writes another's) and the final table equal one
-    single-GPU Membership's. The table spans 5 buckets, so ranks own 3+2 or 2+2+1 of them; the
-    last batch sends 300 changes each to an address of the first and of the last rank (past the
-    bucket fold's LDS list: the overflow fold)."""
-    n, k, nbatch = 4 * 4096 + 1234, 9000, 5
+    single-GPU Membership's. A table of 5 buckets gives ranks 3+2 or 2+2+1 of them; one of 2
+    buckets over 3 ranks leaves the last rank none (its updates fold nothing). The last batch sends
+    300 changes each to an address of the first and of the last rank (past the bucket fold's LDS
+    list: the overflow fold)."""
+    k, nbatch = 9000, 5
     out = str(tmp_path / "part.npz")
     port = _free_port()
     worker = os.path.join(REPO, "tests", "workers", "part_merge_worker.py")
