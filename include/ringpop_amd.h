@@ -190,7 +190,8 @@ int rp_members_update_dev(rp_members *m, const uint32_t *d_ids, const uint8_t *d
  * changes are left as they were, *d_n_applied counts this range's applied changes, and rows
  * outside the range are not touched. No checksum is computed: a caller holding the table in
  * ranges brings the rows together (rp_members_rows_copy) and calls rp_members_compute_checksum.
- * Always the bucket path (no damp scoring, at most 8M ids). Stream-ordered, no host sync. */
+ * Always the bucket path (no damp scoring, at most 8M ids); a range past the table folds nothing
+ * (*d_n_applied = 0). Stream-ordered, no host sync. */
 int rp_members_update_range_dev(rp_members *m, const uint32_t *d_ids, const uint8_t *d_status,
                                 const int64_t *d_inc, uint32_t k, int64_t now_ms, uint32_t id_lo, uint32_t id_hi,
                                 uint8_t *d_applied, uint8_t *d_new_status, int64_t *d_new_inc,
