@@ -1131,6 +1131,271 @@ __global__ __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(4)))
     }
 }
 
+// ---- The wave-specialised lean kernel (round 6, A/B: RP_LOOKUP_WS). The lean kernel's waves run
+// every phase in turn (key stream, hash, index trip, window trip, stores), and s_waitcnt vmcnt
+// retires in issue order, so a wave cannot keep its next keys in flight behind its lookups. Here
+// the NP producer waves of a workgroup only stream keys (16-B non-temporal loads, transposed
+// through an 18-KB LDS tile per producer, the next tile's loads in flight) and hash them into an LDS ring (slots of 512 hashes),
+// and the NC consumer waves only take the index and window trips and store the rows (a 12-B
+// buffer store per key: 768 contiguous bytes per wave instruction; second-window keys' rows
+// from the lane that finishes them). Producer p serves consumers p, p + NP, ...; the ring's
+// counters are LDS words (prod[c]: wave-tiles filled, cons[c]: wave-tiles read). Every wait is
+// bounded (kWsSpin polls): past it the wave stops waiting and sets *err, so the grid always
+// drains (the launch's results are then wrong; the launcher reports it under RP_LOOKUP_DEBUG).
+// Deferred keys go to per-wave-tile lists (k_lookupn_fix_tiles with TK 512).
+constexpr int kWsSlots = 2;
+constexpr uint32_t kWsSpin = 1u << 22;
+typedef uint32_t u32x3v __attribute__((ext_vector_type(3)));
+
+// ABL (diagnostics, RP_LOOKUP_WS_ABL; results wrong, times only): 1 = producers load no keys (the
+// hashes are made from the key index), 2 = consumers take no trips (the row is the hash).
+template <int NP, int NC, int ABL = 0>
+__global__ __launch_bounds__((NP + NC) * 64) __attribute__((amdgpu_waves_per_eu(4))) void k_lookupn_ws(const uint8_t* __restrict__ keys, uint64_t nwt,
+                                                               CompactView cv, uint32_t* __restrict__ out,
+                                                               uint32_t out_bytes, uint8_t* __restrict__ counts,
+                                                               uint32_t* __restrict__ slow_list,
+                                                               uint32_t* __restrict__ slow_cnt,
+                                                               uint32_t* __restrict__ err) {
+    constexpr int NEED = 3, KPL = 8, LEN = 36, W4 = LEN / 4;
+    constexpr int TK = 64 * KPL;         // keys a wave-tile
+    constexpr int V4 = TK * W4 / 4;      // its 16-B pieces
+    constexpr int PER = V4 / 64;         // per producer lane
+    constexpr uint32_t SPAN = 5 - NEED;
+    constexpr uint32_t AG = 64;
+    static_assert(V4 % 64 == 0, "wave-tile shape");
+    __shared__ __attribute__((aligned(16))) uint32_t stg[NP][V4 * 4];
+    __shared__ uint32_t ring[NC][kWsSlots][TK];
+    __shared__ uint32_t ag[NC][3][AG];
+    __shared__ uint32_t prod[NC], cons[NC], nsl[NC];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid < NC) {
+        prod[tid] = 0;
+        cons[tid] = 0;
+    }
+    __syncthreads();
+    const uint64_t nwg = (nwt + NC - 1) / NC;  // workgroup tiles: NC wave-tiles each
+    // until *p >= target (wave-uniform: one LDS word read by the whole wave)
+    auto wait_ge = [&](uint32_t* p, uint32_t target) {
+        for (uint32_t n = 0;; n++) {
+            const uint32_t v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+            if (v >= target) break;
+            if (n == kWsSpin) {
+                if (lane == 0) atomicOr(err, 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            asm volatile("" ::: "memory");
+        }
+        asm volatile("" ::: "memory");
+    };
+    if (wv < NP) {
+        // producer: item j is consumer c = wv + (j % cnt) NP's wave-tile of workgroup tile
+        // blockIdx.x + (j / cnt) gridDim.x (ring sequence j / cnt). The whole wave-tile's keys go
+        // to LDS at once, and the next item's 18 loads a lane are issued before this one is
+        // hashed, so the key stream stays in flight behind the hashing and the ring waits.
+        const int cnt = (NC - wv + NP - 1) / NP;
+        auto item_wt = [&](uint32_t j) -> uint64_t {
+            const uint64_t T = blockIdx.x + (uint64_t)(j / cnt) * gridDim.x;
+            const uint64_t wt = T * NC + wv + (j % cnt) * NP;
+            return T < nwg && wt < nwt ? wt : ~0ull;
+        };
+        u32x4 pre[PER];
+        auto issue = [&](uint64_t wt) {
+            const u32x4* s4 = reinterpret_cast<const u32x4*>(keys + wt * (uint64_t)(TK * LEN));
+#pragma unroll
+            for (int q = 0; q < PER; q++) pre[q] = __builtin_nontemporal_load(s4 + lane + 64 * q);
+        };
+        uint64_t wt = item_wt(0);
+        if (ABL != 1 && wt != ~0ull) issue(wt);
+        for (uint32_t j = 0; wt != ~0ull; j++) {
+            const uint64_t wn = item_wt(j + 1);
+            uint32_t h[KPL];
+            if constexpr (ABL == 1) {
+#pragma unroll
+                for (int k = 0; k < KPL; k++) h[k] = (uint32_t)(wt * TK + lane + 64 * k) * 0x9E3779B1u;
+            } else {
+                u32x4* st4 = reinterpret_cast<u32x4*>(stg[wv]);
+#pragma unroll
+                for (int q = 0; q < PER; q++) st4[lane + 64 * q] = pre[q];
+                __builtin_amdgcn_wave_barrier();
+                if (wn != ~0ull) issue(wn);
+#pragma unroll
+                for (int k = 0; k < KPL; k++) {
+                    uint32_t w[W4];
+#pragma unroll
+                    for (int x = 0; x < W4; x++) w[x] = stg[wv][(lane + 64 * k) * W4 + x];
+                    h[k] = fh::hash32_words<LEN>(w);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            const int c = wv + (int)(j % cnt) * NP;
+            const uint32_t i = j / cnt;
+            wait_ge(&cons[c], i + 1 > (uint32_t)kWsSlots ? i + 1 - kWsSlots : 0u);
+            uint32_t* slot = ring[c][i % kWsSlots];
+#pragma unroll
+            for (int k = 0; k < KPL; k++) slot[lane + 64 * k] = h[k];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane == 0) __hip_atomic_store(&prod[c], i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            wt = wn;
+        }
+        return;
+    }
+    // consumer c: its wave-tile of every workgroup tile
+    const int c = wv - NP;
+    const uint32_t omask = (1u << cv.ob) - 1u, obit = 1u << cv.ob;
+    const uint32_t bsh = 32u - cv.cb;
+    const uint32_t rmask = (1u << bsh) - 1u;
+    const __amdgpu_buffer_rsrc_t ent_r =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(cv.ent), 0, (int)cv.ent_bytes, 0x00020000);
+    const bool hinted = cv.idxh != nullptr;
+    const __amdgpu_buffer_rsrc_t idx_r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint32_t*>(hinted ? cv.idxh : cv.idx), 0, (int)cv.idx_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t out_r = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)out_bytes, 0x00020000);
+    auto load16 = [&](uint32_t pos) {
+        return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ent_r, (int)(3u * pos), 0, 0));
+    };
+    auto ent5v = [&](const u32x4 v, uint32_t (&e)[5]) {
+        e[0] = v.x & 0xFFFFFFu;
+        e[1] = (v.x >> 24) | ((v.y & 0xFFFFu) << 8);
+        e[2] = (v.y >> 16) | ((v.z & 0xFFu) << 16);
+        e[3] = v.z >> 8;
+        e[4] = v.w & 0xFFFFFFu;
+    };
+    auto wstart = [&](uint32_t hk, uint32_t bck, uint32_t hint) -> uint32_t {
+        const int fl = (int)((((hk << cv.cb) >> 24) * bck) >> 8) - 2 + (int)hint;
+        return (cv.wpred && bck <= 10u && fl > 0) ? (uint32_t)fl : 0u;
+    };
+    auto store_row = [&](uint64_t key, uint32_t a, uint32_t b, uint32_t d) {
+        const u32x3v v = {a, b, d};
+        __builtin_amdgcn_raw_buffer_store_b96(v, out_r, (int)(key * 12u), 0, 2);
+    };
+    uint32_t i = 0;
+    for (uint64_t T = blockIdx.x; T < nwg; T += gridDim.x, i++) {
+        const uint64_t wt = T * NC + c;
+        if (wt >= nwt) break;
+        const uint64_t base = wt * TK;
+        wait_ge(&prod[c], i + 1);
+        uint32_t h[KPL];
+        const uint32_t* slot = ring[c][i % kWsSlots];
+#pragma unroll
+        for (int k = 0; k < KPL; k++) h[k] = slot[lane + 64 * k];
+        if (lane == 0) nsl[c] = 0;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(&cons[c], i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if constexpr (ABL == 2) {
+#pragma unroll
+            for (int k = 0; k < KPL; k++) store_row(base + lane + 64 * k, h[k], h[k] + 1u, h[k] + 2u);
+            if (lane == 0) slow_cnt[wt] = 0;
+            continue;
+        }
+        u32x2 rec[KPL];
+#pragma unroll
+        for (int k = 0; k < KPL; k++)
+            rec[k] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(idx_r, (int)((h[k] >> (bsh + 3u)) * 8u), 0, 0));
+        uint32_t lo[KPL], bc[KPL], ws[KPL];
+        u32x4 win[KPL];
+#pragma unroll
+        for (int k = 0; k < KPL; k++) {
+            const uint32_t s4 = ((h[k] >> bsh) & 7u) * 4u;
+            const uint32_t below = rec[k].y & ((1u << s4) - 1u);
+            uint32_t b0 = rec[k].x, hint = 1u;
+            if (hinted) {
+                const uint32_t g = h[k] >> (bsh + 3u);
+                b0 = (uint32_t)(((uint64_t)g * cv.M) >> (cv.cb - 3u)) + (uint32_t)((int32_t)(rec[k].x << 18) >> 18);
+                hint = (rec[k].x >> (14u + (s4 >> 1))) & 3u;
+            }
+            lo[k] = b0 + __builtin_amdgcn_sad_u8(below & 0x0F0F0F0Fu, 0u, __builtin_amdgcn_sad_u8((below >> 4) & 0x0F0F0F0Fu, 0u, 0u));
+            bc[k] = (rec[k].y >> s4) & 15u;
+            ws[k] = wstart(h[k], bc[k], hint);
+            win[k] = load16(lo[k] + ws[k]);
+        }
+        uint32_t nag = 0;
+#pragma unroll
+        for (int k = 0; k < KPL; k++) {
+            uint32_t e[5];
+            ent5v(win[k], e);
+            const uint32_t K = ((h[k] & rmask) >> cv.fsh) << cv.ob;
+            const uint32_t w = ws[k];
+            uint32_t lt = 0;
+            bool tie = false;
+#pragma unroll
+            for (int j = 0; j < 5; j++) {
+                const bool inb = (uint32_t)j + w < bc[k];
+                lt += (inb && e[j] < K);
+                tie |= (inb && e[j] - K < obit);
+            }
+            uint32_t r[NEED];
+#pragma unroll
+            for (int q = 0; q < NEED; q++) {
+                uint32_t v = e[q] & omask;
+#pragma unroll
+                for (uint32_t d = 1; d <= SPAN; d++) v = lt == d ? (e[q + d] & omask) : v;
+                r[q] = v;
+            }
+            const bool dup = r[0] == r[1] || r[0] == r[2] || r[1] == r[2];
+            const uint32_t kk = lane + 64 * k;
+            bool slow = (tie && !cv.exact) | (lo[k] + 20u > cv.M);
+            const bool under = w > 0u && lt == 0u;
+            const bool again = !slow && (lt > SPAN || dup || under);
+            const uint64_t m = __ballot(again);
+            const uint32_t pos = nag + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            nag += (uint32_t)__popcll(m);
+            if (again) {
+                if (pos < AG) {
+                    const uint32_t b0 = under ? (w > 2u ? w - 2u : 0u) : w + 5u;
+                    const bool search = under || (lt == 5u && bc[k] > w + 5u);
+                    ag[c][0][pos] = lo[k] + (search ? b0 : w + lt);
+                    ag[c][1][pos] = K;
+                    ag[c][2][pos] = kk | (bc[k] << 12) | ((uint32_t)search << 16) | ((search ? b0 : 0u) << 17) |
+                                    ((uint32_t)(under && b0 > 0u) << 21);
+                } else {
+                    slow = true;
+                }
+            }
+            if (!again || pos >= AG) {
+                store_row(base + kk, r[0], r[1], r[2]);
+                if (counts) counts[base + kk] = (uint8_t)NEED;
+            }
+            if (slow) {
+                const uint32_t sp = atomicAdd(&nsl[c], 1u);
+                if (sp < kSlowPerTile) slow_list[wt * kSlowPerTile + sp] = kk;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        for (uint32_t j = lane; j < (nag < AG ? nag : AG); j += 64) {
+            const u32x4 wn = load16(ag[c][0][j]);
+            const uint32_t K = ag[c][1][j], w2 = ag[c][2][j];
+            const uint32_t kk = w2 & 0xFFFu, bck = (w2 >> 12) & 15u, b0 = (w2 >> 17) & 15u;
+            uint32_t e2[5];
+            ent5v(wn, e2);
+            uint32_t off = 0;
+            bool slow = false;
+            if ((w2 >> 16) & 1u) {
+                bool tie = false;
+#pragma unroll
+                for (int j2 = 0; j2 < 5; j2++) {
+                    const bool inb = (uint32_t)j2 + b0 < bck;
+                    off += (inb && e2[j2] < K);
+                    tie |= (inb && e2[j2] - K < obit);
+                }
+                slow = (tie && !cv.exact) | (off == 5u && bck > b0 + 5u) | (((w2 >> 21) & 1u) && off == 0u);
+            }
+            uint32_t res[4] = {NIL, NIL, NIL, NIL};
+            const uint32_t rc = dedupe5(e2, off, omask, NEED, res);
+            slow |= rc < (uint32_t)NEED;
+            if (slow) {
+                const uint32_t sp = atomicAdd(&nsl[c], 1u);
+                if (sp < kSlowPerTile) slow_list[wt * kSlowPerTile + sp] = kk;
+            }
+            store_row(base + kk, res[0], res[1], res[2]);
+            if (counts) counts[base + kk] = (uint8_t)rc;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) slow_cnt[wt] = __hip_atomic_load(&nsl[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+
 // ---- The LDS-index kernel (round 6). The lean kernel above takes two dependent L2 trips per key
 // (the index record, then the window); its ablations price the index trip at 0.21 of 0.93 ms, and
 // the access-pattern microbenchmark (profiles/r01c/ub_access_patterns.txt) puts one random 16-B
@@ -2599,6 +2864,78 @@ static void launch_lookupn(Ring& r, const uint8_t* keys, const uint64_t* off, ui
         RP_REQUIRE(n < (1ull << 32), "lookupn: at most 2^32-1 keys per call");
         if (r.chint_pending && need == 3) ring_build_hint(r);
         const CompactView cv = r.cview();
+        // the wave-specialised kernel (round 6, A/B): RP_LOOKUP_WS = "NP:NC" producer and consumer
+        // waves a workgroup (1:3, 2:6, 1:7, 4:12, 2:2, 1:15, 2:14; "1" = 1:3)
+        const char* ws_env = getenv("RP_LOOKUP_WS");
+        if (ws_env && strcmp(ws_env, "0") && need == 3 && !getenv("RP_LOOKUP_KPL") && cv.ablate == 0 &&
+            n >= 512ull * 4 && n * 12ull < (1ull << 31)) {
+            int wnp = 1, wnc = 3;
+            if (strchr(ws_env, ':') && sscanf(ws_env, "%d:%d", &wnp, &wnc) != 2) wnp = 0;
+            constexpr uint64_t TK = 512;
+            const uint64_t nwt = n / TK, done = nwt * TK;
+            r.slow.reserve(nwt * kSlowPerTile + 1);
+            r.nslow.reserve(nwt + 2);
+            uint32_t* err = r.nslow.p + nwt + 1;
+            RP_HIP(hipMemsetAsync(err, 0, 4, st));
+            static const int cus = [] {
+                int dev = 0, c = 0;
+                (void)hipGetDevice(&dev);
+                (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+                return c > 0 ? c : 256;
+            }();
+            const uint64_t nwg = (nwt + (uint64_t)wnc - 1) / (uint64_t)(wnc > 0 ? wnc : 1);
+            // workgroups a CU: 16 waves (<= 128 VGPRs), and the LDS (an 18-KB key tile a producer,
+            // kWsSlots 2-KB ring slots and a 768-B list a consumer)
+            const uint64_t lds_wg = (uint64_t)wnp * 18432 + (uint64_t)wnc * (kWsSlots * 2048 + 780);
+            const uint64_t per_cu = wnp + wnc > 0 ? std::max<uint64_t>(1, std::min<uint64_t>(16 / (uint64_t)(wnp + wnc), 163840 / lds_wg)) : 1;
+            const unsigned g = (unsigned)std::min<uint64_t>(nwg, env_pos("RP_LOOKUP_WS_GRID", (uint64_t)cus * per_cu));
+            const int wabl = getenv("RP_LOOKUP_WS_ABL") ? atoi(getenv("RP_LOOKUP_WS_ABL")) : 0;  // diagnostics
+#define RP_WSK(P, C) \
+    hipLaunchKernelGGL((k_lookupn_ws<P, C>), dim3(g), dim3((P + C) * 64), 0, st, keys, nwt, cv, out, (uint32_t)(n * 12ull), counts, r.slow.p, r.nslow.p, err)
+            if (wnp == 1 && wnc == 3)
+                RP_WSK(1, 3);
+            else if (wnp == 2 && wnc == 6)
+                RP_WSK(2, 6);
+            else if (wnp == 1 && wnc == 7)
+                RP_WSK(1, 7);
+            else if (wnp == 4 && wnc == 12 && wabl == 1)
+                hipLaunchKernelGGL((k_lookupn_ws<4, 12, 1>), dim3(g), dim3(16 * 64), 0, st, keys, nwt, cv, out, (uint32_t)(n * 12ull), counts, r.slow.p, r.nslow.p, err);
+            else if (wnp == 4 && wnc == 12 && wabl == 2)
+                hipLaunchKernelGGL((k_lookupn_ws<4, 12, 2>), dim3(g), dim3(16 * 64), 0, st, keys, nwt, cv, out, (uint32_t)(n * 12ull), counts, r.slow.p, r.nslow.p, err);
+            else if (wnp == 4 && wnc == 12)
+                RP_WSK(4, 12);
+            else if (wnp == 2 && wnc == 2)
+                RP_WSK(2, 2);
+            else if (wnp == 1 && wnc == 15)
+                RP_WSK(1, 15);
+            else if (wnp == 2 && wnc == 14)
+                RP_WSK(2, 14);
+            else
+                RP_REQUIRE(false, "RP_LOOKUP_WS: one of 1:3, 2:6, 1:7, 4:12, 2:2, 1:15, 2:14");
+#undef RP_WSK
+            RP_HIP(hipGetLastError());
+            const CompactFixView fv{r.tok.p, r.own.p, r.cidx.p, r.view(), r.M, r.ccb};
+            const uint64_t fthreads = nwt * kSlowPerTile;
+            hipLaunchKernelGGL((k_lookupn_fix_tiles<CompactFixView>), dim3((unsigned)((fthreads + 255) / 256)), dim3(256),
+                               0, st, keys, fv, np, W, out, counts, r.slow.p, r.nslow.p, nwt, (uint32_t)TK);
+            RP_HIP(hipGetLastError());
+            if (getenv_flag("RP_LOOKUP_DEBUG")) {
+                std::vector<uint32_t> c(nwt + 2);
+                RP_HIP(hipMemcpyAsync(c.data(), r.nslow.p, 4 * (nwt + 2), hipMemcpyDeviceToHost, st));
+                RP_HIP(hipStreamSynchronize(st));
+                uint64_t tot = 0, over = 0;
+                for (uint64_t t = 0; t < nwt; t++) {
+                    tot += c[t];
+                    over += c[t] > kSlowPerTile;
+                }
+                fprintf(stderr, "[rp] ws lookupN %d:%d: %llu keys, %llu deferred, %llu overflowed wave-tiles, err %u\n", wnp,
+                        wnc, (unsigned long long)done, (unsigned long long)tot, (unsigned long long)over, c[nwt + 1]);
+            }
+            if (done < n)
+                launch_lookupn_view(r.view(), keys + done * 36, nullptr, 36, nullptr, n - done, np, W, out + done * W,
+                                    counts ? counts + done : nullptr, st);
+            return;
+        }
         // lookupN(3) (the C2 bench): 8 keys per lane, staged through LDS in four slices (0.925-0.926
         // against 0.962-0.970 ms for 4 keys per lane; two slices 0.926-0.932; 6 keys per lane
         // 0.956-0.959; profiles/r02/ab_lookup_lean.json); the other widths 4 keys per lane.

@@ -152,13 +152,25 @@ LAYOUTS = {
     "lds": {"RP_LOOKUP_LDS": "1"},
     "lds-grid3": {"RP_LOOKUP_LDS": "1", "RP_LOOKUP_LDS_GRID": "3"},
     "lean": {"RP_LOOKUP_LDS": "0"},
+    # the wave-specialised kernel (round 6, k_lookupn_ws): producer waves stream and hash the keys
+    # into an LDS ring, consumer waves take the index and window trips; NP:NC waves a workgroup,
+    # "ws-grid1": one workgroup through every wave-tile (the ring's slots reused many times)
+    "ws": {"RP_LOOKUP_WS": "1:3"},
+    "ws-2-6": {"RP_LOOKUP_WS": "2:6"},
+    "ws-1-7": {"RP_LOOKUP_WS": "1:7"},
+    "ws-4-12": {"RP_LOOKUP_WS": "4:12"},
+    "ws-2-2": {"RP_LOOKUP_WS": "2:2"},
+    "ws-1-15": {"RP_LOOKUP_WS": "1:15"},
+    "ws-2-14": {"RP_LOOKUP_WS": "2:14"},
+    "ws-grid1": {"RP_LOOKUP_WS": "1:3", "RP_LOOKUP_WS_GRID": "1"},
 }
 
 
 def set_layout(monkeypatch, layout):
     for k in ("RP_RING_WIDE", "RP_RING_NOWINDOW", "RP_RING_LAYOUT", "RP_LOOKUP_KPL", "RP_LOOKUP_LEAN", "RP_LOOKUP_HALF",
               "RP_LOOKUP_GRID", "RP_LOOKUP_FUSEFIX", "RP_LOOKUP_WPRED", "RP_LOOKUP_STG", "RP_LOOKUP_LH",
-              "RP_LOOKUP_STGHS", "RP_LOOKUP_HINT", "RP_LOOKUP_LDS", "RP_LOOKUP_LDS_GRID"):
+              "RP_LOOKUP_STGHS", "RP_LOOKUP_HINT", "RP_LOOKUP_LDS", "RP_LOOKUP_LDS_GRID", "RP_LOOKUP_WS",
+              "RP_LOOKUP_WS_GRID"):
         monkeypatch.delenv(k, raising=False)
     if layout != "compact" and not layout.startswith("lds"):  # every other layout names a lean / older kernel
         monkeypatch.setenv("RP_LOOKUP_LDS", "0")
@@ -527,7 +539,7 @@ def _c2_oracle_owners(orc, oracle, n):
 
 
 @pytest.mark.parametrize("layout", ["compact", "round1", "lean-kpl4", "half-kpl8", "fusefix", "wpred0", "stg2", "stg1", "hint0",
-                                    "lds", "lean"])
+                                    "lds", "lean", "ws", "ws-2-6", "ws-1-7", "ws-4-12", "ws-2-2", "ws-1-15", "ws-2-14"])
 def test_c2_full_size_properties(gpu, orc, layout, monkeypatch):
     set_layout(monkeypatch, layout)
     # C2: 10k servers x 100 points (~1M tokens); 2^24 keys on device; size-independent
@@ -578,7 +590,7 @@ def test_edge_cases(gpu):
 
 @pytest.mark.parametrize("layout", ["compact", "compact-kpl1", "compact-kpl3", "compact-kpl8", "round1",
                                     "round1-kpl1", "half", "half-kpl2", "half-kpl8", "quarter-kpl8", "lean-kpl4", "window",
-                                    "fusefix", "wpred0", "stg2", "stg2-hs4"])
+                                    "fusefix", "wpred0", "stg2", "stg2-hs4", "ws", "ws-4-12", "ws-grid1"])
 @pytest.mark.parametrize("nserv,R", [(1, 100), (2, 2000), (3, 700), (5, 5), (40, 1), (64, 3)])
 def test_window_kernel_slow_paths_vs_oracle(gpu, orc, nserv, R, layout, monkeypatch):
     """Rings that force the window kernels' exact fallbacks: long buckets, runs of one owner,

@@ -82,10 +82,22 @@ def main():
         "lds-abl3/lookupN3": ({"RP_LOOKUP_LDS": "1", "RP_LOOKUP_LDS_ABL": "3"}, 3),
         "lds-abl4/lookupN3": ({"RP_LOOKUP_LDS": "1", "RP_LOOKUP_LDS_ABL": "4"}, 3),
         "lds-abl7/lookupN3": ({"RP_LOOKUP_LDS": "1", "RP_LOOKUP_LDS_ABL": "7"}, 3),
+        # round 6: the wave-specialised kernel (NP producer : NC consumer waves a workgroup)
+        "ws13/lookupN3": ({"RP_LOOKUP_WS": "1:3"}, 3),
+        "ws26/lookupN3": ({"RP_LOOKUP_WS": "2:6"}, 3),
+        "ws17/lookupN3": ({"RP_LOOKUP_WS": "1:7"}, 3),
+        "ws412/lookupN3": ({"RP_LOOKUP_WS": "4:12"}, 3),
+        "ws22/lookupN3": ({"RP_LOOKUP_WS": "2:2"}, 3),
+        "ws115/lookupN3": ({"RP_LOOKUP_WS": "1:15"}, 3),
+        "ws214/lookupN3": ({"RP_LOOKUP_WS": "2:14"}, 3),
+        "ws412-abl1/lookupN3": ({"RP_LOOKUP_WS": "4:12", "RP_LOOKUP_WS_ABL": "1"}, 3),
+        "ws412-abl2/lookupN3": ({"RP_LOOKUP_WS": "4:12", "RP_LOOKUP_WS_ABL": "2"}, 3),
+        "ws13-g512/lookupN3": ({"RP_LOOKUP_WS": "1:3", "RP_LOOKUP_WS_GRID": "512"}, 3),
+        "ws13-g2048/lookupN3": ({"RP_LOOKUP_WS": "1:3", "RP_LOOKUP_WS_GRID": "2048"}, 3),
     }
     if a.only:
         variants = {k: v for k, v in variants.items() if k in a.only.split(",")}
-    knobs = ("RP_LOOKUP_HALF", "RP_LOOKUP_LEAN", "RP_LOOKUP_KPL", "RP_RING_LAYOUT", "RP_LOOKUP_ABLATE", "RP_RING_WIDE", "RP_LOOKUP_GRID", "RP_LOOKUP_OCC", "RP_LOOKUP_STG", "RP_LOOKUP_LH", "RP_LOOKUP_STGHS", "RP_LOOKUP_LDS", "RP_LOOKUP_LDS_GRID", "RP_LOOKUP_LDS_STG", "RP_LOOKUP_LDS_ABL")
+    knobs = ("RP_LOOKUP_HALF", "RP_LOOKUP_LEAN", "RP_LOOKUP_KPL", "RP_RING_LAYOUT", "RP_LOOKUP_ABLATE", "RP_RING_WIDE", "RP_LOOKUP_GRID", "RP_LOOKUP_OCC", "RP_LOOKUP_STG", "RP_LOOKUP_LH", "RP_LOOKUP_STGHS", "RP_LOOKUP_LDS", "RP_LOOKUP_LDS_GRID", "RP_LOOKUP_LDS_STG", "RP_LOOKUP_LDS_ABL", "RP_LOOKUP_WS", "RP_LOOKUP_WS_GRID", "RP_LOOKUP_WS_ABL")
     times = {k: [] for k in variants}
     digests = {}
     for r in range(a.rounds + 1):
